@@ -1,0 +1,188 @@
+"""Benchmark: unlabeled images/sec of the FixMatch ViT-S/16 SSL step (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N>1: launched by torch.distributed.run, one rank per GPU, RCCL over xGMI)
+
+Workload F1 (BASELINE configs[1]): FixMatch, ViT-Small/16, B=64 labeled + mu*B = 448 unlabeled
+weak/strong pairs per rank, 224x224x3, 23 classes, bf16 MFMA compute with fp32 master weights.
+Synthetic, HBM-resident inputs (seed 0): uint8 images -> ImageNet-normalised fp32 (code/dataset.py:21-22).
+Weak scaling: every rank runs the full F1 batch; the gradient all-reduce is the only exchange.
+One step = weak forward (448) + train forward/backward (64+448) + fused losses + grad
+all-reduce + Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.
+
+Reported beside it:
+  roofline      dominant kernel = the fc1 forward GEMM (gemm_nt, GELU epilogue), timed live with
+                HIP events on its launch stream over the timed steps; achieved = algorithmic FLOP
+                (2*M*N*K per launch) / mean launch time vs the bf16 dense MFMA peak.
+  step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.
+  cpu_baseline  the oracle (CPU fp32 restatement pinned to the reference, kind "port") timed on a
+                bounded sample (B=8, mu=7: 56 unlabeled images/step) on the host cores, rank 0, N=1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+MEAN = (0.485, 0.456, 0.406)
+STD = (0.229, 0.224, 0.225)
+PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12  # 2516.6 dense (MI355X_MICROARCH.md)
+STEP_TFLOP_F1 = 18.247  # fwd 960 imgs + bwd 512 imgs, 9.197 GFLOP/img fwd
+
+
+def synth_images(n, size, gen, device):
+    u8 = torch.randint(0, 256, (n, 3, size, size), generator=gen, dtype=torch.uint8, device=device)
+    x = u8.float().div_(255.0)
+    m = torch.tensor(MEAN, device=device).view(1, 3, 1, 1)
+    s = torch.tensor(STD, device=device).view(1, 3, 1, 1)
+    return x.sub_(m).div_(s)
+
+
+def cpu_baseline(B=8, MU=7, steps=2):
+    """Oracle (pinned CPU restatement) FixMatch step on the host cores -- a reported baseline."""
+    from oracle import ref
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    torch.set_num_threads(threads)
+    cfg = ref.Cfg()
+    params = ref.random_params(cfg, seed=0)
+    fm = ref.FixMatchRef(params, cfg, class_weights=None, thres=0.95, lambda_u=1.0)
+    g = torch.Generator().manual_seed(0)
+    x = synth_images(B, 224, g, "cpu")
+    y = torch.randint(0, 23, (B,), generator=g)
+    uw = synth_images(B * MU, 224, g, "cpu")
+    us = synth_images(B * MU, 224, g, "cpu")
+    fm.step(x, y, uw, us)  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fm.step(x, y, uw, us)
+    dt = (time.perf_counter() - t0) / steps
+    cpu = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(B * MU / dt, 3), "unit": "unlabeled images/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step), "
+                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', os.cpu_count()={os.cpu_count()}"}
+
+
+def pmc_traffic(kernel_substr):
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        for k, v in d.get("kernels", {}).items():
+            if kernel_substr in k:
+                return v.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--mu", type=int, default=7)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    from endossl import dist
+    from endossl.fixmatch import FixMatch
+    from endossl.utils import AttrDict
+    from endossl.vit import NativeViT, ViTConfig
+
+    rank, world, local = dist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, MU = args.batch, args.mu
+    model = NativeViT(ViTConfig(), seed=0)
+    tr = FixMatch(model, device=dev)
+    cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
+                   MODEL=AttrDict(NAME="vit_small_patch16_224", NUM_CLASSES=23),
+                   TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=1,
+                                  CLS_WEIGHT=False, THRES=0.95, T=1.0, LAMBDA_U=1.0, EPOCHS=1, WARMUP_EPOCHS=0,
+                                  DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const"))
+    tr.get_dataloader((None, None), None)
+    tr.get_config(cfg)
+    # class weights as the SSL configs use (CLS_WEIGHT: True): balanced weights over 23 classes
+    tr.class_weights = torch.linspace(0.5, 2.0, 23, device=dev)
+
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    x = synth_images(B, 224, g, dev)
+    y = torch.randint(0, 23, (B,), generator=g, device=dev)
+    uw = synth_images(B * MU, 224, g, dev)
+    us = synth_images(B * MU, 224, g, dev)
+    batch = ((x, y), ((uw, us), None))
+
+    for _ in range(args.warmup):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    probe = {"label": "fc1_fwd", "events": []}
+    model.engine().probe = probe
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = tr.step(batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t1 = time.perf_counter()
+    model.engine().probe = None
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    T = elapsed.item()
+    loss = out["loss"].item()
+
+    ev_ms = [e0.elapsed_time(e1) for e0, e1, _ in probe["events"]]
+    flops = [f for _, _, f in probe["events"]]
+    mean_ms = sum(ev_ms) / len(ev_ms)
+    achieved = sum(flops) / (sum(ev_ms) / 1e3) / 1e12  # TFLOP/s over the probed launches
+    traffic = pmc_traffic("gemm_nt_kernelILi1E")
+
+    if rank == 0:
+        ms = T / args.steps * 1e3
+        res = {
+            "metric": "unlabeled images/sec/node (FixMatch ViT-S, 224², μ=7)",
+            "value": round(world * B * MU * args.steps / T, 2),
+            "unit": "unlabeled images/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16", "data": "synthetic (HBM-resident uint8->ImageNet-normalised fp32, seed 0)",
+            "config": {"workload": f"F1: FixMatch ViT-S/16 step, B={B} labeled + mu*B={B * MU} unlabeled "
+                                   f"weak/strong pairs per GPU, 224^2, C=23, tau=0.95, lambda_u=1, Adam 1e-3, "
+                                   f"EMA 0.999", "global_batch": world * B * (1 + 2 * MU), "seq_len": 197,
+                       "parallelism": f"dp{world}"},
+            "step_tflops": round(STEP_TFLOP_F1 / (ms / 1e3), 1),
+            "step_mfma_frac": round(STEP_TFLOP_F1 / (ms / 1e3) / PEAK_BF16_TFLOPS, 4),
+            "final_loss": round(loss, 6),
+            "roofline": {"kernel": "gemm_nt_kernel<EPI_GELU> (fc1 forward, M=100864|88256, N=1536, K=384)",
+                         "bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                         "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms), "traffic": traffic},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(res), flush=True)
+    dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+// Shared device helpers for the endossl gfx950 (CDNA4 / MI355X) kernels.
+//
+// Conventions used by every kernel in this library:
+//  * wave = 64 lanes; lane = threadIdx.x & 63; g = lane >> 4 (16-lane group), r = lane & 15.
+//  * MFMA is v_mfma_f32_16x16x32_bf16.  Operand maps (cdna_hip_programming.md §3):
+//      A: lane holds A[row r][k = 8g + j], j = 0..7     B: lane holds B[k = 8g + j][col r]
+//      D: lane holds D[row 4g + i][col r], i = 0..3
+//  * Token-major activation buffers are padded to a multiple of 256 rows; pad rows are zero and
+//    are never written, so GEMM tiles may read them freely (DESIGN.md "HBM layout").
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
+
+enum EsStatus {
+  ES_OK = 0,
+  ES_BAD_SHAPE = -1,
+  ES_BAD_ARG = -2,
+  ES_HIP_ERROR = -3,
+};
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// ds_read_b64_tr_b16: within each 16-lane group, lane 4q+p supplies &tile[row q][col 4p];
+// lane t of the group receives column t of the 4 rows (row q in element q).
+__device__ __forceinline__ bf16x4 lds_tr4(const void* lds_byte_addr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4bf16(
+      (__attribute__((address_space(3))) bf16x4*)(lds_byte_addr));
+}
+
+__device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
+  bf16x8 r;
+  r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+  r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+  return r;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// exact (erf) GELU, nn.GELU() default (code/models/conformer.py:9,14)
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+// blocks b and b+8 share an XCD; give each XCD a contiguous range of logical tile ids so that
+// neighbouring tiles (which share an operand panel) hit the same L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
+template <typename K>
+inline void allow_lds(K kernel, size_t bytes) {
+  if (bytes > 65536)
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}

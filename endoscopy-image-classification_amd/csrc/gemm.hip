@@ -1,0 +1,338 @@
+// bf16 MFMA GEMMs for the ViT step (gfx950).
+//
+//  gemm_nt : C[M,N] = A[M,K] . B[N,K]^T (+ fused epilogue)      -- forward Linear / conv and dgrad
+//            (dgrad uses the transposed bf16 weight image W^T [K_in, N_out] that the optimizer
+//             writes, so it is an NT product too)
+//  gemm_tn : P[s][N1,N2] = sum_{m in split s} A1[m,N1]^T . A2[m,N2] -- wgrad, split over tokens
+//  splitk_reduce, colsum_partial : fp32 slab reductions (wgrad partials, bias grads)
+//
+// Replaces the reference's implicit aten::addmm / mm / conv2d calls on the ViT path
+// (code/models/conformer.py:13-23,35-50 Linear layers; timm PatchEmbed Conv2d(3,D,16,16)).
+//
+// Tiling (both kernels): 128x128 output tile, 64-deep K step, 256 threads = 4 waves in a 2x2
+// arrangement, each wave 64x64 = 4x4 MFMA 16x16x32 tiles.  Operand tiles are staged HBM->LDS with
+// global_load_lds_dwordx4 (1 KiB per wave-instruction, lane-linear destination), XOR-swizzled on
+// the SOURCE address so the fragment reads are bank-conflict free; two LDS stages; the stage for
+// step k+1 is issued before the MFMAs of step k.
+#include "common.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int STAGE_BYTES = 2 * BM * BK * 2;  // A + B tile, bf16
+
+enum Epi {
+  EPI_BF16 = 0,       // C bf16 = acc (+bias)
+  EPI_GELU = 1,       // C bf16 = acc+bias (pre-activation), C2 bf16 = gelu(acc+bias)
+  EPI_F32_RESID = 2,  // C f32 = acc (+bias) + aux_f32
+  EPI_DGELU = 3,      // C bf16 = acc * gelu'(aux_bf16)
+  EPI_F32 = 4,        // C f32 = acc (+bias)
+  EPI_PATCH = 5,      // C f32 at token row (img*(np+1)+1+p) = acc + bias + pos[1+p]
+};
+
+struct NTArgs {
+  const bf16* A; const bf16* B; const float* bias;
+  void* C; void* C2; const void* aux;
+  int M, N, K, lda, ldb, ldc, ldaux, np;
+};
+
+// 128-byte rows (64 bf16), 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7).
+__device__ __forceinline__ int swz128(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = p.N / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int g = lane >> 4, r = lane & 15;
+
+  // ---- global -> LDS staging addresses (per lane, constant over k) ----
+  const bf16* ga[4];
+  const bf16* gb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (w * 4 + j) * 8 + (lane >> 3);
+    const int lc = swz128(row, lane & 7);
+    ga[j] = p.A + (size_t)(m0 + row) * p.lda + lc * 8;
+    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + lc * 8;
+  }
+  auto stage = [&](int buf, int k0) {
+    char* As = smem + buf * STAGE_BYTES;
+    char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_global_load_lds(ga[j] + k0, LDS_PTR(As + (w * 4 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(gb[j] + k0, LDS_PTR(Bs + (w * 4 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    const char* As = smem + cur * STAGE_BYTES;
+    const char* Bs = As + BM * BK * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra = wm * 64 + i * 16 + r;
+        af[i] = *(const bf16x8*)(As + ra * 128 + swz128(ra, kk * 4 + g) * 16);
+        const int rb = wn * 64 + i * 16 + r;
+        bfr[i] = *(const bf16x8*)(Bs + rb * 128 + swz128(rb, kk * 4 + g) * 16);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bfr[ni], af[mi], acc[mi][ni]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m = .. + r][n = .. + 4g + i], i = 0..3 ----
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + r;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wn * 64 + ni * 16 + 4 * g;
+      f32x4 v = acc[mi][ni];
+      if (p.bias) {
+        const f32x4 b = *(const f32x4*)(p.bias + n);
+        v += b;
+      }
+      if constexpr (EPI == EPI_BF16) {
+        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+      } else if constexpr (EPI == EPI_GELU) {
+        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
+        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+        *(bf16x4*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
+      } else if constexpr (EPI == EPI_F32_RESID) {
+        const f32x4 res = *(const f32x4*)((const float*)p.aux + (size_t)m * p.ldaux + n);
+        *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v + res;
+      } else if constexpr (EPI == EPI_DGELU) {
+        const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (size_t)m * p.ldaux + n);
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)(v[i] * gelu_grad_f((float)pre[i]));
+        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+      } else if constexpr (EPI == EPI_F32) {
+        *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v;
+      } else if constexpr (EPI == EPI_PATCH) {
+        const int img = m / p.np, pi = m - img * p.np;
+        const f32x4 pos = *(const f32x4*)((const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n);
+        *(f32x4*)((float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n) = v + pos;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// TN (wgrad): 256-byte LDS rows (128 bf16 of the N1 / N2 axis), read with ds_read_b64_tr_b16.
+// Chunk c of row r stored at c ^ f(r), f(r) = ((r&3)<<1) | (((r>>3)&1)<<3): the 8 rows x 32 B that
+// one 32-lane half of a transposed read touches land on 16 distinct bank slots.
+__device__ __forceinline__ int swz256(int r, int c) { return c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3)); }
+
+struct TNArgs {
+  const bf16* A1; const bf16* A2; float* P;
+  int M, N1, N2, ld1, ld2, mchunk;
+};
+
+__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TNArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nt2 = p.N2 / BN, ntiles = (p.N1 / BM) * nt2;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / ntiles, tile = wg - split * ntiles;
+  const int n1_0 = (tile / nt2) * BM, n2_0 = (tile % nt2) * BN;
+  const int mbeg = split * p.mchunk;
+  const int mend = min(mbeg + p.mchunk, (p.M + BK - 1) / BK * BK);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wa = w >> 1, wb = w & 1;
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p4 = t & 3;
+
+  const bf16* g1[4];
+  const bf16* g2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (w * 4 + j) * 4 + (lane >> 4);
+    const int lc = swz256(row, lane & 15);
+    g1[j] = p.A1 + (size_t)(mbeg + row) * p.ld1 + n1_0 + lc * 8;
+    g2[j] = p.A2 + (size_t)(mbeg + row) * p.ld2 + n2_0 + lc * 8;
+  }
+  auto stage = [&](int buf, int mo) {
+    char* T1 = smem + buf * STAGE_BYTES;
+    char* T2 = T1 + BK * BM * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_global_load_lds(g1[j] + (size_t)mo * p.ld1, LDS_PTR(T1 + (w * 4 + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(g2[j] + (size_t)mo * p.ld2, LDS_PTR(T2 + (w * 4 + j) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (mend - mbeg) / BK;
+  if (nk > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+    const char* T1 = smem + cur * STAGE_BYTES;
+    const char* T2 = T1 + BK * BM * 2;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      bf16x8 af[4], bfr[4];
+      const int r1 = hh * 32 + 8 * g + q, r2 = r1 + 4;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ca = (wa * 64 + i * 16) / 8 + (p4 >> 1);
+        const int off = (p4 & 1) * 8;
+        af[i] = cat8(lds_tr4(T2 + r1 * 256 + swz256(r1, ca) * 16 + off),
+                     lds_tr4(T2 + r2 * 256 + swz256(r2, ca) * 16 + off));
+        const int cb = (wb * 64 + i * 16) / 8 + (p4 >> 1);
+        bfr[i] = cat8(lds_tr4(T1 + r1 * 256 + swz256(r1, cb) * 16 + off),
+                      lds_tr4(T1 + r2 * 256 + swz256(r2, cb) * 16 + off));
+      }
+#pragma unroll
+      for (int ai = 0; ai < 4; ++ai)
+#pragma unroll
+        for (int bi = 0; bi < 4; ++bi) acc[ai][bi] = mfma16(af[ai], bfr[bi], acc[ai][bi]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // lane holds D[n2 = .. + 4g + i][n1 = .. + t]  ->  P[split][n1][n2 .. n2+3]
+  float* P = p.P + (size_t)split * p.N1 * p.N2;
+#pragma unroll
+  for (int bi = 0; bi < 4; ++bi) {
+    const int n1 = n1_0 + wb * 64 + bi * 16 + t;
+#pragma unroll
+    for (int ai = 0; ai < 4; ++ai) {
+      const int n2 = n2_0 + wa * 64 + ai * 16 + 4 * g;
+      *(f32x4*)(P + (size_t)n1 * p.N2 + n2) = acc[ai][bi];
+    }
+  }
+}
+
+// out[i] = (accumulate ? out[i] : 0) + sum_s P[s][i]   (n % 4 == 0)
+__global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restrict__ out, int S, int n,
+                                     int accumulate) {
+  const int n4 = n >> 2;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
+    f32x4 s = accumulate ? ((const f32x4*)out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k = 0; k < S; ++k) s += ((const f32x4*)(P + (size_t)k * n))[i];
+    ((f32x4*)out)[i] = s;
+  }
+}
+
+// P[gblk][n] = sum over this block's rows of Y[m][n]  (bias gradients)
+__global__ void colsum_partial_kernel(const bf16* __restrict__ Y, int ld, int M, int N, int rows_per,
+                                      float* __restrict__ P) {
+  const int m0 = blockIdx.x * rows_per, m1 = min(m0 + rows_per, M);
+  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    float s = 0.f;
+    for (int m = m0; m < m1; ++m) s += (float)Y[(size_t)m * ld + n];
+    P[(size_t)blockIdx.x * N + n] = s;
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------- C-ABI entry points
+extern "C" {
+
+int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C,
+               int ldc, void* C2, const void* aux, int ldaux, int M, int N, int K, int np,
+               hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || (N % BN) || (K % BK) || (lda % 8) || (ldb % 8) || (ldc % 4))
+    return ES_BAD_SHAPE;
+  if (!A || !B || !C) return ES_BAD_ARG;
+  if ((epi == EPI_GELU && !C2) || ((epi == EPI_F32_RESID || epi == EPI_DGELU || epi == EPI_PATCH) && !aux))
+    return ES_BAD_ARG;
+  if (epi == EPI_PATCH && np <= 0) return ES_BAD_ARG;
+  NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
+  const int grid = ((M + BM - 1) / BM) * (N / BN);
+  const size_t lds = 2 * STAGE_BYTES;
+  switch (epi) {
+    case EPI_BF16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_BF16>, grid, 256, lds, stream, a); break;
+    case EPI_GELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_GELU>, grid, 256, lds, stream, a); break;
+    case EPI_F32_RESID: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32_RESID>, grid, 256, lds, stream, a); break;
+    case EPI_DGELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_DGELU>, grid, 256, lds, stream, a); break;
+    case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, 256, lds, stream, a); break;
+    case EPI_PATCH: hipLaunchKernelGGL(gemm_nt_kernel<EPI_PATCH>, grid, 256, lds, stream, a); break;
+    default: return ES_BAD_ARG;
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// workspace floats needed by es_gemm_tn for `splits` splits
+size_t es_gemm_tn_workspace(int N1, int N2, int splits) { return (size_t)splits * N1 * N2; }
+
+int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
+               float* workspace, float* out, int accumulate, hipStream_t stream) {
+  if (M <= 0 || (N1 % BM) || (N2 % BN) || splits <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
+  if (!A1 || !A2 || !out) return ES_BAD_ARG;
+  const int msteps = (M + BK - 1) / BK;
+  const int per = (msteps + splits - 1) / splits;
+  const int S = (msteps + per - 1) / per;
+  const bool direct = (S == 1 && !accumulate);
+  float* P = direct ? out : workspace;
+  if (!P) return ES_BAD_ARG;
+  TNArgs a{(const bf16*)A1, (const bf16*)A2, P, M, N1, N2, ld1, ld2, per * BK};
+  const int grid = S * (N1 / BM) * (N2 / BN);
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, 256, 2 * STAGE_BYTES, stream, a);
+  if (!direct) {
+    const int n = N1 * N2;
+    int rg = (n / 4 + 255) / 256;
+    rg = rg > 2048 ? 2048 : rg;
+    hipLaunchKernelGGL(splitk_reduce_kernel, rg, 256, 0, stream, P, out, S, n, accumulate);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream) {
+  if (n % 4 || S <= 0) return ES_BAD_SHAPE;
+  int rg = (n / 4 + 255) / 256;
+  rg = rg > 2048 ? 2048 : rg;
+  hipLaunchKernelGGL(splitk_reduce_kernel, rg, 256, 0, stream, P, out, S, n, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// bias gradient: out[n] (+)= sum_m Y[m][n]; workspace >= blocks*N floats (blocks <= 1024)
+int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
+              hipStream_t stream) {
+  if (M <= 0 || N <= 0 || N % 4 || blocks <= 0) return ES_BAD_SHAPE;
+  const int rows_per = (M + blocks - 1) / blocks;
+  const int G = (M + rows_per - 1) / rows_per;
+  hipLaunchKernelGGL(colsum_partial_kernel, G, 256, 0, stream, (const bf16*)Y, ld, M, N, rows_per, workspace);
+  int rg = (N / 4 + 255) / 256;
+  hipLaunchKernelGGL(splitk_reduce_kernel, rg, 256, 0, stream, workspace, out, G, N, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+}  // extern "C"

@@ -1,0 +1,167 @@
+// LayerNorm(eps=1e-6) forward / backward over the fp32 residual stream (gfx950).
+//
+// Replaces Block.norm1 / norm2 (code/models/conformer.py:58,60,65,70-71; nn.LayerNorm(dim, 1e-6)).
+// One wave per token row, D/128 float2 per lane (coalesced), statistics in fp32 with a two-pass
+// variance.  Forward writes the bf16 GEMM operand and the per-row (mean, rstd) the backward needs.
+// Backward fuses the residual-gradient add (dx = dres + LN'(dy)), writes fp32 and bf16 copies of
+// dx, and per-workgroup partial sums of dgamma / dbeta that es_splitk_reduce folds into the grads.
+#include "common.h"
+
+namespace {
+
+template <int V>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int ldx,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     bf16* __restrict__ y, int ldy, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out, int M, float eps) {
+  constexpr int D = V * 128;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (size_t)row * ldx;
+  float2 v[V];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    v[j] = *(const float2*)(xr + (j * 64 + lane) * 2);
+    s += v[j].x + v[j].y;
+  }
+  const float mean = warp_sum(s) * (1.0f / D);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const float a = v[j].x - mean, b = v[j].y - mean;
+    ss += a * a + b * b;
+  }
+  const float rstd = 1.0f / sqrtf(warp_sum(ss) * (1.0f / D) + eps);
+  bf16* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = (j * 64 + lane) * 2;
+    const float2 gm = *(const float2*)(gamma + c), bt = *(const float2*)(beta + c);
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    bf16x2 o = {(bf16)((v[j].x - mean) * rstd * gm.x + bt.x), (bf16)((v[j].y - mean) * rstd * gm.y + bt.y)};
+    *(bf16x2*)(yr + c) = o;
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const float* __restrict__ x,
+                                                     int ldx, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, const float* __restrict__ gamma,
+                                                     const float* __restrict__ dres, int ldres, float* __restrict__ dx,
+                                                     int lddx, bf16* __restrict__ dxb, int lddxb,
+                                                     float* __restrict__ pg, float* __restrict__ pb, int M) {
+  constexpr int D = V * 128;
+  __shared__ float red[2][4][D];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float2 ag[V], ab[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) ag[j] = ab[j] = make_float2(0.f, 0.f);
+  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float2 xh[V], gd[V];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (j * 64 + lane) * 2;
+      const float2 d = *(const float2*)(dy + (size_t)row * lddy + c);
+      const float2 xv = *(const float2*)(x + (size_t)row * ldx + c);
+      const float2 gm = *(const float2*)(gamma + c);
+      xh[j] = make_float2((xv.x - mean) * rstd, (xv.y - mean) * rstd);
+      gd[j] = make_float2(d.x * gm.x, d.y * gm.y);
+      s1 += gd[j].x + gd[j].y;
+      s2 += gd[j].x * xh[j].x + gd[j].y * xh[j].y;
+      ag[j].x += d.x * xh[j].x;
+      ag[j].y += d.y * xh[j].y;
+      ab[j].x += d.x;
+      ab[j].y += d.y;
+    }
+    s1 = warp_sum(s1) * (1.0f / D);
+    s2 = warp_sum(s2) * (1.0f / D);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const int c = (j * 64 + lane) * 2;
+      float2 o = make_float2(rstd * (gd[j].x - s1 - xh[j].x * s2), rstd * (gd[j].y - s1 - xh[j].y * s2));
+      if (dres) {
+        const float2 r = *(const float2*)(dres + (size_t)row * ldres + c);
+        o.x += r.x;
+        o.y += r.y;
+      }
+      *(float2*)(dx + (size_t)row * lddx + c) = o;
+      if (dxb) {
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 ob = {(bf16)o.x, (bf16)o.y};
+        *(bf16x2*)(dxb + (size_t)row * lddxb + c) = ob;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = (j * 64 + lane) * 2;
+    red[0][w][c] = ag[j].x;
+    red[0][w][c + 1] = ag[j].y;
+    red[1][w][c] = ab[j].x;
+    red[1][w][c + 1] = ab[j].y;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < D; c += blockDim.x) {
+    pg[(size_t)blockIdx.x * D + c] = red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c];
+    pb[(size_t)blockIdx.x * D + c] = red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c];
+  }
+}
+
+__global__ void reduce_rows_kernel(const float* __restrict__ P, float* __restrict__ out, int S, int n, int accumulate) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    float s = accumulate ? out[i] : 0.f;
+    for (int k = 0; k < S; ++k) s += P[(size_t)k * n + i];
+    out[i] = s;
+  }
+}
+
+}  // namespace
+
+#define LN_DISPATCH(KER, V_, GRID, STREAM, ...)                                \
+  switch (V_) {                                                                \
+    case 1: hipLaunchKernelGGL(KER<1>, GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL(KER<2>, GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL(KER<3>, GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL(KER<4>, GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 6: hipLaunchKernelGGL(KER<6>, GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    default: return ES_BAD_SHAPE;                                              \
+  }
+
+extern "C" {
+
+int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,
+                     float* rstd, int M, int D, float eps, hipStream_t stream) {
+  if (M <= 0 || D % 128 || ldx % 2 || ldy % 2) return ES_BAD_SHAPE;
+  if (!x || !gamma || !beta || !y || !mean || !rstd) return ES_BAD_ARG;
+  const int grid = (M + 3) / 4;
+  LN_DISPATCH(ln_fwd_kernel, D / 128, grid, stream, x, ldx, gamma, beta, (bf16*)y, ldy, mean, rstd, M, eps);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// workspace: 2 * blocks * D floats.  dgamma / dbeta are accumulated (+=) when accumulate != 0.
+int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
+                     const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
+                     float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
+                     hipStream_t stream) {
+  if (M <= 0 || D % 128 || blocks <= 0) return ES_BAD_SHAPE;
+  if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || !workspace) return ES_BAD_ARG;
+  const int grid = blocks < (M + 3) / 4 ? blocks : (M + 3) / 4;
+  float* pg = workspace;
+  float* pb = workspace + (size_t)grid * D;
+  LN_DISPATCH(ln_bwd_kernel, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,
+              (bf16*)dxb, lddxb, pg, pb, M);
+  const int rg = (D + 255) / 256;
+  hipLaunchKernelGGL(reduce_rows_kernel, rg, 256, 0, stream, pg, dgamma, grid, D, accumulate);
+  hipLaunchKernelGGL(reduce_rows_kernel, rg, 256, 0, stream, pb, dbeta, grid, D, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+}  // extern "C"

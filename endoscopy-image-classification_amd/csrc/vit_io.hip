@@ -1,0 +1,237 @@
+// ViT input and output ends: patch extraction, CLS/pos-embed rows, embedding backward, and the
+// fused final-LayerNorm + classifier head on the CLS token (gfx950).
+//
+// timm 0.5.4 VisionTransformer (reference build path code/build.py:196-197; same pattern as
+// code/models/conformer.py:337,420,430,442-443):
+//   x = PatchEmbed(img)            Conv2d(3, D, 16, 16): stride == kernel -> im2col is a pure
+//                                  permutation; the projection is an MFMA GEMM (gemm.hip, EPI_PATCH)
+//   x = cat(cls_token, x) + pos_embed
+//   ...blocks...
+//   logits = head(norm(x)[:, 0])   only the CLS row reaches the loss
+#include "common.h"
+
+namespace {
+
+// img fp32 [n, 3, S, S] -> patches bf16 [n*G*G, 3*P*P], column k = c*P*P + ky*P + kx (Conv2d weight order)
+template <int P>
+__global__ void im2col_kernel(const float* __restrict__ img, bf16* __restrict__ out, int n, int S) {
+  const int G = S / P, np = G * G, K = 3 * P * P;
+  const long total = (long)n * np * (K / 8);
+  for (long id = blockIdx.x * (long)blockDim.x + threadIdx.x; id < total; id += (long)gridDim.x * blockDim.x) {
+    const int k8 = (int)(id % (K / 8));
+    const long row = id / (K / 8);
+    const int im = (int)(row / np), pi = (int)(row % np);
+    const int py = pi / G, px = pi % G;
+    const int k = k8 * 8, c = k / (P * P), ky = (k / P) % P, kx = k % P;
+    const float* src = img + (((size_t)im * 3 + c) * S + py * P + ky) * S + px * P + kx;
+    const float4 a = *(const float4*)src, b = *(const float4*)(src + 4);
+    bf16x8 o = {(bf16)a.x, (bf16)a.y, (bf16)a.z, (bf16)a.w, (bf16)b.x, (bf16)b.y, (bf16)b.z, (bf16)b.w};
+    *(bf16x8*)(out + row * K + k) = o;
+  }
+}
+
+// x[img*T + 0][d] = cls[d] + pos[0][d]
+__global__ void cls_init_kernel(float* __restrict__ x, int ldx, const float* __restrict__ cls,
+                                const float* __restrict__ pos, int n, int T, int D) {
+  const int total = n * D;
+  for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < total; id += gridDim.x * blockDim.x) {
+    const int im = id / D, d = id % D;
+    x[(size_t)im * T * ldx + d] = cls[d] + pos[d];
+  }
+}
+
+// dx fp32 [n*T, D] -> dpatch bf16 [n*(T-1), D]; dpos[t][d] (+)= sum_img dx; dcls[d] (+)= dpos[0][d]
+__global__ void embed_bwd_kernel(const float* __restrict__ dx, int lddx, bf16* __restrict__ dpatch, int ldp,
+                                 float* __restrict__ dpos, float* __restrict__ dcls, int n, int T, int D,
+                                 int accumulate) {
+  const int total = T * D;
+  for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < total; id += gridDim.x * blockDim.x) {
+    const int t = id / D, d = id % D;
+    float s = 0.f;
+    for (int im = 0; im < n; ++im) {
+      const float v = dx[((size_t)im * T + t) * lddx + d];
+      s += v;
+      if (t > 0) dpatch[((size_t)im * (T - 1) + t - 1) * ldp + d] = (bf16)v;
+    }
+    dpos[id] = accumulate ? dpos[id] + s : s;
+    if (t == 0) dcls[d] = accumulate ? dcls[d] + s : s;
+  }
+}
+
+// One wave per image: y = LN(x_cls) (eps), logits = y W^T + b.  Saves xhat (pre-affine) + rstd.
+template <int V>
+__global__ __launch_bounds__(256) void cls_head_fwd_kernel(const float* __restrict__ x, int ldx, int T,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ beta,
+                                                           const float* __restrict__ W, const float* __restrict__ b,
+                                                           float* __restrict__ logits, int ldl,
+                                                           float* __restrict__ xhat, float* __restrict__ rstd_out,
+                                                           int n, int C, float eps) {
+  constexpr int D = V * 64;
+  const int lane = threadIdx.x & 63;
+  const int im = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (im >= n) return;
+  const float* xr = x + (size_t)im * T * ldx;
+  float v[V], s = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    v[j] = xr[j * 64 + lane];
+    s += v[j];
+  }
+  const float mean = warp_sum(s) * (1.0f / D);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) ss += (v[j] - mean) * (v[j] - mean);
+  const float rstd = 1.0f / sqrtf(warp_sum(ss) * (1.0f / D) + eps);
+  float y[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int d = j * 64 + lane;
+    const float xh = (v[j] - mean) * rstd;
+    xhat[(size_t)im * D + d] = xh;
+    y[j] = xh * gamma[d] + beta[d];
+  }
+  if (lane == 0) rstd_out[im] = rstd;
+  for (int c = 0; c < C; ++c) {
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc += y[j] * W[(size_t)c * D + j * 64 + lane];
+    acc = warp_sum(acc);
+    if (lane == 0) logits[(size_t)im * ldl + c] = acc + b[c];
+  }
+}
+
+// One wave per image: dy = dlogits . W; dx_cls = LN'(dy) written to dx row img*T (other rows untouched).
+template <int V>
+__global__ __launch_bounds__(256) void cls_head_bwd_kernel(const float* __restrict__ dl, int lddl,
+                                                           const float* __restrict__ W,
+                                                           const float* __restrict__ gamma,
+                                                           const float* __restrict__ xhat,
+                                                           const float* __restrict__ rstd_in,
+                                                           float* __restrict__ dyn, float* __restrict__ dx, int lddx,
+                                                           int T, int n, int C) {
+  constexpr int D = V * 64;
+  const int lane = threadIdx.x & 63;
+  const int im = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (im >= n) return;
+  float dy[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) dy[j] = 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float g = dl[(size_t)im * lddl + c];
+#pragma unroll
+    for (int j = 0; j < V; ++j) dy[j] += g * W[(size_t)c * D + j * 64 + lane];
+  }
+  float xh[V], gd[V], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int d = j * 64 + lane;
+    dyn[(size_t)im * D + d] = dy[j];
+    xh[j] = xhat[(size_t)im * D + d];
+    gd[j] = dy[j] * gamma[d];
+    s1 += gd[j];
+    s2 += gd[j] * xh[j];
+  }
+  s1 = warp_sum(s1) * (1.0f / D);
+  s2 = warp_sum(s2) * (1.0f / D);
+  const float rstd = rstd_in[im];
+#pragma unroll
+  for (int j = 0; j < V; ++j) dx[(size_t)im * T * lddx + j * 64 + lane] = rstd * (gd[j] - s1 - xh[j] * s2);
+}
+
+// Parameter grads of the head + final norm, summed over images (fp32 atomics, small):
+//  dW[c][d] += sum dl[i][c] * y[i][d], db[c] += sum dl[i][c], dgamma[d] += sum dyn*xhat, dbeta += sum dyn
+__global__ void cls_head_wgrad_kernel(const float* __restrict__ dl, int lddl, const float* __restrict__ xhat,
+                                      const float* __restrict__ dyn, const float* __restrict__ gamma,
+                                      const float* __restrict__ beta, float* __restrict__ dW, float* __restrict__ db,
+                                      float* __restrict__ dgamma, float* __restrict__ dbeta, int n, int C, int D,
+                                      int chunk) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i0 = blockIdx.y * chunk, i1 = min(i0 + chunk, n);
+  if (d < D) {
+    float sg = 0.f, sb = 0.f;
+    for (int i = i0; i < i1; ++i) {
+      sg += dyn[(size_t)i * D + d] * xhat[(size_t)i * D + d];
+      sb += dyn[(size_t)i * D + d];
+    }
+    atomicAdd(dgamma + d, sg);
+    atomicAdd(dbeta + d, sb);
+    for (int c = 0; c < C; ++c) {
+      float s = 0.f;
+      for (int i = i0; i < i1; ++i) s += dl[(size_t)i * lddl + c] * (xhat[(size_t)i * D + d] * gamma[d] + beta[d]);
+      atomicAdd(dW + (size_t)c * D + d, s);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < C) {
+    float s = 0.f;
+    for (int i = i0; i < i1; ++i) s += dl[(size_t)i * lddl + threadIdx.x];
+    atomicAdd(db + threadIdx.x, s);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int es_patch_im2col(const float* img, void* patches, int n, int S, int P, hipStream_t stream) {
+  if (n <= 0 || P != 16 || S % P) return ES_BAD_SHAPE;
+  if (!img || !patches) return ES_BAD_ARG;
+  const long total = (long)n * (S / P) * (S / P) * (3 * P * P / 8);
+  long grid = (total + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  hipLaunchKernelGGL(im2col_kernel<16>, (int)grid, 256, 0, stream, img, (bf16*)patches, n, S);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_cls_init(float* x, int ldx, const float* cls, const float* pos, int n, int T, int D, hipStream_t stream) {
+  if (n <= 0 || T <= 0 || D <= 0) return ES_BAD_SHAPE;
+  const int grid = (n * D + 255) / 256;
+  hipLaunchKernelGGL(cls_init_kernel, grid, 256, 0, stream, x, ldx, cls, pos, n, T, D);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_embed_bwd(const float* dx, int lddx, void* dpatch, int ldp, float* dpos, float* dcls, int n, int T, int D,
+                 int accumulate, hipStream_t stream) {
+  if (n <= 0 || T <= 1 || D <= 0) return ES_BAD_SHAPE;
+  const int grid = (T * D + 255) / 256;
+  hipLaunchKernelGGL(embed_bwd_kernel, grid, 256, 0, stream, dx, lddx, (bf16*)dpatch, ldp, dpos, dcls, n, T, D,
+                     accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+#define HEAD_DISPATCH(KER, V_, GRID, STREAM, ...)                                  \
+  switch (V_) {                                                                    \
+    case 2: hipLaunchKernelGGL(KER<2>, GRID, 256, 0, STREAM, __VA_ARGS__); break;  \
+    case 4: hipLaunchKernelGGL(KER<4>, GRID, 256, 0, STREAM, __VA_ARGS__); break;  \
+    case 6: hipLaunchKernelGGL(KER<6>, GRID, 256, 0, STREAM, __VA_ARGS__); break;  \
+    case 8: hipLaunchKernelGGL(KER<8>, GRID, 256, 0, STREAM, __VA_ARGS__); break;  \
+    case 12: hipLaunchKernelGGL(KER<12>, GRID, 256, 0, STREAM, __VA_ARGS__); break;\
+    default: return ES_BAD_SHAPE;                                                  \
+  }
+
+int es_cls_head_fwd(const float* x, int ldx, int T, const float* gamma, const float* beta, const float* W,
+                    const float* b, float* logits, int ldl, float* xhat, float* rstd, int n, int D, int C, float eps,
+                    hipStream_t stream) {
+  if (n <= 0 || D % 64 || C <= 0) return ES_BAD_SHAPE;
+  const int grid = (n + 3) / 4;
+  HEAD_DISPATCH(cls_head_fwd_kernel, D / 64, grid, stream, x, ldx, T, gamma, beta, W, b, logits, ldl, xhat, rstd, n,
+                C, eps);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// dx rows img*T receive the CLS gradient (caller zeroes the other rows); dW/db/dgamma/dbeta are
+// ACCUMULATED with atomics (caller zeroes them per step); dyn: scratch [n, D].
+int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
+                    const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW, float* db,
+                    float* dgamma, float* dbeta, int n, int D, int C, hipStream_t stream) {
+  if (n <= 0 || D % 64 || C <= 0 || C > 256) return ES_BAD_SHAPE;
+  const int grid = (n + 3) / 4;
+  HEAD_DISPATCH(cls_head_bwd_kernel, D / 64, grid, stream, dl, lddl, W, gamma, xhat, rstd, dyn, dx, lddx, T, n, C);
+  const int chunk = 64;
+  dim3 g2((D + 255) / 256, (n + chunk - 1) / chunk);
+  hipLaunchKernelGGL(cls_head_wgrad_kernel, g2, 256, 0, stream, dl, lddl, xhat, dyn, gamma, beta, dW, db, dgamma,
+                     dbeta, n, C, D, chunk);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+}  // extern "C"

@@ -1,0 +1,101 @@
+"""ctypes binding of libendossl_hip.so -- the C-ABI declared in include/endossl.h.
+
+This is the only way the Python host reaches the GPU compute path: there is no CPU fallback.
+If the shared library is missing (not built, or built for another arch) every compute call
+raises `EndosslLibraryError` -- loudly, never silently degrading to PyTorch ops.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ENDOSSL_LIB", os.path.join(_HERE, "lib", "libendossl_hip.so"))
+
+V, I, L, F, Z = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_size_t
+
+# name -> (restype, argtypes).  Mirrors include/endossl.h one-to-one (tests/test_abi.py checks it).
+SIGNATURES = {
+    "es_abi_version": (I, []),
+    "es_gemm_nt": (I, [I, V, I, V, I, V, V, I, V, V, I, I, I, I, I, V]),
+    "es_gemm_tn_workspace": (Z, [I, I, I]),
+    "es_gemm_tn": (I, [V, I, V, I, I, I, I, I, V, V, I, V]),
+    "es_splitk_reduce": (I, [V, V, I, I, I, V]),
+    "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
+    "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
+    "es_attn_bwd": (I, [V, I, V, I, V, V, I, V, I, I, I, I, F, V]),
+    "es_layernorm_fwd": (I, [V, I, V, V, V, I, V, V, I, I, F, V]),
+    "es_layernorm_bwd": (I, [V, I, V, I, V, V, V, V, I, V, I, V, I, V, V, V, I, I, I, I, V]),
+    "es_gelu_fwd": (I, [V, V, L, V]),
+    "es_gelu_bwd": (I, [V, V, V, L, V]),
+    "es_patch_im2col": (I, [V, V, I, I, I, V]),
+    "es_cls_init": (I, [V, I, V, V, I, I, I, V]),
+    "es_embed_bwd": (I, [V, I, V, I, V, V, I, I, I, I, V]),
+    "es_cls_head_fwd": (I, [V, I, I, V, V, V, V, V, I, V, V, I, I, I, F, V]),
+    "es_cls_head_bwd": (I, [V, I, V, V, V, V, V, V, V, I, I, V, V, V, V, I, I, I, V]),
+    "es_fm_consistency_fwd_bwd": (I, [V, I, V, I, I, I, F, F, V, V, V, V, I, V, V]),
+    "es_poly_ce_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, I, V, V]),
+    "es_adam_ema_step": (I, [V, V, V, V, V, L, F, F, F, F, F, F, F, F, V]),
+    "es_ema_entry_size": (I, []),
+    "es_ema_update_multi": (I, [V, V, I, F, F, V]),
+    "es_pack_entry_size": (I, []),
+    "es_pack_weights": (I, [V, V, I, V]),
+    "es_cast_f32_bf16": (I, [V, V, L, V]),
+}
+
+ABI_VERSION = 1
+_STATUS = {-1: "bad shape", -2: "bad argument", -3: "HIP error"}
+
+
+class EndosslLibraryError(RuntimeError):
+    pass
+
+
+class EndosslCallError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path=None):
+    """Load (once) and type the shared library.  Raises EndosslLibraryError if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise EndosslLibraryError(
+            f"endossl HIP library not found at {p}; build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (make -C endoscopy-image-classification_amd/csrc).  There is no CPU fallback.")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.es_abi_version() != ABI_VERSION:
+        raise EndosslLibraryError(f"ABI mismatch: library {lib.es_abi_version()} != python {ABI_VERSION}")
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def call(name, *args):
+    """Invoke an entry point and raise on a non-zero status."""
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise EndosslCallError(f"{name} failed: {_STATUS.get(rc, rc)}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL).  Refuses CPU tensors: no CPU fallback exists."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise EndosslCallError("endossl kernels take device tensors only (got a CPU tensor)")
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream

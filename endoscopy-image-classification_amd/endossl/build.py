@@ -1,0 +1,33 @@
+"""build_model (code/build.py:29-222) for the SSL hot path.
+
+The reference builds its FixMatch backbone with `timm.create_model(name, pretrained=True,
+num_classes=C)` (code/build.py:196-197) -- a network weight download, and timm is absent here.
+This factory returns the native ViT for the `vit_*` names instead (random timm-style init, or a
+checkpoint from MODEL.PRE_TRAIN_PATH loaded with weights_only=True, head dropped when its class
+count differs -- the reference re-heads abnormality checkpoints the same way, :180-194).
+CNN / Swin / Conformer backbones are outside round-1 scope.
+"""
+import torch
+
+from .vit import VIT_CONFIGS, NativeViT, ViTConfig
+
+
+def build_model(config, is_pathology=True, seed=0):
+    name = config.MODEL.NAME
+    C = int(config.MODEL.NUM_CLASSES)
+    if name not in VIT_CONFIGS:
+        raise NotImplementedError(f"backbone {name!r}: native builds exist for {sorted(VIT_CONFIGS)}")
+    if getattr(config.MODEL, "TYPE_SEMI", "FixMatch") == "CoMatch" and getattr(config.TRAIN, "IS_SSL", True):
+        raise NotImplementedError("CoMatch ModelwEmb head on the native ViT is a later §8 row")
+    kw = dict(VIT_CONFIGS[name])
+    if "IMG_SIZE" in config.DATA and int(config.DATA.IMG_SIZE) != kw["img_size"]:
+        kw["img_size"] = int(config.DATA.IMG_SIZE)
+    model = NativeViT(ViTConfig(num_classes=C, **kw), seed=seed)
+    path = getattr(config.MODEL, "PRE_TRAIN_PATH", "None")
+    if path not in (None, "None", ""):
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        sd = ck.get("model_state_dict", ck)
+        if sd.get("head.weight") is not None and sd["head.weight"].shape[0] != C:
+            sd = {k: v for k, v in sd.items() if not k.startswith("head.")}
+        model.load_state_dict(sd, strict=False)
+    return model

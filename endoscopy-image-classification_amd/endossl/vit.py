@@ -1,0 +1,451 @@
+"""Native ViT backbone for the SSL step: timm-0.5.4 layout, MI355X kernels underneath.
+
+Reference: `build.build_model` -> `timm.create_model('vit_small_patch16_224', num_classes=C)`
+(code/build.py:196-197); block arithmetic pinned by code/models/conformer.py:8-72 (Mlp,
+Attention, Block: LN eps 1e-6, qkv_bias, scale hd^-0.5, exact GELU); wrapper = timm
+VisionTransformer (PatchEmbed Conv2d(3,D,16,16) -> cat CLS -> + pos_embed -> blocks -> norm ->
+head on CLS, as in code/models/conformer.py:420,430,442-443).
+
+MI355X-first layout:
+  * every parameter lives in ONE fp32 flat buffer (`flat`), state_dict names/order identical to
+    timm (checkpoints interchange); grads, Adam moments and the EMA are flat buffers of the same
+    layout, so the optimizer + EMA is a single HBM sweep (optim.hip);
+  * the GEMMs read bf16 weight images W [N,K] and W^T [K,N] that the optimizer step re-packs;
+  * activations are token-major [tokens, features], padded to 256 rows (zero pad), fp32 for the
+    residual stream, bf16 for GEMM operands;
+  * forward / backward are explicit sequences of C-ABI launches on the current stream (no
+    autograd graph on the hot path); `NativeViT.forward` wraps them in one autograd.Function so
+    `model(x)` / `loss.backward()` still work as a drop-in nn.Module.
+"""
+import ctypes
+import math
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import call, ptr
+
+EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH = range(6)
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+class ViTConfig:
+    def __init__(self, img_size=224, patch=16, dim=384, depth=12, heads=6, mlp_ratio=4.0, num_classes=23,
+                 eps=1e-6):
+        self.img_size, self.patch, self.dim, self.depth = img_size, patch, dim, depth
+        self.heads, self.num_classes, self.eps = heads, num_classes, eps
+        self.hidden = int(dim * mlp_ratio)
+        self.grid = img_size // patch
+        self.np = self.grid * self.grid
+        self.T = self.np + 1
+        assert dim == heads * 64, "kernels assume head_dim 64"
+        assert dim % 128 == 0 and self.hidden % 128 == 0
+
+    def as_dict(self):
+        return dict(img_size=self.img_size, patch=self.patch, dim=self.dim, depth=self.depth, heads=self.heads,
+                    mlp_ratio=self.hidden / self.dim, num_classes=self.num_classes, eps=self.eps)
+
+
+VIT_CONFIGS = {
+    "vit_small_patch16_224": dict(img_size=224, dim=384, depth=12, heads=6),
+    "vit_small_patch16_384": dict(img_size=384, dim=384, depth=12, heads=6),
+    "vit_base_patch16_224": dict(img_size=224, dim=768, depth=12, heads=12),
+    "vit_tiny_test": dict(img_size=64, dim=128, depth=2, heads=2),
+}
+
+
+def param_layout(cfg):
+    """timm 0.5.4 VisionTransformer state_dict order: (name, shape)."""
+    D, Hd, C = cfg.dim, cfg.hidden, cfg.num_classes
+    out = [("cls_token", (1, 1, D)), ("pos_embed", (1, cfg.T, D)),
+           ("patch_embed.proj.weight", (D, 3, cfg.patch, cfg.patch)), ("patch_embed.proj.bias", (D,))]
+    for i in range(cfg.depth):
+        b = f"blocks.{i}."
+        out += [(b + "norm1.weight", (D,)), (b + "norm1.bias", (D,)),
+                (b + "attn.qkv.weight", (3 * D, D)), (b + "attn.qkv.bias", (3 * D,)),
+                (b + "attn.proj.weight", (D, D)), (b + "attn.proj.bias", (D,)),
+                (b + "norm2.weight", (D,)), (b + "norm2.bias", (D,)),
+                (b + "mlp.fc1.weight", (Hd, D)), (b + "mlp.fc1.bias", (Hd,)),
+                (b + "mlp.fc2.weight", (D, Hd)), (b + "mlp.fc2.bias", (D,))]
+    out += [("norm.weight", (D,)), ("norm.bias", (D,)), ("head.weight", (C, D)), ("head.bias", (C,))]
+    offs, o = {}, 0
+    for name, shape in out:
+        offs[name] = o
+        o = _rup(o + math.prod(shape), 64)  # 256-B aligned tensors (16-B vector access everywhere)
+    return out, offs, o
+
+
+def timm_init_(flat, cfg, layout, offs, generator=None):
+    """timm 0.5.4 `_init_vit_weights` (jax_impl=False): Linear trunc_normal(.02)/zero bias, head
+    zero, LayerNorm ones/zeros, pos_embed & cls_token trunc_normal(.02); patch conv keeps the
+    PyTorch Conv2d default (kaiming_uniform a=sqrt(5)).  Parity unpinned (timm absent here)."""
+    with torch.no_grad():
+        flat.zero_()
+        for name, shape in layout:
+            t = flat[offs[name]:offs[name] + math.prod(shape)].view(shape)
+            if name in ("cls_token", "pos_embed"):
+                nn.init.trunc_normal_(t, std=0.02, generator=generator)
+            elif name == "patch_embed.proj.weight":
+                nn.init.kaiming_uniform_(t, a=math.sqrt(5), generator=generator)
+            elif name == "patch_embed.proj.bias":
+                bound = 1.0 / math.sqrt(3 * cfg.patch * cfg.patch)
+                nn.init.uniform_(t, -bound, bound, generator=generator)
+            elif name.startswith("head"):
+                t.zero_()
+            elif name.endswith("weight") and len(shape) == 2:
+                nn.init.trunc_normal_(t, std=0.02, generator=generator)
+            elif "norm" in name and name.endswith("weight"):
+                t.fill_(1.0)
+            else:
+                t.zero_()
+
+
+class _Acts:
+    """Token-major activation buffers for one batch size (train keeps every layer's tensors)."""
+
+    def __init__(self, cfg, n, train, device):
+        D, Hd, L = cfg.dim, cfg.hidden, cfg.depth
+        self.n, self.train = n, train
+        self.M = n * cfg.T
+        Mp = _rup(self.M, 256)
+        self.Mp = Mp
+        Lk = L if train else 1
+        f32, b16 = torch.float32, torch.bfloat16
+        z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
+        self.patches = z(_rup(n * cfg.np, 256), 3 * cfg.patch * cfg.patch, dt=b16)
+        self.x = z(L + 1 if train else 2, Mp, D)
+        self.xmid = z(Lk, Mp, D)
+        self.h1 = z(Lk, Mp, D, dt=b16)
+        self.h2 = z(Lk, Mp, D, dt=b16)
+        self.mean1, self.rstd1 = z(Lk, Mp), z(Lk, Mp)
+        self.mean2, self.rstd2 = z(Lk, Mp), z(Lk, Mp)
+        self.qkv = z(Lk, Mp, 3 * D, dt=b16)
+        self.o = z(Lk, Mp, D, dt=b16)
+        self.lse = z(Lk, n * cfg.heads * cfg.T)
+        self.pre = z(Lk, Mp, Hd, dt=b16)
+        self.act = z(Lk, Mp, Hd, dt=b16)
+        self.xhat = z(n, D)
+        self.rstd_cls = z(n)
+        self.logits = z(n, cfg.num_classes)
+
+
+class _Grads:
+    """Backward scratch (one layer's worth, reused top-down)."""
+
+    def __init__(self, cfg, n, device):
+        D, Hd = cfg.dim, cfg.hidden
+        Mp = _rup(n * cfg.T, 256)
+        f32, b16 = torch.float32, torch.bfloat16
+        z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
+        self.n = n
+        self.dx, self.dxb = z(Mp, D), z(Mp, D, dt=b16)
+        self.dxm, self.dxmb = z(Mp, D), z(Mp, D, dt=b16)
+        self.dh = z(Mp, D)
+        self.dpre = z(Mp, Hd, dt=b16)
+        self.dqkv = z(Mp, 3 * D, dt=b16)
+        self.do = z(Mp, D, dt=b16)
+        self.dpatch = z(_rup(n * cfg.np, 256), D, dt=b16)
+        self.dyn = z(n, D)
+
+
+class Engine:
+    """Explicit forward / backward of the ViT over C-ABI kernels.  One per (model, device)."""
+
+    TN_TARGET_BLOCKS = 512
+
+    def __init__(self, cfg, device):
+        self.cfg, self.device = cfg, device
+        self.layout, self.offs, self.numel = param_layout(cfg)
+        self.shapes = dict(self.layout)
+        self._acts = {}
+        self._grads = {}
+        self._ws = None
+        self._packed_version = -1
+        D, Hd = cfg.dim, cfg.hidden
+        b16 = torch.bfloat16
+        # bf16 weight images: W [N,K] for forward, W^T [K,N] for dgrad
+        mats = [("patch_embed.proj.weight", D, 3 * cfg.patch * cfg.patch, False)]
+        for i in range(cfg.depth):
+            b = f"blocks.{i}."
+            mats += [(b + "attn.qkv.weight", 3 * D, D, True), (b + "attn.proj.weight", D, D, True),
+                     (b + "mlp.fc1.weight", Hd, D, True), (b + "mlp.fc2.weight", D, Hd, True)]
+        self.wb, self.wt = {}, {}
+        esz = _lib.load().es_pack_entry_size()
+        raw = bytearray(esz * len(mats))
+        for j, (name, N, K, need_t) in enumerate(mats):
+            self.wb[name] = torch.zeros(N, K, dtype=b16, device=device)
+            if need_t:
+                self.wt[name] = torch.zeros(K, N, dtype=b16, device=device)
+            dst_t = self.wt[name].data_ptr() if need_t else 0
+            entry = (ctypes.c_long(self.offs[name]), ctypes.c_void_p(self.wb[name].data_ptr()),
+                     ctypes.c_void_p(dst_t), ctypes.c_int(N), ctypes.c_int(K))
+            buf = b"".join(bytes(e) for e in entry)
+            raw[j * esz:j * esz + len(buf)] = buf
+        self._pack_tab = torch.frombuffer(raw, dtype=torch.uint8).to(device)
+        self._nmat = len(mats)
+        # optional live timing of one launch site: {"label": str, "events": [(start, end, flops)]}
+        self.probe = None
+
+    def _gemm(self, label, *args):
+        """es_gemm_nt, optionally bracketed by HIP events on the launch stream (bench roofline)."""
+        pr = self.probe
+        if pr is not None and pr["label"] == label:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            call("es_gemm_nt", *args)
+            e1.record()
+            M, N, K = args[11], args[12], args[13]
+            pr["events"].append((e0, e1, 2.0 * M * N * K))
+        else:
+            call("es_gemm_nt", *args)
+
+    # -------------------------------------------------------------- helpers
+    def view(self, flat, name):
+        o = self.offs[name]
+        return flat[o:o + math.prod(self.shapes[name])]
+
+    def pack(self, flat, version=None):
+        """Refresh the bf16 weight images from the fp32 master (skipped if `version` unchanged)."""
+        if version is not None and version == self._packed_version:
+            return
+        call("es_pack_weights", ptr(flat), ptr(self._pack_tab), self._nmat, _lib.stream())
+        self._packed_version = version if version is not None else -1
+
+    def acts(self, n, train):
+        key = (n, train)
+        if key not in self._acts:
+            self._acts[key] = _Acts(self.cfg, n, train, self.device)
+        return self._acts[key]
+
+    def workspace(self):
+        if self._ws is None:
+            cfg = self.cfg
+            D, Hd = cfg.dim, cfg.hidden
+            n_tn = max(a * b for a, b in ((3 * D, D), (D, D), (Hd, D), (D, Hd), (D, 3 * cfg.patch * cfg.patch)))
+            self._ws = torch.empty(64 * n_tn + 2 * 1024 * max(Hd, 3 * D), dtype=torch.float32, device=self.device)
+        return self._ws
+
+    # -------------------------------------------------------------- forward
+    def forward(self, flat, images_list, train):
+        """images_list: fp32 [n_i, 3, S, S] device tensors, processed as one batch (no concat copy).
+        Returns fp32 logits [n, C] (a view into the engine's buffer)."""
+        cfg = self.cfg
+        s = _lib.stream()
+        n = sum(int(t.shape[0]) for t in images_list)
+        A = self.acts(n, train)
+        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
+        K0 = 3 * cfg.patch * cfg.patch
+        row = 0
+        for t in images_list:
+            if t.shape[1:] != (3, cfg.img_size, cfg.img_size) or t.dtype != torch.float32:
+                raise ValueError(f"expected fp32 [n,3,{cfg.img_size},{cfg.img_size}] images, got {tuple(t.shape)}")
+            t = t.contiguous()
+            call("es_patch_im2col", ptr(t), ptr(A.patches[row * cfg.np:]), int(t.shape[0]), cfg.img_size,
+                 cfg.patch, s)
+            row += int(t.shape[0])
+        x0 = A.x[0]
+        pos = self.view(flat, "pos_embed")
+        call("es_gemm_nt", EPI_PATCH, ptr(A.patches), K0, ptr(self.wb["patch_embed.proj.weight"]), K0,
+             ptr(self.view(flat, "patch_embed.proj.bias")), ptr(x0), D, None, ptr(pos), D, n * cfg.np, D, K0,
+             cfg.np, s)
+        call("es_cls_init", ptr(x0), D, ptr(self.view(flat, "cls_token")), ptr(pos), n, T, D, s)
+        M = A.M
+        for i in range(cfg.depth):
+            b = f"blocks.{i}."
+            li = i if train else 0
+            xin = A.x[i] if train else A.x[i & 1]
+            xout = A.x[i + 1] if train else A.x[(i + 1) & 1]
+            xmid, h1, h2 = A.xmid[li], A.h1[li], A.h2[li]
+            call("es_layernorm_fwd", ptr(xin), D, ptr(self.view(flat, b + "norm1.weight")),
+                 ptr(self.view(flat, b + "norm1.bias")), ptr(h1), D, ptr(A.mean1[li]), ptr(A.rstd1[li]), M, D,
+                 cfg.eps, s)
+            call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(self.wb[b + "attn.qkv.weight"]), D,
+                 ptr(self.view(flat, b + "attn.qkv.bias")), ptr(A.qkv[li]), 3 * D, None, None, 0, M, 3 * D, D, 0, s)
+            call("es_attn_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.o[li]), D, ptr(A.lse[li]), n, T, H, 64 ** -0.5, s)
+            call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
+                 ptr(self.view(flat, b + "attn.proj.bias")), ptr(xmid), D, None, ptr(xin), D, M, D, D, 0, s)
+            call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
+                 ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
+                 cfg.eps, s)
+            self._gemm("fc1_fwd", EPI_GELU, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+                 ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.pre[li]), Hd, ptr(A.act[li]), None, 0, M, Hd, D,
+                 0, s)
+            call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
+                 ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xout), D, None, ptr(xmid), D, M, D, Hd, 0, s)
+        xl = A.x[cfg.depth] if train else A.x[cfg.depth & 1]
+        call("es_cls_head_fwd", ptr(xl), D, T, ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")),
+             ptr(self.view(flat, "head.weight")), ptr(self.view(flat, "head.bias")), ptr(A.logits),
+             cfg.num_classes, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.num_classes, cfg.eps, s)
+        return A.logits
+
+    # -------------------------------------------------------------- backward
+    def _tn_splits(self, M, N1, N2):
+        tiles = (N1 // 128) * (N2 // 128)
+        msteps = (M + 63) // 64
+        return max(1, min(msteps, -(-self.TN_TARGET_BLOCKS // tiles)))
+
+    def _wgrad(self, dy, N1, x, N2, M, out):
+        ws = self.workspace()
+        splits = self._tn_splits(M, N1, N2)
+        call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, _lib.stream())
+
+    def _bgrad(self, dy, N, M, out):
+        ws = self.workspace()
+        call("es_colsum", ptr(dy), N, M, N, ptr(ws), 256, ptr(out), 0, _lib.stream())
+
+    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M):
+        D = self.cfg.dim
+        ws = self.workspace()
+        call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
+             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
+
+    def backward(self, flat, grad, dlogits):
+        """dlogits fp32 [n, C] for the last train forward -> grad (flat fp32, overwritten)."""
+        cfg = self.cfg
+        s = _lib.stream()
+        n = int(dlogits.shape[0])
+        A = self.acts(n, True)
+        if n not in self._grads:
+            self._grads[n] = _Grads(cfg, n, self.device)
+        G = self._grads[n]
+        D, Hd, T, H, M = cfg.dim, cfg.hidden, cfg.T, cfg.heads, A.M
+        gv = lambda name: self.view(grad, name)  # noqa: E731
+        fv = lambda name: self.view(flat, name)  # noqa: E731
+        grad.zero_()
+        G.dx.zero_()
+        dlogits = dlogits.contiguous()
+        call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
+             ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(G.dx), D, T, ptr(gv("head.weight")),
+             ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D, cfg.num_classes, s)
+        call("es_cast_f32_bf16", ptr(G.dx), ptr(G.dxb), M * D, s)
+        for i in reversed(range(cfg.depth)):
+            b = f"blocks.{i}."
+            # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
+            call("es_gemm_nt", EPI_DGELU, ptr(G.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(G.dpre),
+                 Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
+            self._wgrad(G.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"))
+            self._bgrad(G.dxb, D, M, gv(b + "mlp.fc2.bias"))
+            call("es_gemm_nt", EPI_F32, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh), D,
+                 None, None, 0, M, D, Hd, 0, s)
+            self._wgrad(G.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"))
+            self._bgrad(G.dpre, Hd, M, gv(b + "mlp.fc1.bias"))
+            self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, G.dxmb,
+                         gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
+            # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
+            call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
+                 None, None, 0, M, D, D, 0, s)
+            self._wgrad(G.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"))
+            self._bgrad(G.dxmb, D, M, gv(b + "attn.proj.bias"))
+            call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.do), D, ptr(G.dqkv),
+                 3 * D, n, T, H, 64 ** -0.5, s)
+            call("es_gemm_nt", EPI_F32, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+                 ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
+            self._wgrad(G.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"))
+            self._bgrad(G.dqkv, 3 * D, M, gv(b + "attn.qkv.bias"))
+            self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), G.dxm, G.dx, G.dxb,
+                         gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
+        # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
+        K0 = 3 * cfg.patch * cfg.patch
+        call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,
+             s)
+        npat = n * cfg.np
+        self._wgrad(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"))
+        self._bgrad(G.dpatch, D, npat, gv("patch_embed.proj.bias"))
+        return grad
+
+
+class _ViTFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, module, *params):
+        ctx.module = module
+        ctx.n = int(x.shape[0])
+        logits = module.engine().forward(module.flat, [x], train=True)
+        return logits.clone()
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        m = ctx.module
+        g = m.engine().backward(m.flat, m.flat_grad, dlogits.float())
+        return (None, None) + tuple(m.engine().view(g, name).view(shape) for name, shape in m.layout)
+
+
+class NativeViT(nn.Module):
+    """timm-compatible VisionTransformer whose compute runs in libendossl_hip.so."""
+
+    def __init__(self, cfg=None, seed=None, **kw):
+        super().__init__()
+        self.cfg = cfg if cfg is not None else ViTConfig(**kw)
+        self.layout, self.offs, self.numel = param_layout(self.cfg)
+        flat = torch.zeros(self.numel, dtype=torch.float32)
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        timm_init_(flat, self.cfg, self.layout, self.offs, generator=gen)
+        self._set_flat(flat)
+        self._engine = None
+        self.version = 0  # bumped whenever the fp32 master changes (bf16 images re-packed lazily)
+
+    # parameters are views into one flat buffer --------------------------------------------
+    def _set_flat(self, flat):
+        self.flat = flat
+        self.flat_grad = torch.zeros_like(flat)
+        for name, shape in self.layout:
+            view = flat[self.offs[name]:self.offs[name] + math.prod(shape)].view(shape)
+            mod, attr = self._resolve(name)
+            p = nn.Parameter(view, requires_grad=True)
+            mod._parameters[attr] = p
+
+    def _resolve(self, name):
+        parts = name.split(".")
+        mod = self
+        for p in parts[:-1]:
+            if p not in mod._modules:
+                mod._modules[p] = nn.Module()
+            mod = mod._modules[p]
+        return mod, parts[-1]
+
+    def _apply(self, fn, recurse=True):
+        new = fn(self.flat)
+        if new is not self.flat:
+            self._set_flat(new.contiguous())
+            self._engine = None
+        return self
+
+    def __deepcopy__(self, memo):
+        other = NativeViT.__new__(NativeViT)
+        nn.Module.__init__(other)
+        other.cfg, other.layout, other.offs, other.numel = self.cfg, self.layout, self.offs, self.numel
+        other._set_flat(self.flat.detach().clone())
+        other._engine = None
+        other.version = 0
+        other.train(self.training)
+        return other
+
+    def engine(self):
+        if self._engine is None or self._engine.device != self.flat.device:
+            if not self.flat.is_cuda:
+                raise _lib.EndosslCallError("NativeViT runs on the MI355X only: move it to a cuda device first")
+            self._engine = Engine(self.cfg, self.flat.device)
+        return self._engine
+
+    @property
+    def fc(self):  # code/fixmatch.py:48 freezes `model.fc`; timm ViTs call it `head`
+        return self.head
+
+    def mark_updated(self):
+        self.version += 1
+
+    def load_state_dict(self, state_dict, strict=True):
+        r = super().load_state_dict(state_dict, strict=strict)
+        self.mark_updated()
+        return r
+
+    def forward(self, x):
+        eng = self.engine()
+        eng.pack(self.flat, self.version)
+        if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):
+            params = [self.get_parameter(name) for name, _ in self.layout]
+            return _ViTFunction.apply(x, self, *params)
+        return eng.forward(self.flat, [x], train=False).clone()

@@ -1,0 +1,104 @@
+/* endossl C-ABI: the MI355X (gfx950) kernels behind the FixMatch / CoMatch SSL training step.
+ *
+ * libendossl_hip.so exports exactly these functions.  Conventions:
+ *  - every pointer is a caller-owned DEVICE pointer; no function allocates or synchronises;
+ *  - every call takes the HIP stream it is enqueued on (last argument) and returns an int
+ *    status: 0 = OK, -1 = bad shape, -2 = bad argument (null / inconsistent), -3 = HIP error;
+ *  - no C++ exception crosses this boundary; functions are stateless and re-entrant;
+ *  - bf16 tensors are passed as void* (raw 16-bit bfloat16 storage), fp32 as float*;
+ *  - token-major activations are row-major [tokens, features]; buffers read by the GEMMs are
+ *    padded to a multiple of 256 rows whose pad rows are zero (DESIGN.md "HBM layout").
+ *
+ * The reference has no FFI (pure Python / PyTorch); each entry point cites the
+ * reference computation it replaces.  The Python host side (endossl/_lib.py) binds them with
+ * ctypes exactly as INTEGRATION.md shows.
+ */
+#ifndef ENDOSSL_H
+#define ENDOSSL_H
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- identity ---------------------------------------------------------------------------- */
+int es_abi_version(void);
+
+/* ---- GEMMs (code/models/conformer.py:13-23,35-50 nn.Linear; timm PatchEmbed Conv2d) ------- */
+/* C[M,N] = A[M,K] . B[N,K]^T with a fused epilogue:
+ *   epi 0: C bf16 = acc (+bias)                      (qkv, dgrad to a bf16 operand)
+ *   epi 1: C bf16 = acc+bias, C2 bf16 = GELU(acc+bias) (Mlp.fc1 + act, conformer.py:19-20)
+ *   epi 2: C f32 = acc (+bias) + aux f32              (Attention.proj / Mlp.fc2 + residual, :70-71)
+ *   epi 3: C bf16 = acc * GELU'(aux bf16)             (fc2 dgrad through the activation)
+ *   epi 4: C f32 = acc (+bias)                        (dgrad into LayerNorm backward)
+ *   epi 5: C f32 at token row img*(np+1)+1+p = acc + bias + aux[1+p]   (patch embed + pos_embed)
+ * N % 128 == 0, K % 64 == 0; A readable for round_up(M,128) rows. */
+int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
+               void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
+/* weight gradient: out[N1,N2] (+)= sum_m A1[m,N1]^T A2[m,N2], token axis split `splits` ways into
+ * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced.  N1,N2 % 128 == 0; rows in
+ * [M, round_up(M,64)) of A1 must be zero. */
+size_t es_gemm_tn_workspace(int N1, int N2, int splits);
+int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
+               float* workspace, float* out, int accumulate, hipStream_t stream);
+int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream);
+/* bias gradient: out[n] (+)= sum_m Y[m][n]  (workspace >= blocks*N floats) */
+int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
+              hipStream_t stream);
+
+/* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 256 --------------- */
+int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
+                hipStream_t stream);
+int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
+                void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
+
+/* ---- LayerNorm(eps) (code/models/conformer.py:58,60,65) -------------------------------------- */
+int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,
+                     float* rstd, int M, int D, float eps, hipStream_t stream);
+int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
+                     const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
+                     float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
+                     hipStream_t stream);
+
+/* ---- standalone GELU (nn.GELU, exact erf) ---------------------------------------------------- */
+int es_gelu_fwd(const void* x, void* y, long n, hipStream_t stream);
+int es_gelu_bwd(const void* x, const void* dy, void* dx, long n, hipStream_t stream);
+
+/* ---- ViT ends: patches, CLS/pos rows, embedding backward, final LN + head on CLS ------------- */
+int es_patch_im2col(const float* img, void* patches, int n, int S, int P, hipStream_t stream);
+int es_cls_init(float* x, int ldx, const float* cls, const float* pos, int n, int T, int D, hipStream_t stream);
+int es_embed_bwd(const float* dx, int lddx, void* dpatch, int ldp, float* dpos, float* dcls, int n, int T, int D,
+                 int accumulate, hipStream_t stream);
+int es_cls_head_fwd(const float* x, int ldx, int T, const float* gamma, const float* beta, const float* W,
+                    const float* b, float* logits, int ldl, float* xhat, float* rstd, int n, int D, int C, float eps,
+                    hipStream_t stream);
+int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
+                    const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW, float* db,
+                    float* dgamma, float* dbeta, int n, int D, int C, hipStream_t stream);
+
+/* ---- FixMatch losses, forward + gradient fused ------------------------------------------------ */
+/* code/loss.py:126-164 consistency_loss(name='ce', use_hard_labels=True); out[0]=loss, out[1]=mask mean */
+int es_fm_consistency_fwd_bwd(const float* logits_w, int ldw, const float* logits_s, int lds, int n, int C,
+                              float tau, float grad_scale, int* pseudo_label, uint8_t* mask, float* row_loss,
+                              float* dlogits_s, int lddls, float* out, hipStream_t stream);
+/* code/loss.py:103-114,308-364 ce_loss(type_loss='poly') = PolyLoss(epsilon=2); out[0]=loss */
+int es_poly_ce_fwd_bwd(const float* logits, int ldl, const int64_t* targets, const float* weights, int n, int C,
+                       float epsilon, float grad_scale, float* dlogits, int lddl, float* out, hipStream_t stream);
+
+/* ---- optimizer / EMA (code/optimizer.py:50-51, code/ema.py:51-62) ----------------------------- */
+int es_adam_ema_step(float* p, const float* g, float* m, float* v, float* ema, long n, float beta1, float beta2,
+                     float eps, float neg_step, float bc2_sqrt, float decay, float one_minus_decay,
+                     float grad_scale, hipStream_t stream);
+int es_ema_entry_size(void);
+int es_ema_update_multi(const void* entries, const void* chunks, int nchunks, float decay, float one_minus_decay,
+                        hipStream_t stream);
+int es_pack_entry_size(void);
+int es_pack_weights(const float* flat, const void* entries, int nmat, hipStream_t stream);
+int es_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ENDOSSL_H */

@@ -1,0 +1,367 @@
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE implementation.
+
+Test infrastructure only.  Runs in the build container, where the read-only reference tree is
+mounted at /root/reference; it refuses to run anywhere else.  The reference source is imported
+(never copied): `sys.path.insert(0, '/root/reference/code')` plus stub modules for the
+off-path third-party imports the container lacks (seaborn, cv2, timm), exactly as SURVEY.md
+Appendix B records.  What is committed is DATA only: inputs and the reference's outputs, as
+small .npz files.
+
+Fixtures (all fp32, torch 2.10 CPU):
+  consistency_*.npz  reference `loss.consistency_loss` (code/loss.py:126-164) at tau in
+                     {0.7, 0.95, median-max-prob}: loss, mask_mean, pseudo-labels (captured from
+                     the reference's own `ce_loss` call, code/loss.py:157), per-row masked loss and
+                     d(loss)/d(logits_s) from autograd through the reference function.
+  poly_*.npz         reference `loss.ce_loss(type_loss='poly')` (code/loss.py:103-114,308-364)
+                     with and without the sklearn-'balanced' class weights of
+                     resource/hyper_kvasir/df_split_mock_1_9.csv (code/fixmatch.py:61-66).
+  ema.npz            reference `ema.ModelEMA.update` (code/ema.py:51-59) on a module with
+                     parameters AND BatchNorm buffers (incl. the int64 num_batches_tracked).
+  fixmatch_step_*.npz  reference `FixMatch.train_one` (code/fixmatch.py:82-133), EVAL_STEP=2, on
+                     a tiny timm-0.5.4-layout ViT whose blocks are the reference's own
+                     `models.conformer.Block` (code/models/conformer.py:55-72).  Records the
+                     initial state, the inputs, every step's lx/lu/mask_mean/pseudo-labels, the
+                     final model state and the final EMA state.
+
+Usage (from the repo root):  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+REF = "/root/reference/code"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_stubs():
+    """Stub modules for imports that are off the arithmetic path."""
+    sys.modules.setdefault("seaborn", types.ModuleType("seaborn"))
+    cv2 = types.ModuleType("cv2")
+    cv2.INTER_LINEAR = 1
+    sys.modules.setdefault("cv2", cv2)
+
+    timm = types.ModuleType("timm")
+    timm_loss = types.ModuleType("timm.loss")
+    timm_loss.SoftTargetCrossEntropy = object
+    timm_sched = types.ModuleType("timm.scheduler")
+
+    class _ConstLR:
+        """Records step_update calls, keeps the LR constant."""
+
+        def __init__(self, optimizer, *a, **k):
+            self.optimizer = optimizer
+            self.updates = []
+
+        def step_update(self, n):
+            self.updates.append(int(n))
+
+        def state_dict(self):
+            return {}
+
+        def load_state_dict(self, sd):
+            pass
+
+    mods = {}
+    for name, attr in (("cosine_lr", "CosineLRScheduler"), ("step_lr", "StepLRScheduler"),
+                       ("scheduler", "Scheduler")):
+        m = types.ModuleType("timm.scheduler." + name)
+        setattr(m, attr, _ConstLR)
+        mods[name] = m
+        setattr(timm_sched, name, m)
+    timm_models = types.ModuleType("timm.models")
+    timm_layers = types.ModuleType("timm.models.layers")
+    timm_layers.DropPath = nn.Identity
+    timm_layers.trunc_normal_ = nn.init.trunc_normal_
+    timm_layers.to_2tuple = lambda x: (x, x)
+    timm_models.layers = timm_layers
+    timm.loss, timm.scheduler, timm.models = timm_loss, timm_sched, timm_models
+    sys.modules["timm"] = timm
+    sys.modules["timm.loss"] = timm_loss
+    sys.modules["timm.scheduler"] = timm_sched
+    for name, m in mods.items():
+        sys.modules["timm.scheduler." + name] = m
+    sys.modules["timm.models"] = timm_models
+    sys.modules["timm.models.layers"] = timm_layers
+
+
+def _import_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit("make_golden.py needs the reference tree at /root/reference (build container only)")
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    _install_stubs()
+    sys.path.insert(0, REF)
+    import loss as ref_loss
+    import ema as ref_ema
+    import fixmatch as ref_fixmatch
+    from models import conformer as ref_conformer
+    import utils as ref_utils
+    return ref_loss, ref_ema, ref_fixmatch, ref_conformer, ref_utils
+
+
+def _peaky_logits(g, n, c):
+    """Rows whose softmax max spans (1/c, 1): per-row temperature drawn from U(0, 9)."""
+    base = torch.randn(n, c, generator=g)
+    scale = torch.rand(n, 1, generator=g) * 9.0
+    return (base * scale).float()
+
+
+def gen_consistency(ref_loss):
+    g = torch.Generator().manual_seed(1234)
+    n, c = 448, 23
+    lw = _peaky_logits(g, n, c)
+    ls = _peaky_logits(g, n, c)
+    # force an exact tie in one row to pin first-index argmax (reference: torch.max, first index)
+    lw[5, 3] = lw[5].max() + 1.0
+    lw[5, 17] = lw[5, 3]
+    pmax = torch.softmax(lw, -1).max(-1).values
+    taus = {"0p7": 0.7, "0p95": 0.95, "median": float(pmax.median())}
+    for tag, tau in taus.items():
+        captured = {}
+        orig = ref_loss.ce_loss
+
+        def spy(logits, targets, *a, **k):
+            out = orig(logits, targets, *a, **k)
+            captured["targets"] = targets.detach().clone()
+            captured["ce_rows"] = out.detach().clone()
+            return out
+
+        ref_loss.ce_loss = spy
+        try:
+            s = ls.clone().requires_grad_(True)
+            loss, mask_mean = ref_loss.consistency_loss(lw.clone(), s, name="ce", T=1.0, p_cutoff=tau,
+                                                        use_hard_labels=True)
+            loss.backward()
+        finally:
+            ref_loss.ce_loss = orig
+        ce_rows = captured["ce_rows"]
+        # mask recovered from the reference's own per-row CE and the ge() definition it documents
+        mask = (torch.softmax(lw, -1).max(-1).values >= tau).float()
+        np.savez_compressed(
+            os.path.join(OUT, f"consistency_{tag}.npz"),
+            logits_w=lw.numpy(), logits_s=ls.numpy(), tau=np.float32(tau),
+            loss=np.float32(loss.item()), mask_mean=np.float32(mask_mean.item()),
+            pseudo_label=captured["targets"].numpy().astype(np.int64),
+            ce_rows=ce_rows.numpy(), mask=mask.numpy(),
+            grad_logits_s=s.grad.numpy())
+        print(f"consistency tau={tau:.4f} loss={loss.item():.6f} mask_mean={mask_mean.item():.4f}")
+
+
+def class_weights_mock():
+    """sklearn 'balanced' weights over the labeled rows of df_split_mock_1_9.csv.
+
+    code/fixmatch.py:61-66 passes `classes` as a list; sklearn>=1.x needs an ndarray
+     -- same arithmetic: n_samples / (n_classes * bincount).
+    """
+    import pandas as pd
+    from sklearn.utils import class_weight
+    df = pd.read_csv("/root/reference/resource/hyper_kvasir/df_split_mock_1_9.csv")
+    df = df[df.is_labeled == True]  # noqa: E712
+    y = df["target"].values
+    w = class_weight.compute_class_weight(class_weight="balanced", classes=np.unique(y), y=y)
+    return w.astype(np.float32), y
+
+
+def gen_poly(ref_loss):
+    g = torch.Generator().manual_seed(99)
+    n, c = 64, 23
+    logits = (torch.randn(n, c, generator=g) * 2.0).float()
+    y = torch.randint(0, c, (n,), generator=g)
+    w, _ = class_weights_mock()
+    for tag, cw in (("weighted", torch.tensor(w)), ("plain", None)):
+        x = logits.clone().requires_grad_(True)
+        loss = ref_loss.ce_loss(x, y, class_weights=cw, reduction="mean", type_loss="poly")
+        loss.backward()
+        np.savez_compressed(
+            os.path.join(OUT, f"poly_{tag}.npz"), logits=logits.numpy(), targets=y.numpy(),
+            weights=(w if cw is not None else np.zeros(0, np.float32)), loss=np.float32(loss.item()),
+            grad_logits=x.grad.numpy())
+        print(f"poly {tag}: loss={loss.item():.6f}")
+
+
+def gen_ema(ref_ema):
+    torch.manual_seed(7)
+    m = nn.Sequential(nn.Linear(16, 32), nn.BatchNorm1d(32), nn.ReLU(), nn.Linear(32, 5))
+    m.train()
+    m(torch.randn(8, 16))  # populate BN running stats / num_batches_tracked
+    e = ref_ema.ModelEMA(m, decay=0.999, device=None)
+    before = {k: v.detach().clone() for k, v in e.ema.state_dict().items()}
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(torch.randn_like(p))
+    m(torch.randn(8, 16))
+    model_sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    e.update(m)
+    after = e.ema.state_dict()
+    arrs = {}
+    for k in before:
+        arrs["ema_before/" + k] = before[k].numpy()
+        arrs["model/" + k] = model_sd[k].numpy()
+        arrs["ema_after/" + k] = after[k].numpy()
+    np.savez_compressed(os.path.join(OUT, "ema.npz"), decay=np.float64(0.999), **arrs)
+    print("ema: nbt after", after["1.num_batches_tracked"].item())
+
+
+# ---------------------------------------------------------------- FixMatch step golden
+def make_tiny_vit(conformer, img=64, patch=16, dim=128, depth=2, heads=2, num_classes=23):
+    """timm-0.5.4 VisionTransformer layout (patch_embed.proj / cls_token / pos_embed / blocks /
+    norm / head on the CLS token) built from the reference's own Block."""
+
+    class PatchEmbed(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.proj = nn.Conv2d(3, dim, patch, patch)
+
+    class TinyViT(nn.Module):
+        def __init__(self):
+            super().__init__()
+            npatch = (img // patch) ** 2
+            self.patch_embed = PatchEmbed()
+            self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+            self.pos_embed = nn.Parameter(torch.zeros(1, npatch + 1, dim))
+            self.blocks = nn.Sequential(*[conformer.Block(dim, heads, 4.0, qkv_bias=True) for _ in range(depth)])
+            self.norm = nn.LayerNorm(dim, eps=1e-6)
+            self.head = nn.Linear(dim, num_classes)
+
+        def forward(self, x):
+            x = self.patch_embed.proj(x).flatten(2).transpose(1, 2)
+            x = torch.cat((self.cls_token.expand(x.shape[0], -1, -1), x), dim=1) + self.pos_embed
+            x = self.norm(self.blocks(x))
+            return self.head(x[:, 0])
+
+    return TinyViT()
+
+
+class _FakeIter:
+    def __init__(self, items):
+        self._it = iter(items)
+
+    def next(self):
+        return next(self._it)
+
+    __next__ = next
+
+
+class _FakeDS:
+    def __init__(self, df):
+        self.df = df
+
+
+class FakeDL:
+    """torch-1.10-style loader: its iterator has .next()."""
+
+    def __init__(self, items, df=None):
+        self.items = items
+        self.dataset = _FakeDS(df)
+
+    def __iter__(self):
+        return _FakeIter(self.items)
+
+    def __len__(self):
+        return len(self.items)
+
+
+def gen_fixmatch_step(ref_fixmatch, ref_conformer, ref_utils, tag, thres, head_std, full_state):
+    import pandas as pd
+    from sklearn.utils import class_weight as skcw
+    torch.manual_seed(2024)
+    model = make_tiny_vit(ref_conformer)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if name.endswith("weight") and p.dim() >= 2:
+                nn.init.trunc_normal_(p, std=0.02)
+            elif name in ("cls_token", "pos_embed"):
+                nn.init.trunc_normal_(p, std=0.02)
+            elif "norm" in name and name.endswith("weight"):
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+            else:
+                p.copy_(0.02 * torch.randn_like(p))
+        model.head.weight.normal_(0.0, head_std)
+    init_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+    B, MU, C, steps = 2, 2, 23, 2
+    g = torch.Generator().manual_seed(77)
+    # the labeled df drives the class weights; 23 classes, skewed counts
+    df_y = np.concatenate([np.full(i + 1, i) for i in range(C)])
+    df = pd.DataFrame({"target": df_y})
+    lab, unlab = [], []
+    for _ in range(steps):
+        x = torch.randn(B, 3, 64, 64, generator=g)
+        y = torch.randint(0, C, (B,), generator=g)
+        uw = torch.randn(B * MU, 3, 64, 64, generator=g)
+        us = torch.randn(B * MU, 3, 64, 64, generator=g)
+        lab.append((x, y))
+        unlab.append(((uw, us), torch.arange(B * MU)))
+    cfg = ref_utils.AttrDict(
+        DATA=ref_utils.AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+        MODEL=ref_utils.AttrDict(NAME="vit_tiny_test", NUM_CLASSES=C, MARGIN="None", TYPE_SEMI="FixMatch"),
+        TRAIN=ref_utils.AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3,
+                                 EVAL_STEP=steps, CLS_WEIGHT=True, THRES=thres, T=1.0, LAMBDA_U=1.0,
+                                 IS_SSL=True, EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10,
+                                 WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="step"))
+    orig_ccw = skcw.compute_class_weight
+
+    def ccw(class_weight, classes, y):  # sklearn>=1.x wants ndarray classes
+        return orig_ccw(class_weight=class_weight, classes=np.asarray(classes), y=np.asarray(y))
+
+    ref_fixmatch.class_weight.compute_class_weight = ccw
+    rec = {"lx": [], "lu": [], "mask_mean": [], "pl": [], "cw": None}
+    o_ce, o_cons = ref_fixmatch.ce_loss, ref_fixmatch.consistency_loss
+
+    def ce_spy(*a, **k):
+        out = o_ce(*a, **k)
+        rec["lx"].append(out.item())
+        return out
+
+    def cons_spy(lw, ls, *a, **k):
+        out = o_cons(lw, ls, *a, **k)
+        rec["lu"].append(out[0].item())
+        rec["mask_mean"].append(out[1].item())
+        rec["pl"].append(torch.softmax(lw.detach(), -1).max(-1).indices.numpy())
+        return out
+
+    ref_fixmatch.ce_loss, ref_fixmatch.consistency_loss = ce_spy, cons_spy
+    try:
+        tr = ref_fixmatch.FixMatch(model, opt_func="Adam", lr=1e-3, device="cpu")
+        tr.get_dataloader((FakeDL(lab, df), FakeDL(unlab)), None)
+        tr.get_config(cfg)
+        rec["cw"] = tr.class_weights.numpy()
+        meter = tr.train_one(1)
+    finally:
+        ref_fixmatch.ce_loss, ref_fixmatch.consistency_loss = o_ce, o_cons
+        ref_fixmatch.class_weight.compute_class_weight = orig_ccw
+    final_sd = model.state_dict()
+    ema_sd = tr.ema_model.ema.state_dict()
+    arrs = dict(thres=np.float32(thres), B=B, MU=MU, steps=steps, class_weights=rec["cw"],
+                lx=np.array(rec["lx"], np.float32), lu=np.array(rec["lu"], np.float32),
+                mask_mean=np.array(rec["mask_mean"], np.float32), pseudo_label=np.stack(rec["pl"]),
+                meter_avg=np.float32(meter.avg), lr_updates=np.array(tr.lr_scheduler.updates))
+    for i, ((x, y), ((uw, us), _)) in enumerate(zip(lab, unlab)):
+        arrs[f"x{i}"], arrs[f"y{i}"], arrs[f"uw{i}"], arrs[f"us{i}"] = x.numpy(), y.numpy(), uw.numpy(), us.numpy()
+    for k in init_sd:
+        arrs["init/" + k] = init_sd[k].numpy()
+        if full_state:
+            arrs["final/" + k] = final_sd[k].numpy()
+            arrs["ema/" + k] = ema_sd[k].numpy()
+        else:
+            arrs["final_sum/" + k] = np.float64(final_sd[k].double().sum().item())
+            arrs["ema_sum/" + k] = np.float64(ema_sd[k].double().sum().item())
+    np.savez_compressed(os.path.join(OUT, f"fixmatch_step_{tag}.npz"), **arrs)
+    print(f"fixmatch {tag}: lx={rec['lx']} lu={rec['lu']} mask={rec['mask_mean']} lr_updates={tr.lr_scheduler.updates}")
+
+
+def main():
+    ref_loss, ref_ema, ref_fixmatch, ref_conformer, ref_utils = _import_reference()
+    gen_consistency(ref_loss)
+    gen_poly(ref_loss)
+    gen_ema(ref_ema)
+    gen_fixmatch_step(ref_fixmatch, ref_conformer, ref_utils, "t0p7", 0.7, 0.6, True)
+    gen_fixmatch_step(ref_fixmatch, ref_conformer, ref_utils, "t0p95", 0.95, 0.6, False)
+
+
+if __name__ == "__main__":
+    main()

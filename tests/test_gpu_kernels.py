@@ -1,0 +1,368 @@
+"""Kernel-level parity on the MI355X: every C-ABI entry point against a plain fp32 reference of the
+same op (torch on the same device, same bf16 inputs), plus exact-integer layout checks and the
+reference-generated golden fixtures for the loss / EMA kernels."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from endossl import _lib  # noqa: E402
+from endossl._lib import call, ptr  # noqa: E402
+
+DEV = "cuda"
+EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH = range(6)
+
+
+def S():
+    return _lib.stream()
+
+
+def _int_bf16(*shape, lo=-3, hi=4, gen=None):
+    return torch.randint(lo, hi, shape, generator=gen, dtype=torch.int32).to(torch.bfloat16).to(DEV)
+
+
+def _pad_rows(t, mult=256):
+    M = t.shape[0]
+    Mp = (M + mult - 1) // mult * mult
+    out = torch.zeros((Mp,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    out[:M] = t
+    return out
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    _lib.load()
+
+
+# ------------------------------------------------------------------------------------- GEMM NT
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 384, 384), (128, 128, 64)])
+def test_gemm_nt_exact_integers(M, N, K):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = _pad_rows(_int_bf16(M, K, gen=g))
+    B = _int_bf16(N, K, gen=g)
+    bias = torch.randint(-4, 5, (N,), generator=g).float().to(DEV)
+    ref = A[:M].float() @ B.float().t() + bias
+    C = torch.zeros(M, N, dtype=torch.float32, device=DEV)
+    call("es_gemm_nt", EPI_F32, ptr(A), K, ptr(B), K, ptr(bias), ptr(C), N, None, None, 0, M, N, K, 0, S())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(C, ref, rtol=0, atol=0)
+    Cb = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    call("es_gemm_nt", EPI_BF16, ptr(A), K, ptr(B), K, ptr(bias), ptr(Cb), N, None, None, 0, M, N, K, 0, S())
+    torch.testing.assert_close(Cb.float(), ref.bfloat16().float(), rtol=0, atol=0)
+
+
+def test_gemm_nt_epilogues_vs_fp32():
+    torch.manual_seed(0)
+    M, N, K = 777, 512, 384
+    A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
+    B = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(N, device=DEV) * 0.1
+    acc = A[:M].float() @ B.float().t() + bias
+    # GELU: pre and act
+    pre = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    act = torch.zeros_like(pre)
+    call("es_gemm_nt", EPI_GELU, ptr(A), K, ptr(B), K, ptr(bias), ptr(pre), N, ptr(act), None, 0, M, N, K, 0, S())
+    torch.testing.assert_close(pre.float(), acc, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(act.float(), F.gelu(acc), rtol=1e-2, atol=1e-2)
+    # residual fp32
+    res = torch.randn(M, N, device=DEV)
+    out = torch.zeros(M, N, device=DEV)
+    call("es_gemm_nt", EPI_F32_RESID, ptr(A), K, ptr(B), K, ptr(bias), ptr(out), N, None, ptr(res), N, M, N, K, 0,
+         S())
+    torch.testing.assert_close(out, acc + res, rtol=1e-5, atol=1e-4)
+    # dgelu: acc(no bias) * gelu'(pre)
+    xpre = torch.randn(M, N, device=DEV).bfloat16()
+    dpre = torch.zeros(M, N, dtype=torch.bfloat16, device=DEV)
+    call("es_gemm_nt", EPI_DGELU, ptr(A), K, ptr(B), K, None, ptr(dpre), N, None, ptr(xpre), N, M, N, K, 0, S())
+    xp = xpre.float().requires_grad_(True)
+    F.gelu(xp).backward(torch.ones_like(xp))
+    ref = (A[:M].float() @ B.float().t()) * xp.grad
+    torch.testing.assert_close(dpre.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_gemm_nt_patch_epilogue():
+    torch.manual_seed(1)
+    n, npch, D, K = 3, 16, 128, 768
+    M = n * npch
+    A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
+    B = (torch.randn(D, K, device=DEV) * 0.02).bfloat16()
+    bias = torch.randn(D, device=DEV)
+    pos = torch.randn(npch + 1, D, device=DEV)
+    x = torch.full((n * (npch + 1), D), 7.0, device=DEV)
+    call("es_gemm_nt", EPI_PATCH, ptr(A), K, ptr(B), K, ptr(bias), ptr(x), D, None, ptr(pos), D, M, D, K, npch, S())
+    ref = (A[:M].float() @ B.float().t() + bias).view(n, npch, D) + pos[1:]
+    xv = x.view(n, npch + 1, D)
+    torch.testing.assert_close(xv[:, 1:], ref, rtol=1e-5, atol=1e-4)
+    assert torch.all(xv[:, 0] == 7.0)  # CLS rows untouched
+
+
+# ------------------------------------------------------------------------------------- GEMM TN
+@pytest.mark.parametrize("M,N1,N2,splits", [(1000, 128, 256, 1), (1000, 384, 128, 5), (4096, 256, 384, 17)])
+def test_gemm_tn_exact_integers(M, N1, N2, splits):
+    g = torch.Generator().manual_seed(M + splits)
+    A1 = _pad_rows(_int_bf16(M, N1, lo=-2, hi=3, gen=g))
+    A2 = _pad_rows(_int_bf16(M, N2, lo=-2, hi=3, gen=g))
+    ref = A1[:M].float().t() @ A2[:M].float()
+    ws = torch.empty(_lib.load().es_gemm_tn_workspace(N1, N2, splits), device=DEV)
+    out = torch.full((N1, N2), 3.0, device=DEV)
+    call("es_gemm_tn", ptr(A1), N1, ptr(A2), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, S())
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    call("es_gemm_tn", ptr(A1), N1, ptr(A2), N2, M, N1, N2, splits, ptr(ws), ptr(out), 1, S())
+    torch.testing.assert_close(out, 2 * ref, rtol=0, atol=0)
+
+
+def test_colsum():
+    torch.manual_seed(2)
+    M, N = 5000, 1152
+    Y = torch.randn(M, N, device=DEV).bfloat16()
+    ws = torch.empty(256 * N, device=DEV)
+    out = torch.zeros(N, device=DEV)
+    call("es_colsum", ptr(Y), N, M, N, ptr(ws), 256, ptr(out), 0, S())
+    torch.testing.assert_close(out, Y.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
+# ------------------------------------------------------------------------------------- attention
+def _attn_ref(qkv, n, T, H):
+    D = H * 64
+    q, k, v = qkv.float().view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-2, -1)) * 64 ** -0.5
+    lse = torch.logsumexp(s, -1)
+    o = (s.softmax(-1) @ v).transpose(1, 2).reshape(n * T, D)
+    return o, lse
+
+
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 64, 1), (2, 250, 2)])
+def test_attention_fwd(n, T, H):
+    torch.manual_seed(T)
+    D = H * 64
+    qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
+    o = torch.zeros(qkv.shape[0], D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(n * H * T, device=DEV)
+    call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
+    o_ref, lse_ref = _attn_ref(qkv[:n * T], n, T, H)
+    torch.testing.assert_close(o[:n * T].float(), o_ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(lse.view(n, H, T), lse_ref, rtol=1e-3, atol=2e-3)
+    assert torch.all(o[n * T:] == 0)
+
+
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 17, 2)])
+def test_attention_bwd(n, T, H):
+    torch.manual_seed(100 + T)
+    D = H * 64
+    qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
+    dout = _pad_rows(torch.randn(n * T, D, device=DEV).bfloat16())
+    o = torch.zeros(qkv.shape[0], D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(n * H * T, device=DEV)
+    call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
+    dqkv = torch.zeros_like(qkv)
+    call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(dout), D, ptr(dqkv), 3 * D, n, T, H, 64 ** -0.5,
+         S())
+    x = qkv[:n * T].float().requires_grad_(True)
+    o_ref, _ = _attn_ref(x, n, T, H)
+    o_ref.backward(dout[:n * T].float())
+    ref = x.grad
+    got = dqkv[:n * T].float()
+    for part in range(3):
+        a, b = got[:, part * D:(part + 1) * D], ref[:, part * D:(part + 1) * D]
+        err = (a - b).abs().max().item() / b.abs().max().item()
+        assert err < 3e-2, (part, err)
+    assert torch.all(dqkv[n * T:] == 0)
+
+
+# ------------------------------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("D", [128, 384, 768])
+def test_layernorm_fwd_bwd(D):
+    torch.manual_seed(D)
+    M = 1000
+    x = torch.randn(M, D, device=DEV) * 2 + 0.5
+    gamma = 1 + 0.1 * torch.randn(D, device=DEV)
+    beta = 0.1 * torch.randn(D, device=DEV)
+    y = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    mean, rstd = torch.zeros(M, device=DEV), torch.zeros(M, device=DEV)
+    call("es_layernorm_fwd", ptr(x), D, ptr(gamma), ptr(beta), ptr(y), D, ptr(mean), ptr(rstd), M, D, 1e-6, S())
+    xr = x.clone().requires_grad_(True)
+    gr = gamma.clone().requires_grad_(True)
+    br = beta.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (D,), gr, br, 1e-6)
+    torch.testing.assert_close(y.float(), yr.detach(), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(mean, x.mean(1), rtol=1e-5, atol=1e-5)
+    dy = torch.randn(M, D, device=DEV)
+    dres = torch.randn(M, D, device=DEV)
+    yr.backward(dy)
+    dx = torch.zeros(M, D, device=DEV)
+    dxb = torch.zeros(M, D, dtype=torch.bfloat16, device=DEV)
+    dg, db = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ws = torch.empty(2 * 1024 * D, device=DEV)
+    call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
+         ptr(dxb), D, ptr(dg), ptr(db), ptr(ws), 1024, M, D, 0, S())
+    torch.testing.assert_close(dx, xr.grad + dres, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(dxb.float(), (xr.grad + dres), rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+
+
+# ------------------------------------------------------------------------------------- ViT ends
+def test_im2col_matches_unfold():
+    torch.manual_seed(3)
+    n, Sz = 3, 64
+    img = torch.randn(n, 3, Sz, Sz, device=DEV)
+    pt = torch.zeros(n * 16, 768, dtype=torch.bfloat16, device=DEV)
+    call("es_patch_im2col", ptr(img), ptr(pt), n, Sz, 16, S())
+    ref = F.unfold(img, 16, stride=16).transpose(1, 2).reshape(n * 16, 768)
+    torch.testing.assert_close(pt.float(), ref.bfloat16().float(), rtol=0, atol=0)
+
+
+def test_cls_head_fwd_bwd():
+    torch.manual_seed(4)
+    n, T, D, C = 37, 5, 384, 23
+    x = torch.randn(n * T, D, device=DEV)
+    gamma = 1 + 0.1 * torch.randn(D, device=DEV)
+    beta = 0.1 * torch.randn(D, device=DEV)
+    W = 0.05 * torch.randn(C, D, device=DEV)
+    b = 0.1 * torch.randn(C, device=DEV)
+    logits = torch.zeros(n, C, device=DEV)
+    xhat, rstd = torch.zeros(n, D, device=DEV), torch.zeros(n, device=DEV)
+    call("es_cls_head_fwd", ptr(x), D, T, ptr(gamma), ptr(beta), ptr(W), ptr(b), ptr(logits), C, ptr(xhat), ptr(rstd),
+         n, D, C, 1e-6, S())
+    xr, gr, br, Wr, bhr = (t.clone().requires_grad_(True) for t in (x, gamma, beta, W, b))
+    lr = F.linear(F.layer_norm(xr.view(n, T, D)[:, 0], (D,), gr, br, 1e-6), Wr, bhr)
+    torch.testing.assert_close(logits, lr.detach(), rtol=1e-5, atol=1e-5)
+    dl = torch.randn(n, C, device=DEV)
+    lr.backward(dl)
+    dx = torch.zeros(n * T, D, device=DEV)
+    dyn = torch.zeros(n, D, device=DEV)
+    dW, db, dg, dbt = torch.zeros_like(W), torch.zeros_like(b), torch.zeros_like(gamma), torch.zeros_like(beta)
+    call("es_cls_head_bwd", ptr(dl), C, ptr(W), ptr(gamma), ptr(beta), ptr(xhat), ptr(rstd), ptr(dyn), ptr(dx), D, T,
+         ptr(dW), ptr(db), ptr(dg), ptr(dbt), n, D, C, S())
+    torch.testing.assert_close(dx, xr.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dW, Wr.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(db, bhr.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(dbt, br.grad, rtol=1e-4, atol=1e-5)
+
+
+def test_embed_bwd():
+    torch.manual_seed(5)
+    n, T, D = 6, 17, 128
+    dx = torch.randn(n * T, D, device=DEV)
+    dp = torch.zeros(n * (T - 1), D, dtype=torch.bfloat16, device=DEV)
+    dpos, dcls = torch.zeros(T, D, device=DEV), torch.zeros(D, device=DEV)
+    call("es_embed_bwd", ptr(dx), D, ptr(dp), D, ptr(dpos), ptr(dcls), n, T, D, 0, S())
+    v = dx.view(n, T, D)
+    torch.testing.assert_close(dpos, v.sum(0), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dcls, v[:, 0].sum(0), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(dp.float(), v[:, 1:].reshape(-1, D).bfloat16().float(), rtol=0, atol=0)
+
+
+# ------------------------------------------------------------------------------------- losses (golden)
+def test_consistency_kernel_vs_reference_fixture(golden):
+    for tag in ("0p7", "0p95", "median"):
+        d = golden(f"consistency_{tag}.npz")
+        lw = torch.tensor(d["logits_w"], device=DEV)
+        ls = torch.tensor(d["logits_s"], device=DEV)
+        n, C = ls.shape
+        tau = float(d["tau"])
+        pl = torch.zeros(n, dtype=torch.int32, device=DEV)
+        mask = torch.zeros(n, dtype=torch.uint8, device=DEV)
+        rows = torch.zeros(n, device=DEV)
+        dls = torch.zeros(n, C, device=DEV)
+        out = torch.zeros(2, device=DEV)
+        call("es_fm_consistency_fwd_bwd", ptr(lw), C, ptr(ls), C, n, C, tau, 1.0 / n, ptr(pl), ptr(mask), ptr(rows),
+             ptr(dls), C, ptr(out), S())
+        torch.cuda.synchronize()
+        pmax = torch.softmax(torch.tensor(d["logits_w"], dtype=torch.float64), -1).max(-1).values.numpy()
+        near = np.abs(pmax - tau) < 1e-6  # rows whose max-prob is within ulps of tau: mask undefined
+        np.testing.assert_array_equal(pl.cpu().numpy(), d["pseudo_label"])  # integer labels bit-exact
+        np.testing.assert_array_equal(mask.cpu().numpy()[~near], d["mask"][~near].astype(np.uint8))
+        np.testing.assert_allclose(out[0].item(), float(d["loss"]), rtol=1e-5)
+        np.testing.assert_allclose(out[1].item(), float(d["mask_mean"]), rtol=0, atol=1.0 / n * near.sum())
+        np.testing.assert_allclose(rows.cpu().numpy(), d["ce_rows"], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(dls.cpu().numpy(), d["grad_logits_s"], rtol=1e-4, atol=1e-7)
+
+
+def test_poly_kernel_vs_reference_fixture(golden):
+    for tag in ("weighted", "plain"):
+        d = golden(f"poly_{tag}.npz")
+        lg = torch.tensor(d["logits"], device=DEV)
+        y = torch.tensor(d["targets"], device=DEV)
+        w = torch.tensor(d["weights"], device=DEV) if d["weights"].size else None
+        n, C = lg.shape
+        dl = torch.zeros(n, C, device=DEV)
+        out = torch.zeros(1, device=DEV)
+        call("es_poly_ce_fwd_bwd", ptr(lg), C, ptr(y), ptr(w), n, C, 2.0, 1.0 / n, ptr(dl), C, ptr(out), S())
+        np.testing.assert_allclose(out.item(), float(d["loss"]), rtol=1e-5)
+        np.testing.assert_allclose(dl.cpu().numpy(), d["grad_logits"], rtol=1e-4, atol=1e-6)
+
+
+def test_loss_module_api_autograd(golden):
+    from endossl.loss import ce_loss, consistency_loss
+    d = golden("consistency_0p95.npz")
+    lw = torch.tensor(d["logits_w"], device=DEV)
+    ls = torch.tensor(d["logits_s"], device=DEV).requires_grad_(True)
+    loss, mm = consistency_loss(lw, ls, T=1.0, p_cutoff=float(d["tau"]))
+    (2.0 * loss).backward()
+    np.testing.assert_allclose(ls.grad.cpu().numpy(), 2.0 * d["grad_logits_s"], rtol=1e-4, atol=1e-7)
+    d = golden("poly_weighted.npz")
+    x = torch.tensor(d["logits"], device=DEV).requires_grad_(True)
+    lx = ce_loss(x, torch.tensor(d["targets"], device=DEV), class_weights=torch.tensor(d["weights"], device=DEV),
+                 reduction="mean", type_loss="poly")
+    lx.backward()
+    np.testing.assert_allclose(lx.item(), float(d["loss"]), rtol=1e-5)
+    np.testing.assert_allclose(x.grad.cpu().numpy(), d["grad_logits"], rtol=1e-4, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------------- EMA / Adam
+def test_ema_multi_bit_exact_vs_reference_fixture(golden):
+    import torch.nn as nn
+    from endossl.ema import ModelEMA
+    d = golden("ema.npz")
+    keys = [k.split("/", 1)[1] for k in d.files if k.startswith("ema_before/")]
+    m = nn.Sequential(nn.Linear(16, 32), nn.BatchNorm1d(32), nn.ReLU(), nn.Linear(32, 5)).to(DEV)
+    m.load_state_dict({k: torch.tensor(d["ema_before/" + k]) for k in keys})
+    e = ModelEMA(m, decay=0.999, device=DEV)
+    m.load_state_dict({k: torch.tensor(d["model/" + k]) for k in keys})
+    e.update(m)
+    torch.cuda.synchronize()
+    for k, v in e.ema.state_dict().items():
+        np.testing.assert_array_equal(v.cpu().numpy(), d["ema_after/" + k], err_msg=k)
+
+
+def test_adam_ema_step_vs_torch_adam():
+    torch.manual_seed(6)
+    n = 10_000
+    p0 = torch.randn(n)
+    grads = [torch.randn(n) * 10 ** (-i) for i in range(3)]
+    # torch.optim.Adam on CPU = the reference optimizer
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0)
+    er = p0.clone()
+    p, m, v, e = p0.to(DEV), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV), p0.to(DEV)
+    for t, gr in enumerate(grads, 1):
+        pr.grad = gr.clone()
+        opt.step()
+        er = 0.999 * er + (1.0 - 0.999) * pr.detach()
+        g = gr.to(DEV)
+        bc1, bc2 = 1 - 0.9 ** t, 1 - 0.999 ** t
+        call("es_adam_ema_step", ptr(p), ptr(g), ptr(m), ptr(v), ptr(e), n, 0.9, 0.999, 1e-8, -1e-3 / bc1,
+             math.sqrt(bc2), 0.999, 1.0 - 0.999, 1.0, S())
+    torch.testing.assert_close(p.cpu(), pr.detach(), rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(e.cpu(), er, rtol=1e-6, atol=1e-7)
+
+
+def test_pack_weights_exact():
+    from endossl.vit import Engine, NativeViT, ViTConfig
+    m = NativeViT(ViTConfig(img_size=64, dim=128, depth=2, heads=2), seed=3).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat)
+    torch.cuda.synchronize()
+    sd = m.state_dict()
+    for name, wb in eng.wb.items():
+        W = sd[name].reshape(wb.shape[0], -1)
+        assert torch.equal(wb, W.bfloat16()), name
+        if name in eng.wt:
+            assert torch.equal(eng.wt[name], W.t().contiguous().bfloat16()), name

@@ -1,0 +1,85 @@
+"""Pin the oracle (oracle/ref.py) against fixtures produced by the REFERENCE implementation
+(tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import torch
+
+from oracle import ref
+
+
+def test_consistency_matches_reference(golden):
+    for tag in ("0p7", "0p95", "median"):
+        d = golden(f"consistency_{tag}.npz")
+        lw = torch.tensor(d["logits_w"])
+        ls = torch.tensor(d["logits_s"]).requires_grad_(True)
+        loss, mm, pl, mask = ref.consistency(lw, ls, float(d["tau"]))
+        loss.backward()
+        assert loss.item() == float(d["loss"]), tag
+        assert mm.item() == float(d["mask_mean"]), tag
+        np.testing.assert_array_equal(pl.numpy(), d["pseudo_label"])
+        np.testing.assert_array_equal(mask.numpy(), d["mask"])
+        np.testing.assert_array_equal(ls.grad.numpy(), d["grad_logits_s"])
+    # the forced tie in row 5 resolves to the FIRST max index, as torch.max does in the reference
+    d = golden("consistency_0p7.npz")
+    assert d["pseudo_label"][5] == 3
+
+
+def test_poly_matches_reference(golden):
+    for tag in ("weighted", "plain"):
+        d = golden(f"poly_{tag}.npz")
+        x = torch.tensor(d["logits"]).requires_grad_(True)
+        w = torch.tensor(d["weights"]) if d["weights"].size else None
+        loss = ref.poly_ce(x, torch.tensor(d["targets"]), w)
+        loss.backward()
+        np.testing.assert_allclose(loss.item(), float(d["loss"]), rtol=1e-6)
+        np.testing.assert_allclose(x.grad.numpy(), d["grad_logits"], rtol=1e-5, atol=1e-7)
+
+
+def test_ema_matches_reference(golden):
+    d = golden("ema.npz")
+    keys = sorted({k.split("/", 1)[1] for k in d.files if k.startswith("ema_before/")})
+    ema = {k: torch.tensor(d["ema_before/" + k]) for k in keys}
+    model = {k: torch.tensor(d["model/" + k]) for k in keys}
+    ref.ema_update(ema, model, float(d["decay"]))
+    for k in keys:
+        np.testing.assert_array_equal(ema[k].numpy(), d["ema_after/" + k], err_msg=k)
+    # int64 buffer: 0.999*1 + 0.001*2 = 1.001 truncates back to 1 -- the EMA counter never advances
+    assert int(d["ema_before/1.num_batches_tracked"]) == 1 and int(d["model/1.num_batches_tracked"]) == 2
+    assert int(d["ema_after/1.num_batches_tracked"]) == 1
+
+
+def _tiny_cfg():
+    return ref.Cfg(img_size=64, patch=16, dim=128, depth=2, heads=2, num_classes=23)
+
+
+def test_fixmatch_step_matches_reference(golden):
+    for tag, full in (("t0p7", True), ("t0p95", False)):
+        d = golden(f"fixmatch_step_{tag}.npz")
+        cfg = _tiny_cfg()
+        params = {n: torch.tensor(d["init/" + n]) for n, _ in ref.param_shapes(cfg)}
+        fm = ref.FixMatchRef(params, cfg, class_weights=torch.tensor(d["class_weights"]),
+                             thres=float(d["thres"]), lambda_u=1.0, lr=1e-3, ema_decay=0.999)
+        for i in range(int(d["steps"])):
+            out = fm.step(torch.tensor(d[f"x{i}"]), torch.tensor(d[f"y{i}"]), torch.tensor(d[f"uw{i}"]),
+                          torch.tensor(d[f"us{i}"]))
+            np.testing.assert_allclose(out["lx"], d["lx"][i], rtol=1e-6)
+            np.testing.assert_allclose(out["lu"], d["lu"][i], rtol=1e-6, atol=1e-7)
+            assert out["mask_mean"] == d["mask_mean"][i]
+            np.testing.assert_array_equal(out["pseudo_label"].numpy(), d["pseudo_label"][i])
+        for n, _ in ref.param_shapes(cfg):
+            if full:
+                np.testing.assert_allclose(fm.p[n].detach().numpy(), d["final/" + n], rtol=1e-5, atol=1e-7,
+                                           err_msg=n)
+                np.testing.assert_allclose(fm.ema[n].numpy(), d["ema/" + n], rtol=1e-5, atol=1e-7, err_msg=n)
+            else:
+                np.testing.assert_allclose(fm.p[n].detach().double().sum().item(), d["final_sum/" + n],
+                                           rtol=1e-5, atol=1e-5, err_msg=n)
+                np.testing.assert_allclose(fm.ema[n].double().sum().item(), d["ema_sum/" + n], rtol=1e-5,
+                                           atol=1e-5, err_msg=n)
+        # the reference's LR scheduler saw epoch*EVAL_STEP + batch_idx, starting at epoch 1
+        np.testing.assert_array_equal(d["lr_updates"], [2, 3])
+
+
+def test_vit_s_param_count():
+    cfg = ref.Cfg()
+    n = sum(int(np.prod(s)) for _, s in ref.param_shapes(cfg))
+    assert n == 21_674_519
