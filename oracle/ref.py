@@ -32,27 +32,45 @@ def param_shapes(cfg):
     return out
 
 
-def vit_forward(p, x, cfg):
-    """timm VisionTransformer.forward with conformer.Block blocks (code/models/conformer.py:27-72)."""
+def _bf(t):
+    """Round to bf16 and back (the MI355X path's GEMM-operand rounding points)."""
+    return t.bfloat16().float()
+
+
+def vit_forward(p, x, cfg, bf16=False):
+    """timm VisionTransformer.forward with conformer.Block blocks (code/models/conformer.py:27-72).
+
+    bf16=False: the reference arithmetic in fp32.
+    bf16=True : the same arithmetic with the MI355X path's rounding points applied -- GEMM operands
+    (images, LN outputs, qkv, unnormalised softmax numerators, attention output, GELU output and
+    every GEMM weight) rounded to bf16; accumulation, LN/softmax statistics, the residual stream,
+    biases and the CLS head stay fp32.  This is the numerical contract of the bf16 kernels; the
+    difference between the two modes is the bf16 error envelope the parity tests report.
+    """
     B, D, H = x.shape[0], cfg.dim, cfg.heads
     hd = D // H
-    t = F.conv2d(x, p["patch_embed.proj.weight"], p["patch_embed.proj.bias"], stride=cfg.patch)
+    r = _bf if bf16 else (lambda t: t)
+    t = F.conv2d(r(x), r(p["patch_embed.proj.weight"]), p["patch_embed.proj.bias"], stride=cfg.patch)
     t = t.flatten(2).transpose(1, 2)
     t = torch.cat((p["cls_token"].expand(B, -1, -1), t), dim=1) + p["pos_embed"]
     N = t.shape[1]
     for i in range(cfg.depth):
         b = f"blocks.{i}."
-        h = F.layer_norm(t, (D,), p[b + "norm1.weight"], p[b + "norm1.bias"], cfg.eps)
-        qkv = F.linear(h, p[b + "attn.qkv.weight"], p[b + "attn.qkv.bias"])
+        h = r(F.layer_norm(t, (D,), p[b + "norm1.weight"], p[b + "norm1.bias"], cfg.eps))
+        qkv = r(F.linear(h, r(p[b + "attn.qkv.weight"]), p[b + "attn.qkv.bias"]))
         qkv = qkv.reshape(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         attn = (q @ k.transpose(-2, -1)) * hd ** -0.5
-        attn = attn.softmax(dim=-1)
-        o = (attn @ v).transpose(1, 2).reshape(B, N, D)
-        t = t + F.linear(o, p[b + "attn.proj.weight"], p[b + "attn.proj.bias"])
-        h = F.layer_norm(t, (D,), p[b + "norm2.weight"], p[b + "norm2.bias"], cfg.eps)
-        h = F.gelu(F.linear(h, p[b + "mlp.fc1.weight"], p[b + "mlp.fc1.bias"]))
-        t = t + F.linear(h, p[b + "mlp.fc2.weight"], p[b + "mlp.fc2.bias"])
+        if bf16:
+            e = torch.exp(attn - attn.amax(-1, keepdim=True))
+            o = (_bf(e) @ v) / e.sum(-1, keepdim=True)
+        else:
+            o = attn.softmax(dim=-1) @ v
+        o = r(o.transpose(1, 2).reshape(B, N, D))
+        t = t + F.linear(o, r(p[b + "attn.proj.weight"]), p[b + "attn.proj.bias"])
+        h = r(F.layer_norm(t, (D,), p[b + "norm2.weight"], p[b + "norm2.bias"], cfg.eps))
+        h = r(F.gelu(F.linear(h, r(p[b + "mlp.fc1.weight"]), p[b + "mlp.fc1.bias"])))
+        t = t + F.linear(h, r(p[b + "mlp.fc2.weight"]), p[b + "mlp.fc2.bias"])
     t = F.layer_norm(t, (D,), p["norm.weight"], p["norm.bias"], cfg.eps)
     return F.linear(t[:, 0], p["head.weight"], p["head.bias"])
 
@@ -85,8 +103,9 @@ def ema_update(ema_sd, model_sd, decay):
 class FixMatchRef:
     """One-step restatement of FixMatch.train_one's body (code/fixmatch.py:91-131)."""
 
-    def __init__(self, params, cfg, class_weights=None, thres=0.95, lambda_u=1.0, lr=1e-3, ema_decay=0.999):
-        self.cfg = cfg
+    def __init__(self, params, cfg, class_weights=None, thres=0.95, lambda_u=1.0, lr=1e-3, ema_decay=0.999,
+                 bf16=False):
+        self.cfg, self.bf16 = cfg, bf16
         self.names = [n for n, _ in param_shapes(cfg)]
         self.p = {k: params[k].detach().clone().float().requires_grad_(True) for k in self.names}
         self.ema = {k: params[k].detach().clone().float() for k in self.names}
@@ -97,7 +116,7 @@ class FixMatchRef:
 
     def step(self, x, y, uw, us):
         B = x.shape[0]
-        out = vit_forward(self.p, torch.cat((x, uw, us)), self.cfg)
+        out = vit_forward(self.p, torch.cat((x, uw, us)), self.cfg, bf16=self.bf16)
         ox = out[:B]
         ow, os_ = out[B:].chunk(2)
         lx = poly_ce(ox, y, self.cw)

@@ -281,7 +281,8 @@ def test_consistency_kernel_vs_reference_fixture(golden):
         np.testing.assert_array_equal(mask.cpu().numpy()[~near], d["mask"][~near].astype(np.uint8))
         np.testing.assert_allclose(out[0].item(), float(d["loss"]), rtol=1e-5)
         np.testing.assert_allclose(out[1].item(), float(d["mask_mean"]), rtol=0, atol=1.0 / n * near.sum())
-        np.testing.assert_allclose(rows.cpu().numpy(), d["ce_rows"], rtol=1e-5, atol=1e-6)
+        # the fixture's ce_rows are the reference's per-row CE BEFORE `* mask` (code/loss.py:157-160)
+        np.testing.assert_allclose(rows.cpu().numpy(), d["ce_rows"] * d["mask"], rtol=1e-5, atol=1e-6)
         np.testing.assert_allclose(dls.cpu().numpy(), d["grad_logits_s"], rtol=1e-4, atol=1e-7)
 
 

@@ -83,3 +83,17 @@ def test_vit_s_param_count():
     cfg = ref.Cfg()
     n = sum(int(np.prod(s)) for _, s in ref.param_shapes(cfg))
     assert n == 21_674_519
+
+
+def test_bf16_envelope():
+    """The oracle's bf16 mode (the MI355X path's rounding points) stays within a few 1e-3 of the
+    fp32 reference arithmetic -- the envelope the GPU parity tests are bounded by."""
+    import torch
+    cfg = ref.Cfg(img_size=64, patch=16, dim=128, depth=2, heads=2, num_classes=23)
+    p = ref.random_params(cfg, seed=11, head_std=0.6)
+    x = torch.randn(8, 3, 64, 64, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        l32 = ref.vit_forward(p, x, cfg)
+        l16 = ref.vit_forward(p, x, cfg, bf16=True)
+    rel = (l16 - l32).abs().max().item() / l32.abs().max().item()
+    assert 1e-4 < rel < 2e-2, rel
