@@ -23,7 +23,7 @@
 namespace {
 
 struct AttnArgs {
-  const bf16* qkv; bf16* o; float* lse;
+  const bf16* qkv; bf16* o; float* lse; float* delta;
   const bf16* dout; bf16* dqkv;
   int ldqkv, ldo, lddo, lddqkv;
   int T, H;
@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     for (int j = 0; j < 8; ++j) delta += (float)df0[j] * (float)of0[j] + (float)df1[j] * (float)of1[j];
     delta += __shfl_xor(delta, 16, 64);
     delta += __shfl_xor(delta, 32, 64);
+    if (qv && g == 0) a.delta[(size_t)bh * T + q] = delta;  // consumed by attn_bwd_dkv_kernel
     const float lq = qv ? a.lse[(size_t)bh * T + q] : 0.f;
 
     f32x4 dq[4];
@@ -224,15 +225,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   load_head_tile(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   for (int t = threadIdx.x; t < TP; t += blockDim.x) lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] : INFINITY;
-  for (int t = w; t < TP; t += 4) {  // delta[t] = sum_d dO[t][d] * O[t][d]
-    float v = 0.f;
-    if (t < T) {
-      const size_t tok = (size_t)img * T + t;
-      v = (float)a.dout[tok * a.lddo + h * 64 + lane] * (float)a.o[tok * a.ldo + h * 64 + lane];
-    }
-    v = warp_sum(v);
-    if (lane == 0) del_s[t] = v;
-  }
+  for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
   __syncthreads();
 
   const int nkt = (T + 15) >> 4;
@@ -309,22 +302,23 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
   if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || ldo < H * 64 || (ldqkv % 8) || (ldo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse) return ES_BAD_ARG;
-  AttnArgs a{(const bf16*)qkv, (bf16*)o, lse, nullptr, nullptr, ldqkv, ldo, 0, 0, T, H, scale};
+  AttnArgs a{(const bf16*)qkv, (bf16*)o, lse, nullptr, nullptr, nullptr, ldqkv, ldo, 0, 0, T, H, scale};
   const int nkc = (T + 31) / 32;
   const size_t lds = 2 * (size_t)nkc * 32 * 128;
   ATTN_DISPATCH(attn_fwd_kernel, nkc, nimg * H, lds, stream, a);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-// dout [nimg*T, lddo] + forward (qkv, o, lse) -> dqkv [nimg*T, lddqkv] (q, k and v parts)
-int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
-                void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
+// dout [nimg*T, lddo] + forward (qkv, o, lse) -> dqkv [nimg*T, lddqkv] (q, k and v parts).
+// delta: workspace [nimg*H*T] fp32 (rowsum(dO*O), written by the dQ pass, read by the dK/dV pass).
+int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
+                int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
   if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
       (lddqkv % 8) || (ldo % 8) || (lddo % 8))
     return ES_BAD_SHAPE;
-  if (!qkv || !o || !lse || !dout || !dqkv) return ES_BAD_ARG;
-  AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo, lddqkv,
-             T, H, scale};
+  if (!qkv || !o || !lse || !delta || !dout || !dqkv) return ES_BAD_ARG;
+  AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, delta, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
+             lddqkv, T, H, scale};
   const int nkc = (T + 31) / 32;
   const size_t lds_dq = 2 * (size_t)nkc * 32 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nkc * 32 * 4;

@@ -28,6 +28,7 @@ enum Epi {
   EPI_DGELU = 3,      // C bf16 = acc * gelu'(aux_bf16)
   EPI_F32 = 4,        // C f32 = acc (+bias)
   EPI_PATCH = 5,      // C f32 at token row (img*(np+1)+1+p) = acc + bias + pos[1+p]
+  EPI_GELU_ACT = 6,   // C bf16 = gelu(acc+bias) only (inference: no pre-activation kept)
 };
 
 struct NTArgs {
@@ -124,6 +125,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
         bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
         *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
         *(bf16x4*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
+      } else if constexpr (EPI == EPI_GELU_ACT) {
+        bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
+        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = a;
       } else if constexpr (EPI == EPI_F32_RESID) {
         const f32x4 res = *(const f32x4*)((const float*)p.aux + (size_t)m * p.ldaux + n);
         *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v + res;
@@ -239,25 +243,74 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TNArgs p) {
   }
 }
 
-// out[i] = (accumulate ? out[i] : 0) + sum_s P[s][i]   (n % 4 == 0)
+// out[i] = (accumulate ? out[i] : 0) + sum_s P[s][i]   (n % 4 == 0); 4 independent partial sums
+// per thread keep 4 slab loads in flight.
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restrict__ out, int S, int n,
                                      int accumulate) {
   const int n4 = n >> 2;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
-    f32x4 s = accumulate ? ((const f32x4*)out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k = 0; k < S; ++k) s += ((const f32x4*)(P + (size_t)k * n))[i];
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+    int k = 0;
+    for (; k + 4 <= S; k += 4) {
+      s0 += ((const f32x4*)(P + (size_t)k * n))[i];
+      s1 += ((const f32x4*)(P + (size_t)(k + 1) * n))[i];
+      s2 += ((const f32x4*)(P + (size_t)(k + 2) * n))[i];
+      s3 += ((const f32x4*)(P + (size_t)(k + 3) * n))[i];
+    }
+    for (; k < S; ++k) s0 += ((const f32x4*)(P + (size_t)k * n))[i];
+    f32x4 s = (s0 + s1) + (s2 + s3);
+    if (accumulate) s += ((const f32x4*)out)[i];
     ((f32x4*)out)[i] = s;
   }
 }
 
-// P[gblk][n] = sum over this block's rows of Y[m][n]  (bias gradients)
-__global__ void colsum_partial_kernel(const bf16* __restrict__ Y, int ld, int M, int N, int rows_per,
-                                      float* __restrict__ P) {
+// Column sums of a bf16 [M, N] matrix (bias gradients), HBM-streaming: each thread owns one
+// 8-column chunk (16-B loads) and strides over rows; per-block partials P[block][N].
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restrict__ Y, int ld, int M, int N,
+                                                             int rows_per, float* __restrict__ P) {
+  __shared__ float red[256 * 8];
+  const int nc = N >> 3;                 // 8-column chunks
+  const int groups = 256 / nc;           // row groups per block (nc <= 256)
+  const int t = threadIdx.x, c = t % nc, rg = t / nc;
   const int m0 = blockIdx.x * rows_per, m1 = min(m0 + rows_per, M);
-  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (rg < groups) {
+    for (int m = m0 + rg; m < m1; m += groups) {
+      const bf16x8 v = *(const bf16x8*)(Y + (size_t)m * ld + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[t * 8 + j] = acc[j];
+  __syncthreads();
+  for (int col = t; col < N; col += 256) {
+    const int cc = col >> 3, j = col & 7;
     float s = 0.f;
-    for (int m = m0; m < m1; ++m) s += (float)Y[(size_t)m * ld + n];
-    P[(size_t)blockIdx.x * N + n] = s;
+    for (int g = 0; g < groups; ++g) s += red[(g * nc + cc) * 8 + j];
+    P[(size_t)blockIdx.x * N + col] = s;
+  }
+}
+
+// out[n] (+)= sum_g P[g][n]: 64 columns x 4 row-groups per block, then a 4-way LDS combine.
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ P, float* __restrict__ out,
+                                                              int G, int N, int accumulate) {
+  __shared__ float red[4][64];
+  const int col = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
+  float s0 = 0.f, s1 = 0.f;
+  if (col < N) {
+    int g = rg;
+    for (; g + 4 < G; g += 8) {
+      s0 += P[(size_t)g * N + col];
+      s1 += P[(size_t)(g + 4) * N + col];
+    }
+    for (; g < G; g += 4) s0 += P[(size_t)g * N + col];
+  }
+  red[rg][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (rg == 0 && col < N) {
+    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    out[col] = accumulate ? out[col] + s : s;
   }
 }
 
@@ -285,6 +338,7 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     case EPI_DGELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_DGELU>, grid, 256, lds, stream, a); break;
     case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, 256, lds, stream, a); break;
     case EPI_PATCH: hipLaunchKernelGGL(gemm_nt_kernel<EPI_PATCH>, grid, 256, lds, stream, a); break;
+    case EPI_GELU_ACT: hipLaunchKernelGGL(gemm_nt_kernel<EPI_GELU_ACT>, grid, 256, lds, stream, a); break;
     default: return ES_BAD_ARG;
   }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -323,15 +377,22 @@ int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, h
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-// bias gradient: out[n] (+)= sum_m Y[m][n]; workspace >= blocks*N floats (blocks <= 1024)
+// bias gradient: out[n] (+)= sum_m Y[m][n]; workspace >= blocks*N floats.  N % 8 == 0, N <= 2048.
 int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
               hipStream_t stream) {
-  if (M <= 0 || N <= 0 || N % 4 || blocks <= 0) return ES_BAD_SHAPE;
+  if (M <= 0 || N <= 0 || N % 8 || N > 2048 || ld % 8 || blocks <= 0) return ES_BAD_SHAPE;
+  if (!Y || !workspace || !out) return ES_BAD_ARG;
   const int rows_per = (M + blocks - 1) / blocks;
   const int G = (M + rows_per - 1) / rows_per;
   hipLaunchKernelGGL(colsum_partial_kernel, G, 256, 0, stream, (const bf16*)Y, ld, M, N, rows_per, workspace);
-  int rg = (N / 4 + 255) / 256;
-  hipLaunchKernelGGL(splitk_reduce_kernel, rg, 256, 0, stream, workspace, out, G, N, accumulate);
+  hipLaunchKernelGGL(reduce_partials_kernel, (N + 63) / 64, 256, 0, stream, workspace, out, G, N, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// out[n] (+)= sum_g P[g][n]  (partials of the LayerNorm / colsum kernels)
+int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream) {
+  if (G <= 0 || N <= 0) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(reduce_partials_kernel, (N + 63) / 64, 256, 0, stream, P, out, G, N, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

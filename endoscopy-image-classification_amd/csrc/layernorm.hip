@@ -115,15 +115,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
   }
 }
 
-__global__ void reduce_rows_kernel(const float* __restrict__ P, float* __restrict__ out, int S, int n, int accumulate) {
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    float s = accumulate ? out[i] : 0.f;
-    for (int k = 0; k < S; ++k) s += P[(size_t)k * n + i];
-    out[i] = s;
-  }
-}
-
 }  // namespace
+
+extern "C" int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream);
 
 #define LN_DISPATCH(KER, V_, GRID, STREAM, ...)                                \
   switch (V_) {                                                                \
@@ -158,10 +152,10 @@ int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const f
   float* pb = workspace + (size_t)grid * D;
   LN_DISPATCH(ln_bwd_kernel, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,
               (bf16*)dxb, lddxb, pg, pb, M);
-  const int rg = (D + 255) / 256;
-  hipLaunchKernelGGL(reduce_rows_kernel, rg, 256, 0, stream, pg, dgamma, grid, D, accumulate);
-  hipLaunchKernelGGL(reduce_rows_kernel, rg, 256, 0, stream, pb, dbeta, grid, D, accumulate);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  if (hipGetLastError() != hipSuccess) return ES_HIP_ERROR;
+  int rc = es_reduce_partials(pg, dgamma, grid, D, accumulate, stream);
+  if (rc) return rc;
+  return es_reduce_partials(pb, dbeta, grid, D, accumulate, stream);
 }
 
 }  // extern "C"

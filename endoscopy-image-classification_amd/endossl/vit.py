@@ -26,7 +26,7 @@ import torch.nn as nn
 from . import _lib
 from ._lib import call, ptr
 
-EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH = range(6)
+EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT = range(7)
 
 
 def _rup(x, m):
@@ -126,7 +126,7 @@ class _Acts:
         self.qkv = z(Lk, Mp, 3 * D, dt=b16)
         self.o = z(Lk, Mp, D, dt=b16)
         self.lse = z(Lk, n * cfg.heads * cfg.T)
-        self.pre = z(Lk, Mp, Hd, dt=b16)
+        self.pre = z(Lk if train else 0, Mp, Hd, dt=b16)
         self.act = z(Lk, Mp, Hd, dt=b16)
         self.xhat = z(n, D)
         self.rstd_cls = z(n)
@@ -150,6 +150,7 @@ class _Grads:
         self.do = z(Mp, D, dt=b16)
         self.dpatch = z(_rup(n * cfg.np, 256), D, dt=b16)
         self.dyn = z(n, D)
+        self.delta = z(n * cfg.heads * cfg.T)
 
 
 class Engine:
@@ -271,9 +272,14 @@ class Engine:
             call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
                  ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
                  cfg.eps, s)
-            self._gemm("fc1_fwd", EPI_GELU, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
-                 ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.pre[li]), Hd, ptr(A.act[li]), None, 0, M, Hd, D,
-                 0, s)
+            if train:
+                self._gemm("fc1_fwd", EPI_GELU, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+                           ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.pre[li]), Hd, ptr(A.act[li]), None, 0, M,
+                           Hd, D, 0, s)
+            else:
+                self._gemm("fc1_fwd", EPI_GELU_ACT, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+                           ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.act[li]), Hd, None, None, 0, M, Hd, D, 0,
+                           s)
             call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
                  ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xout), D, None, ptr(xmid), D, M, D, Hd, 0, s)
         xl = A.x[cfg.depth] if train else A.x[cfg.depth & 1]
@@ -295,13 +301,13 @@ class Engine:
 
     def _bgrad(self, dy, N, M, out):
         ws = self.workspace()
-        call("es_colsum", ptr(dy), N, M, N, ptr(ws), 256, ptr(out), 0, _lib.stream())
+        call("es_colsum", ptr(dy), N, M, N, ptr(ws), 512, ptr(out), 0, _lib.stream())
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M):
         D = self.cfg.dim
         ws = self.workspace()
         call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
-             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
+             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 512, M, D, 0, _lib.stream())
 
     def backward(self, flat, grad, dlogits):
         """dlogits fp32 [n, C] for the last train forward -> grad (flat fp32, overwritten)."""
@@ -340,7 +346,8 @@ class Engine:
                  None, None, 0, M, D, D, 0, s)
             self._wgrad(G.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"))
             self._bgrad(G.dxmb, D, M, gv(b + "attn.proj.bias"))
-            call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.do), D, ptr(G.dqkv),
+            call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
+                 ptr(G.dqkv),
                  3 * D, n, T, H, 64 ** -0.5, s)
             call("es_gemm_nt", EPI_F32, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)

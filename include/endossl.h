@@ -34,6 +34,7 @@ int es_abi_version(void);
  *   epi 3: C bf16 = acc * GELU'(aux bf16)             (fc2 dgrad through the activation)
  *   epi 4: C f32 = acc (+bias)                        (dgrad into LayerNorm backward)
  *   epi 5: C f32 at token row img*(np+1)+1+p = acc + bias + aux[1+p]   (patch embed + pos_embed)
+ *   epi 6: C bf16 = GELU(acc+bias) only                (fc1 + act in inference forwards)
  * N % 128 == 0, K % 64 == 0; A readable for round_up(M,128) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
@@ -47,12 +48,15 @@ int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, h
 /* bias gradient: out[n] (+)= sum_m Y[m][n]  (workspace >= blocks*N floats) */
 int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
               hipStream_t stream);
+/* out[n] (+)= sum_g P[g][n]  (per-workgroup partials -> parameter gradient) */
+int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream);
 
 /* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 256 --------------- */
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream);
-int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
-                void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
+/* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass) */
+int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
+                int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
 
 /* ---- LayerNorm(eps) (code/models/conformer.py:58,60,65) -------------------------------------- */
 int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,

@@ -97,3 +97,23 @@ def test_bf16_envelope():
         l16 = ref.vit_forward(p, x, cfg, bf16=True)
     rel = (l16 - l32).abs().max().item() / l32.abs().max().item()
     assert 1e-4 < rel < 2e-2, rel
+
+
+def test_bf16_rounding_is_discontinuous_at_depth():
+    """Why the full-depth GPU bar is envelope-based: under the bf16 contract a 1e-7 relative nudge
+    of the weights (which only flips bf16 rounding decisions) moves ViT-S logits by a sizeable
+    fraction of the whole bf16-vs-fp32 envelope, while the fp32 arithmetic barely moves.  Any two
+    bf16 implementations of the 12-layer step therefore agree only to within that envelope."""
+    import torch
+    cfg = ref.Cfg(depth=12)
+    p = ref.random_params(cfg, seed=11, head_std=0.3)
+    q = {k: v * (1 + 1e-7 * torch.randn(v.shape, generator=torch.Generator().manual_seed(2))) for k, v in p.items()}
+    x = torch.randn(2, 3, 224, 224, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        a16, b16 = ref.vit_forward(p, x, cfg, bf16=True), ref.vit_forward(q, x, cfg, bf16=True)
+        a32, b32 = ref.vit_forward(p, x, cfg), ref.vit_forward(q, x, cfg)
+    envelope = (a16 - a32).abs().max().item()
+    drift16 = (a16 - b16).abs().max().item()
+    drift32 = (a32 - b32).abs().max().item()
+    assert drift16 > 0.2 * envelope
+    assert drift32 < 1e-3 * envelope * 10
