@@ -40,6 +40,127 @@ struct NTArgs {
 // 128-byte rows (64 bf16), 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7).
 __device__ __forceinline__ int swz128(int r, int c) { return c ^ ((r >> 1) & 7); }
 
+// One lane's 4 consecutive outputs C[m][n .. n+3] through the fused epilogue.
+template <int EPI>
+__device__ __forceinline__ void epi_store(const NTArgs& p, int m, int n, f32x4 v) {
+  if (p.bias) v += *(const f32x4*)(p.bias + n);
+  if constexpr (EPI == EPI_BF16) {
+    bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+  } else if constexpr (EPI == EPI_GELU) {
+    bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
+    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+    *(bf16x4*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
+  } else if constexpr (EPI == EPI_GELU_ACT) {
+    bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
+    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = a;
+  } else if constexpr (EPI == EPI_F32_RESID) {
+    const f32x4 res = *(const f32x4*)((const float*)p.aux + (size_t)m * p.ldaux + n);
+    *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v + res;
+  } else if constexpr (EPI == EPI_DGELU) {
+    const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (size_t)m * p.ldaux + n);
+    bf16x4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (bf16)(v[i] * gelu_grad_f((float)pre[i]));
+    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+  } else if constexpr (EPI == EPI_F32) {
+    *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v;
+  } else if constexpr (EPI == EPI_PATCH) {
+    const int img = m / p.np, pi = m - img * p.np;
+    const f32x4 pos = *(const f32x4*)((const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n);
+    *(f32x4*)((float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n) = v + pos;
+  }
+}
+
+// v2: 256x128 output tile, 8 waves (4 M x 2 N, 64x64 each), 3-stage LDS ring (48 KiB per stage,
+// 144 KiB total: one workgroup per CU).  Stage k+2 is issued right after the barrier that
+// publishes stage k, so two stages stay in flight behind the MFMAs; the wait for stage k is a
+// COUNTED vmcnt (6 = the younger stage's glds) and the barrier is a raw s_barrier, never
+// __syncthreads() (which would drain every glds -- cdna_hip_programming.md §5).
+constexpr int BM2 = 256;
+constexpr int STAGE2 = (BM2 + BN) * BK * 2;  // 49152 B
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntn = p.N / BN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * BM2, n0 = (wg % ntn) * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int g = lane >> 4, r = lane & 15;
+
+  const bf16* ga[4];
+  const bf16* gb[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (w * 4 + j) * 8 + (lane >> 3);
+    ga[j] = p.A + (size_t)(m0 + row) * p.lda + swz128(row, lane & 7) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (w * 2 + j) * 8 + (lane >> 3);
+    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + swz128(row, lane & 7) * 8;
+  }
+  auto issue = [&](int buf, int k0) {
+    char* As = smem + buf * STAGE2;
+    char* Bs = As + BM2 * BK * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_global_load_lds(ga[j] + k0, LDS_PTR(As + (w * 4 + j) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      __builtin_amdgcn_global_load_lds(gb[j] + k0, LDS_PTR(Bs + (w * 2 + j) * 1024), 16, 0, 0);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  issue(0, 0);
+  if (nk > 1) issue(1, BK);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + 2 < nk) issue(buf == 0 ? 2 : buf - 1, (kt + 2) * BK);
+    const char* As = smem + buf * STAGE2;
+    const char* Bs = As + BM2 * BK * 2;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra = wm * 64 + i * 16 + r;
+        af[i] = *(const bf16x8*)(As + ra * 128 + swz128(ra, kk * 4 + g) * 16);
+        const int rb = wn * 64 + i * 16 + r;
+        bfr[i] = *(const bf16x8*)(Bs + rb * 128 + swz128(rb, kk * 4 + g) * 16);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bfr[ni], af[mi], acc[mi][ni]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    buf = buf == 2 ? 0 : buf + 1;
+  }
+
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + mi * 16 + r;
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) epi_store<EPI>(p, m, n0 + wn * 64 + ni * 16 + 4 * g, acc[mi][ni]);
+  }
+}
+
+
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -110,41 +231,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
     const int m = m0 + wm * 64 + mi * 16 + r;
     if (m >= p.M) continue;
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wn * 64 + ni * 16 + 4 * g;
-      f32x4 v = acc[mi][ni];
-      if (p.bias) {
-        const f32x4 b = *(const f32x4*)(p.bias + n);
-        v += b;
-      }
-      if constexpr (EPI == EPI_BF16) {
-        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-      } else if constexpr (EPI == EPI_GELU) {
-        bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
-        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-        *(bf16x4*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
-      } else if constexpr (EPI == EPI_GELU_ACT) {
-        bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
-        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = a;
-      } else if constexpr (EPI == EPI_F32_RESID) {
-        const f32x4 res = *(const f32x4*)((const float*)p.aux + (size_t)m * p.ldaux + n);
-        *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v + res;
-      } else if constexpr (EPI == EPI_DGELU) {
-        const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (size_t)m * p.ldaux + n);
-        bf16x4 o;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (bf16)(v[i] * gelu_grad_f((float)pre[i]));
-        *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-      } else if constexpr (EPI == EPI_F32) {
-        *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v;
-      } else if constexpr (EPI == EPI_PATCH) {
-        const int img = m / p.np, pi = m - img * p.np;
-        const f32x4 pos = *(const f32x4*)((const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n);
-        *(f32x4*)((float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n) = v + pos;
-      }
-    }
+    for (int ni = 0; ni < 4; ++ni) epi_store<EPI>(p, m, n0 + wn * 64 + ni * 16 + 4 * g, acc[mi][ni]);
   }
 }
 
@@ -317,18 +404,37 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
 }  // namespace
 
 // ----------------------------------------------------------------- C-ABI entry points
+static int g_gemm_variant = 1;
+
 extern "C" {
 
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C,
                int ldc, void* C2, const void* aux, int ldaux, int M, int N, int K, int np,
                hipStream_t stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || (N % BN) || (K % BK) || (lda % 8) || (ldb % 8) || (ldc % 4))
+  if (M <= 0 || N <= 0 || K <= 0 || (N % BN) || (K % BK) || (lda % 8) || (ldb % 8) || (ldc % 4))  // NOLINT
     return ES_BAD_SHAPE;
   if (!A || !B || !C) return ES_BAD_ARG;
   if ((epi == EPI_GELU && !C2) || ((epi == EPI_F32_RESID || epi == EPI_DGELU || epi == EPI_PATCH) && !aux))
     return ES_BAD_ARG;
   if (epi == EPI_PATCH && np <= 0) return ES_BAD_ARG;
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
+  if (g_gemm_variant == 1) {
+    const int grid = ((M + BM2 - 1) / BM2) * (N / BN);
+    const size_t lds = 3 * STAGE2;
+#define L2(E) allow_lds(gemm_nt256_kernel<E>, lds); hipLaunchKernelGGL(gemm_nt256_kernel<E>, grid, 512, lds, stream, a); break;
+    switch (epi) {
+      case EPI_BF16: L2(EPI_BF16)
+      case EPI_GELU: L2(EPI_GELU)
+      case EPI_F32_RESID: L2(EPI_F32_RESID)
+      case EPI_DGELU: L2(EPI_DGELU)
+      case EPI_F32: L2(EPI_F32)
+      case EPI_PATCH: L2(EPI_PATCH)
+      case EPI_GELU_ACT: L2(EPI_GELU_ACT)
+      default: return ES_BAD_ARG;
+    }
+#undef L2
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   const int grid = ((M + BM - 1) / BM) * (N / BN);
   const size_t lds = 2 * STAGE_BYTES;
   switch (epi) {
@@ -342,6 +448,14 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     default: return ES_BAD_ARG;
   }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Tuning knob: which NT kernel family es_gemm_nt launches (0 = 128x128 2-stage, 1 = 256x128
+// 3-stage ring).  Returns the previous value.
+int es_set_gemm_variant(int v) {
+  const int old = g_gemm_variant;
+  g_gemm_variant = v;
+  return old;
 }
 
 // workspace floats needed by es_gemm_tn for `splits` splits

@@ -18,6 +18,7 @@ V, I, L, F, Z = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ct
 SIGNATURES = {
     "es_abi_version": (I, []),
     "es_gemm_nt": (I, [I, V, I, V, I, V, V, I, V, V, I, I, I, I, I, V]),
+    "es_set_gemm_variant": (I, [I]),
     "es_gemm_tn_workspace": (Z, [I, I, I]),
     "es_gemm_tn": (I, [V, I, V, I, I, I, I, I, V, V, I, V]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),

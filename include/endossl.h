@@ -35,9 +35,11 @@ int es_abi_version(void);
  *   epi 4: C f32 = acc (+bias)                        (dgrad into LayerNorm backward)
  *   epi 5: C f32 at token row img*(np+1)+1+p = acc + bias + aux[1+p]   (patch embed + pos_embed)
  *   epi 6: C bf16 = GELU(acc+bias) only                (fc1 + act in inference forwards)
- * N % 128 == 0, K % 64 == 0; A readable for round_up(M,128) rows. */
+ * N % 128 == 0, K % 64 == 0; A readable for round_up(M,256) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
+/* tuning knob: NT kernel family (0 = 128x128 two-stage, 1 = 256x128 three-stage ring); returns the old one */
+int es_set_gemm_variant(int variant);
 /* weight gradient: out[N1,N2] (+)= sum_m A1[m,N1]^T A2[m,N2], token axis split `splits` ways into
  * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced.  N1,N2 % 128 == 0; rows in
  * [M, round_up(M,64)) of A1 must be zero. */

@@ -1,0 +1,95 @@
+"""GEMM microbenchmark: every NT / TN shape of the ViT-S F1 step, kernel variants A/B'd in ONE
+process (interleaved rounds, median), random operands.  Prints TFLOP/s per shape and variant.
+
+  python scripts/gemm_bench.py [--variants 0,1] [--rounds 5] [--iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+import torch  # noqa: E402
+
+from endossl import _lib  # noqa: E402
+from endossl._lib import call, ptr  # noqa: E402
+
+M_T, M_W = 512 * 197, 448 * 197
+D, HD = 384, 1536
+# (name, epi, M, N, K)  -- NT: C[M,N] = A[M,K] B[N,K]^T
+NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 1, M_T, HD, D),
+      ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 3, M_T, HD, D),
+      ("fc1_dgrad", 4, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 4, M_T, D, 3 * D)]
+# (name, M, N1, N2)  -- TN: out[N1,N2] = sum_m A1[m,N1] A2[m,N2]
+TN = [("fc2_wgrad", M_T, D, HD), ("fc1_wgrad", M_T, HD, D), ("proj_wgrad", M_T, D, D), ("qkv_wgrad", M_T, 3 * D, D)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    lib = _lib.load()
+    lib.es_set_gemm_variant.restype = _lib.I
+    lib.es_set_gemm_variant.argtypes = [_lib.I]
+    variants = [int(v) for v in args.variants.split(",")]
+    dev = "cuda"
+    torch.manual_seed(0)
+    s = _lib.stream()
+    Mp = (M_T + 255) // 256 * 256
+    A = torch.randn(Mp, HD * 2, device=dev).bfloat16()
+    Bw = (torch.randn(HD * 2, HD * 2, device=dev) * 0.05).bfloat16()
+    bias = torch.randn(HD * 2, device=dev)
+    C = torch.empty(Mp, HD * 2, device=dev)  # big enough for f32 [M, 1536]
+    C2 = torch.empty(Mp, HD, device=dev, dtype=torch.bfloat16)
+    aux = torch.randn(Mp, HD, device=dev)
+    results = {}
+    for name, epi, M, N, K in NT:
+        flops = 2.0 * M * N * K
+        times = {v: [] for v in variants}
+        for _ in range(args.rounds):
+            for v in variants:
+                lib.es_set_gemm_variant(v)
+                auxp = aux if epi in (2,) else (aux.bfloat16() if epi == 3 else None)
+                st = [ptr(A), K, ptr(Bw), K, ptr(bias) if epi not in (3, 4) else None, ptr(C), N,
+                      ptr(C2) if epi == 1 else None, ptr(auxp) if auxp is not None else None, N, M, N, K, 0, s]
+                call("es_gemm_nt", epi, *st)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    call("es_gemm_nt", epi, *st)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.iters)
+        row = {}
+        for v in variants:
+            t = sorted(times[v])[len(times[v]) // 2]
+            row[v] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1)}
+        results[name] = row
+        print(name, json.dumps(row), flush=True)
+    ws = torch.empty(64 * HD * D, device=dev)
+    out = torch.empty(HD, HD, device=dev)
+    for name, M, N1, N2 in TN:
+        flops = 2.0 * M * N1 * N2
+        tiles = (N1 // 128) * (N2 // 128)
+        splits = max(1, min((M + 63) // 64, -(-512 // tiles)))
+        for _ in range(2):
+            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, s)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.iters):
+            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, s)
+        e1.record()
+        torch.cuda.synchronize()
+        t = e0.elapsed_time(e1) / args.iters
+        results[name] = {"tn": {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}}
+        print(name, json.dumps(results[name]), flush=True)
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    json.dump(results, open(os.path.join(out_dir, "gemm_bench.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

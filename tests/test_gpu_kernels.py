@@ -40,8 +40,15 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 384, 384), (128, 128, 64)])
-def test_gemm_nt_exact_integers(M, N, K):
+@pytest.fixture(params=[0, 1], ids=["v0_128x128", "v1_256x128"])
+def gemm_variant(request):
+    old = _lib.load().es_set_gemm_variant(request.param)
+    yield request.param
+    _lib.load().es_set_gemm_variant(old)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 384, 384), (128, 128, 64), (5000, 1152, 1536)])
+def test_gemm_nt_exact_integers(M, N, K, gemm_variant):
     g = torch.Generator().manual_seed(M + N + K)
     A = _pad_rows(_int_bf16(M, K, gen=g))
     B = _int_bf16(N, K, gen=g)
@@ -56,7 +63,7 @@ def test_gemm_nt_exact_integers(M, N, K):
     torch.testing.assert_close(Cb.float(), ref.bfloat16().float(), rtol=0, atol=0)
 
 
-def test_gemm_nt_epilogues_vs_fp32():
+def test_gemm_nt_epilogues_vs_fp32(gemm_variant):
     torch.manual_seed(0)
     M, N, K = 777, 512, 384
     A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
@@ -85,7 +92,7 @@ def test_gemm_nt_epilogues_vs_fp32():
     torch.testing.assert_close(dpre.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-def test_gemm_nt_patch_epilogue():
+def test_gemm_nt_patch_epilogue(gemm_variant):
     torch.manual_seed(1)
     n, npch, D, K = 3, 16, 128, 768
     M = n * npch

@@ -193,7 +193,8 @@ def test_fixmatch_trainer_vs_reference_train_one(golden, tag):
     rec["max_ema_delta"] = worst_e
     _record(f"trainer_{tag}", **{k: (json.dumps(v) if isinstance(v, dict) else v) for k, v in rec.items()})
     assert worst <= 2e-3 * steps + 1e-5
-    assert worst_e <= 1e-3 * 2e-3 * steps + 1e-6
+    # EMA deviation accumulates (1-d) * sum_t (2*lr*t): each step's param deviation is <= 2*lr*t
+    assert worst_e <= 1e-3 * 2e-3 * steps * (steps + 1) / 2 + 1e-6
 
 
 def test_vit_s_small_batch_vs_oracle():
