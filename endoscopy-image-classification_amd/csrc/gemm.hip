@@ -161,9 +161,43 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
 }
 
 
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
+// vmcnt immediates must be literals: counted waits for the stage pipelines below.
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
+    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// v0 family: 128x128 output tile, 4 waves (2x2, 64x64 each), K step BKT in {32, 64}, NST-stage
+// LDS ring.  Stage k+NST-1 is issued right after the barrier that publishes stage k; the wait
+// for stage k is a counted vmcnt (the younger stages' glds stay in flight), the barrier a raw
+// s_barrier.  Small footprints (BKT=32: 16 KiB per stage) let 3-4 workgroups share a CU, so one
+// tile's epilogue overlaps other tiles' MFMAs.
+//   BKT=64: 128-B LDS rows, chunk c of row r at c ^ ((r>>1)&7)
+//   BKT=32:  64-B LDS rows, chunk c of row r at c ^ ((r>>2)&3)   (both conflict-free for the
+//            16-row x 16-B fragment reads)
+template <int BKT>
+__device__ __forceinline__ int swzk(int r, int c) {
+  if constexpr (BKT == 64) return c ^ ((r >> 1) & 7);
+  else return c ^ ((r >> 2) & 3);
+}
+
+template <int EPI, int BKT, int NST>
+__global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int ROWB = BKT * 2;              // bytes per LDS row
+  constexpr int RPI = 1024 / ROWB;           // rows per 1-KiB glds instruction
+  constexpr int CPR = ROWB / 16;             // 16-B chunks per row
+  constexpr int IPW = (BM / RPI) / 4;        // glds instructions per wave per operand per stage
+  constexpr int PER = 2 * IPW;               // per stage per wave
+  constexpr int TILE = BM * ROWB;            // bytes per operand tile
+  constexpr int STAGE = 2 * TILE;
   const int ntn = p.N / BN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
@@ -171,23 +205,22 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
   const int wm = w >> 1, wn = w & 1;
   const int g = lane >> 4, r = lane & 15;
 
-  // ---- global -> LDS staging addresses (per lane, constant over k) ----
-  const bf16* ga[4];
-  const bf16* gb[4];
+  const bf16* ga[IPW];
+  const bf16* gb[IPW];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (w * 4 + j) * 8 + (lane >> 3);
-    const int lc = swz128(row, lane & 7);
+  for (int j = 0; j < IPW; ++j) {
+    const int row = (w * IPW + j) * RPI + lane / CPR;
+    const int lc = swzk<BKT>(row, lane % CPR);
     ga[j] = p.A + (size_t)(m0 + row) * p.lda + lc * 8;
     gb[j] = p.B + (size_t)(n0 + row) * p.ldb + lc * 8;
   }
-  auto stage = [&](int buf, int k0) {
-    char* As = smem + buf * STAGE_BYTES;
-    char* Bs = As + BM * BK * 2;
+  auto issue = [&](int buf, int k0) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + TILE;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      __builtin_amdgcn_global_load_lds(ga[j] + k0, LDS_PTR(As + (w * 4 + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(gb[j] + k0, LDS_PTR(Bs + (w * 4 + j) * 1024), 16, 0, 0);
+    for (int j = 0; j < IPW; ++j) {
+      __builtin_amdgcn_global_load_lds(ga[j] + k0, LDS_PTR(As + (w * IPW + j) * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(gb[j] + k0, LDS_PTR(Bs + (w * IPW + j) * 1024), 16, 0, 0);
     }
   };
 
@@ -197,32 +230,38 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(NTArgs p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-    const char* As = smem + cur * STAGE_BYTES;
-    const char* Bs = As + BM * BK * 2;
+  const int nk = p.K / BKT;
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) issue(st, st * BKT);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int younger = min(NST - 2, nk - 1 - kt);
+    wait_vmcnt(younger * PER);
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nk) {
+      int nb = buf + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
+      issue(nb, (kt + NST - 1) * BKT);
+    }
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + TILE;
+#pragma unroll
+    for (int kk = 0; kk < BKT / 32; ++kk) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ra = wm * 64 + i * 16 + r;
-        af[i] = *(const bf16x8*)(As + ra * 128 + swz128(ra, kk * 4 + g) * 16);
+        af[i] = *(const bf16x8*)(As + ra * ROWB + swzk<BKT>(ra, kk * 4 + g) * 16);
         const int rb = wn * 64 + i * 16 + r;
-        bfr[i] = *(const bf16x8*)(Bs + rb * 128 + swz128(rb, kk * 4 + g) * 16);
+        bfr[i] = *(const bf16x8*)(Bs + rb * ROWB + swzk<BKT>(rb, kk * 4 + g) * 16);
       }
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bfr[ni], af[mi], acc[mi][ni]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    buf = buf + 1 == NST ? 0 : buf + 1;
   }
 
   // ---- epilogue: lane holds C[m = .. + r][n = .. + 4g + i], i = 0..3 ----
@@ -404,7 +443,28 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
 }  // namespace
 
 // ----------------------------------------------------------------- C-ABI entry points
-static int g_gemm_variant = 1;
+static int g_gemm_variant = 2;
+
+template <int BKT, int NST>
+static int launch_nt(int epi, int grid, hipStream_t stream, const NTArgs& a) {
+  const size_t lds = (size_t)NST * 2 * BM * BKT * 2;
+#define L1(E)                                                                   \
+  allow_lds(gemm_nt_kernel<E, BKT, NST>, lds);                                  \
+  hipLaunchKernelGGL((gemm_nt_kernel<E, BKT, NST>), grid, 256, lds, stream, a); \
+  break;
+  switch (epi) {
+    case EPI_BF16: L1(EPI_BF16)
+    case EPI_GELU: L1(EPI_GELU)
+    case EPI_F32_RESID: L1(EPI_F32_RESID)
+    case EPI_DGELU: L1(EPI_DGELU)
+    case EPI_F32: L1(EPI_F32)
+    case EPI_PATCH: L1(EPI_PATCH)
+    case EPI_GELU_ACT: L1(EPI_GELU_ACT)
+    default: return ES_BAD_ARG;
+  }
+#undef L1
+  return ES_OK;
+}
 
 extern "C" {
 
@@ -436,22 +496,22 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   const int grid = ((M + BM - 1) / BM) * (N / BN);
-  const size_t lds = 2 * STAGE_BYTES;
-  switch (epi) {
-    case EPI_BF16: hipLaunchKernelGGL(gemm_nt_kernel<EPI_BF16>, grid, 256, lds, stream, a); break;
-    case EPI_GELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_GELU>, grid, 256, lds, stream, a); break;
-    case EPI_F32_RESID: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32_RESID>, grid, 256, lds, stream, a); break;
-    case EPI_DGELU: hipLaunchKernelGGL(gemm_nt_kernel<EPI_DGELU>, grid, 256, lds, stream, a); break;
-    case EPI_F32: hipLaunchKernelGGL(gemm_nt_kernel<EPI_F32>, grid, 256, lds, stream, a); break;
-    case EPI_PATCH: hipLaunchKernelGGL(gemm_nt_kernel<EPI_PATCH>, grid, 256, lds, stream, a); break;
-    case EPI_GELU_ACT: hipLaunchKernelGGL(gemm_nt_kernel<EPI_GELU_ACT>, grid, 256, lds, stream, a); break;
-    default: return ES_BAD_ARG;
+  int rc = ES_OK;
+  switch (g_gemm_variant) {
+    case 0: rc = launch_nt<64, 2>(epi, grid, stream, a); break;
+    case 2: rc = launch_nt<32, 3>(epi, grid, stream, a); break;
+    case 3: rc = launch_nt<32, 4>(epi, grid, stream, a); break;
+    case 4: rc = launch_nt<64, 3>(epi, grid, stream, a); break;
+    case 5: rc = launch_nt<32, 2>(epi, grid, stream, a); break;
+    default: rc = launch_nt<32, 3>(epi, grid, stream, a); break;
   }
+  if (rc) return rc;
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-// Tuning knob: which NT kernel family es_gemm_nt launches (0 = 128x128 2-stage, 1 = 256x128
-// 3-stage ring).  Returns the previous value.
+// Tuning knob: which NT kernel family es_gemm_nt launches (0 = 128x128 BK64 2-stage, 1 = 256x128
+// BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage, 4 = 128x128 BK64 3-stage).
+// Returns the previous value.
 int es_set_gemm_variant(int v) {
   const int old = g_gemm_variant;
   g_gemm_variant = v;

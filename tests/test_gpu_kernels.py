@@ -40,7 +40,7 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-@pytest.fixture(params=[0, 1], ids=["v0_128x128", "v1_256x128"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["v0", "v1", "v2", "v3", "v4", "v5"])
 def gemm_variant(request):
     old = _lib.load().es_set_gemm_variant(request.param)
     yield request.param
