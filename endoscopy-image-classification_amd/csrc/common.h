@@ -18,6 +18,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 #define LDS_PTR(p) ((__attribute__((address_space(3))) void*)(p))
 
+// 16-byte global -> LDS DMA (global_load_lds_dwordx4).  Kept in a non-template function: inside a
+// kernel template the address-space-3 cast of a value-dependent pointer fails host-side template
+// substitution and hipcc then silently emits no host stub for the kernel.
+__device__ __forceinline__ void glds16(const void* src, char* lds) {
+  __builtin_amdgcn_global_load_lds(src, LDS_PTR(lds), 16, 0, 0);
+}
+
 enum EsStatus {
   ES_OK = 0,
   ES_BAD_SHAPE = -1,
