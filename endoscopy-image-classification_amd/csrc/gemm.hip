@@ -14,6 +14,8 @@
 // global_load_lds_dwordx4 (1 KiB per wave-instruction, lane-linear destination), XOR-swizzled on
 // the SOURCE address so the fragment reads are bank-conflict free; two LDS stages; the stage for
 // step k+1 is issued before the MFMAs of step k.
+#include <algorithm>
+
 #include "common.h"
 
 namespace es_gemm {
@@ -70,6 +72,85 @@ __device__ __forceinline__ void epi_store(const NTArgs& p, int m, int n, f32x4 v
     const int img = m / p.np, pi = m - img * p.np;
     const f32x4 pos = *(const f32x4*)((const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n);
     *(f32x4*)((float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n) = v + pos;
+  }
+}
+
+// Row-segment epilogue: 8 consecutive outputs C[m][n .. n+7] (fp32 values, bias not yet added).
+template <int EPI>
+__device__ __forceinline__ void epi_store8(const NTArgs& p, int m, int n, f32x4 v0, f32x4 v1) {
+  if (p.bias) {
+    v0 += *(const f32x4*)(p.bias + n);
+    v1 += *(const f32x4*)(p.bias + n + 4);
+  }
+  float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+  if constexpr (EPI == EPI_BF16) {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+    *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+  } else if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_ACT) {
+    bf16x8 a;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = (bf16)gelu_f(v[i]);
+    if constexpr (EPI == EPI_GELU) {
+      bf16x8 o;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+      *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+      *(bf16x8*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
+    } else {
+      *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = a;
+    }
+  } else if constexpr (EPI == EPI_F32_RESID) {
+    const float* rs = (const float*)p.aux + (size_t)m * p.ldaux + n;
+    float* out = (float*)p.C + (size_t)m * p.ldc + n;
+    *(f32x4*)out = v0 + *(const f32x4*)rs;
+    *(f32x4*)(out + 4) = v1 + *(const f32x4*)(rs + 4);
+  } else if constexpr (EPI == EPI_DGELU) {
+    const bf16x8 pre = *(const bf16x8*)((const bf16*)p.aux + (size_t)m * p.ldaux + n);
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)(v[i] * gelu_grad_f((float)pre[i]));
+    *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+  } else if constexpr (EPI == EPI_F32) {
+    float* out = (float*)p.C + (size_t)m * p.ldc + n;
+    *(f32x4*)out = v0;
+    *(f32x4*)(out + 4) = v1;
+  } else if constexpr (EPI == EPI_PATCH) {
+    const int img = m / p.np, pi = m - img * p.np;
+    const float* pos = (const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n;
+    float* out = (float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n;
+    *(f32x4*)out = v0 + *(const f32x4*)pos;
+    *(f32x4*)(out + 4) = v1 + *(const f32x4*)(pos + 4);
+  }
+}
+
+// A wave's 64x64 fp32 accumulator tile -> its private LDS region (rows padded to 272 B so the
+// 16-row ds_write_b128 of one accumulator is conflict-free) -> read back as row segments of 8
+// (2 x ds_read_b128) -> epilogue with 16-B global accesses: every wave store instruction covers
+// 8 whole rows of the tile (full 128-B lines for bf16 outputs, 256 B for fp32).
+constexpr int EPI_ROWB = 64 * 4 + 16;
+constexpr int EPI_WAVE_BYTES = 64 * EPI_ROWB;  // 17408
+
+template <int EPI>
+__device__ __forceinline__ void staged_epilogue(const NTArgs& p, char* wlds, const f32x4 (&acc)[4][4], int mw0,
+                                                int nw0, int lane) {
+  const int g = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni)
+      *(f32x4*)(wlds + (mi * 16 + r) * EPI_ROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+  const int rr = lane >> 3, c0 = (lane & 7) * 8;
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int row = it * 8 + rr;
+    const f32x4 v0 = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4);
+    const f32x4 v1 = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4 + 16);
+    const int m = mw0 + row;
+    if (m < p.M) epi_store8<EPI>(p, m, nw0 + c0, v0, v1);
   }
 }
 
@@ -151,13 +232,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
     buf = buf == 2 ? 0 : buf + 1;
   }
 
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int m = m0 + wm * 64 + mi * 16 + r;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) epi_store<EPI>(p, m, n0 + wn * 64 + ni * 16 + 4 * g, acc[mi][ni]);
-  }
+  __builtin_amdgcn_s_barrier();
+  staged_epilogue<EPI>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 
@@ -263,14 +339,9 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
     buf = buf + 1 == NST ? 0 : buf + 1;
   }
 
-  // ---- epilogue: lane holds C[m = .. + r][n = .. + 4g + i], i = 0..3 ----
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int m = m0 + wm * 64 + mi * 16 + r;
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) epi_store<EPI>(p, m, n0 + wn * 64 + ni * 16 + 4 * g, acc[mi][ni]);
-  }
+  // ---- epilogue through LDS (stage buffers are free once every wave passed the last MFMA) ----
+  __builtin_amdgcn_s_barrier();
+  staged_epilogue<EPI>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 #undef NT_ISSUE
 
@@ -446,7 +517,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
 // gets no host stub).
 #define NT_LAUNCH(E, BKT_, NST_)                                                           \
   {                                                                                        \
-    const size_t lds = (size_t)NST_ * 2 * BM * BKT_ * 2;                                   \
+    const size_t lds = std::max((size_t)NST_ * 2 * BM * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES); \
     allow_lds(gemm_nt_kernel<E, BKT_, NST_>, lds);                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_kernel<E, BKT_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
     return ES_OK;                                                                          \
