@@ -549,7 +549,7 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
 using namespace es_gemm;
 
 // ----------------------------------------------------------------- C-ABI entry points
-static int g_gemm_variant = 2;
+static int g_gemm_variant = 0;
 
 
 extern "C" {
