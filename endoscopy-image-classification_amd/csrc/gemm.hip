@@ -462,17 +462,26 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restr
 }
 
 // Column sums of a bf16 [M, N] matrix (bias gradients), HBM-streaming: each thread owns one
-// 8-column chunk (16-B loads) and strides over rows; per-block partials P[block][N].
+// 8-column chunk (16-B loads) of a row group and keeps 4 rows in flight; per-block partials P[block][N].
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restrict__ Y, int ld, int M, int N,
                                                              int rows_per, float* __restrict__ P) {
   __shared__ float red[256 * 8];
-  const int nc = N >> 3;                 // 8-column chunks
-  const int groups = 256 / nc;           // row groups per block (nc <= 256)
+  const int nc = N >> 3;        // 8-column chunks (<= 256)
+  const int groups = 256 / nc;  // row groups per block
   const int t = threadIdx.x, c = t % nc, rg = t / nc;
   const int m0 = blockIdx.x * rows_per, m1 = min(m0 + rows_per, M);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (rg < groups) {
-    for (int m = m0 + rg; m < m1; m += groups) {
+    int m = m0 + rg;
+    for (; m + 3 * groups < m1; m += 4 * groups) {
+      const bf16x8 v0 = *(const bf16x8*)(Y + (size_t)m * ld + c * 8);
+      const bf16x8 v1 = *(const bf16x8*)(Y + (size_t)(m + groups) * ld + c * 8);
+      const bf16x8 v2 = *(const bf16x8*)(Y + (size_t)(m + 2 * groups) * ld + c * 8);
+      const bf16x8 v3 = *(const bf16x8*)(Y + (size_t)(m + 3 * groups) * ld + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += ((float)v0[j] + (float)v1[j]) + ((float)v2[j] + (float)v3[j]);
+    }
+    for (; m < m1; m += groups) {
       const bf16x8 v = *(const bf16x8*)(Y + (size_t)m * ld + c * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[j] += (float)v[j];
@@ -483,34 +492,39 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restr
   __syncthreads();
   for (int col = t; col < N; col += 256) {
     const int cc = col >> 3, j = col & 7;
-    float s = 0.f;
-    for (int g = 0; g < groups; ++g) s += red[(g * nc + cc) * 8 + j];
-    P[(size_t)blockIdx.x * N + col] = s;
+    float sum = 0.f;
+    for (int gg = 0; gg < groups; ++gg) sum += red[(gg * nc + cc) * 8 + j];
+    P[(size_t)blockIdx.x * N + col] = sum;
   }
 }
 
-// out[n] (+)= sum_g P[g][n]: 64 columns x 4 row-groups per block, then a 4-way LDS combine.
+// out[n] (+)= sum_g P[g][n]: 16 columns x 16 row-groups per block (4 loads in flight per
+// thread), then a 16-way LDS combine.
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ P, float* __restrict__ out,
                                                               int G, int N, int accumulate) {
-  __shared__ float red[4][64];
-  const int col = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
-  float s0 = 0.f, s1 = 0.f;
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int g = rg;
-    for (; g + 4 < G; g += 8) {
+    for (; g + 48 < G; g += 64) {
       s0 += P[(size_t)g * N + col];
-      s1 += P[(size_t)(g + 4) * N + col];
+      s1 += P[(size_t)(g + 16) * N + col];
+      s2 += P[(size_t)(g + 32) * N + col];
+      s3 += P[(size_t)(g + 48) * N + col];
     }
-    for (; g < G; g += 4) s0 += P[(size_t)g * N + col];
+    for (; g < G; g += 16) s0 += P[(size_t)g * N + col];
   }
-  red[rg][threadIdx.x & 63] = s0 + s1;
+  red[rg][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (rg == 0 && col < N) {
-    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
-    out[col] = accumulate ? out[col] + s : s;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sum += red[k][cl];
+    out[col] = accumulate ? out[col] + sum : sum;
   }
 }
-
 
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
 // template commas out of the launch macro; a kernel referenced only through a function pointer
@@ -637,14 +651,14 @@ int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks,
   const int rows_per = (M + blocks - 1) / blocks;
   const int G = (M + rows_per - 1) / rows_per;
   hipLaunchKernelGGL(colsum_partial_kernel, G, 256, 0, stream, (const bf16*)Y, ld, M, N, rows_per, workspace);
-  hipLaunchKernelGGL(reduce_partials_kernel, (N + 63) / 64, 256, 0, stream, workspace, out, G, N, accumulate);
+  hipLaunchKernelGGL(reduce_partials_kernel, (N + 15) / 16, 256, 0, stream, workspace, out, G, N, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
 // out[n] (+)= sum_g P[g][n]  (partials of the LayerNorm / colsum kernels)
 int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream) {
   if (G <= 0 || N <= 0) return ES_BAD_SHAPE;
-  hipLaunchKernelGGL(reduce_partials_kernel, (N + 63) / 64, 256, 0, stream, P, out, G, N, accumulate);
+  hipLaunchKernelGGL(reduce_partials_kernel, (N + 15) / 16, 256, 0, stream, P, out, G, N, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -40,19 +40,41 @@ __global__ void cls_init_kernel(float* __restrict__ x, int ldx, const float* __r
   }
 }
 
-// dx fp32 [n*T, D] -> dpatch bf16 [n*(T-1), D]; dpos[t][d] (+)= sum_img dx; dcls[d] (+)= dpos[0][d]
-__global__ void embed_bwd_kernel(const float* __restrict__ dx, int lddx, bf16* __restrict__ dpatch, int ldp,
-                                 float* __restrict__ dpos, float* __restrict__ dcls, int n, int T, int D,
-                                 int accumulate) {
+// dx fp32 [n*T, D] -> dpatch bf16 [n*(T-1), D]; dpos[t][d] (+)= sum_img dx; dcls[d] (+)= dpos[0][d].
+// Block = 64 features x 4 image groups; the 4 partial sums meet in LDS.
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ dx, int lddx,
+                                                        bf16* __restrict__ dpatch, int ldp, float* __restrict__ dpos,
+                                                        float* __restrict__ dcls, int n, int T, int D, int accumulate) {
+  __shared__ float red[4][64];
+  const int id = blockIdx.x * 64 + (threadIdx.x & 63), ig = threadIdx.x >> 6;
   const int total = T * D;
-  for (int id = blockIdx.x * blockDim.x + threadIdx.x; id < total; id += gridDim.x * blockDim.x) {
-    const int t = id / D, d = id % D;
-    float s = 0.f;
-    for (int im = 0; im < n; ++im) {
+  float s0 = 0.f, s1 = 0.f;
+  int t = 0, d = 0;
+  if (id < total) {
+    t = id / D;
+    d = id % D;
+    int im = ig;
+    for (; im + 4 < n; im += 8) {
+      const float v0 = dx[((size_t)im * T + t) * lddx + d];
+      const float v1 = dx[((size_t)(im + 4) * T + t) * lddx + d];
+      s0 += v0;
+      s1 += v1;
+      if (t > 0) {
+        dpatch[((size_t)im * (T - 1) + t - 1) * ldp + d] = (bf16)v0;
+        dpatch[((size_t)(im + 4) * (T - 1) + t - 1) * ldp + d] = (bf16)v1;
+      }
+    }
+    for (; im < n; im += 4) {
       const float v = dx[((size_t)im * T + t) * lddx + d];
-      s += v;
+      s0 += v;
       if (t > 0) dpatch[((size_t)im * (T - 1) + t - 1) * ldp + d] = (bf16)v;
     }
+  }
+  red[ig][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (ig == 0 && id < total) {
+    const int l = threadIdx.x & 63;
+    const float s = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
     dpos[id] = accumulate ? dpos[id] + s : s;
     if (t == 0) dcls[d] = accumulate ? dcls[d] + s : s;
   }
@@ -193,7 +215,7 @@ int es_cls_init(float* x, int ldx, const float* cls, const float* pos, int n, in
 int es_embed_bwd(const float* dx, int lddx, void* dpatch, int ldp, float* dpos, float* dcls, int n, int T, int D,
                  int accumulate, hipStream_t stream) {
   if (n <= 0 || T <= 1 || D <= 0) return ES_BAD_SHAPE;
-  const int grid = (T * D + 255) / 256;
+  const int grid = (T * D + 63) / 64;
   hipLaunchKernelGGL(embed_bwd_kernel, grid, 256, 0, stream, dx, lddx, (bf16*)dpatch, ldp, dpos, dcls, n, T, D,
                      accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;

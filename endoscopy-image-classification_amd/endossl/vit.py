@@ -301,7 +301,7 @@ class Engine:
 
     def _bgrad(self, dy, N, M, out):
         ws = self.workspace()
-        call("es_colsum", ptr(dy), N, M, N, ptr(ws), 512, ptr(out), 0, _lib.stream())
+        call("es_colsum", ptr(dy), N, M, N, ptr(ws), 1024, ptr(out), 0, _lib.stream())
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M):
         D = self.cfg.dim
