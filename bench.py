@@ -77,7 +77,8 @@ def cpu_baseline(B=8, MU=7, steps=2):
 
 
 def pmc_traffic(kernel_substr):
-    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary."""
+    """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json: FETCH_SIZE x2 (gfx950 half-count correction) + WRITE_SIZE, KiB->B)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
@@ -154,7 +155,7 @@ def main():
     flops = [f for _, _, f in probe["events"]]
     mean_ms = sum(ev_ms) / len(ev_ms)
     achieved = sum(flops) / (sum(ev_ms) / 1e3) / 1e12  # TFLOP/s over the probed launches
-    traffic = pmc_traffic("gemm_nt_kernelILi1E")
+    traffic = pmc_traffic("gemm_nt_kernel<1,")
 
     if rank == 0:
         ms = T / args.steps * 1e3
@@ -173,7 +174,8 @@ def main():
             "step_tflops": round(STEP_TFLOP_F1 / (ms / 1e3), 1),
             "step_mfma_frac": round(STEP_TFLOP_F1 / (ms / 1e3) / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(loss, 6),
-            "roofline": {"kernel": "gemm_nt_kernel<EPI_GELU> (fc1 forward, M=100864|88256, N=1536, K=384)",
+            "roofline": {"kernel": "gemm_nt_kernel<EPI_GELU> (train fc1 forward: M=100864, N=1536, K=384, "
+                                   "bias + exact-GELU epilogue writing pre-activation and activation, bf16)",
                          "bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
                          "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms), "traffic": traffic},

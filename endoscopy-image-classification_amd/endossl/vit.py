@@ -277,7 +277,7 @@ class Engine:
                            ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.pre[li]), Hd, ptr(A.act[li]), None, 0, M,
                            Hd, D, 0, s)
             else:
-                self._gemm("fc1_fwd", EPI_GELU_ACT, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+                self._gemm("fc1_fwd_weak", EPI_GELU_ACT, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
                            ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.act[li]), Hd, None, None, 0, M, Hd, D, 0,
                            s)
             call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,

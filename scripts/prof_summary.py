@@ -1,0 +1,43 @@
+"""Summarise a rocprofv3 --kernel-trace --stats run of bench.py into profiles/<tag>_*.
+
+  python scripts/prof_summary.py gpurun_out/prof <tag> [steps_profiled]
+Writes <tag>_kernel_stats.csv (rocprofv3's own summary, copied) and <tag>_summary.md
+(per-kernel ms/step, per-shape GEMM/attention breakdown from the trace)."""
+import collections
+import csv
+import os
+import re
+import shutil
+import sys
+
+src, tag = sys.argv[1], sys.argv[2]
+steps = int(sys.argv[3]) if len(sys.argv) > 3 else 7  # warmup 2 + steps 5 under rocprofv3
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+out = os.path.join(root, "profiles")
+os.makedirs(out, exist_ok=True)
+shutil.copy(os.path.join(src, "run_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+rows = list(csv.DictReader(open(os.path.join(src, "run_kernel_stats.csv"))))
+tot = sum(float(r["TotalDurationNs"]) for r in rows)
+lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2` (F1, 1x MI355X)", "",
+         f"Total GPU kernel time / step: **{tot / 1e6 / steps:.2f} ms** ({steps} profiled steps)", "",
+         "| ms/step | % | calls/step | avg us | kernel |", "|---:|---:|---:|---:|---|"]
+for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:30]:
+    name = re.sub(r"\(anonymous namespace\)::|es_gemm::", "", r["Name"])[:110].replace("|", "/")
+    lines.append(f"| {float(r['TotalDurationNs']) / 1e6 / steps:.3f} | {float(r['Percentage']):.1f} | "
+                 f"{int(r['Calls']) / steps:.1f} | {float(r['AverageNs']) / 1e3:.1f} | `{name}` |")
+tr = os.path.join(src, "run_kernel_trace.csv")
+if os.path.exists(tr):
+    agg = collections.defaultdict(lambda: [0, 0.0])
+    for r in csv.DictReader(open(tr)):
+        m = re.search(r"(gemm_nt\w*<[^>]*>|gemm_tn_kernel|attn_\w+<\d>)", r["Kernel_Name"])
+        if not m:
+            continue
+        k = (m.group(1), int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
+        agg[k][0] += 1
+        agg[k][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    lines += ["", "Per launch shape (workgroups identify M,N):", "", "| ms/step | calls/step | avg us | kernel | grid |",
+              "|---:|---:|---:|---|---:|"]
+    for (n, g), (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
+        lines.append(f"| {t / steps / 1e3:.3f} | {c / steps:.1f} | {t / c:.1f} | `{n}` | {g} |")
+open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+print("\n".join(lines[:20]))
