@@ -125,32 +125,39 @@ __device__ __forceinline__ void epi_store8(const NTArgs& p, int m, int n, f32x4 
   }
 }
 
-// A wave's 64x64 fp32 accumulator tile -> its private LDS region (rows padded to 272 B so the
-// 16-row ds_write_b128 of one accumulator is conflict-free) -> read back as row segments of 8
-// (2 x ds_read_b128) -> epilogue with 16-B global accesses: every wave store instruction covers
-// 8 whole rows of the tile (full 128-B lines for bf16 outputs, 256 B for fp32).
+// A wave's 64x64 fp32 accumulator tile goes through its private LDS region 16 rows at a time
+// (rows padded to 272 B so each 16-row ds_write_b128 is conflict-free), read back as row segments
+// of 8 (2 x ds_read_b128) and stored with 16-B global accesses: each wave store instruction covers
+// 8 whole 64-column row segments (128 B bf16 / 256 B fp32).  17 KiB per 4-wave workgroup, so the
+// staging does not limit occupancy.
 constexpr int EPI_ROWB = 64 * 4 + 16;
-constexpr int EPI_WAVE_BYTES = 64 * EPI_ROWB;  // 17408
+constexpr int EPI_WAVE_BYTES = 16 * EPI_ROWB;  // 4352
 
 template <int EPI>
 __device__ __forceinline__ void staged_epilogue(const NTArgs& p, char* wlds, const f32x4 (&acc)[4][4], int mw0,
                                                 int nw0, int lane) {
   const int g = lane >> 4, r = lane & 15;
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni)
-      *(f32x4*)(wlds + (mi * 16 + r) * EPI_ROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
   const int rr = lane >> 3, c0 = (lane & 7) * 8;
-#pragma unroll 2
-  for (int it = 0; it < 8; ++it) {
-    const int row = it * 8 + rr;
-    const f32x4 v0 = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4);
-    const f32x4 v1 = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4 + 16);
-    const int m = mw0 + row;
-    if (m < p.M) epi_store8<EPI>(p, m, nw0 + c0, v0, v1);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) *(f32x4*)(wlds + r * EPI_ROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    f32x4 v[2][2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int row = it * 8 + rr;
+      v[it][0] = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4);
+      v[it][1] = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4 + 16);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int m = mw0 + mi * 16 + it * 8 + rr;
+      if (m < p.M) epi_store8<EPI>(p, m, nw0 + c0, v[it][0], v[it][1]);
+    }
   }
 }
 
@@ -531,7 +538,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
 // gets no host stub).
 #define NT_LAUNCH(E, BKT_, NST_)                                                           \
   {                                                                                        \
-    const size_t lds = std::max((size_t)NST_ * 2 * BM * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES); \
+    const size_t lds = std::max((size_t)NST_ * 2 * BM * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES);   \
     allow_lds(gemm_nt_kernel<E, BKT_, NST_>, lds);                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_kernel<E, BKT_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
     return ES_OK;                                                                          \
