@@ -359,60 +359,75 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
 __device__ __forceinline__ int swz256(int r, int c) { return c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3)); }
 
 struct TNArgs {
-  const bf16* A1; const bf16* A2; float* P;
+  const bf16* A1; const bf16* A2; float* P; float* PB;
   int M, N1, N2, ld1, ld2, mchunk;
 };
 
-__global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TNArgs p) {
+// BKM-deep token steps (32 or 64), NST-stage glds ring, counted vmcnt.  With PB != null the
+// workgroups of the first N2 tile also sum their A1 (= dY) tile columns from LDS: the bias
+// gradient of the same Linear, written as per-split partials PB[split][N1].
+template <int BKM, int NST>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(TNArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int IPW = (BKM / 4) / 4;    // 1-KiB glds (4 rows of 256 B) per wave per operand per stage
+  constexpr int PER = 2 * IPW;
+  constexpr int TILE = BKM * BM * 2;     // bytes per operand tile
+  constexpr int STAGE = 2 * TILE;
   const int nt2 = p.N2 / BN, ntiles = (p.N1 / BM) * nt2;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int split = wg / ntiles, tile = wg - split * ntiles;
   const int n1_0 = (tile / nt2) * BM, n2_0 = (tile % nt2) * BN;
+  const bool do_bias = p.PB != nullptr && (tile % nt2) == 0;
   const int mbeg = split * p.mchunk;
-  const int mend = min(mbeg + p.mchunk, (p.M + BK - 1) / BK * BK);
+  const int mend = min(mbeg + p.mchunk, (p.M + BKM - 1) / BKM * BKM);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wa = w >> 1, wb = w & 1;
   const int g = lane >> 4, t = lane & 15, q = t >> 2, p4 = t & 3;
 
-  const bf16* g1[4];
-  const bf16* g2[4];
+  const bf16* g1[IPW];
+  const bf16* g2[IPW];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int row = (w * 4 + j) * 4 + (lane >> 4);
+  for (int j = 0; j < IPW; ++j) {
+    const int row = (w * IPW + j) * 4 + (lane >> 4);
     const int lc = swz256(row, lane & 15);
     g1[j] = p.A1 + (size_t)(mbeg + row) * p.ld1 + n1_0 + lc * 8;
     g2[j] = p.A2 + (size_t)(mbeg + row) * p.ld2 + n2_0 + lc * 8;
   }
-  auto stage = [&](int buf, int mo) {
-    char* T1 = smem + buf * STAGE_BYTES;
-    char* T2 = T1 + BK * BM * 2;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      __builtin_amdgcn_global_load_lds(g1[j] + (size_t)mo * p.ld1, LDS_PTR(T1 + (w * 4 + j) * 1024), 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(g2[j] + (size_t)mo * p.ld2, LDS_PTR(T2 + (w * 4 + j) * 1024), 16, 0, 0);
-    }
-  };
+#define TN_ISSUE(BUF, MO)                                                        \
+  {                                                                              \
+    char* T1_ = smem + (BUF) * STAGE;                                            \
+    _Pragma("unroll") for (int j = 0; j < IPW; ++j) {                            \
+      glds16(g1[j] + (size_t)(MO) * p.ld1, T1_ + (w * IPW + j) * 1024);          \
+      glds16(g2[j] + (size_t)(MO) * p.ld2, T1_ + TILE + (w * IPW + j) * 1024);   \
+    }                                                                            \
+  }
 
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+  const int bc = tid & 127, bh = tid >> 7;  // bias: column, row half
 
-  const int nk = (mend - mbeg) / BK;
-  if (nk > 0) {
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-    const char* T1 = smem + cur * STAGE_BYTES;
-    const char* T2 = T1 + BK * BM * 2;
+  const int nk = (mend - mbeg) / BKM;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) TN_ISSUE(st, st * BKM)
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int younger = min(NST - 2, nk - 1 - kt);
+    wait_vmcnt(younger * PER);
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nk) {
+      int nb = buf + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
+      TN_ISSUE(nb, (kt + NST - 1) * BKM)
+    }
+    const char* T1 = smem + buf * STAGE;
+    const char* T2 = T1 + TILE;
+#pragma unroll
+    for (int hh = 0; hh < BKM / 32; ++hh) {
       bf16x8 af[4], bfr[4];
       const int r1 = hh * 32 + 8 * g + q, r2 = r1 + 4;
 #pragma unroll
@@ -430,9 +445,14 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TNArgs p) {
 #pragma unroll
         for (int bi = 0; bi < 4; ++bi) acc[ai][bi] = mfma16(af[ai], bfr[bi], acc[ai][bi]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if (do_bias) {
+#pragma unroll 8
+      for (int rr = bh * (BKM / 2); rr < (bh + 1) * (BKM / 2); ++rr)
+        bsum += (float)*(const bf16*)(T1 + rr * 256 + swz256(rr, bc >> 3) * 16 + (bc & 7) * 2);
+    }
+    buf = buf + 1 == NST ? 0 : buf + 1;
   }
+#undef TN_ISSUE
 
   // lane holds D[n2 = .. + 4g + i][n1 = .. + t]  ->  P[split][n1][n2 .. n2+3]
   float* P = p.P + (size_t)split * p.N1 * p.N2;
@@ -444,6 +464,13 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_kernel(TNArgs p) {
       const int n2 = n2_0 + wa * 64 + ai * 16 + 4 * g;
       *(f32x4*)(P + (size_t)n1 * p.N2 + n2) = acc[ai][bi];
     }
+  }
+  if (do_bias) {
+    __builtin_amdgcn_s_barrier();
+    float* red = (float*)smem;
+    if (bh == 1) red[bc] = bsum;
+    __syncthreads();
+    if (bh == 0) p.PB[(size_t)split * p.N1 + n1_0 + bc] = bsum + red[bc];
   }
 }
 
@@ -570,7 +597,7 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
 using namespace es_gemm;
 
 // ----------------------------------------------------------------- C-ABI entry points
-static int g_gemm_variant = 0;
+static int g_gemm_variant = -1;
 
 
 extern "C" {
@@ -585,7 +612,12 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     return ES_BAD_ARG;
   if (epi == EPI_PATCH && np <= 0) return ES_BAD_ARG;
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
-  if (g_gemm_variant == 1) {
+  // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py): short K
+  // (<= 384) is epilogue-bound -> BK32 two-stage at 5 workgroups/CU (BK32 three-stage for the
+  // read-modify-write DGELU epilogue); long K -> 256x128 three-stage ring.
+  int variant = g_gemm_variant;
+  if (variant < 0) variant = K <= 384 ? (epi == EPI_DGELU ? 2 : 5) : 1;
+  if (variant == 1) {
     const int grid = ((M + BM2 - 1) / BM2) * (N / BN);
     const size_t lds = 3 * STAGE2;
 #define L2(E) allow_lds(gemm_nt256_kernel<E>, lds); hipLaunchKernelGGL(gemm_nt256_kernel<E>, grid, 512, lds, stream, a); break;
@@ -603,13 +635,14 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   const int grid = ((M + BM - 1) / BM) * (N / BN);
-  const int rc = launch_nt(g_gemm_variant, epi, grid, stream, a);
+  const int rc = launch_nt(variant, epi, grid, stream, a);
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-// Tuning knob: which NT kernel family es_gemm_nt launches (0 = 128x128 BK64 2-stage, 1 = 256x128
-// BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage, 4 = 128x128 BK64 3-stage).
+// Tuning knob: which NT kernel family es_gemm_nt launches (-1 = per-shape default, 0 = 128x128
+// BK64 2-stage, 1 = 256x128 BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage,
+// 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage).
 // Returns the previous value.
 int es_set_gemm_variant(int v) {
   const int old = g_gemm_variant;
@@ -617,28 +650,33 @@ int es_set_gemm_variant(int v) {
   return old;
 }
 
-// workspace floats needed by es_gemm_tn for `splits` splits
-size_t es_gemm_tn_workspace(int N1, int N2, int splits) { return (size_t)splits * N1 * N2; }
+// workspace floats needed by es_gemm_tn for `splits` splits (slabs + bias partials)
+size_t es_gemm_tn_workspace(int N1, int N2, int splits) { return (size_t)splits * N1 * N2 + (size_t)splits * N1; }
 
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
-               float* workspace, float* out, int accumulate, hipStream_t stream) {
+               float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream) {
   if (M <= 0 || (N1 % BM) || (N2 % BN) || splits <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
-  if (!A1 || !A2 || !out) return ES_BAD_ARG;
-  const int msteps = (M + BK - 1) / BK;
+  if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
+  // token step: 32 (5 workgroups/CU) -- measured faster than 64 on every ViT-S wgrad shape
+  constexpr int BKM = 32, NST = 2;
+  const int msteps = (M + BKM - 1) / BKM;
   const int per = (msteps + splits - 1) / splits;
   const int S = (msteps + per - 1) / per;
   const bool direct = (S == 1 && !accumulate);
   float* P = direct ? out : workspace;
-  if (!P) return ES_BAD_ARG;
-  TNArgs a{(const bf16*)A1, (const bf16*)A2, P, M, N1, N2, ld1, ld2, per * BK};
+  float* PB = bias_out ? workspace + (size_t)S * N1 * N2 : nullptr;
+  TNArgs a{(const bf16*)A1, (const bf16*)A2, P, PB, M, N1, N2, ld1, ld2, per * BKM};
   const int grid = S * (N1 / BM) * (N2 / BN);
-  hipLaunchKernelGGL(gemm_tn_kernel, grid, 256, 2 * STAGE_BYTES, stream, a);
+  const size_t lds = (size_t)NST * 2 * BKM * BM * 2;
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_kernel<BKM, NST>), dim3(grid), dim3(256), lds, stream, a);
   if (!direct) {
     const int n = N1 * N2;
     int rg = (n / 4 + 255) / 256;
     rg = rg > 2048 ? 2048 : rg;
     hipLaunchKernelGGL(splitk_reduce_kernel, rg, 256, 0, stream, P, out, S, n, accumulate);
   }
+  if (bias_out)
+    hipLaunchKernelGGL(reduce_partials_kernel, (N1 + 15) / 16, 256, 0, stream, PB, bias_out, S, N1, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -291,17 +291,15 @@ class Engine:
     # -------------------------------------------------------------- backward
     def _tn_splits(self, M, N1, N2):
         tiles = (N1 // 128) * (N2 // 128)
-        msteps = (M + 63) // 64
+        msteps = (M + 31) // 32
         return max(1, min(msteps, -(-self.TN_TARGET_BLOCKS // tiles)))
 
-    def _wgrad(self, dy, N1, x, N2, M, out):
+    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None):
+        """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy."""
         ws = self.workspace()
         splits = self._tn_splits(M, N1, N2)
-        call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, _lib.stream())
-
-    def _bgrad(self, dy, N, M, out):
-        ws = self.workspace()
-        call("es_colsum", ptr(dy), N, M, N, ptr(ws), 1024, ptr(out), 0, _lib.stream())
+        call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
+             _lib.stream())
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M):
         D = self.cfg.dim
@@ -333,26 +331,22 @@ class Engine:
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
             call("es_gemm_nt", EPI_DGELU, ptr(G.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(G.dpre),
                  Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
-            self._wgrad(G.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"))
-            self._bgrad(G.dxb, D, M, gv(b + "mlp.fc2.bias"))
+            self._wgrad(G.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
             call("es_gemm_nt", EPI_F32, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh), D,
                  None, None, 0, M, D, Hd, 0, s)
-            self._wgrad(G.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"))
-            self._bgrad(G.dpre, Hd, M, gv(b + "mlp.fc1.bias"))
+            self._wgrad(G.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
             self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, G.dxmb,
                          gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
             # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
             call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
                  None, None, 0, M, D, D, 0, s)
-            self._wgrad(G.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"))
-            self._bgrad(G.dxmb, D, M, gv(b + "attn.proj.bias"))
+            self._wgrad(G.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
             call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
                  ptr(G.dqkv),
                  3 * D, n, T, H, 64 ** -0.5, s)
             call("es_gemm_nt", EPI_F32, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
-            self._wgrad(G.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"))
-            self._bgrad(G.dqkv, 3 * D, M, gv(b + "attn.qkv.bias"))
+            self._wgrad(G.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
             self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), G.dxm, G.dx, G.dxb,
                          gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
         # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
@@ -360,8 +354,7 @@ class Engine:
         call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,
              s)
         npat = n * cfg.np
-        self._wgrad(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"))
-        self._bgrad(G.dpatch, D, npat, gv("patch_embed.proj.bias"))
+        self._wgrad(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
         return grad
 
 

@@ -38,14 +38,15 @@ int es_abi_version(void);
  * N % 128 == 0, K % 64 == 0; A readable for round_up(M,256) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
-/* tuning knob: NT kernel family (0 = 128x128 two-stage, 1 = 256x128 three-stage ring); returns the old one */
+/* tuning knob: NT kernel family (-1 = per-shape default, 0..5 = fixed tilings, see gemm.hip); returns the old one */
 int es_set_gemm_variant(int variant);
 /* weight gradient: out[N1,N2] (+)= sum_m A1[m,N1]^T A2[m,N2], token axis split `splits` ways into
- * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced.  N1,N2 % 128 == 0; rows in
- * [M, round_up(M,64)) of A1 must be zero. */
+ * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced; bias_out (nullable) (+)=
+ * sum_m A1[m,:] computed from the same LDS tiles.  N1,N2 % 128 == 0; rows in [M, round_up(M,64))
+ * of A1 must be zero. */
 size_t es_gemm_tn_workspace(int N1, int N2, int splits);
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
-               float* workspace, float* out, int accumulate, hipStream_t stream);
+               float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream);
 int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream);
 /* bias gradient: out[n] (+)= sum_m Y[m][n]  (workspace >= blocks*N floats) */
 int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,

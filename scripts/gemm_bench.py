@@ -74,13 +74,13 @@ def main():
     for name, M, N1, N2 in TN:
         flops = 2.0 * M * N1 * N2
         tiles = (N1 // 128) * (N2 // 128)
-        splits = max(1, min((M + 63) // 64, -(-512 // tiles)))
+        splits = max(1, min((M + 31) // 32, -(-512 // tiles)))
         for _ in range(2):
-            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, s)
+            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(args.iters):
-            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, s)
+            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
         e1.record()
         torch.cuda.synchronize()
         t = e0.elapsed_time(e1) / args.iters

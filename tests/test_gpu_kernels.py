@@ -40,7 +40,7 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["v0", "v1", "v2", "v3", "v4", "v5"])
+@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5], ids=["auto", "v0", "v1", "v2", "v3", "v4", "v5"])
 def gemm_variant(request):
     old = _lib.load().es_set_gemm_variant(request.param)
     yield request.param
@@ -117,9 +117,11 @@ def test_gemm_tn_exact_integers(M, N1, N2, splits):
     ref = A1[:M].float().t() @ A2[:M].float()
     ws = torch.empty(_lib.load().es_gemm_tn_workspace(N1, N2, splits), device=DEV)
     out = torch.full((N1, N2), 3.0, device=DEV)
-    call("es_gemm_tn", ptr(A1), N1, ptr(A2), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, S())
+    bias = torch.full((N1,), 5.0, device=DEV)
+    call("es_gemm_tn", ptr(A1), N1, ptr(A2), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), S())
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
-    call("es_gemm_tn", ptr(A1), N1, ptr(A2), N2, M, N1, N2, splits, ptr(ws), ptr(out), 1, S())
+    torch.testing.assert_close(bias, A1[:M].float().sum(0), rtol=0, atol=0)  # fused bias grad
+    call("es_gemm_tn", ptr(A1), N1, ptr(A2), N2, M, N1, N2, splits, ptr(ws), ptr(out), 1, None, S())
     torch.testing.assert_close(out, 2 * ref, rtol=0, atol=0)
 
 
