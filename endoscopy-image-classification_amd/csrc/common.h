@@ -25,6 +25,22 @@ __device__ __forceinline__ void glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, LDS_PTR(lds), 16, 0, 0);
 }
 
+// Raw buffer access (range-checked by the resource: out-of-range loads return 0, out-of-range
+// stores are dropped).  Epilogues map rows past M to an out-of-range offset with a select instead
+// of branching, which keeps the code straight-line so the waitcnt pass can count (a divergent
+// branch around a store makes it fall back to vmcnt(0) at every join).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned ES_OOB = 0x7ffffff0u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ u32x4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+}
+__device__ __forceinline__ void buf_store16(u32x4 v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+
 enum EsStatus {
   ES_OK = 0,
   ES_BAD_SHAPE = -1,
@@ -64,9 +80,11 @@ __device__ __forceinline__ float warp_max(float v) {
 // erf for the GELU epilogues: Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute (30x below
 // half a bf16 ulp at 1.0, so the bf16 outputs match torch's exact erf), ~12 VALU ops with one
 // v_exp and one v_rcp instead of ocml's piecewise erff -- the GELU epilogue runs beside MFMAs.
+// The reciprocal is the raw v_rcp_f32 (1 ulp): __frcp_rn / 1.f/x compile to a correctly rounded
+// division (div_scale x2, div_fmas, div_fixup, Newton steps), ~6 extra VALU per element.
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
   float y = fmaf(1.061405429f, t, -1.453152027f);
   y = fmaf(y, t, 1.421413741f);
   y = fmaf(y, t, -0.284496736f);

@@ -21,7 +21,6 @@
 namespace es_gemm {
 
 constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int STAGE_BYTES = 2 * BM * BK * 2;  // A + B tile, bf16
 
 enum Epi {
   EPI_BF16 = 0,       // C bf16 = acc (+bias)
@@ -41,123 +40,177 @@ struct NTArgs {
 
 // 128-byte rows (64 bf16), 16-byte chunk c of row r stored at chunk c ^ ((r >> 1) & 7).
 __device__ __forceinline__ int swz128(int r, int c) { return c ^ ((r >> 1) & 7); }
+// 64-byte rows (32 bf16), chunk c of row r at c ^ ((-(r >> 2)) & 3): conflict-free fragment reads.
+__device__ __forceinline__ int swz64(int r, int c) { return c ^ ((4 - ((r >> 2) & 3)) & 3); }
 
-// One lane's 4 consecutive outputs C[m][n .. n+3] through the fused epilogue.
+// ---- fused epilogue on 8-column row segments ------------------------------------------------
+// Operands an epilogue reads besides the accumulator: per lane, the bias of its 8 columns (loaded
+// once -- a lane's columns do not change across row chunks) and per segment the row-dependent
+// aux (fp32 residual, bf16 pre-activation, fp32 position embedding), issued one row chunk ahead
+// of the stores.  All aux loads and C stores are buffer operations on range-checked resources
+// with rows >= M mapped to ES_OOB (no branches: vmcnt counts loads and stores together on gfx9,
+// and straight-line code lets the compiler count instead of draining).
 template <int EPI>
-__device__ __forceinline__ void epi_store(const NTArgs& p, int m, int n, f32x4 v) {
-  if (p.bias) v += *(const f32x4*)(p.bias + n);
-  if constexpr (EPI == EPI_BF16) {
-    bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-  } else if constexpr (EPI == EPI_GELU) {
-    bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-    bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
-    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-    *(bf16x4*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
-  } else if constexpr (EPI == EPI_GELU_ACT) {
-    bf16x4 a = {(bf16)gelu_f(v[0]), (bf16)gelu_f(v[1]), (bf16)gelu_f(v[2]), (bf16)gelu_f(v[3])};
-    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = a;
-  } else if constexpr (EPI == EPI_F32_RESID) {
-    const f32x4 res = *(const f32x4*)((const float*)p.aux + (size_t)m * p.ldaux + n);
-    *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v + res;
-  } else if constexpr (EPI == EPI_DGELU) {
-    const bf16x4 pre = *(const bf16x4*)((const bf16*)p.aux + (size_t)m * p.ldaux + n);
-    bf16x4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (bf16)(v[i] * gelu_grad_f((float)pre[i]));
-    *(bf16x4*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-  } else if constexpr (EPI == EPI_F32) {
-    *(f32x4*)((float*)p.C + (size_t)m * p.ldc + n) = v;
-  } else if constexpr (EPI == EPI_PATCH) {
-    const int img = m / p.np, pi = m - img * p.np;
-    const f32x4 pos = *(const f32x4*)((const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n);
-    *(f32x4*)((float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n) = v + pos;
-  }
+struct EpiCtx {
+  __amdgpu_buffer_rsrc_t c, c2, aux;
+  int esz;  // bytes per C element
+};
+
+template <int EPI>
+__device__ __forceinline__ EpiCtx<EPI> epi_ctx(const NTArgs& p) {
+  EpiCtx<EPI> x;
+  constexpr bool f32out = (EPI == EPI_F32_RESID || EPI == EPI_F32 || EPI == EPI_PATCH);
+  x.esz = f32out ? 4 : 2;
+  const unsigned crows = EPI == EPI_PATCH ? (unsigned)(p.M / p.np) * (p.np + 1) : (unsigned)p.M;
+  x.c = buf_rsrc(p.C, crows * p.ldc * x.esz);
+  x.c2 = buf_rsrc(EPI == EPI_GELU ? p.C2 : p.C, crows * p.ldc * x.esz);
+  if constexpr (EPI == EPI_F32_RESID) x.aux = buf_rsrc(p.aux, (unsigned)p.M * p.ldaux * 4);
+  else if constexpr (EPI == EPI_DGELU) x.aux = buf_rsrc(p.aux, (unsigned)p.M * p.ldaux * 2);
+  else if constexpr (EPI == EPI_PATCH) x.aux = buf_rsrc(p.aux, (unsigned)(p.np + 1) * p.ldaux * 4);
+  else x.aux = x.c;
+  return x;
 }
 
-// Row-segment epilogue: 8 consecutive outputs C[m][n .. n+7] (fp32 values, bias not yet added).
+struct EpiAuxRegs { u32x4 a0, a1; };
+
 template <int EPI>
-__device__ __forceinline__ void epi_store8(const NTArgs& p, int m, int n, f32x4 v0, f32x4 v1) {
-  if (p.bias) {
-    v0 += *(const f32x4*)(p.bias + n);
-    v1 += *(const f32x4*)(p.bias + n + 4);
+__device__ __forceinline__ EpiAuxRegs epi_load_aux(const NTArgs& p, const EpiCtx<EPI>& x, int m, int n) {
+  EpiAuxRegs r;
+  const bool ok = m < p.M;
+  if constexpr (EPI == EPI_F32_RESID) {
+    const unsigned off = ok ? (unsigned)(m * p.ldaux + n) * 4u : ES_OOB;
+    r.a0 = buf_load16(x.aux, off);
+    r.a1 = buf_load16(x.aux, off + 16);
+  } else if constexpr (EPI == EPI_PATCH) {
+    const int pi = m - (m / p.np) * p.np;
+    const unsigned off = ok ? (unsigned)((1 + pi) * p.ldaux + n) * 4u : ES_OOB;
+    r.a0 = buf_load16(x.aux, off);
+    r.a1 = buf_load16(x.aux, off + 16);
+  } else if constexpr (EPI == EPI_DGELU) {
+    r.a0 = buf_load16(x.aux, ok ? (unsigned)(m * p.ldaux + n) * 2u : ES_OOB);
   }
+  return r;
+}
+
+__device__ __forceinline__ u32x4 pack_bf16x8(const float* v) {
+  bf16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+  return __builtin_bit_cast(u32x4, o);
+}
+
+// 8 consecutive outputs C[m][n .. n+7]: v0, v1 = accumulator + bias.
+template <int EPI>
+__device__ __forceinline__ void epi_store8(const NTArgs& p, const EpiCtx<EPI>& x, int m, int n, f32x4 v0, f32x4 v1,
+                                           const EpiAuxRegs& a) {
+  const bool ok = m < p.M;
+  int crow = m;
+  if constexpr (EPI == EPI_PATCH) {
+    const int img = m / p.np;
+    crow = img * (p.np + 1) + 1 + (m - img * p.np);
+  }
+  const unsigned off = ok ? (unsigned)(crow * p.ldc + n) * (unsigned)x.esz : ES_OOB;
   float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
   if constexpr (EPI == EPI_BF16) {
-    bf16x8 o;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
-    *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+    buf_store16(pack_bf16x8(v), x.c, off);
   } else if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_ACT) {
-    bf16x8 a;
+    float g[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = (bf16)gelu_f(v[i]);
+    for (int i = 0; i < 8; ++i) g[i] = gelu_f(v[i]);
     if constexpr (EPI == EPI_GELU) {
-      bf16x8 o;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
-      *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
-      *(bf16x8*)((bf16*)p.C2 + (size_t)m * p.ldc + n) = a;
+      buf_store16(pack_bf16x8(v), x.c, off);
+      buf_store16(pack_bf16x8(g), x.c2, off);
     } else {
-      *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = a;
+      buf_store16(pack_bf16x8(g), x.c, off);
     }
-  } else if constexpr (EPI == EPI_F32_RESID) {
-    const float* rs = (const float*)p.aux + (size_t)m * p.ldaux + n;
-    float* out = (float*)p.C + (size_t)m * p.ldc + n;
-    *(f32x4*)out = v0 + *(const f32x4*)rs;
-    *(f32x4*)(out + 4) = v1 + *(const f32x4*)(rs + 4);
+  } else if constexpr (EPI == EPI_F32_RESID || EPI == EPI_PATCH) {
+    buf_store16(__builtin_bit_cast(u32x4, v0 + __builtin_bit_cast(f32x4, a.a0)), x.c, off);
+    buf_store16(__builtin_bit_cast(u32x4, v1 + __builtin_bit_cast(f32x4, a.a1)), x.c, off + 16);
   } else if constexpr (EPI == EPI_DGELU) {
-    const bf16x8 pre = *(const bf16x8*)((const bf16*)p.aux + (size_t)m * p.ldaux + n);
-    bf16x8 o;
+    const bf16x8 pre = __builtin_bit_cast(bf16x8, a.a0);
+    float o[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (bf16)(v[i] * gelu_grad_f((float)pre[i]));
-    *(bf16x8*)((bf16*)p.C + (size_t)m * p.ldc + n) = o;
+    for (int i = 0; i < 8; ++i) o[i] = v[i] * gelu_grad_f((float)pre[i]);
+    buf_store16(pack_bf16x8(o), x.c, off);
   } else if constexpr (EPI == EPI_F32) {
-    float* out = (float*)p.C + (size_t)m * p.ldc + n;
-    *(f32x4*)out = v0;
-    *(f32x4*)(out + 4) = v1;
-  } else if constexpr (EPI == EPI_PATCH) {
-    const int img = m / p.np, pi = m - img * p.np;
-    const float* pos = (const float*)p.aux + (size_t)(1 + pi) * p.ldaux + n;
-    float* out = (float*)p.C + (size_t)(img * (p.np + 1) + 1 + pi) * p.ldc + n;
-    *(f32x4*)out = v0 + *(const f32x4*)pos;
-    *(f32x4*)(out + 4) = v1 + *(const f32x4*)(pos + 4);
+    buf_store16(__builtin_bit_cast(u32x4, v0), x.c, off);
+    buf_store16(__builtin_bit_cast(u32x4, v1), x.c, off + 16);
   }
 }
 
-// A wave's 64x64 fp32 accumulator tile goes through its private LDS region 16 rows at a time
-// (rows padded to 272 B so each 16-row ds_write_b128 is conflict-free), read back as row segments
-// of 8 (2 x ds_read_b128) and stored with 16-B global accesses: each wave store instruction covers
-// 8 whole 64-column row segments (128 B bf16 / 256 B fp32).  17 KiB per 4-wave workgroup, so the
-// staging does not limit occupancy.
-constexpr int EPI_ROWB = 64 * 4 + 16;
-constexpr int EPI_WAVE_BYTES = 16 * EPI_ROWB;  // 4352
+// A wave's (MF*16) x (NF*16) fp32 accumulator tile goes through its private LDS region 16 rows
+// at a time (rows padded by 16 B so each 16-row ds_write_b128 is conflict-free), read back as
+// 8-column row segments (2 x ds_read_b128) and stored with 16-B accesses (each wave store
+// instruction covers whole row segments).
+template <int NF>
+__host__ __device__ constexpr int epi_wave_bytes() { return 16 * (NF * 64 + 16); }
+constexpr int EPI_WAVE_BYTES = epi_wave_bytes<4>();  // 4352
 
-template <int EPI>
-__device__ __forceinline__ void staged_epilogue(const NTArgs& p, char* wlds, const f32x4 (&acc)[4][4], int mw0,
-                                                int nw0, int lane) {
+template <int EPI, int MF, int NF>
+__device__ __forceinline__ void staged_epilogue_g(const NTArgs& p, char* wlds, const f32x4 (&acc)[MF][NF], int mw0,
+                                                  int nw0, int lane) {
+  constexpr int ROWB = NF * 64 + 16;
+  constexpr int SEGR = NF * 2;          // 8-column segments per row
+  constexpr int SEGS = 16 * SEGR;       // per 16-row chunk
+  constexpr int IT = (SEGS + 63) / 64;  // segments per lane per chunk
+  constexpr bool kAux = (EPI == EPI_F32_RESID || EPI == EPI_PATCH || EPI == EPI_DGELU);
   const int g = lane >> 4, r = lane & 15;
-  const int rr = lane >> 3, c0 = (lane & 7) * 8;
+  const EpiCtx<EPI> x = epi_ctx<EPI>(p);
+  int srow[IT], scol[IT];
+  f32x4 b0[IT], b1[IT];
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-#pragma unroll
-    for (int ni = 0; ni < 4; ++ni) *(f32x4*)(wlds + r * EPI_ROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    f32x4 v[2][2];
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int row = it * 8 + rr;
-      v[it][0] = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4);
-      v[it][1] = *(const f32x4*)(wlds + row * EPI_ROWB + c0 * 4 + 16);
+  for (int it = 0; it < IT; ++it) {
+    const int sg = it * 64 + lane;
+    const bool valid = (SEGS % 64 == 0) || sg < SEGS;
+    srow[it] = valid ? sg / SEGR : (1 << 20);  // an invalid segment lands past M: dropped
+    scol[it] = valid ? (sg % SEGR) * 8 : 0;
+    b0[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+    b1[it] = b0[it];
+    if (p.bias) {
+      b0[it] = *(const f32x4*)(p.bias + nw0 + scol[it]);
+      b1[it] = *(const f32x4*)(p.bias + nw0 + scol[it] + 4);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
+  }
+  EpiAuxRegs aux[2][IT];
+  if constexpr (kAux) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int m = mw0 + mi * 16 + it * 8 + rr;
-      if (m < p.M) epi_store8<EPI>(p, m, nw0 + c0, v[it][0], v[it][1]);
+    for (int it = 0; it < IT; ++it) aux[0][it] = epi_load_aux<EPI>(p, x, mw0 + srow[it], nw0 + scol[it]);
+  }
+#pragma unroll
+  for (int mi = 0; mi < MF; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < NF; ++ni) *(f32x4*)(wlds + r * ROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
+    __builtin_amdgcn_wave_barrier();
+    f32x4 v[IT][2];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int rr = min(srow[it], 15);
+      v[it][0] = *(const f32x4*)(wlds + rr * ROWB + scol[it] * 4);
+      v[it][1] = *(const f32x4*)(wlds + rr * ROWB + scol[it] * 4 + 16);
     }
+    __builtin_amdgcn_wave_barrier();
+    if constexpr (kAux) {
+      if (mi + 1 < MF) {
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+          aux[(mi + 1) & 1][it] = epi_load_aux<EPI>(p, x, mw0 + (mi + 1) * 16 + srow[it], nw0 + scol[it]);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+      epi_store8<EPI>(p, x, mw0 + mi * 16 + srow[it], nw0 + scol[it], v[it][0] + b0[it], v[it][1] + b1[it],
+                      aux[mi & 1][it]);
+  }
+}
+
+// vmcnt immediates must be literals: counted waits for the stage pipelines below.
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define ES_VMC(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    ES_VMC(1) ES_VMC(2) ES_VMC(3) ES_VMC(4) ES_VMC(5) ES_VMC(6) ES_VMC(7) ES_VMC(8) ES_VMC(9) ES_VMC(10)
+    ES_VMC(12) ES_VMC(15) ES_VMC(16) ES_VMC(18) ES_VMC(20) ES_VMC(24)
+#undef ES_VMC
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
 
@@ -240,21 +293,109 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
   }
 
   __builtin_amdgcn_s_barrier();
-  staged_epilogue<EPI>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
+  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 
 
-// vmcnt immediates must be literals: counted waits for the stage pipelines below.
-__device__ __forceinline__ void wait_vmcnt(int n) {
-  switch (n) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
-    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
-    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
-    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
-    case 16: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+// Big-tile family: (WM*MF*16) x ((8/WM)*NF*16) output tile, 8 waves (WM along M), one
+// workgroup per CU.  K step 32 (64-B LDS rows, swz64), NST-stage glds ring: stage k+NST-1 is
+// issued right after the barrier that publishes stage k, so NST-1 stages stay in flight
+// ACROSS the barriers (counted vmcnt, raw s_barrier -- cdna_hip_programming.md §5 T3/T4).
+// 128-row wave tiles (WM=2) read 12 KiB of LDS per 32 MFMAs instead of 16 KiB for 64x64 tiles.
+// The B tile may have a half glds instruction per wave (BN = 192: 24 rows per wave); the
+// instruction count per wave stays uniform so the vmcnt arithmetic holds for every wave.
+template <int EPI, int WM, int MF, int NF, int NST>
+__global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int WN = 8 / WM;
+  constexpr int TBM = WM * MF * 16, TBN = WN * NF * 16;
+  constexpr int IA = TBM / 128;                 // full 1-KiB glds per wave for A (16 rows each)
+  constexpr int IBF = TBN / 128;                // full glds per wave for B
+  constexpr int IBH = (TBN % 128) ? 1 : 0;      // plus one half (8 rows, lanes 0..31)
+  static_assert(TBM % 128 == 0 && (TBN % 128 == 0 || TBN % 128 == 64), "tile");
+  constexpr int PER = IA + IBF + IBH;
+  constexpr int TA = TBM * 64, STAGE = (TBM + TBN) * 64;
+  const int ntn = p.N / TBN;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (wg / ntn) * TBM, n0 = (wg % ntn) * TBN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int g = lane >> 4, r = lane & 15;
+
+  const bf16* ga[IA];
+  const bf16* gb[IBF + IBH];
+  int da[IA], db[IBF + IBH];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = (j * 8 + w) * 16 + (lane >> 2);
+    ga[j] = p.A + (size_t)(m0 + row) * p.lda + swz64(row, lane & 3) * 8;
+    da[j] = (j * 8 + w) * 1024;
   }
+#pragma unroll
+  for (int j = 0; j < IBF; ++j) {
+    const int row = (j * 8 + w) * 16 + (lane >> 2);
+    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + swz64(row, lane & 3) * 8;
+    db[j] = TA + (j * 8 + w) * 1024;
+  }
+  if constexpr (IBH) {
+    const int row = IBF * 128 + w * 8 + ((lane & 31) >> 2);
+    gb[IBF] = p.B + (size_t)(n0 + row) * p.ldb + swz64(row, lane & 3) * 8;
+    db[IBF] = TA + IBF * 128 * 64 + w * 512;
+  }
+#define BIG_ISSUE(BUF, K0)                                                        \
+  {                                                                               \
+    char* S_ = smem + (BUF) * STAGE;                                              \
+    _Pragma("unroll") for (int j = 0; j < IA; ++j) glds16(ga[j] + (K0), S_ + da[j]); \
+    _Pragma("unroll") for (int j = 0; j < IBF; ++j) glds16(gb[j] + (K0), S_ + db[j]); \
+    if constexpr (IBH) {                                                          \
+      if (lane < 32) glds16(gb[IBF] + (K0), S_ + db[IBF]);                        \
+    }                                                                             \
+  }
+
+  f32x4 acc[MF][NF];
+#pragma unroll
+  for (int i = 0; i < MF; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / 32;
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) BIG_ISSUE(st, st * 32)
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vmcnt(min(NST - 2, nk - 1 - kt) * PER);
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nk) {
+      int nb = buf + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
+      BIG_ISSUE(nb, (kt + NST - 1) * 32)
+    }
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + TA;
+    bf16x8 af[MF], bfr[NF];
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int rb = wn * NF * 16 + j * 16 + r;
+      bfr[j] = *(const bf16x8*)(Bs + rb * 64 + swz64(rb, g) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+      const int ra = wm * MF * 16 + i * 16 + r;
+      af[i] = *(const bf16x8*)(As + ra * 64 + swz64(ra, g) * 16);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    buf = buf + 1 == NST ? 0 : buf + 1;
+  }
+#undef BIG_ISSUE
+  __builtin_amdgcn_s_barrier();
+  staged_epilogue_g<EPI, MF, NF>(p, smem + w * 16 * (NF * 64 + 16), acc, m0 + wm * MF * 16, n0 + wn * NF * 16,
+                                 lane);
 }
 
 // v0 family: 128x128 output tile, 4 waves (2x2, 64x64 each), K step BKT in {32, 64}, NST-stage
@@ -263,12 +404,13 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 // s_barrier.  Small footprints (BKT=32: 16 KiB per stage) let 3-4 workgroups share a CU, so one
 // tile's epilogue overlaps other tiles' MFMAs.
 //   BKT=64: 128-B LDS rows, chunk c of row r at c ^ ((r>>1)&7)
-//   BKT=32:  64-B LDS rows, chunk c of row r at c ^ ((r>>2)&3)   (both conflict-free for the
-//            16-row x 16-B fragment reads)
+//   BKT=32:  64-B LDS rows, chunk c of row r at c ^ ((-(r>>2))&3)   (both conflict-free for the
+//            16-row x 16-B fragment reads under the ds_read_b128 lane groups of
+//            MI355X_MICROARCH.md §LDS; the plain c ^ ((r>>2)&3) is 2-way conflicted there)
 template <int BKT>
 __device__ __forceinline__ int swzk(int r, int c) {
   if constexpr (BKT == 64) return c ^ ((r >> 1) & 7);
-  else return c ^ ((r >> 2) & 3);
+  else return swz64(r, c);
 }
 
 template <int EPI, int BKT, int NST>
@@ -348,7 +490,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
 
   // ---- epilogue through LDS (stage buffers are free once every wave passed the last MFMA) ----
   __builtin_amdgcn_s_barrier();
-  staged_epilogue<EPI>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
+  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
 }
 #undef NT_ISSUE
 
@@ -593,6 +735,35 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
 #undef NT_EPIS
 #undef NT_LAUNCH
 
+#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_)                                                   \
+  {                                                                                          \
+    const size_t lds = (size_t)NST_ * (WM_ * MF_ * 16 + (8 / WM_) * NF_ * 16) * 64;          \
+    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_>, lds);                              \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_>), dim3(grid), dim3(512), lds, \
+                       stream, a);                                                           \
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;                           \
+  }
+#define BIG_EPIS(WM_, MF_, NF_, NST_)                                 \
+  switch (epi) {                                                      \
+    case EPI_BF16: BIG_LAUNCH(EPI_BF16, WM_, MF_, NF_, NST_)          \
+    case EPI_GELU: BIG_LAUNCH(EPI_GELU, WM_, MF_, NF_, NST_)          \
+    case EPI_F32_RESID: BIG_LAUNCH(EPI_F32_RESID, WM_, MF_, NF_, NST_) \
+    case EPI_DGELU: BIG_LAUNCH(EPI_DGELU, WM_, MF_, NF_, NST_)        \
+    case EPI_F32: BIG_LAUNCH(EPI_F32, WM_, MF_, NF_, NST_)            \
+    case EPI_PATCH: BIG_LAUNCH(EPI_PATCH, WM_, MF_, NF_, NST_)        \
+    case EPI_GELU_ACT: BIG_LAUNCH(EPI_GELU_ACT, WM_, MF_, NF_, NST_)  \
+    default: return ES_BAD_ARG;                                       \
+  }
+int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
+  switch (cfg) {
+    case 6: BIG_EPIS(2, 8, 4, 4)   // 256x256
+    case 7: BIG_EPIS(2, 8, 3, 4)   // 256x192
+    default: BIG_EPIS(4, 4, 4, 4)  // 256x128
+  }
+}
+#undef BIG_EPIS
+#undef BIG_LAUNCH
+
 }  // namespace es_gemm
 using namespace es_gemm;
 
@@ -614,9 +785,9 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
   // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py): short K
   // (<= 384) is epilogue-bound -> BK32 two-stage at 5 workgroups/CU (BK32 three-stage for the
-  // read-modify-write DGELU epilogue); long K -> 256x128 three-stage ring.
+  // epilogues that read an aux operand: DGELU, residual); long K -> 256x128 three-stage ring.
   int variant = g_gemm_variant;
-  if (variant < 0) variant = K <= 384 ? (epi == EPI_DGELU ? 2 : 5) : 1;
+  if (variant < 0) variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
   if (variant == 1) {
     const int grid = ((M + BM2 - 1) / BM2) * (N / BN);
     const size_t lds = 3 * STAGE2;
@@ -634,6 +805,11 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
+  if (variant >= 6 && variant <= 8) {
+    const int tbn = variant == 6 ? 256 : variant == 7 ? 192 : 128;
+    if (N % tbn) return ES_BAD_SHAPE;
+    return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
+  }
   const int grid = ((M + BM - 1) / BM) * (N / BN);
   const int rc = launch_nt(variant, epi, grid, stream, a);
   if (rc) return rc;
@@ -642,7 +818,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 
 // Tuning knob: which NT kernel family es_gemm_nt launches (-1 = per-shape default, 0 = 128x128
 // BK64 2-stage, 1 = 256x128 BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage,
-// 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage).
+// 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage, 6 = 256x256 / 7 = 256x192 / 8 = 256x128 BK32
+// 4-stage, 8 waves, one workgroup per CU; 6/7 need N % 256 / N % 192 == 0).
 // Returns the previous value.
 int es_set_gemm_variant(int v) {
   const int old = g_gemm_variant;

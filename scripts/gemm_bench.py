@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--variants", default="0,1")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
     args = ap.parse_args()
     lib = _lib.load()
     lib.es_set_gemm_variant.restype = _lib.I
@@ -46,11 +47,16 @@ def main():
     C2 = torch.empty(Mp, HD, device=dev, dtype=torch.bfloat16)
     aux = torch.randn(Mp, HD, device=dev)
     results = {}
+    only = set(args.only.split(",")) if args.only else None
     for name, epi, M, N, K in NT:
+        if only and name not in only:
+            continue
         flops = 2.0 * M * N * K
         times = {v: [] for v in variants}
         for _ in range(args.rounds):
             for v in variants:
+                if N % {6: 256, 7: 192}.get(v, 128):
+                    continue
                 lib.es_set_gemm_variant(v)
                 auxp = aux if epi in (2,) else (aux.bfloat16() if epi == 3 else None)
                 st = [ptr(A), K, ptr(Bw), K, ptr(bias) if epi not in (3, 4) else None, ptr(C), N,
@@ -65,6 +71,8 @@ def main():
                 times[v].append(e0.elapsed_time(e1) / args.iters)
         row = {}
         for v in variants:
+            if not times[v]:
+                continue
             t = sorted(times[v])[len(times[v]) // 2]
             row[v] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1)}
         results[name] = row
@@ -72,6 +80,8 @@ def main():
     ws = torch.empty(64 * HD * D, device=dev)
     out = torch.empty(HD, HD, device=dev)
     for name, M, N1, N2 in TN:
+        if only and name not in only:
+            continue
         flops = 2.0 * M * N1 * N2
         tiles = (N1 // 128) * (N2 // 128)
         splits = max(1, min((M + 31) // 32, -(-512 // tiles)))

@@ -3,5 +3,5 @@
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; OUT="$GRAFT_REPO_ROOT/gpurun_out"
 timeout -k 10 300 python -m pytest tests/test_gpu_kernels.py -q -rf -p no:cacheprovider -k gemm > "$OUT/kg.log" 2>&1; rc=$?
 echo "gemm tests rc=$rc"; tail -3 "$OUT/kg.log"
-[ $rc -le 1 ] && { timeout -k 10 400 python scripts/gemm_bench.py --variants 0,1,2,5 --rounds 3 > "$OUT/gb.log" 2>&1; echo "gemm bench rc=$?"; cat "$OUT/gb.log"; }
+[ $rc -le 1 ] && { timeout -k 10 400 python scripts/gemm_bench.py --variants ${VARIANTS:-1,2,5,6,7,8} --rounds 3 > "$OUT/gb.log" 2>&1; echo "gemm bench rc=$?"; cat "$OUT/gb.log"; }
 exit 0

@@ -40,15 +40,26 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5], ids=["auto", "v0", "v1", "v2", "v3", "v4", "v5"])
+GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8]
+_TILE_N = {6: 256, 7: 192}  # big-tile variants that need N to be a multiple of their tile width
+
+
+@pytest.fixture(params=GEMM_VARIANTS, ids=["auto"] + [f"v{v}" for v in GEMM_VARIANTS[1:]])
 def gemm_variant(request):
     old = _lib.load().es_set_gemm_variant(request.param)
     yield request.param
     _lib.load().es_set_gemm_variant(old)
 
 
-@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 384, 384), (128, 128, 64), (5000, 1152, 1536)])
+def _skip_untileable(variant, N):
+    if N % _TILE_N.get(variant, 128):
+        pytest.skip(f"variant {variant} tiles N by {_TILE_N[variant]}")
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 384, 384), (128, 128, 64), (5000, 1152, 1536),
+                                   (600, 768, 320)])
 def test_gemm_nt_exact_integers(M, N, K, gemm_variant):
+    _skip_untileable(gemm_variant, N)
     g = torch.Generator().manual_seed(M + N + K)
     A = _pad_rows(_int_bf16(M, K, gen=g))
     B = _int_bf16(N, K, gen=g)
@@ -63,9 +74,11 @@ def test_gemm_nt_exact_integers(M, N, K, gemm_variant):
     torch.testing.assert_close(Cb.float(), ref.bfloat16().float(), rtol=0, atol=0)
 
 
-def test_gemm_nt_epilogues_vs_fp32(gemm_variant):
+@pytest.mark.parametrize("N", [512, 384])
+def test_gemm_nt_epilogues_vs_fp32(N, gemm_variant):
+    _skip_untileable(gemm_variant, N)
     torch.manual_seed(0)
-    M, N, K = 777, 512, 384
+    M, K = 777, 384
     A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
     B = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
     bias = torch.randn(N, device=DEV) * 0.1
@@ -92,9 +105,11 @@ def test_gemm_nt_epilogues_vs_fp32(gemm_variant):
     torch.testing.assert_close(dpre.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-def test_gemm_nt_patch_epilogue(gemm_variant):
+@pytest.mark.parametrize("D", [128, 768])
+def test_gemm_nt_patch_epilogue(D, gemm_variant):
+    _skip_untileable(gemm_variant, D)
     torch.manual_seed(1)
-    n, npch, D, K = 3, 16, 128, 768
+    n, npch, K = 3, 16, 768
     M = n * npch
     A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
     B = (torch.randn(D, K, device=DEV) * 0.02).bfloat16()
