@@ -12,8 +12,11 @@ all-reduce + Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.
 
 Reported beside it:
   roofline      dominant kernel = the fc1 forward GEMM (gemm_nt, GELU epilogue), timed live with
-                HIP events on its launch stream over the timed steps; achieved = algorithmic FLOP
-                (2*M*N*K per launch) / mean launch time vs the bf16 dense MFMA peak.
+                HIP events on its launch stream over the timed steps.  Its binding roofline is HBM:
+                698.4 MB algorithmic bytes per launch (A [M,384] bf16 read once + pre-activation and
+                activation [M,1536] bf16 written once) take 87 us at 8 TB/s, its 119 GFLOP 47 us at
+                the bf16 dense MFMA peak.  achieved = algorithmic bytes / mean launch time; the MFMA
+                view (algorithmic FLOP / time vs 2516.6 TFLOP/s) is reported beside it.
   step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.
   cpu_baseline  the oracle (CPU fp32 restatement pinned to the reference, kind "port") timed on a
                 bounded sample (B=8, mu=7: 56 unlabeled images/step) on the host cores, rank 0, N=1.
@@ -33,6 +36,7 @@ import torch  # noqa: E402
 MEAN = (0.485, 0.456, 0.406)
 STD = (0.229, 0.224, 0.225)
 PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12  # 2516.6 dense (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md §HBM; ~6300 achievable)
 STEP_TFLOP_F1 = 18.247  # fwd 960 imgs + bwd 512 imgs, 9.197 GFLOP/img fwd
 
 
@@ -154,7 +158,11 @@ def main():
     ev_ms = [e0.elapsed_time(e1) for e0, e1, _ in probe["events"]]
     flops = [f for _, _, f in probe["events"]]
     mean_ms = sum(ev_ms) / len(ev_ms)
-    achieved = sum(flops) / (sum(ev_ms) / 1e3) / 1e12  # TFLOP/s over the probed launches
+    tflops = sum(flops) / (sum(ev_ms) / 1e3) / 1e12  # TFLOP/s over the probed launches
+    M_tok, N_hid, K_dim = B * (1 + MU) * 197, 1536, 384
+    # A read + pre/act written (bf16) + weight image and bias read once
+    alg_bytes = 2 * M_tok * K_dim + 2 * 2 * M_tok * N_hid + 2 * N_hid * K_dim + 4 * N_hid
+    gbs = alg_bytes / (mean_ms / 1e3) / 1e9
     traffic = pmc_traffic("gemm_nt_kernel<1,")
 
     if rank == 0:
@@ -174,11 +182,13 @@ def main():
             "step_tflops": round(STEP_TFLOP_F1 / (ms / 1e3), 1),
             "step_mfma_frac": round(STEP_TFLOP_F1 / (ms / 1e3) / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(loss, 6),
-            "roofline": {"kernel": "gemm_nt_kernel<EPI_GELU> (train fc1 forward: M=100864, N=1536, K=384, "
+            "roofline": {"kernel": f"gemm_nt_kernel<EPI_GELU> (train fc1 forward: M={M_tok}, N=1536, K=384, "
                                    "bias + exact-GELU epilogue writing pre-activation and activation, bf16)",
-                         "bound": "mfma", "achieved": round(achieved, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
-                         "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms), "traffic": traffic},
+                         "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
+                         "algorithmic_bytes": alg_bytes, "mean_launch_ms": round(mean_ms, 4),
+                         "launches": len(ev_ms), "mfma_tflops": round(tflops, 1),
+                         "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4)},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline()

@@ -76,12 +76,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   const int nqt = (T + 15) >> 4;
+  const float sl = a.scale * 1.44269504088896341f;
   for (int qb = w; qb < nqt; qb += 4) {
     const int q = qb * 16 + r;
     const bool qv = q < T;
     const bf16* qrow = base + (size_t)q * a.ldqkv + h * 64;
     const bf16x8 qf0 = ld_row8(qrow + 8 * g, qv), qf1 = ld_row8(qrow + 32 + 8 * g, qv);
 
+    // scores in log2 units (scale * log2 e folded in): p = exp2(s - max) is one v_exp_f32; keys
+    // are masked only in the partial last tile (the branch is uniform per tile).
     f32x4 s[2 * NKC];
     float mx = -INFINITY;
 #pragma unroll
@@ -89,13 +92,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       acc = mfma16(lds_row8(Ks, t * 16 + r, g), qf0, acc);
       acc = mfma16(lds_row8(Ks, t * 16 + r, 4 + g), qf1, acc);
+      acc *= sl;
+      if (t * 16 + 16 > T) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = t * 16 + 4 * g + i;
-        const float v = key < T ? acc[i] * a.scale : -INFINITY;
-        acc[i] = v;
-        mx = fmaxf(mx, v);
+        for (int i = 0; i < 4; ++i)
+          if (t * 16 + 4 * g + i >= T) acc[i] = -INFINITY;
       }
+      mx = fmaxf(mx, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
       s[t] = acc;
     }
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
@@ -105,7 +108,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     for (int t = 0; t < 2 * NKC; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float pv = __expf(s[t][i] - mx);
+        const float pv = __builtin_amdgcn_exp2f(s[t][i] - mx);
         s[t][i] = pv;
         l += pv;
       }
@@ -134,7 +137,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
         bf16x4 v = {(bf16)(o[dt][0] * inv), (bf16)(o[dt][1] * inv), (bf16)(o[dt][2] * inv), (bf16)(o[dt][3] * inv)};
         *(bf16x4*)(orow + dt * 16 + 4 * g) = v;
       }
-      if (g == 0) a.lse[(size_t)bh * T + q] = mx + __logf(l);
+      if (g == 0) a.lse[(size_t)bh * T + q] = (mx + __log2f(l)) * 0.69314718055994531f;  // natural log
     }
   }
 }
@@ -171,7 +174,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     delta += __shfl_xor(delta, 16, 64);
     delta += __shfl_xor(delta, 32, 64);
     if (qv && g == 0) a.delta[(size_t)bh * T + q] = delta;  // consumed by attn_bwd_dkv_kernel
-    const float lq = qv ? a.lse[(size_t)bh * T + q] : 0.f;
+    const float lq = qv ? a.lse[(size_t)bh * T + q] * 1.44269504088896341f : 0.f;  // log2 units
+    const float sl = a.scale * 1.44269504088896341f;
 
     f32x4 dq[4];
 #pragma unroll
@@ -187,12 +191,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
         sv = mfma16(lds_row8(Ks, t * 16 + r, 4 + g), qf1, sv);
         dp = mfma16(lds_row8(Vs, t * 16 + r, g), df0, dp);
         dp = mfma16(lds_row8(Vs, t * 16 + r, 4 + g), df1, dp);
+        f32x4 pv;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int key = t * 16 + 4 * g + i;
-          const float pv = key < T ? __expf(sv[i] * a.scale - lq) : 0.f;
-          dsf[4 * hf + i] = (bf16)(pv * (dp[i] - delta));
+        for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sv[i] * sl - lq);
+        if (t * 16 + 16 > T) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (t * 16 + 4 * g + i >= T) pv[i] = 0.f;
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dsf[4 * hf + i] = (bf16)(pv[i] * (dp[i] - delta));
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(lds_trT(Ks, sc * 32, dt * 16, g, r), dsf, dq[dt]);
@@ -224,7 +232,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   load_head_tile(Qs, base + h * 64, a.ldqkv, T, TP);
   load_head_tile(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
-  for (int t = threadIdx.x; t < TP; t += blockDim.x) lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] : INFINITY;
+  // lse in log2 units; padded queries get +inf so their probabilities are exactly 0
+  for (int t = threadIdx.x; t < TP; t += blockDim.x)
+    lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] * 1.44269504088896341f : INFINITY;
+  const float sl = a.scale * 1.44269504088896341f;
   for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
   __syncthreads();
 
@@ -254,7 +265,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
         const f32x4 d4 = *(const f32x4*)(del_s + u * 16 + 4 * g);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float pv = __expf(sv[i] * a.scale - l4[i]);
+          const float pv = __builtin_amdgcn_exp2f(sv[i] * sl - l4[i]);
           pf[4 * hf + i] = (bf16)pv;
           dsf[4 * hf + i] = (bf16)(pv * (dp[i] - d4[i]));
         }

@@ -769,6 +769,7 @@ using namespace es_gemm;
 
 // ----------------------------------------------------------------- C-ABI entry points
 static int g_gemm_variant = -1;
+static int g_tn_variant = -1;
 
 
 extern "C" {
@@ -827,6 +828,14 @@ int es_set_gemm_variant(int v) {
   return old;
 }
 
+// Tuning knob for es_gemm_tn: -1 = default, 0..4 = (token step, ring depth) in
+// {32x2, 32x3, 32x4, 64x2, 64x3}.  Returns the previous value.
+int es_set_tn_variant(int v) {
+  const int old = g_tn_variant;
+  g_tn_variant = v;
+  return old;
+}
+
 // workspace floats needed by es_gemm_tn for `splits` splits (slabs + bias partials)
 size_t es_gemm_tn_workspace(int N1, int N2, int splits) { return (size_t)splits * N1 * N2 + (size_t)splits * N1; }
 
@@ -834,8 +843,9 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream) {
   if (M <= 0 || (N1 % BM) || (N2 % BN) || splits <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
-  // token step: 32 (5 workgroups/CU) -- measured faster than 64 on every ViT-S wgrad shape
-  constexpr int BKM = 32, NST = 2;
+  // variant: token step BKM and ring depth NST (0 = 32x2, 1 = 32x3, 2 = 32x4, 3 = 64x2, 4 = 64x3)
+  const int v = g_tn_variant < 0 ? 2 : g_tn_variant;
+  const int BKM = v >= 3 ? 64 : 32;
   const int msteps = (M + BKM - 1) / BKM;
   const int per = (msteps + splits - 1) / splits;
   const int S = (msteps + per - 1) / per;
@@ -844,8 +854,20 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
   float* PB = bias_out ? workspace + (size_t)S * N1 * N2 : nullptr;
   TNArgs a{(const bf16*)A1, (const bf16*)A2, P, PB, M, N1, N2, ld1, ld2, per * BKM};
   const int grid = S * (N1 / BM) * (N2 / BN);
-  const size_t lds = (size_t)NST * 2 * BKM * BM * 2;
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_kernel<BKM, NST>), dim3(grid), dim3(256), lds, stream, a);
+#define TN_LAUNCH(BKM_, NST_)                                                                           \
+  {                                                                                                   \
+    const size_t lds = (size_t)NST_ * 2 * BKM_ * BM * 2;                                              \
+    allow_lds(gemm_tn_kernel<BKM_, NST_>, lds);                                                       \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_kernel<BKM_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
+  }
+  switch (v) {
+    case 0: TN_LAUNCH(32, 2) break;
+    case 1: TN_LAUNCH(32, 3) break;
+    case 3: TN_LAUNCH(64, 2) break;
+    case 4: TN_LAUNCH(64, 3) break;
+    default: TN_LAUNCH(32, 4) break;
+  }
+#undef TN_LAUNCH
   if (!direct) {
     const int n = N1 * N2;
     int rg = (n / 4 + 255) / 256;

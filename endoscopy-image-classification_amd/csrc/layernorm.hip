@@ -1,54 +1,73 @@
 // LayerNorm(eps=1e-6) forward / backward over the fp32 residual stream (gfx950).
 //
 // Replaces Block.norm1 / norm2 (code/models/conformer.py:58,60,65,70-71; nn.LayerNorm(dim, 1e-6)).
-// One wave per token row, D/128 float2 per lane (coalesced), statistics in fp32 with a two-pass
-// variance.  Forward writes the bf16 GEMM operand and the per-row (mean, rstd) the backward needs.
+// One wave per token row (two rows in flight), D/128 float2 per lane (coalesced), statistics in
+// fp32 with a two-pass variance.  Forward writes the bf16 GEMM operand and the per-row (mean, rstd) the backward needs.
 // Backward fuses the residual-gradient add (dx = dres + LN'(dy)), writes fp32 and bf16 copies of
 // dx, and per-workgroup partial sums of dgamma / dbeta that es_splitk_reduce folds into the grads.
 #include "common.h"
 
 namespace {
 
+// Two rows per wave (R = 2): 3 KiB of loads in flight per wave at D = 384 -- with one row per wave
+// the ~48 KiB in flight per CU did not cover HBM latency (MI355X_MICROARCH.md §HBM).
 template <int V>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x, int ldx,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      bf16* __restrict__ y, int ldy, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out, int M, float eps) {
-  constexpr int D = V * 128;
+  constexpr int D = V * 128, R = 2;
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= M) return;
-  const float* xr = x + (size_t)row * ldx;
-  float2 v[V];
-  float s = 0.f;
+  const int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= M) return;
+  float2 v[R][V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    v[j] = *(const float2*)(xr + (j * 64 + lane) * 2);
-    s += v[j].x + v[j].y;
-  }
-  const float mean = warp_sum(s) * (1.0f / D);
-  float ss = 0.f;
+  for (int q = 0; q < R; ++q) {
+    const int row = min(row0 + q, M - 1);
+    const float* xr = x + (size_t)row * ldx;
 #pragma unroll
-  for (int j = 0; j < V; ++j) {
-    const float a = v[j].x - mean, b = v[j].y - mean;
-    ss += a * a + b * b;
+    for (int j = 0; j < V; ++j) v[q][j] = *(const float2*)(xr + (j * 64 + lane) * 2);
   }
-  const float rstd = 1.0f / sqrtf(warp_sum(ss) * (1.0f / D) + eps);
-  bf16* yr = y + (size_t)row * ldy;
+  float2 gm[V], bt[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) {
     const int c = (j * 64 + lane) * 2;
-    const float2 gm = *(const float2*)(gamma + c), bt = *(const float2*)(beta + c);
-    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-    bf16x2 o = {(bf16)((v[j].x - mean) * rstd * gm.x + bt.x), (bf16)((v[j].y - mean) * rstd * gm.y + bt.y)};
-    *(bf16x2*)(yr + c) = o;
+    gm[j] = *(const float2*)(gamma + c);
+    bt[j] = *(const float2*)(beta + c);
   }
-  if (lane == 0) {
-    mean_out[row] = mean;
-    rstd_out[row] = rstd;
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int row = row0 + q;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) s += v[q][j].x + v[q][j].y;
+    const float mean = warp_sum(s) * (1.0f / D);
+    float ss = 0.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      const float a = v[q][j].x - mean, b = v[q][j].y - mean;
+      ss += a * a + b * b;
+    }
+    const float rstd = 1.0f / sqrtf(warp_sum(ss) * (1.0f / D) + eps);
+    if (row < M) {
+      bf16* yr = y + (size_t)row * ldy;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = (j * 64 + lane) * 2;
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        bf16x2 o = {(bf16)((v[q][j].x - mean) * rstd * gm[j].x + bt[j].x),
+                    (bf16)((v[q][j].y - mean) * rstd * gm[j].y + bt[j].y)};
+        *(bf16x2*)(yr + c) = o;
+      }
+      if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+      }
+    }
   }
 }
 
+// Each wave walks rows two at a time (both rows' dy / x / dres loads issued before any math).
 template <int V>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const float* __restrict__ x,
                                                      int ldx, const float* __restrict__ mean_in,
@@ -56,47 +75,61 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      const float* __restrict__ dres, int ldres, float* __restrict__ dx,
                                                      int lddx, bf16* __restrict__ dxb, int lddxb,
                                                      float* __restrict__ pg, float* __restrict__ pb, int M) {
-  constexpr int D = V * 128;
+  constexpr int D = V * 128, R = 2;
   __shared__ float red[2][4][D];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float2 ag[V], ab[V];
+  float2 ag[V], ab[V], gm[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) ag[j] = ab[j] = make_float2(0.f, 0.f);
-  for (int row = blockIdx.x * 4 + w; row < M; row += gridDim.x * 4) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float2 xh[V], gd[V];
-    float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < V; ++j) {
+    ag[j] = ab[j] = make_float2(0.f, 0.f);
+    gm[j] = *(const float2*)(gamma + (j * 64 + lane) * 2);
+  }
+  for (int row0 = (blockIdx.x * 4 + w) * R; row0 < M; row0 += gridDim.x * 4 * R) {
+    float2 d[R][V], xv[R][V], rv[R][V];
+    float mean[R], rstd[R];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const int c = (j * 64 + lane) * 2;
-      const float2 d = *(const float2*)(dy + (size_t)row * lddy + c);
-      const float2 xv = *(const float2*)(x + (size_t)row * ldx + c);
-      const float2 gm = *(const float2*)(gamma + c);
-      xh[j] = make_float2((xv.x - mean) * rstd, (xv.y - mean) * rstd);
-      gd[j] = make_float2(d.x * gm.x, d.y * gm.y);
-      s1 += gd[j].x + gd[j].y;
-      s2 += gd[j].x * xh[j].x + gd[j].y * xh[j].y;
-      ag[j].x += d.x * xh[j].x;
-      ag[j].y += d.y * xh[j].y;
-      ab[j].x += d.x;
-      ab[j].y += d.y;
-    }
-    s1 = warp_sum(s1) * (1.0f / D);
-    s2 = warp_sum(s2) * (1.0f / D);
+    for (int q = 0; q < R; ++q) {
+      const int row = min(row0 + q, M - 1);
+      mean[q] = mean_in[row];
+      rstd[q] = rstd_in[row];
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-      const int c = (j * 64 + lane) * 2;
-      float2 o = make_float2(rstd * (gd[j].x - s1 - xh[j].x * s2), rstd * (gd[j].y - s1 - xh[j].y * s2));
-      if (dres) {
-        const float2 r = *(const float2*)(dres + (size_t)row * ldres + c);
-        o.x += r.x;
-        o.y += r.y;
+      for (int j = 0; j < V; ++j) {
+        const int c = (j * 64 + lane) * 2;
+        d[q][j] = *(const float2*)(dy + (size_t)row * lddy + c);
+        xv[q][j] = *(const float2*)(x + (size_t)row * ldx + c);
+        rv[q][j] = dres ? *(const float2*)(dres + (size_t)row * ldres + c) : make_float2(0.f, 0.f);
       }
-      *(float2*)(dx + (size_t)row * lddx + c) = o;
-      if (dxb) {
-        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-        bf16x2 ob = {(bf16)o.x, (bf16)o.y};
-        *(bf16x2*)(dxb + (size_t)row * lddxb + c) = ob;
+    }
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int row = row0 + q;
+      if (row >= M) break;
+      float2 xh[V], gd[V];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        xh[j] = make_float2((xv[q][j].x - mean[q]) * rstd[q], (xv[q][j].y - mean[q]) * rstd[q]);
+        gd[j] = make_float2(d[q][j].x * gm[j].x, d[q][j].y * gm[j].y);
+        s1 += gd[j].x + gd[j].y;
+        s2 += gd[j].x * xh[j].x + gd[j].y * xh[j].y;
+        ag[j].x += d[q][j].x * xh[j].x;
+        ag[j].y += d[q][j].y * xh[j].y;
+        ab[j].x += d[q][j].x;
+        ab[j].y += d[q][j].y;
+      }
+      s1 = warp_sum(s1) * (1.0f / D);
+      s2 = warp_sum(s2) * (1.0f / D);
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int c = (j * 64 + lane) * 2;
+        const float2 o = make_float2(rstd[q] * (gd[j].x - s1 - xh[j].x * s2) + rv[q][j].x,
+                                     rstd[q] * (gd[j].y - s1 - xh[j].y * s2) + rv[q][j].y);
+        *(float2*)(dx + (size_t)row * lddx + c) = o;
+        if (dxb) {
+          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+          bf16x2 ob = {(bf16)o.x, (bf16)o.y};
+          *(bf16x2*)(dxb + (size_t)row * lddxb + c) = ob;
+        }
       }
     }
   }
@@ -135,7 +168,7 @@ int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* b
                      float* rstd, int M, int D, float eps, hipStream_t stream) {
   if (M <= 0 || D % 128 || ldx % 2 || ldy % 2) return ES_BAD_SHAPE;
   if (!x || !gamma || !beta || !y || !mean || !rstd) return ES_BAD_ARG;
-  const int grid = (M + 3) / 4;
+  const int grid = (M + 7) / 8;  // 4 waves x 2 rows
   LN_DISPATCH(ln_fwd_kernel, D / 128, grid, stream, x, ldx, gamma, beta, (bf16*)y, ldy, mean, rstd, M, eps);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
@@ -147,7 +180,7 @@ int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const f
                      hipStream_t stream) {
   if (M <= 0 || D % 128 || blocks <= 0) return ES_BAD_SHAPE;
   if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || !workspace) return ES_BAD_ARG;
-  const int grid = blocks < (M + 3) / 4 ? blocks : (M + 3) / 4;
+  const int grid = blocks < (M + 7) / 8 ? blocks : (M + 7) / 8;
   float* pg = workspace;
   float* pb = workspace + (size_t)grid * D;
   LN_DISPATCH(ln_bwd_kernel, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,

@@ -305,7 +305,7 @@ class Engine:
         D = self.cfg.dim
         ws = self.workspace()
         call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
-             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 512, M, D, 0, _lib.stream())
+             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
     def backward(self, flat, grad, dlogits):
         """dlogits fp32 [n, C] for the last train forward -> grad (flat fp32, overwritten)."""

@@ -44,6 +44,9 @@ int es_set_gemm_variant(int variant);
  * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced; bias_out (nullable) (+)=
  * sum_m A1[m,:] computed from the same LDS tiles.  N1,N2 % 128 == 0; rows in [M, round_up(M,64))
  * of A1 must be zero. */
+/* tuning knob for es_gemm_tn: -1 = default, 0..4 = (token step, ring depth) 32x2, 32x3, 32x4, 64x2,
+ * 64x3; returns the previous value */
+int es_set_tn_variant(int variant);
 size_t es_gemm_tn_workspace(int N1, int N2, int splits);
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream);

@@ -31,10 +31,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
+    ap.add_argument("--tn-variants", default="0,2")
     args = ap.parse_args()
     lib = _lib.load()
     lib.es_set_gemm_variant.restype = _lib.I
     lib.es_set_gemm_variant.argtypes = [_lib.I]
+    lib.es_set_tn_variant.restype = _lib.I
+    lib.es_set_tn_variant.argtypes = [_lib.I]
+    tn_variants = [int(v) for v in args.tn_variants.split(",")]
     variants = [int(v) for v in args.variants.split(",")]
     dev = "cuda"
     torch.manual_seed(0)
@@ -85,17 +89,25 @@ def main():
         flops = 2.0 * M * N1 * N2
         tiles = (N1 // 128) * (N2 // 128)
         splits = max(1, min((M + 31) // 32, -(-512 // tiles)))
-        for _ in range(2):
-            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(args.iters):
-            call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
-        e1.record()
-        torch.cuda.synchronize()
-        t = e0.elapsed_time(e1) / args.iters
-        results[name] = {"tn": {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}}
-        print(name, json.dumps(results[name]), flush=True)
+        times = {v: [] for v in tn_variants}
+        for _ in range(args.rounds):
+            for v in tn_variants:
+                lib.es_set_tn_variant(v)
+                call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.iters):
+                    call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.iters)
+        lib.es_set_tn_variant(-1)
+        row = {}
+        for v in tn_variants:
+            t = sorted(times[v])[len(times[v]) // 2]
+            row[f"tn{v}"] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}
+        results[name] = row
+        print(name, json.dumps(row), flush=True)
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
     json.dump(results, open(os.path.join(out_dir, "gemm_bench.json"), "w"), indent=1)

@@ -1,16 +1,17 @@
 #!/bin/bash
-# SQ / TA counter passes (one group per pass, no tracing) over selected GEMM shapes:
-# where do the waves' cycles go (parked on waits, issue-stalled, active VALU / MFMA / LDS)?
+# SQ / TA / TCP / TCC counter passes (one group per pass, no tracing) over selected GEMM shapes:
+# where do the waves' cycles go, and which memory-pipeline stage stalls?
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; OUT="$GRAFT_REPO_ROOT/gpurun_out"; export TMPDIR=/tmp
-timeout -k 10 120 rocprofv3 -L > "$OUT/counters_avail.txt" 2>&1; echo "list rc=$?"
-B="python3 $GRAFT_REPO_ROOT/scripts/gemm_bench.py --variants ${VARIANTS:-5,1} --rounds 1 --iters 2 --only ${ONLY:-fc1_fwd,fc2_fwd,fc1_dgrad,fc2_wgrad}"
+B="python3 $GRAFT_REPO_ROOT/scripts/gemm_bench.py --variants ${VARIANTS:-5,1} --rounds 1 --iters 2 --only ${ONLY:-fc1_fwd,fc2_fwd,fc2_wgrad}"
 i=0
-for C in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
-         "SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM GRBM_GUI_ACTIVE" \
-         "TA_TA_BUSY_sum TA_BUSY_avr TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum GRBM_COUNT"; do
+for C in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_VMEM_WR_TA_DATA_FIFO_FULL SQ_VMEM_TA_CMD_FIFO_FULL" \
+         "TCP_PENDING_STALL_CYCLES_sum TCP_UTCL1_THRASHING_STALL_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum GRBM_GUI_ACTIVE" \
+         "TCP_TCC_WRITE_REQ_LATENCY_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_UTCL1_STALL_MULTI_MISS_sum" \
+         "TCC_EA0_WRREQ_STALL_sum TCC_TAG_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_BUSY_sum" \
+         "TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TA_TA_BUSY_sum TCP_TCC_WRITE_REQ_sum TCP_TCC_READ_REQ_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/sq$i" -o run --output-format csv -- $B > "$OUT/sq$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"
-  [ $rc -ne 0 ] && { tail -5 "$OUT/sq$i.log"; [ $rc -gt 1 ] && [ $rc -ne 2 ] && break; }
+  [ $rc -ne 0 ] && { tail -5 "$OUT/sq$i.log"; [ $rc -gt 1 ] && break; }
 done
 exit 0

@@ -124,8 +124,16 @@ def test_gemm_nt_patch_epilogue(D, gemm_variant):
 
 
 # ------------------------------------------------------------------------------------- GEMM TN
-@pytest.mark.parametrize("M,N1,N2,splits", [(1000, 128, 256, 1), (1000, 384, 128, 5), (4096, 256, 384, 17)])
-def test_gemm_tn_exact_integers(M, N1, N2, splits):
+@pytest.fixture(params=[-1, 0, 1, 2, 3, 4], ids=["auto", "t0", "t1", "t2", "t3", "t4"])
+def tn_variant(request):
+    old = _lib.load().es_set_tn_variant(request.param)
+    yield request.param
+    _lib.load().es_set_tn_variant(old)
+
+
+@pytest.mark.parametrize("M,N1,N2,splits", [(1000, 128, 256, 1), (1000, 384, 128, 5), (4096, 256, 384, 17),
+                                            (3000, 128, 128, 2)])
+def test_gemm_tn_exact_integers(M, N1, N2, splits, tn_variant):
     g = torch.Generator().manual_seed(M + splits)
     A1 = _pad_rows(_int_bf16(M, N1, lo=-2, hi=3, gen=g))
     A2 = _pad_rows(_int_bf16(M, N2, lo=-2, hi=3, gen=g))
@@ -206,9 +214,9 @@ def test_attention_bwd(n, T, H):
 
 # ------------------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("D", [128, 384, 768])
-def test_layernorm_fwd_bwd(D):
+@pytest.mark.parametrize("M", [1000, 1001, 7])
+def test_layernorm_fwd_bwd(D, M):
     torch.manual_seed(D)
-    M = 1000
     x = torch.randn(M, D, device=DEV) * 2 + 0.5
     gamma = 1 + 0.1 * torch.randn(D, device=DEV)
     beta = 0.1 * torch.randn(D, device=DEV)
@@ -234,6 +242,13 @@ def test_layernorm_fwd_bwd(D):
     torch.testing.assert_close(dxb.float(), (xr.grad + dres), rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+    # few workgroups: each wave walks many row pairs (grid-stride path)
+    dx2, dg2, db2 = torch.zeros_like(dx), torch.zeros_like(dg), torch.zeros_like(db)
+    call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx2), D,
+         None, D, ptr(dg2), ptr(db2), ptr(ws), 5, M, D, 0, S())
+    torch.testing.assert_close(dx2, dx, rtol=0, atol=0)
+    torch.testing.assert_close(dg2, gr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db2, br.grad, rtol=1e-4, atol=1e-3)
 
 
 # ------------------------------------------------------------------------------------- ViT ends
