@@ -844,7 +844,7 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
   if (M <= 0 || (N1 % BM) || (N2 % BN) || splits <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
   // variant: token step BKM and ring depth NST (0 = 32x2, 1 = 32x3, 2 = 32x4, 3 = 64x2, 4 = 64x3)
-  const int v = g_tn_variant < 0 ? 2 : g_tn_variant;
+  const int v = g_tn_variant < 0 ? 0 : g_tn_variant;  // 32x2 measured fastest (deeper rings cost occupancy)
   const int BKM = v >= 3 ? 64 : 32;
   const int msteps = (M + BKM - 1) / BKM;
   const int per = (msteps + splits - 1) / splits;
@@ -865,7 +865,8 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
     case 1: TN_LAUNCH(32, 3) break;
     case 3: TN_LAUNCH(64, 2) break;
     case 4: TN_LAUNCH(64, 3) break;
-    default: TN_LAUNCH(32, 4) break;
+    case 2: TN_LAUNCH(32, 4) break;
+    default: TN_LAUNCH(32, 2) break;
   }
 #undef TN_LAUNCH
   if (!direct) {

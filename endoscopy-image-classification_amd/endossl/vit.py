@@ -156,7 +156,11 @@ class _Grads:
 class Engine:
     """Explicit forward / backward of the ViT over C-ABI kernels.  One per (model, device)."""
 
-    TN_TARGET_BLOCKS = 512
+    # split-K sizing of the weight-gradient GEMMs: ~6 workgroups per CU (scripts/gemm_bench.py
+    # --tn-blocks sweep on MI355X: 1536 beat 512 by 10-25% on the fc1/fc2/qkv shapes); the split
+    # count is capped so the fp32 slabs stay small for the square 384x384 projection
+    TN_TARGET_BLOCKS = 1536
+    TN_MAX_SPLITS = 128
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -227,7 +231,8 @@ class Engine:
             cfg = self.cfg
             D, Hd = cfg.dim, cfg.hidden
             n_tn = max(a * b for a, b in ((3 * D, D), (D, D), (Hd, D), (D, Hd), (D, 3 * cfg.patch * cfg.patch)))
-            self._ws = torch.empty(64 * n_tn + 2 * 1024 * max(Hd, 3 * D), dtype=torch.float32, device=self.device)
+            self._ws = torch.empty(self.TN_MAX_SPLITS * n_tn + 2 * 1024 * max(Hd, 3 * D), dtype=torch.float32,
+                                   device=self.device)
         return self._ws
 
     # -------------------------------------------------------------- forward
@@ -292,12 +297,14 @@ class Engine:
     def _tn_splits(self, M, N1, N2):
         tiles = (N1 // 128) * (N2 // 128)
         msteps = (M + 31) // 32
-        return max(1, min(msteps, -(-self.TN_TARGET_BLOCKS // tiles)))
+        return max(1, min(msteps, self.TN_MAX_SPLITS, -(-self.TN_TARGET_BLOCKS // tiles)))
 
     def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None):
         """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy."""
         ws = self.workspace()
         splits = self._tn_splits(M, N1, N2)
+        if _lib.load().es_gemm_tn_workspace(N1, N2, splits) > ws.numel():
+            raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
         call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
              _lib.stream())
 

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--tn-variants", default="0,2")
+    ap.add_argument("--tn-blocks", default="512", help="target workgroup counts (split-K sizing) to sweep")
     args = ap.parse_args()
     lib = _lib.load()
     lib.es_set_gemm_variant.restype = _lib.I
@@ -81,31 +82,33 @@ def main():
             row[v] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1)}
         results[name] = row
         print(name, json.dumps(row), flush=True)
-    ws = torch.empty(64 * HD * D, device=dev)
+    ws = torch.empty(160 * HD * D, device=dev)
     out = torch.empty(HD, HD, device=dev)
     for name, M, N1, N2 in TN:
         if only and name not in only:
             continue
         flops = 2.0 * M * N1 * N2
         tiles = (N1 // 128) * (N2 // 128)
-        splits = max(1, min((M + 31) // 32, -(-512 // tiles)))
-        times = {v: [] for v in tn_variants}
-        for _ in range(args.rounds):
-            for v in tn_variants:
-                lib.es_set_tn_variant(v)
-                call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(args.iters):
-                    call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
-                e1.record()
-                torch.cuda.synchronize()
-                times[v].append(e0.elapsed_time(e1) / args.iters)
-        lib.es_set_tn_variant(-1)
         row = {}
-        for v in tn_variants:
-            t = sorted(times[v])[len(times[v]) // 2]
-            row[f"tn{v}"] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}
+        for tb in [int(x) for x in args.tn_blocks.split(",")]:
+            splits = max(1, min((M + 31) // 32, -(-tb // tiles)))
+            times = {v: [] for v in tn_variants}
+            for _ in range(args.rounds):
+                for v in tn_variants:
+                    lib.es_set_tn_variant(v)
+                    call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias), s)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(args.iters):
+                        call("es_gemm_tn", ptr(A), N1, ptr(A), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias),
+                             s)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times[v].append(e0.elapsed_time(e1) / args.iters)
+            lib.es_set_tn_variant(-1)
+            for v in tn_variants:
+                t = sorted(times[v])[len(times[v]) // 2]
+                row[f"tn{v}_b{tb}"] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}
         results[name] = row
         print(name, json.dumps(row), flush=True)
     out_dir = os.path.join(ROOT, "gpurun_out")
