@@ -8,6 +8,13 @@
 // Layout: qkv bf16 [tokens, 3*D] with per-token column order [3][H][64] (the reference reshape);
 // o / dout bf16 [tokens, D] with column h*64+d; lse fp32 [image][head][token].
 //
+// Head tiles are padded to NT16*16 rows (208 for T = 197: 52 KiB for two tiles, so three
+// workgroups share a CU) and staged by LDS-DMA (global_load_lds_dwordx4, 8 rows per
+// wave-instruction); pad rows re-read token T-1, so they hold finite values whose probabilities
+// are exactly zero.  Key (or query) chunks are 32 wide for the P.V-type products; an odd last
+// 16-row tile uses the K=16 MFMA (v_mfma_f32_16x16x16_bf16), whose operand maps are the first
+// half of the K=32 ones.
+//
 // MFMA orientation (v_mfma_f32_16x16x32_bf16, maps in common.h):
 //   fwd / dQ : S^T = K . Q^T  -> lane owns one query, keys in registers ("query on the lane"),
 //              so row max / sum are register reductions + 2 shuffles, and P^T is directly the
@@ -32,13 +39,15 @@ struct AttnArgs {
 
 __device__ __forceinline__ int aswz(int r, int c) { return c ^ (((r >> 1) & 3) << 1); }
 
-// [TP][64] bf16 tile of rows [0, T) of `src` (row stride ld), zero rows >= T.
-__device__ __forceinline__ void load_head_tile(char* lds, const bf16* src, int ld, int T, int TP) {
-  for (int id = threadIdx.x; id < TP * 8; id += blockDim.x) {
-    const int r = id >> 3, c = id & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r < T) v = *(const uint4*)(src + (size_t)r * ld + c * 8);
-    *(uint4*)(lds + r * 128 + aswz(r, c) * 16) = v;
+// [TP][64] bf16 image of rows [0, TP) of `src` (row stride ld) by LDS-DMA: wave-instruction i moves
+// rows 8i..8i+7 (lane -> row 8i + lane/8, physical chunk lane%8 holding logical chunk
+// aswz(row, lane%8)); rows >= T re-read row T-1.  Caller waits (vmcnt) and barriers.
+__device__ __forceinline__ void stage_head(char* lds, const bf16* src, int ld, int T, int TP) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = w; i < TP / 8; i += 4) {
+    const int row = i * 8 + (lane >> 3);
+    const int sr = row < T ? row : T - 1;
+    glds16(src + (size_t)sr * ld + aswz(row, lane & 7) * 8, lds + i * 1024);
   }
 }
 
@@ -56,22 +65,37 @@ __device__ __forceinline__ bf16x8 lds_trT(const char* lds, int base, int d0, int
               lds_tr4(lds + r2 * 128 + aswz(r2, c) * 16 + off));
 }
 
+// first half of lds_trT: rows base+4g..+3 of column d0 + t (A operand of the K=16 MFMA)
+__device__ __forceinline__ bf16x4 lds_trT4(const char* lds, int base, int d0, int g, int t) {
+  const int q = t >> 2, p4 = t & 3;
+  const int c = (d0 >> 3) + (p4 >> 1), off = (p4 & 1) * 8;
+  const int r1 = base + 4 * g + q;
+  return lds_tr4(lds + r1 * 128 + aswz(r1, c) * 16 + off);
+}
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16k16(bf16x4 a, bf16x4 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a), __builtin_bit_cast(s16x4, b), c, 0,
+                                                   0, 0);
+}
+
 __device__ __forceinline__ bf16x8 ld_row8(const bf16* p, bool valid) {
   if (!valid) return bf16x8{};
   return *(const bf16x8*)p;
 }
 
-template <int NKC>  // 32-key chunks: T <= 32*NKC
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
+template <int NT16, int OCC>  // 16-key tiles: T <= 16*NT16; OCC workgroups per CU (register budget)
+__global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TP = NKC * 32;
+  constexpr int TP = NT16 * 16;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
   const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
   char* Ks = smem;
   char* Vs = smem + TP * 128;
-  load_head_tile(Ks, base + D + h * 64, a.ldqkv, T, TP);
-  load_head_tile(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
+  stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
@@ -85,10 +109,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 
     // scores in log2 units (scale * log2 e folded in): p = exp2(s - max) is one v_exp_f32; keys
     // are masked only in the partial last tile (the branch is uniform per tile).
-    f32x4 s[2 * NKC];
+    f32x4 s[NT16];
     float mx = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 2 * NKC; ++t) {
+    for (int t = 0; t < NT16; ++t) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
       acc = mfma16(lds_row8(Ks, t * 16 + r, g), qf0, acc);
       acc = mfma16(lds_row8(Ks, t * 16 + r, 4 + g), qf1, acc);
@@ -105,7 +129,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float l = 0.f;
 #pragma unroll
-    for (int t = 0; t < 2 * NKC; ++t)
+    for (int t = 0; t < NT16; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float pv = __builtin_amdgcn_exp2f(s[t][i] - mx);
@@ -119,7 +143,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int sc = 0; sc < NKC; ++sc) {
+    for (int sc = 0; sc < NT16 / 2; ++sc) {
       bf16x8 pf;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -128,6 +152,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(lds_trT(Vs, sc * 32, dt * 16, g, r), pf, o[dt]);
+    }
+    if constexpr (NT16 & 1) {
+      const bf16x4 pf = {(bf16)s[NT16 - 1][0], (bf16)s[NT16 - 1][1], (bf16)s[NT16 - 1][2], (bf16)s[NT16 - 1][3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16k16(lds_trT4(Vs, (NT16 - 1) * 16, dt * 16, g, r), pf, o[dt]);
     }
     if (qv) {
       const float inv = 1.0f / l;
@@ -143,21 +172,23 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // dQ: query on the lane; delta = rowsum(dO * O) computed in-register for the wave's queries.
-template <int NKC>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
+template <int NT16>
+__global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TP = NKC * 32;
+  constexpr int TP = NT16 * 16;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
   const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
   char* Ks = smem;
   char* Vs = smem + TP * 128;
-  load_head_tile(Ks, base + D + h * 64, a.ldqkv, T, TP);
-  load_head_tile(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
+  stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   const int nqt = (T + 15) >> 4;
+  const float sl = a.scale * 1.44269504088896341f;
   for (int qb = w; qb < nqt; qb += 4) {
     const int q = qb * 16 + r;
     const bool qv = q < T;
@@ -175,35 +206,48 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
     delta += __shfl_xor(delta, 32, 64);
     if (qv && g == 0) a.delta[(size_t)bh * T + q] = delta;  // consumed by attn_bwd_dkv_kernel
     const float lq = qv ? a.lse[(size_t)bh * T + q] * 1.44269504088896341f : 0.f;  // log2 units
-    const float sl = a.scale * 1.44269504088896341f;
+
+    // dS^T tile t (keys 16t + 4g + i on this lane's query), in fp32
+    auto ds_tile = [&](int t) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      sv = mfma16(lds_row8(Ks, t * 16 + r, g), qf0, sv);
+      sv = mfma16(lds_row8(Ks, t * 16 + r, 4 + g), qf1, sv);
+      dp = mfma16(lds_row8(Vs, t * 16 + r, g), df0, dp);
+      dp = mfma16(lds_row8(Vs, t * 16 + r, 4 + g), df1, dp);
+      f32x4 pv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sv[i] * sl - lq);
+      if (t * 16 + 16 > T) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (t * 16 + 4 * g + i >= T) pv[i] = 0.f;
+      }
+      f32x4 ds;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ds[i] = pv[i] * (dp[i] - delta);
+      return ds;
+    };
 
     f32x4 dq[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-    for (int sc = 0; sc < NKC; ++sc) {
+    for (int sc = 0; sc < NT16 / 2; ++sc) {
+      const f32x4 d0 = ds_tile(2 * sc), d1 = ds_tile(2 * sc + 1);
       bf16x8 dsf;
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int t = 2 * sc + hf;
-        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-        sv = mfma16(lds_row8(Ks, t * 16 + r, g), qf0, sv);
-        sv = mfma16(lds_row8(Ks, t * 16 + r, 4 + g), qf1, sv);
-        dp = mfma16(lds_row8(Vs, t * 16 + r, g), df0, dp);
-        dp = mfma16(lds_row8(Vs, t * 16 + r, 4 + g), df1, dp);
-        f32x4 pv;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sv[i] * sl - lq);
-        if (t * 16 + 16 > T) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (t * 16 + 4 * g + i >= T) pv[i] = 0.f;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) dsf[4 * hf + i] = (bf16)(pv[i] * (dp[i] - delta));
+      for (int i = 0; i < 4; ++i) {
+        dsf[i] = (bf16)d0[i];
+        dsf[4 + i] = (bf16)d1[i];
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(lds_trT(Ks, sc * 32, dt * 16, g, r), dsf, dq[dt]);
+    }
+    if constexpr (NT16 & 1) {
+      const f32x4 d0 = ds_tile(NT16 - 1);
+      const bf16x4 dsf = {(bf16)d0[0], (bf16)d0[1], (bf16)d0[2], (bf16)d0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16k16(lds_trT4(Ks, (NT16 - 1) * 16, dt * 16, g, r), dsf, dq[dt]);
     }
     if (qv) {
       bf16* drow = a.dqkv + tok * a.lddqkv + h * 64;
@@ -218,10 +262,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // dK, dV: key on the lane; Q and dO of the whole head in LDS with lse / delta per query.
-template <int NKC>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
+template <int NT16>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TP = NKC * 32;
+  constexpr int TP = NT16 * 16;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
   const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
@@ -229,15 +273,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   char* Ds = smem + TP * 128;
   float* lse_s = (float*)(smem + 2 * TP * 128);
   float* del_s = lse_s + TP;
-  load_head_tile(Qs, base + h * 64, a.ldqkv, T, TP);
-  load_head_tile(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
+  stage_head(Qs, base + h * 64, a.ldqkv, T, TP);
+  stage_head(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   // lse in log2 units; padded queries get +inf so their probabilities are exactly 0
   for (int t = threadIdx.x; t < TP; t += blockDim.x)
     lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] * 1.44269504088896341f : INFINITY;
-  const float sl = a.scale * 1.44269504088896341f;
   for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  const float sl = a.scale * 1.44269504088896341f;
 
   const int nkt = (T + 15) >> 4;
   for (int kb = w; kb < nkt; kb += 4) {
@@ -247,33 +292,52 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
     const bf16* vrow = krow + D;
     const bf16x8 kf0 = ld_row8(krow + 8 * g, kv), kf1 = ld_row8(krow + 32 + 8 * g, kv);
     const bf16x8 vf0 = ld_row8(vrow + 8 * g, kv), vf1 = ld_row8(vrow + 32 + 8 * g, kv);
+    // P and dS for query tile u (queries 16u + 4g + i, this lane's key)
+    auto p_ds = [&](int u, f32x4& p, f32x4& ds) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      sv = mfma16(lds_row8(Qs, u * 16 + r, g), kf0, sv);
+      sv = mfma16(lds_row8(Qs, u * 16 + r, 4 + g), kf1, sv);
+      dp = mfma16(lds_row8(Ds, u * 16 + r, g), vf0, dp);
+      dp = mfma16(lds_row8(Ds, u * 16 + r, 4 + g), vf1, dp);
+      const f32x4 l4 = *(const f32x4*)(lse_s + u * 16 + 4 * g);
+      const f32x4 d4 = *(const f32x4*)(del_s + u * 16 + 4 * g);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p[i] = __builtin_amdgcn_exp2f(sv[i] * sl - l4[i]);
+        ds[i] = p[i] * (dp[i] - d4[i]);
+      }
+    };
     f32x4 dk[4], dv[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-    for (int sc = 0; sc < NKC; ++sc) {
+    for (int sc = 0; sc < NT16 / 2; ++sc) {
+      f32x4 p0, p1, s0, s1;
+      p_ds(2 * sc, p0, s0);
+      p_ds(2 * sc + 1, p1, s1);
       bf16x8 pf, dsf;
 #pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int u = 2 * sc + hf;
-        f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
-        sv = mfma16(lds_row8(Qs, u * 16 + r, g), kf0, sv);
-        sv = mfma16(lds_row8(Qs, u * 16 + r, 4 + g), kf1, sv);
-        dp = mfma16(lds_row8(Ds, u * 16 + r, g), vf0, dp);
-        dp = mfma16(lds_row8(Ds, u * 16 + r, 4 + g), vf1, dp);
-        const f32x4 l4 = *(const f32x4*)(lse_s + u * 16 + 4 * g);
-        const f32x4 d4 = *(const f32x4*)(del_s + u * 16 + 4 * g);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float pv = __builtin_amdgcn_exp2f(sv[i] * sl - l4[i]);
-          pf[4 * hf + i] = (bf16)pv;
-          dsf[4 * hf + i] = (bf16)(pv * (dp[i] - d4[i]));
-        }
+      for (int i = 0; i < 4; ++i) {
+        pf[i] = (bf16)p0[i];
+        pf[4 + i] = (bf16)p1[i];
+        dsf[i] = (bf16)s0[i];
+        dsf[4 + i] = (bf16)s1[i];
       }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         dv[dt] = mfma16(lds_trT(Ds, sc * 32, dt * 16, g, r), pf, dv[dt]);
         dk[dt] = mfma16(lds_trT(Qs, sc * 32, dt * 16, g, r), dsf, dk[dt]);
+      }
+    }
+    if constexpr (NT16 & 1) {
+      f32x4 p0, s0;
+      p_ds(NT16 - 1, p0, s0);
+      const bf16x4 pf = {(bf16)p0[0], (bf16)p0[1], (bf16)p0[2], (bf16)p0[3]};
+      const bf16x4 dsf = {(bf16)s0[0], (bf16)s0[1], (bf16)s0[2], (bf16)s0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16k16(lds_trT4(Ds, (NT16 - 1) * 16, dt * 16, g, r), pf, dv[dt]);
+        dk[dt] = mfma16k16(lds_trT4(Qs, (NT16 - 1) * 16, dt * 16, g, r), dsf, dk[dt]);
       }
     }
     if (kv) {
@@ -290,22 +354,56 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
-#define ATTN_DISPATCH(KERNEL, NKC_, GRID, LDS, STREAM, ARGS)                         \
-  switch (NKC_) {                                                                    \
-    case 1: allow_lds(KERNEL<1>, LDS); hipLaunchKernelGGL(KERNEL<1>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 2: allow_lds(KERNEL<2>, LDS); hipLaunchKernelGGL(KERNEL<2>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 3: allow_lds(KERNEL<3>, LDS); hipLaunchKernelGGL(KERNEL<3>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 4: allow_lds(KERNEL<4>, LDS); hipLaunchKernelGGL(KERNEL<4>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 5: allow_lds(KERNEL<5>, LDS); hipLaunchKernelGGL(KERNEL<5>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 6: allow_lds(KERNEL<6>, LDS); hipLaunchKernelGGL(KERNEL<6>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 7: allow_lds(KERNEL<7>, LDS); hipLaunchKernelGGL(KERNEL<7>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    case 8: allow_lds(KERNEL<8>, LDS); hipLaunchKernelGGL(KERNEL<8>, GRID, 256, LDS, STREAM, ARGS); break;      \
-    default: return ES_BAD_SHAPE;                                                    \
+#define ATTN_CASE(KERNEL, N_, GRID, LDS, STREAM, ARGS) \
+  case N_: allow_lds(KERNEL<N_>, LDS); hipLaunchKernelGGL(KERNEL<N_>, GRID, 256, LDS, STREAM, ARGS); break;
+
+#define ATTN_DISPATCH(KERNEL, NT16_, GRID, LDS, STREAM, ARGS)                                               \
+  switch (NT16_) {                                                                                        \
+    ATTN_CASE(KERNEL, 1, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 2, GRID, LDS, STREAM, ARGS)            \
+    ATTN_CASE(KERNEL, 3, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 4, GRID, LDS, STREAM, ARGS)            \
+    ATTN_CASE(KERNEL, 5, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 6, GRID, LDS, STREAM, ARGS)            \
+    ATTN_CASE(KERNEL, 7, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 8, GRID, LDS, STREAM, ARGS)            \
+    ATTN_CASE(KERNEL, 9, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 10, GRID, LDS, STREAM, ARGS)           \
+    ATTN_CASE(KERNEL, 11, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 12, GRID, LDS, STREAM, ARGS)          \
+    ATTN_CASE(KERNEL, 13, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 14, GRID, LDS, STREAM, ARGS)          \
+    ATTN_CASE(KERNEL, 15, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 16, GRID, LDS, STREAM, ARGS)          \
+    default: return ES_BAD_SHAPE;                                                                         \
   }
+
+#define FWD_CASE(N_, OCC_, GRID, LDS, STREAM, ARGS)                                                  \
+  case N_:                                                                                          \
+    allow_lds(attn_fwd_kernel<N_, OCC_>, LDS);                                                      \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_fwd_kernel<N_, OCC_>), GRID, 256, LDS, STREAM, ARGS);   \
+    break;
+#define FWD_DISPATCH(NT16_, OCC_, GRID, LDS, STREAM, ARGS)                                            \
+  switch (NT16_) {                                                                                  \
+    FWD_CASE(1, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(2, OCC_, GRID, LDS, STREAM, ARGS)            \
+    FWD_CASE(3, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(4, OCC_, GRID, LDS, STREAM, ARGS)            \
+    FWD_CASE(5, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(6, OCC_, GRID, LDS, STREAM, ARGS)            \
+    FWD_CASE(7, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(8, OCC_, GRID, LDS, STREAM, ARGS)            \
+    FWD_CASE(9, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(10, OCC_, GRID, LDS, STREAM, ARGS)           \
+    FWD_CASE(11, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(12, OCC_, GRID, LDS, STREAM, ARGS)          \
+    FWD_CASE(13, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(14, OCC_, GRID, LDS, STREAM, ARGS)          \
+    FWD_CASE(15, OCC_, GRID, LDS, STREAM, ARGS) FWD_CASE(16, OCC_, GRID, LDS, STREAM, ARGS)          \
+    default: return ES_BAD_SHAPE;                                                                   \
+  }
+
+// forward occupancy target (workgroups per CU the register budget is sized for): 2 = no cap
+// (measured faster: 108 vs 150 us at the F1 shape, scripts/attn_bench.py),
+// 3 = 168 VGPRs (three 52-KiB heads per CU, small spill)
+int g_attn_fwd_occ = 2;
 
 }  // namespace
 
 extern "C" {
+
+// tuning knob: forward attention workgroups per CU the register budget targets (2 or 3)
+int es_set_attn_variant(int occ) {
+  const int old = g_attn_fwd_occ;
+  g_attn_fwd_occ = occ;
+  return old;
+}
+
 
 // qkv [nimg*T, ldqkv] -> o [nimg*T, ldo], lse [nimg*H*T]; head dim 64, T <= 256.
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
@@ -314,9 +412,13 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, lse, nullptr, nullptr, nullptr, ldqkv, ldo, 0, 0, T, H, scale};
-  const int nkc = (T + 31) / 32;
-  const size_t lds = 2 * (size_t)nkc * 32 * 128;
-  ATTN_DISPATCH(attn_fwd_kernel, nkc, nimg * H, lds, stream, a);
+  const int nt16 = (T + 15) / 16;
+  const size_t lds = 2 * (size_t)nt16 * 16 * 128;
+  if (g_attn_fwd_occ == 2) {
+    FWD_DISPATCH(nt16, 2, nimg * H, lds, stream, a);
+  } else {
+    FWD_DISPATCH(nt16, 3, nimg * H, lds, stream, a);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -330,11 +432,11 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   if (!qkv || !o || !lse || !delta || !dout || !dqkv) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, delta, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
              lddqkv, T, H, scale};
-  const int nkc = (T + 31) / 32;
-  const size_t lds_dq = 2 * (size_t)nkc * 32 * 128;
-  const size_t lds_dkv = lds_dq + 2 * (size_t)nkc * 32 * 4;
-  ATTN_DISPATCH(attn_bwd_dq_kernel, nkc, nimg * H, lds_dq, stream, a);
-  ATTN_DISPATCH(attn_bwd_dkv_kernel, nkc, nimg * H, lds_dkv, stream, a);
+  const int nt16 = (T + 15) / 16;
+  const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
+  const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
+  ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
+  ATTN_DISPATCH(attn_bwd_dkv_kernel, nt16, nimg * H, lds_dkv, stream, a);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -203,6 +203,13 @@ __device__ __forceinline__ void staged_epilogue_g(const NTArgs& p, char* wlds, c
   }
 }
 
+// chunk swizzle for a BKT-deep K step: 128-B rows (BKT 64) or 64-B rows (BKT 32)
+template <int BKT>
+__device__ __forceinline__ int swzk(int r, int c) {
+  if constexpr (BKT == 64) return c ^ ((r >> 1) & 7);
+  else return swz64(r, c);
+}
+
 // vmcnt immediates must be literals: counted waits for the stage pipelines below.
 __device__ __forceinline__ void wait_vmcnt(int n) {
   switch (n) {
@@ -298,23 +305,27 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
 
 
 // Big-tile family: (WM*MF*16) x ((8/WM)*NF*16) output tile, 8 waves (WM along M), one
-// workgroup per CU.  K step 32 (64-B LDS rows, swz64), NST-stage glds ring: stage k+NST-1 is
-// issued right after the barrier that publishes stage k, so NST-1 stages stay in flight
-// ACROSS the barriers (counted vmcnt, raw s_barrier -- cdna_hip_programming.md §5 T3/T4).
-// 128-row wave tiles (WM=2) read 12 KiB of LDS per 32 MFMAs instead of 16 KiB for 64x64 tiles.
-// The B tile may have a half glds instruction per wave (BN = 192: 24 rows per wave); the
-// instruction count per wave stays uniform so the vmcnt arithmetic holds for every wave.
-template <int EPI, int WM, int MF, int NF, int NST>
+// workgroup per CU.  K step BKT (32: 64-B LDS rows, swz64; 64: 128-B rows, swz128), NST-stage
+// glds ring: stage k+NST-1 is issued right after the barrier that publishes stage k, so NST-1
+// stages stay in flight ACROSS the barriers (counted vmcnt, raw s_barrier --
+// cdna_hip_programming.md §5 T3/T4).  128-row wave tiles (WM=2) read 12 KiB of LDS per 32 MFMAs
+// instead of 16 KiB for 64x64 tiles.  With BKT = 32 the B tile may need a half glds instruction
+// per wave (BN = 192: 24 rows per wave); the instruction count per wave stays uniform so the
+// vmcnt arithmetic holds for every wave.
+template <int EPI, int WM, int MF, int NF, int NST, int BKT>
 __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int WN = 8 / WM;
   constexpr int TBM = WM * MF * 16, TBN = WN * NF * 16;
-  constexpr int IA = TBM / 128;                 // full 1-KiB glds per wave for A (16 rows each)
-  constexpr int IBF = TBN / 128;                // full glds per wave for B
-  constexpr int IBH = (TBN % 128) ? 1 : 0;      // plus one half (8 rows, lanes 0..31)
-  static_assert(TBM % 128 == 0 && (TBN % 128 == 0 || TBN % 128 == 64), "tile");
+  constexpr int ROWB = BKT * 2, RPI = 1024 / ROWB, CPR = ROWB / 16;  // row bytes, rows / chunks per glds
+  constexpr int RPW = 8 * RPI;                   // rows per round of 8 waves
+  constexpr int IA = TBM / RPW;                  // full glds per wave for A
+  constexpr int IBF = TBN / RPW;                 // full glds per wave for B
+  constexpr int IBH = (TBN % RPW) ? 1 : 0;       // plus one half (RPI/2 rows, lanes 0..31)
+  static_assert(TBM % RPW == 0 && (TBN % RPW == 0 || TBN % RPW == RPW / 2), "tile");
+  static_assert(BKT == 32 || BKT == 64, "K step");
   constexpr int PER = IA + IBF + IBH;
-  constexpr int TA = TBM * 64, STAGE = (TBM + TBN) * 64;
+  constexpr int TA = TBM * ROWB, STAGE = (TBM + TBN) * ROWB;
   const int ntn = p.N / TBN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (wg / ntn) * TBM, n0 = (wg % ntn) * TBN;
@@ -327,20 +338,20 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
   int da[IA], db[IBF + IBH];
 #pragma unroll
   for (int j = 0; j < IA; ++j) {
-    const int row = (j * 8 + w) * 16 + (lane >> 2);
-    ga[j] = p.A + (size_t)(m0 + row) * p.lda + swz64(row, lane & 3) * 8;
+    const int row = (j * 8 + w) * RPI + lane / CPR;
+    ga[j] = p.A + (size_t)(m0 + row) * p.lda + swzk<BKT>(row, lane % CPR) * 8;
     da[j] = (j * 8 + w) * 1024;
   }
 #pragma unroll
   for (int j = 0; j < IBF; ++j) {
-    const int row = (j * 8 + w) * 16 + (lane >> 2);
-    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + swz64(row, lane & 3) * 8;
+    const int row = (j * 8 + w) * RPI + lane / CPR;
+    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + swzk<BKT>(row, lane % CPR) * 8;
     db[j] = TA + (j * 8 + w) * 1024;
   }
   if constexpr (IBH) {
-    const int row = IBF * 128 + w * 8 + ((lane & 31) >> 2);
-    gb[IBF] = p.B + (size_t)(n0 + row) * p.ldb + swz64(row, lane & 3) * 8;
-    db[IBF] = TA + IBF * 128 * 64 + w * 512;
+    const int row = IBF * RPW + w * (RPI / 2) + (lane & 31) / CPR;
+    gb[IBF] = p.B + (size_t)(n0 + row) * p.ldb + swzk<BKT>(row, lane % CPR) * 8;
+    db[IBF] = TA + IBF * RPW * ROWB + w * 512;
   }
 #define BIG_ISSUE(BUF, K0)                                                        \
   {                                                                               \
@@ -358,10 +369,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = p.K / 32;
+  const int nk = p.K / BKT;
 #pragma unroll
   for (int st = 0; st < NST - 1; ++st)
-    if (st < nk) BIG_ISSUE(st, st * 32)
+    if (st < nk) BIG_ISSUE(st, st * BKT)
   int buf = 0;
   for (int kt = 0; kt < nk; ++kt) {
     wait_vmcnt(min(NST - 2, nk - 1 - kt) * PER);
@@ -369,32 +380,35 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
     if (kt + NST - 1 < nk) {
       int nb = buf + NST - 1;
       nb = nb >= NST ? nb - NST : nb;
-      BIG_ISSUE(nb, (kt + NST - 1) * 32)
+      BIG_ISSUE(nb, (kt + NST - 1) * BKT)
     }
     const char* As = smem + buf * STAGE;
     const char* Bs = As + TA;
-    bf16x8 af[MF], bfr[NF];
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int rb = wn * NF * 16 + j * 16 + r;
-      bfr[j] = *(const bf16x8*)(Bs + rb * 64 + swz64(rb, g) * 16);
+    for (int kk = 0; kk < BKT / 32; ++kk) {
+      bf16x8 af[MF], bfr[NF];
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        const int rb = wn * NF * 16 + j * 16 + r;
+        bfr[j] = *(const bf16x8*)(Bs + rb * ROWB + swzk<BKT>(rb, kk * 4 + g) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < MF; ++i) {
+        const int ra = wm * MF * 16 + i * 16 + r;
+        af[i] = *(const bf16x8*)(As + ra * ROWB + swzk<BKT>(ra, kk * 4 + g) * 16);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
     }
-#pragma unroll
-    for (int i = 0; i < MF; ++i) {
-      const int ra = wm * MF * 16 + i * 16 + r;
-      af[i] = *(const bf16x8*)(As + ra * 64 + swz64(ra, g) * 16);
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int i = 0; i < MF; ++i)
-#pragma unroll
-      for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-    __builtin_amdgcn_s_setprio(0);
     buf = buf + 1 == NST ? 0 : buf + 1;
   }
 #undef BIG_ISSUE
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, MF, NF>(p, smem + w * 16 * (NF * 64 + 16), acc, m0 + wm * MF * 16, n0 + wn * NF * 16,
+  staged_epilogue_g<EPI, MF, NF>(p, smem + w * epi_wave_bytes<NF>(), acc, m0 + wm * MF * 16, n0 + wn * NF * 16,
                                  lane);
 }
 
@@ -407,11 +421,6 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
 //   BKT=32:  64-B LDS rows, chunk c of row r at c ^ ((-(r>>2))&3)   (both conflict-free for the
 //            16-row x 16-B fragment reads under the ds_read_b128 lane groups of
 //            MI355X_MICROARCH.md §LDS; the plain c ^ ((r>>2)&3) is 2-way conflicted there)
-template <int BKT>
-__device__ __forceinline__ int swzk(int r, int c) {
-  if constexpr (BKT == 64) return c ^ ((r >> 1) & 7);
-  else return swz64(r, c);
-}
 
 template <int EPI, int BKT, int NST>
 __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
@@ -735,30 +744,31 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
 #undef NT_EPIS
 #undef NT_LAUNCH
 
-#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_)                                                   \
-  {                                                                                          \
-    const size_t lds = (size_t)NST_ * (WM_ * MF_ * 16 + (8 / WM_) * NF_ * 16) * 64;          \
-    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_>, lds);                              \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_>), dim3(grid), dim3(512), lds, \
-                       stream, a);                                                           \
-    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;                           \
+#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_, BKT_)                                                   \
+  {                                                                                                 \
+    const size_t lds = (size_t)NST_ * (WM_ * MF_ * 16 + (8 / WM_) * NF_ * 16) * BKT_ * 2;            \
+    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_>, lds);                               \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_>), dim3(grid), dim3(512), \
+                       lds, stream, a);                                                             \
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;                                  \
   }
-#define BIG_EPIS(WM_, MF_, NF_, NST_)                                 \
-  switch (epi) {                                                      \
-    case EPI_BF16: BIG_LAUNCH(EPI_BF16, WM_, MF_, NF_, NST_)          \
-    case EPI_GELU: BIG_LAUNCH(EPI_GELU, WM_, MF_, NF_, NST_)          \
-    case EPI_F32_RESID: BIG_LAUNCH(EPI_F32_RESID, WM_, MF_, NF_, NST_) \
-    case EPI_DGELU: BIG_LAUNCH(EPI_DGELU, WM_, MF_, NF_, NST_)        \
-    case EPI_F32: BIG_LAUNCH(EPI_F32, WM_, MF_, NF_, NST_)            \
-    case EPI_PATCH: BIG_LAUNCH(EPI_PATCH, WM_, MF_, NF_, NST_)        \
-    case EPI_GELU_ACT: BIG_LAUNCH(EPI_GELU_ACT, WM_, MF_, NF_, NST_)  \
-    default: return ES_BAD_ARG;                                       \
+#define BIG_EPIS(WM_, MF_, NF_, NST_, BKT_)                                         \
+  switch (epi) {                                                                    \
+    case EPI_BF16: BIG_LAUNCH(EPI_BF16, WM_, MF_, NF_, NST_, BKT_)                  \
+    case EPI_GELU: BIG_LAUNCH(EPI_GELU, WM_, MF_, NF_, NST_, BKT_)                  \
+    case EPI_F32_RESID: BIG_LAUNCH(EPI_F32_RESID, WM_, MF_, NF_, NST_, BKT_)        \
+    case EPI_DGELU: BIG_LAUNCH(EPI_DGELU, WM_, MF_, NF_, NST_, BKT_)                \
+    case EPI_F32: BIG_LAUNCH(EPI_F32, WM_, MF_, NF_, NST_, BKT_)                    \
+    case EPI_PATCH: BIG_LAUNCH(EPI_PATCH, WM_, MF_, NF_, NST_, BKT_)                \
+    case EPI_GELU_ACT: BIG_LAUNCH(EPI_GELU_ACT, WM_, MF_, NF_, NST_, BKT_)          \
+    default: return ES_BAD_ARG;                                                     \
   }
 int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   switch (cfg) {
-    case 6: BIG_EPIS(2, 8, 4, 4)   // 256x256
-    case 7: BIG_EPIS(2, 8, 3, 4)   // 256x192
-    default: BIG_EPIS(4, 4, 4, 4)  // 256x128
+    case 6: BIG_EPIS(2, 8, 4, 2, 64)   // 256x256, BK64, 2 stages (128 KiB)
+    case 7: BIG_EPIS(2, 8, 3, 2, 64)   // 256x192, BK64, 2 stages (112 KiB)
+    case 9: BIG_EPIS(2, 8, 3, 4, 32)   // 256x192, BK32, 4 stages
+    default: BIG_EPIS(2, 8, 4, 4, 32)  // 8: 256x256, BK32, 4 stages
   }
 }
 #undef BIG_EPIS
@@ -806,8 +816,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
-  if (variant >= 6 && variant <= 8) {
-    const int tbn = variant == 6 ? 256 : variant == 7 ? 192 : 128;
+  if (variant >= 6 && variant <= 9) {
+    const int tbn = (variant == 6 || variant == 8) ? 256 : 192;
     if (N % tbn) return ES_BAD_SHAPE;
     return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
   }
@@ -819,8 +829,9 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 
 // Tuning knob: which NT kernel family es_gemm_nt launches (-1 = per-shape default, 0 = 128x128
 // BK64 2-stage, 1 = 256x128 BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage,
-// 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage, 6 = 256x256 / 7 = 256x192 / 8 = 256x128 BK32
-// 4-stage, 8 waves, one workgroup per CU; 6/7 need N % 256 / N % 192 == 0).
+// 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage; 8 waves, one workgroup per CU, 128x64 or
+// 128x48 per wave: 6 = 256x256 BK64 2-stage, 7 = 256x192 BK64 2-stage, 8 = 256x256 BK32
+// 4-stage, 9 = 256x192 BK32 4-stage; 6/8 need N % 256 == 0, 7/9 N % 192 == 0).
 // Returns the previous value.
 int es_set_gemm_variant(int v) {
   const int old = g_gemm_variant;

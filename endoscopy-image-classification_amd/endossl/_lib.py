@@ -22,6 +22,7 @@ SIGNATURES = {
     "es_gemm_tn_workspace": (Z, [I, I, I]),
     "es_gemm_tn": (I, [V, I, V, I, I, I, I, I, V, V, I, V, V]),
     "es_set_tn_variant": (I, [I]),
+    "es_set_attn_variant": (I, [I]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),
     "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
     "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),

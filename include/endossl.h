@@ -57,6 +57,8 @@ int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks,
 /* out[n] (+)= sum_g P[g][n]  (per-workgroup partials -> parameter gradient) */
 int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream);
 
+/* tuning knob: forward attention occupancy target (2 or 3 workgroups per CU); returns previous */
+int es_set_attn_variant(int occ);
 /* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 256 --------------- */
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream);

@@ -40,8 +40,8 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8]
-_TILE_N = {6: 256, 7: 192}  # big-tile variants that need N to be a multiple of their tile width
+GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9]
+_TILE_N = {6: 256, 7: 192, 8: 256, 9: 192}  # big-tile variants: N must be a multiple of the tile width
 
 
 @pytest.fixture(params=GEMM_VARIANTS, ids=["auto"] + [f"v{v}" for v in GEMM_VARIANTS[1:]])
@@ -173,8 +173,15 @@ def _attn_ref(qkv, n, T, H):
     return o, lse
 
 
-@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 64, 1), (2, 250, 2)])
-def test_attention_fwd(n, T, H):
+@pytest.fixture(params=[2, 3], ids=["occ2", "occ3"])
+def attn_occ(request):
+    old = _lib.load().es_set_attn_variant(request.param)
+    yield request.param
+    _lib.load().es_set_attn_variant(old)
+
+
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 64, 1), (2, 250, 2), (3, 40, 2), (2, 1, 1)])
+def test_attention_fwd(n, T, H, attn_occ):
     torch.manual_seed(T)
     D = H * 64
     qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
@@ -187,7 +194,7 @@ def test_attention_fwd(n, T, H):
     assert torch.all(o[n * T:] == 0)
 
 
-@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 17, 2)])
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 17, 2), (3, 40, 2), (2, 250, 1), (2, 1, 1)])
 def test_attention_bwd(n, T, H):
     torch.manual_seed(100 + T)
     D = H * 64
@@ -207,7 +214,8 @@ def test_attention_bwd(n, T, H):
     got = dqkv[:n * T].float()
     for part in range(3):
         a, b = got[:, part * D:(part + 1) * D], ref[:, part * D:(part + 1) * D]
-        err = (a - b).abs().max().item() / b.abs().max().item()
+        # scale floor: with one token O = V, so dQ = dK = 0 exactly and only an absolute bound applies
+        err = (a - b).abs().max().item() / max(b.abs().max().item(), 1e-2)
         assert err < 3e-2, (part, err)
     assert torch.all(dqkv[n * T:] == 0)
 
