@@ -37,6 +37,13 @@ def _bf(t):
     return t.bfloat16().float()
 
 
+def vit_features(p, x, cfg, bf16=False):
+    """The ViT trunk up to the final LayerNorm, CLS token only: the 384-d `fts` of ModelwEmb
+    (code/models/custom_model.py:207-213 over a ViT backbone).  Rounding points as
+    in vit_forward."""
+    return _trunk(p, x, cfg, bf16)[:, 0]
+
+
 def vit_forward(p, x, cfg, bf16=False):
     """timm VisionTransformer.forward with conformer.Block blocks (code/models/conformer.py:27-72).
 
@@ -47,6 +54,11 @@ def vit_forward(p, x, cfg, bf16=False):
     biases and the CLS head stay fp32.  This is the numerical contract of the bf16 kernels; the
     difference between the two modes is the bf16 error envelope the parity tests report.
     """
+    t = _trunk(p, x, cfg, bf16)
+    return F.linear(t[:, 0], p["head.weight"], p["head.bias"])
+
+
+def _trunk(p, x, cfg, bf16):
     B, D, H = x.shape[0], cfg.dim, cfg.heads
     hd = D // H
     r = _bf if bf16 else (lambda t: t)
@@ -71,8 +83,7 @@ def vit_forward(p, x, cfg, bf16=False):
         h = r(F.layer_norm(t, (D,), p[b + "norm2.weight"], p[b + "norm2.bias"], cfg.eps))
         h = r(F.gelu(F.linear(h, r(p[b + "mlp.fc1.weight"]), p[b + "mlp.fc1.bias"])))
         t = t + F.linear(h, r(p[b + "mlp.fc2.weight"]), p[b + "mlp.fc2.bias"])
-    t = F.layer_norm(t, (D,), p["norm.weight"], p["norm.bias"], cfg.eps)
-    return F.linear(t[:, 0], p["head.weight"], p["head.bias"])
+    return F.layer_norm(t, (D,), p["norm.weight"], p["norm.bias"], cfg.eps)
 
 
 def poly_ce(logits, targets, weights=None, epsilon=2.0):
@@ -147,3 +158,121 @@ def random_params(cfg, seed=0, std=0.02, head_std=0.02):
             t = 0.02 * torch.randn(shape, generator=g)
         out[name] = t.float()
     return out
+
+
+# ------------------------------------------------------------------------------------ CoMatch
+DROP_P = 0.2  # build_head's Dropout(0.2) (code/models/custom_model.py:113)
+
+
+def emb_param_shapes(cfg, low_dim):
+    """ModelwEmb-style parameters over the ViT trunk: the trunk in timm order (no `head`), then
+    fc = build_head(D, C, is_complex=True) (code/models/custom_model.py:110-116: 0 Linear(D, D/4),
+    1 ReLU, 2 Dropout, 3 BatchNorm1d, 4 Linear(D/4, C)) and head_emb (:201-205: 0 Linear(D, 3L),
+    1 LeakyReLU(0.1), 2 Linear(3L, L), 3 Normalize)."""
+    D, C, L, Fh = cfg.dim, cfg.num_classes, low_dim, cfg.dim // 4
+    trunk = [s for s in param_shapes(cfg) if not s[0].startswith("head.")]
+    return trunk + [("fc.0.weight", (Fh, D)), ("fc.0.bias", (Fh,)), ("fc.3.weight", (Fh,)), ("fc.3.bias", (Fh,)),
+                    ("fc.4.weight", (C, Fh)), ("fc.4.bias", (C,)), ("head_emb.0.weight", (3 * L, D)),
+                    ("head_emb.0.bias", (3 * L,)), ("head_emb.2.weight", (L, 3 * L)), ("head_emb.2.bias", (L,))]
+
+
+BN_BUFFERS = ("fc.3.running_mean", "fc.3.running_var", "fc.3.num_batches_tracked")
+
+
+def emb_heads(p, bufs, fts, drop_keep, train=True):
+    """fc and head_emb of ModelwEmb on the features (code/models/custom_model.py:110-116,136-145,
+    201-213).  drop_keep: uint8/bool [N, D/4] keep-mask of the Dropout (replayed, since the reference
+    draws it from torch's CPU generator); BatchNorm1d in training mode updates `bufs` in place."""
+    h = F.relu(F.linear(fts, p["fc.0.weight"], p["fc.0.bias"]))
+    if train:
+        h = h * drop_keep.to(h.dtype) * (1.0 / (1.0 - DROP_P))
+    h = F.batch_norm(h, bufs["fc.3.running_mean"], bufs["fc.3.running_var"], p["fc.3.weight"], p["fc.3.bias"],
+                     training=train, momentum=0.1, eps=1e-5)
+    if train:
+        bufs["fc.3.num_batches_tracked"] += 1
+    logits = F.linear(h, p["fc.4.weight"], p["fc.4.bias"])
+    e = F.leaky_relu(F.linear(fts, p["head_emb.0.weight"], p["head_emb.0.bias"]), 0.1)
+    v = F.linear(e, p["head_emb.2.weight"], p["head_emb.2.bias"])
+    z = v.div(v.pow(2).sum(1, keepdim=True).pow(0.5))
+    return logits, z
+
+
+class CoMatchRef:
+    """One-step restatement of CoMatch.train_one's body (code/comatch.py:141-231): 4-way concat,
+    poly-CE, distribution alignment over <= 32 batch means, memory smoothing against the bank,
+    gated bank write, contrastive loss on the pseudo-label graph, focal unsupervised loss, Adam,
+    EMA over parameters and BatchNorm buffers."""
+
+    def __init__(self, params, bufs, cfg, low_dim, num_classes, queue_size, class_weights=None, thres=0.95,
+                 lambda_u=1.0, lambda_c=1.0, lr=1e-3, ema_decay=0.999, bf16=False):
+        self.cfg, self.bf16, self.L, self.C = cfg, bf16, low_dim, num_classes
+        self.names = [n for n, _ in emb_param_shapes(cfg, low_dim)]
+        self.p = {k: params[k].detach().clone().float().requires_grad_(True) for k in self.names}
+        self.bufs = {k: bufs[k].detach().clone() for k in BN_BUFFERS}
+        self.ema = {k: params[k].detach().clone().float() for k in self.names}
+        self.ema.update({k: bufs[k].detach().clone() for k in BN_BUFFERS})
+        self.cw, self.thres, self.lambda_u, self.lambda_c, self.decay = class_weights, thres, lambda_u, lambda_c, ema_decay
+        self.opt = torch.optim.Adam([self.p[k] for k in self.names], lr=lr, betas=(0.9, 0.999), eps=1e-8,
+                                    weight_decay=0)
+        # code/comatch.py:30-39,90-96
+        self.alpha, self.temperature, self.contrast_th, self.gamma = 0.9, 0.2, 0.8, 2
+        self.queue_size = queue_size
+        self.queue_feats = torch.zeros(queue_size, low_dim)
+        self.queue_probs = torch.zeros(queue_size, num_classes)
+        self.queue_ptr = 0
+        self.prob_list = []
+
+    def step(self, x, y, uw, us0, us1, drop_keep):
+        bt, btu = x.shape[0], uw.shape[0]
+        imgs = torch.cat([x, uw, us0, us1], dim=0)
+        fts = vit_features(self.p, imgs, self.cfg, bf16=self.bf16)
+        logits, feats = emb_heads(self.p, self.bufs, fts, drop_keep, train=True)
+        logits_x = logits[:bt]
+        logits_u_w, logits_u_s0, _ = torch.split(logits[bt:], btu)
+        feats_x = feats[:bt]
+        feats_u_w, feats_u_s0, feats_u_s1 = torch.split(feats[bt:], btu)
+        loss_x = poly_ce(logits_x, y, self.cw)
+        with torch.no_grad():
+            probs = torch.softmax(logits_u_w.detach(), dim=1)
+            self.prob_list.append(probs.mean(0))
+            if len(self.prob_list) > 32:
+                self.prob_list.pop(0)
+            prob_avg = torch.stack(self.prob_list, dim=0).mean(0)
+            probs = probs / prob_avg
+            probs = probs / probs.sum(dim=1, keepdim=True)
+            probs_orig = probs.clone()
+            fw = feats_u_w.detach()
+            A = torch.exp(torch.mm(fw, self.queue_feats.t()) / self.temperature)
+            A = A / A.sum(1, keepdim=True)
+            probs = self.alpha * probs + (1 - self.alpha) * torch.mm(A, self.queue_probs)
+            scores, lbs = torch.max(probs, dim=1)
+            mask = scores.ge(self.thres).float()
+            feats_w = torch.cat([fw, feats_x.detach()], dim=0)
+            onehot = torch.zeros(bt, self.C).scatter(1, y.view(-1, 1), 1)
+            probs_w = torch.cat([probs_orig, onehot], dim=0)
+            n = bt + btu
+            if n == self.queue_size:
+                self.queue_feats[self.queue_ptr:self.queue_ptr + n, :] = feats_w
+                self.queue_probs[self.queue_ptr:self.queue_ptr + n, :] = probs_w
+                self.queue_ptr = (self.queue_ptr + n) % self.queue_size
+        sim = torch.exp(torch.mm(feats_u_s0, feats_u_s1.t()) / self.temperature)
+        sim_probs = sim / sim.sum(1, keepdim=True)
+        Q = torch.mm(probs, probs.t())
+        Q.fill_diagonal_(1)
+        Q = Q * (Q >= self.contrast_th).float()
+        Q = Q / Q.sum(1, keepdim=True)
+        loss_contrast = -(torch.log(sim_probs + 1e-7) * Q).sum(1).mean()
+        logp = -torch.sum(F.log_softmax(logits_u_s0, dim=1) * probs, dim=1) * mask
+        pp = torch.exp(-logp)
+        loss_u = ((1 - pp) ** self.gamma * logp).mean()
+        loss = loss_x + self.lambda_u * loss_u + self.lambda_c * loss_contrast
+        self.opt.zero_grad()
+        loss.backward()
+        grads = {k: self.p[k].grad.detach().clone() for k in self.names}
+        self.opt.step()
+        state = {k: self.p[k].detach() for k in self.names}
+        state.update(self.bufs)
+        ema_update(self.ema, state, self.decay)
+        return {"lx": loss_x.item(), "lu": loss_u.item(), "lc": loss_contrast.item(), "loss": loss.item(),
+                "probs": probs, "probs_orig": probs_orig, "mask": mask, "pseudo_label": lbs,
+                "logits": logits.detach(), "fts": fts.detach(), "z": feats.detach(), "grads": grads}

@@ -22,8 +22,16 @@ Fixtures (all fp32, torch 2.10 CPU):
                      `models.conformer.Block` (code/models/conformer.py:55-72).  Records the
                      initial state, the inputs, every step's lx/lu/mask_mean/pseudo-labels, the
                      final model state and the final EMA state.
+  comatch_step_*.npz reference `CoMatch.train_one` (code/comatch.py:133-235), 2 steps, on the
+                     same tiny ViT trunk (features = final-LN CLS token) with
+                     ModelwEmb's heads built by the reference's own `build_head(is_complex=True)`
+                     and `Normalize` (code/models/custom_model.py:107-145,201-205).  Dropout masks
+                     are captured by a forward hook so the restatement can replay them.  Variants:
+                     "closed" (reference default queue_batch=5: the bank is never written) and
+                     "open" (queue_batch=1: queue_size == B + mu*B, the bank is written every step
+                     and the memory smoothing reads it in step 2).
 
-Usage (from the repo root):  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Usage (from the repo root):  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [all|comatch]
 """
 import os
 import sys
@@ -101,6 +109,17 @@ def _import_reference():
     from models import conformer as ref_conformer
     import utils as ref_utils
     return ref_loss, ref_ema, ref_fixmatch, ref_conformer, ref_utils
+
+
+def _import_comatch():
+    """comatch + models.custom_model (needs torchvision.transforms, off the arithmetic path)."""
+    tv = types.ModuleType("torchvision")
+    tv.transforms = types.ModuleType("torchvision.transforms")
+    sys.modules.setdefault("torchvision", tv)
+    sys.modules.setdefault("torchvision.transforms", tv.transforms)
+    import comatch as ref_comatch
+    from models import custom_model as ref_custom
+    return ref_comatch, ref_custom
 
 
 def _peaky_logits(g, n, c):
@@ -354,8 +373,140 @@ def gen_fixmatch_step(ref_fixmatch, ref_conformer, ref_utils, tag, thres, head_s
     print(f"fixmatch {tag}: lx={rec['lx']} lu={rec['lu']} mask={rec['mask_mean']} lr_updates={tr.lr_scheduler.updates}")
 
 
+# ---------------------------------------------------------------- CoMatch step golden
+def make_tiny_vit_emb(conformer, custom, img=64, patch=16, dim=128, depth=2, heads=2, num_classes=23, low_dim=16):
+    """ModelwEmb-style model (code/models/custom_model.py:147-213) over the tiny ViT trunk:
+    fts = final-LN CLS token; fc = build_head(dim, C, is_complex=True); head_emb = Linear(dim, 3L) ->
+    LeakyReLU(0.1) -> Linear(3L, L) -> Normalize(2).  forward -> (logits, fts, z)."""
+    trunk = make_tiny_vit(conformer, img, patch, dim, depth, heads, num_classes)
+
+    class TinyViTEmb(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.cls_token, self.pos_embed, self.patch_embed = trunk.cls_token, trunk.pos_embed, trunk.patch_embed
+            self.blocks, self.norm = trunk.blocks, trunk.norm
+            self.fc = custom.build_head(dim, num_classes, is_complex=True)
+            self.head_emb = nn.Sequential(nn.Linear(dim, low_dim * 3), nn.LeakyReLU(inplace=True, negative_slope=0.1),
+                                          nn.Linear(low_dim * 3, low_dim), custom.Normalize(2))
+
+        def forward(self, x):
+            x = self.patch_embed.proj(x).flatten(2).transpose(1, 2)
+            x = torch.cat((self.cls_token.expand(x.shape[0], -1, -1), x), dim=1) + self.pos_embed
+            fts = self.norm(self.blocks(x))[:, 0]
+            return self.fc(fts), fts, self.head_emb(fts)
+
+    return TinyViTEmb()
+
+
+def gen_comatch_step(ref_comatch, ref_custom, ref_conformer, ref_utils, tag, queue_batch, thres, full_state):
+    torch.manual_seed(4242)
+    model = make_tiny_vit_emb(ref_conformer, ref_custom)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if name.endswith("weight") and p.dim() >= 2:
+                nn.init.trunc_normal_(p, std=0.05 if name.startswith(("fc", "head_emb")) else 0.02)
+            elif name in ("cls_token", "pos_embed"):
+                nn.init.trunc_normal_(p, std=0.02)
+            elif name.endswith("weight"):  # LayerNorm / BatchNorm scales
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+            else:
+                p.copy_(0.02 * torch.randn_like(p))
+        model.fc[4].weight.normal_(0.0, 0.6)  # peaky logits: some pseudo-labels pass the threshold
+    init_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+    B, MU, C, L, steps = 2, 2, 23, 16, 2
+    g = torch.Generator().manual_seed(91)
+    lab, unlab = [], []
+    for _ in range(steps):
+        x = torch.randn(B, 3, 64, 64, generator=g)
+        y = torch.randint(0, C, (B,), generator=g)
+        uw, us0, us1 = (torch.randn(B * MU, 3, 64, 64, generator=g) for _ in range(3))
+        lab.append((x, y))
+        unlab.append(((uw, us0, us1), torch.arange(B * MU)))
+    cfg = ref_utils.AttrDict(
+        DATA=ref_utils.AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+        MODEL=ref_utils.AttrDict(NAME="vit_tiny_test", NUM_CLASSES=C, MARGIN="None", TYPE_SEMI="CoMatch",
+                                 LOW_DIM=L),
+        TRAIN=ref_utils.AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=steps,
+                                 CLS_WEIGHT=False, THRES=thres, T=1.0, LAMBDA_U=2.0, LAMBDA_C=2.0, IS_SSL=True,
+                                 EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8,
+                                 SCH_NAME="step", MARGIN="None", S=30.0, M=0.4))
+    # AngularPenaltySMLoss(config) is constructed in get_config but never used on the step path
+    ref_comatch.AngularPenaltySMLoss = lambda *a, **k: None
+    rec = {"masks": [], "outputs": [], "lx": []}
+
+    def drop_hook(mod, inp, out):
+        i, o = inp[0].detach(), out.detach()
+        keep = torch.where(i != 0, (o != 0), torch.ones_like(o, dtype=torch.bool))
+        rec["masks"].append(keep.numpy().astype(np.uint8))
+
+    def out_hook(mod, inp, out):
+        rec["outputs"].append(tuple(t.detach().clone().numpy() for t in out))
+
+    h1 = model.fc[2].register_forward_hook(drop_hook)
+    h2 = model.register_forward_hook(out_hook)
+    o_ce = ref_comatch.ce_loss
+
+    def ce_spy(*a, **k):
+        out = o_ce(*a, **k)
+        rec["lx"].append(out.item())
+        return out
+
+    ref_comatch.ce_loss = ce_spy
+    o_meter = ref_comatch.AverageMeter
+
+    class RecMeter(o_meter):
+        def update(self, val, n=1):
+            rec.setdefault("loss", []).append(val)
+            super().update(val, n)
+
+    ref_comatch.AverageMeter = RecMeter
+    try:
+        tr = ref_comatch.CoMatch(model, opt_func="Adam", lr=1e-3, device="cpu")
+        tr.queue_batch = queue_batch
+        tr.get_dataloader((FakeDL(lab), FakeDL(unlab)), None)
+        tr.get_config(cfg)
+        meter = tr.train_one(1)
+    finally:
+        ref_comatch.ce_loss = o_ce
+        ref_comatch.AverageMeter = o_meter
+        h1.remove()
+        h2.remove()
+    final_sd = model.state_dict()
+    ema_sd = tr.ema_model.ema.state_dict()
+    arrs = dict(thres=np.float32(thres), B=B, MU=MU, L=L, steps=steps, queue_batch=queue_batch,
+                queue_size=tr.queue_size, queue_ptr=tr.queue_ptr, lambda_u=np.float32(2.0),
+                lambda_c=np.float32(2.0), lx=np.array(rec["lx"], np.float32), loss=np.array(rec["loss"], np.float64),
+                meter_avg=np.float32(meter.avg),
+                meter_sum=np.float64(meter.sum), queue_feats=tr.queue_feats.numpy(), queue_probs=tr.queue_probs.numpy(),
+                prob_list=torch.stack(tr.prob_list).numpy(), lr_updates=np.array(tr.lr_scheduler.updates))
+    for i, ((x, y), ((uw, us0, us1), _)) in enumerate(zip(lab, unlab)):
+        arrs[f"x{i}"], arrs[f"y{i}"] = x.numpy(), y.numpy()
+        arrs[f"uw{i}"], arrs[f"us0_{i}"], arrs[f"us1_{i}"] = uw.numpy(), us0.numpy(), us1.numpy()
+        arrs[f"dropmask{i}"] = rec["masks"][i]
+        arrs[f"logits{i}"], arrs[f"fts{i}"], arrs[f"z{i}"] = rec["outputs"][i]
+    for k in init_sd:
+        arrs["init/" + k] = init_sd[k].numpy()
+        if full_state:
+            arrs["final/" + k] = final_sd[k].numpy()
+            arrs["ema/" + k] = ema_sd[k].numpy()
+        else:
+            arrs["final_sum/" + k] = np.float64(final_sd[k].double().sum().item())
+            arrs["ema_sum/" + k] = np.float64(ema_sd[k].double().sum().item())
+    np.savez_compressed(os.path.join(OUT, f"comatch_step_{tag}.npz"), **arrs)
+    print(f"comatch {tag}: lx={rec['lx']} meter_sum={meter.sum:.6f} queue_ptr={tr.queue_ptr} "
+          f"bank_nonzero={int((tr.queue_feats != 0).any(1).sum())}")
+
+
 def main():
+    only = sys.argv[1] if len(sys.argv) > 1 else "all"
     ref_loss, ref_ema, ref_fixmatch, ref_conformer, ref_utils = _import_reference()
+    if only in ("all", "comatch"):
+        ref_comatch, ref_custom = _import_comatch()
+        gen_comatch_step(ref_comatch, ref_custom, ref_conformer, ref_utils, "closed", 5, 0.6, False)
+        gen_comatch_step(ref_comatch, ref_custom, ref_conformer, ref_utils, "open", 1, 0.6, True)
+    if only == "comatch":
+        return
     gen_consistency(ref_loss)
     gen_poly(ref_loss)
     gen_ema(ref_ema)

@@ -79,6 +79,53 @@ def test_fixmatch_step_matches_reference(golden):
         np.testing.assert_array_equal(d["lr_updates"], [2, 3])
 
 
+def _comatch_ref(d, cfg):
+    L, C = int(d["L"]), cfg.num_classes
+    params = {n: torch.tensor(d["init/" + n]) for n, _ in ref.emb_param_shapes(cfg, L)}
+    bufs = {n: torch.tensor(d["init/" + n]) for n in ref.BN_BUFFERS}
+    return ref.CoMatchRef(params, bufs, cfg, L, C, int(d["queue_size"]), class_weights=None,
+                          thres=float(d["thres"]), lambda_u=float(d["lambda_u"]), lambda_c=float(d["lambda_c"]),
+                          lr=1e-3, ema_decay=0.999)
+
+
+def test_comatch_step_matches_reference(golden):
+    """CoMatch.train_one (code/comatch.py:133-235), two steps, bank gate closed (reference default)
+    and open (queue_batch=1).  The labeled batch is the FIRST one in both steps: the reference
+    calls next() on the DataLoader itself, which raises, and falls back to a fresh iterator every
+    step (code/comatch.py:135-138)."""
+    cfg = _tiny_cfg()
+    for tag, full in (("open", True), ("closed", False)):
+        d = golden(f"comatch_step_{tag}.npz")
+        cm = _comatch_ref(d, cfg)
+        for i in range(int(d["steps"])):
+            out = cm.step(torch.tensor(d["x0"]), torch.tensor(d["y0"]), torch.tensor(d[f"uw{i}"]),
+                          torch.tensor(d[f"us0_{i}"]), torch.tensor(d[f"us1_{i}"]), torch.tensor(d[f"dropmask{i}"]))
+            np.testing.assert_allclose(out["logits"].numpy(), d[f"logits{i}"], rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(out["fts"].numpy(), d[f"fts{i}"], rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(out["z"].numpy(), d[f"z{i}"], rtol=1e-5, atol=1e-6)
+            np.testing.assert_allclose(out["lx"], d["lx"][i], rtol=1e-6)
+            np.testing.assert_allclose(out["loss"], d["loss"][i], rtol=1e-6)
+        np.testing.assert_allclose(torch.stack(cm.prob_list).numpy(), d["prob_list"], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(cm.queue_feats.numpy(), d["queue_feats"], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(cm.queue_probs.numpy(), d["queue_probs"], rtol=1e-6, atol=1e-7)
+        assert cm.queue_ptr == int(d["queue_ptr"])
+        names = [n for n, _ in ref.emb_param_shapes(cfg, int(d["L"]))] + list(ref.BN_BUFFERS)
+        for n in names:
+            got = cm.p[n].detach() if n in cm.p else cm.bufs[n]
+            if full:
+                np.testing.assert_allclose(got.numpy(), d["final/" + n], rtol=1e-5, atol=1e-7, err_msg=n)
+                np.testing.assert_allclose(cm.ema[n].numpy(), d["ema/" + n], rtol=1e-5, atol=1e-7, err_msg=n)
+            else:
+                np.testing.assert_allclose(got.double().sum().item(), d["final_sum/" + n], rtol=1e-5, atol=1e-5,
+                                           err_msg=n)
+                np.testing.assert_allclose(cm.ema[n].double().sum().item(), d["ema_sum/" + n], rtol=1e-5,
+                                           atol=1e-5, err_msg=n)
+        np.testing.assert_array_equal(d["lr_updates"], [2, 3])
+    # the open variant actually exercises the bank: rows written in step 1, read in step 2
+    assert np.abs(golden("comatch_step_open.npz")["queue_feats"]).sum() > 0
+    assert np.abs(golden("comatch_step_closed.npz")["queue_feats"]).sum() == 0
+
+
 def test_vit_s_param_count():
     cfg = ref.Cfg()
     n = sum(int(np.prod(s)) for _, s in ref.param_shapes(cfg))
