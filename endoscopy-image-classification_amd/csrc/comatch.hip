@@ -1,0 +1,696 @@
+// CoMatch on the MI355X (gfx950): ModelwEmb heads over the ViT features and the CoMatch step's
+// pseudo-labelling / losses (code/comatch.py:141-222, code/models/custom_model.py:107-145,201-213).
+//
+//  Heads (fp32, rows = images; tiny next to the backbone):
+//    fc       = Linear(D, D/4) -> ReLU -> Dropout(0.2) -> BatchNorm1d(D/4) -> Linear(D/4, C)
+//    head_emb = Linear(D, 3L) -> LeakyReLU(0.1) -> Linear(3L, L) -> Normalize(2)
+//  es_dense_fwd / es_dense_bwd   Linear (+ activation, + replayed dropout keep-mask)
+//  es_bn1d_fwd / es_bn1d_bwd     BatchNorm1d over the batch rows (training statistics, running
+//                                buffers with momentum 0.1 and the unbiased variance, as nn.BatchNorm1d)
+//  es_l2norm_fwd / _bwd          Normalize(2): v / sqrt(sum v^2)
+//  Step (code/comatch.py:162-220):
+//  es_comatch_pseudo             softmax(weak) -> distribution alignment over <= 32 batch means
+//                                (device ring) -> memory smoothing against the bank
+//                                A = exp(z_w . bank^T / T) / rowsum, p = a p + (1-a) A . bank_probs
+//                                -> max / first-index argmax / mask (>= thres)
+//  es_comatch_bank_write         the gated ring write of [z_w; z_x] and [p_orig; onehot(y)]
+//  es_comatch_contrastive_fwd_bwd  sim = exp(z0 z1^T / T) row-normalised, Q = p p^T (diag 1,
+//                                >= th, row-normalised), L_c = -mean_i sum_j Q log(sim + 1e-7),
+//                                and dL_c / dz0, dz1
+//  es_comatch_focal_fwd_bwd      logp = -sum log_softmax(l) p * mask, L_u = mean((1-e^-logp)^g logp)
+#include "common.h"
+
+namespace {
+
+constexpr int DR = 16;  // rows per dense workgroup
+
+// Y[i][c] = act(X[i] . W[c] + b[c]) (* keep[i][c] * keep_scale); 16 rows per workgroup staged in
+// LDS, one output column per thread with 16 row accumulators.
+// act: 0 none, 1 ReLU, 2 LeakyReLU(slope)
+__global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict__ X, int ldx,
+                                                        const float* __restrict__ W,
+                                                        const float* __restrict__ b, float* __restrict__ Y, int ldy,
+                                                        int n, int K, int N, int act, float slope,
+                                                        const uint8_t* __restrict__ keep, float keep_scale) {
+  extern __shared__ float xs[];  // [DR][K]
+  const int r0 = blockIdx.x * DR;
+  const int rows = min(DR, n - r0);
+  for (int id = threadIdx.x; id < DR * K; id += blockDim.x) {
+    const int r = id / K, k = id - r * K;
+    xs[id] = r < rows ? X[(size_t)(r0 + r) * ldx + k] : 0.f;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < N; c += blockDim.x) {
+    float acc[DR];
+#pragma unroll
+    for (int r = 0; r < DR; ++r) acc[r] = 0.f;
+    const float* w = W + (size_t)c * K;
+    for (int k = 0; k < K; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int r = 0; r < DR; ++r) acc[r] = fmaf(xs[r * K + k], wk, acc[r]);
+    }
+    const float bc = b ? b[c] : 0.f;
+    for (int r = 0; r < rows; ++r) {
+      float v = acc[r] + bc;
+      if (act == 1) v = fmaxf(v, 0.f);
+      else if (act == 2) v = v > 0.f ? v : v * slope;
+      if (keep) v = v * ((float)keep[(size_t)(r0 + r) * N + c] * keep_scale);
+      Y[(size_t)(r0 + r) * ldy + c] = v;
+    }
+  }
+}
+
+// dpre[i][c] = dY[i][c] * act'(Yact[i][c]) (* keep * scale).  The activation derivative is read
+// off the stored output: ReLU / LeakyReLU(slope > 0) outputs are > 0 exactly where their inputs
+// are, and a dropped element's gradient is 0 whatever the sign.
+__global__ void dense_dpre_kernel(const float* __restrict__ dY, int lddy, const float* __restrict__ Yact, int ldya,
+                                  int act, float slope, const uint8_t* __restrict__ keep, float keep_scale,
+                                  float* __restrict__ dpre, int n, int N) {
+  const int id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n * N) return;
+  const int i = id / N, c = id - i * N;
+  float g = dY[(size_t)i * lddy + c];
+  if (keep) g *= (float)keep[id] * keep_scale;
+  if (act) {
+    const float y = Yact[(size_t)i * ldya + c];
+    if (!(y > 0.f)) g = act == 1 ? 0.f : g * slope;
+  }
+  dpre[id] = g;
+}
+
+// dX[i][k] (+)= sum_c dpre[i][c] W[c][k]: 16 rows of dpre in LDS, one column k per thread.
+__global__ __launch_bounds__(256) void dense_dx_kernel(const float* __restrict__ dpre, const float* __restrict__ W,
+                                                       float* __restrict__ dX, int lddx, int n, int K, int N,
+                                                       int accumulate) {
+  extern __shared__ float ds[];  // [DR][N]
+  const int r0 = blockIdx.x * DR;
+  const int rows = min(DR, n - r0);
+  for (int id = threadIdx.x; id < DR * N; id += blockDim.x) {
+    const int r = id / N;
+    ds[id] = r < rows ? dpre[(size_t)r0 * N + id] : 0.f;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    float acc[DR];
+#pragma unroll
+    for (int r = 0; r < DR; ++r) acc[r] = 0.f;
+    for (int c = 0; c < N; ++c) {
+      const float w = W[(size_t)c * K + k];
+#pragma unroll
+      for (int r = 0; r < DR; ++r) acc[r] = fmaf(ds[r * N + c], w, acc[r]);
+    }
+    for (int r = 0; r < rows; ++r) {
+      float* o = dX + (size_t)(r0 + r) * lddx + k;
+      *o = accumulate ? *o + acc[r] : acc[r];
+    }
+  }
+}
+
+// dW[c][k] = sum_i dpre[i][c] X[i][k] (column c per blockIdx.y, k over threads); db[c] = sum_i dpre[i][c]
+__global__ __launch_bounds__(256) void dense_dw_kernel(const float* __restrict__ dpre, const float* __restrict__ X,
+                                                       int ldx, float* __restrict__ dW, float* __restrict__ db, int n,
+                                                       int K, int N) {
+  const int c = blockIdx.y;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) {
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int i = 0;
+    for (; i + 4 <= n; i += 4) {
+      a0 = fmaf(dpre[(size_t)i * N + c], X[(size_t)i * ldx + k], a0);
+      a1 = fmaf(dpre[(size_t)(i + 1) * N + c], X[(size_t)(i + 1) * ldx + k], a1);
+      a2 = fmaf(dpre[(size_t)(i + 2) * N + c], X[(size_t)(i + 2) * ldx + k], a2);
+      a3 = fmaf(dpre[(size_t)(i + 3) * N + c], X[(size_t)(i + 3) * ldx + k], a3);
+    }
+    for (; i < n; ++i) a0 = fmaf(dpre[(size_t)i * N + c], X[(size_t)i * ldx + k], a0);
+    dW[(size_t)c * K + k] = (a0 + a1) + (a2 + a3);
+  }
+  if (db && blockIdx.x == 0 && threadIdx.x == 0) {
+    float s = 0.f;
+    for (int i = 0; i < n; ++i) s += dpre[(size_t)i * N + c];
+    db[c] = s;
+  }
+}
+
+// BatchNorm1d over rows, one workgroup per feature: batch mean / biased variance (two passes),
+// y = xhat * gamma + beta; running stats <- (1-m) r + m (mean, unbiased var); eval uses them.
+__global__ __launch_bounds__(256) void bn1d_fwd_kernel(const float* __restrict__ U, int ldu,
+                                                       const float* __restrict__ gamma,
+                                                       const float* __restrict__ beta, float* running_mean,
+                                                       float* running_var, long long* nbt, float momentum, float eps,
+                                                       int train, float* __restrict__ Y, int ldy,
+                                                       float* __restrict__ xhat, float* __restrict__ rstd_out, int n,
+                                                       int F) {
+  __shared__ float red[256];
+  const int f = blockIdx.x, t = threadIdx.x;
+  float mean, rstd;
+  if (train) {
+    float s = 0.f;
+    for (int i = t; i < n; i += blockDim.x) s += U[(size_t)i * ldu + f];
+    red[t] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] += red[t + o];
+      __syncthreads();
+    }
+    mean = red[0] / n;
+    __syncthreads();
+    float ss = 0.f;
+    for (int i = t; i < n; i += blockDim.x) {
+      const float d = U[(size_t)i * ldu + f] - mean;
+      ss += d * d;
+    }
+    red[t] = ss;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] += red[t + o];
+      __syncthreads();
+    }
+    const float var = red[0] / n;
+    rstd = 1.0f / sqrtf(var + eps);
+    if (t == 0) {
+      running_mean[f] = (1.f - momentum) * running_mean[f] + momentum * mean;
+      running_var[f] = (1.f - momentum) * running_var[f] + momentum * (n > 1 ? var * n / (n - 1) : var);
+      if (f == 0 && nbt) *nbt += 1;
+      rstd_out[f] = rstd;
+    }
+  } else {
+    mean = running_mean[f];
+    rstd = 1.0f / sqrtf(running_var[f] + eps);
+  }
+  const float g = gamma[f], bt = beta[f];
+  for (int i = t; i < n; i += blockDim.x) {
+    const float xh = (U[(size_t)i * ldu + f] - mean) * rstd;
+    if (xhat) xhat[(size_t)i * F + f] = xh;
+    Y[(size_t)i * ldy + f] = xh * g + bt;
+  }
+}
+
+// dU = gamma * rstd * (dY - mean(dY) - xhat * mean(dY * xhat)); dgamma = sum dY xhat, dbeta = sum dY
+__global__ __launch_bounds__(256) void bn1d_bwd_kernel(const float* __restrict__ dY, int lddy,
+                                                       const float* __restrict__ xhat,
+                                                       const float* __restrict__ rstd,
+                                                       const float* __restrict__ gamma, float* __restrict__ dU,
+                                                       int lddu, float* __restrict__ dgamma,
+                                                       float* __restrict__ dbeta, int n, int F) {
+  __shared__ float r1[256], r2[256];
+  const int f = blockIdx.x, t = threadIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = t; i < n; i += blockDim.x) {
+    const float g = dY[(size_t)i * lddy + f];
+    s1 += g;
+    s2 += g * xhat[(size_t)i * F + f];
+  }
+  r1[t] = s1;
+  r2[t] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      r1[t] += r1[t + o];
+      r2[t] += r2[t + o];
+    }
+    __syncthreads();
+  }
+  const float sdy = r1[0], sdyx = r2[0];
+  if (t == 0) {
+    dgamma[f] = sdyx;
+    dbeta[f] = sdy;
+  }
+  const float k = gamma[f] * rstd[f], m1 = sdy / n, m2 = sdyx / n;
+  for (int i = t; i < n; i += blockDim.x)
+    dU[(size_t)i * lddu + f] = k * (dY[(size_t)i * lddy + f] - m1 - xhat[(size_t)i * F + f] * m2);
+}
+
+// Normalize(2): one wave per row, L <= 256
+__global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict__ V, int ldv, float* __restrict__ Z,
+                                                         int ldz, float* __restrict__ nrm, int n, int L) {
+  const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < L; c += 64) {
+    const float v = V[(size_t)i * ldv + c];
+    s += v * v;
+  }
+  const float nv = sqrtf(warp_sum(s));
+  for (int c = lane; c < L; c += 64) Z[(size_t)i * ldz + c] = V[(size_t)i * ldv + c] / nv;
+  if (lane == 0) nrm[i] = nv;
+}
+
+// dV = (dZ - Z (Z . dZ)) / norm
+__global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict__ dZ, int lddz,
+                                                         const float* __restrict__ Z, int ldz,
+                                                         const float* __restrict__ nrm, float* __restrict__ dV,
+                                                         int lddv, int n, int L) {
+  const int lane = threadIdx.x & 63, i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  float s = 0.f;
+  for (int c = lane; c < L; c += 64) s += Z[(size_t)i * ldz + c] * dZ[(size_t)i * lddz + c];
+  s = warp_sum(s);
+  const float inv = 1.0f / nrm[i];
+  for (int c = lane; c < L; c += 64)
+    dV[(size_t)i * lddv + c] = (dZ[(size_t)i * lddz + c] - Z[(size_t)i * ldz + c] * s) * inv;
+}
+
+// ---- CoMatch pseudo-labels (code/comatch.py:162-185) -------------------------------------------
+// Stage 1 (one workgroup): softmax of the weak logits, the batch mean appended to the DA ring
+// (hist[pos]), prob_avg = mean of the ring's len entries oldest -> newest, p /= prob_avg,
+// p /= rowsum -> probs_orig.
+__global__ __launch_bounds__(256) void comatch_da_kernel(const float* __restrict__ lw, int ldl, int nu, int C,
+                                                         float* __restrict__ hist, int cap, int len, int pos,
+                                                         float* __restrict__ probs_orig) {
+  __shared__ float colsum[256];
+  __shared__ float avg[256];
+  const int t = threadIdx.x;
+  // softmax rows: one thread per row (C <= 256 is tiny)
+  for (int i = t; i < nu; i += blockDim.x) {
+    const float* l = lw + (size_t)i * ldl;
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, l[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(l[c] - mx);
+    for (int c = 0; c < C; ++c) probs_orig[(size_t)i * C + c] = expf(l[c] - mx) / s;
+  }
+  __syncthreads();
+  if (t < C) {
+    float s = 0.f;
+    for (int i = 0; i < nu; ++i) s += probs_orig[(size_t)i * C + t];
+    hist[(size_t)pos * C + t] = s / nu;
+  }
+  __syncthreads();
+  if (t < C) {
+    float s = 0.f;
+    for (int j = 0; j < len; ++j) {
+      int e = pos - (len - 1) + j;
+      e = e < 0 ? e + cap : e;
+      s += hist[(size_t)e * C + t];
+    }
+    avg[t] = s / len;
+  }
+  __syncthreads();
+  for (int i = t; i < nu; i += blockDim.x) {
+    float* p = probs_orig + (size_t)i * C;
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) {
+      p[c] = p[c] / avg[c];
+      s += p[c];
+    }
+    for (int c = 0; c < C; ++c) p[c] = p[c] / s;
+  }
+  (void)colsum;
+}
+
+// Stage 2: memory smoothing partials.  Workgroup (chunk, row group): 64 weak rows x SB bank rows;
+// thread t holds row t/4's embedding in registers and walks every 4th bank row of the chunk:
+// e = exp((z . b) / T), S_e += e, S_p[c] += e * bank_probs[c].  Partials [chunk][row][C+1].
+constexpr int SB = 256;
+__global__ __launch_bounds__(256) void comatch_smooth_partial_kernel(const float* __restrict__ zw, int ldz, int nu,
+                                                                     int L, const float* __restrict__ bf,
+                                                                     const float* __restrict__ bp, int Q, int C,
+                                                                     float temperature, float* __restrict__ part) {
+  extern __shared__ float sm[];  // bank feats [SB][L] then probs [SB][C]
+  float* fs = sm;
+  float* ps = sm + SB * L;
+  const int chunk = blockIdx.x, j0 = chunk * SB, nb = min(SB, Q - j0);
+  for (int id = threadIdx.x; id < SB * L; id += blockDim.x) fs[id] = id / L < nb ? bf[(size_t)j0 * L + id] : 0.f;
+  for (int id = threadIdx.x; id < SB * C; id += blockDim.x) ps[id] = id / C < nb ? bp[(size_t)j0 * C + id] : 0.f;
+  __syncthreads();
+  const int r = blockIdx.y * 64 + (threadIdx.x >> 2), sub = threadIdx.x & 3;
+  if (r >= nu) return;
+  float z[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) z[c] = c < L ? zw[(size_t)r * ldz + c] : 0.f;
+  float se = 0.f, sp[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) sp[c] = 0.f;
+  for (int j = sub; j < nb; j += 4) {
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < 64; ++c)
+      if (c < L) d = fmaf(z[c], fs[j * L + c], d);
+    const float e = expf(d / temperature);
+    se += e;
+#pragma unroll
+    for (int c = 0; c < 32; ++c)
+      if (c < C) sp[c] = fmaf(e, ps[j * C + c], sp[c]);
+  }
+  // combine the 4 sub-lanes of a row
+#pragma unroll
+  for (int o = 1; o < 4; o <<= 1) {
+    se += __shfl_xor(se, o, 64);
+#pragma unroll
+    for (int c = 0; c < 32; ++c) sp[c] += __shfl_xor(sp[c], o, 64);
+  }
+  if (sub == 0) {
+    float* out = part + ((size_t)chunk * nu + r) * (C + 1);
+    for (int c = 0; c < C; ++c) out[c] = sp[c];
+    out[C] = se;
+  }
+}
+
+// Stage 3 (one thread per weak row): p = a p_orig + (1-a) (sum_chunks S_p) / (sum_chunks S_e);
+// score / first-index argmax / mask.
+__global__ void comatch_pseudo_final_kernel(const float* __restrict__ probs_orig, const float* __restrict__ part,
+                                            int nchunks, int nu, int C, float alpha, float thres,
+                                            float* __restrict__ probs, int* __restrict__ pl,
+                                            float* __restrict__ mask) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nu) return;
+  float se = 0.f;
+  for (int k = 0; k < nchunks; ++k) se += part[((size_t)k * nu + i) * (C + 1) + C];
+  float best = -INFINITY;
+  int bi = 0;
+  for (int c = 0; c < C; ++c) {
+    float s = 0.f;
+    for (int k = 0; k < nchunks; ++k) s += part[((size_t)k * nu + i) * (C + 1) + c];
+    const float v = alpha * probs_orig[(size_t)i * C + c] + (1.f - alpha) * (s / se);
+    probs[(size_t)i * C + c] = v;
+    if (v > best) {  // strict: first index on ties (torch.max)
+      best = v;
+      bi = c;
+    }
+  }
+  pl[i] = bi;
+  mask[i] = best >= thres ? 1.f : 0.f;
+}
+
+// bank rows [ptr, ptr + nu) <- z_w, probs_orig; [ptr + nu, ptr + nu + bt) <- z_x, onehot(y)
+__global__ void comatch_bank_write_kernel(const float* __restrict__ zw, int ldzw, int nu,
+                                          const float* __restrict__ zx, int ldzx, int bt, int L,
+                                          const float* __restrict__ probs_orig, const long long* __restrict__ y,
+                                          int C, float* __restrict__ bf, float* __restrict__ bp, int ptr) {
+  const int i = blockIdx.x;  // bank row offset
+  const int row = ptr + i;
+  for (int c = threadIdx.x; c < L; c += blockDim.x)
+    bf[(size_t)row * L + c] = i < nu ? zw[(size_t)i * ldzw + c] : zx[(size_t)(i - nu) * ldzx + c];
+  for (int c = threadIdx.x; c < C; c += blockDim.x)
+    bp[(size_t)row * C + c] = i < nu ? probs_orig[(size_t)i * C + c] : (y[i - nu] == c ? 1.f : 0.f);
+}
+
+// ---- contrastive (code/comatch.py:199-213) ------------------------------------------------------
+// One workgroup per anchor row i: sim_ij = exp((z0_i . z1_j) / T), P = sim / rowsum; Q_ij = p_i . p_j
+// with Q_ii = 1, zeroed below th, row-normalised; loss_i = -sum_j Q_ij log(P_ij + 1e-7).
+// dloss_i/ds_ik = P_ik sum_j w_ij - w_ik with w_ij = Q_ij P_ij / (P_ij + 1e-7); the rows of
+// G = scale * dloss/ds / T feed dz0 = G z1 and dz1 = G^T z0.
+__global__ __launch_bounds__(256) void contrast_rows_kernel(const float* __restrict__ z0, int ldz0,
+                                                            const float* __restrict__ z1, int ldz1,
+                                                            const float* __restrict__ probs, int nu, int L, int C,
+                                                            float temperature, float th, float scale,
+                                                            float* __restrict__ G, float* __restrict__ row_loss) {
+  extern __shared__ float sm[];  // sim [nu], q [nu], z0_i [L], p_i [C]
+  __shared__ float red[256];
+  float* sim = sm;
+  float* q = sm + nu;
+  float* zi = q + nu;
+  float* pi = zi + L;
+  const int i = blockIdx.x, t = threadIdx.x;
+  for (int c = t; c < L; c += blockDim.x) zi[c] = z0[(size_t)i * ldz0 + c];
+  for (int c = t; c < C; c += blockDim.x) pi[c] = probs[(size_t)i * C + c];
+  __syncthreads();
+  float ssum = 0.f, qsum = 0.f;
+  for (int j = t; j < nu; j += blockDim.x) {
+    float d = 0.f;
+    for (int c = 0; c < L; ++c) d = fmaf(zi[c], z1[(size_t)j * ldz1 + c], d);
+    const float e = expf(d / temperature);
+    sim[j] = e;
+    ssum += e;
+    float qq = 0.f;
+    for (int c = 0; c < C; ++c) qq = fmaf(pi[c], probs[(size_t)j * C + c], qq);
+    if (j == i) qq = 1.f;
+    qq = qq >= th ? qq : 0.f;
+    q[j] = qq;
+    qsum += qq;
+  }
+  auto block_sum = [&](float v) {
+    red[t] = v;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (t < o) red[t] += red[t + o];
+      __syncthreads();
+    }
+    const float r = red[0];
+    __syncthreads();
+    return r;
+  };
+  ssum = block_sum(ssum);
+  qsum = block_sum(qsum);
+  float lsum = 0.f, wsum = 0.f;
+  for (int j = t; j < nu; j += blockDim.x) {
+    const float P = sim[j] / ssum, Qn = q[j] / qsum;
+    lsum -= logf(P + 1e-7f) * Qn;
+    const float w = Qn * P / (P + 1e-7f);
+    sim[j] = P;
+    q[j] = w;
+    wsum += w;
+  }
+  lsum = block_sum(lsum);
+  wsum = block_sum(wsum);
+  const float k = scale / temperature;
+  for (int j = t; j < nu; j += blockDim.x) G[(size_t)i * nu + j] = k * (sim[j] * wsum - q[j]);
+  if (t == 0) row_loss[i] = lsum;
+}
+
+// dz0[i] = sum_k G[i][k] z1[k] (blockIdx.y = 0) and dz1[k] = sum_i G[i][k] z0[i] (blockIdx.y = 1):
+// one wave per output row, lanes over L
+__global__ __launch_bounds__(256) void contrast_dz_kernel(const float* __restrict__ G, const float* __restrict__ z0,
+                                                          int ldz0, const float* __restrict__ z1, int ldz1,
+                                                          float* __restrict__ dz0, int lddz0, float* __restrict__ dz1,
+                                                          int lddz1, int nu, int L) {
+  const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= nu) return;
+  const bool t1 = blockIdx.y == 1;
+  for (int c = lane; c < L; c += 64) {
+    float acc = 0.f;
+    if (!t1) {
+      for (int k = 0; k < nu; ++k) acc = fmaf(G[(size_t)r * nu + k], z1[(size_t)k * ldz1 + c], acc);
+      dz0[(size_t)r * lddz0 + c] = acc;
+    } else {
+      for (int i = 0; i < nu; ++i) acc = fmaf(G[(size_t)i * nu + r], z0[(size_t)i * ldz0 + c], acc);
+      dz1[(size_t)r * lddz1 + c] = acc;
+    }
+  }
+}
+
+// mean of per-row values (one workgroup) -> out[0]
+__global__ __launch_bounds__(256) void row_mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
+  __shared__ float red[256];
+  const int t = threadIdx.x;
+  float s = 0.f;
+  for (int i = t; i < n; i += blockDim.x) s += v[i];
+  red[t] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  if (t == 0) out[0] = red[0] / n;
+}
+
+// ---- focal unsupervised loss (code/comatch.py:215-220) ------------------------------------------
+// One thread per row: logp = -mask * sum_c log_softmax(l)_c p_c, q = exp(-logp),
+// loss = (1-q)^g logp; dloss/dl_c = scale * dL/dlogp * (-mask) (p_c - softmax_c sum p),
+// dL/dlogp = g (1-q)^(g-1) q logp + (1-q)^g.  Row losses -> row_loss.
+__global__ void focal_kernel(const float* __restrict__ ls, int ldl, const float* __restrict__ probs,
+                             const float* __restrict__ mask, int nu, int C, float gamma, float scale,
+                             float* __restrict__ dls, int lddl, float* __restrict__ row_loss) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nu) return;
+  const float* l = ls + (size_t)i * ldl;
+  const float* p = probs + (size_t)i * C;
+  float mx = -INFINITY;
+  for (int c = 0; c < C; ++c) mx = fmaxf(mx, l[c]);
+  float se = 0.f;
+  for (int c = 0; c < C; ++c) se += expf(l[c] - mx);
+  const float lse = mx + logf(se);
+  float dot = 0.f, psum = 0.f;
+  for (int c = 0; c < C; ++c) {
+    dot += (l[c] - lse) * p[c];
+    psum += p[c];
+  }
+  const float m = mask[i];
+  const float logp = -dot * m;
+  const float q = expf(-logp);
+  const float om = 1.f - q;
+  const float pw = gamma == 2.f ? om * om : powf(om, gamma);
+  row_loss[i] = pw * logp;
+  const float dpw = gamma == 2.f ? 2.f * om : gamma * powf(om, gamma - 1.f);
+  const float dL = dpw * q * logp + pw;
+  for (int c = 0; c < C; ++c) {
+    const float sm = expf(l[c] - lse);
+    dls[(size_t)i * lddl + c] = scale * dL * (-m) * (p[c] - sm * psum);
+  }
+}
+
+// Dropout keep-mask: counter-based (splitmix64 of seed + element index), keep = u >= p with u the
+// top 24 bits as a uniform [0, 1) -- reproducible for a (seed, offset) pair, no RNG state.
+__global__ void dropout_keep_kernel(uint8_t* __restrict__ keep, long n, float p, unsigned long long seed,
+                                    unsigned long long offset) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  unsigned long long z = seed + 0x9E3779B97F4A7C15ull * (offset + (unsigned long long)i + 1ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(z >> 40) * (1.0f / 16777216.0f);
+  keep[i] = u >= p ? 1 : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Dropout(p) keep-mask for n elements (uint8 0/1); the kept values are scaled by 1/(1-p) by the
+// consumer (es_dense_fwd keep_scale)
+int es_dropout_keep(void* keep, long n, float p, unsigned long long seed, unsigned long long offset,
+                    hipStream_t stream) {
+  if (n < 0 || !(p >= 0.f && p < 1.f)) return ES_BAD_SHAPE;
+  if (!keep) return ES_BAD_ARG;
+  if (n == 0) return ES_OK;
+  hipLaunchKernelGGL(dropout_keep_kernel, (unsigned)((n + 255) / 256), 256, 0, stream, (uint8_t*)keep, n, p, seed,
+                     offset);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+
+int es_dense_fwd(const float* X, int ldx, const float* W, const float* b, float* Y, int ldy, int n, int K, int N,
+                 int act, float slope, const void* keep, float keep_scale, hipStream_t stream) {
+  if (n <= 0 || K <= 0 || N <= 0 || K > 2048 || act < 0 || act > 2) return ES_BAD_SHAPE;
+  if (!X || !W || !Y) return ES_BAD_ARG;
+  const size_t lds = (size_t)DR * K * 4;
+  allow_lds(dense_fwd_kernel, lds);
+  hipLaunchKernelGGL(dense_fwd_kernel, (n + DR - 1) / DR, 256, lds, stream, X, ldx, W, b, Y, ldy, n, K, N, act, slope,
+                     (const uint8_t*)keep, keep_scale);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+size_t es_dense_bwd_workspace(int n, int N) { return (size_t)n * N; }
+
+// Backward of Y = act(X W^T + b) (* keep * scale): dW, db (overwritten), dX (+)= when dX != null.
+// workspace: es_dense_bwd_workspace(n, N) floats.
+int es_dense_bwd(const float* dY, int lddy, const float* Yact, int ldya, int act, float slope, const void* keep,
+                 float keep_scale, const float* X, int ldx, const float* W, float* dX, int lddx, int accumulate_dx,
+                 float* dW, float* db, int n, int K, int N, float* workspace, hipStream_t stream) {
+  if (n <= 0 || K <= 0 || N <= 0 || N > 2048 || act < 0 || act > 2) return ES_BAD_SHAPE;
+  if (!dY || !X || !W || !dW || !workspace || (act && !Yact)) return ES_BAD_ARG;
+  hipLaunchKernelGGL(dense_dpre_kernel, (n * N + 255) / 256, 256, 0, stream, dY, lddy, Yact, ldya, act, slope,
+                     (const uint8_t*)keep, keep_scale, workspace, n, N);
+  hipLaunchKernelGGL(dense_dw_kernel, dim3((K + 255) / 256, N), 256, 0, stream, workspace, X, ldx, dW, db, n, K, N);
+  if (dX) {
+    const size_t lds = (size_t)DR * N * 4;
+    allow_lds(dense_dx_kernel, lds);
+    hipLaunchKernelGGL(dense_dx_kernel, (n + DR - 1) / DR, 256, lds, stream, workspace, W, dX, lddx, n, K, N,
+                       accumulate_dx);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// BatchNorm1d over n rows x F features (nn.BatchNorm1d semantics).  train: batch statistics,
+// running buffers updated (num_batches_tracked += 1 when nbt != null), xhat / rstd saved;
+// eval: running statistics.
+int es_bn1d_fwd(const float* U, int ldu, const float* gamma, const float* beta, float* running_mean, float* running_var,
+                void* num_batches_tracked, float momentum, float eps, int train, float* Y, int ldy, float* xhat,
+                float* rstd, int n, int F, hipStream_t stream) {
+  if (n <= 0 || F <= 0) return ES_BAD_SHAPE;
+  if (!U || !gamma || !beta || !running_mean || !running_var || !Y || (train && (!xhat || !rstd))) return ES_BAD_ARG;
+  hipLaunchKernelGGL(bn1d_fwd_kernel, F, 256, 0, stream, U, ldu, gamma, beta, running_mean, running_var,
+                     (long long*)num_batches_tracked, momentum, eps, train, Y, ldy, xhat, rstd, n, F);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_bn1d_bwd(const float* dY, int lddy, const float* xhat, const float* rstd, const float* gamma, float* dU,
+                int lddu, float* dgamma, float* dbeta, int n, int F, hipStream_t stream) {
+  if (n <= 0 || F <= 0) return ES_BAD_SHAPE;
+  if (!dY || !xhat || !rstd || !gamma || !dU || !dgamma || !dbeta) return ES_BAD_ARG;
+  hipLaunchKernelGGL(bn1d_bwd_kernel, F, 256, 0, stream, dY, lddy, xhat, rstd, gamma, dU, lddu, dgamma, dbeta, n, F);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_l2norm_fwd(const float* V, int ldv, float* Z, int ldz, float* norm, int n, int L, hipStream_t stream) {
+  if (n <= 0 || L <= 0) return ES_BAD_SHAPE;
+  if (!V || !Z || !norm) return ES_BAD_ARG;
+  hipLaunchKernelGGL(l2norm_fwd_kernel, (n + 3) / 4, 256, 0, stream, V, ldv, Z, ldz, norm, n, L);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_l2norm_bwd(const float* dZ, int lddz, const float* Z, int ldz, const float* norm, float* dV, int lddv, int n,
+                  int L, hipStream_t stream) {
+  if (n <= 0 || L <= 0) return ES_BAD_SHAPE;
+  if (!dZ || !Z || !norm || !dV) return ES_BAD_ARG;
+  hipLaunchKernelGGL(l2norm_bwd_kernel, (n + 3) / 4, 256, 0, stream, dZ, lddz, Z, ldz, norm, dV, lddv, n, L);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+size_t es_comatch_pseudo_workspace(int nu, int C, int Q) {
+  const int nchunks = (Q + SB - 1) / SB;
+  return (size_t)nchunks * nu * (C + 1);
+}
+
+// Pseudo-labels of the weak rows: DA (append this batch's mean to hist[hist_pos], average the
+// hist_len newest entries of the hist_cap ring), memory smoothing against the bank (Q rows),
+// argmax / mask.  probs_orig is the DA output (what the bank stores), probs the smoothed one.
+int es_comatch_pseudo(const float* logits_w, int ldl, int nu, int C, float* hist, int hist_cap, int hist_len,
+                      int hist_pos, const float* z_w, int ldz, int L, const float* bank_feats, const float* bank_probs,
+                      int Q, float temperature, float alpha, float thres, float* probs, float* probs_orig, int* pl,
+                      float* mask, float* workspace, hipStream_t stream) {
+  if (nu <= 0 || C <= 0 || C > 32 || L <= 0 || L > 64 || Q <= 0 || hist_cap <= 0 || hist_len <= 0 ||
+      hist_len > hist_cap || hist_pos < 0 || hist_pos >= hist_cap)
+    return ES_BAD_SHAPE;
+  if (!logits_w || !hist || !z_w || !bank_feats || !bank_probs || !probs || !probs_orig || !pl || !mask || !workspace)
+    return ES_BAD_ARG;
+  hipLaunchKernelGGL(comatch_da_kernel, 1, 256, 0, stream, logits_w, ldl, nu, C, hist, hist_cap, hist_len, hist_pos,
+                     probs_orig);
+  const int nchunks = (Q + SB - 1) / SB;
+  const size_t lds = (size_t)SB * (L + C) * 4;
+  allow_lds(comatch_smooth_partial_kernel, lds);
+  hipLaunchKernelGGL(comatch_smooth_partial_kernel, dim3(nchunks, (nu + 63) / 64), 256, lds, stream, z_w, ldz, nu, L,
+                     bank_feats, bank_probs, Q, C, temperature, workspace);
+  hipLaunchKernelGGL(comatch_pseudo_final_kernel, (nu + 255) / 256, 256, 0, stream, probs_orig, workspace, nchunks, nu,
+                     C, alpha, thres, probs, pl, mask);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_comatch_bank_write(const float* z_w, int ldzw, int nu, const float* z_x, int ldzx, int bt, int L,
+                          const float* probs_orig, const void* y_int64, int C, float* bank_feats, float* bank_probs,
+                          int ptr, int Q, hipStream_t stream) {
+  if (nu < 0 || bt < 0 || L <= 0 || C <= 0 || ptr < 0 || ptr + nu + bt > Q) return ES_BAD_SHAPE;
+  if (!z_w || !z_x || !probs_orig || !y_int64 || !bank_feats || !bank_probs) return ES_BAD_ARG;
+  if (nu + bt == 0) return ES_OK;
+  hipLaunchKernelGGL(comatch_bank_write_kernel, nu + bt, 64, 0, stream, z_w, ldzw, nu, z_x, ldzx, bt, L, probs_orig,
+                     (const long long*)y_int64, C, bank_feats, bank_probs, ptr);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+size_t es_comatch_contrastive_workspace(int nu) { return (size_t)nu * nu + nu; }
+
+// loss_out[0] = L_c = mean_i L_i (unscaled); dz0 / dz1 = grad_scale * d(sum_i L_i) / dz (overwritten)
+int es_comatch_contrastive_fwd_bwd(const float* z0, int ldz0, const float* z1, int ldz1, const float* probs, int nu,
+                                   int L, int C, float temperature, float contrast_th, float grad_scale,
+                                   float* loss_out, float* dz0, int lddz0, float* dz1, int lddz1, float* workspace,
+                                   hipStream_t stream) {
+  if (nu <= 0 || L <= 0 || C <= 0 || nu > 8192) return ES_BAD_SHAPE;
+  if (!z0 || !z1 || !probs || !loss_out || !dz0 || !dz1 || !workspace) return ES_BAD_ARG;
+  float* G = workspace;
+  float* row_loss = workspace + (size_t)nu * nu;
+  const size_t lds = (size_t)(2 * nu + L + C) * 4;
+  allow_lds(contrast_rows_kernel, lds);
+  hipLaunchKernelGGL(contrast_rows_kernel, nu, 256, lds, stream, z0, ldz0, z1, ldz1, probs, nu, L, C, temperature,
+                     contrast_th, grad_scale, G, row_loss);
+  hipLaunchKernelGGL(contrast_dz_kernel, dim3((nu + 3) / 4, 2), 256, 0, stream, G, z0, ldz0, z1, ldz1, dz0, lddz0, dz1,
+                     lddz1, nu, L);
+  hipLaunchKernelGGL(row_mean_kernel, 1, 256, 0, stream, row_loss, nu, loss_out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// loss_out[0] = L_u = mean_i L_i (unscaled); dls = grad_scale * d(sum_i L_i) / dlogits_s0 (overwritten);
+// workspace nu floats
+int es_comatch_focal_fwd_bwd(const float* ls, int ldl, const float* probs, const float* mask, int nu, int C,
+                             float gamma, float grad_scale, float* loss_out, float* dls, int lddl, float* workspace,
+                             hipStream_t stream) {
+  if (nu <= 0 || C <= 0) return ES_BAD_SHAPE;
+  if (!ls || !probs || !mask || !loss_out || !dls || !workspace) return ES_BAD_ARG;
+  hipLaunchKernelGGL(focal_kernel, (nu + 255) / 256, 256, 0, stream, ls, ldl, probs, mask, nu, C, gamma, grad_scale,
+                     dls, lddl, workspace);
+  hipLaunchKernelGGL(row_mean_kernel, 1, 256, 0, stream, workspace, nu, loss_out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+}  // extern "C"

@@ -191,6 +191,72 @@ __global__ void cls_head_wgrad_kernel(const float* __restrict__ dl, int lddl, co
   }
 }
 
+// CoMatch features: one wave per image, fts = LN(x_cls) (the ModelwEmb `fts` over a ViT trunk,
+// code/models/custom_model.py:207-209); xhat / rstd saved for the backward.
+template <int V>
+__global__ __launch_bounds__(256) void cls_ln_fwd_kernel(const float* __restrict__ x, int ldx, int T,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, float* __restrict__ fts,
+                                                         int ldf, float* __restrict__ xhat,
+                                                         float* __restrict__ rstd_out, int n, float eps) {
+  constexpr int D = V * 64;
+  const int lane = threadIdx.x & 63;
+  const int im = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (im >= n) return;
+  const float* xr = x + (size_t)im * T * ldx;
+  float v[V], s = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    v[j] = xr[j * 64 + lane];
+    s += v[j];
+  }
+  const float mean = warp_sum(s) * (1.0f / D);
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) ss += (v[j] - mean) * (v[j] - mean);
+  const float rstd = 1.0f / sqrtf(warp_sum(ss) * (1.0f / D) + eps);
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int d = j * 64 + lane;
+    const float xh = (v[j] - mean) * rstd;
+    xhat[(size_t)im * D + d] = xh;
+    fts[(size_t)im * ldf + d] = xh * gamma[d] + beta[d];
+  }
+  if (lane == 0) rstd_out[im] = rstd;
+}
+
+// dx_cls = LN'(dfts) into row img*T of dx (other rows untouched); dgamma / dbeta partials per
+// 4-image workgroup folded with fp32 atomics (the grad buffer is zeroed per step).
+template <int V>
+__global__ __launch_bounds__(256) void cls_ln_bwd_kernel(const float* __restrict__ dfts, int lddf,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ xhat,
+                                                         const float* __restrict__ rstd_in, float* __restrict__ dx,
+                                                         int lddx, int T, float* __restrict__ dgamma,
+                                                         float* __restrict__ dbeta, int n) {
+  constexpr int D = V * 64;
+  const int lane = threadIdx.x & 63;
+  const int im = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (im >= n) return;
+  float dy[V], xh[V], gd[V], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int d = j * 64 + lane;
+    dy[j] = dfts[(size_t)im * lddf + d];
+    xh[j] = xhat[(size_t)im * D + d];
+    gd[j] = dy[j] * gamma[d];
+    s1 += gd[j];
+    s2 += gd[j] * xh[j];
+    atomicAdd(dgamma + d, dy[j] * xh[j]);
+    atomicAdd(dbeta + d, dy[j]);
+  }
+  s1 = warp_sum(s1) * (1.0f / D);
+  s2 = warp_sum(s2) * (1.0f / D);
+  const float rstd = rstd_in[im];
+#pragma unroll
+  for (int j = 0; j < V; ++j) dx[(size_t)im * T * lddx + j * 64 + lane] = rstd * (gd[j] - s1 - xh[j] * s2);
+}
+
 }  // namespace
 
 extern "C" {
@@ -253,6 +319,25 @@ int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamm
   dim3 g2((D + 255) / 256, (n + chunk - 1) / chunk);
   hipLaunchKernelGGL(cls_head_wgrad_kernel, g2, 256, 0, stream, dl, lddl, xhat, dyn, gamma, beta, dW, db, dgamma,
                      dbeta, n, C, D, chunk);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// CoMatch feature path: fts [n, D] = LN(x_cls) and its backward (dgamma / dbeta accumulated)
+int es_cls_ln_fwd(const float* x, int ldx, int T, const float* gamma, const float* beta, float* fts, int ldf,
+                  float* xhat, float* rstd, int n, int D, float eps, hipStream_t stream) {
+  if (n <= 0 || D % 64) return ES_BAD_SHAPE;
+  if (!x || !gamma || !beta || !fts || !xhat || !rstd) return ES_BAD_ARG;
+  const int grid = (n + 3) / 4;
+  HEAD_DISPATCH(cls_ln_fwd_kernel, D / 64, grid, stream, x, ldx, T, gamma, beta, fts, ldf, xhat, rstd, n, eps);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_cls_ln_bwd(const float* dfts, int lddf, const float* gamma, const float* xhat, const float* rstd, float* dx,
+                  int lddx, int T, float* dgamma, float* dbeta, int n, int D, hipStream_t stream) {
+  if (n <= 0 || D % 64) return ES_BAD_SHAPE;
+  if (!dfts || !gamma || !xhat || !rstd || !dx || !dgamma || !dbeta) return ES_BAD_ARG;
+  const int grid = (n + 3) / 4;
+  HEAD_DISPATCH(cls_ln_bwd_kernel, D / 64, grid, stream, dfts, lddf, gamma, xhat, rstd, dx, lddx, T, dgamma, dbeta, n);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ENDOSSL_LIB", os.path.join(_HERE, "lib", "libendossl_hip.so"))
 
 V, I, L, F, Z = ctypes.c_void_p, ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_size_t
+U64 = ctypes.c_ulonglong
 
 # name -> (restype, argtypes).  Mirrors include/endossl.h one-to-one (tests/test_abi.py checks it).
 SIGNATURES = {
@@ -37,6 +38,22 @@ SIGNATURES = {
     "es_embed_bwd": (I, [V, I, V, I, V, V, I, I, I, I, V]),
     "es_cls_head_fwd": (I, [V, I, I, V, V, V, V, V, I, V, V, I, I, I, F, V]),
     "es_cls_head_bwd": (I, [V, I, V, V, V, V, V, V, V, I, I, V, V, V, V, I, I, I, V]),
+    "es_cls_ln_fwd": (I, [V, I, I, V, V, V, I, V, V, I, I, F, V]),
+    "es_cls_ln_bwd": (I, [V, I, V, V, V, V, I, I, V, V, I, I, V]),
+    "es_dense_fwd": (I, [V, I, V, V, V, I, I, I, I, I, F, V, F, V]),
+    "es_dense_bwd_workspace": (Z, [I, I]),
+    "es_dense_bwd": (I, [V, I, V, I, I, F, V, F, V, I, V, V, I, I, V, V, I, I, I, V, V]),
+    "es_bn1d_fwd": (I, [V, I, V, V, V, V, V, F, F, I, V, I, V, V, I, I, V]),
+    "es_bn1d_bwd": (I, [V, I, V, V, V, V, I, V, V, I, I, V]),
+    "es_dropout_keep": (I, [V, L, F, U64, U64, V]),
+    "es_l2norm_fwd": (I, [V, I, V, I, V, I, I, V]),
+    "es_l2norm_bwd": (I, [V, I, V, I, V, V, I, I, I, V]),
+    "es_comatch_pseudo_workspace": (Z, [I, I, I]),
+    "es_comatch_pseudo": (I, [V, I, I, I, V, I, I, I, V, I, I, V, V, I, F, F, F, V, V, V, V, V, V]),
+    "es_comatch_bank_write": (I, [V, I, I, V, I, I, I, V, V, I, V, V, I, I, V]),
+    "es_comatch_contrastive_workspace": (Z, [I]),
+    "es_comatch_contrastive_fwd_bwd": (I, [V, I, V, I, V, I, I, I, F, F, F, V, V, I, V, I, V, V]),
+    "es_comatch_focal_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, V, I, V, V]),
     "es_fm_consistency_fwd_bwd": (I, [V, I, V, I, I, I, F, F, V, V, V, V, I, V, V]),
     "es_poly_ce_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, I, V, V]),
     "es_adam_ema_step": (I, [V, V, V, V, V, L, F, F, F, F, F, F, F, F, V]),

@@ -5,10 +5,13 @@ num_classes=C)` (code/build.py:196-197) -- a network weight download, and timm i
 This factory returns the native ViT for the `vit_*` names instead (random timm-style init, or a
 checkpoint from MODEL.PRE_TRAIN_PATH loaded with weights_only=True, head dropped when its class
 count differs -- the reference re-heads abnormality checkpoints the same way, :180-194).
+For MODEL.TYPE_SEMI == 'CoMatch' it returns ModelwEmb over the native ViT (:175-178;
+comatch_model.NativeViTEmb, forward -> (logits, fts, z), LOW_DIM-d embedding).
 CNN / Swin / Conformer backbones are outside round-1 scope.
 """
 import torch
 
+from .comatch_model import NativeViTEmb
 from .vit import VIT_CONFIGS, NativeViT, ViTConfig
 
 
@@ -17,12 +20,14 @@ def build_model(config, is_pathology=True, seed=0):
     C = int(config.MODEL.NUM_CLASSES)
     if name not in VIT_CONFIGS:
         raise NotImplementedError(f"backbone {name!r}: native builds exist for {sorted(VIT_CONFIGS)}")
-    if getattr(config.MODEL, "TYPE_SEMI", "FixMatch") == "CoMatch" and getattr(config.TRAIN, "IS_SSL", True):
-        raise NotImplementedError("CoMatch ModelwEmb head on the native ViT is a later §8 row")
+    comatch = getattr(config.MODEL, "TYPE_SEMI", "FixMatch") == "CoMatch" and getattr(config.TRAIN, "IS_SSL", True)
     kw = dict(VIT_CONFIGS[name])
     if "IMG_SIZE" in config.DATA and int(config.DATA.IMG_SIZE) != kw["img_size"]:
         kw["img_size"] = int(config.DATA.IMG_SIZE)
-    model = NativeViT(ViTConfig(num_classes=C, **kw), seed=seed)
+    if comatch:
+        model = NativeViTEmb(ViTConfig(num_classes=C, head="emb", low_dim=int(config.MODEL.LOW_DIM), **kw), seed=seed)
+    else:
+        model = NativeViT(ViTConfig(num_classes=C, **kw), seed=seed)
     path = getattr(config.MODEL, "PRE_TRAIN_PATH", "None")
     if path not in (None, "None", ""):
         ck = torch.load(path, map_location="cpu", weights_only=True)

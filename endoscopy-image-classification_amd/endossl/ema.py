@@ -24,16 +24,21 @@ class ModelEMA(object):
         if self.device is not None:
             self.ema.to(device=device)
         self._tab = None
+        self._btab = None
 
     # reference arithmetic: decay * e + (1. - decay) * m, scalars rounded to fp32
     def _scalars(self):
         return float(self.decay), float(1.0 - self.decay)
 
-    def _build_table(self, model):
-        pairs = list(zip(self.ema.state_dict().values(), model.state_dict().values()))
-        key = tuple((e.data_ptr(), m.data_ptr()) for e, m in pairs)
-        if self._tab is not None and self._tab[0] == key:
-            return self._tab
+    def _build_table(self, model, buffers_only=False):
+        if buffers_only:
+            pairs = [(e, m) for (_, e), (_, m) in zip(self.ema.named_buffers(), model.named_buffers())]
+        else:
+            pairs = list(zip(self.ema.state_dict().values(), model.state_dict().values()))
+        key = (buffers_only,) + tuple((e.data_ptr(), m.data_ptr()) for e, m in pairs)
+        cache = self._btab if buffers_only else self._tab
+        if cache is not None and cache[0] == key:
+            return cache
         esz = _lib.load().es_ema_entry_size()
         raw = bytearray(esz * len(pairs))
         chunks = []
@@ -54,8 +59,11 @@ class ModelEMA(object):
         dev = next(iter(self.ema.state_dict().values())).device
         tab = torch.frombuffer(raw, dtype=torch.uint8).to(dev)
         ch = torch.tensor(chunks, dtype=torch.int32).to(dev)
-        self._tab = (key, tab, ch)
-        return self._tab
+        if buffers_only:
+            self._btab = (key, tab, ch)
+        else:
+            self._tab = (key, tab, ch)
+        return (key, tab, ch)
 
     def _update(self, model, decay, one_minus):
         _, tab, ch = self._build_table(model)
@@ -66,6 +74,15 @@ class ModelEMA(object):
     def update(self, model):
         d, omd = self._scalars()
         self._update(model, d, omd)
+
+    def update_buffers(self, model):
+        """EMA of the buffers only (BatchNorm running stats + num_batches_tracked): the trainers
+        fuse the parameters' EMA into the Adam sweep (es_adam_ema_step)."""
+        if not any(True for _ in model.named_buffers()):
+            return
+        d, omd = self._scalars()
+        _, tab, ch = self._build_table(model, buffers_only=True)
+        call("es_ema_update_multi", ptr(tab), ptr(ch), int(ch.shape[0]), d, omd, _lib.stream())
 
     def set(self, model):
         # update_fn = lambda e, m: m  ->  0*e + 1*m (exact for finite e)

@@ -34,10 +34,17 @@ def _rup(x, m):
 
 
 class ViTConfig:
+    """head = "cls": timm's Linear head on the CLS token (FixMatch / SemiFormer-style models);
+    head = "emb": ModelwEmb's heads on the final-LN CLS feature (CoMatch, code/models/custom_model.py:
+    147-213): fc = Linear(D, D/4) -> ReLU -> Dropout(0.2) -> BatchNorm1d -> Linear(D/4, C) and
+    head_emb = Linear(D, 3L) -> LeakyReLU(0.1) -> Linear(3L, L) -> Normalize(2), L = low_dim."""
+
     def __init__(self, img_size=224, patch=16, dim=384, depth=12, heads=6, mlp_ratio=4.0, num_classes=23,
-                 eps=1e-6):
+                 eps=1e-6, head="cls", low_dim=64):
         self.img_size, self.patch, self.dim, self.depth = img_size, patch, dim, depth
         self.heads, self.num_classes, self.eps = heads, num_classes, eps
+        self.head, self.low_dim = head, low_dim
+        assert head in ("cls", "emb")
         self.hidden = int(dim * mlp_ratio)
         self.grid = img_size // patch
         self.np = self.grid * self.grid
@@ -47,7 +54,8 @@ class ViTConfig:
 
     def as_dict(self):
         return dict(img_size=self.img_size, patch=self.patch, dim=self.dim, depth=self.depth, heads=self.heads,
-                    mlp_ratio=self.hidden / self.dim, num_classes=self.num_classes, eps=self.eps)
+                    mlp_ratio=self.hidden / self.dim, num_classes=self.num_classes, eps=self.eps, head=self.head,
+                    low_dim=self.low_dim)
 
 
 VIT_CONFIGS = {
@@ -58,8 +66,18 @@ VIT_CONFIGS = {
 }
 
 
+def emb_head_layout(cfg):
+    """ModelwEmb heads (code/models/custom_model.py:110-116 build_head(is_complex=True) indices
+    0 Linear, 3 BatchNorm1d, 4 Linear; :201-205 head_emb indices 0 Linear, 2 Linear)."""
+    D, C, L, F = cfg.dim, cfg.num_classes, cfg.low_dim, cfg.dim // 4
+    return [("fc.0.weight", (F, D)), ("fc.0.bias", (F,)), ("fc.3.weight", (F,)), ("fc.3.bias", (F,)),
+            ("fc.4.weight", (C, F)), ("fc.4.bias", (C,)), ("head_emb.0.weight", (3 * L, D)),
+            ("head_emb.0.bias", (3 * L,)), ("head_emb.2.weight", (L, 3 * L)), ("head_emb.2.bias", (L,))]
+
+
 def param_layout(cfg):
-    """timm 0.5.4 VisionTransformer state_dict order: (name, shape)."""
+    """timm 0.5.4 VisionTransformer state_dict order: (name, shape); the "emb" head replaces
+    `head` with ModelwEmb's fc / head_emb parameters."""
     D, Hd, C = cfg.dim, cfg.hidden, cfg.num_classes
     out = [("cls_token", (1, 1, D)), ("pos_embed", (1, cfg.T, D)),
            ("patch_embed.proj.weight", (D, 3, cfg.patch, cfg.patch)), ("patch_embed.proj.bias", (D,))]
@@ -71,7 +89,11 @@ def param_layout(cfg):
                 (b + "norm2.weight", (D,)), (b + "norm2.bias", (D,)),
                 (b + "mlp.fc1.weight", (Hd, D)), (b + "mlp.fc1.bias", (Hd,)),
                 (b + "mlp.fc2.weight", (D, Hd)), (b + "mlp.fc2.bias", (D,))]
-    out += [("norm.weight", (D,)), ("norm.bias", (D,)), ("head.weight", (C, D)), ("head.bias", (C,))]
+    out += [("norm.weight", (D,)), ("norm.bias", (D,))]
+    if cfg.head == "emb":
+        out += emb_head_layout(cfg)
+    else:
+        out += [("head.weight", (C, D)), ("head.bias", (C,))]
     offs, o = {}, 0
     for name, shape in out:
         offs[name] = o
@@ -94,6 +116,19 @@ def timm_init_(flat, cfg, layout, offs, generator=None):
             elif name == "patch_embed.proj.bias":
                 bound = 1.0 / math.sqrt(3 * cfg.patch * cfg.patch)
                 nn.init.uniform_(t, -bound, bound, generator=generator)
+            elif name.startswith(("fc.", "head_emb.")):
+                # ModelwEmb heads keep the PyTorch defaults: Linear kaiming_uniform(a=sqrt(5)) with
+                # bias U(+-1/sqrt(fan_in)), BatchNorm1d weight 1 / bias 0
+                if name == "fc.3.weight":
+                    t.fill_(1.0)
+                elif name == "fc.3.bias":
+                    t.zero_()
+                elif len(shape) == 2:
+                    nn.init.kaiming_uniform_(t, a=math.sqrt(5), generator=generator)
+                else:
+                    w = [sh for nm, sh in layout if nm == name[:-len("bias")] + "weight"][0]
+                    bound = 1.0 / math.sqrt(w[1])
+                    nn.init.uniform_(t, -bound, bound, generator=generator)
             elif name.startswith("head"):
                 t.zero_()
             elif name.endswith("weight") and len(shape) == 2:
@@ -131,6 +166,7 @@ class _Acts:
         self.xhat = z(n, D)
         self.rstd_cls = z(n)
         self.logits = z(n, cfg.num_classes)
+        self.fts = z(n, D) if cfg.head == "emb" else None
 
 
 class _Grads:
@@ -238,7 +274,8 @@ class Engine:
     # -------------------------------------------------------------- forward
     def forward(self, flat, images_list, train):
         """images_list: fp32 [n_i, 3, S, S] device tensors, processed as one batch (no concat copy).
-        Returns fp32 logits [n, C] (a view into the engine's buffer)."""
+        Returns fp32 logits [n, C] (head "cls") or the CLS features [n, D] (head "emb"), a view into
+        the engine's buffer."""
         cfg = self.cfg
         s = _lib.stream()
         n = sum(int(t.shape[0]) for t in images_list)
@@ -288,6 +325,10 @@ class Engine:
             call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
                  ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xout), D, None, ptr(xmid), D, M, D, Hd, 0, s)
         xl = A.x[cfg.depth] if train else A.x[cfg.depth & 1]
+        if cfg.head == "emb":  # CLS features for ModelwEmb's heads (comatch_model.py)
+            call("es_cls_ln_fwd", ptr(xl), D, T, ptr(self.view(flat, "norm.weight")),
+                 ptr(self.view(flat, "norm.bias")), ptr(A.fts), D, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.eps, s)
+            return A.fts
         call("es_cls_head_fwd", ptr(xl), D, T, ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")),
              ptr(self.view(flat, "head.weight")), ptr(self.view(flat, "head.bias")), ptr(A.logits),
              cfg.num_classes, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.num_classes, cfg.eps, s)
@@ -314,11 +355,17 @@ class Engine:
         call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
-    def backward(self, flat, grad, dlogits):
-        """dlogits fp32 [n, C] for the last train forward -> grad (flat fp32, overwritten)."""
+    def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True):
+        """dlogits fp32 [n, C] (head "cls") or dfts fp32 [n, D] (head "emb") for the last train
+        forward -> grad (flat fp32).  zero_grad=False when the caller already zeroed `grad` and
+        wrote the head gradients into it (the trunk's entries are overwritten either way; the
+        final-norm grads are accumulated)."""
         cfg = self.cfg
         s = _lib.stream()
-        n = int(dlogits.shape[0])
+        top = dfts if cfg.head == "emb" else dlogits
+        if top is None:
+            raise ValueError("Engine.backward needs dlogits (cls head) or dfts (emb head)")
+        n = int(top.shape[0])
         A = self.acts(n, True)
         if n not in self._grads:
             self._grads[n] = _Grads(cfg, n, self.device)
@@ -326,12 +373,19 @@ class Engine:
         D, Hd, T, H, M = cfg.dim, cfg.hidden, cfg.T, cfg.heads, A.M
         gv = lambda name: self.view(grad, name)  # noqa: E731
         fv = lambda name: self.view(flat, name)  # noqa: E731
-        grad.zero_()
+        if zero_grad:
+            grad.zero_()
         G.dx.zero_()
-        dlogits = dlogits.contiguous()
-        call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
-             ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(G.dx), D, T, ptr(gv("head.weight")),
-             ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D, cfg.num_classes, s)
+        if cfg.head == "emb":
+            dfts = dfts.contiguous()
+            call("es_cls_ln_bwd", ptr(dfts), D, ptr(fv("norm.weight")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dx), D, T,
+                 ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D, s)
+        else:
+            dlogits = dlogits.contiguous()
+            call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
+                 ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(G.dx), D, T,
+                 ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
+                 cfg.num_classes, s)
         call("es_cast_f32_bf16", ptr(G.dx), ptr(G.dxb), M * D, s)
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."

@@ -90,6 +90,65 @@ int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamm
                     const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW, float* db,
                     float* dgamma, float* dbeta, int n, int D, int C, hipStream_t stream);
 
+/* CoMatch features: fts [n, D] = LN(x_cls) (ModelwEmb's `fts` over the ViT trunk,
+ * code/models/custom_model.py:207-209) and its backward into the CLS rows of dx; dgamma / dbeta
+ * accumulated (+=). */
+int es_cls_ln_fwd(const float* x, int ldx, int T, const float* gamma, const float* beta, float* fts, int ldf,
+                  float* xhat, float* rstd, int n, int D, float eps, hipStream_t stream);
+int es_cls_ln_bwd(const float* dfts, int lddf, const float* gamma, const float* xhat, const float* rstd, float* dx,
+                  int lddx, int T, float* dgamma, float* dbeta, int n, int D, hipStream_t stream);
+
+/* ---- CoMatch heads (fp32; code/models/custom_model.py:107-145,201-205) ------------------------- */
+/* Y = act(X W^T + b) (* keep * keep_scale, the replayed Dropout keep-mask, uint8 [n, N]);
+ * act 0 = none, 1 = ReLU, 2 = LeakyReLU(slope) */
+int es_dense_fwd(const float* X, int ldx, const float* W, const float* b, float* Y, int ldy, int n, int K, int N,
+                 int act, float slope, const void* keep, float keep_scale, hipStream_t stream);
+size_t es_dense_bwd_workspace(int n, int N);
+/* backward of es_dense_fwd given its output Yact: dW, db overwritten; dX (+)= when dX != NULL */
+int es_dense_bwd(const float* dY, int lddy, const float* Yact, int ldya, int act, float slope, const void* keep,
+                 float keep_scale, const float* X, int ldx, const float* W, float* dX, int lddx, int accumulate_dx,
+                 float* dW, float* db, int n, int K, int N, float* workspace, hipStream_t stream);
+/* BatchNorm1d (nn.BatchNorm1d semantics): train = batch statistics + running-buffer update
+ * (momentum, unbiased variance, num_batches_tracked int64 += 1), eval = running statistics */
+int es_bn1d_fwd(const float* U, int ldu, const float* gamma, const float* beta, float* running_mean, float* running_var,
+                void* num_batches_tracked, float momentum, float eps, int train, float* Y, int ldy, float* xhat,
+                float* rstd, int n, int F, hipStream_t stream);
+int es_bn1d_bwd(const float* dY, int lddy, const float* xhat, const float* rstd, const float* gamma, float* dU,
+                int lddu, float* dgamma, float* dbeta, int n, int F, hipStream_t stream);
+/* Dropout(p) keep-mask (uint8 0/1), counter-based hash of (seed, offset + i) */
+int es_dropout_keep(void* keep, long n, float p, unsigned long long seed, unsigned long long offset,
+                    hipStream_t stream);
+/* Normalize(2) (code/models/custom_model.py:136-145) */
+int es_l2norm_fwd(const float* V, int ldv, float* Z, int ldz, float* norm, int n, int L, hipStream_t stream);
+int es_l2norm_bwd(const float* dZ, int lddz, const float* Z, int ldz, const float* norm, float* dV, int lddv, int n,
+                  int L, hipStream_t stream);
+
+/* ---- CoMatch step (code/comatch.py:162-220) ---------------------------------------------------- */
+size_t es_comatch_pseudo_workspace(int nu, int C, int Q);
+/* softmax(weak) -> distribution alignment (batch mean appended at hist[hist_pos] of a hist_cap
+ * ring, mean of the hist_len newest) -> memory smoothing against the Q-row bank -> argmax / mask.
+ * C <= 32, L <= 64. */
+int es_comatch_pseudo(const float* logits_w, int ldl, int nu, int C, float* hist, int hist_cap, int hist_len,
+                      int hist_pos, const float* z_w, int ldz, int L, const float* bank_feats, const float* bank_probs,
+                      int Q, float temperature, float alpha, float thres, float* probs, float* probs_orig, int* pl,
+                      float* mask, float* workspace, hipStream_t stream);
+/* ring write of [z_w; z_x] and [probs_orig; onehot(y)] at bank row ptr (code/comatch.py:187-196) */
+int es_comatch_bank_write(const float* z_w, int ldzw, int nu, const float* z_x, int ldzx, int bt, int L,
+                          const float* probs_orig, const void* y_int64, int C, float* bank_feats, float* bank_probs,
+                          int ptr, int Q, hipStream_t stream);
+size_t es_comatch_contrastive_workspace(int nu);
+/* loss_out[0] = L_c = mean_i L_i; dz0 / dz1 = grad_scale * d(sum_i L_i)/dz -- pass lambda_c / nu for the
+ * gradient of lambda_c * L_c (code/comatch.py:199-213) */
+int es_comatch_contrastive_fwd_bwd(const float* z0, int ldz0, const float* z1, int ldz1, const float* probs, int nu,
+                                   int L, int C, float temperature, float contrast_th, float grad_scale,
+                                   float* loss_out, float* dz0, int lddz0, float* dz1, int lddz1, float* workspace,
+                                   hipStream_t stream);
+/* loss_out[0] = L_u = mean_i L_i; dls = grad_scale * d(sum_i L_i)/dlogits -- pass lambda_u / nu
+ * (code/comatch.py:215-220); workspace nu floats */
+int es_comatch_focal_fwd_bwd(const float* ls, int ldl, const float* probs, const float* mask, int nu, int C,
+                             float gamma, float grad_scale, float* loss_out, float* dls, int lddl, float* workspace,
+                             hipStream_t stream);
+
 /* ---- FixMatch losses, forward + gradient fused ------------------------------------------------ */
 /* code/loss.py:126-164 consistency_loss(name='ce', use_hard_labels=True); out[0]=loss, out[1]=mask mean */
 int es_fm_consistency_fwd_bwd(const float* logits_w, int ldw, const float* logits_s, int lds, int n, int C,

@@ -148,3 +148,35 @@ def test_average_meter():
     m.update(2.0, 4)
     m.update(4.0, 4)
     assert m.avg == 3.0 and m.count == 8
+
+
+def test_vit_emb_layout_matches_reference_modelwemb(golden):
+    """NativeViTEmb's state_dict = the reference ModelwEmb-style model's (names, shapes, order,
+    BatchNorm1d buffers), on the CPU (no kernel calls)."""
+    from endossl.comatch_model import NativeViTEmb
+    from endossl.vit import ViTConfig
+    d = golden("comatch_step_closed.npz")
+    m = NativeViTEmb(ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23, head="emb",
+                               low_dim=int(d["L"])), seed=0)
+    sd = m.state_dict()
+    ref_keys = [k[5:] for k in d.files if k.startswith("init/")]
+    assert list(sd.keys()) == ref_keys
+    for k in ref_keys:
+        assert tuple(sd[k].shape) == d["init/" + k].shape, k
+        assert sd[k].dtype == {"float32": torch.float32, "int64": torch.int64}[str(d["init/" + k].dtype)], k
+    m.load_state_dict({k: torch.tensor(d["init/" + k]) for k in ref_keys})
+    assert torch.equal(m.fc[4].weight.detach() if hasattr(m.fc, "__getitem__") else
+                       m.fc._modules["4"].weight.detach(), torch.tensor(d["init/fc.4.weight"]))
+    import copy
+    e = copy.deepcopy(m)
+    assert torch.equal(e.state_dict()["fc.3.running_var"], sd["fc.3.running_var"])
+
+
+def test_build_model_routes_comatch():
+    from endossl.build import build_model
+    from endossl.comatch_model import NativeViTEmb
+    from endossl.utils import AttrDict, with_defaults
+    cfg = with_defaults(AttrDict(MODEL=AttrDict(NAME="vit_tiny_test", NUM_CLASSES=23, TYPE_SEMI="CoMatch", LOW_DIM=16),
+                                 TRAIN=AttrDict(IS_SSL=True), DATA=AttrDict(IMG_SIZE=64)))
+    m = build_model(cfg)
+    assert isinstance(m, NativeViTEmb) and m.cfg.low_dim == 16 and m.cfg.head == "emb"

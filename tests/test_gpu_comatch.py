@@ -1,0 +1,363 @@
+"""CoMatch on the MI355X: every CoMatch C-ABI kernel against a plain torch fp32 restatement of the
+reference arithmetic (autograd for the gradients), and the native CoMatch trainer against the
+reference's own CoMatch.train_one fixtures (tests/golden/comatch_step_{open,closed}.npz, bank
+gate open / closed), replaying the reference's dropout masks.
+
+Bars: kernels within fp32 tolerances (rtol 1e-4 .. 1e-5); trainer losses / logits as the FixMatch
+step test (tests/test_gpu_step.py): step 0 within 1e-3 * scale of the bf16-contract oracle, and
+|HIP - reference| <= 1.5 * |bf16 contract - reference| + 1e-3 * scale; post-step params within
+2 * lr * steps (+1e-5); pseudo-labels / masks bit-exact on decidable rows.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from endossl import _lib  # noqa: E402
+from endossl._lib import call, ptr  # noqa: E402
+from oracle import ref  # noqa: E402
+
+DEV = "cuda"
+
+
+def S():
+    return _lib.stream()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    _lib.load()
+
+
+# ------------------------------------------------------------------------------------- kernels
+@pytest.mark.parametrize("n,T,D", [(5, 17, 128), (9, 197, 384)])
+def test_cls_ln_fwd_bwd(n, T, D):
+    torch.manual_seed(n)
+    x = torch.randn(n * T, D, device=DEV) * 2 + 0.3
+    g = 1 + 0.1 * torch.randn(D, device=DEV)
+    b = 0.1 * torch.randn(D, device=DEV)
+    fts = torch.zeros(n, D, device=DEV)
+    xhat, rstd = torch.zeros(n, D, device=DEV), torch.zeros(n, device=DEV)
+    call("es_cls_ln_fwd", ptr(x), D, T, ptr(g), ptr(b), ptr(fts), D, ptr(xhat), ptr(rstd), n, D, 1e-6, S())
+    xr = x.view(n, T, D)[:, 0].clone().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (D,), gr, br, 1e-6)
+    torch.testing.assert_close(fts, yr.detach(), rtol=1e-5, atol=1e-5)
+    dy = torch.randn(n, D, device=DEV)
+    yr.backward(dy)
+    dx = torch.full((n * T, D), 7.0, device=DEV)
+    dg, db = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    call("es_cls_ln_bwd", ptr(dy), D, ptr(g), ptr(xhat), ptr(rstd), ptr(dx), D, T, ptr(dg), ptr(db), n, D, S())
+    torch.testing.assert_close(dx.view(n, T, D)[:, 0], xr.grad, rtol=1e-4, atol=1e-4)
+    assert torch.all(dx.view(n, T, D)[:, 1:] == 7.0)  # only CLS rows written
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("with_keep", [False, True])
+def test_dense_fwd_bwd(act, with_keep):
+    torch.manual_seed(act * 2 + with_keep)
+    n, K, N = 37, 384, 96
+    X = torch.randn(n, K, device=DEV)
+    W = torch.randn(N, K, device=DEV) * 0.05
+    b = torch.randn(N, device=DEV) * 0.1
+    keep = (torch.rand(n, N, device=DEV) >= 0.2).to(torch.uint8) if with_keep else None
+    scale = 1.25
+    Y = torch.zeros(n, N, device=DEV)
+    call("es_dense_fwd", ptr(X), K, ptr(W), ptr(b), ptr(Y), N, n, K, N, act, 0.1, ptr(keep) if with_keep else None,
+         scale, S())
+    Xr, Wr, br = (t.clone().requires_grad_(True) for t in (X, W, b))
+    pre = Xr @ Wr.t() + br
+    y = pre if act == 0 else (F.relu(pre) if act == 1 else F.leaky_relu(pre, 0.1))
+    if with_keep:
+        y = y * keep.float() * scale
+    torch.testing.assert_close(Y, y.detach(), rtol=1e-5, atol=1e-5)
+    dY = torch.randn(n, N, device=DEV)
+    y.backward(dY)
+    dX = torch.full((n, K), 0.5, device=DEV)
+    dW, db = torch.zeros(N, K, device=DEV), torch.zeros(N, device=DEV)
+    ws = torch.zeros(_lib.load().es_dense_bwd_workspace(n, N), device=DEV)
+    call("es_dense_bwd", ptr(dY), N, ptr(Y) if act else None, N, act, 0.1, ptr(keep) if with_keep else None, scale,
+         ptr(X), K, ptr(W), ptr(dX), K, 1, ptr(dW), ptr(db), n, K, N, ptr(ws), S())
+    torch.testing.assert_close(dX, Xr.grad + 0.5, rtol=1e-4, atol=1e-4)  # accumulate = 1
+    torch.testing.assert_close(dW, Wr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("n,Fe", [(1408, 96), (14, 32), (2, 8)])
+def test_bn1d_fwd_bwd(n, Fe):
+    torch.manual_seed(n)
+    U = torch.randn(n, Fe, device=DEV) * 1.7 + 0.4
+    g = 1 + 0.1 * torch.randn(Fe, device=DEV)
+    bt = 0.1 * torch.randn(Fe, device=DEV)
+    rm, rv = torch.randn(Fe, device=DEV) * 0.1, 1 + torch.rand(Fe, device=DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    rm_ref, rv_ref = rm.clone(), rv.clone()
+    Y, xhat, rstd = torch.zeros(n, Fe, device=DEV), torch.zeros(n, Fe, device=DEV), torch.zeros(Fe, device=DEV)
+    call("es_bn1d_fwd", ptr(U), Fe, ptr(g), ptr(bt), ptr(rm), ptr(rv), ptr(nbt), 0.1, 1e-5, 1, ptr(Y), Fe, ptr(xhat),
+         ptr(rstd), n, Fe, S())
+    Ur, gr, br = (t.clone().requires_grad_(True) for t in (U, g, bt))
+    y = F.batch_norm(Ur, rm_ref, rv_ref, gr, br, training=True, momentum=0.1, eps=1e-5)
+    torch.testing.assert_close(Y, y.detach(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rm, rm_ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv, rv_ref, rtol=1e-5, atol=1e-6)
+    assert int(nbt.item()) == 1
+    dY = torch.randn(n, Fe, device=DEV)
+    y.backward(dY)
+    dU, dg, db = torch.zeros(n, Fe, device=DEV), torch.zeros(Fe, device=DEV), torch.zeros(Fe, device=DEV)
+    call("es_bn1d_bwd", ptr(dY), Fe, ptr(xhat), ptr(rstd), ptr(g), ptr(dU), Fe, ptr(dg), ptr(db), n, Fe, S())
+    torch.testing.assert_close(dU, Ur.grad, rtol=1e-3, atol=1e-4)
+    torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(db, br.grad, rtol=1e-4, atol=1e-3)
+    # eval mode: running statistics
+    Y2 = torch.zeros(n, Fe, device=DEV)
+    call("es_bn1d_fwd", ptr(U), Fe, ptr(g), ptr(bt), ptr(rm), ptr(rv), None, 0.1, 1e-5, 0, ptr(Y2), Fe, None, None, n,
+         Fe, S())
+    torch.testing.assert_close(Y2, F.batch_norm(U, rm, rv, g, bt, training=False, eps=1e-5), rtol=1e-5, atol=1e-5)
+
+
+def test_l2norm_fwd_bwd():
+    torch.manual_seed(5)
+    n, L = 50, 64
+    V = torch.randn(n, L, device=DEV)
+    Z, nrm = torch.zeros(n, L, device=DEV), torch.zeros(n, device=DEV)
+    call("es_l2norm_fwd", ptr(V), L, ptr(Z), L, ptr(nrm), n, L, S())
+    Vr = V.clone().requires_grad_(True)
+    z = Vr.div(Vr.pow(2).sum(1, keepdim=True).pow(0.5))  # Normalize(2), code/models/custom_model.py:136-145
+    torch.testing.assert_close(Z, z.detach(), rtol=1e-5, atol=1e-6)
+    dZ = torch.randn(n, L, device=DEV)
+    z.backward(dZ)
+    dV = torch.zeros(n, L, device=DEV)
+    call("es_l2norm_bwd", ptr(dZ), L, ptr(Z), L, ptr(nrm), ptr(dV), L, n, L, S())
+    torch.testing.assert_close(dV, Vr.grad, rtol=1e-4, atol=1e-5)
+
+
+def _unit(t):
+    return t / t.norm(dim=1, keepdim=True)
+
+
+@pytest.mark.parametrize("Q,zero_bank", [(600, False), (2560, True), (65536, False)])
+def test_comatch_pseudo_vs_reference_formula(Q, zero_bank):
+    """DA over a 3-entry history + memory smoothing (code/comatch.py:167-185) vs torch fp64."""
+    torch.manual_seed(Q)
+    nu, C, L, T, alpha, thres = 448, 23, 64, 0.2, 0.9, 0.6
+    lw = torch.randn(nu, C, device=DEV) * torch.rand(nu, 1, device=DEV) * 6
+    zw = _unit(torch.randn(nu, L, device=DEV))
+    bf = torch.zeros(Q, L, device=DEV) if zero_bank else _unit(torch.randn(Q, L, device=DEV))
+    bp = torch.zeros(Q, C, device=DEV) if zero_bank else torch.softmax(torch.randn(Q, C, device=DEV) * 3, -1)
+    hist = torch.zeros(32, C, device=DEV)
+    prev = [torch.softmax(torch.randn(C, device=DEV), -1) for _ in range(2)]
+    hist[30], hist[31] = prev  # ring: two older entries at slots 30, 31; the new one goes to slot 0
+    probs, porig = torch.zeros(nu, C, device=DEV), torch.zeros(nu, C, device=DEV)
+    pl, mask = torch.zeros(nu, dtype=torch.int32, device=DEV), torch.zeros(nu, device=DEV)
+    ws = torch.zeros(_lib.load().es_comatch_pseudo_workspace(nu, C, Q), device=DEV)
+    call("es_comatch_pseudo", ptr(lw), C, nu, C, ptr(hist), 32, 3, 0, ptr(zw), L, L, ptr(bf), ptr(bp), Q, T, alpha,
+         thres, ptr(probs), ptr(porig), ptr(pl), ptr(mask), ptr(ws), S())
+    p = torch.softmax(lw.double(), 1)
+    plist = [t.double() for t in prev] + [p.mean(0)]
+    torch.testing.assert_close(hist[0].double(), plist[-1], rtol=1e-5, atol=1e-7)
+    p = p / torch.stack(plist).mean(0)
+    p = p / p.sum(1, keepdim=True)
+    torch.testing.assert_close(porig.double(), p, rtol=1e-5, atol=1e-7)
+    A = torch.exp(zw.double() @ bf.double().t() / T)
+    A = A / A.sum(1, keepdim=True)
+    p = alpha * p + (1 - alpha) * A @ bp.double()
+    torch.testing.assert_close(probs.double(), p, rtol=1e-5, atol=1e-6)
+    sc, lb = p.max(1)
+    top2 = p.topk(2, 1).values
+    ok = (top2[:, 0] - top2[:, 1]) > 1e-5
+    assert torch.equal(pl.long()[ok], lb[ok])
+    okm = (sc - thres).abs() > 1e-5
+    assert torch.equal(mask.bool()[okm], (sc >= thres)[okm])
+
+
+def test_comatch_bank_write():
+    torch.manual_seed(2)
+    nu, bt, L, C, Q, ptr0 = 14, 2, 16, 23, 48, 16
+    zw, zx = torch.randn(nu, L, device=DEV), torch.randn(bt, L, device=DEV)
+    po = torch.rand(nu, C, device=DEV)
+    y = torch.tensor([3, 22], dtype=torch.int64, device=DEV)
+    bf, bp = torch.full((Q, L), 9.0, device=DEV), torch.full((Q, C), 9.0, device=DEV)
+    call("es_comatch_bank_write", ptr(zw), L, nu, ptr(zx), L, bt, L, ptr(po), ptr(y), C, ptr(bf), ptr(bp), ptr0, Q, S())
+    torch.testing.assert_close(bf[ptr0:ptr0 + nu + bt], torch.cat([zw, zx]), rtol=0, atol=0)
+    onehot = torch.zeros(bt, C, device=DEV).scatter(1, y.view(-1, 1), 1)
+    torch.testing.assert_close(bp[ptr0:ptr0 + nu + bt], torch.cat([po, onehot]), rtol=0, atol=0)
+    assert torch.all(bf[:ptr0] == 9.0) and torch.all(bf[ptr0 + nu + bt:] == 9.0)
+
+
+@pytest.mark.parametrize("nu", [448, 4])
+def test_comatch_contrastive_fwd_bwd(nu):
+    torch.manual_seed(nu)
+    L, C, T, th, scale = 64, 23, 0.2, 0.8, 2.0 / nu
+    z0, z1 = _unit(torch.randn(nu, L, device=DEV)), _unit(torch.randn(nu, L, device=DEV))
+    probs = torch.softmax(torch.randn(nu, C, device=DEV) * 4, -1) * 0.9
+    loss = torch.zeros(1, device=DEV)
+    dz0, dz1 = torch.zeros(nu, L, device=DEV), torch.zeros(nu, L, device=DEV)
+    ws = torch.zeros(_lib.load().es_comatch_contrastive_workspace(nu), device=DEV)
+    call("es_comatch_contrastive_fwd_bwd", ptr(z0), L, ptr(z1), L, ptr(probs), nu, L, C, T, th, scale, ptr(loss),
+         ptr(dz0), L, ptr(dz1), L, ptr(ws), S())
+    a, b = z0.clone().requires_grad_(True), z1.clone().requires_grad_(True)
+    sim = torch.exp(a @ b.t() / T)  # code/comatch.py:200-213
+    sp = sim / sim.sum(1, keepdim=True)
+    Qm = probs @ probs.t()
+    Qm.fill_diagonal_(1)
+    Qm = Qm * (Qm >= th).float()
+    Qm = Qm / Qm.sum(1, keepdim=True)
+    lc = -(torch.log(sp + 1e-7) * Qm).sum(1).mean()
+    (lc * (scale * nu)).backward()
+    np.testing.assert_allclose(loss.item(), lc.item(), rtol=1e-5)
+    torch.testing.assert_close(dz0, a.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(dz1, b.grad, rtol=1e-4, atol=1e-6)
+
+
+def test_comatch_focal_fwd_bwd():
+    torch.manual_seed(9)
+    nu, C, scale = 448, 23, 2.0 / 448
+    ls = torch.randn(nu, C, device=DEV) * 3
+    probs = torch.softmax(torch.randn(nu, C, device=DEV) * 3, -1) * 0.9  # rows sum to alpha (empty bank)
+    mask = (torch.rand(nu, device=DEV) > 0.4).float()
+    loss, dls = torch.zeros(1, device=DEV), torch.zeros(nu, C, device=DEV)
+    ws = torch.zeros(nu, device=DEV)
+    call("es_comatch_focal_fwd_bwd", ptr(ls), C, ptr(probs), ptr(mask), nu, C, 2.0, scale, ptr(loss), ptr(dls), C,
+         ptr(ws), S())
+    lr = ls.clone().requires_grad_(True)
+    logp = -torch.sum(F.log_softmax(lr, dim=1) * probs, dim=1) * mask  # code/comatch.py:216-220
+    p = torch.exp(-logp)
+    lu = ((1 - p) ** 2 * logp).mean()
+    (lu * (scale * nu)).backward()
+    np.testing.assert_allclose(loss.item(), lu.item(), rtol=1e-5)
+    torch.testing.assert_close(dls, lr.grad, rtol=1e-4, atol=1e-7)
+
+
+def test_dropout_keep_mask():
+    n = 1 << 20
+    a, b = torch.zeros(n, dtype=torch.uint8, device=DEV), torch.zeros(n, dtype=torch.uint8, device=DEV)
+    call("es_dropout_keep", ptr(a), n, 0.2, 7, 0, S())
+    call("es_dropout_keep", ptr(b), n, 0.2, 7, 0, S())
+    assert torch.equal(a, b)  # reproducible for (seed, offset)
+    frac = a.float().mean().item()
+    assert abs(frac - 0.8) < 3e-3, frac
+    call("es_dropout_keep", ptr(b), n, 0.2, 7, n, S())
+    assert not torch.equal(a, b)
+
+
+# ------------------------------------------------------------------------------------- trainer
+class _DL:
+    def __init__(self, items, df=None):
+        self.items = items
+
+        class _DS:
+            pass
+
+        self.dataset = _DS()
+        self.dataset.df = df
+
+    def __iter__(self):
+        return iter(self.items)
+
+    def __len__(self):
+        return len(self.items)
+
+
+def _cfg(thres, steps, B, MU, L):
+    from endossl.utils import AttrDict
+    return AttrDict(
+        DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+        MODEL=AttrDict(NAME="vit_tiny_test", NUM_CLASSES=23, MARGIN="None", TYPE_SEMI="CoMatch", LOW_DIM=L),
+        TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=steps, CLS_WEIGHT=False,
+                       THRES=thres, T=1.0, LAMBDA_U=2.0, LAMBDA_C=2.0, IS_SSL=True, EPOCHS=1, WARMUP_EPOCHS=0,
+                       DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const", FREQ_EVAL=1))
+
+
+@pytest.mark.parametrize("tag", ["open", "closed"])
+def test_comatch_trainer_vs_reference_train_one(golden, tag):
+    from endossl.comatch import CoMatch
+    from endossl.comatch_model import NativeViTEmb
+    from endossl.vit import ViTConfig
+    d = golden(f"comatch_step_{tag}.npz")
+    L, steps, B, MU = int(d["L"]), int(d["steps"]), int(d["B"]), int(d["MU"])
+    rcfg = ref.Cfg(img_size=64, patch=16, dim=128, depth=2, heads=2, num_classes=23)
+    vcfg = ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23, head="emb", low_dim=L)
+    names = [n for n, _ in ref.emb_param_shapes(rcfg, L)]
+    params = {n: torch.tensor(d["init/" + n]) for n in names}
+    bufs = {n: torch.tensor(d["init/" + n]) for n in ref.BN_BUFFERS}
+    m = NativeViTEmb(vcfg, seed=0)
+    assert list(m.state_dict().keys()) == [k[5:] for k in d.files if k.startswith("init/")]  # ModelwEmb names/order
+    m.load_state_dict({**params, **bufs})
+    m = m.to(DEV)
+    tr = CoMatch(m, opt_func="Adam", lr=1e-3, device=DEV)
+    tr.queue_batch = int(d["queue_batch"])
+    lab = (torch.tensor(d["x0"]), torch.tensor(d["y0"]))  # fresh labeled iterator every step (reference)
+    unl = [((torch.tensor(d[f"uw{i}"]), torch.tensor(d[f"us0_{i}"]), torch.tensor(d[f"us1_{i}"])), None)
+           for i in range(steps)]
+    tr.get_dataloader((_DL([lab]), _DL(unl)), None)
+    tr.get_config(_cfg(float(d["thres"]), steps, B, MU, L))
+    assert tr.queue_size == int(d["queue_size"])
+    emu = ref.CoMatchRef(params, bufs, rcfg, L, 23, int(d["queue_size"]), thres=float(d["thres"]), lambda_u=2.0,
+                         lambda_c=2.0, bf16=True)
+    f32 = ref.CoMatchRef(params, bufs, rcfg, L, 23, int(d["queue_size"]), thres=float(d["thres"]), lambda_u=2.0,
+                         lambda_c=2.0)
+    rec = {}
+    for i in range(steps):
+        keep = torch.tensor(d[f"dropmask{i}"])
+        o = tr.step((lab, unl[i]), drop_keep=keep)
+        imgs = unl[i][0]
+        r = emu.step(*lab, *imgs, keep)
+        r32 = f32.step(*lab, *imgs, keep)
+        lg, lg16, lg32 = o["logits"].detach().cpu().double(), r["logits"].double(), torch.tensor(d[f"logits{i}"]).double()
+        env = (lg16 - lg32).abs().max().item()
+        err = (lg - lg32).abs().max().item()
+        sc = max(1.0, lg32.abs().max().item())
+        rec[f"step{i}_logits"] = {"hip_vs_ref": err, "bf16_envelope": env}
+        if i == 0:
+            assert (lg - lg16).abs().max().item() <= 1e-3 * sc
+        assert err <= 1.5 * env + 1e-3 * sc, (i, err, env)
+        for k, ref_v in (("lx", float(d["lx"][i])), ("loss", float(d["loss"][i]))):
+            hip, em = o[k].item(), r[k]
+            s2 = max(1.0, abs(ref_v))
+            rec[f"step{i}_{k}"] = {"hip": hip, "reference": ref_v, "bf16_contract": em}
+            if i == 0:
+                assert abs(hip - em) <= 1e-3 * s2, (i, k, hip, em)
+            assert abs(hip - ref_v) <= 1.5 * abs(em - ref_v) + 1e-3 * s2, (i, k, hip, ref_v, em)
+        # pseudo-labels / masks on decidable rows (smoothed probs, fp32 vs bf16-contract spread)
+        p32, p16 = r32["probs"].double(), r["probs"].double()
+        envp = (p32 - p16).abs().max().item()
+        top2 = p32.topk(2, -1).values
+        ok = ((top2[:, 0] - top2[:, 1]) > 2 * envp + 1e-6).numpy()
+        okm = ((p32.max(-1).values - float(d["thres"])).abs() > 2 * envp + 1e-6).numpy()
+        np.testing.assert_array_equal(o["pseudo_label"].cpu().numpy()[ok], r32["pseudo_label"].numpy()[ok])
+        np.testing.assert_array_equal(o["mask"].cpu().numpy().astype(bool)[okm], r32["mask"].numpy().astype(bool)[okm])
+        rec[f"step{i}_decidable_rows"] = f"{int(ok.sum())}/{len(ok)} labels, {int(okm.sum())}/{len(okm)} masks"
+    # DA history and bank (fp32 reference fixture vs HIP, within the bf16 envelope of the inputs)
+    hist = torch.stack(tr.prob_list).cpu()
+    torch.testing.assert_close(hist, torch.tensor(d["prob_list"]), rtol=0, atol=5e-3)
+    assert tr.queue_ptr == int(d["queue_ptr"])
+    if tag == "open":
+        torch.testing.assert_close(tr.queue_feats.cpu(), torch.tensor(d["queue_feats"]), rtol=0, atol=2e-2)
+        torch.testing.assert_close(tr.queue_probs.cpu(), torch.tensor(d["queue_probs"]), rtol=0, atol=5e-3)
+    else:
+        assert torch.count_nonzero(tr.queue_feats) == 0
+    sd, esd = m.state_dict(), tr.ema_model.ema.state_dict()
+    worst, worst_e = 0.0, 0.0
+    for n in names:
+        if ("final/" + n) in d.files:
+            worst = max(worst, (sd[n].cpu() - torch.tensor(d["final/" + n])).abs().max().item())
+            worst_e = max(worst_e, (esd[n].cpu() - torch.tensor(d["ema/" + n])).abs().max().item())
+        else:
+            assert abs(sd[n].double().sum().item() - float(d["final_sum/" + n])) <= (2e-3 * steps + 1e-5) * sd[n].numel()
+    for n in ref.BN_BUFFERS:  # running stats follow the batch statistics of the (bf16-trunk) features
+        key = ("final/" + n) if ("final/" + n) in d.files else None
+        if n.endswith("num_batches_tracked"):
+            assert int(sd[n].item()) == steps
+        elif key:
+            torch.testing.assert_close(sd[n].cpu(), torch.tensor(d[key]), rtol=2e-2, atol=2e-3)
+    rec["max_param_delta"], rec["max_ema_delta"] = worst, worst_e
+    print(json.dumps(rec))
+    assert worst <= 2e-3 * steps + 1e-5
+    assert worst_e <= 1e-3 * 2e-3 * steps * (steps + 1) / 2 + 1e-6
