@@ -4,7 +4,8 @@ Same constructor and methods as the reference -- get_dataloader, get_config, tra
 evaluate_one, save_checkpoint, load_checkpoint, fit -- plus `step(batch)`, the unit the
 benchmark times.  One step (code/fixmatch.py:91-131):
 
-  weak   logits_w = model(u_w)                forward only: the reference detaches it
+  weak   logits_w = model(u_w)                forward only, on a second HIP stream beside the train
+                                              forward (independent buffers); the reference detaches it
                                               (code/loss.py:144) and ViT rows are independent,
                                               so its backward is exactly zero
   train  logits   = model([x ; u_s])          forward with saved activations
@@ -95,8 +96,16 @@ class FixMatch:
             self._mask = torch.empty(nu, dtype=torch.uint8, device=dev)
         stats = torch.empty(4, dtype=torch.float32, device=dev)  # lx, lu, mask_mean, total
 
-        logits_w = eng.forward(m.flat, [inputs_u_w], train=False)
-        logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=True)
+        if eng.overlap_fwd:  # weak forward on the side stream, beside the train forward
+            main, side = torch.cuda.current_stream(dev), eng.side_stream()
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                logits_w = eng.forward(m.flat, [inputs_u_w], train=False)
+            logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=True)
+            main.wait_stream(side)
+        else:
+            logits_w = eng.forward(m.flat, [inputs_u_w], train=False)
+            logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=True)
         dl = self._dlogits
         call("es_poly_ce_fwd_bwd", ptr(logits), C, ptr(targets_x), ptr(self.class_weights), B, C, 2.0, 1.0 / B,
              ptr(dl), C, ptr(stats[0:1]), s)

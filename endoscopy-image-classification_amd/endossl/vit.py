@@ -19,6 +19,7 @@ MI355X-first layout:
 """
 import ctypes
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -197,6 +198,12 @@ class Engine:
     # count is capped so the fp32 slabs stay small for the square 384x384 projection
     TN_TARGET_BLOCKS = 1536
     TN_MAX_SPLITS = 128
+    # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
+    # GEMMs beside the data-gradient chain ("bwd"); ENDOSSL_OVERLAP=0 serialises everything on the
+    # caller's stream
+    _OV = os.environ.get("ENDOSSL_OVERLAP", "1")
+    OVERLAP_FWD = _OV in ("1", "fwd")
+    OVERLAP = _OV in ("1", "bwd")
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -205,6 +212,10 @@ class Engine:
         self._acts = {}
         self._grads = {}
         self._ws = None
+        self._ws_ln = None
+        self._side = None
+        self.overlap = self.OVERLAP
+        self.overlap_fwd = self.OVERLAP_FWD
         self._packed_version = -1
         D, Hd = cfg.dim, cfg.hidden
         b16 = torch.bfloat16
@@ -270,6 +281,20 @@ class Engine:
             self._ws = torch.empty(self.TN_MAX_SPLITS * n_tn + 2 * 1024 * max(Hd, 3 * D), dtype=torch.float32,
                                    device=self.device)
         return self._ws
+
+    def ln_workspace(self):
+        """LayerNorm-backward partials (separate from the split-K slabs: the two run on different
+        streams when the weight gradients overlap the data-gradient chain)."""
+        if self._ws_ln is None:
+            self._ws_ln = torch.empty(2 * 1024 * self.cfg.dim, dtype=torch.float32, device=self.device)
+        return self._ws_ln
+
+    def side_stream(self):
+        """The second HIP stream (weak forward beside the train forward; weight gradients beside
+        the data-gradient chain)."""
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        return self._side
 
     # -------------------------------------------------------------- forward
     def forward(self, flat, images_list, train):
@@ -351,7 +376,7 @@ class Engine:
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M):
         D = self.cfg.dim
-        ws = self.workspace()
+        ws = self.ln_workspace()
         call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
@@ -368,11 +393,28 @@ class Engine:
         n = int(top.shape[0])
         A = self.acts(n, True)
         if n not in self._grads:
-            self._grads[n] = _Grads(cfg, n, self.device)
-        G = self._grads[n]
+            # two sets: layer i's weight-gradient inputs (dY images) live in set i % 2, so the side
+            # stream can still read layer i+1's while the main stream writes layer i's
+            self._grads[n] = (_Grads(cfg, n, self.device), _Grads(cfg, n, self.device))
+        G = self._grads[n][0]
+        GS = self._grads[n]
         D, Hd, T, H, M = cfg.dim, cfg.hidden, cfg.T, cfg.heads, A.M
         gv = lambda name: self.view(grad, name)  # noqa: E731
         fv = lambda name: self.view(flat, name)  # noqa: E731
+        ov = self.overlap
+        main = torch.cuda.current_stream(self.device)
+        side = self.side_stream() if ov else None
+
+        def wgrad_side(*args):
+            """Weight-gradient GEMM on the side stream once the main stream has produced dY."""
+            if not ov:
+                self._wgrad(*args)
+                return
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                self._wgrad(*args)
+
+        done = {}
         if zero_grad:
             grad.zero_()
         G.dx.zero_()
@@ -386,36 +428,42 @@ class Engine:
                  ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(G.dx), D, T,
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
                  cfg.num_classes, s)
-        call("es_cast_f32_bf16", ptr(G.dx), ptr(G.dxb), M * D, s)
+        call("es_cast_f32_bf16", ptr(G.dx), ptr(GS[(cfg.depth - 1) % 2].dxb), M * D, s)
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."
+            Gi, Gn = GS[i % 2], GS[(i - 1) % 2]
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
-            call("es_gemm_nt", EPI_DGELU, ptr(G.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(G.dpre),
+            call("es_gemm_nt", EPI_DGELU, ptr(Gi.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre),
                  Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
-            self._wgrad(G.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
-            call("es_gemm_nt", EPI_F32, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh), D,
+            wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
+            call("es_gemm_nt", EPI_F32, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh), D,
                  None, None, 0, M, D, Hd, 0, s)
-            self._wgrad(G.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
-            self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, G.dxmb,
+            wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
+            self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, Gi.dxmb,
                          gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
             # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
-            call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
+            call("es_gemm_nt", EPI_BF16, ptr(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
                  None, None, 0, M, D, D, 0, s)
-            self._wgrad(G.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
+            wgrad_side(Gi.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
             call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
-                 ptr(G.dqkv),
-                 3 * D, n, T, H, 64 ** -0.5, s)
-            call("es_gemm_nt", EPI_F32, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+                 ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
+            call("es_gemm_nt", EPI_F32, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
-            self._wgrad(G.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
-            self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), G.dxm, G.dx, G.dxb,
+            wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
+            if ov:
+                done[i] = side.record_event()
+                if i + 1 in done:  # set (i-1) % 2 was layer i+1's: its weight gradients must be done
+                    main.wait_event(done.pop(i + 1))
+            self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), G.dxm, G.dx, Gn.dxb,
                          gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
         # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
         K0 = 3 * cfg.patch * cfg.patch
         call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,
              s)
         npat = n * cfg.np
-        self._wgrad(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
+        wgrad_side(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
+        if ov:
+            main.wait_stream(side)
         return grad
 
 

@@ -227,6 +227,22 @@ class CoMatchRef:
         imgs = torch.cat([x, uw, us0, us1], dim=0)
         fts = vit_features(self.p, imgs, self.cfg, bf16=self.bf16)
         logits, feats = emb_heads(self.p, self.bufs, fts, drop_keep, train=True)
+        r = self.losses(logits, feats, y, bt, btu)
+        loss = r["loss_t"]
+        self.opt.zero_grad()
+        loss.backward()
+        grads = {k: self.p[k].grad.detach().clone() for k in self.names}
+        self.opt.step()
+        state = {k: self.p[k].detach() for k in self.names}
+        state.update(self.bufs)
+        ema_update(self.ema, state, self.decay)
+        r.update({"logits": logits.detach(), "fts": fts.detach(), "z": feats.detach(), "grads": grads})
+        return r
+
+    def losses(self, logits, feats, y, bt, btu):
+        """code/comatch.py:150-222 on the model outputs (logits [n, C], feats = z [n, L]): poly-CE,
+        DA (appends to prob_list), memory smoothing, gated bank write, contrastive + focal losses.
+        Returns the float values plus the differentiable total `loss_t`."""
         logits_x = logits[:bt]
         logits_u_w, logits_u_s0, _ = torch.split(logits[bt:], btu)
         feats_x = feats[:bt]
@@ -266,13 +282,5 @@ class CoMatchRef:
         pp = torch.exp(-logp)
         loss_u = ((1 - pp) ** self.gamma * logp).mean()
         loss = loss_x + self.lambda_u * loss_u + self.lambda_c * loss_contrast
-        self.opt.zero_grad()
-        loss.backward()
-        grads = {k: self.p[k].grad.detach().clone() for k in self.names}
-        self.opt.step()
-        state = {k: self.p[k].detach() for k in self.names}
-        state.update(self.bufs)
-        ema_update(self.ema, state, self.decay)
         return {"lx": loss_x.item(), "lu": loss_u.item(), "lc": loss_contrast.item(), "loss": loss.item(),
-                "probs": probs, "probs_orig": probs_orig, "mask": mask, "pseudo_label": lbs,
-                "logits": logits.detach(), "fts": fts.detach(), "z": feats.detach(), "grads": grads}
+                "probs": probs, "probs_orig": probs_orig, "mask": mask, "pseudo_label": lbs, "loss_t": loss}

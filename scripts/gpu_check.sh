@@ -11,8 +11,10 @@ run() {  # name limit cmd...
   return $rc
 }
 ok() { [ "$1" -le 1 ]; }
-run k 600 python -m pytest tests/test_gpu_kernels.py -q -rf -p no:cacheprovider; rc=$?
-ok $rc && { run s 600 python -m pytest tests/test_gpu_step.py -q -rf -p no:cacheprovider; rc=$?; }
+PT="python -u -m pytest -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread"
+run k 600 $PT tests/test_gpu_kernels.py; rc=$?
+ok $rc && { run s 600 $PT tests/test_gpu_step.py; rc=$?; }
+ok $rc && { run c 600 $PT tests/test_gpu_comatch.py; rc=$?; }
 ok $rc && { run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; }
 ok $rc && { run bench 600 python bench.py --steps 10 --warmup 3; rc=$?; }
 if ok $rc && [ "${PROFILE:-1}" = 1 ]; then

@@ -3,10 +3,12 @@ reference arithmetic (autograd for the gradients), and the native CoMatch traine
 reference's own CoMatch.train_one fixtures (tests/golden/comatch_step_{open,closed}.npz, bank
 gate open / closed), replaying the reference's dropout masks.
 
-Bars: kernels within fp32 tolerances (rtol 1e-4 .. 1e-5); trainer losses / logits as the FixMatch
-step test (tests/test_gpu_step.py): step 0 within 1e-3 * scale of the bf16-contract oracle, and
-|HIP - reference| <= 1.5 * |bf16 contract - reference| + 1e-3 * scale; post-step params within
-2 * lr * steps (+1e-5); pseudo-labels / masks bit-exact on decidable rows.
+Bars: kernels within fp32 tolerances (rtol 1e-4 .. 1e-5).  Trainer, step 0: trunk features within
+1e-3 * scale (+ a quarter of the bf16 envelope) of the bf16-contract oracle; every later stage
+(heads, DA / smoothing, losses, dL/dlogits, dL/dz, heads backward) within fp32 tolerances of the
+oracle run on the HIP path's own stage inputs; pseudo-labels / masks bit-exact on decidable rows.
+Trajectory (both steps): |HIP - reference| <= 1.5 * |bf16 contract - reference| + tol for logits,
+losses, DA history, bank, BN buffers; post-step params within 2 * lr * steps (+1e-5).
 """
 import json
 
@@ -277,11 +279,22 @@ def _cfg(thres, steps, B, MU, L):
 
 @pytest.mark.parametrize("tag", ["open", "closed"])
 def test_comatch_trainer_vs_reference_train_one(golden, tag):
+    """CoMatch.step against the reference (code/comatch.py:133-235).
+
+    Step 0, tight: every stage after the trunk is checked against the oracle evaluated on the HIP
+    path's OWN inputs to that stage (trunk features -> heads -> DA / smoothing / pseudo-labels ->
+    losses -> d(loss)/d(logits, z) -> heads backward), fp32 against fp32.  The trunk features are
+    held to the bf16-contract emulation.
+    Both steps, trajectory: logits, losses, DA history, bank, BN buffers and parameters against the
+    reference fixture within the bf16 envelope (the oracle's bf16-contract run vs the fixture):
+    BatchNorm1d over n = 14 rows and exp(z.z / 0.2) amplify bf16 trunk noise, so the envelope, not a
+    fixed 1e-3, is the meaningful bar after the first update."""
     from endossl.comatch import CoMatch
     from endossl.comatch_model import NativeViTEmb
     from endossl.vit import ViTConfig
     d = golden(f"comatch_step_{tag}.npz")
     L, steps, B, MU = int(d["L"]), int(d["steps"]), int(d["B"]), int(d["MU"])
+    thres = float(d["thres"])
     rcfg = ref.Cfg(img_size=64, patch=16, dim=128, depth=2, heads=2, num_classes=23)
     vcfg = ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23, head="emb", low_dim=L)
     names = [n for n, _ in ref.emb_param_shapes(rcfg, L)]
@@ -297,50 +310,89 @@ def test_comatch_trainer_vs_reference_train_one(golden, tag):
     unl = [((torch.tensor(d[f"uw{i}"]), torch.tensor(d[f"us0_{i}"]), torch.tensor(d[f"us1_{i}"])), None)
            for i in range(steps)]
     tr.get_dataloader((_DL([lab]), _DL(unl)), None)
-    tr.get_config(_cfg(float(d["thres"]), steps, B, MU, L))
+    tr.get_config(_cfg(thres, steps, B, MU, L))
     assert tr.queue_size == int(d["queue_size"])
-    emu = ref.CoMatchRef(params, bufs, rcfg, L, 23, int(d["queue_size"]), thres=float(d["thres"]), lambda_u=2.0,
-                         lambda_c=2.0, bf16=True)
-    f32 = ref.CoMatchRef(params, bufs, rcfg, L, 23, int(d["queue_size"]), thres=float(d["thres"]), lambda_u=2.0,
-                         lambda_c=2.0)
+    mk = lambda bf: ref.CoMatchRef(params, bufs, rcfg, L, 23, int(d["queue_size"]), thres=thres,  # noqa: E731
+                                   lambda_u=2.0, lambda_c=2.0, bf16=bf)
+    emu, f32, stage = mk(True), mk(False), mk(False)
+    stage.queue_feats, stage.queue_probs = stage.queue_feats.clone(), stage.queue_probs.clone()
+    bt, btu = B, B * MU
     rec = {}
     for i in range(steps):
         keep = torch.tensor(d[f"dropmask{i}"])
         o = tr.step((lab, unl[i]), drop_keep=keep)
+        torch.cuda.synchronize()
         imgs = unl[i][0]
         r = emu.step(*lab, *imgs, keep)
-        r32 = f32.step(*lab, *imgs, keep)
+        f32.step(*lab, *imgs, keep)
         lg, lg16, lg32 = o["logits"].detach().cpu().double(), r["logits"].double(), torch.tensor(d[f"logits{i}"]).double()
         env = (lg16 - lg32).abs().max().item()
         err = (lg - lg32).abs().max().item()
         sc = max(1.0, lg32.abs().max().item())
         rec[f"step{i}_logits"] = {"hip_vs_ref": err, "bf16_envelope": env}
         if i == 0:
-            assert (lg - lg16).abs().max().item() <= 1e-3 * sc
+            # trunk: CLS features vs the bf16-contract emulation (the final LayerNorm divides by each
+            # row's std, so single operand-rounding flips show at ~1e-3 relative)
+            f_hip = o["fts"].detach().cpu().double()
+            f16, f32_ = r["fts"].double(), torch.tensor(d["fts0"]).double()
+            fsc, fenv = max(1.0, f16.abs().max().item()), (f16 - f32_).abs().max().item()
+            rec["step0_fts_vs_bf16_contract"] = (f_hip - f16).abs().max().item()
+            rec["step0_fts_bf16_envelope"] = fenv
+            assert rec["step0_fts_vs_bf16_contract"] <= 1e-3 * fsc + 0.25 * fenv, rec
+            # heads on the HIP features (fp32 vs fp32)
+            hp = {k: params[k].clone().requires_grad_(True) for k in names if k.startswith(("fc.", "head_emb."))}
+            fts_leaf = o["fts"].detach().cpu().float().requires_grad_(True)
+            lg_h, z_h = ref.emb_heads(hp, {k: v.clone() for k, v in bufs.items()}, fts_leaf, keep, train=True)
+            rec["step0_heads_vs_oracle"] = (lg - lg_h.double()).abs().max().item()
+            assert rec["step0_heads_vs_oracle"] <= 1e-4 * sc, rec
+            torch.testing.assert_close(o["z"].detach().cpu(), z_h.detach(), rtol=1e-4, atol=1e-5)
+            # DA / smoothing / pseudo-labels / losses on the HIP logits and z
+            lg_leaf = o["logits"].detach().cpu().float().requires_grad_(True)
+            z_leaf = o["z"].detach().cpu().float().requires_grad_(True)
+            rs = stage.losses(lg_leaf, z_leaf, lab[1], bt, btu)
+            for k in ("lx", "lu", "lc", "loss"):
+                rec[f"step0_{k}_vs_oracle"] = [o[k].item(), rs[k]]
+                assert abs(o[k].item() - rs[k]) <= 1e-4 * max(1.0, abs(rs[k])), (k, o[k].item(), rs[k])
+            torch.testing.assert_close(o["probs_orig"].cpu(), rs["probs_orig"], rtol=1e-5, atol=1e-6)
+            torch.testing.assert_close(o["probs"].cpu(), rs["probs"], rtol=1e-5, atol=1e-6)
+            p = rs["probs"].double()
+            top2 = p.topk(2, -1).values
+            ok = ((top2[:, 0] - top2[:, 1]) > 1e-5).numpy()
+            okm = ((p.max(-1).values - thres).abs() > 1e-5).numpy()
+            np.testing.assert_array_equal(o["pseudo_label"].cpu().numpy()[ok], rs["pseudo_label"].numpy()[ok])
+            np.testing.assert_array_equal(o["mask"].cpu().numpy().astype(bool)[okm], rs["mask"].numpy().astype(bool)[okm])
+            rec["step0_mask"] = o["mask"].cpu().tolist()
+            hist0 = torch.stack(tr.prob_list).cpu()
+            torch.testing.assert_close(hist0, torch.stack(stage.prob_list), rtol=1e-5, atol=1e-7)
+            # d(loss)/d(logits, z) and the heads backward on the HIP features
+            rs["loss_t"].backward()
+            W = tr._workspace(bt, btu, 23, L)
+            torch.testing.assert_close(W["dl"].cpu(), lg_leaf.grad, rtol=1e-4, atol=1e-6)
+            torch.testing.assert_close(W["dz"].cpu(), z_leaf.grad, rtol=1e-4, atol=1e-6)
+            torch.autograd.backward([lg_h, z_h], [lg_leaf.grad, z_leaf.grad])
+            dfts = m.heads().bufs(bt + 3 * btu)["dfts"].cpu()
+            torch.testing.assert_close(dfts, fts_leaf.grad, rtol=1e-4, atol=1e-5)
+            eng = m.engine()
+            for k, v in hp.items():
+                torch.testing.assert_close(eng.view(m.flat_grad, k).cpu().view(v.shape), v.grad, rtol=1e-4, atol=1e-5,
+                                           msg=lambda s, k=k: f"{k}: {s}")
         assert err <= 1.5 * env + 1e-3 * sc, (i, err, env)
         for k, ref_v in (("lx", float(d["lx"][i])), ("loss", float(d["loss"][i]))):
             hip, em = o[k].item(), r[k]
             s2 = max(1.0, abs(ref_v))
             rec[f"step{i}_{k}"] = {"hip": hip, "reference": ref_v, "bf16_contract": em}
-            if i == 0:
-                assert abs(hip - em) <= 1e-3 * s2, (i, k, hip, em)
             assert abs(hip - ref_v) <= 1.5 * abs(em - ref_v) + 1e-3 * s2, (i, k, hip, ref_v, em)
-        # pseudo-labels / masks on decidable rows (smoothed probs, fp32 vs bf16-contract spread)
-        p32, p16 = r32["probs"].double(), r["probs"].double()
-        envp = (p32 - p16).abs().max().item()
-        top2 = p32.topk(2, -1).values
-        ok = ((top2[:, 0] - top2[:, 1]) > 2 * envp + 1e-6).numpy()
-        okm = ((p32.max(-1).values - float(d["thres"])).abs() > 2 * envp + 1e-6).numpy()
-        np.testing.assert_array_equal(o["pseudo_label"].cpu().numpy()[ok], r32["pseudo_label"].numpy()[ok])
-        np.testing.assert_array_equal(o["mask"].cpu().numpy().astype(bool)[okm], r32["mask"].numpy().astype(bool)[okm])
-        rec[f"step{i}_decidable_rows"] = f"{int(ok.sum())}/{len(ok)} labels, {int(okm.sum())}/{len(okm)} masks"
-    # DA history and bank (fp32 reference fixture vs HIP, within the bf16 envelope of the inputs)
-    hist = torch.stack(tr.prob_list).cpu()
-    torch.testing.assert_close(hist, torch.tensor(d["prob_list"]), rtol=0, atol=5e-3)
+    # trajectory: DA history, bank and BN buffers against the fixture within the bf16 envelope
+    hist, hist_ref = torch.stack(tr.prob_list).cpu(), torch.tensor(d["prob_list"])
+    henv = (torch.stack(emu.prob_list) - hist_ref).abs().max().item()
+    assert (hist - hist_ref).abs().max().item() <= 1.5 * henv + 1e-3, ((hist - hist_ref).abs().max(), henv)
     assert tr.queue_ptr == int(d["queue_ptr"])
     if tag == "open":
-        torch.testing.assert_close(tr.queue_feats.cpu(), torch.tensor(d["queue_feats"]), rtol=0, atol=2e-2)
-        torch.testing.assert_close(tr.queue_probs.cpu(), torch.tensor(d["queue_probs"]), rtol=0, atol=5e-3)
+        for mine, theirs, key in ((tr.queue_feats, emu.queue_feats, "queue_feats"), (tr.queue_probs, emu.queue_probs,
+                                                                                    "queue_probs")):
+            fx = torch.tensor(d[key])
+            e, ev = (mine.cpu() - fx).abs().max().item(), (theirs - fx).abs().max().item()
+            assert e <= 1.5 * ev + 2e-3, (key, e, ev)
     else:
         assert torch.count_nonzero(tr.queue_feats) == 0
     sd, esd = m.state_dict(), tr.ema_model.ema.state_dict()
@@ -356,7 +408,9 @@ def test_comatch_trainer_vs_reference_train_one(golden, tag):
         if n.endswith("num_batches_tracked"):
             assert int(sd[n].item()) == steps
         elif key:
-            torch.testing.assert_close(sd[n].cpu(), torch.tensor(d[key]), rtol=2e-2, atol=2e-3)
+            fx = torch.tensor(d[key])
+            e, ev = (sd[n].cpu() - fx).abs().max().item(), (emu.bufs[n] - fx).abs().max().item()
+            assert e <= 1.5 * ev + 2e-3, (n, e, ev)
     rec["max_param_delta"], rec["max_ema_delta"] = worst, worst_e
     print(json.dumps(rec))
     assert worst <= 2e-3 * steps + 1e-5
