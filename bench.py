@@ -12,7 +12,8 @@ all-reduce + Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.
 
 Reported beside it:
   roofline      dominant kernel = the fc1 forward GEMM (gemm_nt, GELU epilogue), timed live with
-                HIP events on its launch stream over the timed steps.  Its binding roofline is HBM:
+                HIP events on its launch stream over the timed steps (where it shares the chip with the
+                weak forward on the second stream; "isolated" = the same launch with that stream off).  Its binding roofline is HBM:
                 698.4 MB algorithmic bytes per launch (A [M,384] bf16 read once + pre-activation and
                 activation [M,1536] bf16 written once) take 87 us at 8 TB/s, its 119 GFLOP 47 us at
                 the bf16 dense MFMA peak.  achieved = algorithmic bytes / mean launch time; the MFMA
@@ -155,6 +156,20 @@ def main():
     T = elapsed.item()
     loss = out["loss"].item()
 
+    # the same launches with the second stream off (untimed, after the timed region): the kernel's
+    # duration when it has the chip to itself, reported beside the live (co-scheduled) figure
+    eng = model.engine()
+    ov = (eng.overlap, eng.overlap_fwd)
+    eng.overlap = eng.overlap_fwd = False
+    iso = {"label": "fc1_fwd", "events": []}
+    eng.probe = iso
+    for _ in range(2):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    eng.probe = None
+    eng.overlap, eng.overlap_fwd = ov
+    iso_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / len(iso["events"])
+
     ev_ms = [e0.elapsed_time(e1) for e0, e1, _ in probe["events"]]
     flops = [f for _, _, f in probe["events"]]
     mean_ms = sum(ev_ms) / len(ev_ms)
@@ -188,7 +203,13 @@ def main():
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes": alg_bytes, "mean_launch_ms": round(mean_ms, 4),
                          "launches": len(ev_ms), "mfma_tflops": round(tflops, 1),
-                         "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4)},
+                         "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+                         "streams": 2 if ov[1] else 1,
+                         "isolated": {"mean_launch_ms": round(iso_ms, 4),
+                                      "achieved": round(alg_bytes / (iso_ms / 1e3) / 1e9, 1),
+                                      "frac": round(alg_bytes / (iso_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+                                      "note": "same launch with the second HIP stream off (2 untimed steps); the "
+                                              "live figure above shares the CUs with the weak-forward stream"}},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline()
