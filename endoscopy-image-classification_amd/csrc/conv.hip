@@ -1,0 +1,900 @@
+// CNN-branch kernels of the Conformer (SemiFormer's backbone):
+// code/models/conformer.py:75-445 -- ConvBlock / Med_ConvBlock / FCUDown / FCUUp / stem.
+//
+//  es_conv2d_fwd / _bwd_data / _bwd_weight   Conv2d (groups = 1) as an fp32 implicit GEMM over
+//                                            NHWC maps with element strides (so the first conv
+//                                            reads the NCHW images and the FCU convs read / write
+//                                            token rows of the transformer buffer directly)
+//  es_chan_sum                               per-channel sums (bias gradients)
+//  es_bn2d_fwd / es_bn2d_bwd                 BatchNorm2d (train: batch statistics + running
+//                                            update; eval: running statistics), fused residual
+//                                            add and ReLU (ConvBlock's bn3 + residual + act3)
+//  es_maxpool2d_fwd / _bwd                   MaxPool2d(k, s, p), first maximum wins (torch CPU)
+//  es_avgpool2d_fwd / _bwd                   AvgPool2d(k, k) (FCUDown) and AdaptiveAvgPool2d(1)
+//  es_upsample_add_fwd / _bwd                x + interpolate(x_t, nearest, x s) (FCUUp -> conv2)
+//  es_fcu_down_tokens_fwd / _bwd             FCUDown's LayerNorm + GELU + cat(cls) and the
+//                                            `x_st + x_t` of ConvTransBlock.forward (:345-346)
+//  es_tokens_cls_set                         x_t[:, 0] = cls_token (Conformer.forward :422-429)
+//
+// MI355X notes: the CNN branch of Conformer-Ti is ~0.7 GMAC per image against the transformer
+// branch's ~4.6, and its tensors are small-channel (16..256) maps, so these kernels are fp32 SIMT
+// implicit GEMMs (64x64 / 128x32 / 256x16 output tiles, 4x4 per thread, 16-deep K steps staged
+// through LDS) -- no bf16 rounding on the BatchNorm-coupled CNN path (BatchNorm over the whole
+// batch amplifies operand noise, the same effect as CoMatch's BatchNorm1d head).
+#include "common.h"
+
+namespace {
+
+struct ConvGeom {
+  int N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad;
+  long sxn, sxh, sxw, sxc;  // input element strides (n, h, w, c)
+  long syn, syh, syw;       // output strides (channel stride 1)
+};
+
+constexpr int CBK = 16;
+
+// ---- forward: y[n,ho,wo,co] = bias[co] + sum_{ky,kx,ci} x[n, ho*s-p+ky, wo*s-p+kx, ci] w[co,ci,ky,kx]
+// GEMM rows m = (n, ho, wo), cols co, K = (ky, kx, ci) (ci fastest: NHWC-contiguous gathers).
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, float* __restrict__ y,
+                                                       ConvGeom g, int accumulate) {
+  constexpr int TX = BN / 4, TM = BM * BN / 1024;
+  __shared__ float As[CBK][BM + 1];
+  __shared__ float Bs[CBK][BN + 4];
+  const int M = g.N * g.Ho * g.Wo, K = g.kh * g.kw * g.Cin, KK = g.kh * g.kw;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+  float acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += CBK) {
+    for (int e = tid; e < BM * CBK; e += 256) {
+      const int mi = e / CBK, ki = e % CBK, m = m0 + mi, k = k0 + ki;
+      float v = 0.f;
+      if (m < M && k < K) {
+        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
+        const int ci = k % g.Cin, t2 = k / g.Cin, kx = t2 % g.kw, ky = t2 / g.kw;
+        const int h = ho * g.stride - g.pad + ky, ww = wo * g.stride - g.pad + kx;
+        if (h >= 0 && h < g.H && ww >= 0 && ww < g.W) v = x[n * g.sxn + h * g.sxh + ww * g.sxw + ci * g.sxc];
+      }
+      As[ki][mi] = v;
+    }
+    for (int e = tid; e < CBK * BN; e += 256) {
+      const int ki = e / BN, ni = e % BN, k = k0 + ki, co = n0 + ni;
+      float v = 0.f;
+      if (k < K && co < g.Cout) {
+        const int ci = k % g.Cin, t2 = k / g.Cin;  // t2 = ky*kw + kx
+        v = w[((long)co * g.Cin + ci) * KK + t2];
+      }
+      Bs[ki][ni] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) {
+      float a[TM], b[4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[kk][ty * TM + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + ty * TM + i;
+    if (m >= M) continue;
+    const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
+    float* yr = y + n * g.syn + ho * g.syh + wo * g.syw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = n0 + tx * 4 + j;
+      if (co < g.Cout) {
+        const float v = acc[i][j] + (bias ? bias[co] : 0.f);
+        yr[co] = accumulate ? yr[co] + v : v;
+      }
+    }
+  }
+}
+
+// ---- data gradient: dx[n,h,w,ci] (+)= sum_{ky,kx,co} dy[n,ho,wo,co] w[co,ci,ky,kx],
+// ho = (h + p - ky) / s when divisible and in range.  Rows m = (n, h, w), cols ci, K = (ky, kx, co).
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_dx_kernel(const float* __restrict__ dy, const float* __restrict__ w,
+                                                      float* __restrict__ dx, ConvGeom g, int accumulate) {
+  constexpr int TX = BN / 4, TM = BM * BN / 1024;
+  __shared__ float As[CBK][BM + 1];
+  __shared__ float Bs[CBK][BN + 4];
+  const int M = g.N * g.H * g.W, K = g.kh * g.kw * g.Cout, KK = g.kh * g.kw;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+  float acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += CBK) {
+    for (int e = tid; e < BM * CBK; e += 256) {
+      const int mi = e / CBK, ki = e % CBK, m = m0 + mi, k = k0 + ki;
+      float v = 0.f;
+      if (m < M && k < K) {
+        const int ww = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
+        const int co = k % g.Cout, t2 = k / g.Cout, kx = t2 % g.kw, ky = t2 / g.kw;
+        const int hn = h + g.pad - ky, wn = ww + g.pad - kx;
+        if (hn >= 0 && wn >= 0 && hn % g.stride == 0 && wn % g.stride == 0) {
+          const int ho = hn / g.stride, wo = wn / g.stride;
+          if (ho < g.Ho && wo < g.Wo) v = dy[n * g.syn + ho * g.syh + wo * g.syw + co];
+        }
+      }
+      As[ki][mi] = v;
+    }
+    for (int e = tid; e < CBK * BN; e += 256) {
+      const int ki = e / BN, ni = e % BN, k = k0 + ki, ci = n0 + ni;
+      float v = 0.f;
+      if (k < K && ci < g.Cin) {
+        const int co = k % g.Cout, t2 = k / g.Cout;
+        v = w[((long)co * g.Cin + ci) * KK + t2];
+      }
+      Bs[ki][ni] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) {
+      float a[TM], b[4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[kk][ty * TM + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + ty * TM + i;
+    if (m >= M) continue;
+    const int ww = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
+    float* xr = dx + n * g.sxn + h * g.sxh + ww * g.sxw;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ci = n0 + tx * 4 + j;
+      if (ci < g.Cin) {
+        float* p = xr + ci * g.sxc;
+        *p = accumulate ? *p + acc[i][j] : acc[i][j];
+      }
+    }
+  }
+}
+
+// ---- weight gradient partials: P[split][co][k'] = sum_{m in split} dy[m, co] A[m, k'],
+// k' = (ci, ky, kx) (the weight's own layout), A = im2col(x).  Rows co, cols k', reduction over the
+// output pixels m of this split (16 per step).
+template <int BM, int BN>
+__global__ __launch_bounds__(256) void conv_dw_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                      float* __restrict__ P, ConvGeom g, int mchunk) {
+  constexpr int TX = BN / 4, TM = BM * BN / 1024;
+  __shared__ float As[CBK][BM + 1];  // dy^T  [m][co]
+  __shared__ float Bs[CBK][BN + 4];  // im2col [m][k']
+  const int M = g.N * g.Ho * g.Wo, KK = g.kh * g.kw, K = g.Cin * KK;
+  const int c0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = blockIdx.z;
+  const int mb = split * mchunk, me = min(mb + mchunk, M);
+  const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+  float acc[TM][4];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+  for (int mm = mb; mm < me; mm += CBK) {
+    for (int e = tid; e < BM * CBK; e += 256) {
+      const int mi = e / BM, ci = e % BM, m = mm + mi, co = c0 + ci;  // co fastest: contiguous dy
+      float v = 0.f;
+      if (m < me && co < g.Cout) {
+        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
+        v = dy[n * g.syn + ho * g.syh + wo * g.syw + co];
+      }
+      As[mi][ci] = v;
+    }
+    for (int e = tid; e < CBK * BN; e += 256) {
+      const int mi = e / BN, ni = e % BN, m = mm + mi, k = n0 + ni;
+      float v = 0.f;
+      if (m < me && k < K) {
+        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
+        const int ci = k / KK, t2 = k % KK, kx = t2 % g.kw, ky = t2 / g.kw;
+        const int h = ho * g.stride - g.pad + ky, ww = wo * g.stride - g.pad + kx;
+        if (h >= 0 && h < g.H && ww >= 0 && ww < g.W) v = x[n * g.sxn + h * g.sxh + ww * g.sxw + ci * g.sxc];
+      }
+      Bs[mi][ni] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < CBK; ++kk) {
+      float a[TM], b[4];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[kk][ty * TM + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[j] = Bs[kk][tx * 4 + j];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  float* out = P + (long)split * g.Cout * K;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int co = c0 + ty * TM + i;
+    if (co >= g.Cout) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = n0 + tx * 4 + j;
+      if (k < K) out[(long)co * K + k] = acc[i][j];
+    }
+  }
+}
+
+// out[i] (+)= sum_s P[s][i]
+__global__ void sum_slabs_kernel(const float* __restrict__ P, float* __restrict__ out, int S, long n, int accumulate) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float s0 = 0.f, s1 = 0.f;
+    int k = 0;
+    for (; k + 2 <= S; k += 2) {
+      s0 += P[(long)k * n + i];
+      s1 += P[(long)(k + 1) * n + i];
+    }
+    if (k < S) s0 += P[(long)k * n + i];
+    const float v = s0 + s1;
+    out[i] = accumulate ? out[i] + v : v;
+  }
+}
+
+// ---- per-channel reductions over the rows of a [rows, C] view: row r at (r / HW) * sn + (r % HW) * sp.
+// One workgroup per row chunk writes partial[block][c]; a second pass sums the blocks.
+struct RowMap {
+  long sn, sp;
+  int HW;
+};
+__device__ __forceinline__ long row_off(const RowMap& rm, int r) { return (long)(r / rm.HW) * rm.sn + (long)(r % rm.HW) * rm.sp; }
+
+// MODE 0: sum v;  MODE 1: sum (v - mean[c])^2;  MODE 2: sum g, sum g * xhat  (g = dy * [y > 0 if relu],
+// xhat = (x - mean) * rstd), written as partial[block][c] and partial[block][C + c]
+template <int MODE>
+__global__ __launch_bounds__(256) void chan_partial_kernel(const float* __restrict__ v, RowMap rm, int rows, int C,
+                                                           int rows_per, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, const float* __restrict__ dy,
+                                                           const float* __restrict__ y, int relu,
+                                                           float* __restrict__ partial) {
+  __shared__ float red[256];
+  __shared__ float red2[256];
+  const int cpp = C < 256 ? C : 256;  // columns per pass
+  const int rp = 256 / cpp;           // row lanes
+  const int t = threadIdx.x, cc = t % cpp, rl = t / cpp;
+  const int r0 = blockIdx.x * rows_per, r1 = min(r0 + rows_per, rows);
+  for (int c0 = 0; c0 < C; c0 += cpp) {
+    const int c = c0 + cc;
+    float s = 0.f, s2 = 0.f;
+    if (rl < rp && c < C) {
+      const float mu = (MODE >= 1) ? mean[c] : 0.f;
+      const float rs = (MODE == 2) ? rstd[c] : 0.f;
+      for (int r = r0 + rl; r < r1; r += rp) {
+        const long o = row_off(rm, r) + c;
+        if (MODE == 0) {
+          s += v[o];
+        } else if (MODE == 1) {
+          const float d = v[o] - mu;
+          s = fmaf(d, d, s);
+        } else {
+          float gg = dy[o];
+          if (relu && !(y[o] > 0.f)) gg = 0.f;
+          s += gg;
+          s2 = fmaf(gg, (v[o] - mu) * rs, s2);
+        }
+      }
+    }
+    red[t] = s;
+    red2[t] = s2;
+    __syncthreads();
+    if (t < cpp && c0 + t < C) {
+      float a = 0.f, b = 0.f;
+      for (int j = 0; j < rp; ++j) {
+        a += red[j * cpp + t];
+        b += red2[j * cpp + t];
+      }
+      partial[(long)blockIdx.x * (MODE == 2 ? 2 * C : C) + c0 + t] = a;
+      if (MODE == 2) partial[(long)blockIdx.x * 2 * C + C + c0 + t] = b;
+    }
+    __syncthreads();
+  }
+}
+
+// BatchNorm statistics from the partials: mean (MODE 0 result / rows) and, after the second pass,
+// rstd = 1/sqrt(var_biased + eps); running stats <- (1-m) r + m (mean, var_unbiased)  (nn.BatchNorm2d)
+__global__ void bn_mean_kernel(const float* __restrict__ partial, int G, int C, int rows, float* __restrict__ mean) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int gI = 0; gI < G; ++gI) s += partial[(long)gI * C + c];
+  mean[c] = s / (float)rows;
+}
+__global__ void bn_var_kernel(const float* __restrict__ partial, int G, int C, int rows, float eps,
+                              const float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ run_mean,
+                              float* __restrict__ run_var, float momentum) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int gI = 0; gI < G; ++gI) s += partial[(long)gI * C + c];
+  const float var = s / (float)rows;
+  rstd[c] = 1.0f / sqrtf(var + eps);
+  if (run_mean) {
+    const float unb = rows > 1 ? s / (float)(rows - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean[c];
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+__global__ void nbt_inc_kernel(int64_t* nbt) { *nbt += 1; }
+
+// y = (x - mean) * rstd * gamma + beta (+ res) (relu); eval: rstd from the running variance
+__global__ void bn_apply_kernel(const float* __restrict__ x, long n, int C, const float* __restrict__ mean,
+                                const float* __restrict__ rstd, const float* __restrict__ rvar, float eps,
+                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                const float* __restrict__ res, int relu, float* __restrict__ y) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const float rs = rvar ? 1.0f / sqrtf(rvar[c] + eps) : rstd[c];
+    float v = (x[i] - mean[c]) * rs * gamma[c] + beta[c];
+    if (res) v += res[i];
+    if (relu) v = fmaxf(v, 0.f);
+    y[i] = v;
+  }
+}
+
+// dx = rstd * gamma * (g - sum(g)/P - xhat * sum(g xhat)/P); g = dy [* (y > 0)] (written to gout
+// when given: the residual branch's gradient)
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                    const float* __restrict__ y, int relu, long n, int C, int rows,
+                                    const float* __restrict__ mean, const float* __restrict__ rstd,
+                                    const float* __restrict__ gamma, const float* __restrict__ sums,
+                                    float* __restrict__ dx, float* __restrict__ gout) {
+  const float inv = 1.0f / (float)rows;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float gg = dy[i];
+    if (relu && !(y[i] > 0.f)) gg = 0.f;
+    if (gout) gout[i] = gg;
+    const float xh = (x[i] - mean[c]) * rstd[c];
+    dx[i] = rstd[c] * gamma[c] * (gg - sums[c] * inv - xh * sums[C + c] * inv);
+  }
+}
+
+// eval-mode BatchNorm backward is an affine map: dx = g * gamma * rstd_running (not on the training
+// path; kept for completeness of the autograd surface)
+__global__ void bn_bwd_eval_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu, long n, int C,
+                                   const float* __restrict__ rvar, float eps, const float* __restrict__ gamma,
+                                   float* __restrict__ dx, float* __restrict__ gout) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    float gg = dy[i];
+    if (relu && !(y[i] > 0.f)) gg = 0.f;
+    if (gout) gout[i] = gg;
+    dx[i] = gg * gamma[c] / sqrtf(rvar[c] + eps);
+  }
+}
+
+// ---- pooling / upsampling (NHWC contiguous)
+__global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int k, int s, int p,
+                                   int Ho, int Wo, float* __restrict__ y, int8_t* __restrict__ arg) {
+  const long n_out = (long)N * Ho * Wo * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho), n = (int)(t / Ho);
+    float best = -INFINITY;
+    int bi = 0;
+    for (int ky = 0; ky < k; ++ky) {
+      const int h = ho * s - p + ky;
+      if (h < 0 || h >= H) continue;
+      for (int kx = 0; kx < k; ++kx) {
+        const int w = wo * s - p + kx;
+        if (w < 0 || w >= W) continue;
+        const float v = x[(((long)n * H + h) * W + w) * C + c];
+        if (v > best || isnan(v)) {
+          best = v;
+          bi = ky * k + kx;
+          if (isnan(v)) break;
+        }
+      }
+    }
+    y[i] = best;
+    arg[i] = (int8_t)bi;
+  }
+}
+
+__global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int8_t* __restrict__ arg, int N, int H, int W,
+                                   int C, int k, int s, int p, int Ho, int Wo, float* __restrict__ dx) {
+  const long n_in = (long)N * H * W * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H), n = (int)(t / H);
+    float acc = 0.f;
+    const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
+    const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
+    for (int ho = ho_lo; ho <= ho_hi; ++ho) {
+      const int ky = h + p - ho * s;
+      if (ky < 0 || ky >= k) continue;
+      for (int wo = wo_lo; wo <= wo_hi; ++wo) {
+        const int kx = w + p - wo * s;
+        if (kx < 0 || kx >= k) continue;
+        const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+        if (arg[o] == ky * k + kx) acc += dy[o];
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
+// AvgPool2d(k, stride k) / AdaptiveAvgPool2d(1) (k = H = W): y[n,ho,wo,c] = mean of the k x k block
+__global__ void avgpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int k, int Ho, int Wo,
+                                   float* __restrict__ y) {
+  const long n_out = (long)N * Ho * Wo * C;
+  const float inv = 1.0f / (float)(k * k);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int wo = (int)(t % Wo);
+    t /= Wo;
+    const int ho = (int)(t % Ho), n = (int)(t / Ho);
+    float s = 0.f;
+    for (int ky = 0; ky < k; ++ky)
+      for (int kx = 0; kx < k; ++kx) s += x[(((long)n * H + ho * k + ky) * W + wo * k + kx) * C + c];
+    y[i] = s * inv;
+  }
+}
+__global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int H, int W, int C, int k, int Ho, int Wo,
+                                   float* __restrict__ dx, int accumulate) {
+  const long n_in = (long)N * H * W * C;
+  const float inv = 1.0f / (float)(k * k);
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H), n = (int)(t / H);
+    const float v = dy[(((long)n * Ho + h / k) * Wo + w / k) * C + c] * inv;
+    dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+// out = base + nearest-upsample(src, x s)
+__global__ void upsample_add_fwd_kernel(const float* __restrict__ base, const float* __restrict__ src, int N, int H,
+                                        int W, int C, int s, float* __restrict__ out) {
+  const int h2 = H / s, w2 = W / s;
+  const long n = (long)N * H * W * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int w = (int)(t % W);
+    t /= W;
+    const int h = (int)(t % H), nn = (int)(t / H);
+    out[i] = base[i] + src[(((long)nn * h2 + h / s) * w2 + w / s) * C + c];
+  }
+}
+// dsrc[n, hs, ws, c] = sum of dout over the s x s block
+__global__ void upsample_bwd_kernel(const float* __restrict__ dout, int N, int H, int W, int C, int s,
+                                    float* __restrict__ dsrc) {
+  const int h2 = H / s, w2 = W / s;
+  const long n = (long)N * h2 * w2 * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    long t = i / C;
+    const int ws = (int)(t % w2);
+    t /= w2;
+    const int hs = (int)(t % h2), nn = (int)(t / h2);
+    float a = 0.f;
+    for (int dy = 0; dy < s; ++dy)
+      for (int dx = 0; dx < s; ++dx) a += dout[(((long)nn * H + hs * s + dy) * W + ws * s + dx) * C + c];
+    dsrc[i] = a;
+  }
+}
+
+// ---- FCUDown tokens: out[n][0] = 2 x_t[n][0]; out[n][1+p] = gelu(LN(pooled[n][p])) + x_t[n][1+p]
+// (the `x_st + x_t` of ConvTransBlock: x_st's cls row is x_t[:, 0] itself, code/models/conformer.py
+// :176-177,345).  One wave per row, D <= 1024; saves mean / rstd per row.
+__global__ __launch_bounds__(256) void fcu_down_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ xt,
+                                                           const float* __restrict__ gam, const float* __restrict__ bet,
+                                                           float* __restrict__ out, float* __restrict__ mean,
+                                                           float* __restrict__ rstd, int N, int np, int D, float eps) {
+  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const int T = np + 1;
+  if (wv >= N * T) return;
+  const int n = wv / T, tk = wv % T;
+  const float* xr = xt + (long)wv * D;
+  float* orow = out + (long)wv * D;
+  if (tk == 0) {
+    for (int c = lane; c < D; c += 64) orow[c] = 2.f * xr[c];
+    return;
+  }
+  const float* pr = pooled + ((long)n * np + tk - 1) * D;
+  float s = 0.f;
+  for (int c = lane; c < D; c += 64) s += pr[c];
+  const float mu = warp_sum(s) / (float)D;
+  float q = 0.f;
+  for (int c = lane; c < D; c += 64) {
+    const float d = pr[c] - mu;
+    q = fmaf(d, d, q);
+  }
+  const float rs = 1.0f / sqrtf(warp_sum(q) / (float)D + eps);
+  if (lane == 0) {
+    mean[(long)n * np + tk - 1] = mu;
+    rstd[(long)n * np + tk - 1] = rs;
+  }
+  for (int c = lane; c < D; c += 64) {
+    const float z = (pr[c] - mu) * rs * gam[c] + bet[c];
+    orow[c] = 0.5f * z * (1.0f + erff(z * 0.70710678118654752f)) + xr[c];
+  }
+}
+
+// backward: dxt = dout (cls row doubled); dpooled = LN backward of dout * gelu'(z); per-block
+// partial gamma / beta gradients partial[block][0..D) / [D..2D)
+__global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ pooled,
+                                                           const float* __restrict__ gam, const float* __restrict__ bet,
+                                                           const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                           float* __restrict__ dxt, float* __restrict__ dpooled,
+                                                           float* __restrict__ partial, int N, int np, int D,
+                                                           int rows_per_block) {
+  extern __shared__ float pg[];  // [2 * D] per block
+  const int T = np + 1, wv_in_blk = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) pg[c] = 0.f;
+  __syncthreads();
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(r0 + rows_per_block, N * T);
+  for (int row = r0 + wv_in_blk; row < r1; row += 4) {
+    const int n = row / T, tk = row % T;
+    const float* dr = dout + (long)row * D;
+    float* xr = dxt + (long)row * D;
+    if (tk == 0) {
+      for (int c = lane; c < D; c += 64) xr[c] = 2.f * dr[c];
+      continue;
+    }
+    for (int c = lane; c < D; c += 64) xr[c] = dr[c];
+    const long pi = (long)n * np + tk - 1;
+    const float* pr = pooled + pi * D;
+    const float mu = mean[pi], rs = rstd[pi];
+    float s1 = 0.f, s2 = 0.f;
+    for (int c = lane; c < D; c += 64) {
+      const float xh = (pr[c] - mu) * rs;
+      const float z = xh * gam[c] + bet[c];
+      const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+      const float gz = dr[c] * fmaf(z, 0.39894228040143268f * __expf(-0.5f * z * z), cdf);
+      atomicAdd(&pg[c], gz * xh);  // LDS atomics: 4 waves per block share the partial row
+      atomicAdd(&pg[D + c], gz);
+      const float gx = gz * gam[c];
+      s1 += gx;
+      s2 = fmaf(gx, xh, s2);
+    }
+    s1 = warp_sum(s1) / (float)D;
+    s2 = warp_sum(s2) / (float)D;
+    float* dp = dpooled + pi * D;
+    for (int c = lane; c < D; c += 64) {
+      const float xh = (pr[c] - mu) * rs;
+      const float z = xh * gam[c] + bet[c];
+      const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+      const float gz = dr[c] * fmaf(z, 0.39894228040143268f * __expf(-0.5f * z * z), cdf);
+      dp[c] = rs * (gz * gam[c] - s1 - xh * s2);
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) partial[(long)blockIdx.x * 2 * D + c] = pg[c];
+}
+
+__global__ void fcu_param_reduce_kernel(const float* __restrict__ partial, int G, int D, float* __restrict__ dw,
+                                        float* __restrict__ db, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * D) return;
+  float s = 0.f;
+  for (int gI = 0; gI < G; ++gI) s += partial[(long)gI * 2 * D + c];
+  float* o = c < D ? dw + c : db + (c - D);
+  *o = accumulate ? *o + s : s;
+}
+
+__global__ void tokens_cls_set_kernel(float* __restrict__ xt, int N, int T, int D, const float* __restrict__ cls) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)N * D) return;
+  const int n = (int)(i / D), c = (int)(i % D);
+  xt[(long)n * T * D + c] = cls[c];
+}
+
+inline int grid1d(long n) {
+  long b = (n + 255) / 256;
+  return (int)(b > 16384 ? 16384 : (b < 1 ? 1 : b));
+}
+
+ConvGeom make_geom(int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc, int Cout, int kh, int kw,
+                   int stride, int pad, long syn, long syh, long syw) {
+  ConvGeom g;
+  g.N = N; g.H = H; g.W = W; g.Cin = Cin; g.Cout = Cout; g.kh = kh; g.kw = kw; g.stride = stride; g.pad = pad;
+  g.Ho = (H + 2 * pad - kh) / stride + 1;
+  g.Wo = (W + 2 * pad - kw) / stride + 1;
+  g.sxn = sxn; g.sxh = sxh; g.sxw = sxw; g.sxc = sxc;
+  g.syn = syn; g.syh = syh; g.syw = syw;
+  return g;
+}
+
+bool geom_ok(const ConvGeom& g) {
+  return g.N > 0 && g.H > 0 && g.W > 0 && g.Cin > 0 && g.Cout > 0 && g.kh > 0 && g.kw > 0 && g.stride > 0 &&
+         g.pad >= 0 && g.Ho > 0 && g.Wo > 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// y[n, ho, wo, co] (+)= conv(x)  (Conv2d, groups = 1).  x at element strides (sxn, sxh, sxw, sxc),
+// y at (syn, syh, syw) with channel stride 1.  Ho = (H + 2p - kh) / s + 1.
+int es_conv2d_fwd(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                  const float* w, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y, long syn,
+                  long syh, long syw, int accumulate, hipStream_t stream) {
+  if (!x || !w || !y) return ES_BAD_ARG;
+  const ConvGeom g = make_geom(N, H, W, Cin, sxn, sxh, sxw, sxc, Cout, kh, kw, stride, pad, syn, syh, syw);
+  if (!geom_ok(g)) return ES_BAD_SHAPE;
+  const int M = N * g.Ho * g.Wo;
+  if (Cout <= 16) {
+    hipLaunchKernelGGL((conv_fwd_kernel<256, 16>), dim3((M + 255) / 256, (Cout + 15) / 16), 256, 0, stream, x, w, bias,
+                       y, g, accumulate);
+  } else if (Cout <= 32) {
+    hipLaunchKernelGGL((conv_fwd_kernel<128, 32>), dim3((M + 127) / 128, (Cout + 31) / 32), 256, 0, stream, x, w, bias,
+                       y, g, accumulate);
+  } else {
+    hipLaunchKernelGGL((conv_fwd_kernel<64, 64>), dim3((M + 63) / 64, (Cout + 63) / 64), 256, 0, stream, x, w, bias, y,
+                       g, accumulate);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// dx (+)= conv^T(dy): the data gradient, written at dx's element strides (sxn, sxh, sxw, sxc)
+int es_conv2d_bwd_data(const float* dy, long syn, long syh, long syw, const float* w, int N, int H, int W, int Cin,
+                       int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh, long sxw, long sxc,
+                       int accumulate, hipStream_t stream) {
+  if (!dy || !w || !dx) return ES_BAD_ARG;
+  const ConvGeom g = make_geom(N, H, W, Cin, sxn, sxh, sxw, sxc, Cout, kh, kw, stride, pad, syn, syh, syw);
+  if (!geom_ok(g)) return ES_BAD_SHAPE;
+  const int M = N * H * W;
+  if (Cin <= 16) {
+    hipLaunchKernelGGL((conv_dx_kernel<256, 16>), dim3((M + 255) / 256, (Cin + 15) / 16), 256, 0, stream, dy, w, dx, g,
+                       accumulate);
+  } else if (Cin <= 32) {
+    hipLaunchKernelGGL((conv_dx_kernel<128, 32>), dim3((M + 127) / 128, (Cin + 31) / 32), 256, 0, stream, dy, w, dx, g,
+                       accumulate);
+  } else {
+    hipLaunchKernelGGL((conv_dx_kernel<64, 64>), dim3((M + 63) / 64, (Cin + 63) / 64), 256, 0, stream, dy, w, dx, g,
+                       accumulate);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+size_t es_conv2d_bwd_weight_workspace(int Cout, int Cin, int kh, int kw, int splits) {
+  return (size_t)splits * Cout * Cin * kh * kw;
+}
+
+// dw[co, ci, ky, kx] (+)= sum over output pixels of dy x im2col(x); `splits` pixel ranges reduced
+// through workspace (es_conv2d_bwd_weight_workspace floats)
+int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                         const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride, int pad,
+                         int splits, float* workspace, float* dw, int accumulate, hipStream_t stream) {
+  if (!x || !dy || !dw || !workspace) return ES_BAD_ARG;
+  const ConvGeom g = make_geom(N, H, W, Cin, sxn, sxh, sxw, sxc, Cout, kh, kw, stride, pad, syn, syh, syw);
+  if (!geom_ok(g) || splits <= 0) return ES_BAD_SHAPE;
+  const int M = N * g.Ho * g.Wo, K = Cin * kh * kw;
+  int chunk = (M + splits - 1) / splits;
+  chunk = (chunk + CBK - 1) / CBK * CBK;
+  const int S = (M + chunk - 1) / chunk;
+  if (Cout <= 16) {
+    hipLaunchKernelGGL((conv_dw_kernel<16, 256>), dim3((Cout + 15) / 16, (K + 255) / 256, S), 256, 0, stream, x, dy,
+                       workspace, g, chunk);
+  } else if (Cout <= 32) {
+    hipLaunchKernelGGL((conv_dw_kernel<32, 128>), dim3((Cout + 31) / 32, (K + 127) / 128, S), 256, 0, stream, x, dy,
+                       workspace, g, chunk);
+  } else {
+    hipLaunchKernelGGL((conv_dw_kernel<64, 64>), dim3((Cout + 63) / 64, (K + 63) / 64, S), 256, 0, stream, x, dy,
+                       workspace, g, chunk);
+  }
+  const long n = (long)Cout * K;
+  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(n), 256, 0, stream, workspace, dw, S, n, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+size_t es_chan_workspace(int rows, int C) {
+  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  return (size_t)G * 2 * C + 2 * C;
+}
+
+// out[c] (+)= sum over rows of v; row r at (r / HW) * sn + (r % HW) * sp (bias gradients)
+int es_chan_sum(const float* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
+                int accumulate, hipStream_t stream) {
+  if (!v || !out || !workspace) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || HW <= 0) return ES_BAD_SHAPE;
+  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{sn, sp, HW};
+  hipLaunchKernelGGL(chan_partial_kernel<0>, G, 256, 0, stream, v, rm, rows, C, per, nullptr, nullptr, nullptr,
+                     nullptr, 0, workspace);
+  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(C), 256, 0, stream, workspace, out, G, (long)C, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// BatchNorm2d over x [rows = N*H*W, C] (NHWC contiguous).  train: batch mean / biased variance,
+// running stats updated with momentum (unbiased variance) and num_batches_tracked += 1 (nullable);
+// mean / rstd saved for the backward.  eval: running statistics.  y = bn(x) (+ res) then ReLU if relu.
+int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const float* res,
+                int relu, float* y, float* mean, float* rstd, float* workspace, hipStream_t stream) {
+  if (!x || !gamma || !beta || !y || !running_mean || !running_var) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (!train) {
+    hipLaunchKernelGGL(bn_apply_kernel, grid1d(n), 256, 0, stream, x, n, C, running_mean, nullptr, running_var, eps,
+                       gamma, beta, res, relu, y);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
+  if (!mean || !rstd || !workspace) return ES_BAD_ARG;
+  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  hipLaunchKernelGGL(chan_partial_kernel<0>, G, 256, 0, stream, x, rm, rows, C, per, nullptr, nullptr, nullptr,
+                     nullptr, 0, workspace);
+  hipLaunchKernelGGL(bn_mean_kernel, (C + 255) / 256, 256, 0, stream, workspace, G, C, rows, mean);
+  hipLaunchKernelGGL(chan_partial_kernel<1>, G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr, nullptr,
+                     0, workspace);
+  hipLaunchKernelGGL(bn_var_kernel, (C + 255) / 256, 256, 0, stream, workspace, G, C, rows, eps, mean, rstd,
+                     running_mean, running_var, momentum);
+  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+  hipLaunchKernelGGL(bn_apply_kernel, grid1d(n), 256, 0, stream, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res,
+                     relu, y);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Backward of es_bn2d_fwd (train mode): g = dy * [y > 0 if relu] (written to gout when non-null: the
+// gradient of the residual input), dx = BN backward of g, dgamma (+)= sum g xhat, dbeta (+)= sum g.
+// eval mode (train = 0): dx = g * gamma / sqrt(running_var + eps), no parameter gradients.
+int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
+                const float* mean, const float* rstd, int train, const float* running_var, float eps, float* dx,
+                float* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t stream) {
+  if (!x || !dy || !dx || !gamma || (relu && !y)) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (!train) {
+    if (!running_var) return ES_BAD_ARG;
+    hipLaunchKernelGGL(bn_bwd_eval_kernel, grid1d(n), 256, 0, stream, dy, y, relu, n, C, running_var, eps, gamma, dx,
+                       gout);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
+  if (!mean || !rstd || !workspace || !dgamma || !dbeta) return ES_BAD_ARG;
+  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  float* sums = workspace + (size_t)G * 2 * C;  // [2C]: sum g, sum g xhat
+  hipLaunchKernelGGL(chan_partial_kernel<2>, G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
+                     workspace);
+  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(2 * C), 256, 0, stream, workspace, sums, G, (long)(2 * C), 0);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid1d(n), 256, 0, stream, x, dy, y, relu, n, C, rows, mean, rstd, gamma,
+                     sums, dx, gout);
+  // dgamma = sum g xhat (sums[C..2C)), dbeta = sum g (sums[0..C))
+  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(C), 256, 0, stream, sums + C, dgamma, 1, (long)C, accumulate);
+  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(C), 256, 0, stream, sums, dbeta, 1, (long)C, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// MaxPool2d(k, s, p) over NHWC; arg = int8 window index of the (first) maximum
+int es_maxpool2d_fwd(const float* x, int N, int H, int W, int C, int k, int s, int p, float* y, void* arg,
+                     hipStream_t stream) {
+  if (!x || !y || !arg) return ES_BAD_ARG;
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 11 || s <= 0 || p < 0 || 2 * p > k) return ES_BAD_SHAPE;
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  hipLaunchKernelGGL(maxpool_fwd_kernel, grid1d((long)N * Ho * Wo * C), 256, 0, stream, x, N, H, W, C, k, s, p, Ho, Wo,
+                     y, (int8_t*)arg);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,
+                     hipStream_t stream) {
+  if (!dy || !dx || !arg) return ES_BAD_ARG;
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 11 || s <= 0 || p < 0) return ES_BAD_SHAPE;
+  const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
+  hipLaunchKernelGGL(maxpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, dy, (const int8_t*)arg, N, H, W,
+                     C, k, s, p, Ho, Wo, dx);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// AvgPool2d(kernel k, stride k, no padding) over NHWC (H, W multiples of k)
+int es_avgpool2d_fwd(const float* x, int N, int H, int W, int C, int k, float* y, hipStream_t stream) {
+  if (!x || !y) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(avgpool_fwd_kernel, grid1d((long)N * (H / k) * (W / k) * C), 256, 0, stream, x, N, H, W, C, k,
+                     H / k, W / k, y);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_avgpool2d_bwd(const float* dy, int N, int H, int W, int C, int k, float* dx, int accumulate,
+                     hipStream_t stream) {
+  if (!dy || !dx) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(avgpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, dy, N, H, W, C, k, H / k, W / k,
+                     dx, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// out[N, H, W, C] = base + nearest-upsample(src [N, H/s, W/s, C], x s)
+int es_upsample_add_fwd(const float* base, const float* src, int N, int H, int W, int C, int s, float* out,
+                        hipStream_t stream) {
+  if (!base || !src || !out) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(upsample_add_fwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, base, src, N, H, W, C, s,
+                     out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// dsrc = block sums of dout (the base's gradient is dout itself)
+int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float* dsrc, hipStream_t stream) {
+  if (!dout || !dsrc) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(upsample_bwd_kernel, grid1d((long)N * (H / s) * (W / s) * C), 256, 0, stream, dout, N, H, W, C,
+                     s, dsrc);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// FCUDown + ConvTransBlock's sum: out [N, np+1, D] (token rows) from pooled [N, np, D] and x_t.
+int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln_w, const float* ln_b, float* out,
+                           float* mean, float* rstd, int N, int np, int D, float eps, hipStream_t stream) {
+  if (!pooled || !xt || !ln_w || !ln_b || !out || !mean || !rstd) return ES_BAD_ARG;
+  if (N <= 0 || np <= 0 || D <= 0 || D > 4096) return ES_BAD_SHAPE;
+  const long waves = (long)N * (np + 1);
+  hipLaunchKernelGGL(fcu_down_fwd_kernel, (unsigned)((waves + 3) / 4), 256, 0, stream, pooled, xt, ln_w, ln_b, out,
+                     mean, rstd, N, np, D, eps);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+size_t es_fcu_down_workspace(int N, int np, int D) {
+  const int rows = N * (np + 1);
+  const int blocks = rows < 1024 ? (rows + 3) / 4 : 256;
+  return (size_t)blocks * 2 * D;
+}
+
+// backward: dxt [N, np+1, D] (overwritten), dpooled [N, np, D] (overwritten), ln_w / ln_b grads (+)=
+int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
+                           const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
+                           float* dln_b, int accumulate, int N, int np, int D, float* workspace, hipStream_t stream) {
+  if (!dout || !pooled || !ln_w || !ln_b || !mean || !rstd || !dxt || !dpooled || !dln_w || !dln_b || !workspace)
+    return ES_BAD_ARG;
+  if (N <= 0 || np <= 0 || D <= 0 || D > 4096) return ES_BAD_SHAPE;
+  const int rows = N * (np + 1);
+  const int blocks = rows < 1024 ? (rows + 3) / 4 : 256;
+  const int per = (rows + blocks - 1) / blocks;
+  const size_t lds = (size_t)2 * D * 4;
+  hipLaunchKernelGGL(fcu_down_bwd_kernel, blocks, 256, lds, stream, dout, pooled, ln_w, ln_b, mean, rstd, dxt, dpooled,
+                     workspace, N, np, D, per);
+  // partial[b][0..D) = dgamma, [D..2D) = dbeta
+  hipLaunchKernelGGL(fcu_param_reduce_kernel, (2 * D + 255) / 256, 256, 0, stream, workspace, blocks, D, dln_w, dln_b,
+                     accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_tokens_cls_set(float* xt, int N, int T, int D, const float* cls, hipStream_t stream) {
+  if (!xt || !cls) return ES_BAD_ARG;
+  if (N <= 0 || T <= 0 || D <= 0) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(tokens_cls_set_kernel, (unsigned)(((long)N * D + 255) / 256), 256, 0, stream, xt, N, T, D, cls);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+}  // extern "C"

@@ -109,9 +109,52 @@ __global__ __launch_bounds__(256) void poly_ce_kernel(const float* __restrict__ 
   if (threadIdx.x == 0) out[0] = sum / (float)n;
 }
 
+// F.cross_entropy(logits, y, weight=w, reduction='mean') = sum_i w[y_i] l_i / sum_i w[y_i]
+// (code/loss.py:118, the SemiFormer heads' loss, code/semiformer.py:125-126); one workgroup.
+__global__ __launch_bounds__(256) void ce_weighted_kernel(const float* __restrict__ l, int ldl,
+                                                          const int64_t* __restrict__ y, const float* __restrict__ w,
+                                                          int n, int C, float grad_scale, float* __restrict__ dl,
+                                                          int lddl, float* __restrict__ out) {
+  __shared__ float red[16];
+  float ws = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) ws += w ? w[(int)y[i]] : 1.f;
+  const float W = block_sum(ws, red);
+  __syncthreads();
+  const float invW = 1.0f / W;
+  float sum = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float* lr = l + (size_t)i * ldl;
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, lr[c]);
+    float se = 0.f;
+    for (int c = 0; c < C; ++c) se += __expf(lr[c] - mx);
+    const float lse = mx + __logf(se);
+    const int yi = (int)y[i];
+    const float wy = w ? w[yi] : 1.f;
+    sum += wy * (lse - lr[yi]);
+    const float coef = grad_scale * wy * invW;
+    for (int c = 0; c < C; ++c) {
+      const float p = __expf(lr[c] - lse);
+      dl[(size_t)i * lddl + c] = coef * (p - (c == yi ? 1.f : 0.f));
+    }
+  }
+  sum = block_sum(sum, red);
+  if (threadIdx.x == 0) out[0] = sum * invW;
+}
+
 }  // namespace
 
 extern "C" {
+
+// out[0] = weighted-mean CE (weights nullable -> plain mean); dl = grad_scale * d(out[0])/d logits
+int es_ce_weighted_fwd_bwd(const float* logits, int ldl, const int64_t* targets, const float* weights, int n, int C,
+                           float grad_scale, float* dlogits, int lddl, float* out, hipStream_t stream) {
+  if (n <= 0 || C <= 0) return ES_BAD_SHAPE;
+  if (!logits || !targets || !dlogits || !out) return ES_BAD_ARG;
+  hipLaunchKernelGGL(ce_weighted_kernel, 1, 256, 0, stream, logits, ldl, targets, weights, n, C, grad_scale, dlogits,
+                     lddl, out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
 
 // out[0] = loss (mean over n of masked CE), out[1] = mask mean.  dls = d(grad_scale*loss*n)/d l_s
 // i.e. pass grad_scale = lambda_u / n for d(lambda_u * loss).  pl / mask_out / row_loss nullable.

@@ -56,6 +56,25 @@ SIGNATURES = {
     "es_comatch_focal_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, V, I, V, V]),
     "es_fm_consistency_fwd_bwd": (I, [V, I, V, I, I, I, F, F, V, V, V, V, I, V, V]),
     "es_poly_ce_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, I, V, V]),
+    "es_conv2d_fwd": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, I, V]),
+    "es_conv2d_bwd_data": (I, [V, L, L, L, V, I, I, I, I, I, I, I, I, I, V, L, L, L, L, I, V]),
+    "es_conv2d_bwd_weight_workspace": (Z, [I, I, I, I, I]),
+    "es_conv2d_bwd_weight": (I, [V, I, I, I, I, L, L, L, L, V, L, L, L, I, I, I, I, I, I, V, V, I, V]),
+    "es_chan_workspace": (Z, [I, I]),
+    "es_chan_sum": (I, [V, I, I, L, L, I, V, V, I, V]),
+    "es_bn2d_fwd": (I, [V, I, I, V, V, V, V, V, F, F, I, V, I, V, V, V, V, V]),
+    "es_bn2d_bwd": (I, [V, V, V, I, I, I, V, V, V, I, V, F, V, V, V, V, I, V, V]),
+    "es_maxpool2d_fwd": (I, [V, I, I, I, I, I, I, I, V, V, V]),
+    "es_maxpool2d_bwd": (I, [V, V, I, I, I, I, I, I, I, V, V]),
+    "es_avgpool2d_fwd": (I, [V, I, I, I, I, I, V, V]),
+    "es_avgpool2d_bwd": (I, [V, I, I, I, I, I, V, I, V]),
+    "es_upsample_add_fwd": (I, [V, V, I, I, I, I, I, V, V]),
+    "es_upsample_bwd": (I, [V, I, I, I, I, I, V, V]),
+    "es_fcu_down_tokens_fwd": (I, [V, V, V, V, V, V, V, I, I, I, F, V]),
+    "es_fcu_down_workspace": (Z, [I, I, I]),
+    "es_fcu_down_tokens_bwd": (I, [V, V, V, V, V, V, V, V, V, V, I, I, I, I, V, V]),
+    "es_tokens_cls_set": (I, [V, I, I, I, V, V]),
+    "es_ce_weighted_fwd_bwd": (I, [V, I, V, V, I, I, F, V, I, V, V]),
     "es_adam_ema_step": (I, [V, V, V, V, V, L, F, F, F, F, F, F, F, F, V]),
     "es_ema_entry_size": (I, []),
     "es_ema_update_multi": (I, [V, V, I, F, F, V]),

@@ -158,6 +158,55 @@ int es_fm_consistency_fwd_bwd(const float* logits_w, int ldw, const float* logit
 int es_poly_ce_fwd_bwd(const float* logits, int ldl, const int64_t* targets, const float* weights, int n, int C,
                        float epsilon, float grad_scale, float* dlogits, int lddl, float* out, hipStream_t stream);
 
+/* ---- Conformer CNN branch (SemiFormer backbone, code/models/conformer.py:75-445) ---------------
+ * fp32 NHWC maps with element strides; Conv2d groups = 1, weights in the reference layout
+ * [Cout][Cin][kh][kw].  Replaces the reference's aten conv2d / batch_norm / max_pool2d /
+ * avg_pool2d / upsample_nearest2d calls in ConvBlock, FCUDown, FCUUp and the stem. */
+int es_conv2d_fwd(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                  const float* w, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y, long syn,
+                  long syh, long syw, int accumulate, hipStream_t stream);
+int es_conv2d_bwd_data(const float* dy, long syn, long syh, long syw, const float* w, int N, int H, int W, int Cin,
+                       int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh, long sxw, long sxc,
+                       int accumulate, hipStream_t stream);
+size_t es_conv2d_bwd_weight_workspace(int Cout, int Cin, int kh, int kw, int splits);
+int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                         const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride, int pad,
+                         int splits, float* workspace, float* dw, int accumulate, hipStream_t stream);
+size_t es_chan_workspace(int rows, int C);
+/* out[c] (+)= sum_r v[(r / HW) * sn + (r % HW) * sp + c]  (bias gradients) */
+int es_chan_sum(const float* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
+                int accumulate, hipStream_t stream);
+/* BatchNorm2d (train: batch stats, running update, num_batches_tracked += 1; eval: running stats),
+ * y = bn(x) (+ res) then ReLU if relu.  workspace: es_chan_workspace(rows, C) floats. */
+int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const float* res,
+                int relu, float* y, float* mean, float* rstd, float* workspace, hipStream_t stream);
+int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
+                const float* mean, const float* rstd, int train, const float* running_var, float eps, float* dx,
+                float* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t stream);
+int es_maxpool2d_fwd(const float* x, int N, int H, int W, int C, int k, int s, int p, float* y, void* arg,
+                     hipStream_t stream);
+int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,
+                     hipStream_t stream);
+int es_avgpool2d_fwd(const float* x, int N, int H, int W, int C, int k, float* y, hipStream_t stream);
+int es_avgpool2d_bwd(const float* dy, int N, int H, int W, int C, int k, float* dx, int accumulate,
+                     hipStream_t stream);
+int es_upsample_add_fwd(const float* base, const float* src, int N, int H, int W, int C, int s, float* out,
+                        hipStream_t stream);
+int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float* dsrc, hipStream_t stream);
+/* FCUDown LayerNorm + GELU + cat(cls) fused with ConvTransBlock's x_st + x_t */
+int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln_w, const float* ln_b, float* out,
+                           float* mean, float* rstd, int N, int np, int D, float eps, hipStream_t stream);
+size_t es_fcu_down_workspace(int N, int np, int D);
+int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
+                           const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
+                           float* dln_b, int accumulate, int N, int np, int D, float* workspace, hipStream_t stream);
+int es_tokens_cls_set(float* xt, int N, int T, int D, const float* cls, hipStream_t stream);
+/* F.cross_entropy(weight=w, reduction='mean') (code/loss.py:118): out[0] = sum w_y l / sum w_y;
+ * dlogits = grad_scale * d(out[0]) / d logits */
+int es_ce_weighted_fwd_bwd(const float* logits, int ldl, const int64_t* targets, const float* weights, int n, int C,
+                           float grad_scale, float* dlogits, int lddl, float* out, hipStream_t stream);
+
 /* ---- optimizer / EMA (code/optimizer.py:50-51, code/ema.py:51-62) ----------------------------- */
 int es_adam_ema_step(float* p, const float* g, float* m, float* v, float* ema, long n, float beta1, float beta2,
                      float eps, float neg_step, float bc2_sqrt, float decay, float one_minus_decay,

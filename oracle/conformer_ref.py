@@ -1,0 +1,183 @@
+"""ORACLE (test infrastructure only): CPU fp32 restatement of the reference Conformer and one
+SemiFormer step.
+
+  * Conformer.forward            code/models/conformer.py:418-445 (stem, conv_1, trans_patch_conv,
+                                 trans_1, ConvTransBlocks, pooled conv head, trans_norm + head)
+  * ConvBlock.forward            code/models/conformer.py:107-144 (conv2(x + x_t) when fused)
+  * FCUDown / FCUUp              code/models/conformer.py:152-200
+  * ConvTransBlock.forward       code/models/conformer.py:338-356 (x_st + x_t: the cls row doubles)
+  * Conformer.__init__ stages    code/models/conformer.py:373-416 (channels, strides, dw_stride,
+                                 res_conv on the first block of a stage, last_fusion)
+  * Block / Attention / Mlp      code/models/conformer.py:8-72 (the ViT-block restatement of ref.py)
+  * SemiFormer.train_one SSL     code/semiformer.py:103-146 (two CE heads, two consistency losses
+                                 against the conv head's weak logits, Adam, EMA over every entry)
+
+Pinned by tests/test_oracle_golden.py against tests/golden/semiformer_step.npz, which
+tests/golden/make_golden.py produces by running the reference's own SemiFormer.train_one on a
+tiny Conformer.  bf16=True applies the MI355X path's rounding points to the transformer blocks
+only (the CNN branch, the FCU bridges and the heads run in fp32 on the device too).
+"""
+import torch
+import torch.nn.functional as F
+
+from .ref import _bf, consistency, ema_update
+
+BN_EPS_BLOCK = 1e-6   # ConvBlock / FCUUp norm_layer = partial(nn.BatchNorm2d, eps=1e-6)
+BN_EPS_STEM = 1e-5    # Conformer.bn1 = nn.BatchNorm2d(64)
+LN_EPS_BLOCK = 1e-6   # Block / FCUDown LayerNorm(eps=1e-6)
+LN_EPS_TRANS_NORM = 1e-5  # Conformer.trans_norm = nn.LayerNorm(embed_dim)
+
+
+class ConformerCfg:
+    def __init__(self, img_size=224, patch=16, base_channel=64, channel_ratio=1, embed_dim=384, depth=12, heads=6,
+                 mlp_ratio=4.0, num_classes=23):
+        assert depth % 3 == 0
+        self.img_size, self.patch, self.base, self.ratio = img_size, patch, base_channel, channel_ratio
+        self.dim, self.depth, self.heads, self.num_classes = embed_dim, depth, heads, num_classes
+        self.hidden = int(embed_dim * mlp_ratio)
+        self.stem = img_size // 4
+        self.grid = self.stem // (patch // 4)
+        self.np = self.grid * self.grid
+        self.T = self.np + 1
+
+
+def stages(cfg):
+    """(name, inplanes, outplanes, res_conv, stride, dw_stride, last_fusion) per ConvTransBlock
+    (code/models/conformer.py:385-416)."""
+    s1, dw = cfg.base * cfg.ratio, cfg.patch // 4
+    out = []
+    fin = cfg.depth // 3 + 1
+    for i in range(2, fin):
+        out.append((f"conv_trans_{i}", s1, s1, False, 1, dw, False))
+    s2 = s1 * 2
+    init, fin = fin, fin + cfg.depth // 3
+    for i in range(init, fin):
+        out.append((f"conv_trans_{i}", s1 if i == init else s2, s2, i == init, 2 if i == init else 1, dw // 2, False))
+    s3 = s2 * 2
+    init, fin = fin, fin + cfg.depth // 3
+    for i in range(init, fin):
+        out.append((f"conv_trans_{i}", s2 if i == init else s3, s3, i == init, 2 if i == init else 1, dw // 4,
+                    i == cfg.depth))
+    return out
+
+
+def _bn(x, p, bufs, pre, eps, train):
+    y = F.batch_norm(x, bufs[pre + "running_mean"], bufs[pre + "running_var"], p[pre + "weight"], p[pre + "bias"],
+                     training=train, momentum=0.1, eps=eps)
+    if train:
+        bufs[pre + "num_batches_tracked"] += 1
+    return y
+
+
+def conv_block(p, bufs, pre, x, stride, res_conv, x_t=None, train=True):
+    """ConvBlock.forward (code/models/conformer.py:107-144); returns (x, x2)."""
+    residual = x
+    x = F.relu(_bn(F.conv2d(x, p[pre + "conv1.weight"]), p, bufs, pre + "bn1.", BN_EPS_BLOCK, train))
+    x = F.conv2d(x if x_t is None else x + x_t, p[pre + "conv2.weight"], stride=stride, padding=1)
+    x2 = F.relu(_bn(x, p, bufs, pre + "bn2.", BN_EPS_BLOCK, train))
+    x = _bn(F.conv2d(x2, p[pre + "conv3.weight"]), p, bufs, pre + "bn3.", BN_EPS_BLOCK, train)
+    if res_conv:
+        residual = _bn(F.conv2d(residual, p[pre + "residual_conv.weight"], stride=stride), p, bufs,
+                       pre + "residual_bn.", BN_EPS_BLOCK, train)
+    return F.relu(x + residual), x2
+
+
+def block(p, pre, t, heads, bf16=False):
+    """conformer.Block (code/models/conformer.py:55-72), rounding points as ref._trunk."""
+    B, N, D = t.shape
+    hd = D // heads
+    r = _bf if bf16 else (lambda v: v)
+    h = r(F.layer_norm(t, (D,), p[pre + "norm1.weight"], p[pre + "norm1.bias"], LN_EPS_BLOCK))
+    qkv = r(F.linear(h, r(p[pre + "attn.qkv.weight"]), p[pre + "attn.qkv.bias"]))
+    qkv = qkv.reshape(B, N, 3, heads, hd).permute(2, 0, 3, 1, 4)
+    q, k, v = qkv[0], qkv[1], qkv[2]
+    attn = (q @ k.transpose(-2, -1)) * hd ** -0.5
+    if bf16:
+        e = torch.exp(attn - attn.amax(-1, keepdim=True))
+        o = (_bf(e) @ v) / e.sum(-1, keepdim=True)
+    else:
+        o = attn.softmax(dim=-1) @ v
+    o = r(o.transpose(1, 2).reshape(B, N, D))
+    t = t + F.linear(o, r(p[pre + "attn.proj.weight"]), p[pre + "attn.proj.bias"])
+    h = r(F.layer_norm(t, (D,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_EPS_BLOCK))
+    h = r(F.gelu(F.linear(h, r(p[pre + "mlp.fc1.weight"]), p[pre + "mlp.fc1.bias"])))
+    return t + F.linear(h, r(p[pre + "mlp.fc2.weight"]), p[pre + "mlp.fc2.bias"])
+
+
+def fcu_down(p, pre, x2, x_t, dw):
+    """FCUDown.forward (code/models/conformer.py:161-170)."""
+    x = F.conv2d(x2, p[pre + "conv_project.weight"], p[pre + "conv_project.bias"])
+    x = F.avg_pool2d(x, dw, dw).flatten(2).transpose(1, 2)
+    x = F.gelu(F.layer_norm(x, (x.shape[-1],), p[pre + "ln.weight"], p[pre + "ln.bias"], LN_EPS_BLOCK))
+    return torch.cat([x_t[:, 0][:, None, :], x], dim=1)
+
+
+def fcu_up(p, bufs, pre, x_t, H, W, up, train=True):
+    """FCUUp.forward (code/models/conformer.py:187-194)."""
+    B, _, C = x_t.shape
+    x_r = x_t[:, 1:].transpose(1, 2).reshape(B, C, H, W)
+    x_r = F.relu(_bn(F.conv2d(x_r, p[pre + "conv_project.weight"], p[pre + "conv_project.bias"]), p, bufs,
+                     pre + "bn.", BN_EPS_BLOCK, train))
+    return F.interpolate(x_r, size=(H * up, W * up))
+
+
+def conformer_forward(p, bufs, x, cfg, train=True, bf16=False):
+    """Conformer.forward (code/models/conformer.py:418-445) -> (conv_cls, trans_cls)."""
+    B = x.shape[0]
+    x_base = F.max_pool2d(F.relu(_bn(F.conv2d(x, p["conv1.weight"], stride=2, padding=3), p, bufs, "bn1.",
+                                     BN_EPS_STEM, train)), 3, 2, 1)
+    x, _ = conv_block(p, bufs, "conv_1.", x_base, 1, True, train=train)
+    x_t = F.conv2d(x_base, p["trans_patch_conv.weight"], p["trans_patch_conv.bias"], stride=cfg.patch // 4)
+    x_t = torch.cat([p["cls_token"].expand(B, -1, -1), x_t.flatten(2).transpose(1, 2)], dim=1)
+    x_t = block(p, "trans_1.", x_t, cfg.heads, bf16)
+    for name, _, _, res_conv, stride, dw, last in stages(cfg):
+        pre = name + "."
+        x, x2 = conv_block(p, bufs, pre + "cnn_block.", x, stride, res_conv, train=train)
+        H, W = x2.shape[2:]
+        x_st = fcu_down(p, pre + "squeeze_block.", x2, x_t, dw)
+        x_t = block(p, pre + "trans_block.", x_st + x_t, cfg.heads, bf16)
+        x_t_r = fcu_up(p, bufs, pre + "expand_block.", x_t, H // dw, W // dw, dw, train)
+        x, _ = conv_block(p, bufs, pre + "fusion_block.", x, 2 if last else 1, last, x_t=x_t_r, train=train)
+    conv_cls = F.linear(F.adaptive_avg_pool2d(x, 1).flatten(1), p["conv_cls_head.weight"], p["conv_cls_head.bias"])
+    x_t = F.layer_norm(x_t, (cfg.dim,), p["trans_norm.weight"], p["trans_norm.bias"], LN_EPS_TRANS_NORM)
+    trans_cls = F.linear(x_t[:, 0], p["trans_cls_head.weight"], p["trans_cls_head.bias"])
+    return conv_cls, trans_cls
+
+
+def is_buffer(name):
+    return name.endswith(("running_mean", "running_var", "num_batches_tracked"))
+
+
+class SemiFormerRef:
+    """One SSL step of SemiFormer.train_one (code/semiformer.py:103-146)."""
+
+    def __init__(self, state, cfg, class_weights=None, thres=0.95, lambda_u=1.0, lr=1e-3, ema_decay=0.999,
+                 bf16=False):
+        self.cfg, self.bf16 = cfg, bf16
+        self.names = [k for k in state if not is_buffer(k)]
+        self.p = {k: state[k].detach().clone().float().requires_grad_(True) for k in self.names}
+        self.bufs = {k: state[k].detach().clone() for k in state if is_buffer(k)}
+        self.ema = {k: v.detach().clone() for k, v in state.items()}
+        self.cw, self.thres, self.lambda_u, self.decay = class_weights, thres, lambda_u, ema_decay
+        self.opt = torch.optim.Adam([self.p[k] for k in self.names], lr=lr, betas=(0.9, 0.999), eps=1e-8,
+                                    weight_decay=0)
+
+    def step(self, x, y, uw, us):
+        bs = x.shape[0]
+        out_conv, out_trans = conformer_forward(self.p, self.bufs, torch.cat((x, uw, us)), self.cfg, True, self.bf16)
+        w_conv, s_conv = out_conv[bs:].chunk(2)
+        s_trans = out_trans[bs:].chunk(2)[1]
+        lx = F.cross_entropy(out_conv[:bs], y, weight=self.cw) + F.cross_entropy(out_trans[:bs], y, weight=self.cw)
+        lu_c, _, pl, mask = consistency(w_conv, s_conv, self.thres)
+        lu_t, mask_mean, _, _ = consistency(w_conv, s_trans, self.thres)
+        loss = lx + self.lambda_u * (lu_c + lu_t)
+        self.opt.zero_grad()
+        loss.backward()
+        grads = {k: self.p[k].grad.detach().clone() for k in self.names}
+        self.opt.step()
+        state = {k: self.p[k].detach() for k in self.names}
+        state.update(self.bufs)
+        ema_update(self.ema, state, self.decay)
+        return {"lx": lx.item(), "lu": (lu_c + lu_t).item(), "loss": loss.item(), "mask_mean": mask_mean.item(),
+                "pseudo_label": pl, "mask": mask, "out_conv": out_conv.detach(), "out_trans": out_trans.detach(),
+                "grads": grads}

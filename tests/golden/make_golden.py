@@ -504,6 +504,111 @@ def gen_comatch_step(ref_comatch, ref_custom, ref_conformer, ref_utils, tag, que
           f"bank_nonzero={int((tr.queue_feats != 0).any(1).sum())}")
 
 
+# ---------------------------------------------------------------- SemiFormer step golden
+def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
+    """SemiFormer.train_one SSL branch (code/semiformer.py:103-146) on a tiny Conformer: 64x64
+    images, embed 128, 2 heads, depth 6 (one stride-1 ConvTransBlock, a stride-2 res_conv block and
+    a stride-1 block at 2x channels, a stride-2 block and the last_fusion block at 4x channels),
+    CLS_WEIGHT on, two steps; records both heads' logits, losses, pseudo-labels and the state."""
+    import pandas as pd
+    from sklearn.utils import class_weight as skcw
+    import semiformer as ref_semiformer
+    torch.manual_seed(5150)
+    model = ref_conformer.Conformer(patch_size=16, num_classes=23, channel_ratio=1, embed_dim=128, depth=6,
+                                    num_heads=2, mlp_ratio=4, qkv_bias=True)
+    with torch.no_grad():
+        for name, p in model.named_parameters():
+            if name.endswith(("norm1.weight", "norm2.weight", "ln.weight", "trans_norm.weight")) or \
+                    ("bn" in name and name.endswith("weight")):
+                p.copy_(1.0 + 0.1 * torch.randn_like(p))
+            elif name.endswith("bias"):
+                p.copy_(0.02 * torch.randn_like(p))
+        model.conv_cls_head.weight.normal_(0.0, 0.12)  # peaky logits: some pseudo-labels pass the threshold
+        model.trans_cls_head.weight.normal_(0.0, 0.12)
+        nn.init.trunc_normal_(model.cls_token, std=0.02)
+    init_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+
+    B, MU, C = 2, 2, 23
+    g = torch.Generator().manual_seed(66)
+    df_y = np.concatenate([np.full(i + 1, i) for i in range(C)])
+    df = pd.DataFrame({"target": df_y})
+    lab, unlab = [], []
+    for _ in range(steps):
+        x = torch.randn(B, 3, 64, 64, generator=g)
+        y = torch.randint(0, C, (B,), generator=g)
+        uw = torch.randn(B * MU, 3, 64, 64, generator=g)
+        us = torch.randn(B * MU, 3, 64, 64, generator=g)
+        lab.append((x, y))
+        unlab.append(((uw, us), torch.arange(B * MU)))
+    thres = 0.28  # between the weak rows' max-probabilities: mixed masks in both steps
+    cfg = ref_utils.AttrDict(
+        DATA=ref_utils.AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+        MODEL=ref_utils.AttrDict(NAME="conformer", NUM_CLASSES=C, MARGIN="None", TYPE_SEMI="SemiFormer"),
+        TRAIN=ref_utils.AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=steps,
+                                 EVAL_STEP_SUP=0, CLS_WEIGHT=True, THRES=thres, T=1.0, LAMBDA_U=1.0, IS_SSL=True,
+                                 EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8,
+                                 SCH_NAME="step"))
+    orig_ccw = skcw.compute_class_weight
+
+    def ccw(class_weight, classes, y):  # sklearn>=1.x wants ndarray classes (SURVEY §8(a) a5)
+        return orig_ccw(class_weight=class_weight, classes=np.asarray(classes), y=np.asarray(y))
+
+    ref_semiformer.class_weight.compute_class_weight = ccw
+    rec = {"lx": [], "lu": [], "mask_mean": [], "pl": [], "outputs": []}
+    o_ce, o_cons = ref_semiformer.ce_loss, ref_semiformer.consistency_loss
+
+    def ce_spy(*a, **k):
+        out = o_ce(*a, **k)
+        rec["lx"].append(out.item())
+        return out
+
+    def cons_spy(lw, ls, *a, **k):
+        out = o_cons(lw, ls, *a, **k)
+        rec["lu"].append(out[0].item())
+        rec["mask_mean"].append(out[1].item())
+        rec["pl"].append(torch.softmax(lw.detach(), -1).max(-1).indices.numpy())
+        return out
+
+    def out_hook(mod, inp, out):
+        if mod.training:
+            rec["outputs"].append(tuple(t.detach().clone().numpy() for t in out))
+
+    h = model.register_forward_hook(out_hook)
+    ref_semiformer.ce_loss, ref_semiformer.consistency_loss = ce_spy, cons_spy
+    try:
+        tr = ref_semiformer.SemiFormer(model, opt_func="Adam", lr=1e-3, device="cpu")
+        tr.get_dataloader((FakeDL(lab, df), FakeDL(unlab)), None)
+        tr.get_config(cfg)
+        cw = tr.class_weights.numpy()
+        meter = tr.train_one(1)
+    finally:
+        ref_semiformer.ce_loss, ref_semiformer.consistency_loss = o_ce, o_cons
+        ref_semiformer.class_weight.compute_class_weight = orig_ccw
+        h.remove()
+    final_sd = model.state_dict()
+    ema_sd = tr.ema_model.ema.state_dict()
+    arrs = dict(thres=np.float32(thres), B=B, MU=MU, steps=steps, class_weights=cw,
+                lx=np.array(rec["lx"], np.float32), lu=np.array(rec["lu"], np.float32),
+                mask_mean=np.array(rec["mask_mean"], np.float32), pseudo_label=np.stack(rec["pl"]),
+                meter_avg=np.float32(meter.avg), meter_sum=np.float64(meter.sum),
+                lr_updates=np.array(tr.lr_scheduler.updates))
+    for i, ((x, y), ((uw, us), _)) in enumerate(zip(lab, unlab)):
+        arrs[f"x{i}"], arrs[f"y{i}"], arrs[f"uw{i}"], arrs[f"us{i}"] = x.numpy(), y.numpy(), uw.numpy(), us.numpy()
+        arrs[f"out_conv{i}"], arrs[f"out_trans{i}"] = rec["outputs"][i]
+    full = ("cls_token", "conv1.", "bn1.", "trans_norm.", "trans_cls_head.", "conv_cls_head.", "conv_trans_6.")
+    for k in init_sd:  # full post-step tensors for the stem, the heads and the last stage; sums elsewhere
+        arrs["init/" + k] = init_sd[k].numpy()
+        if k.startswith(full) or k.endswith(("running_mean", "running_var", "num_batches_tracked")):
+            arrs["final/" + k] = final_sd[k].numpy()
+            arrs["ema/" + k] = ema_sd[k].numpy()
+        else:
+            arrs["final_sum/" + k] = np.float64(final_sd[k].double().sum().item())
+            arrs["final_abs/" + k] = np.float64(final_sd[k].double().abs().sum().item())
+            arrs["ema_sum/" + k] = np.float64(ema_sd[k].double().sum().item())
+    np.savez_compressed(os.path.join(OUT, "semiformer_step.npz"), **arrs)
+    print(f"semiformer: lx={rec['lx']} lu={rec['lu']} mask={rec['mask_mean']} meter_sum={meter.sum:.6f}")
+
+
 def main():
     only = sys.argv[1] if len(sys.argv) > 1 else "all"
     ref_loss, ref_ema, ref_fixmatch, ref_conformer, ref_utils = _import_reference()
@@ -512,6 +617,10 @@ def main():
         gen_comatch_step(ref_comatch, ref_custom, ref_conformer, ref_utils, "closed", 5, 0.16, False)
         gen_comatch_step(ref_comatch, ref_custom, ref_conformer, ref_utils, "open", 1, 0.16, True)
     if only == "comatch":
+        return
+    if only in ("all", "semiformer"):
+        gen_semiformer_step(ref_conformer, ref_utils)
+    if only == "semiformer":
         return
     gen_consistency(ref_loss)
     gen_poly(ref_loss)

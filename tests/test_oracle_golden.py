@@ -164,3 +164,34 @@ def test_bf16_rounding_is_discontinuous_at_depth():
     drift32 = (a32 - b32).abs().max().item()
     assert drift16 > 0.2 * envelope
     assert drift32 < 1e-3 * envelope * 10
+
+
+def test_semiformer_step_matches_reference(golden):
+    """SemiFormer.train_one SSL branch (code/semiformer.py:103-146) on a tiny Conformer
+    (code/models/conformer.py:75-445): both heads' logits, the losses and the post-step state."""
+    from oracle import conformer_ref as cr
+    d = golden("semiformer_step.npz")
+    cfg = cr.ConformerCfg(img_size=64, patch=16, base_channel=64, channel_ratio=1, embed_dim=128, depth=6, heads=2,
+                          num_classes=23)
+    state = {k[5:]: torch.tensor(d[k]) for k in d.files if k.startswith("init/")}
+    r = cr.SemiFormerRef(state, cfg, class_weights=torch.tensor(d["class_weights"]).float(), thres=float(d["thres"]))
+    for i in range(int(d["steps"])):
+        x, y, uw, us = (torch.tensor(d[k]) for k in (f"x{i}", f"y{i}", f"uw{i}", f"us{i}"))
+        o = r.step(x, y, uw, us)
+        torch.testing.assert_close(o["out_conv"], torch.tensor(d[f"out_conv{i}"]), rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(o["out_trans"], torch.tensor(d[f"out_trans{i}"]), rtol=1e-5, atol=1e-5)
+        assert abs(o["lx"] - float(d["lx"][2 * i] + d["lx"][2 * i + 1])) < 1e-5
+        assert abs(o["lu"] - float(d["lu"][2 * i] + d["lu"][2 * i + 1])) < 1e-5
+        np.testing.assert_array_equal(o["pseudo_label"].numpy(), d["pseudo_label"][2 * i])
+    assert 0.0 < float(d["mask_mean"][0]) < 1.0  # mixed masks: the threshold is exercised
+    for k, v in r.p.items():
+        if "final/" + k in d.files:
+            torch.testing.assert_close(v.detach(), torch.tensor(d["final/" + k]), rtol=1e-5, atol=1e-6)
+        else:
+            assert abs(v.detach().double().sum().item() - float(d["final_sum/" + k])) <= 1e-5 * max(
+                1.0, float(d["final_abs/" + k]))
+    for k, v in r.bufs.items():
+        torch.testing.assert_close(v, torch.tensor(d["final/" + k]), rtol=1e-5, atol=1e-6)
+    for k in d.files:
+        if k.startswith("ema/"):
+            torch.testing.assert_close(r.ema[k[4:]], torch.tensor(d[k]), rtol=1e-5, atol=1e-6)
