@@ -96,6 +96,11 @@ __global__ __launch_bounds__(256) void poly_ce_kernel(const float* __restrict__ 
     for (int c = 0; c < C; ++c) se += __expf(lr[c] - mx);
     const float lse = mx + __logf(se);
     const int yi = (int)y[i];
+    if ((unsigned)yi >= (unsigned)C) {  // invalid target: NaN loss, no gradient, no out-of-range read
+      sum += __int_as_float(0x7fc00000);
+      for (int c = 0; c < C; ++c) dl[(size_t)i * lddl + c] = 0.f;
+      continue;
+    }
     const float wy = w ? w[yi] : 1.f;
     const float py = __expf(lr[yi] - lse);
     sum += wy * (lse - lr[yi]) + eps * (1.f - py);
@@ -117,7 +122,10 @@ __global__ __launch_bounds__(256) void ce_weighted_kernel(const float* __restric
                                                           int lddl, float* __restrict__ out) {
   __shared__ float red[16];
   float ws = 0.f;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) ws += w ? w[(int)y[i]] : 1.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int yi = (int)y[i];
+    ws += (unsigned)yi >= (unsigned)C ? __int_as_float(0x7fc00000) : (w ? w[yi] : 1.f);
+  }
   const float W = block_sum(ws, red);
   __syncthreads();
   const float invW = 1.0f / W;
@@ -130,6 +138,10 @@ __global__ __launch_bounds__(256) void ce_weighted_kernel(const float* __restric
     for (int c = 0; c < C; ++c) se += __expf(lr[c] - mx);
     const float lse = mx + __logf(se);
     const int yi = (int)y[i];
+    if ((unsigned)yi >= (unsigned)C) {  // invalid target: NaN loss (via the weight sum), no gradient
+      for (int c = 0; c < C; ++c) dl[(size_t)i * lddl + c] = 0.f;
+      continue;
+    }
     const float wy = w ? w[yi] : 1.f;
     sum += wy * (lse - lr[yi]);
     const float coef = grad_scale * wy * invW;

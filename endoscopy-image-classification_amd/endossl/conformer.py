@@ -1,0 +1,745 @@
+"""Native Conformer -- SemiFormer's backbone on MI355X kernels.
+
+Reference: `Conformer` (code/models/conformer.py:359-445) with ConvBlock (:75-144), FCUDown
+(:147-170), FCUUp (:173-194), ConvTransBlock (:250-356) and the ViT Block (:55-72); built by
+code/build.py:135-142 as Conformer-Ti (patch 16, channel_ratio 1, embed 384, depth 12, 6 heads,
+qkv_bias).  `model(x) -> (conv_logits, trans_logits)` as SemiFormer expects (code/semiformer.py:122).
+
+MI355X-first layout:
+  * parameters live in ONE fp32 flat buffer in the reference's state_dict order (checkpoints
+    interchange; the fused Adam + EMA sweep of optim.hip updates all of them in one pass); the
+    BatchNorm running statistics are ordinary buffers of the BN submodules;
+  * the CNN branch keeps NHWC fp32 maps and runs on conv.hip (fp32 implicit-GEMM convolutions,
+    BatchNorm2d with fused residual + ReLU, pools, nearest upsampling); the transformer branch is a
+    [tokens, D] fp32 residual stream padded to 256 rows (zero pad) and runs on the same bf16 MFMA
+    kernels as the ViT (gemm / attention / layernorm); the FCU bridges read and write token rows
+    in place through element strides (no transposes);
+  * every op is a torch.autograd.Function over the C-ABI; the backward writes parameter gradients
+    straight into the flat gradient buffer (each parameter is used once per forward, so every
+    launch overwrites its slice), which the native Adam reads.  PyTorch provides the autograd
+    graph, device memory and streams only.
+"""
+import ctypes
+import math
+from copy import deepcopy
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from ._lib import call, ptr
+
+EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32 = 0, 1, 2, 3, 4
+BN_EPS_BLOCK, BN_EPS_STEM, LN_EPS, LN_EPS_TRANS_NORM = 1e-6, 1e-5, 1e-6, 1e-5
+BN_MOMENTUM = 0.1
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+class ConformerConfig:
+    def __init__(self, img_size=224, patch=16, base_channel=64, channel_ratio=1, embed_dim=384, depth=12, heads=6,
+                 mlp_ratio=4.0, num_classes=23, num_med_block=0):
+        if depth % 3:
+            raise ValueError("Conformer depth must be a multiple of 3 (code/models/conformer.py:366)")
+        if num_med_block:
+            raise NotImplementedError("num_med_block > 0 (Med_ConvBlock) is not used by build.py's Conformer")
+        if embed_dim != heads * 64 or embed_dim % 128:
+            raise ValueError("the transformer kernels assume head_dim 64 and embed_dim % 128 == 0")
+        self.img_size, self.patch, self.base, self.ratio = img_size, patch, base_channel, channel_ratio
+        self.dim, self.depth, self.heads, self.num_classes = embed_dim, depth, heads, num_classes
+        self.hidden = int(embed_dim * mlp_ratio)
+        self.stem = img_size // 4                 # after conv1 (s2) and the max-pool (s2)
+        self.dw = patch // 4
+        self.grid = self.stem // self.dw
+        self.np = self.grid * self.grid
+        self.T = self.np + 1
+        s1 = base_channel * channel_ratio
+        self.s1, self.s3 = s1, 4 * s1
+
+    def stages(self):
+        """(name, inplanes, outplanes, res_conv, stride, dw_stride, last_fusion), code/models/conformer.py:385-416."""
+        s1, dw = self.s1, self.dw
+        out, fin = [], self.depth // 3 + 1
+        for i in range(2, fin):
+            out.append((f"conv_trans_{i}", s1, s1, False, 1, dw, False))
+        s2 = 2 * s1
+        init, fin = fin, fin + self.depth // 3
+        for i in range(init, fin):
+            out.append((f"conv_trans_{i}", s1 if i == init else s2, s2, i == init, 2 if i == init else 1, dw // 2,
+                        False))
+        s3 = 2 * s2
+        init, fin = fin, fin + self.depth // 3
+        for i in range(init, fin):
+            out.append((f"conv_trans_{i}", s2 if i == init else s3, s3, i == init, 2 if i == init else 1, dw // 4,
+                        i == self.depth))
+        return out
+
+
+# ------------------------------------------------------------------------------------ layout
+def _bn_entries(pre, C):
+    return [(pre + "weight", (C,), "p"), (pre + "bias", (C,), "p"), (pre + "running_mean", (C,), "rm"),
+            (pre + "running_var", (C,), "rv"), (pre + "num_batches_tracked", (), "nbt")]
+
+
+def _conv_block_entries(pre, inp, outp, res_conv):
+    med = outp // 4
+    out = [(pre + "conv1.weight", (med, inp, 1, 1), "p")] + _bn_entries(pre + "bn1.", med)
+    out += [(pre + "conv2.weight", (med, med, 3, 3), "p")] + _bn_entries(pre + "bn2.", med)
+    out += [(pre + "conv3.weight", (outp, med, 1, 1), "p")] + _bn_entries(pre + "bn3.", outp)
+    if res_conv:
+        out += [(pre + "residual_conv.weight", (outp, inp, 1, 1), "p")] + _bn_entries(pre + "residual_bn.", outp)
+    return out
+
+
+def _block_entries(pre, D, Hd):
+    return [(pre + "norm1.weight", (D,), "p"), (pre + "norm1.bias", (D,), "p"),
+            (pre + "attn.qkv.weight", (3 * D, D), "p"), (pre + "attn.qkv.bias", (3 * D,), "p"),
+            (pre + "attn.proj.weight", (D, D), "p"), (pre + "attn.proj.bias", (D,), "p"),
+            (pre + "norm2.weight", (D,), "p"), (pre + "norm2.bias", (D,), "p"),
+            (pre + "mlp.fc1.weight", (Hd, D), "p"), (pre + "mlp.fc1.bias", (Hd,), "p"),
+            (pre + "mlp.fc2.weight", (D, Hd), "p"), (pre + "mlp.fc2.bias", (D,), "p")]
+
+
+def conformer_layout(cfg):
+    """(name, shape, kind) in the reference Conformer's state_dict order (module registration order
+    of code/models/conformer.py:362-411); kind p = parameter, rm / rv / nbt = BatchNorm buffers."""
+    D, C = cfg.dim, cfg.num_classes
+    out = [("cls_token", (1, 1, D), "p"), ("trans_norm.weight", (D,), "p"), ("trans_norm.bias", (D,), "p"),
+           ("trans_cls_head.weight", (C, D), "p"), ("trans_cls_head.bias", (C,), "p"),
+           ("conv_cls_head.weight", (C, cfg.s3), "p"), ("conv_cls_head.bias", (C,), "p"),
+           ("conv1.weight", (64, 3, 7, 7), "p")] + _bn_entries("bn1.", 64)
+    out += _conv_block_entries("conv_1.", 64, cfg.s1, True)
+    out += [("trans_patch_conv.weight", (D, 64, cfg.dw, cfg.dw), "p"), ("trans_patch_conv.bias", (D,), "p")]
+    out += _block_entries("trans_1.", D, cfg.hidden)
+    for name, inp, outp, res_conv, _, _, last in cfg.stages():
+        pre = name + "."
+        med = outp // 4
+        out += _conv_block_entries(pre + "cnn_block.", inp, outp, res_conv)
+        out += _conv_block_entries(pre + "fusion_block.", outp, outp, last)
+        out += [(pre + "squeeze_block.conv_project.weight", (D, med, 1, 1), "p"),
+                (pre + "squeeze_block.conv_project.bias", (D,), "p"),
+                (pre + "squeeze_block.ln.weight", (D,), "p"), (pre + "squeeze_block.ln.bias", (D,), "p"),
+                (pre + "expand_block.conv_project.weight", (med, D, 1, 1), "p"),
+                (pre + "expand_block.conv_project.bias", (med,), "p")]
+        out += _bn_entries(pre + "expand_block.bn.", med)
+        out += _block_entries(pre + "trans_block.", D, cfg.hidden)
+    return out
+
+
+def init_conformer_(flat, layout, offs, generator=None):
+    """Conformer._init_weights (code/models/conformer.py:396-411): Linear trunc_normal(.02) / zero
+    bias, LayerNorm and BatchNorm 1 / 0, Conv2d kaiming_normal(fan_out, relu), conv biases keep the
+    PyTorch default U(+-1/sqrt(fan_in)), cls_token trunc_normal(.02)."""
+    with torch.no_grad():
+        for name, shape, kind in layout:
+            if kind != "p":
+                continue
+            t = flat[offs[name]:offs[name] + math.prod(shape)].view(shape)
+            if name == "cls_token" or (len(shape) == 2):
+                nn.init.trunc_normal_(t, std=0.02, generator=generator)
+            elif len(shape) == 4:
+                nn.init.kaiming_normal_(t, mode="fan_out", nonlinearity="relu", generator=generator)
+            elif name.endswith("weight"):
+                t.fill_(1.0)
+            else:
+                wname = name[:-len("bias")] + "weight"
+                wshape = [s for n, s, _ in layout if n == wname][0]
+                if len(wshape) == 4:  # Conv2d bias: PyTorch default
+                    bound = 1.0 / math.sqrt(math.prod(wshape[1:]))
+                    nn.init.uniform_(t, -bound, bound, generator=generator)
+                else:
+                    t.zero_()
+
+
+# ------------------------------------------------------------------------------------ ops
+def _s():
+    return _lib.stream()
+
+
+class _Map:
+    """An NHWC view: tensor t, element offset, (N, H, W, C) and element strides (n, h, w, c)."""
+
+    def __init__(self, t, N, H, W, C, sn=None, sh=None, sw=None, sc=1, off=0):
+        self.t, self.N, self.H, self.W, self.C = t, N, H, W, C
+        self.sn = sn if sn is not None else H * W * C
+        self.sh = sh if sh is not None else W * C
+        self.sw = sw if sw is not None else C
+        self.sc, self.off = sc, off
+
+    def p(self):
+        return ptr(self.t) + 4 * self.off
+
+    @staticmethod
+    def nhwc(t):
+        N, H, W, C = t.shape
+        return _Map(t, N, H, W, C)
+
+
+def _tn_splits(M, N1, N2):
+    tiles = (N1 // 128) * (N2 // 128)
+    return max(1, min((M + 31) // 32, 128, -(-1536 // tiles)))
+
+
+class _ConvFn(torch.autograd.Function):
+    """Conv2d (groups 1, optional bias) on an NHWC view -> new NHWC map (code/models/conformer.py
+    ConvBlock / FCU convs, Conformer.conv1)."""
+
+    @staticmethod
+    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None):
+        Ho, Wo = (xmap.H + 2 * p - k) // s + 1, (xmap.W + 2 * p - k) // s + 1
+        y = torch.empty(xmap.N, Ho, Wo, Cout, dtype=torch.float32, device=x.device)
+        call("es_conv2d_fwd", xmap.p(), xmap.N, xmap.H, xmap.W, xmap.C, xmap.sn, xmap.sh, xmap.sw, xmap.sc,
+             ptr(m.pview(wname)), ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout,
+             Wo * Cout, Cout, 0, _s())
+        ctx.save_for_backward(x)
+        ctx.m, ctx.xmap, ctx.spec = m, xmap, (wname, bname, Cout, k, s, p, Ho, Wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        m, xm = ctx.m, ctx.xmap
+        wname, bname, Cout, k, s, p, Ho, Wo = ctx.spec
+        dy = dy.contiguous()
+        xp = ptr(x) + 4 * xm.off
+        M = xm.N * Ho * Wo
+        K = xm.C * k * k
+        tiles = -(-Cout // 64) * -(-K // 64)
+        splits = max(1, min(-(-M // 16), -(-512 // tiles)))
+        lib = _lib.load()
+        ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits), device=dy.device)
+        call("es_conv2d_bwd_weight", xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy), Ho * Wo * Cout,
+             Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0, _s())
+        if bname:
+            wsb = torch.empty(lib.es_chan_workspace(M, Cout), device=dy.device)
+            call("es_chan_sum", ptr(dy), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(m.gview(bname)), 0, _s())
+        dx = None
+        if ctx.needs_input_grad[0]:
+            full = xm.off == 0 and xm.sc == 1 and xm.sn * xm.N == x.numel()
+            dx = torch.empty_like(x) if full else torch.zeros_like(x)
+            call("es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout, ptr(m.pview(wname)), xm.N, xm.H,
+                 xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, 0, _s())
+        return dx, None, None, None, None, None, None, None, None, None
+
+
+def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None):
+    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor)
+
+
+class _BNFn(torch.autograd.Function):
+    """BatchNorm2d (+ residual) (+ ReLU) on an NHWC map (ConvBlock bn1/bn2/bn3+residual+act3,
+    residual_bn, FCUUp bn, Conformer.bn1)."""
+
+    @staticmethod
+    def forward(ctx, x, res, m, pre, eps, relu):
+        x = x.contiguous()
+        N, H, W, C = x.shape
+        rows = N * H * W
+        y = torch.empty_like(x)
+        train = m.training
+        mean = torch.empty(C, device=x.device)
+        rstd = torch.empty(C, device=x.device)
+        ws = torch.empty(_lib.load().es_chan_workspace(rows, C), device=x.device)
+        rm, rv, nbt = m.bn_buffers(pre)
+        res_c = res.contiguous() if res is not None else None  # keep temporaries alive across the launch
+        call("es_bn2d_fwd", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")), ptr(rm),
+             ptr(rv), ptr(nbt) if train else None, BN_MOMENTUM, eps, 1 if train else 0, ptr(res_c),
+             1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), _s())
+        ctx.save_for_backward(x, y, mean, rstd)
+        ctx.m, ctx.pre, ctx.eps, ctx.relu, ctx.train, ctx.has_res = m, pre, eps, relu, train, res is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, rstd = ctx.saved_tensors
+        m, pre = ctx.m, ctx.pre
+        N, H, W, C = x.shape
+        rows = N * H * W
+        dy = dy.contiguous()
+        dx = torch.empty_like(x)
+        gout = torch.empty_like(x) if ctx.has_res else None
+        ws = torch.empty(_lib.load().es_chan_workspace(rows, C), device=x.device)
+        _, rv, _ = m.bn_buffers(pre)
+        call("es_bn2d_bwd", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(m.pview(pre + "weight")),
+             ptr(mean), ptr(rstd), 1 if ctx.train else 0, ptr(rv), ctx.eps, ptr(dx), ptr(gout),
+             ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(ws), _s())
+        return dx, gout, None, None, None, None
+
+
+def bn(m, x, pre, eps=BN_EPS_BLOCK, relu=False, res=None):
+    return _BNFn.apply(x, res, m, pre, eps, relu)
+
+
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        N, H, W, C = x.shape
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        y = torch.empty(N, Ho, Wo, C, device=x.device)
+        arg = torch.empty(N, Ho, Wo, C, dtype=torch.int8, device=x.device)
+        call("es_maxpool2d_fwd", ptr(x), N, H, W, C, k, s, p, ptr(y), ptr(arg), _s())
+        ctx.save_for_backward(arg)
+        ctx.geom = (N, H, W, C, k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        N, H, W, C, k, s, p = ctx.geom
+        dx = torch.empty(N, H, W, C, device=dy.device)
+        call("es_maxpool2d_bwd", ptr(dy.contiguous()), ptr(arg), N, H, W, C, k, s, p, ptr(dx), _s())
+        return dx, None, None, None
+
+
+class _AvgPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        N, H, W, C = x.shape
+        y = torch.empty(N, H // k, W // k, C, device=x.device)
+        call("es_avgpool2d_fwd", ptr(x.contiguous()), N, H, W, C, k, ptr(y), _s())
+        ctx.geom = (N, H, W, C, k)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        N, H, W, C, k = ctx.geom
+        dx = torch.empty(N, H, W, C, device=dy.device)
+        call("es_avgpool2d_bwd", ptr(dy.contiguous()), N, H, W, C, k, ptr(dx), 0, _s())
+        return dx, None
+
+
+class _UpsampleAddFn(torch.autograd.Function):
+    """base + F.interpolate(src, nearest, x s)  (FCUUp output added before conv2, :120,194)."""
+
+    @staticmethod
+    def forward(ctx, base, src, s):
+        N, H, W, C = base.shape
+        out = torch.empty_like(base)
+        base_c, src_c = base.contiguous(), src.contiguous()
+        call("es_upsample_add_fwd", ptr(base_c), ptr(src_c), N, H, W, C, s, ptr(out), _s())
+        ctx.geom = (N, H, W, C, s)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        N, H, W, C, s = ctx.geom
+        dout = dout.contiguous()
+        dsrc = torch.empty(N, H // s, W // s, C, device=dout.device)
+        call("es_upsample_bwd", ptr(dout), N, H, W, C, s, ptr(dsrc), _s())
+        return dout, dsrc, None
+
+
+class _FcuTokensFn(torch.autograd.Function):
+    """FCUDown's LayerNorm + GELU + cat(cls) fused with ConvTransBlock's `x_st + x_t`."""
+
+    @staticmethod
+    def forward(ctx, pooled, xt, m, pre):
+        N, h, w, D = pooled.shape
+        np_ = h * w
+        out = torch.zeros_like(xt)
+        mean = torch.empty(N * np_, device=xt.device)
+        rstd = torch.empty(N * np_, device=xt.device)
+        call("es_fcu_down_tokens_fwd", ptr(pooled.contiguous()), ptr(xt), ptr(m.pview(pre + "ln.weight")),
+             ptr(m.pview(pre + "ln.bias")), ptr(out), ptr(mean), ptr(rstd), N, np_, D, LN_EPS, _s())
+        ctx.save_for_backward(pooled, mean, rstd)
+        ctx.m, ctx.pre = m, pre
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pooled, mean, rstd = ctx.saved_tensors
+        m, pre = ctx.m, ctx.pre
+        N, h, w, D = pooled.shape
+        np_ = h * w
+        dout = dout.contiguous()
+        dxt = torch.zeros_like(dout)
+        dpooled = torch.empty_like(pooled)
+        ws = torch.empty(_lib.load().es_fcu_down_workspace(N, np_, D), device=dout.device)
+        call("es_fcu_down_tokens_bwd", ptr(dout), ptr(pooled), ptr(m.pview(pre + "ln.weight")),
+             ptr(m.pview(pre + "ln.bias")), ptr(mean), ptr(rstd), ptr(dxt), ptr(dpooled),
+             ptr(m.gview(pre + "ln.weight")), ptr(m.gview(pre + "ln.bias")), 0, N, np_, D, ptr(ws), _s())
+        return dpooled, dxt, None, None
+
+
+class _PatchTokensFn(torch.autograd.Function):
+    """trans_patch_conv (k = s = patch/4) into token rows 1.., cls_token into row 0
+    (Conformer.forward :426-428; no position embedding)."""
+
+    @staticmethod
+    def forward(ctx, xb, m):
+        cfg = m.cfg
+        N, H, W, C = xb.shape
+        D, T, g, dw = cfg.dim, cfg.T, cfg.grid, cfg.dw
+        xt = torch.zeros(_rup(N * T, 256), D, device=xb.device)
+        call("es_conv2d_fwd", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, ptr(m.pview("trans_patch_conv.weight")),
+             ptr(m.pview("trans_patch_conv.bias")), D, dw, dw, dw, 0, ptr(xt) + 4 * D, T * D, g * D, D, 0, _s())
+        call("es_tokens_cls_set", ptr(xt), N, T, D, ptr(m.pview("cls_token")), _s())
+        ctx.save_for_backward(xb)
+        ctx.m = m
+        return xt
+
+    @staticmethod
+    def backward(ctx, dxt):
+        (xb,) = ctx.saved_tensors
+        m = ctx.m
+        cfg = m.cfg
+        N, H, W, C = xb.shape
+        D, T, g, dw = cfg.dim, cfg.T, cfg.grid, cfg.dw
+        dxt = dxt.contiguous()
+        lib = _lib.load()
+        M = N * cfg.np
+        splits = max(1, min(-(-M // 16), -(-512 // (-(-D // 64) * -(-(C * dw * dw) // 64)))))
+        ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(D, C, dw, dw, splits), device=dxt.device)
+        dyp = ptr(dxt) + 4 * D
+        call("es_conv2d_bwd_weight", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, dyp, T * D, g * D, D, D, dw, dw, dw,
+             0, splits, ptr(ws), ptr(m.gview("trans_patch_conv.weight")), 0, _s())
+        wsb = torch.empty(lib.es_chan_workspace(M, D), device=dxt.device)
+        call("es_chan_sum", dyp, M, D, T * D, D, cfg.np, ptr(wsb), ptr(m.gview("trans_patch_conv.bias")), 0, _s())
+        call("es_chan_sum", ptr(dxt), N, D, T * D, 0, 1, ptr(wsb), ptr(m.gview("cls_token")), 0, _s())
+        dxb = torch.empty_like(xb)
+        call("es_conv2d_bwd_data", dyp, T * D, g * D, D, ptr(m.pview("trans_patch_conv.weight")), N, H, W, C, D, dw,
+             dw, dw, 0, ptr(dxb), H * W * C, W * C, C, 1, 0, _s())
+        return dxb, None
+
+
+class _BlockFn(torch.autograd.Function):
+    """conformer.Block (code/models/conformer.py:55-72) on the padded token buffer [Mp, D]: bf16
+    MFMA GEMMs, fused attention, LayerNorm kernels (the ViT engine's launch sequence)."""
+
+    @staticmethod
+    def forward(ctx, xt, m, pre):
+        cfg = m.cfg
+        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
+        Mp = xt.shape[0]
+        n = m.cur_n
+        M = n * T
+        s = _s()
+        dev = xt.device
+        b16 = torch.bfloat16
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+        h1, h2 = z(Mp, D, dt=b16), z(Mp, D, dt=b16)
+        mean1, rstd1, mean2, rstd2 = z(Mp), z(Mp), z(Mp), z(Mp)
+        qkv, o = z(Mp, 3 * D, dt=b16), z(Mp, D, dt=b16)
+        lse = z(n * H * T)
+        xmid, out = z(Mp, D), z(Mp, D)
+        pre_, act = z(Mp, Hd, dt=b16), z(Mp, Hd, dt=b16)
+        pv, wb = m.pview, m.wb
+        call("es_layernorm_fwd", ptr(xt), D, ptr(pv(pre + "norm1.weight")), ptr(pv(pre + "norm1.bias")), ptr(h1), D,
+             ptr(mean1), ptr(rstd1), M, D, LN_EPS, s)
+        call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(wb[pre + "attn.qkv.weight"]), D, ptr(pv(pre + "attn.qkv.bias")),
+             ptr(qkv), 3 * D, None, None, 0, M, 3 * D, D, 0, s)
+        call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, s)
+        call("es_gemm_nt", EPI_F32_RESID, ptr(o), D, ptr(wb[pre + "attn.proj.weight"]), D,
+             ptr(pv(pre + "attn.proj.bias")), ptr(xmid), D, None, ptr(xt), D, M, D, D, 0, s)
+        call("es_layernorm_fwd", ptr(xmid), D, ptr(pv(pre + "norm2.weight")), ptr(pv(pre + "norm2.bias")), ptr(h2), D,
+             ptr(mean2), ptr(rstd2), M, D, LN_EPS, s)
+        call("es_gemm_nt", EPI_GELU, ptr(h2), D, ptr(wb[pre + "mlp.fc1.weight"]), D, ptr(pv(pre + "mlp.fc1.bias")),
+             ptr(pre_), Hd, ptr(act), None, 0, M, Hd, D, 0, s)
+        call("es_gemm_nt", EPI_F32_RESID, ptr(act), Hd, ptr(wb[pre + "mlp.fc2.weight"]), Hd,
+             ptr(pv(pre + "mlp.fc2.bias")), ptr(out), D, None, ptr(xmid), D, M, D, Hd, 0, s)
+        ctx.save_for_backward(xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, pre_, act)
+        ctx.m, ctx.pre, ctx.n = m, pre, n
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, pre_, act = ctx.saved_tensors
+        m, pre, n = ctx.m, ctx.pre, ctx.n
+        cfg = m.cfg
+        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
+        Mp = xt.shape[0]
+        M = n * T
+        s = _s()
+        dev = xt.device
+        b16 = torch.bfloat16
+        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+        lib = _lib.load()
+        dout = dout.contiguous()
+        dxb = z(Mp, D, dt=b16)
+        call("es_cast_f32_bf16", ptr(dout), ptr(dxb), Mp * D, s)
+        wt, pv, gv = m.wt, m.pview, m.gview
+        ws_ln = torch.empty(2 * 1024 * D, device=dev)
+
+        def wgrad(dy, N1, x, N2, wname, bname):
+            sp = _tn_splits(M, N1, N2)
+            ws = torch.empty(lib.es_gemm_tn_workspace(N1, N2, sp), device=dev)
+            call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, sp, ptr(ws), ptr(gv(wname)), 0, ptr(gv(bname)), s)
+
+        dpre = z(Mp, Hd, dt=b16)
+        call("es_gemm_nt", EPI_DGELU, ptr(dxb), D, ptr(wt[pre + "mlp.fc2.weight"]), D, None, ptr(dpre), Hd, None,
+             ptr(pre_), Hd, M, Hd, D, 0, s)
+        wgrad(dxb, D, act, Hd, pre + "mlp.fc2.weight", pre + "mlp.fc2.bias")
+        dh = z(Mp, D)
+        call("es_gemm_nt", EPI_F32, ptr(dpre), Hd, ptr(wt[pre + "mlp.fc1.weight"]), Hd, None, ptr(dh), D, None, None,
+             0, M, D, Hd, 0, s)
+        wgrad(dpre, Hd, h2, D, pre + "mlp.fc1.weight", pre + "mlp.fc1.bias")
+        dxm, dxmb = z(Mp, D), z(Mp, D, dt=b16)
+        call("es_layernorm_bwd", ptr(dh), D, ptr(xmid), D, ptr(mean2), ptr(rstd2), ptr(pv(pre + "norm2.weight")),
+             ptr(dout), D, ptr(dxm), D, ptr(dxmb), D, ptr(gv(pre + "norm2.weight")), ptr(gv(pre + "norm2.bias")),
+             ptr(ws_ln), 1024, M, D, 0, s)
+        do = z(Mp, D, dt=b16)
+        call("es_gemm_nt", EPI_BF16, ptr(dxmb), D, ptr(wt[pre + "attn.proj.weight"]), D, None, ptr(do), D, None,
+             None, 0, M, D, D, 0, s)
+        wgrad(dxmb, D, o, D, pre + "attn.proj.weight", pre + "attn.proj.bias")
+        dqkv = z(Mp, 3 * D, dt=b16)
+        delta = z(n * H * T)
+        call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(do), D, ptr(dqkv), 3 * D, n, T, H,
+             64 ** -0.5, s)
+        dh2 = z(Mp, D)
+        call("es_gemm_nt", EPI_F32, ptr(dqkv), 3 * D, ptr(wt[pre + "attn.qkv.weight"]), 3 * D, None, ptr(dh2), D,
+             None, None, 0, M, D, 3 * D, 0, s)
+        wgrad(dqkv, 3 * D, h1, D, pre + "attn.qkv.weight", pre + "attn.qkv.bias")
+        dx = z(Mp, D)
+        call("es_layernorm_bwd", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
+             ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
+             ptr(ws_ln), 1024, M, D, 0, s)
+        return dx, None, None
+
+
+class _ConvHeadFn(torch.autograd.Function):
+    """AdaptiveAvgPool2d(1) + flatten + conv_cls_head Linear (Conformer.forward :438-439)."""
+
+    @staticmethod
+    def forward(ctx, x, m):
+        N, H, W, C = x.shape
+        ncls = m.cfg.num_classes
+        pooled = torch.empty(N, C, device=x.device)
+        call("es_avgpool2d_fwd", ptr(x.contiguous()), N, H, W, C, H, ptr(pooled), _s())
+        logits = torch.empty(N, ncls, device=x.device)
+        call("es_dense_fwd", ptr(pooled), C, ptr(m.pview("conv_cls_head.weight")), ptr(m.pview("conv_cls_head.bias")),
+             ptr(logits), ncls, N, C, ncls, 0, 0.0, None, 1.0, _s())
+        ctx.save_for_backward(pooled)
+        ctx.m, ctx.geom = m, (N, H, W, C)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dl):
+        (pooled,) = ctx.saved_tensors
+        m = ctx.m
+        N, H, W, C = ctx.geom
+        ncls = m.cfg.num_classes
+        dl = dl.contiguous()
+        dpooled = torch.empty(N, C, device=dl.device)
+        ws = torch.empty(_lib.load().es_dense_bwd_workspace(N, ncls), device=dl.device)
+        call("es_dense_bwd", ptr(dl), ncls, None, 0, 0, 0.0, None, 1.0, ptr(pooled), C,
+             ptr(m.pview("conv_cls_head.weight")), ptr(dpooled), C, 0, ptr(m.gview("conv_cls_head.weight")),
+             ptr(m.gview("conv_cls_head.bias")), N, C, ncls, ptr(ws), _s())
+        dx = torch.empty(N, H, W, C, device=dl.device)
+        call("es_avgpool2d_bwd", ptr(dpooled), N, H, W, C, H, ptr(dx), 0, _s())
+        return dx, None
+
+
+class _TransHeadFn(torch.autograd.Function):
+    """trans_norm (LayerNorm eps 1e-5) + trans_cls_head on the CLS token (Conformer.forward :441-443)."""
+
+    @staticmethod
+    def forward(ctx, xt, m):
+        cfg = m.cfg
+        n, D, ncls = m.cur_n, cfg.dim, cfg.num_classes
+        logits = torch.empty(n, ncls, device=xt.device)
+        xhat = torch.empty(n, D, device=xt.device)
+        rstd = torch.empty(n, device=xt.device)
+        call("es_cls_head_fwd", ptr(xt), D, cfg.T, ptr(m.pview("trans_norm.weight")), ptr(m.pview("trans_norm.bias")),
+             ptr(m.pview("trans_cls_head.weight")), ptr(m.pview("trans_cls_head.bias")), ptr(logits), ncls,
+             ptr(xhat), ptr(rstd), n, D, ncls, LN_EPS_TRANS_NORM, _s())
+        ctx.save_for_backward(xhat, rstd)
+        ctx.m, ctx.n, ctx.Mp = m, n, xt.shape[0]
+        return logits
+
+    @staticmethod
+    def backward(ctx, dl):
+        xhat, rstd = ctx.saved_tensors
+        m, n = ctx.m, ctx.n
+        cfg = m.cfg
+        D, ncls = cfg.dim, cfg.num_classes
+        dx = torch.zeros(ctx.Mp, D, device=dl.device)
+        dyn = torch.empty(n, D, device=dl.device)
+        call("es_cls_head_bwd", ptr(dl.contiguous()), ncls, ptr(m.pview("trans_cls_head.weight")),
+             ptr(m.pview("trans_norm.weight")), ptr(m.pview("trans_norm.bias")), ptr(xhat), ptr(rstd), ptr(dyn),
+             ptr(dx), D, cfg.T, ptr(m.gview("trans_cls_head.weight")), ptr(m.gview("trans_cls_head.bias")),
+             ptr(m.gview("trans_norm.weight")), ptr(m.gview("trans_norm.bias")), n, D, ncls, _s())
+        return dx, None
+
+
+# ------------------------------------------------------------------------------------ model
+class NativeConformer(nn.Module):
+    """Conformer whose compute runs in libendossl_hip.so; state_dict identical to the reference's."""
+
+    def __init__(self, cfg=None, seed=None, **kw):
+        super().__init__()
+        self.cfg = cfg if cfg is not None else ConformerConfig(**kw)
+        self.layout = conformer_layout(self.cfg)
+        self.offs, o = {}, 0
+        for name, shape, kind in self.layout:
+            if kind == "p":
+                self.offs[name] = o
+                o = _rup(o + math.prod(shape), 64)
+        self.numel = o
+        self.shapes = {name: shape for name, shape, _ in self.layout}
+        flat = torch.zeros(self.numel, dtype=torch.float32)
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        init_conformer_(flat, self.layout, self.offs, generator=gen)
+        self._build(flat, device=torch.device("cpu"))
+        self.version = 0
+        self.cur_n = 0
+
+    # ---- parameters: views of one flat buffer; BN running stats: module buffers ------------
+    def _resolve(self, name):
+        parts = name.split(".")
+        mod = self
+        for p in parts[:-1]:
+            if p not in mod._modules:
+                mod._modules[p] = nn.Module()
+            mod = mod._modules[p]
+        return mod, parts[-1]
+
+    def _build(self, flat, device, buffers=None):
+        self.flat = flat
+        self.flat_grad = torch.zeros_like(flat)
+        for name, shape, kind in self.layout:
+            mod, attr = self._resolve(name)
+            if kind == "p":
+                view = flat[self.offs[name]:self.offs[name] + math.prod(shape)].view(shape)
+                mod._parameters[attr] = nn.Parameter(view, requires_grad=True)
+            else:
+                if buffers is not None:
+                    t = buffers[name]
+                elif kind == "rm":
+                    t = torch.zeros(shape, device=device)
+                elif kind == "rv":
+                    t = torch.ones(shape, device=device)
+                else:
+                    t = torch.zeros((), dtype=torch.int64, device=device)
+                mod._buffers[attr] = t
+        self._packed_version = -1
+        self._wtab = None
+        self._anchor = torch.zeros((), device=device, requires_grad=True)
+
+    def _apply(self, fn, recurse=True):
+        new = fn(self.flat)
+        bufs = {name: fn(self.get_buffer(name)) for name, _, kind in self.layout if kind != "p"}
+        self._build(new.contiguous(), device=new.device, buffers=bufs)
+        return self
+
+    def __deepcopy__(self, memo):
+        other = NativeConformer.__new__(NativeConformer)
+        nn.Module.__init__(other)
+        other.cfg, other.layout, other.offs, other.numel, other.shapes = (self.cfg, self.layout, self.offs,
+                                                                          self.numel, self.shapes)
+        bufs = {name: self.get_buffer(name).detach().clone() for name, _, kind in self.layout if kind != "p"}
+        other._build(self.flat.detach().clone(), device=self.flat.device, buffers=bufs)
+        other.version, other.cur_n = 0, 0
+        other.train(self.training)
+        return other
+
+    def mark_updated(self):
+        self.version += 1
+
+    def load_state_dict(self, state_dict, strict=True):
+        r = super().load_state_dict(state_dict, strict=strict)
+        self.mark_updated()
+        return r
+
+    def pview(self, name):
+        return self.flat[self.offs[name]:self.offs[name] + math.prod(self.shapes[name])]
+
+    def gview(self, name):
+        return self.flat_grad[self.offs[name]:self.offs[name] + math.prod(self.shapes[name])]
+
+    def bn_buffers(self, pre):
+        return (self.get_buffer(pre + "running_mean"), self.get_buffer(pre + "running_var"),
+                self.get_buffer(pre + "num_batches_tracked"))
+
+    @property
+    def fc(self):  # SemiFormer freezes conv_cls_head / trans_cls_head; FixMatch-style callers ask for .fc
+        return self.trans_cls_head
+
+    def _pack(self):
+        """bf16 images W [N, K] / W^T [K, N] of every transformer-block matrix (re-packed after
+        each optimizer step, es_pack_weights)."""
+        if self._wtab is None:
+            D, Hd = self.cfg.dim, self.cfg.hidden
+            pres = ["trans_1."] + [s[0] + ".trans_block." for s in self.cfg.stages()]
+            mats = []
+            for pre in pres:
+                mats += [(pre + "attn.qkv.weight", 3 * D, D), (pre + "attn.proj.weight", D, D),
+                         (pre + "mlp.fc1.weight", Hd, D), (pre + "mlp.fc2.weight", D, Hd)]
+            dev = self.flat.device
+            self.wb, self.wt = {}, {}
+            esz = _lib.load().es_pack_entry_size()
+            raw = bytearray(esz * len(mats))
+            for j, (name, N, K) in enumerate(mats):
+                self.wb[name] = torch.zeros(N, K, dtype=torch.bfloat16, device=dev)
+                self.wt[name] = torch.zeros(K, N, dtype=torch.bfloat16, device=dev)
+                entry = (ctypes.c_long(self.offs[name]), ctypes.c_void_p(self.wb[name].data_ptr()),
+                         ctypes.c_void_p(self.wt[name].data_ptr()), ctypes.c_int(N), ctypes.c_int(K))
+                buf = b"".join(bytes(e) for e in entry)
+                raw[j * esz:j * esz + len(buf)] = buf
+            self._wtab = (torch.frombuffer(raw, dtype=torch.uint8).to(dev), len(mats))
+        if self._packed_version != self.version:
+            tab, nmat = self._wtab
+            call("es_pack_weights", ptr(self.flat), ptr(tab), nmat, _lib.stream())
+            self._packed_version = self.version
+
+    # ---- forward (code/models/conformer.py:418-445) ------------------------------------------
+    def _conv_block(self, pre, x, stride, res_conv, x_t=None, return_x2=True):
+        """ConvBlock.forward (:107-144)."""
+        med = self.shapes[pre + "conv1.weight"][0]
+        outp = self.shapes[pre + "conv3.weight"][0]
+        residual = x
+        h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1), pre + "bn1.", relu=True)
+        if x_t is not None:
+            h = _UpsampleAddFn.apply(h, x_t, h.shape[1] // x_t.shape[1])
+        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1)
+        x2 = bn(self, h, pre + "bn2.", relu=True)
+        h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1)
+        if res_conv:
+            r = conv(self, residual, _Map.nhwc(residual), pre + "residual_conv.weight", None, outp, 1, stride)
+            residual = bn(self, r, pre + "residual_bn.")
+        out = bn(self, h, pre + "bn3.", relu=True, res=residual)
+        return (out, x2) if return_x2 else out
+
+    def forward(self, x):
+        cfg = self.cfg
+        if not self.flat.is_cuda:
+            raise _lib.EndosslCallError("NativeConformer runs on the MI355X only: move it to a cuda device first")
+        if x.dim() != 4 or x.shape[1:] != (3, cfg.img_size, cfg.img_size):
+            raise ValueError(f"expected [n, 3, {cfg.img_size}, {cfg.img_size}] images, got {tuple(x.shape)}")
+        self._pack()
+        x = x.float().contiguous()
+        n, S = x.shape[0], cfg.img_size
+        self.cur_n = n
+        D = cfg.dim
+        # stem: conv1 7x7/2 (NCHW images read through strides) -> bn1 -> ReLU -> maxpool 3/2
+        img = _Map(x, n, S, S, 3, sn=3 * S * S, sh=S, sw=1, sc=S * S)
+        # the parameters are not autograd inputs (their gradients go straight to flat_grad): a leaf that
+        # requires grad, passed to the stem conv, puts the graph on the tape in training mode
+        anchor = self._anchor if (torch.is_grad_enabled() and self.training) else None
+        h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor)
+        x_base = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1)
+        xc = self._conv_block("conv_1.", x_base, 1, True, return_x2=False)
+        xt = _PatchTokensFn.apply(x_base, self)
+        xt = _BlockFn.apply(xt, self, "trans_1.")
+        T, g = cfg.T, cfg.grid
+        for name, _, outp, res_conv, stride, dw, last in cfg.stages():
+            pre = name + "."
+            med = outp // 4
+            xc, x2 = self._conv_block(pre + "cnn_block.", xc, stride, res_conv)
+            # FCUDown (:161-170): 1x1 conv (bias) -> avg-pool dw -> LN -> GELU -> cat(cls), + x_t
+            sq = conv(self, x2, _Map.nhwc(x2), pre + "squeeze_block.conv_project.weight",
+                      pre + "squeeze_block.conv_project.bias", D, 1)
+            pooled = _AvgPoolFn.apply(sq, dw) if dw > 1 else sq
+            xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.")
+            xt = _BlockFn.apply(xt, self, pre + "trans_block.")
+            # FCUUp (:187-194): token rows 1.. as a [n, g, g, D] map -> 1x1 conv (bias) -> BN -> ReLU;
+            # the nearest upsampling is fused into the fusion block's conv2 input
+            tok = _Map(xt, n, g, g, D, sn=T * D, sh=g * D, sw=D, sc=1, off=D)
+            up = conv(self, xt, tok, pre + "expand_block.conv_project.weight", pre + "expand_block.conv_project.bias",
+                      med, 1)
+            up = bn(self, up, pre + "expand_block.bn.", relu=True)
+            xc = self._conv_block(pre + "fusion_block.", xc, 2 if last else 1, last, x_t=up, return_x2=False)
+        conv_cls = _ConvHeadFn.apply(xc, self)
+        trans_cls = _TransHeadFn.apply(xt, self)
+        return conv_cls, trans_cls

@@ -180,3 +180,34 @@ def test_build_model_routes_comatch():
                                  TRAIN=AttrDict(IS_SSL=True), DATA=AttrDict(IMG_SIZE=64)))
     m = build_model(cfg)
     assert isinstance(m, NativeViTEmb) and m.cfg.low_dim == 16 and m.cfg.head == "emb"
+
+
+def test_conformer_layout_matches_reference_state_dict(golden):
+    """NativeConformer's state_dict = the reference Conformer's (names, order, shapes), taken from
+    the fixture the reference itself produced (tests/golden/make_golden.py gen_semiformer_step)."""
+    from endossl.conformer import ConformerConfig, NativeConformer
+    d = golden("semiformer_step.npz")
+    keys = [k[5:] for k in d.files if k.startswith("init/")]
+    m = NativeConformer(ConformerConfig(img_size=64, embed_dim=128, depth=6, heads=2, num_classes=23), seed=0)
+    sd = m.state_dict()
+    assert list(sd.keys()) == keys
+    for k in keys:
+        assert tuple(sd[k].shape) == tuple(d["init/" + k].shape), k
+        assert sd[k].dtype == torch.from_numpy(d["init/" + k]).dtype, k
+    m.load_state_dict({k: torch.tensor(d["init/" + k]) for k in keys})
+    assert torch.equal(m.get_parameter("conv_trans_6.trans_block.mlp.fc2.weight"),
+                       torch.tensor(d["init/conv_trans_6.trans_block.mlp.fc2.weight"]))
+    # parameters are views of the flat buffer (one Adam + EMA sweep)
+    p = m.get_parameter("conv1.weight")
+    assert p.data_ptr() == m.flat.data_ptr() + 4 * m.offs["conv1.weight"]
+
+
+def test_build_model_routes_conformer():
+    from endossl.build import build_model
+    from endossl.utils import AttrDict
+    cfg = AttrDict(DATA=AttrDict(IMG_SIZE=224), MODEL=AttrDict(NAME="conformer", NUM_CLASSES=23, PRE_TRAIN_PATH="None"),
+                   TRAIN=AttrDict())
+    m = build_model(cfg)
+    assert type(m).__name__ == "NativeConformer"
+    assert m.cfg.dim == 384 and m.cfg.depth == 12 and m.cfg.heads == 6 and m.cfg.T == 197
+    assert m.get_parameter("conv_cls_head.weight").shape == (23, 256)

@@ -1,0 +1,464 @@
+"""Conformer / SemiFormer on the MI355X.
+
+Kernels (conv.hip, es_ce_weighted_fwd_bwd) against plain torch fp64 CPU restatements of the same ops
+(autograd for the gradients): fp32 tolerances.  The native Conformer against the oracle
+(oracle/conformer_ref.py, pinned bit-exact to the reference's SemiFormer.train_one fixture): forward
+logits within 1e-3 * scale of the bf16-contract emulation (the transformer blocks round their GEMM
+operands to bf16, the CNN branch is fp32); the SemiFormer trainer against the reference fixture over
+two steps within the bf16 envelope, pseudo-labels / masks bit-exact on decidable rows, parameters
+within 2 * lr * steps.
+"""
+import json
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+from endossl import _lib  # noqa: E402
+from endossl._lib import call, ptr  # noqa: E402
+from oracle import conformer_ref as cr  # noqa: E402
+
+DEV = "cuda"
+
+
+def S():
+    return _lib.stream()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    assert torch.cuda.is_available(), "GPU tests need the MI355X"
+    _lib.load()
+
+
+_KEEP = []
+
+
+@pytest.fixture(autouse=True)
+def _keep_alive():
+    """Device copies made inline in a call's argument list must outlive the launch: a temporary
+    freed right after ptr() can hand its block to the next argument's copy (aliased operands)."""
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
+
+
+def dv(t, dtype=torch.float32):
+    """A device copy kept alive until the end of the test."""
+    t = t.to(dtype).to(DEV).contiguous()
+    _KEEP.append(t)
+    return t
+
+
+def _nhwc(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def _close(a, b, rtol=1e-4, atol=1e-4):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    sc = max(1.0, b.abs().max().item())
+    err = (a - b).abs().max().item()
+    assert err <= atol * sc, (err, sc)
+
+
+# ------------------------------------------------------------------------------------ conv
+@pytest.mark.parametrize("N,Cin,H,Cout,k,s,p", [(3, 5, 11, 7, 3, 2, 1), (2, 64, 16, 16, 1, 1, 0),
+                                                (2, 16, 16, 16, 3, 1, 1), (2, 32, 12, 128, 1, 2, 0),
+                                                (2, 64, 16, 96, 4, 4, 0), (1, 40, 9, 33, 3, 1, 1)])
+def test_conv2d_fwd_bwd(N, Cin, H, Cout, k, s, p):
+    torch.manual_seed(N * 100 + Cin + Cout)
+    x = torch.randn(N, Cin, H, H, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, dtype=torch.float64) * 0.2
+    b = torch.randn(Cout, dtype=torch.float64)
+    xr, wr, br = (t.clone().requires_grad_(True) for t in (x, w, b))
+    y = F.conv2d(xr, wr, br, stride=s, padding=p)
+    Ho = y.shape[2]
+    xd, wd, bd = _nhwc(x).float().to(DEV), w.float().to(DEV), b.float().to(DEV)
+    yd = torch.empty(N, Ho, Ho, Cout, device=DEV)
+    call("es_conv2d_fwd", ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(wd), ptr(bd), Cout, k, k, s, p,
+         ptr(yd), Ho * Ho * Cout, Ho * Cout, Cout, 0, S())
+    _close(_nchw(yd.cpu()), y)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dyd = _nhwc(dy).float().to(DEV)
+    dxd = torch.empty(N, H, H, Cin, device=DEV)
+    call("es_conv2d_bwd_data", ptr(dyd), Ho * Ho * Cout, Ho * Cout, Cout, ptr(wd), N, H, H, Cin, Cout, k, k, s, p,
+         ptr(dxd), H * H * Cin, H * Cin, Cin, 1, 0, S())
+    _close(_nchw(dxd.cpu()), xr.grad)
+    for splits in (1, 3):
+        ws = torch.empty(_lib.load().es_conv2d_bwd_weight_workspace(Cout, Cin, k, k, splits), device=DEV)
+        dwd = torch.empty_like(wd)
+        call("es_conv2d_bwd_weight", ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(dyd), Ho * Ho * Cout,
+             Ho * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(dwd), 0, S())
+        _close(dwd.cpu(), wr.grad)
+    M = N * Ho * Ho
+    wsb = torch.empty(_lib.load().es_chan_workspace(M, Cout), device=DEV)
+    dbd = torch.full((Cout,), 3.0, device=DEV)
+    call("es_chan_sum", ptr(dyd), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(dbd), 1, S())
+    _close(dbd.cpu() - 3.0, br.grad)
+
+
+def test_conv2d_strided_views():
+    """NCHW image input (the stem) and token-row output / input (trans_patch_conv, FCUUp)."""
+    torch.manual_seed(3)
+    N, Cin, H, Cout, k = 2, 3, 20, 8, 4
+    T = (H // k) ** 2 + 1
+    x = torch.randn(N, Cin, H, H)
+    w = torch.randn(Cout, Cin, k, k) * 0.2
+    y = F.conv2d(x.double(), w.double(), stride=k)  # [N, Cout, 5, 5]
+    g = H // k
+    xd, wd = x.to(DEV), w.to(DEV)
+    tok = torch.full((N * T, Cout), 9.0, device=DEV)
+    call("es_conv2d_fwd", ptr(xd), N, H, H, Cin, Cin * H * H, H, 1, H * H, ptr(wd), None, Cout, k, k, k, 0,
+         ptr(tok) + 4 * Cout, T * Cout, g * Cout, Cout, 0, S())
+    t = tok.view(N, T, Cout).cpu()
+    assert torch.all(t[:, 0] == 9.0)
+    _close(t[:, 1:].reshape(N, g, g, Cout), _nhwc(y))
+    # token rows read back as an NHWC map by a 1x1 conv, data gradient written into token rows
+    w2 = torch.randn(5, Cout, 1, 1) * 0.3
+    y2 = F.conv2d(_nchw(t[:, 1:].reshape(N, g, g, Cout)).double(), w2.double())
+    out = torch.empty(N, g, g, 5, device=DEV)
+    call("es_conv2d_fwd", ptr(tok) + 4 * Cout, N, g, g, Cout, T * Cout, g * Cout, Cout, 1, ptr(dv(w2)), None, 5,
+         1, 1, 1, 0, ptr(out), g * g * 5, g * 5, 5, 0, S())
+    _close(_nchw(out.cpu()), y2)
+    dy = torch.randn(N, g, g, 5)
+    dtok = torch.zeros(N * T, Cout, device=DEV)
+    call("es_conv2d_bwd_data", ptr(dv(dy)), g * g * 5, g * 5, 5, ptr(dv(w2)), N, g, g, Cout, 5, 1, 1, 1, 0,
+         ptr(dtok) + 4 * Cout, T * Cout, g * Cout, Cout, 1, 0, S())
+    ref = torch.einsum("nhwo,oc->nhwc", dy.double(), w2.double().view(5, Cout))
+    d = dtok.view(N, T, Cout).cpu()
+    assert torch.all(d[:, 0] == 0)
+    _close(d[:, 1:].reshape(N, g, g, Cout), ref)
+
+
+# ------------------------------------------------------------------------------------ batchnorm
+@pytest.mark.parametrize("rows_shape,C,relu,with_res", [((4, 6, 6), 16, True, False), ((3, 5, 5), 64, False, True),
+                                                        ((2, 3, 3), 300, True, True), ((64, 14, 14), 32, True, False)])
+def test_bn2d_fwd_bwd(rows_shape, C, relu, with_res):
+    torch.manual_seed(C)
+    N, H, W = rows_shape
+    x = torch.randn(N, H, W, C, dtype=torch.float64) * 1.5 + 0.3
+    res = torch.randn(N, H, W, C, dtype=torch.float64) if with_res else None
+    g = 1 + 0.1 * torch.randn(C, dtype=torch.float64)
+    b = 0.1 * torch.randn(C, dtype=torch.float64)
+    rm, rv = 0.1 * torch.randn(C, dtype=torch.float64), 1 + torch.rand(C, dtype=torch.float64)
+    rm_r, rv_r = rm.clone(), rv.clone()
+    xr, gr, br = (t.clone().requires_grad_(True) for t in (x, g, b))
+    resr = res.clone().requires_grad_(True) if with_res else None
+    y = F.batch_norm(_nchw(xr), rm_r, rv_r, gr, br, training=True, momentum=0.1, eps=1e-6)
+    y = _nhwc(y)
+    if with_res:
+        y = y + resr
+    if relu:
+        y = F.relu(y)
+    rows = N * H * W
+    f = dv
+    xd, gd, bdv, rmd, rvd = f(x), f(g), f(b), f(rm), f(rv)
+    resd = f(res) if with_res else None
+    yd, mean, rstd = torch.empty_like(xd), torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+    ws = torch.empty(_lib.load().es_chan_workspace(rows, C), device=DEV)
+    call("es_bn2d_fwd", ptr(xd), rows, C, ptr(gd), ptr(bdv), ptr(rmd), ptr(rvd), ptr(nbt), 0.1, 1e-6, 1, ptr(resd),
+         int(relu), ptr(yd), ptr(mean), ptr(rstd), ptr(ws), S())
+    _close(yd.cpu(), y, atol=2e-5)
+    _close(rmd.cpu(), rm_r, atol=1e-6)
+    _close(rvd.cpu(), rv_r, atol=1e-5)
+    assert int(nbt.item()) == 1
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dx, gout = torch.empty_like(xd), torch.empty_like(xd) if with_res else None
+    dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+    call("es_bn2d_bwd", ptr(xd), ptr(yd), ptr(f(dy)), rows, C, int(relu), ptr(gd), ptr(mean), ptr(rstd), 1, ptr(rvd),
+         1e-6, ptr(dx), ptr(gout), ptr(dg), ptr(db), 0, ptr(ws), S())
+    _close(dx.cpu(), xr.grad, atol=2e-4)
+    _close(dg.cpu(), gr.grad, atol=1e-4)
+    _close(db.cpu(), br.grad, atol=1e-4)
+    if with_res:
+        _close(gout.cpu(), resr.grad, atol=1e-6)
+    # eval mode: running statistics
+    y2 = torch.empty_like(xd)
+    call("es_bn2d_fwd", ptr(xd), rows, C, ptr(gd), ptr(bdv), ptr(rmd), ptr(rvd), None, 0.1, 1e-6, 0, None, 0, ptr(y2),
+         None, None, None, S())
+    ref = _nhwc(F.batch_norm(_nchw(x), rmd.cpu().double(), rvd.cpu().double(), g, b, training=False, eps=1e-6))
+    _close(y2.cpu(), ref, atol=2e-5)
+
+
+# ------------------------------------------------------------------------------------ pools
+def test_maxpool_avgpool_upsample():
+    torch.manual_seed(11)
+    N, H, C = 3, 13, 24
+    x = torch.randn(N, C, H, H, dtype=torch.float64)
+    x[0, 0, 2, 2] = x[0, 0, 2, 3] = 5.0  # a tie inside one window: the first (row-major) wins, as torch
+    xr = x.clone().requires_grad_(True)
+    y = F.max_pool2d(xr, 3, 2, 1)
+    Ho = y.shape[2]
+    xd = _nhwc(x).float().to(DEV)
+    yd = torch.empty(N, Ho, Ho, C, device=DEV)
+    arg = torch.empty(N, Ho, Ho, C, dtype=torch.int8, device=DEV)
+    call("es_maxpool2d_fwd", ptr(xd), N, H, H, C, 3, 2, 1, ptr(yd), ptr(arg), S())
+    _close(_nchw(yd.cpu()), y, atol=1e-6)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dxd = torch.empty_like(xd)
+    call("es_maxpool2d_bwd", ptr(dv(_nhwc(dy))), ptr(arg), N, H, H, C, 3, 2, 1, ptr(dxd), S())
+    _close(_nchw(dxd.cpu()), xr.grad, atol=1e-6)
+    # avgpool k x k / k and the global pool
+    for k, Hh in ((4, 16), (7, 7)):
+        z = torch.randn(N, C, Hh, Hh, dtype=torch.float64, requires_grad=True)
+        yz = F.avg_pool2d(z, k, k)
+        zd = _nhwc(z.detach()).float().to(DEV)
+        out = torch.empty(N, Hh // k, Hh // k, C, device=DEV)
+        call("es_avgpool2d_fwd", ptr(zd), N, Hh, Hh, C, k, ptr(out), S())
+        _close(_nchw(out.cpu()), yz, atol=1e-6)
+        dyz = torch.randn_like(yz)
+        yz.backward(dyz)
+        dz = torch.empty_like(zd)
+        call("es_avgpool2d_bwd", ptr(dv(_nhwc(dyz))), N, Hh, Hh, C, k, ptr(dz), 0, S())
+        _close(_nchw(dz.cpu()), z.grad, atol=1e-6)
+    # base + nearest upsample x s
+    base = torch.randn(N, C, 12, 12, dtype=torch.float64, requires_grad=True)
+    src = torch.randn(N, C, 3, 3, dtype=torch.float64, requires_grad=True)
+    o = base + F.interpolate(src, size=(12, 12))
+    od = torch.empty(N, 12, 12, C, device=DEV)
+    call("es_upsample_add_fwd", ptr(dv(_nhwc(base.detach()))), ptr(dv(_nhwc(src.detach()))),
+         N, 12, 12, C, 4, ptr(od), S())
+    _close(_nchw(od.cpu()), o, atol=1e-6)
+    do = torch.randn_like(o)
+    o.backward(do)
+    ds = torch.empty(N, 3, 3, C, device=DEV)
+    call("es_upsample_bwd", ptr(dv(_nhwc(do))), N, 12, 12, C, 4, ptr(ds), S())
+    _close(_nchw(ds.cpu()), src.grad, atol=1e-5)
+
+
+def test_fcu_down_tokens_fwd_bwd():
+    """FCUDown LN + GELU + cat(cls) fused with `x_st + x_t` (code/models/conformer.py:161-170,345)."""
+    torch.manual_seed(21)
+    N, np_, D = 5, 16, 128
+    T = np_ + 1
+    pooled = torch.randn(N, np_, D, dtype=torch.float64) * 2 + 0.5
+    xt = torch.randn(N, T, D, dtype=torch.float64)
+    g = 1 + 0.1 * torch.randn(D, dtype=torch.float64)
+    b = 0.1 * torch.randn(D, dtype=torch.float64)
+    pr, xr, gr, br = (t.clone().requires_grad_(True) for t in (pooled, xt, g, b))
+    xs = torch.cat([xr[:, 0][:, None, :], F.gelu(F.layer_norm(pr, (D,), gr, br, 1e-6))], dim=1)
+    out = xs + xr
+    f = dv
+    od = torch.zeros(N * T, D, device=DEV)
+    mean, rstd = torch.empty(N * np_, device=DEV), torch.empty(N * np_, device=DEV)
+    call("es_fcu_down_tokens_fwd", ptr(f(pooled)), ptr(f(xt)), ptr(f(g)), ptr(f(b)), ptr(od), ptr(mean), ptr(rstd), N,
+         np_, D, 1e-6, S())
+    _close(od.view(N, T, D).cpu(), out, atol=2e-5)
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    dxt, dp = torch.empty(N * T, D, device=DEV), torch.empty(N, np_, D, device=DEV)
+    dg, db = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ws = torch.empty(_lib.load().es_fcu_down_workspace(N, np_, D), device=DEV)
+    call("es_fcu_down_tokens_bwd", ptr(f(dout)), ptr(f(pooled)), ptr(f(g)), ptr(f(b)), ptr(mean), ptr(rstd), ptr(dxt),
+         ptr(dp), ptr(dg), ptr(db), 0, N, np_, D, ptr(ws), S())
+    _close(dxt.view(N, T, D).cpu(), xr.grad, atol=1e-5)
+    _close(dp.cpu(), pr.grad, atol=1e-4)
+    _close(dg.cpu(), gr.grad, atol=1e-4)
+    _close(db.cpu(), br.grad, atol=1e-4)
+
+
+def test_ce_weighted_fwd_bwd():
+    torch.manual_seed(8)
+    n, C = 37, 23
+    lg = torch.randn(n, C, dtype=torch.float64) * 3
+    y = torch.randint(0, C, (n,))
+    w = torch.rand(C, dtype=torch.float64) + 0.5
+    for weights in (w, None):
+        lr = lg.clone().requires_grad_(True)
+        loss = F.cross_entropy(lr, y, weight=weights)
+        loss.backward()
+        out = torch.zeros(1, device=DEV)
+        dl = torch.empty(n, C, device=DEV)
+        call("es_ce_weighted_fwd_bwd", ptr(dv(lg)), C, ptr(dv(y, torch.int64)),
+             ptr(dv(weights)) if weights is not None else None, n, C, 1.0, ptr(dl), C, ptr(out), S())
+        assert abs(out.item() - loss.item()) <= 1e-5 * max(1.0, loss.item())
+        _close(dl.cpu(), lr.grad, atol=1e-6)
+
+
+# ------------------------------------------------------------------------------------ model / trainer
+def _tiny_cfgs():
+    from endossl.conformer import ConformerConfig
+    kw = dict(img_size=64, patch=16, base_channel=64, channel_ratio=1, embed_dim=128, depth=6, heads=2, num_classes=23)
+    return ConformerConfig(**kw), cr.ConformerCfg(**kw)
+
+
+def _model_from_fixture(d):
+    from endossl.conformer import NativeConformer
+    ncfg, _ = _tiny_cfgs()
+    m = NativeConformer(ncfg, seed=0)
+    state = {k[5:]: torch.tensor(d[k]) for k in d.files if k.startswith("init/")}
+    m.load_state_dict(state)
+    return m.to(DEV), state
+
+
+def test_conformer_forward_backward_vs_oracle(golden):
+    """One train-mode forward + backward of the native Conformer vs the oracle (bf16-contract mode:
+    the transformer blocks' GEMM operands rounded like the MFMA kernels)."""
+    d = golden("semiformer_step.npz")
+    m, state = _model_from_fixture(d)
+    _, ocfg = _tiny_cfgs()
+    x = torch.cat([torch.tensor(d[k]) for k in ("x0", "uw0", "us0")])
+    rec = {}
+    res = {}
+    for bf in (True, False):
+        p = {k: v.clone().float().requires_grad_(True) for k, v in state.items() if not cr.is_buffer(k)}
+        bufs = {k: v.clone() for k, v in state.items() if cr.is_buffer(k)}
+        oc, ot = cr.conformer_forward(p, bufs, x, ocfg, train=True, bf16=bf)
+        res[bf] = (oc, ot, p, bufs)
+    m.train()
+    m.flat_grad.zero_()
+    hc, ht = m(x.to(DEV))
+    for name, h, i in (("conv", hc, 0), ("trans", ht, 1)):
+        r16, r32 = res[True][i].detach().double(), res[False][i].detach().double()
+        sc = max(1.0, r32.abs().max().item())
+        e16 = (h.detach().cpu().double() - r16).abs().max().item()
+        env = (r16 - r32).abs().max().item()
+        rec[name] = {"hip_vs_bf16_contract": e16, "bf16_envelope": env, "scale": sc}
+        assert e16 <= 1e-3 * sc + 0.25 * env, rec
+    # BatchNorm running statistics after the train-mode forward
+    for k in ("bn1.running_mean", "conv_trans_4.fusion_block.bn2.running_var", "conv_trans_6.expand_block.bn.running_mean"):
+        _close(m.get_buffer(k).cpu(), res[True][3][k], atol=2e-3)
+    assert int(m.get_buffer("bn1.num_batches_tracked").item()) == int(state["bn1.num_batches_tracked"].item()) + 1
+    # gradients of a fixed random linear functional of both heads
+    g = torch.Generator().manual_seed(4)
+    wc, wt = torch.randn(hc.shape, generator=g), torch.randn(ht.shape, generator=g)
+    (hc * wc.to(DEV)).sum().add((ht * wt.to(DEV)).sum()).backward()
+    grads = {}
+    for bf in (True, False):
+        oc, ot, p, _ = res[bf]
+        ((oc * wc).sum() + (ot * wt).sum()).backward()
+        grads[bf] = {k: v.grad for k, v in p.items()}
+    # per tensor: |HIP - bf16 contract| <= 2e-3 |g| + |bf16 contract - fp32| (+ a floor at 1e-4 of the
+    # largest gradient norm: a conv bias in front of a BatchNorm has an exactly-zero true gradient, so its
+    # computed value is pure rounding noise in every arithmetic)
+    gmax = max(grads[False][k].double().norm().item() for k in grads[False])
+    worst, bad = [], []
+    for k in grads[True]:
+        gh = m.gview(k).cpu().view(grads[True][k].shape).double()
+        g16, g32 = grads[True][k].double(), grads[False][k].double()
+        nrm = g32.norm().item()
+        e, env = (gh - g16).norm().item(), (g16 - g32).norm().item()
+        worst.append((e / (nrm + 1e-12), env / (nrm + 1e-12), k))
+        if e > 2e-3 * nrm + env + 1e-4 * gmax:
+            bad.append((k, e, env, nrm))
+    worst.sort(reverse=True)
+    rec["worst_grad_rel"] = [(round(a, 6), round(b, 6), c) for a, b, c in worst[:8]]
+    print(json.dumps(rec))
+    assert not bad, bad[:8]
+
+
+class _DL:
+    def __init__(self, items, df=None):
+        self.items = items
+
+        class _DS:
+            pass
+
+        self.dataset = _DS()
+        self.dataset.df = df
+
+    def __iter__(self):
+        return iter(self.items)
+
+    def __len__(self):
+        return len(self.items)
+
+
+def test_semiformer_trainer_vs_reference_train_one(golden):
+    import pandas as pd
+    from endossl.semiformer import SemiFormer
+    from endossl.utils import AttrDict
+    d = golden("semiformer_step.npz")
+    m, state = _model_from_fixture(d)
+    _, ocfg = _tiny_cfgs()
+    B, MU, steps, thres = int(d["B"]), int(d["MU"]), int(d["steps"]), float(d["thres"])
+    C = 23
+    df = pd.DataFrame({"target": np.concatenate([np.full(i + 1, i) for i in range(C)])})
+    lab = [(torch.tensor(d[f"x{i}"]), torch.tensor(d[f"y{i}"])) for i in range(steps)]
+    unl = [((torch.tensor(d[f"uw{i}"]), torch.tensor(d[f"us{i}"])), None) for i in range(steps)]
+    tr = SemiFormer(m, opt_func="Adam", lr=1e-3, device=DEV)
+    tr.get_dataloader((_DL(lab, df), _DL(unl)), None)
+    tr.get_config(AttrDict(
+        DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+        MODEL=AttrDict(NAME="conformer", NUM_CLASSES=C),
+        TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=steps, EVAL_STEP_SUP=0,
+                       CLS_WEIGHT=True, THRES=thres, T=1.0, LAMBDA_U=1.0, EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10,
+                       WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const", FREQ_EVAL=1)))
+    np.testing.assert_allclose(tr.class_weights.cpu().numpy(), d["class_weights"], rtol=1e-6)
+    cw = torch.tensor(d["class_weights"]).float()
+    emu = cr.SemiFormerRef(state, ocfg, class_weights=cw, thres=thres, bf16=True)
+    rec = {}
+    for i in range(steps):
+        # the oracle at the HIP path's own pre-step state (parameters + BN buffers): every step is checked
+        # tightly against the bf16-contract emulation of that state, not against a diverging trajectory
+        # (Adam turns bf16 noise on near-zero gradients into +-lr moves, which BatchNorm then amplifies)
+        snap = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+        ref16 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=True)
+        ref32 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=False)
+        o = tr.step((lab[i], unl[i]))
+        r16, r32 = ref16.step(*lab[i], *unl[i][0]), ref32.step(*lab[i], *unl[i][0])
+        r = emu.step(*lab[i], *unl[i][0])
+        for head in ("out_conv", "out_trans"):
+            h = o[head].cpu().double()
+            a16, a32 = r16[head].double(), r32[head].double()
+            sc = max(1.0, a32.abs().max().item())
+            e, env = (h - a16).abs().max().item(), (a16 - a32).abs().max().item()
+            rec[f"step{i}_{head}_vs_contract_at_hip_state"] = {"err": e, "bf16_envelope": env}
+            assert e <= 1e-3 * sc + 0.25 * env, rec
+            if i == 0:  # same initial state as the reference fixture
+                ref = torch.tensor(d[f"{head}{i}"]).double()
+                err, envr = (h - ref).abs().max().item(), (r[head].double() - ref).abs().max().item()
+                rec[f"step0_{head}_vs_reference"] = {"err": err, "bf16_envelope": envr}
+                assert err <= 1.5 * envr + 1e-3 * sc, rec
+        for k in ("lx", "lu", "loss"):
+            hip, a16, a32 = o[k].item(), r16[k], r32[k]
+            rec[f"step{i}_{k}"] = {"hip": hip, "bf16_contract": a16, "fp32": a32}
+            assert abs(hip - a16) <= 1e-3 * max(1.0, abs(a32)) + 0.25 * abs(a16 - a32), rec
+        if i == 0:
+            for k, ref_v in (("lx", float(d["lx"][0] + d["lx"][1])), ("lu", float(d["lu"][0] + d["lu"][1]))):
+                assert abs(o[k].item() - ref_v) <= 1.5 * abs(r[k] - ref_v) + 1e-3 * max(1.0, abs(ref_v)), rec
+        # pseudo-labels / masks of the conv head's weak rows, on decidable rows of the fp32 oracle at
+        # the same state (the reference's own at step 0)
+        wk32 = r32["out_conv"][B:B + B * MU].double()
+        wk16 = r16["out_conv"][B:B + B * MU].double()
+        p32, p16 = torch.softmax(wk32, -1), torch.softmax(wk16, -1)
+        envp = (p32 - p16).abs().max().item()
+        top2 = p32.topk(2, -1).values
+        ok = ((top2[:, 0] - top2[:, 1]) > 2 * envp + 1e-6).numpy()
+        okm = ((p32.max(-1).values - thres).abs() > 2 * envp + 1e-6).numpy()
+        np.testing.assert_array_equal(o["pseudo_label"].cpu().numpy()[ok], r32["pseudo_label"].numpy()[ok])
+        np.testing.assert_array_equal(o["mask"].cpu().numpy().astype(bool)[okm], r32["mask"].numpy().astype(bool)[okm])
+        if i == 0:
+            np.testing.assert_array_equal(r32["pseudo_label"].numpy(), d["pseudo_label"][0])
+        rec[f"step{i}_decidable"] = f"{int(ok.sum())}/{len(ok)} labels, {int(okm.sum())}/{len(okm)} masks"
+    sd, esd = m.state_dict(), tr.ema_model.ema.state_dict()
+    worst = 0.0
+    for k, v in sd.items():
+        if cr.is_buffer(k):
+            if k.endswith("num_batches_tracked"):
+                assert int(v.item()) == int(d["final/" + k])
+                assert int(esd[k].item()) == int(d["ema/" + k])
+            else:
+                fx = torch.tensor(d["final/" + k])
+                e, ev = (v.cpu() - fx).abs().max().item(), (emu.bufs[k] - fx).abs().max().item()
+                assert e <= 1.5 * ev + 2e-3, (k, e, ev)
+            continue
+        if "final/" + k in d.files:
+            worst = max(worst, (v.cpu() - torch.tensor(d["final/" + k])).abs().max().item())
+            assert (esd[k].cpu() - torch.tensor(d["ema/" + k])).abs().max().item() <= 1e-3 * 2e-3 * steps * (steps + 1) / 2 + 1e-6, k
+        else:
+            assert abs(v.double().sum().item() - float(d["final_sum/" + k])) <= (2e-3 * steps + 1e-5) * v.numel(), k
+    rec["max_param_delta"] = worst
+    print(json.dumps(rec))
+    assert worst <= 2e-3 * steps + 1e-5
