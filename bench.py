@@ -97,6 +97,116 @@ def pmc_traffic(kernel_substr):
     return None
 
 
+def conformer_step_tflop(cfg, n_images):
+    """Algorithmic FLOP of one SemiFormer step: 3x the Conformer forward (forward + backward, every
+    row carries gradient through BatchNorm) over n_images.  Forward per image: every conv
+    (2 * Cout * Cin * k^2 per output pixel), the transformer blocks (24 D^2 per token in the linears
+    + 4 T D per token in attention) and the FCU 1x1 convs, at the Conformer's own resolutions."""
+    S = cfg.img_size
+    fl = 2 * 64 * 3 * 49 * (S // 2) ** 2                      # stem conv1
+    hw = cfg.stem ** 2
+
+    def block(inp, outp, stride, res, hw_in):
+        med = outp // 4
+        hw_out = hw_in // (stride * stride)
+        f = 2 * med * inp * hw_in + 2 * med * med * 9 * hw_out + 2 * outp * med * hw_out
+        return f + (2 * outp * inp * hw_out if res else 0), hw_out
+
+    f, hw = block(64, cfg.s1, 1, True, hw)
+    fl += f + 2 * cfg.dim * 64 * cfg.dw ** 2 * cfg.np                       # conv_1, trans_patch_conv
+    tb = cfg.T * (24 * cfg.dim ** 2 + 4 * cfg.T * cfg.dim)                  # one transformer block
+    fl += tb
+    for _, inp, outp, res, stride, dw, last in cfg.stages():
+        f, hw = block(inp, outp, stride, res, hw)
+        med = outp // 4
+        fl += f + 2 * cfg.dim * med * hw + tb + 2 * med * cfg.dim * cfg.np   # cnn_block, FCUDown, block, FCUUp
+        f, hw2 = block(outp, outp, 2 if last else 1, last, hw)
+        fl += f
+        hw = hw2
+    return 3 * fl * n_images / 1e12
+
+
+def run_secondary(args):
+    """--workload c1 / s1: the other BASELINE configs on one GPU (step time and unlabeled images/s).
+    c1: CoMatch ViT-S/16, B=64, mu=7, 65,536-entry bank, EMA 0.999 (configs[3], single-GPU leg);
+    s1: SemiFormer on build.py's Conformer-Ti at 224^2, B=24, mu=7 (configs[4] names a ViT-B/384
+    Conformer that build.py cannot construct -- SURVEY.md §8(a) a20)."""
+    from endossl import dist
+    from endossl.utils import AttrDict
+    rank, world, local = dist.init_from_env()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    if args.workload == "c1":
+        from endossl.comatch import CoMatch
+        from endossl.comatch_model import NativeViTEmb
+        from endossl.vit import ViTConfig
+        B, MU, L, Q = 64, 7, 64, 65536
+        model = NativeViTEmb(ViTConfig(head="emb", low_dim=L), seed=0)
+        tr = CoMatch(model, device=dev)
+        cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
+                       MODEL=AttrDict(NAME="vit_small_patch16_224", NUM_CLASSES=23, LOW_DIM=L, TYPE_SEMI="CoMatch"),
+                       TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=1,
+                                      CLS_WEIGHT=False, THRES=0.95, T=1.0, LAMBDA_U=2.0, LAMBDA_C=2.0, EPOCHS=1,
+                                      WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const"))
+        tr.get_dataloader((None, None), None)
+        tr.get_config(cfg)
+        tr.set_queue_size(Q)
+        # a populated bank (as after earlier epochs): unit features, softmax class rows
+        tr.queue_feats.copy_(torch.nn.functional.normalize(torch.randn(Q, L, generator=g, device=dev), dim=1))
+        tr.queue_probs.copy_(torch.softmax(torch.randn(Q, 23, generator=g, device=dev) * 3, 1))
+        x, y = synth_images(B, 224, g, dev), torch.randint(0, 23, (B,), generator=g, device=dev)
+        batch = ((x, y), tuple(synth_images(B * MU, 224, g, dev) for _ in range(3)), None)
+        batch = (batch[0], (batch[1], None))
+        unl, tfl = B * MU, 3 * 9.197e9 * (B + 3 * B * MU) / 1e12 + 2 * (B * MU) * Q * (L + 23) / 1e12
+        desc = (f"C1: CoMatch ViT-S/16 step, B={B} + 3 x mu*B={B * MU} (weak, strong0, strong1), 224^2, L={L}, "
+                f"bank Q={Q} (memory smoothing over all Q rows), EMA 0.999, lambda_u=lambda_c=2")
+    else:
+        from endossl.conformer import ConformerConfig, NativeConformer
+        from endossl.semiformer import SemiFormer
+        B, MU = 24, 7
+        ccfg = ConformerConfig()
+        model = NativeConformer(ccfg, seed=0)
+        tr = SemiFormer(model, device=dev)
+        cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
+                       MODEL=AttrDict(NAME="conformer", NUM_CLASSES=23),
+                       TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=1,
+                                      EVAL_STEP_SUP=0, CLS_WEIGHT=False, THRES=0.95, T=1.0, LAMBDA_U=1.0, EPOCHS=1,
+                                      WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const"))
+        tr.get_dataloader((None, None), None)
+        tr.get_config(cfg)
+        x, y = synth_images(B, 224, g, dev), torch.randint(0, 23, (B,), generator=g, device=dev)
+        batch = ((x, y), ((synth_images(B * MU, 224, g, dev), synth_images(B * MU, 224, g, dev)), None))
+        unl, tfl = B * MU, conformer_step_tflop(ccfg, B + 2 * B * MU)
+        desc = (f"S1: SemiFormer step on Conformer-Ti (code/build.py:135-142: patch 16, embed 384, depth 12, 6 heads, "
+                f"channel_ratio 1), B={B} + 2 x mu*B={B * MU}, 224^2, C=23, tau=0.95, lambda_u=1, EMA 0.999")
+    for _ in range(args.warmup):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = tr.step(batch)
+    torch.cuda.synchronize()
+    dist.barrier()
+    T = time.perf_counter() - t0
+    elapsed = torch.tensor([T], dtype=torch.float64, device=dev)
+    if world > 1:
+        torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
+    T = elapsed.item()
+    if rank == 0:
+        ms = T / args.steps * 1e3
+        print(json.dumps({
+            "metric": f"unlabeled images/sec/node ({args.workload.upper()})", "value": round(world * unl * args.steps / T, 2),
+            "unit": "unlabeled images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "bf16 (transformer GEMMs) / fp32", "data": "synthetic (HBM-resident, seed 0)",
+            "config": {"workload": desc, "parallelism": f"dp{world}"},
+            "step_tflop": round(tfl, 3), "step_tflops": round(tfl / (ms / 1e3), 1),
+            "final_loss": round(out["loss"].item(), 6)}), flush=True)
+    dist.barrier()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -105,7 +215,11 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--mu", type=int, default=7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", choices=("f1", "c1", "s1"), default="f1",
+                    help="f1 = the BASELINE metric (default); c1 / s1 = CoMatch / SemiFormer configs")
     args = ap.parse_args()
+    if args.workload != "f1":
+        return run_secondary(args)
 
     from endossl import dist
     from endossl.fixmatch import FixMatch
