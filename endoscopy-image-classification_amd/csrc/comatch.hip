@@ -257,7 +257,7 @@ __global__ __launch_bounds__(256) void l2norm_bwd_kernel(const float* __restrict
 // p /= rowsum -> probs_orig.
 __global__ __launch_bounds__(256) void comatch_da_kernel(const float* __restrict__ lw, int ldl, int nu, int C,
                                                          float* __restrict__ hist, int cap, int len, int pos,
-                                                         float* __restrict__ probs_orig) {
+                                                         int hist_given, float* __restrict__ probs_orig) {
   __shared__ float colsum[256];
   __shared__ float avg[256];
   const int t = threadIdx.x;
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(256) void comatch_da_kernel(const float* __restrict
     for (int c = 0; c < C; ++c) probs_orig[(size_t)i * C + c] = expf(l[c] - mx) / s;
   }
   __syncthreads();
-  if (t < C) {
+  if (t < C && !hist_given) {  // hist_given: the entry was written by the caller (all-ranks mean)
     float s = 0.f;
     for (int i = 0; i < nu; ++i) s += probs_orig[(size_t)i * C + t];
     hist[(size_t)pos * C + t] = s / nu;
@@ -624,6 +624,40 @@ size_t es_comatch_pseudo_workspace(int nu, int C, int Q) {
   return (size_t)nchunks * nu * (C + 1);
 }
 
+// out[c] = mean_i softmax(l_i)[c]: the DA batch mean, for the data-parallel path (all-reduced
+// across ranks, then handed to es_comatch_pseudo_ex with hist_given = 1)
+__global__ __launch_bounds__(256) void softmax_colmean_kernel(const float* __restrict__ lw, int ldl, int n, int C,
+                                                              float* __restrict__ out) {
+  __shared__ float acc[32];
+  if (threadIdx.x < 32) acc[threadIdx.x] = 0.f;
+  __syncthreads();
+  float loc[32];
+  for (int c = 0; c < C; ++c) loc[c] = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float* l = lw + (size_t)i * ldl;
+    float mx = -INFINITY;
+    for (int c = 0; c < C; ++c) mx = fmaxf(mx, l[c]);
+    float s = 0.f;
+    for (int c = 0; c < C; ++c) s += expf(l[c] - mx);
+    for (int c = 0; c < C; ++c) loc[c] += expf(l[c] - mx) / s;
+  }
+  for (int c = 0; c < C; ++c) atomicAdd(&acc[c], loc[c]);
+  __syncthreads();
+  if (threadIdx.x < C) out[threadIdx.x] = acc[threadIdx.x] / n;
+}
+
+int es_softmax_colmean(const float* logits, int ldl, int n, int C, float* out, hipStream_t stream) {
+  if (n <= 0 || C <= 0 || C > 32) return ES_BAD_SHAPE;
+  if (!logits || !out) return ES_BAD_ARG;
+  hipLaunchKernelGGL(softmax_colmean_kernel, 1, 256, 0, stream, logits, ldl, n, C, out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_comatch_pseudo_ex(const float* logits_w, int ldl, int nu, int C, float* hist, int hist_cap, int hist_len,
+                         int hist_pos, int hist_given, const float* z_w, int ldz, int L, const float* bank_feats,
+                         const float* bank_probs, int Q, float temperature, float alpha, float thres, float* probs,
+                         float* probs_orig, int* pl, float* mask, float* workspace, hipStream_t stream);
+
 // Pseudo-labels of the weak rows: DA (append this batch's mean to hist[hist_pos], average the
 // hist_len newest entries of the hist_cap ring), memory smoothing against the bank (Q rows),
 // argmax / mask.  probs_orig is the DA output (what the bank stores), probs the smoothed one.
@@ -631,13 +665,23 @@ int es_comatch_pseudo(const float* logits_w, int ldl, int nu, int C, float* hist
                       int hist_pos, const float* z_w, int ldz, int L, const float* bank_feats, const float* bank_probs,
                       int Q, float temperature, float alpha, float thres, float* probs, float* probs_orig, int* pl,
                       float* mask, float* workspace, hipStream_t stream) {
+  return es_comatch_pseudo_ex(logits_w, ldl, nu, C, hist, hist_cap, hist_len, hist_pos, 0, z_w, ldz, L, bank_feats,
+                              bank_probs, Q, temperature, alpha, thres, probs, probs_orig, pl, mask, workspace, stream);
+}
+
+// as es_comatch_pseudo; hist_given = 1: hist[hist_pos] already holds this step's batch mean (the
+// data-parallel path writes the all-ranks mean there) and is not recomputed from the local rows
+int es_comatch_pseudo_ex(const float* logits_w, int ldl, int nu, int C, float* hist, int hist_cap, int hist_len,
+                         int hist_pos, int hist_given, const float* z_w, int ldz, int L, const float* bank_feats,
+                         const float* bank_probs, int Q, float temperature, float alpha, float thres, float* probs,
+                         float* probs_orig, int* pl, float* mask, float* workspace, hipStream_t stream) {
   if (nu <= 0 || C <= 0 || C > 32 || L <= 0 || L > 64 || Q <= 0 || hist_cap <= 0 || hist_len <= 0 ||
       hist_len > hist_cap || hist_pos < 0 || hist_pos >= hist_cap)
     return ES_BAD_SHAPE;
   if (!logits_w || !hist || !z_w || !bank_feats || !bank_probs || !probs || !probs_orig || !pl || !mask || !workspace)
     return ES_BAD_ARG;
   hipLaunchKernelGGL(comatch_da_kernel, 1, 256, 0, stream, logits_w, ldl, nu, C, hist, hist_cap, hist_len, hist_pos,
-                     probs_orig);
+                     hist_given, probs_orig);
   const int nchunks = (Q + SB - 1) / SB;
   const size_t lds = (size_t)SB * (L + C) * 4;
   allow_lds(comatch_smooth_partial_kernel, lds);

@@ -50,6 +50,8 @@ SIGNATURES = {
     "es_l2norm_bwd": (I, [V, I, V, I, V, V, I, I, I, V]),
     "es_comatch_pseudo_workspace": (Z, [I, I, I]),
     "es_comatch_pseudo": (I, [V, I, I, I, V, I, I, I, V, I, I, V, V, I, F, F, F, V, V, V, V, V, V]),
+    "es_comatch_pseudo_ex": (I, [V, I, I, I, V, I, I, I, I, V, I, I, V, V, I, F, F, F, V, V, V, V, V, V]),
+    "es_softmax_colmean": (I, [V, I, I, I, V, V]),
     "es_comatch_bank_write": (I, [V, I, I, V, I, I, I, V, V, I, V, V, I, I, V]),
     "es_comatch_contrastive_workspace": (Z, [I]),
     "es_comatch_contrastive_fwd_bwd": (I, [V, I, V, I, V, I, I, I, F, F, F, V, V, I, V, I, V, V]),

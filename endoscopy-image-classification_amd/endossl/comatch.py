@@ -14,7 +14,9 @@ evaluate_one, save_checkpoint, load_checkpoint, fit) plus `step(batch)`.  One st
          L_u = focal(logits_s0 | p, mask)                         (:215-220)
          losses = L_x + LAMBDA_U L_u + LAMBDA_C L_c               (:222)
   bwd    heads backward -> dL/dfts -> trunk backward over every image (BN1d couples the rows)
-  comm   RCCL all-reduce of the flat grad (data-parallel only; per-rank BN / DA / graph statistics)
+  comm   data-parallel only: all-reduce of the DA batch mean (C floats) and all-gather of the bank
+         rows, so every rank holds the same DA history and bank; RCCL all-reduce of the flat grad.
+         BatchNorm1d statistics and the contrastive graph stay per rank (DDP without SyncBN)
   opt    Adam + parameter EMA in one sweep, EMA of the BatchNorm buffers, lr_scheduler.step_update
 
 Reference behaviour kept on purpose: `train_one` walks the whole unlabeled
@@ -115,14 +117,31 @@ class CoMatch(FixMatch):
              ptr(dl), C, ptr(stats[0:1]), s)
         self._hist_pos = (self._hist_pos + 1) % HIST_CAP
         self._hist_len = min(self._hist_len + 1, HIST_CAP)
-        call("es_comatch_pseudo", ptr(lw), C, btu, C, ptr(self.prob_hist), HIST_CAP, self._hist_len,
-             self._hist_pos, ptr(zw), L, L, ptr(self.queue_feats), ptr(self.queue_probs), self.queue_size,
-             self.temperature, self.alpha, float(cfg.TRAIN.THRES), ptr(W["probs"]), ptr(W["probs_orig"]),
-             ptr(W["pl"]), ptr(W["mask"]), ptr(W["ws_p"]), s)
-        if bt + btu == self.queue_size:  # code/comatch.py:192-196
-            call("es_comatch_bank_write", ptr(zw), L, btu, ptr(zx), L, bt, L, ptr(W["probs_orig"]), ptr(targets_x), C,
-                 ptr(self.queue_feats), ptr(self.queue_probs), self.queue_ptr, self.queue_size, s)
-            self.queue_ptr = (self.queue_ptr + bt + btu) % self.queue_size
+        world = dist.world_size()
+        hist_given = 0
+        if world > 1:  # DA over the global batch: the ranks' batch means, averaged (equal shards)
+            row = self.prob_hist[self._hist_pos]
+            call("es_softmax_colmean", ptr(lw), C, btu, C, ptr(row), s)
+            dist.allreduce_mean_(row)
+            hist_given = 1
+        call("es_comatch_pseudo_ex", ptr(lw), C, btu, C, ptr(self.prob_hist), HIST_CAP, self._hist_len,
+             self._hist_pos, hist_given, ptr(zw), L, L, ptr(self.queue_feats), ptr(self.queue_probs),
+             self.queue_size, self.temperature, self.alpha, float(cfg.TRAIN.THRES), ptr(W["probs"]),
+             ptr(W["probs_orig"]), ptr(W["pl"]), ptr(W["mask"]), ptr(W["ws_p"]), s)
+        n = world * (bt + btu)  # code/comatch.py:192: the (global) batch against the queue size
+        if n == self.queue_size:  # code/comatch.py:192-196
+            if world == 1:
+                call("es_comatch_bank_write", ptr(zw), L, btu, ptr(zx), L, bt, L, ptr(W["probs_orig"]),
+                     ptr(targets_x), C, ptr(self.queue_feats), ptr(self.queue_probs), self.queue_ptr,
+                     self.queue_size, s)
+            else:  # every rank writes every rank's rows, in rank order: identical banks
+                zw_a, zx_a = dist.all_gather_cat(zw.contiguous()), dist.all_gather_cat(zx.contiguous())
+                po_a, y_a = dist.all_gather_cat(W["probs_orig"]), dist.all_gather_cat(targets_x)
+                for r in range(world):
+                    call("es_comatch_bank_write", ptr(zw_a[r * btu:]), L, btu, ptr(zx_a[r * bt:]), L, bt, L,
+                         ptr(po_a[r * btu:]), ptr(y_a[r * bt:]), C, ptr(self.queue_feats), ptr(self.queue_probs),
+                         self.queue_ptr + r * (bt + btu), self.queue_size, s)
+            self.queue_ptr = (self.queue_ptr + n) % self.queue_size
         call("es_comatch_contrastive_fwd_bwd", ptr(z0), L, ptr(z1), L, ptr(W["probs"]), btu, L, C, self.temperature,
              self.contrast_th, lam_c / btu, ptr(stats[2:3]), ptr(dz[bt + btu:]), L, ptr(dz[bt + 2 * btu:]), L,
              ptr(W["ws_c"]), s)

@@ -1,7 +1,9 @@
 """Data-parallel plumbing: one process per GPU, torch.distributed over RCCL ("nccl" backend on
 ROCm) on the GPU box, gloo for the CPU tests.  The reference is single-device; the
 only exchange the FixMatch/ViT step needs is the mean of the flat fp32 gradient buffer
-(rows are independent, loss terms are per-row means over equal shards)."""
+(rows are independent, loss terms are per-row means over equal shards).  CoMatch adds two small
+exchanges (comatch.py): the distribution-alignment batch mean (all-reduce of C floats) and the
+memory-bank rows (all-gather), so every rank holds the same DA history and the same bank."""
 import os
 
 import torch
@@ -45,6 +47,30 @@ def allreduce_sum_(t):
     if w > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return 1.0 / w
+
+
+def allreduce_mean_(t):
+    """In-place mean over ranks (CoMatch's distribution-alignment batch mean)."""
+    w = world_size()
+    if w > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t.mul_(1.0 / w)
+    return t
+
+
+def all_gather_cat(t):
+    """[world * n, ...] concatenation of every rank's t in rank order (CoMatch's bank rows)."""
+    w = world_size()
+    if w == 1:
+        return t
+    t = t.contiguous()
+    if dist.get_backend() == "gloo":  # CPU tests: list form
+        parts = [torch.empty_like(t) for _ in range(w)]
+        dist.all_gather(parts, t)
+        return torch.cat(parts)
+    out = torch.empty((w * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t)
+    return out
 
 
 def barrier():

@@ -132,6 +132,14 @@ int es_comatch_pseudo(const float* logits_w, int ldl, int nu, int C, float* hist
                       int hist_pos, const float* z_w, int ldz, int L, const float* bank_feats, const float* bank_probs,
                       int Q, float temperature, float alpha, float thres, float* probs, float* probs_orig, int* pl,
                       float* mask, float* workspace, hipStream_t stream);
+/* as es_comatch_pseudo; hist_given = 1: hist[hist_pos] already holds the step's batch mean (the
+ * data-parallel path writes the all-ranks mean there: es_softmax_colmean + all-reduce) */
+int es_comatch_pseudo_ex(const float* logits_w, int ldl, int nu, int C, float* hist, int hist_cap, int hist_len,
+                         int hist_pos, int hist_given, const float* z_w, int ldz, int L, const float* bank_feats,
+                         const float* bank_probs, int Q, float temperature, float alpha, float thres, float* probs,
+                         float* probs_orig, int* pl, float* mask, float* workspace, hipStream_t stream);
+/* out[c] = mean over rows of softmax(logits)[c], C <= 32 (the DA batch mean) */
+int es_softmax_colmean(const float* logits, int ldl, int n, int C, float* out, hipStream_t stream);
 /* ring write of [z_w; z_x] and [probs_orig; onehot(y)] at bank row ptr (code/comatch.py:187-196) */
 int es_comatch_bank_write(const float* z_w, int ldzw, int nu, const float* z_x, int ldzx, int bt, int L,
                           const float* probs_orig, const void* y_int64, int C, float* bank_feats, float* bank_probs,

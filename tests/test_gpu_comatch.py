@@ -179,6 +179,34 @@ def test_comatch_pseudo_vs_reference_formula(Q, zero_bank):
     assert torch.equal(mask.bool()[okm], (sc >= thres)[okm])
 
 
+def test_softmax_colmean_and_given_history():
+    """The data-parallel DA path: es_softmax_colmean = mean softmax, and es_comatch_pseudo_ex with
+    hist_given = 1 uses the caller's hist[pos] instead of the local batch mean."""
+    torch.manual_seed(17)
+    nu, C, L, Q = 96, 23, 64, 640
+    lw = torch.randn(nu, C, device=DEV) * 4
+    out = torch.empty(C, device=DEV)
+    call("es_softmax_colmean", ptr(lw), C, nu, C, ptr(out), S())
+    torch.testing.assert_close(out, torch.softmax(lw.double(), 1).mean(0).float(), rtol=1e-5, atol=1e-7)
+    zw = _unit(torch.randn(nu, L, device=DEV))
+    bf, bp = _unit(torch.randn(Q, L, device=DEV)), torch.softmax(torch.randn(Q, C, device=DEV), -1)
+    ws = torch.zeros(_lib.load().es_comatch_pseudo_workspace(nu, C, Q), device=DEV)
+    given = torch.softmax(torch.randn(C, device=DEV), -1)  # e.g. the all-ranks mean
+    res = []
+    for flag in (0, 1):
+        hist = torch.zeros(32, C, device=DEV)
+        hist[0] = given
+        probs, porig = torch.zeros(nu, C, device=DEV), torch.zeros(nu, C, device=DEV)
+        pl, mask = torch.zeros(nu, dtype=torch.int32, device=DEV), torch.zeros(nu, device=DEV)
+        call("es_comatch_pseudo_ex", ptr(lw), C, nu, C, ptr(hist), 32, 1, 0, flag, ptr(zw), L, L, ptr(bf), ptr(bp), Q,
+             0.2, 0.9, 0.5, ptr(probs), ptr(porig), ptr(pl), ptr(mask), ptr(ws), S())
+        res.append((hist[0].clone(), porig.clone()))
+    torch.testing.assert_close(res[0][0], out)          # recomputed from the local rows
+    torch.testing.assert_close(res[1][0], given)        # kept as given
+    p = torch.softmax(lw.double(), 1) / given.double()
+    torch.testing.assert_close(res[1][1].double(), p / p.sum(1, keepdim=True), rtol=1e-5, atol=1e-7)
+
+
 def test_comatch_bank_write():
     torch.manual_seed(2)
     nu, bt, L, C, Q, ptr0 = 14, 2, 16, 23, 48, 16
