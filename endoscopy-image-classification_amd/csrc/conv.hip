@@ -33,44 +33,89 @@ struct ConvGeom {
 
 constexpr int CBK = 16;
 
+// Every implicit-GEMM kernel below runs 256 threads over a 16-deep K (or pixel) step.  The gathers
+// avoid per-element integer division: a thread's K lane (ki = tid & 15) is fixed, so its (ci, kx, ky)
+// decomposition is advanced incrementally by 16 per step; its rows' (n, h, w) decompositions are
+// computed once before the K loop.
+
+// k -> (c, kx, ky) with c fastest (NHWC-contiguous gathers), advanced by `step` per K step
+struct KWalk {
+  int c, kx, ky, t2;  // t2 = ky * kw + kx
+  __device__ void init(int k, int C, int kw) {
+    c = k % C;
+    t2 = k / C;
+    kx = t2 % kw;
+    ky = t2 / kw;
+  }
+  __device__ void advance(int step, int C, int kw) {
+    c += step;
+    while (c >= C) {
+      c -= C;
+      ++t2;
+      if (++kx == kw) {
+        kx = 0;
+        ++ky;
+      }
+    }
+  }
+};
+
 // ---- forward: y[n,ho,wo,co] = bias[co] + sum_{ky,kx,ci} x[n, ho*s-p+ky, wo*s-p+kx, ci] w[co,ci,ky,kx]
-// GEMM rows m = (n, ho, wo), cols co, K = (ky, kx, ci) (ci fastest: NHWC-contiguous gathers).
+// GEMM rows m = (n, ho, wo), cols co, K = (ky, kx, ci).
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                        const float* __restrict__ bias, float* __restrict__ y,
                                                        ConvGeom g, int accumulate) {
-  constexpr int TX = BN / 4, TM = BM * BN / 1024;
+  constexpr int TX = BN / 4, TM = BM * BN / 1024, APR = BM / 16, BPR = BN / 16;
   __shared__ float As[CBK][BM + 1];
   __shared__ float Bs[CBK][BN + 4];
   const int M = g.N * g.Ho * g.Wo, K = g.kh * g.kw * g.Cin, KK = g.kh * g.kw;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+  const int ki = tid & 15, r16 = tid >> 4;
+  long abase[APR];
+  int ahb[APR], awb[APR];
+#pragma unroll
+  for (int j = 0; j < APR; ++j) {
+    const int m = m0 + r16 + 16 * j;
+    if (m < M) {
+      const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
+      abase[j] = n * g.sxn;
+      ahb[j] = ho * g.stride - g.pad;
+      awb[j] = wo * g.stride - g.pad;
+    } else {
+      abase[j] = 0;
+      ahb[j] = -(1 << 28);
+      awb[j] = 0;
+    }
+  }
+  long bbase[BPR];
+#pragma unroll
+  for (int j = 0; j < BPR; ++j) {
+    const int co = n0 + r16 + 16 * j;
+    bbase[j] = co < g.Cout ? (long)co * g.Cin * KK : -1;
+  }
+  KWalk kw;
+  kw.init(ki, g.Cin, g.kw);
   float acc[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   for (int k0 = 0; k0 < K; k0 += CBK) {
-    for (int e = tid; e < BM * CBK; e += 256) {
-      const int mi = e / CBK, ki = e % CBK, m = m0 + mi, k = k0 + ki;
+    const bool kok = k0 + ki < K;
+#pragma unroll
+    for (int j = 0; j < APR; ++j) {
+      const int h = ahb[j] + kw.ky, ww = awb[j] + kw.kx;
       float v = 0.f;
-      if (m < M && k < K) {
-        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
-        const int ci = k % g.Cin, t2 = k / g.Cin, kx = t2 % g.kw, ky = t2 / g.kw;
-        const int h = ho * g.stride - g.pad + ky, ww = wo * g.stride - g.pad + kx;
-        if (h >= 0 && h < g.H && ww >= 0 && ww < g.W) v = x[n * g.sxn + h * g.sxh + ww * g.sxw + ci * g.sxc];
-      }
-      As[ki][mi] = v;
+      if (kok && (unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W)
+        v = x[abase[j] + h * g.sxh + ww * g.sxw + kw.c * g.sxc];
+      As[ki][r16 + 16 * j] = v;
     }
-    for (int e = tid; e < CBK * BN; e += 256) {
-      const int ki = e / BN, ni = e % BN, k = k0 + ki, co = n0 + ni;
-      float v = 0.f;
-      if (k < K && co < g.Cout) {
-        const int ci = k % g.Cin, t2 = k / g.Cin;  // t2 = ky*kw + kx
-        v = w[((long)co * g.Cin + ci) * KK + t2];
-      }
-      Bs[ki][ni] = v;
-    }
+#pragma unroll
+    for (int j = 0; j < BPR; ++j)
+      Bs[ki][r16 + 16 * j] = (kok && bbase[j] >= 0) ? w[bbase[j] + (long)kw.c * KK + kw.t2] : 0.f;
+    kw.advance(CBK, g.Cin, g.kw);
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < CBK; ++kk) {
@@ -108,41 +153,62 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void conv_dx_kernel(const float* __restrict__ dy, const float* __restrict__ w,
                                                       float* __restrict__ dx, ConvGeom g, int accumulate) {
-  constexpr int TX = BN / 4, TM = BM * BN / 1024;
+  constexpr int TX = BN / 4, TM = BM * BN / 1024, APR = BM / 16, BPR = BN / 16;
   __shared__ float As[CBK][BM + 1];
   __shared__ float Bs[CBK][BN + 4];
   const int M = g.N * g.H * g.W, K = g.kh * g.kw * g.Cout, KK = g.kh * g.kw;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+  const int ki = tid & 15, r16 = tid >> 4;
+  const int s = g.stride;
+  long abase[APR];
+  int ahp[APR], awp[APR];
+#pragma unroll
+  for (int j = 0; j < APR; ++j) {
+    const int m = m0 + r16 + 16 * j;
+    if (m < M) {
+      const int ww = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
+      abase[j] = n * g.syn;
+      ahp[j] = h + g.pad;
+      awp[j] = ww + g.pad;
+    } else {
+      abase[j] = 0;
+      ahp[j] = -(1 << 28);
+      awp[j] = 0;
+    }
+  }
+  int bci[BPR];
+#pragma unroll
+  for (int j = 0; j < BPR; ++j) bci[j] = n0 + r16 + 16 * j;
+  KWalk kw;
+  kw.init(ki, g.Cout, g.kw);
   float acc[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   for (int k0 = 0; k0 < K; k0 += CBK) {
-    for (int e = tid; e < BM * CBK; e += 256) {
-      const int mi = e / CBK, ki = e % CBK, m = m0 + mi, k = k0 + ki;
+    const bool kok = k0 + ki < K;
+#pragma unroll
+    for (int j = 0; j < APR; ++j) {
+      const int hn = ahp[j] - kw.ky, wn = awp[j] - kw.kx;
       float v = 0.f;
-      if (m < M && k < K) {
-        const int ww = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
-        const int co = k % g.Cout, t2 = k / g.Cout, kx = t2 % g.kw, ky = t2 / g.kw;
-        const int hn = h + g.pad - ky, wn = ww + g.pad - kx;
-        if (hn >= 0 && wn >= 0 && hn % g.stride == 0 && wn % g.stride == 0) {
-          const int ho = hn / g.stride, wo = wn / g.stride;
-          if (ho < g.Ho && wo < g.Wo) v = dy[n * g.syn + ho * g.syh + wo * g.syw + co];
+      if (kok && hn >= 0 && wn >= 0) {
+        int ho = hn, wo = wn;
+        bool ok = true;
+        if (s != 1) {
+          ok = (hn % s == 0) && (wn % s == 0);
+          ho = hn / s;
+          wo = wn / s;
         }
+        if (ok && ho < g.Ho && wo < g.Wo) v = dy[abase[j] + ho * g.syh + wo * g.syw + kw.c];
       }
-      As[ki][mi] = v;
+      As[ki][r16 + 16 * j] = v;
     }
-    for (int e = tid; e < CBK * BN; e += 256) {
-      const int ki = e / BN, ni = e % BN, k = k0 + ki, ci = n0 + ni;
-      float v = 0.f;
-      if (k < K && ci < g.Cin) {
-        const int co = k % g.Cout, t2 = k / g.Cout;
-        v = w[((long)co * g.Cin + ci) * KK + t2];
-      }
-      Bs[ki][ni] = v;
-    }
+#pragma unroll
+    for (int j = 0; j < BPR; ++j)
+      Bs[ki][r16 + 16 * j] = (kok && bci[j] < g.Cin) ? w[((long)kw.c * g.Cin + bci[j]) * KK + kw.t2] : 0.f;
+    kw.advance(CBK, g.Cout, g.kw);
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < CBK; ++kk) {
@@ -175,44 +241,83 @@ __global__ __launch_bounds__(256) void conv_dx_kernel(const float* __restrict__ 
   }
 }
 
+// pixel index m -> (n, ho, wo), advanced by d (small) without division
+struct PWalk {
+  int n, ho, wo;
+  __device__ void init(int m, int Ho, int Wo) {
+    wo = m % Wo;
+    const int t = m / Wo;
+    ho = t % Ho;
+    n = t / Ho;
+  }
+  __device__ void advance(int d, int Ho, int Wo) {
+    wo += d;
+    while (wo >= Wo) {
+      wo -= Wo;
+      if (++ho == Ho) {
+        ho = 0;
+        ++n;
+      }
+    }
+  }
+};
+
 // ---- weight gradient partials: P[split][co][k'] = sum_{m in split} dy[m, co] A[m, k'],
 // k' = (ci, ky, kx) (the weight's own layout), A = im2col(x).  Rows co, cols k', reduction over the
-// output pixels m of this split (16 per step).
+// output pixels m of this split (16 per step).  A thread owns one co column of the dy tile and one k'
+// column of the im2col tile; its pixels are walked incrementally.
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void conv_dw_kernel(const float* __restrict__ x, const float* __restrict__ dy,
                                                       float* __restrict__ P, ConvGeom g, int mchunk) {
   constexpr int TX = BN / 4, TM = BM * BN / 1024;
+  constexpr int AROWS = 256 / BM, APR = 16 / AROWS;  // dy tile: pixel rows per pass, passes
+  constexpr int BROWS = 256 / BN, BPR = 16 / BROWS;  // im2col tile
   __shared__ float As[CBK][BM + 1];  // dy^T  [m][co]
   __shared__ float Bs[CBK][BN + 4];  // im2col [m][k']
   const int M = g.N * g.Ho * g.Wo, KK = g.kh * g.kw, K = g.Cin * KK;
   const int c0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = blockIdx.z;
   const int mb = split * mchunk, me = min(mb + mchunk, M);
   const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
+  const int aco = c0 + tid % BM, arow = tid / BM;
+  const int bk = n0 + tid % BN, brow = tid / BN;
+  int bci = 0, bky = 0, bkx = 0;
+  const bool bkok = bk < K;
+  if (bkok) {
+    bci = bk / KK;
+    const int t2 = bk % KK;
+    bkx = t2 % g.kw;
+    bky = t2 / g.kw;
+  }
+  PWalk pa[APR], pb[BPR];
+#pragma unroll
+  for (int j = 0; j < APR; ++j) pa[j].init(mb + arow + AROWS * j, g.Ho, g.Wo);
+#pragma unroll
+  for (int j = 0; j < BPR; ++j) pb[j].init(mb + brow + BROWS * j, g.Ho, g.Wo);
   float acc[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
   for (int mm = mb; mm < me; mm += CBK) {
-    for (int e = tid; e < BM * CBK; e += 256) {
-      const int mi = e / BM, ci = e % BM, m = mm + mi, co = c0 + ci;  // co fastest: contiguous dy
+#pragma unroll
+    for (int j = 0; j < APR; ++j) {
+      const int m = mm + arow + AROWS * j;
       float v = 0.f;
-      if (m < me && co < g.Cout) {
-        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
-        v = dy[n * g.syn + ho * g.syh + wo * g.syw + co];
-      }
-      As[mi][ci] = v;
+      if (m < me && aco < g.Cout) v = dy[pa[j].n * g.syn + pa[j].ho * g.syh + pa[j].wo * g.syw + aco];
+      As[arow + AROWS * j][tid % BM] = v;
+      pa[j].advance(CBK, g.Ho, g.Wo);
     }
-    for (int e = tid; e < CBK * BN; e += 256) {
-      const int mi = e / BN, ni = e % BN, m = mm + mi, k = n0 + ni;
+#pragma unroll
+    for (int j = 0; j < BPR; ++j) {
+      const int m = mm + brow + BROWS * j;
       float v = 0.f;
-      if (m < me && k < K) {
-        const int wo = m % g.Wo, t = m / g.Wo, ho = t % g.Ho, n = t / g.Ho;
-        const int ci = k / KK, t2 = k % KK, kx = t2 % g.kw, ky = t2 / g.kw;
-        const int h = ho * g.stride - g.pad + ky, ww = wo * g.stride - g.pad + kx;
-        if (h >= 0 && h < g.H && ww >= 0 && ww < g.W) v = x[n * g.sxn + h * g.sxh + ww * g.sxw + ci * g.sxc];
+      if (m < me && bkok) {
+        const int h = pb[j].ho * g.stride - g.pad + bky, ww = pb[j].wo * g.stride - g.pad + bkx;
+        if ((unsigned)h < (unsigned)g.H && (unsigned)ww < (unsigned)g.W)
+          v = x[pb[j].n * g.sxn + h * g.sxh + ww * g.sxw + bci * g.sxc];
       }
-      Bs[mi][ni] = v;
+      Bs[brow + BROWS * j][tid % BN] = v;
+      pb[j].advance(CBK, g.Ho, g.Wo);
     }
     __syncthreads();
 #pragma unroll
