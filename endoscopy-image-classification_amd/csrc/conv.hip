@@ -363,120 +363,245 @@ __global__ void sum_slabs_kernel(const float* __restrict__ P, float* __restrict_
 }
 
 // ---- per-channel reductions over the rows of a [rows, C] view: row r at (r / HW) * sn + (r % HW) * sp.
-// One workgroup per row chunk writes partial[block][c]; a second pass sums the blocks.
+// One workgroup per row chunk writes partial[block][c]; chan_final_kernel sums the blocks.
 struct RowMap {
   long sn, sp;
   int HW;
 };
-__device__ __forceinline__ long row_off(const RowMap& rm, int r) { return (long)(r / rm.HW) * rm.sn + (long)(r % rm.HW) * rm.sp; }
+
+// VEC consecutive floats (VEC = 4: one 16-byte load)
+template <int VEC>
+__device__ __forceinline__ void ldv(const float* __restrict__ p, float (&o)[VEC]) {
+  if constexpr (VEC == 4) {
+    const f32x4 t = *(const f32x4*)p;
+    o[0] = t[0]; o[1] = t[1]; o[2] = t[2]; o[3] = t[3];
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = p[j];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = v[j];
+  }
+}
 
 // MODE 0: sum v;  MODE 1: sum (v - mean[c])^2;  MODE 2: sum g, sum g * xhat  (g = dy * [y > 0 if relu],
-// xhat = (x - mean) * rstd), written as partial[block][c] and partial[block][C + c]
-template <int MODE>
+// xhat = (x - mean) * rstd), written as partial[block][c] and partial[block][C + c].
+// A thread owns VEC channels and walks every rp-th row of the block's chunk; contiguous views
+// (sn = HW * sp, every BatchNorm) take 4 rows per iteration so 4 (MODE 2: 12) loads are in flight.
+template <int MODE, int VEC>
 __global__ __launch_bounds__(256) void chan_partial_kernel(const float* __restrict__ v, RowMap rm, int rows, int C,
                                                            int rows_per, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, const float* __restrict__ dy,
                                                            const float* __restrict__ y, int relu,
                                                            float* __restrict__ partial) {
-  __shared__ float red[256];
-  __shared__ float red2[256];
-  const int cpp = C < 256 ? C : 256;  // columns per pass
-  const int rp = 256 / cpp;           // row lanes
+  __shared__ float red[256 * VEC];
+  __shared__ float red2[MODE == 2 ? 256 * VEC : 1];
+  const int CV = C / VEC;
+  const int cpp = CV < 256 ? CV : 256;  // vector columns per pass
+  const int rp = 256 / cpp;             // row lanes
   const int t = threadIdx.x, cc = t % cpp, rl = t / cpp;
   const int r0 = blockIdx.x * rows_per, r1 = min(r0 + rows_per, rows);
-  for (int c0 = 0; c0 < C; c0 += cpp) {
-    const int c = c0 + cc;
-    float s = 0.f, s2 = 0.f;
-    if (rl < rp && c < C) {
-      const float mu = (MODE >= 1) ? mean[c] : 0.f;
-      const float rs = (MODE == 2) ? rstd[c] : 0.f;
-      for (int r = r0 + rl; r < r1; r += rp) {
-        const long o = row_off(rm, r) + c;
-        if (MODE == 0) {
-          s += v[o];
-        } else if (MODE == 1) {
-          const float d = v[o] - mu;
-          s = fmaf(d, d, s);
+  const bool contig = rm.sn == (long)rm.HW * rm.sp;
+  for (int c0 = 0; c0 < CV; c0 += cpp) {
+    const int cv = c0 + cc, c = cv * VEC;
+    float s[VEC], s2[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) s[j] = s2[j] = 0.f;
+    if (rl < rp && cv < CV) {
+      float mu[VEC], rs[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) {
+        mu[j] = MODE >= 1 ? mean[c + j] : 0.f;
+        rs[j] = MODE == 2 ? rstd[c + j] : 0.f;
+      }
+      auto acc = [&](long o) {
+        float a[VEC];
+        ldv<VEC>(v + o, a);
+        if constexpr (MODE == 0) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) s[j] += a[j];
+        } else if constexpr (MODE == 1) {
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) {
+            const float d = a[j] - mu[j];
+            s[j] = fmaf(d, d, s[j]);
+          }
         } else {
-          float gg = dy[o];
-          if (relu && !(y[o] > 0.f)) gg = 0.f;
-          s += gg;
-          s2 = fmaf(gg, (v[o] - mu) * rs, s2);
+          float gd[VEC], yy[VEC];
+          ldv<VEC>(dy + o, gd);
+          if (relu) ldv<VEC>(y + o, yy);
+#pragma unroll
+          for (int j = 0; j < VEC; ++j) {
+            const float gg = (relu && !(yy[j] > 0.f)) ? 0.f : gd[j];
+            s[j] += gg;
+            s2[j] = fmaf(gg, (a[j] - mu[j]) * rs[j], s2[j]);
+          }
+        }
+      };
+      int r = r0 + rl;
+      if (contig) {
+        for (; r + 3 * rp < r1; r += 4 * rp) {
+          acc((long)r * rm.sp + c);
+          acc((long)(r + rp) * rm.sp + c);
+          acc((long)(r + 2 * rp) * rm.sp + c);
+          acc((long)(r + 3 * rp) * rm.sp + c);
+        }
+        for (; r < r1; r += rp) acc((long)r * rm.sp + c);
+      } else {
+        int n = r / rm.HW, p = r - n * rm.HW;
+        for (; r < r1; r += rp) {
+          acc((long)n * rm.sn + (long)p * rm.sp + c);
+          p += rp;
+          while (p >= rm.HW) {
+            p -= rm.HW;
+            ++n;
+          }
         }
       }
     }
-    red[t] = s;
-    red2[t] = s2;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      red[t * VEC + j] = s[j];
+      if constexpr (MODE == 2) red2[t * VEC + j] = s2[j];
+    }
     __syncthreads();
-    if (t < cpp && c0 + t < C) {
+    for (int q = t; q < cpp * VEC && c0 * VEC + q < C; q += 256) {
+      const int col = q / VEC, j = q % VEC;
       float a = 0.f, b = 0.f;
-      for (int j = 0; j < rp; ++j) {
-        a += red[j * cpp + t];
-        b += red2[j * cpp + t];
+      for (int l = 0; l < rp; ++l) {
+        a += red[(l * cpp + col) * VEC + j];
+        if constexpr (MODE == 2) b += red2[(l * cpp + col) * VEC + j];
       }
-      partial[(long)blockIdx.x * (MODE == 2 ? 2 * C : C) + c0 + t] = a;
-      if (MODE == 2) partial[(long)blockIdx.x * 2 * C + C + c0 + t] = b;
+      partial[(long)blockIdx.x * (MODE == 2 ? 2 * C : C) + c0 * VEC + q] = a;
+      if constexpr (MODE == 2) partial[(long)blockIdx.x * 2 * C + C + c0 * VEC + q] = b;
     }
     __syncthreads();
   }
 }
 
-// BatchNorm statistics from the partials: mean (MODE 0 result / rows) and, after the second pass,
-// rstd = 1/sqrt(var_biased + eps); running stats <- (1-m) r + m (mean, var_unbiased)  (nn.BatchNorm2d)
-__global__ void bn_mean_kernel(const float* __restrict__ partial, int G, int C, int rows, float* __restrict__ mean) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Second pass over the partials P[G][ncols]: 16 columns x 16 block lanes per workgroup, lanes
+// summed in a fixed order (deterministic).  FIN selects what the column sum s becomes:
+//   0  out[c] (+)= s                                        (bias gradients)
+//   1  out[c] = s / rows                                    (BatchNorm batch mean)
+//   2  out[c] = 1 / sqrt(s / rows + eps); running stats <- (1 - m) r + m (mean, s / (rows - 1))
+//   3  out3[c] = s (when given); c < half: out[c] (+)= s, else out2[c - half] (+)= s
+struct ChanFin {
+  float *out, *out2, *out3;
+  const float* mean;
+  float *run_mean, *run_var;
+  float eps, momentum;
+  int rows, half, accumulate;
+};
+template <int FIN>
+__global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict__ P, int G, int ncols, ChanFin f) {
+  __shared__ float red[16][17];
+  const int t = threadIdx.x, cl = t & 15, gl = t >> 4;
+  const int c = blockIdx.x * 16 + cl;
   float s = 0.f;
-  for (int gI = 0; gI < G; ++gI) s += partial[(long)gI * C + c];
-  mean[c] = s / (float)rows;
-}
-__global__ void bn_var_kernel(const float* __restrict__ partial, int G, int C, int rows, float eps,
-                              const float* __restrict__ mean, float* __restrict__ rstd, float* __restrict__ run_mean,
-                              float* __restrict__ run_var, float momentum) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float s = 0.f;
-  for (int gI = 0; gI < G; ++gI) s += partial[(long)gI * C + c];
-  const float var = s / (float)rows;
-  rstd[c] = 1.0f / sqrtf(var + eps);
-  if (run_mean) {
-    const float unb = rows > 1 ? s / (float)(rows - 1) : var;
-    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mean[c];
-    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  if (c < ncols)
+    for (int gI = gl; gI < G; gI += 16) s += P[(long)gI * ncols + c];
+  red[gl][cl] = s;
+  __syncthreads();
+  if (gl != 0 || c >= ncols) return;
+  s = 0.f;
+#pragma unroll
+  for (int l = 0; l < 16; ++l) s += red[l][cl];
+  if constexpr (FIN == 0) {
+    f.out[c] = f.accumulate ? f.out[c] + s : s;
+  } else if constexpr (FIN == 1) {
+    f.out[c] = s / (float)f.rows;
+  } else if constexpr (FIN == 2) {
+    const float var = s / (float)f.rows;
+    f.out[c] = 1.0f / sqrtf(var + f.eps);
+    if (f.run_mean) {
+      const float unb = f.rows > 1 ? s / (float)(f.rows - 1) : var;
+      f.run_mean[c] = (1.f - f.momentum) * f.run_mean[c] + f.momentum * f.mean[c];
+      f.run_var[c] = (1.f - f.momentum) * f.run_var[c] + f.momentum * unb;
+    }
+  } else {
+    if (f.out3) f.out3[c] = s;
+    float* o = c < f.half ? f.out + c : f.out2 + (c - f.half);
+    *o = f.accumulate ? *o + s : s;
   }
 }
 __global__ void nbt_inc_kernel(int64_t* nbt) { *nbt += 1; }
 
-// y = (x - mean) * rstd * gamma + beta (+ res) (relu); eval: rstd from the running variance
-__global__ void bn_apply_kernel(const float* __restrict__ x, long n, int C, const float* __restrict__ mean,
+// y = (x - mean) * rstd * gamma + beta (+ res) (relu); eval: rstd from the running variance.
+// nv = elements / VEC, CV = C / VEC (32-bit index arithmetic: the host checks nv < 2^31)
+template <int VEC>
+__global__ void bn_apply_kernel(const float* __restrict__ x, int nv, int CV, const float* __restrict__ mean,
                                 const float* __restrict__ rstd, const float* __restrict__ rvar, float eps,
                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                 const float* __restrict__ res, int relu, float* __restrict__ y) {
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    const float rs = rvar ? 1.0f / sqrtf(rvar[c] + eps) : rstd[c];
-    float v = (x[i] - mean[c]) * rs * gamma[c] + beta[c];
-    if (res) v += res[i];
-    if (relu) v = fmaxf(v, 0.f);
-    y[i] = v;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
+    const int c = (int)((unsigned)i % (unsigned)CV) * VEC;
+    float xv[VEC], mu[VEC], ga[VEC], be[VEC], rs[VEC], rv[VEC], o[VEC];
+    ldv<VEC>(x + (long)i * VEC, xv);
+    ldv<VEC>(mean + c, mu);
+    ldv<VEC>(gamma + c, ga);
+    ldv<VEC>(beta + c, be);
+    if (rvar) {
+      ldv<VEC>(rvar + c, rv);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) rs[j] = 1.0f / sqrtf(rv[j] + eps);
+    } else {
+      ldv<VEC>(rstd + c, rs);
+    }
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (xv[j] - mu[j]) * rs[j] * ga[j] + be[j];
+    if (res) {
+      float rr[VEC];
+      ldv<VEC>(res + (long)i * VEC, rr);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] += rr[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    stv<VEC>(y + (long)i * VEC, o);
   }
 }
 
 // dx = rstd * gamma * (g - sum(g)/P - xhat * sum(g xhat)/P); g = dy [* (y > 0)] (written to gout
 // when given: the residual branch's gradient)
+template <int VEC>
 __global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                    const float* __restrict__ y, int relu, long n, int C, int rows,
+                                    const float* __restrict__ y, int relu, int nv, int CV, int rows,
                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                     const float* __restrict__ gamma, const float* __restrict__ sums,
                                     float* __restrict__ dx, float* __restrict__ gout) {
   const float inv = 1.0f / (float)rows;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    float gg = dy[i];
-    if (relu && !(y[i] > 0.f)) gg = 0.f;
-    if (gout) gout[i] = gg;
-    const float xh = (x[i] - mean[c]) * rstd[c];
-    dx[i] = rstd[c] * gamma[c] * (gg - sums[c] * inv - xh * sums[C + c] * inv);
+  const int C = CV * VEC;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
+    const int c = (int)((unsigned)i % (unsigned)CV) * VEC;
+    float xv[VEC], gg[VEC], yy[VEC], mu[VEC], rs[VEC], ga[VEC], s0[VEC], s1[VEC], o[VEC];
+    ldv<VEC>(x + (long)i * VEC, xv);
+    ldv<VEC>(dy + (long)i * VEC, gg);
+    if (relu) {
+      ldv<VEC>(y + (long)i * VEC, yy);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (!(yy[j] > 0.f)) gg[j] = 0.f;
+    }
+    if (gout) stv<VEC>(gout + (long)i * VEC, gg);
+    ldv<VEC>(mean + c, mu);
+    ldv<VEC>(rstd + c, rs);
+    ldv<VEC>(gamma + c, ga);
+    ldv<VEC>(sums + c, s0);
+    ldv<VEC>(sums + C + c, s1);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) {
+      const float xh = (xv[j] - mu[j]) * rs[j];
+      o[j] = rs[j] * ga[j] * (gg[j] - s0[j] * inv - xh * s1[j] * inv);
+    }
+    stv<VEC>(dx + (long)i * VEC, o);
   }
 }
 
@@ -497,13 +622,13 @@ __global__ void bn_bwd_eval_kernel(const float* __restrict__ dy, const float* __
 // ---- pooling / upsampling (NHWC contiguous)
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int k, int s, int p,
                                    int Ho, int Wo, float* __restrict__ y, int8_t* __restrict__ arg) {
-  const long n_out = (long)N * Ho * Wo * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int wo = (int)(t % Wo);
-    t /= Wo;
-    const int ho = (int)(t % Ho), n = (int)(t / Ho);
+  const unsigned n_out = (unsigned)((long)N * Ho * Wo * C);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % (unsigned)C);
+    unsigned t = i / (unsigned)C;
+    const int wo = (int)(t % (unsigned)Wo);
+    t /= (unsigned)Wo;
+    const int ho = (int)(t % (unsigned)Ho), n = (int)(t / (unsigned)Ho);
     float best = -INFINITY;
     int bi = 0;
     for (int ky = 0; ky < k; ++ky) {
@@ -527,13 +652,13 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, in
 
 __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int8_t* __restrict__ arg, int N, int H, int W,
                                    int C, int k, int s, int p, int Ho, int Wo, float* __restrict__ dx) {
-  const long n_in = (long)N * H * W * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H), n = (int)(t / H);
+  const unsigned n_in = (unsigned)((long)N * H * W * C);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % (unsigned)C);
+    unsigned t = i / (unsigned)C;
+    const int w = (int)(t % (unsigned)W);
+    t /= (unsigned)W;
+    const int h = (int)(t % (unsigned)H), n = (int)(t / (unsigned)H);
     float acc = 0.f;
     const int ho_lo = max(0, (h + p - k + s) / s), ho_hi = min(Ho - 1, (h + p) / s);
     const int wo_lo = max(0, (w + p - k + s) / s), wo_hi = min(Wo - 1, (w + p) / s);
@@ -554,14 +679,14 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int8_t* _
 // AvgPool2d(k, stride k) / AdaptiveAvgPool2d(1) (k = H = W): y[n,ho,wo,c] = mean of the k x k block
 __global__ void avgpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int k, int Ho, int Wo,
                                    float* __restrict__ y) {
-  const long n_out = (long)N * Ho * Wo * C;
+  const unsigned n_out = (unsigned)((long)N * Ho * Wo * C);
   const float inv = 1.0f / (float)(k * k);
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int wo = (int)(t % Wo);
-    t /= Wo;
-    const int ho = (int)(t % Ho), n = (int)(t / Ho);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % (unsigned)C);
+    unsigned t = i / (unsigned)C;
+    const int wo = (int)(t % (unsigned)Wo);
+    t /= (unsigned)Wo;
+    const int ho = (int)(t % (unsigned)Ho), n = (int)(t / (unsigned)Ho);
     float s = 0.f;
     for (int ky = 0; ky < k; ++ky)
       for (int kx = 0; kx < k; ++kx) s += x[(((long)n * H + ho * k + ky) * W + wo * k + kx) * C + c];
@@ -570,14 +695,14 @@ __global__ void avgpool_fwd_kernel(const float* __restrict__ x, int N, int H, in
 }
 __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int H, int W, int C, int k, int Ho, int Wo,
                                    float* __restrict__ dx, int accumulate) {
-  const long n_in = (long)N * H * W * C;
+  const unsigned n_in = (unsigned)((long)N * H * W * C);
   const float inv = 1.0f / (float)(k * k);
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H), n = (int)(t / H);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % (unsigned)C);
+    unsigned t = i / (unsigned)C;
+    const int w = (int)(t % (unsigned)W);
+    t /= (unsigned)W;
+    const int h = (int)(t % (unsigned)H), n = (int)(t / (unsigned)H);
     const float v = dy[(((long)n * Ho + h / k) * Wo + w / k) * C + c] * inv;
     dx[i] = accumulate ? dx[i] + v : v;
   }
@@ -587,13 +712,13 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int H, i
 __global__ void upsample_add_fwd_kernel(const float* __restrict__ base, const float* __restrict__ src, int N, int H,
                                         int W, int C, int s, float* __restrict__ out) {
   const int h2 = H / s, w2 = W / s;
-  const long n = (long)N * H * W * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int w = (int)(t % W);
-    t /= W;
-    const int h = (int)(t % H), nn = (int)(t / H);
+  const unsigned n = (unsigned)((long)N * H * W * C);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % (unsigned)C);
+    unsigned t = i / (unsigned)C;
+    const int w = (int)(t % (unsigned)W);
+    t /= (unsigned)W;
+    const int h = (int)(t % (unsigned)H), nn = (int)(t / (unsigned)H);
     out[i] = base[i] + src[(((long)nn * h2 + h / s) * w2 + w / s) * C + c];
   }
 }
@@ -601,13 +726,13 @@ __global__ void upsample_add_fwd_kernel(const float* __restrict__ base, const fl
 __global__ void upsample_bwd_kernel(const float* __restrict__ dout, int N, int H, int W, int C, int s,
                                     float* __restrict__ dsrc) {
   const int h2 = H / s, w2 = W / s;
-  const long n = (long)N * h2 * w2 * C;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C);
-    long t = i / C;
-    const int ws = (int)(t % w2);
-    t /= w2;
-    const int hs = (int)(t % h2), nn = (int)(t / h2);
+  const unsigned n = (unsigned)((long)N * h2 * w2 * C);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c = (int)(i % (unsigned)C);
+    unsigned t = i / (unsigned)C;
+    const int ws = (int)(t % (unsigned)w2);
+    t /= (unsigned)w2;
+    const int hs = (int)(t % (unsigned)h2), nn = (int)(t / (unsigned)h2);
     float a = 0.f;
     for (int dy = 0; dy < s; ++dy)
       for (int dx = 0; dx < s; ++dx) a += dout[(((long)nn * H + hs * s + dy) * W + ws * s + dx) * C + c];
@@ -653,65 +778,86 @@ __global__ __launch_bounds__(256) void fcu_down_fwd_kernel(const float* __restri
 }
 
 // backward: dxt = dout (cls row doubled); dpooled = LN backward of dout * gelu'(z); per-block
-// partial gamma / beta gradients partial[block][0..D) / [D..2D)
+// partial gamma / beta gradients partial[block][0..D) / [D..2D).  A wave owns a row at a time with
+// its D/64 columns per lane in registers (D <= 1024): the row's gelu'(z) and xhat are computed once,
+// and the gamma / beta partials stay in registers until one LDS reduction over the 4 waves at the end.
+constexpr int FCU_NJ = 16;
 __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ pooled,
                                                            const float* __restrict__ gam, const float* __restrict__ bet,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
                                                            float* __restrict__ dxt, float* __restrict__ dpooled,
                                                            float* __restrict__ partial, int N, int np, int D,
                                                            int rows_per_block) {
-  extern __shared__ float pg[];  // [2 * D] per block
-  const int T = np + 1, wv_in_blk = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) pg[c] = 0.f;
-  __syncthreads();
+  extern __shared__ float pg[];  // [4 waves][2 * D]
+  const int T = np + 1, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float ga[FCU_NJ], be[FCU_NJ], pgw[FCU_NJ], pbw[FCU_NJ];
+#pragma unroll
+  for (int j = 0; j < FCU_NJ; ++j) {
+    const int c = j * 64 + lane;
+    ga[j] = c < D ? gam[c] : 0.f;
+    be[j] = c < D ? bet[c] : 0.f;
+    pgw[j] = pbw[j] = 0.f;
+  }
   const int r0 = blockIdx.x * rows_per_block, r1 = min(r0 + rows_per_block, N * T);
-  for (int row = r0 + wv_in_blk; row < r1; row += 4) {
-    const int n = row / T, tk = row % T;
+  for (int row = r0 + wv; row < r1; row += 4) {
+    const int n = row / T, tk = row - n * T;
     const float* dr = dout + (long)row * D;
     float* xr = dxt + (long)row * D;
+    float d[FCU_NJ];
+#pragma unroll
+    for (int j = 0; j < FCU_NJ; ++j) {
+      const int c = j * 64 + lane;
+      d[j] = c < D ? dr[c] : 0.f;
+    }
     if (tk == 0) {
-      for (int c = lane; c < D; c += 64) xr[c] = 2.f * dr[c];
+#pragma unroll
+      for (int j = 0; j < FCU_NJ; ++j)
+        if (j * 64 + lane < D) xr[j * 64 + lane] = 2.f * d[j];
       continue;
     }
-    for (int c = lane; c < D; c += 64) xr[c] = dr[c];
     const long pi = (long)n * np + tk - 1;
     const float* pr = pooled + pi * D;
     const float mu = mean[pi], rs = rstd[pi];
+    float xh[FCU_NJ], gz[FCU_NJ];
     float s1 = 0.f, s2 = 0.f;
-    for (int c = lane; c < D; c += 64) {
-      const float xh = (pr[c] - mu) * rs;
-      const float z = xh * gam[c] + bet[c];
-      const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
-      const float gz = dr[c] * fmaf(z, 0.39894228040143268f * __expf(-0.5f * z * z), cdf);
-      atomicAdd(&pg[c], gz * xh);  // LDS atomics: 4 waves per block share the partial row
-      atomicAdd(&pg[D + c], gz);
-      const float gx = gz * gam[c];
-      s1 += gx;
-      s2 = fmaf(gx, xh, s2);
+#pragma unroll
+    for (int j = 0; j < FCU_NJ; ++j) {
+      const int c = j * 64 + lane;
+      if (c < D) {
+        xr[c] = d[j];
+        xh[j] = (pr[c] - mu) * rs;
+        const float z = xh[j] * ga[j] + be[j];
+        const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
+        gz[j] = d[j] * fmaf(z, 0.39894228040143268f * __expf(-0.5f * z * z), cdf);
+        pgw[j] = fmaf(gz[j], xh[j], pgw[j]);
+        pbw[j] += gz[j];
+        const float gx = gz[j] * ga[j];
+        s1 += gx;
+        s2 = fmaf(gx, xh[j], s2);
+      } else {
+        xh[j] = gz[j] = 0.f;
+      }
     }
     s1 = warp_sum(s1) / (float)D;
     s2 = warp_sum(s2) / (float)D;
     float* dp = dpooled + pi * D;
-    for (int c = lane; c < D; c += 64) {
-      const float xh = (pr[c] - mu) * rs;
-      const float z = xh * gam[c] + bet[c];
-      const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
-      const float gz = dr[c] * fmaf(z, 0.39894228040143268f * __expf(-0.5f * z * z), cdf);
-      dp[c] = rs * (gz * gam[c] - s1 - xh * s2);
+#pragma unroll
+    for (int j = 0; j < FCU_NJ; ++j) {
+      const int c = j * 64 + lane;
+      if (c < D) dp[c] = rs * (gz[j] * ga[j] - s1 - xh[j] * s2);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < FCU_NJ; ++j) {
+    const int c = j * 64 + lane;
+    if (c < D) {
+      pg[wv * 2 * D + c] = pgw[j];
+      pg[wv * 2 * D + D + c] = pbw[j];
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x) partial[(long)blockIdx.x * 2 * D + c] = pg[c];
-}
-
-__global__ void fcu_param_reduce_kernel(const float* __restrict__ partial, int G, int D, float* __restrict__ dw,
-                                        float* __restrict__ db, int accumulate) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * D) return;
-  float s = 0.f;
-  for (int gI = 0; gI < G; ++gI) s += partial[(long)gI * 2 * D + c];
-  float* o = c < D ? dw + c : db + (c - D);
-  *o = accumulate ? *o + s : s;
+  for (int c = threadIdx.x; c < 2 * D; c += blockDim.x)
+    partial[(long)blockIdx.x * 2 * D + c] = (pg[c] + pg[2 * D + c]) + (pg[4 * D + c] + pg[6 * D + c]);
 }
 
 __global__ void tokens_cls_set_kernel(float* __restrict__ xt, int N, int T, int D, const float* __restrict__ cls) {
@@ -720,6 +866,10 @@ __global__ void tokens_cls_set_kernel(float* __restrict__ xt, int N, int T, int 
   const int n = (int)(i / D), c = (int)(i % D);
   xt[(long)n * T * D + c] = cls[c];
 }
+
+// row groups of the per-channel reductions: ~64 rows each, at most 1024 (4 workgroups per CU)
+inline int chan_groups(int rows) { return rows < 64 * 1024 ? (rows + 63) / 64 : 1024; }
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 inline int grid1d(long n) {
   long b = (n + 255) / 256;
@@ -821,7 +971,7 @@ int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn,
 }
 
 size_t es_chan_workspace(int rows, int C) {
-  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int G = chan_groups(rows);
   return (size_t)G * 2 * C + 2 * C;
 }
 
@@ -830,12 +980,17 @@ int es_chan_sum(const float* v, int rows, int C, long sn, long sp, int HW, float
                 int accumulate, hipStream_t stream) {
   if (!v || !out || !workspace) return ES_BAD_ARG;
   if (rows <= 0 || C <= 0 || HW <= 0) return ES_BAD_SHAPE;
-  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int G = chan_groups(rows);
   const int per = (rows + G - 1) / G;
   const RowMap rm{sn, sp, HW};
-  hipLaunchKernelGGL(chan_partial_kernel<0>, G, 256, 0, stream, v, rm, rows, C, per, nullptr, nullptr, nullptr,
-                     nullptr, 0, workspace);
-  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(C), 256, 0, stream, workspace, out, G, (long)C, accumulate);
+  if (C % 4 == 0 && sn % 4 == 0 && sp % 4 == 0 && al16(v))
+    hipLaunchKernelGGL((chan_partial_kernel<0, 4>), G, 256, 0, stream, v, rm, rows, C, per, nullptr, nullptr, nullptr,
+                       nullptr, 0, workspace);
+  else
+    hipLaunchKernelGGL((chan_partial_kernel<0, 1>), G, 256, 0, stream, v, rm, rows, C, per, nullptr, nullptr, nullptr,
+                       nullptr, 0, workspace);
+  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, accumulate};
+  hipLaunchKernelGGL(chan_final_kernel<0>, (C + 15) / 16, 256, 0, stream, workspace, G, C, f);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -848,25 +1003,44 @@ int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float
   if (!x || !gamma || !beta || !y || !running_mean || !running_var) return ES_BAD_ARG;
   if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
   const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) &&
+                  al16(running_mean) && al16(running_var) && (!mean || al16(mean)) && (!rstd || al16(rstd));
+  auto apply = [&](const float* mu, const float* rs, const float* rv) {
+    if (v4)
+      hipLaunchKernelGGL(bn_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mu, rs, rv, eps,
+                         gamma, beta, res, relu, y);
+    else
+      hipLaunchKernelGGL(bn_apply_kernel<1>, grid1d(n), 256, 0, stream, x, (int)n, C, mu, rs, rv, eps, gamma, beta,
+                         res, relu, y);
+  };
   if (!train) {
-    hipLaunchKernelGGL(bn_apply_kernel, grid1d(n), 256, 0, stream, x, n, C, running_mean, nullptr, running_var, eps,
-                       gamma, beta, res, relu, y);
+    apply(running_mean, nullptr, running_var);
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   if (!mean || !rstd || !workspace) return ES_BAD_ARG;
-  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int G = chan_groups(rows);
   const int per = (rows + G - 1) / G;
   const RowMap rm{(long)rows * C, (long)C, rows};
-  hipLaunchKernelGGL(chan_partial_kernel<0>, G, 256, 0, stream, x, rm, rows, C, per, nullptr, nullptr, nullptr,
-                     nullptr, 0, workspace);
-  hipLaunchKernelGGL(bn_mean_kernel, (C + 255) / 256, 256, 0, stream, workspace, G, C, rows, mean);
-  hipLaunchKernelGGL(chan_partial_kernel<1>, G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr, nullptr,
-                     0, workspace);
-  hipLaunchKernelGGL(bn_var_kernel, (C + 255) / 256, 256, 0, stream, workspace, G, C, rows, eps, mean, rstd,
-                     running_mean, running_var, momentum);
+  const dim3 fg((C + 15) / 16);
+  ChanFin fm{mean, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
+  ChanFin fv{rstd, nullptr, nullptr, mean, running_mean, running_var, eps, momentum, rows, 0, 0};
+  if (v4) {
+    hipLaunchKernelGGL((chan_partial_kernel<0, 4>), G, 256, 0, stream, x, rm, rows, C, per, nullptr, nullptr, nullptr,
+                       nullptr, 0, workspace);
+    hipLaunchKernelGGL(chan_final_kernel<1>, fg, 256, 0, stream, workspace, G, C, fm);
+    hipLaunchKernelGGL((chan_partial_kernel<1, 4>), G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr,
+                       nullptr, 0, workspace);
+  } else {
+    hipLaunchKernelGGL((chan_partial_kernel<0, 1>), G, 256, 0, stream, x, rm, rows, C, per, nullptr, nullptr, nullptr,
+                       nullptr, 0, workspace);
+    hipLaunchKernelGGL(chan_final_kernel<1>, fg, 256, 0, stream, workspace, G, C, fm);
+    hipLaunchKernelGGL((chan_partial_kernel<1, 1>), G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr,
+                       nullptr, 0, workspace);
+  }
+  hipLaunchKernelGGL(chan_final_kernel<2>, fg, 256, 0, stream, workspace, G, C, fv);
   if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
-  hipLaunchKernelGGL(bn_apply_kernel, grid1d(n), 256, 0, stream, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res,
-                     relu, y);
+  apply(mean, rstd, nullptr);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -879,6 +1053,7 @@ int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C
   if (!x || !dy || !dx || !gamma || (relu && !y)) return ES_BAD_ARG;
   if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
   const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
   if (!train) {
     if (!running_var) return ES_BAD_ARG;
     hipLaunchKernelGGL(bn_bwd_eval_kernel, grid1d(n), 256, 0, stream, dy, y, relu, n, C, running_var, eps, gamma, dx,
@@ -886,18 +1061,27 @@ int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   if (!mean || !rstd || !workspace || !dgamma || !dbeta) return ES_BAD_ARG;
-  const int G = rows < 256 * 64 ? (rows + 63) / 64 : 256;
+  const int G = chan_groups(rows);
   const int per = (rows + G - 1) / G;
   const RowMap rm{(long)rows * C, (long)C, rows};
   float* sums = workspace + (size_t)G * 2 * C;  // [2C]: sum g, sum g xhat
-  hipLaunchKernelGGL(chan_partial_kernel<2>, G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
-                     workspace);
-  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(2 * C), 256, 0, stream, workspace, sums, G, (long)(2 * C), 0);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, grid1d(n), 256, 0, stream, x, dy, y, relu, n, C, rows, mean, rstd, gamma,
-                     sums, dx, gout);
-  // dgamma = sum g xhat (sums[C..2C)), dbeta = sum g (sums[0..C))
-  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(C), 256, 0, stream, sums + C, dgamma, 1, (long)C, accumulate);
-  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(C), 256, 0, stream, sums, dbeta, 1, (long)C, accumulate);
+  const bool v4 = C % 4 == 0 && al16(x) && al16(dy) && (!y || al16(y)) && al16(dx) && (!gout || al16(gout)) &&
+                  al16(mean) && al16(rstd) && al16(gamma) && al16(sums);
+  if (v4)
+    hipLaunchKernelGGL((chan_partial_kernel<2, 4>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
+                       workspace);
+  else
+    hipLaunchKernelGGL((chan_partial_kernel<2, 1>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
+                       workspace);
+  // sums[0..C) = sum g -> dbeta, sums[C..2C) = sum g xhat -> dgamma
+  ChanFin f{dbeta, dgamma, sums, nullptr, nullptr, nullptr, 0.f, 0.f, rows, C, accumulate};
+  hipLaunchKernelGGL(chan_final_kernel<3>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
+  if (v4)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
+                       rows, mean, rstd, gamma, sums, dx, gout);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows, mean, rstd,
+                       gamma, sums, dx, gout);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -906,6 +1090,7 @@ int es_maxpool2d_fwd(const float* x, int N, int H, int W, int C, int k, int s, i
                      hipStream_t stream) {
   if (!x || !y || !arg) return ES_BAD_ARG;
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 11 || s <= 0 || p < 0 || 2 * p > k) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
   hipLaunchKernelGGL(maxpool_fwd_kernel, grid1d((long)N * Ho * Wo * C), 256, 0, stream, x, N, H, W, C, k, s, p, Ho, Wo,
                      y, (int8_t*)arg);
@@ -916,6 +1101,7 @@ int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int 
                      hipStream_t stream) {
   if (!dy || !dx || !arg) return ES_BAD_ARG;
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 11 || s <= 0 || p < 0) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
   hipLaunchKernelGGL(maxpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, dy, (const int8_t*)arg, N, H, W,
                      C, k, s, p, Ho, Wo, dx);
@@ -926,6 +1112,7 @@ int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int 
 int es_avgpool2d_fwd(const float* x, int N, int H, int W, int C, int k, float* y, hipStream_t stream) {
   if (!x || !y) return ES_BAD_ARG;
   if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   hipLaunchKernelGGL(avgpool_fwd_kernel, grid1d((long)N * (H / k) * (W / k) * C), 256, 0, stream, x, N, H, W, C, k,
                      H / k, W / k, y);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -935,6 +1122,7 @@ int es_avgpool2d_bwd(const float* dy, int N, int H, int W, int C, int k, float* 
                      hipStream_t stream) {
   if (!dy || !dx) return ES_BAD_ARG;
   if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   hipLaunchKernelGGL(avgpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, dy, N, H, W, C, k, H / k, W / k,
                      dx, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -945,6 +1133,7 @@ int es_upsample_add_fwd(const float* base, const float* src, int N, int H, int W
                         hipStream_t stream) {
   if (!base || !src || !out) return ES_BAD_ARG;
   if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   hipLaunchKernelGGL(upsample_add_fwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, base, src, N, H, W, C, s,
                      out);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -954,6 +1143,7 @@ int es_upsample_add_fwd(const float* base, const float* src, int N, int H, int W
 int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float* dsrc, hipStream_t stream) {
   if (!dout || !dsrc) return ES_BAD_ARG;
   if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   hipLaunchKernelGGL(upsample_bwd_kernel, grid1d((long)N * (H / s) * (W / s) * C), 256, 0, stream, dout, N, H, W, C,
                      s, dsrc);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -972,7 +1162,7 @@ int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln
 
 size_t es_fcu_down_workspace(int N, int np, int D) {
   const int rows = N * (np + 1);
-  const int blocks = rows < 1024 ? (rows + 3) / 4 : 256;
+  const int blocks = rows < 4096 ? (rows + 3) / 4 : 1024;
   return (size_t)blocks * 2 * D;
 }
 
@@ -982,16 +1172,16 @@ int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* 
                            float* dln_b, int accumulate, int N, int np, int D, float* workspace, hipStream_t stream) {
   if (!dout || !pooled || !ln_w || !ln_b || !mean || !rstd || !dxt || !dpooled || !dln_w || !dln_b || !workspace)
     return ES_BAD_ARG;
-  if (N <= 0 || np <= 0 || D <= 0 || D > 4096) return ES_BAD_SHAPE;
+  if (N <= 0 || np <= 0 || D <= 0 || D > 64 * FCU_NJ) return ES_BAD_SHAPE;
   const int rows = N * (np + 1);
-  const int blocks = rows < 1024 ? (rows + 3) / 4 : 256;
+  const int blocks = rows < 4096 ? (rows + 3) / 4 : 1024;
   const int per = (rows + blocks - 1) / blocks;
-  const size_t lds = (size_t)2 * D * 4;
+  const size_t lds = (size_t)4 * 2 * D * 4;
   hipLaunchKernelGGL(fcu_down_bwd_kernel, blocks, 256, lds, stream, dout, pooled, ln_w, ln_b, mean, rstd, dxt, dpooled,
                      workspace, N, np, D, per);
   // partial[b][0..D) = dgamma, [D..2D) = dbeta
-  hipLaunchKernelGGL(fcu_param_reduce_kernel, (2 * D + 255) / 256, 256, 0, stream, workspace, blocks, D, dln_w, dln_b,
-                     accumulate);
+  ChanFin f{dln_w, dln_b, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0, D, accumulate};
+  hipLaunchKernelGGL(chan_final_kernel<3>, (2 * D + 15) / 16, 256, 0, stream, workspace, blocks, 2 * D, f);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -140,7 +140,8 @@ def test_conv2d_strided_views():
 
 # ------------------------------------------------------------------------------------ batchnorm
 @pytest.mark.parametrize("rows_shape,C,relu,with_res", [((4, 6, 6), 16, True, False), ((3, 5, 5), 64, False, True),
-                                                        ((2, 3, 3), 300, True, True), ((64, 14, 14), 32, True, False)])
+                                                        ((2, 3, 3), 300, True, True), ((64, 14, 14), 32, True, False),
+                                                        ((8, 96, 96), 64, True, True), ((2, 40, 40), 18, False, False)])
 def test_bn2d_fwd_bwd(rows_shape, C, relu, with_res):
     torch.manual_seed(C)
     N, H, W = rows_shape
@@ -237,10 +238,11 @@ def test_maxpool_avgpool_upsample():
     _close(_nchw(ds.cpu()), src.grad, atol=1e-5)
 
 
-def test_fcu_down_tokens_fwd_bwd():
-    """FCUDown LN + GELU + cat(cls) fused with `x_st + x_t` (code/models/conformer.py:161-170,345)."""
+@pytest.mark.parametrize("N,np_,D", [(5, 16, 128), (3, 4, 100), (260, 16, 384)])
+def test_fcu_down_tokens_fwd_bwd(N, np_, D):
+    """FCUDown LN + GELU + cat(cls) fused with `x_st + x_t` (code/models/conformer.py:161-170,345).
+    (260, 16, 384): more rows than one pass of the 1024 backward workgroups, Conformer-Ti's D."""
     torch.manual_seed(21)
-    N, np_, D = 5, 16, 128
     T = np_ + 1
     pooled = torch.randn(N, np_, D, dtype=torch.float64) * 2 + 0.5
     xt = torch.randn(N, T, D, dtype=torch.float64)
