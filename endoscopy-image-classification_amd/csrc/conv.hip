@@ -966,7 +966,12 @@ int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn,
                        workspace, g, chunk);
   }
   const long n = (long)Cout * K;
-  hipLaunchKernelGGL(sum_slabs_kernel, grid1d(n), 256, 0, stream, workspace, dw, S, n, accumulate);
+  if (S >= 32) {  // many slabs: 16 lanes per column over the slabs
+    ChanFin f{dw, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0, 0, accumulate};
+    hipLaunchKernelGGL(chan_final_kernel<0>, (unsigned)((n + 15) / 16), 256, 0, stream, workspace, S, (int)n, f);
+  } else {
+    hipLaunchKernelGGL(sum_slabs_kernel, grid1d(n), 256, 0, stream, workspace, dw, S, n, accumulate);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

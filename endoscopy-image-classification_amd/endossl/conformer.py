@@ -206,8 +206,15 @@ class _ConvFn(torch.autograd.Function):
         xp = ptr(x) + 4 * xm.off
         M = xm.N * Ho * Wo
         K = xm.C * k * k
-        tiles = -(-Cout // 64) * -(-K // 64)
-        splits = max(1, min(-(-M // 16), -(-512 // tiles)))
+        # workgroup tiles of es_conv2d_bwd_weight (16x256 / 32x128 / 64x64 by Cout); pixel splits sized
+        # for ~2048 workgroups (8 per CU)
+        if Cout <= 16:
+            tiles = -(-K // 256)
+        elif Cout <= 32:
+            tiles = -(-Cout // 32) * -(-K // 128)
+        else:
+            tiles = -(-Cout // 64) * -(-K // 64)
+        splits = max(1, min(-(-M // 64), -(-2048 // tiles)))
         lib = _lib.load()
         ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits), device=dy.device)
         call("es_conv2d_bwd_weight", xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy), Ho * Wo * Cout,
@@ -727,10 +734,14 @@ class NativeConformer(nn.Module):
             pre = name + "."
             med = outp // 4
             xc, x2 = self._conv_block(pre + "cnn_block.", xc, stride, res_conv)
-            # FCUDown (:161-170): 1x1 conv (bias) -> avg-pool dw -> LN -> GELU -> cat(cls), + x_t
-            sq = conv(self, x2, _Map.nhwc(x2), pre + "squeeze_block.conv_project.weight",
-                      pre + "squeeze_block.conv_project.bias", D, 1)
-            pooled = _AvgPoolFn.apply(sq, dw) if dw > 1 else sq
+            # FCUDown (:161-170): 1x1 conv (bias) -> avg-pool dw -> LN -> GELU -> cat(cls), + x_t.
+            # The 1x1 conv and the average pool are both linear maps over different axes (channels /
+            # pixels; the pool averages bias-shifted values to the same bias), so they commute: pooling
+            # the med-channel map first runs the D-channel conv at 1/dw^2 of the pixels (exact in real
+            # arithmetic; fp32 rounding order only)
+            x2p = _AvgPoolFn.apply(x2, dw) if dw > 1 else x2
+            pooled = conv(self, x2p, _Map.nhwc(x2p), pre + "squeeze_block.conv_project.weight",
+                          pre + "squeeze_block.conv_project.bias", D, 1)
             xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.")
             xt = _BlockFn.apply(xt, self, pre + "trans_block.")
             # FCUUp (:187-194): token rows 1.. as a [n, g, g, D] map -> 1x1 conv (bias) -> BN -> ReLU;

@@ -92,7 +92,7 @@ def test_conv2d_fwd_bwd(N, Cin, H, Cout, k, s, p):
     call("es_conv2d_bwd_data", ptr(dyd), Ho * Ho * Cout, Ho * Cout, Cout, ptr(wd), N, H, H, Cin, Cout, k, k, s, p,
          ptr(dxd), H * H * Cin, H * Cin, Cin, 1, 0, S())
     _close(_nchw(dxd.cpu()), xr.grad)
-    for splits in (1, 3):
+    for splits in (1, 3, 40):
         ws = torch.empty(_lib.load().es_conv2d_bwd_weight_workspace(Cout, Cin, k, k, splits), device=DEV)
         dwd = torch.empty_like(wd)
         call("es_conv2d_bwd_weight", ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(dyd), Ho * Ho * Cout,
