@@ -149,39 +149,49 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(const float* __restrict__
 }
 
 // ---- data gradient: dx[n,h,w,ci] (+)= sum_{ky,kx,co} dy[n,ho,wo,co] w[co,ci,ky,kx],
-// ho = (h + p - ky) / s when divisible and in range.  Rows m = (n, h, w), cols ci, K = (ky, kx, co).
+// ho = (h + p - ky) / s when divisible and in range.  Split by stride phase: blockIdx.z = (py, px)
+// takes the pixels h = hq*s + py, w = wq*s + px, whose only valid taps are ky = ky0 + s*kyq with
+// ky0 = (py + p) mod s (likewise kx), so ho = hq + (py + p - ky0)/s - kyq exactly.  Rows m = (n, hq, wq)
+// of the phase, cols ci, K = (kyq, kxq, co): no tap is visited that the stride makes invalid (the
+// strided patch conv k = s = 4 would otherwise waste 15/16 of its K loop).
 template <int BM, int BN>
 __global__ __launch_bounds__(256) void conv_dx_kernel(const float* __restrict__ dy, const float* __restrict__ w,
                                                       float* __restrict__ dx, ConvGeom g, int accumulate) {
   constexpr int TX = BN / 4, TM = BM * BN / 1024, APR = BM / 16, BPR = BN / 16;
   __shared__ float As[CBK][BM + 1];
   __shared__ float Bs[CBK][BN + 4];
-  const int M = g.N * g.H * g.W, K = g.kh * g.kw * g.Cout, KK = g.kh * g.kw;
+  const int s = g.stride;
+  const int py = blockIdx.z / s, px = blockIdx.z - py * s;
+  const int Hq = (g.H - py + s - 1) / s, Wq = (g.W - px + s - 1) / s;
+  const int ky0 = (py + g.pad) % s, kx0 = (px + g.pad) % s;
+  const int khq = g.kh > ky0 ? (g.kh - ky0 + s - 1) / s : 0, kwq = g.kw > kx0 ? (g.kw - kx0 + s - 1) / s : 0;
+  const int qh = (py + g.pad - ky0) / s, qw = (px + g.pad - kx0) / s;
+  const int M = g.N * Hq * Wq, K = khq * kwq * g.Cout, KK = g.kh * g.kw;
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if (m0 >= M) return;  // this phase has fewer pixels (block-uniform)
   const int tid = threadIdx.x, tx = tid % TX, ty = tid / TX;
   const int ki = tid & 15, r16 = tid >> 4;
-  const int s = g.stride;
   long abase[APR];
-  int ahp[APR], awp[APR];
+  int ahq[APR], awq[APR];
 #pragma unroll
   for (int j = 0; j < APR; ++j) {
     const int m = m0 + r16 + 16 * j;
     if (m < M) {
-      const int ww = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
+      const int wq = m % Wq, t = m / Wq, hq = t % Hq, n = t / Hq;
       abase[j] = n * g.syn;
-      ahp[j] = h + g.pad;
-      awp[j] = ww + g.pad;
+      ahq[j] = hq + qh;
+      awq[j] = wq + qw;
     } else {
       abase[j] = 0;
-      ahp[j] = -(1 << 28);
-      awp[j] = 0;
+      ahq[j] = -(1 << 28);
+      awq[j] = 0;
     }
   }
   int bci[BPR];
 #pragma unroll
   for (int j = 0; j < BPR; ++j) bci[j] = n0 + r16 + 16 * j;
-  KWalk kw;
-  kw.init(ki, g.Cout, g.kw);
+  KWalk kw;  // (c, kx = kxq, ky = kyq) over the phase's taps
+  if (K > 0) kw.init(ki, g.Cout, kwq);
   float acc[TM][4];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -191,24 +201,17 @@ __global__ __launch_bounds__(256) void conv_dx_kernel(const float* __restrict__ 
     const bool kok = k0 + ki < K;
 #pragma unroll
     for (int j = 0; j < APR; ++j) {
-      const int hn = ahp[j] - kw.ky, wn = awp[j] - kw.kx;
+      const int ho = ahq[j] - kw.ky, wo = awq[j] - kw.kx;
       float v = 0.f;
-      if (kok && hn >= 0 && wn >= 0) {
-        int ho = hn, wo = wn;
-        bool ok = true;
-        if (s != 1) {
-          ok = (hn % s == 0) && (wn % s == 0);
-          ho = hn / s;
-          wo = wn / s;
-        }
-        if (ok && ho < g.Ho && wo < g.Wo) v = dy[abase[j] + ho * g.syh + wo * g.syw + kw.c];
-      }
+      if (kok && (unsigned)ho < (unsigned)g.Ho && (unsigned)wo < (unsigned)g.Wo)
+        v = dy[abase[j] + ho * g.syh + wo * g.syw + kw.c];
       As[ki][r16 + 16 * j] = v;
     }
+    const int tap = (ky0 + kw.ky * s) * g.kw + kx0 + kw.kx * s;
 #pragma unroll
     for (int j = 0; j < BPR; ++j)
-      Bs[ki][r16 + 16 * j] = (kok && bci[j] < g.Cin) ? w[((long)kw.c * g.Cin + bci[j]) * KK + kw.t2] : 0.f;
-    kw.advance(CBK, g.Cout, g.kw);
+      Bs[ki][r16 + 16 * j] = (kok && bci[j] < g.Cin) ? w[((long)kw.c * g.Cin + bci[j]) * KK + tap] : 0.f;
+    kw.advance(CBK, g.Cout, kwq);
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < CBK; ++kk) {
@@ -228,8 +231,8 @@ __global__ __launch_bounds__(256) void conv_dx_kernel(const float* __restrict__ 
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + ty * TM + i;
     if (m >= M) continue;
-    const int ww = m % g.W, t = m / g.W, h = t % g.H, n = t / g.H;
-    float* xr = dx + n * g.sxn + h * g.sxh + ww * g.sxw;
+    const int wq = m % Wq, t = m / Wq, hq = t % Hq, n = t / Hq;
+    float* xr = dx + n * g.sxn + (hq * s + py) * g.sxh + (wq * s + px) * g.sxw;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ci = n0 + tx * 4 + j;
@@ -925,16 +928,17 @@ int es_conv2d_bwd_data(const float* dy, long syn, long syh, long syw, const floa
   if (!dy || !w || !dx) return ES_BAD_ARG;
   const ConvGeom g = make_geom(N, H, W, Cin, sxn, sxh, sxw, sxc, Cout, kh, kw, stride, pad, syn, syh, syw);
   if (!geom_ok(g)) return ES_BAD_SHAPE;
-  const int M = N * H * W;
+  const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
+  const unsigned ph = (unsigned)(stride * stride);
   if (Cin <= 16) {
-    hipLaunchKernelGGL((conv_dx_kernel<256, 16>), dim3((M + 255) / 256, (Cin + 15) / 16), 256, 0, stream, dy, w, dx, g,
-                       accumulate);
+    hipLaunchKernelGGL((conv_dx_kernel<256, 16>), dim3((Mq + 255) / 256, (Cin + 15) / 16, ph), 256, 0, stream, dy, w,
+                       dx, g, accumulate);
   } else if (Cin <= 32) {
-    hipLaunchKernelGGL((conv_dx_kernel<128, 32>), dim3((M + 127) / 128, (Cin + 31) / 32), 256, 0, stream, dy, w, dx, g,
-                       accumulate);
+    hipLaunchKernelGGL((conv_dx_kernel<128, 32>), dim3((Mq + 127) / 128, (Cin + 31) / 32, ph), 256, 0, stream, dy, w,
+                       dx, g, accumulate);
   } else {
-    hipLaunchKernelGGL((conv_dx_kernel<64, 64>), dim3((M + 63) / 64, (Cin + 63) / 64), 256, 0, stream, dy, w, dx, g,
-                       accumulate);
+    hipLaunchKernelGGL((conv_dx_kernel<64, 64>), dim3((Mq + 63) / 64, (Cin + 63) / 64, ph), 256, 0, stream, dy, w, dx,
+                       g, accumulate);
   }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
