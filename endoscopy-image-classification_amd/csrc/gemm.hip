@@ -683,32 +683,46 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restr
   }
 }
 
-// out[n] (+)= sum_g P[g][n]: 16 columns x 16 row-groups per block (4 loads in flight per
-// thread), then a 16-way LDS combine.
+// out[n] (+)= sum_g P[g][n]: CW columns x (256 / CW) row-groups per block (4 loads in flight per
+// thread), then a fixed-order LDS combine (deterministic).  Narrow blocks (CW = 4) for short rows so
+// a 384-column reduction still spreads over ~100 workgroups.
+template <int CW>
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ P, float* __restrict__ out,
                                                               int G, int N, int accumulate) {
-  __shared__ float red[16][17];
-  const int cl = threadIdx.x & 15, rg = threadIdx.x >> 4;
-  const int col = blockIdx.x * 16 + cl;
+  constexpr int RG = 256 / CW;
+  __shared__ float red[RG][CW + 1];
+  const int cl = threadIdx.x % CW, rg = threadIdx.x / CW;
+  const int col = blockIdx.x * CW + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int g = rg;
-    for (; g + 48 < G; g += 64) {
+    for (; g + 3 * RG < G; g += 4 * RG) {
       s0 += P[(size_t)g * N + col];
-      s1 += P[(size_t)(g + 16) * N + col];
-      s2 += P[(size_t)(g + 32) * N + col];
-      s3 += P[(size_t)(g + 48) * N + col];
+      s1 += P[(size_t)(g + RG) * N + col];
+      s2 += P[(size_t)(g + 2 * RG) * N + col];
+      s3 += P[(size_t)(g + 3 * RG) * N + col];
     }
-    for (; g < G; g += 16) s0 += P[(size_t)g * N + col];
+    for (; g < G; g += RG) s0 += P[(size_t)g * N + col];
   }
   red[rg][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  if (rg == 0 && col < N) {
-    float sum = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) sum += red[k][cl];
+  for (int h = RG / 2; h >= 1; h >>= 1) {
+    if (rg < h) red[rg][cl] += red[rg + h][cl];
+    __syncthreads();
+  }
+  if (rg == 0 && col < N) {
+    const float sum = red[0][cl];
     out[col] = accumulate ? out[col] + sum : sum;
   }
+}
+
+// launch: 4-column blocks when that still leaves <= 512 blocks, else 16-column blocks
+inline void launch_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream) {
+  if (N <= 2048 && G >= 64)
+    hipLaunchKernelGGL(reduce_partials_kernel<4>, (N + 3) / 4, 256, 0, stream, P, out, G, N, accumulate);
+  else
+    hipLaunchKernelGGL(reduce_partials_kernel<16>, (N + 15) / 16, 256, 0, stream, P, out, G, N, accumulate);
 }
 
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
@@ -887,7 +901,7 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
     hipLaunchKernelGGL(splitk_reduce_kernel, rg, 256, 0, stream, P, out, S, n, accumulate);
   }
   if (bias_out)
-    hipLaunchKernelGGL(reduce_partials_kernel, (N1 + 15) / 16, 256, 0, stream, PB, bias_out, S, N1, accumulate);
+    launch_reduce_partials(PB, bias_out, S, N1, accumulate, stream);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -907,14 +921,14 @@ int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks,
   const int rows_per = (M + blocks - 1) / blocks;
   const int G = (M + rows_per - 1) / rows_per;
   hipLaunchKernelGGL(colsum_partial_kernel, G, 256, 0, stream, (const bf16*)Y, ld, M, N, rows_per, workspace);
-  hipLaunchKernelGGL(reduce_partials_kernel, (N + 15) / 16, 256, 0, stream, workspace, out, G, N, accumulate);
+  launch_reduce_partials(workspace, out, G, N, accumulate, stream);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
 // out[n] (+)= sum_g P[g][n]  (partials of the LayerNorm / colsum kernels)
 int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream) {
   if (G <= 0 || N <= 0) return ES_BAD_SHAPE;
-  hipLaunchKernelGGL(reduce_partials_kernel, (N + 15) / 16, 256, 0, stream, P, out, G, N, accumulate);
+  launch_reduce_partials(P, out, G, N, accumulate, stream);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

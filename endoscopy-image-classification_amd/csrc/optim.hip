@@ -110,9 +110,27 @@ __global__ void cast_kernel(const float* __restrict__ x, bf16* __restrict__ y, l
     y[i] = (bf16)x[i];
 }
 
+// y += x over n floats (n % 4 == 0, 16-byte aligned): the two-lane backward's second flat gradient
+__global__ void add_f32_kernel(float* __restrict__ y, const float* __restrict__ x, long n4) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    f32x4 a = ((const f32x4*)y)[i];
+    a += ((const f32x4*)x)[i];
+    ((f32x4*)y)[i] = a;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int es_add_f32(float* y, const float* x, long n, hipStream_t stream) {
+  if (n <= 0 || n % 4) return ES_BAD_SHAPE;
+  if (!y || !x || ((uintptr_t)y & 15) || ((uintptr_t)x & 15)) return ES_BAD_ARG;
+  long grid = (n / 4 + 255) / 256;
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(add_f32_kernel, (int)grid, 256, 0, stream, y, x, n / 4);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
 
 int es_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream) {
   if (n <= 0) return ES_BAD_SHAPE;

@@ -83,6 +83,7 @@ SIGNATURES = {
     "es_pack_entry_size": (I, []),
     "es_pack_weights": (I, [V, V, I, V]),
     "es_cast_f32_bf16": (I, [V, V, L, V]),
+    "es_add_f32": (I, [V, V, L, V]),
 }
 
 ABI_VERSION = 1

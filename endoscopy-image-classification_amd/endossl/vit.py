@@ -204,6 +204,16 @@ class Engine:
     _OV = os.environ.get("ENDOSSL_OVERLAP", "1")
     OVERLAP_FWD = _OV in ("1", "fwd")
     OVERLAP = _OV in ("1", "bwd")
+    # two-lane backward (with OVERLAP): the train batch's images are split in halves and each half's
+    # reverse pass -- its data-gradient chain AND its own weight gradients -- runs on its own HIP
+    # stream, so the two streams carry equal work (the single-lane split, chain vs weight gradients,
+    # leaves the chain stream ~2x busier).  Lane 1 writes a second flat gradient, summed into the
+    # first at the end.  Used when each half's token and patch rows are multiples of 256 (every
+    # half-batch buffer is then an exact GEMM-tile view).  Off by default (ENDOSSL_LANES=2 turns it
+    # on): at F1 it balances the streams (35.4 / 33.9 ms of kernels) but the step gets slower, 40.2
+    # vs 39.1 ms -- the chip is throughput-bound, co-running kernels each take ~2x as long, and the
+    # single-lane split keeps the weight-gradient GEMMs (the most MFMA-dense work) off the chain.
+    LANES = int(os.environ.get("ENDOSSL_LANES", "1"))
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -214,6 +224,8 @@ class Engine:
         self._ws = None
         self._ws_ln = None
         self._side = None
+        self._lane_state = {}
+        self._grad_b = None
         self.overlap = self.OVERLAP
         self.overlap_fwd = self.OVERLAP_FWD
         self._packed_version = -1
@@ -273,21 +285,26 @@ class Engine:
             self._acts[key] = _Acts(self.cfg, n, train, self.device)
         return self._acts[key]
 
-    def workspace(self):
+    def workspace(self, lane=0):
+        """Split-K slabs of the weight-gradient GEMMs (one per backward lane: lanes run concurrently)."""
         if self._ws is None:
+            self._ws = {}
+        if lane not in self._ws:
             cfg = self.cfg
             D, Hd = cfg.dim, cfg.hidden
             n_tn = max(a * b for a, b in ((3 * D, D), (D, D), (Hd, D), (D, Hd), (D, 3 * cfg.patch * cfg.patch)))
-            self._ws = torch.empty(self.TN_MAX_SPLITS * n_tn + 2 * 1024 * max(Hd, 3 * D), dtype=torch.float32,
-                                   device=self.device)
-        return self._ws
+            self._ws[lane] = torch.empty(self.TN_MAX_SPLITS * n_tn + 2 * 1024 * max(Hd, 3 * D), dtype=torch.float32,
+                                         device=self.device)
+        return self._ws[lane]
 
-    def ln_workspace(self):
+    def ln_workspace(self, lane=0):
         """LayerNorm-backward partials (separate from the split-K slabs: the two run on different
         streams when the weight gradients overlap the data-gradient chain)."""
         if self._ws_ln is None:
-            self._ws_ln = torch.empty(2 * 1024 * self.cfg.dim, dtype=torch.float32, device=self.device)
-        return self._ws_ln
+            self._ws_ln = {}
+        if lane not in self._ws_ln:
+            self._ws_ln[lane] = torch.empty(2 * 1024 * self.cfg.dim, dtype=torch.float32, device=self.device)
+        return self._ws_ln[lane]
 
     def side_stream(self):
         """The second HIP stream (weak forward beside the train forward; weight gradients beside
@@ -365,18 +382,18 @@ class Engine:
         msteps = (M + 31) // 32
         return max(1, min(msteps, self.TN_MAX_SPLITS, -(-self.TN_TARGET_BLOCKS // tiles)))
 
-    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None):
+    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0):
         """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy."""
-        ws = self.workspace()
+        ws = self.workspace(lane)
         splits = self._tn_splits(M, N1, N2)
         if _lib.load().es_gemm_tn_workspace(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
         call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
              _lib.stream())
 
-    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M):
+    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0):
         D = self.cfg.dim
-        ws = self.ln_workspace()
+        ws = self.ln_workspace(lane)
         call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
@@ -428,6 +445,10 @@ class Engine:
                  ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(G.dx), D, T,
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
                  cfg.num_classes, s)
+        nh = n // 2
+        if (ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0 and (nh * cfg.np) % 256 == 0
+                and grad.numel() % 4 == 0):
+            return self._backward_lanes(flat, grad, A, G.dx, nh)
         call("es_cast_f32_bf16", ptr(G.dx), ptr(GS[(cfg.depth - 1) % 2].dxb), M * D, s)
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."
@@ -464,6 +485,80 @@ class Engine:
         wgrad_side(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
         if ov:
             main.wait_stream(side)
+        return grad
+
+
+    def _backward_lanes(self, flat, grad, A, dx_full, nh):
+        """Two-lane reverse pass (see LANES): lane 0 = images [0, nh) on the caller's stream into
+        `grad`, lane 1 = images [nh, 2 nh) on the side stream into a second flat gradient.  dx_full
+        holds d(loss)/d(final tokens) for all images (head backward already done); each lane's
+        residual-gradient buffer is its disjoint row range of it.  Issue is interleaved per layer so
+        both streams fill from the start."""
+        cfg = self.cfg
+        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
+        Ml, Pl = nh * T, nh * cfg.np
+        main = torch.cuda.current_stream(self.device)
+        side = self.side_stream()
+        if self._grad_b is None or self._grad_b.numel() != grad.numel():
+            # entries outside the trunk (head, final norm) are never written by a lane: they stay 0
+            self._grad_b = torch.zeros_like(grad)
+        key = nh
+        if key not in self._lane_state:
+            self._lane_state[key] = [_Grads(cfg, nh, self.device), _Grads(cfg, nh, self.device)]
+        lanes = []
+        for ln, (st, g) in enumerate(((main, grad), (side, self._grad_b))):
+            r0 = ln * Ml
+            lanes.append(dict(id=ln, stream=st, grad=g, G=self._lane_state[key][ln], r0=r0, r1=r0 + Ml,
+                              dx=dx_full[r0:r0 + Ml], lse0=ln * nh * H * T, p0=ln * Pl))
+        side.wait_stream(main)  # head backward (dx_full) and the zeroed grad
+        for L in lanes:
+            with torch.cuda.stream(L["stream"]):
+                call("es_cast_f32_bf16", ptr(L["dx"]), ptr(L["G"].dxb), Ml * D, _lib.stream())
+        fv = lambda name: self.view(flat, name)  # noqa: E731
+        for i in reversed(range(cfg.depth)):
+            b = f"blocks.{i}."
+            for L in lanes:
+                with torch.cuda.stream(L["stream"]):
+                    s = _lib.stream()
+                    G, ln, r0, r1 = L["G"], L["id"], L["r0"], L["r1"]
+                    gv = lambda name, _g=L["grad"]: self.view(_g, name)  # noqa: E731
+                    pre, act, h2, h1 = A.pre[i][r0:r1], A.act[i][r0:r1], A.h2[i][r0:r1], A.h1[i][r0:r1]
+                    xmid, x, o, qkv = A.xmid[i][r0:r1], A.x[i][r0:r1], A.o[i][r0:r1], A.qkv[i][r0:r1]
+                    m1, s1 = A.mean1[i][r0:r1], A.rstd1[i][r0:r1]
+                    m2, s2 = A.mean2[i][r0:r1], A.rstd2[i][r0:r1]
+                    lse = A.lse[i][L["lse0"]:]
+                    # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
+                    call("es_gemm_nt", EPI_DGELU, ptr(G.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None,
+                         ptr(G.dpre), Hd, None, ptr(pre), Hd, Ml, Hd, D, 0, s)
+                    self._wgrad(G.dxb, D, act, Hd, Ml, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"), lane=ln)
+                    call("es_gemm_nt", EPI_F32, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
+                         ptr(G.dh), D, None, None, 0, Ml, D, Hd, 0, s)
+                    self._wgrad(G.dpre, Hd, h2, D, Ml, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"), lane=ln)
+                    self._ln_bwd(G.dh, xmid, m2, s2, fv(b + "norm2.weight"), L["dx"], G.dxm, G.dxmb,
+                                 gv(b + "norm2.weight"), gv(b + "norm2.bias"), Ml, lane=ln)
+                    # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
+                    call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
+                         ptr(G.do), D, None, None, 0, Ml, D, D, 0, s)
+                    self._wgrad(G.dxmb, D, o, D, Ml, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"), lane=ln)
+                    call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(G.delta), ptr(G.do), D,
+                         ptr(G.dqkv), 3 * D, nh, T, H, 64 ** -0.5, s)
+                    call("es_gemm_nt", EPI_F32, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D,
+                         None, ptr(G.dh), D, None, None, 0, Ml, D, 3 * D, 0, s)
+                    self._wgrad(G.dqkv, 3 * D, h1, D, Ml, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"),
+                                lane=ln)
+                    self._ln_bwd(G.dh, x, m1, s1, fv(b + "norm1.weight"), G.dxm, L["dx"], G.dxb,
+                                 gv(b + "norm1.weight"), gv(b + "norm1.bias"), Ml, lane=ln)
+        K0 = 3 * cfg.patch * cfg.patch
+        for L in lanes:
+            with torch.cuda.stream(L["stream"]):
+                G = L["G"]
+                gv = lambda name, _g=L["grad"]: self.view(_g, name)  # noqa: E731
+                call("es_embed_bwd", ptr(L["dx"]), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")),
+                     nh, T, D, 0, _lib.stream())
+                self._wgrad(G.dpatch, D, A.patches[L["p0"]:L["p0"] + Pl], K0, Pl, gv("patch_embed.proj.weight"),
+                            gv("patch_embed.proj.bias"), lane=L["id"])
+        main.wait_stream(side)
+        call("es_add_f32", ptr(grad), ptr(self._grad_b), grad.numel(), _lib.stream())
         return grad
 
 

@@ -226,6 +226,10 @@ int es_pack_entry_size(void);
 int es_pack_weights(const float* flat, const void* entries, int nmat, hipStream_t stream);
 int es_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
 
+// y += x over n fp32 values (n % 4 == 0, 16-byte aligned).  Sums the second lane's flat gradient into the
+// first (two-lane backward, endossl/vit.py Engine.backward); no reference counterpart (autograd accumulates).
+int es_add_f32(float* y, const float* x, long n, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -274,3 +274,33 @@ def test_full_size_step_properties():
     # a second identical step is deterministic up to the fp32-atomic head reductions
     _record("full_size_step", loss=out["loss"].item(), lx=out["lx"].item(), lu=out["lu"].item(),
             mask_mean=out["mask_mean"].item())
+
+
+def test_two_lane_backward_matches_single_lane():
+    """Engine.backward's two-lane split (each half-batch's chain + weight gradients on its own
+    stream, second flat gradient summed at the end) equals the single-lane reverse pass up to fp32
+    summation order.  n = 512 tiny-ViT images: each half's 256 x 17 token rows are whole GEMM tiles."""
+    from endossl.vit import NativeViT
+    vcfg, _ = _tiny_cfgs()
+    m = NativeViT(vcfg, seed=5).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.randn(512, 3, 64, 64, device=DEV, generator=g)
+    dl = torch.randn(512, 23, device=DEV, generator=g) * 1e-2
+    grads = {}
+    for lanes in (1, 2):
+        eng.LANES = lanes  # instance override of the class default
+        eng.forward(m.flat, [x], train=True)
+        gr = torch.zeros_like(m.flat)
+        eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        grads[lanes] = gr.clone()
+    del eng.LANES
+    worst = 0.0
+    for name, _ in eng.layout:
+        a, b = eng.view(grads[2], name), eng.view(grads[1], name)
+        assert torch.isfinite(a).all()
+        worst = max(worst, _rel(a, b))
+    _record("two_lane_backward", worst_rel_l2=worst)
+    assert worst <= 1e-5, worst
