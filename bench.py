@@ -5,7 +5,8 @@
 
 Workload F1 (BASELINE configs[1]): FixMatch, ViT-Small/16, B=64 labeled + mu*B = 448 unlabeled
 weak/strong pairs per rank, 224x224x3, 23 classes, bf16 MFMA compute with fp32 master weights.
-Synthetic, HBM-resident inputs (seed 0): uint8 images -> ImageNet-normalised fp32 (code/dataset.py:21-22).
+Synthetic, HBM-resident inputs (seed 0): uint8 pixels whose ToTensor + ImageNet Normalize
+(code/dataset.py:21-22,49-51) run inside the patch gather (--inputs f32: host-normalised fp32 images).
 Weak scaling: every rank runs the full F1 batch; the gradient all-reduce is the only exchange.
 One step = weak forward (448) + train forward/backward (64+448) + fused losses + grad
 all-reduce + Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.
@@ -41,8 +42,12 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md §HBM; ~6300 ach
 STEP_TFLOP_F1 = 18.247  # fwd 960 imgs + bwd 512 imgs, 9.197 GFLOP/img fwd
 
 
+def synth_u8(n, size, gen, device):
+    return torch.randint(0, 256, (n, 3, size, size), generator=gen, dtype=torch.uint8, device=device)
+
+
 def synth_images(n, size, gen, device):
-    u8 = torch.randint(0, 256, (n, 3, size, size), generator=gen, dtype=torch.uint8, device=device)
+    u8 = synth_u8(n, size, gen, device)
     x = u8.float().div_(255.0)
     m = torch.tensor(MEAN, device=device).view(1, 3, 1, 1)
     s = torch.tensor(STD, device=device).view(1, 3, 1, 1)
@@ -215,6 +220,8 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--mu", type=int, default=7)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inputs", choices=("u8", "f32"), default="u8",
+                    help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")
     ap.add_argument("--workload", choices=("f1", "c1", "s1"), default="f1",
                     help="f1 = the BASELINE metric (default); c1 / s1 = CoMatch / SemiFormer configs")
     args = ap.parse_args()
@@ -243,10 +250,13 @@ def main():
     tr.class_weights = torch.linspace(0.5, 2.0, 23, device=dev)
 
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    x = synth_images(B, 224, g, dev)
+    # default: the batch stays uint8 pixels in HBM and ToTensor + Normalize run inside the patch gather
+    # (es_patch_im2col_u8, bit-identical patches); --inputs f32 hands over host-normalised fp32 images
+    make = synth_u8 if args.inputs == "u8" else synth_images
+    x = make(B, 224, g, dev)
     y = torch.randint(0, 23, (B,), generator=g, device=dev)
-    uw = synth_images(B * MU, 224, g, dev)
-    us = synth_images(B * MU, 224, g, dev)
+    uw = make(B * MU, 224, g, dev)
+    us = make(B * MU, 224, g, dev)
     batch = ((x, y), ((uw, us), None))
 
     for _ in range(args.warmup):
@@ -303,7 +313,9 @@ def main():
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16", "data": "synthetic (HBM-resident uint8->ImageNet-normalised fp32, seed 0)",
+            "dtype": "bf16", "data": ("synthetic (HBM-resident uint8 pixels, ImageNet normalisation fused into the "
+                                      "patch gather, seed 0)" if args.inputs == "u8" else
+                                      "synthetic (HBM-resident uint8->ImageNet-normalised fp32, seed 0)"),
             "config": {"workload": f"F1: FixMatch ViT-S/16 step, B={B} labeled + mu*B={B * MU} unlabeled "
                                    f"weak/strong pairs per GPU, 224^2, C=23, tau=0.95, lambda_u=1, Adam 1e-3, "
                                    f"EMA 0.999", "global_batch": world * B * (1 + 2 * MU), "seq_len": 197,

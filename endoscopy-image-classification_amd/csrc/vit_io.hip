@@ -30,6 +30,37 @@ __global__ void im2col_kernel(const float* __restrict__ img, bf16* __restrict__ 
   }
 }
 
+// Same permutation from uint8 images [n, 3, S, S] (the host pipeline's un-normalised pixels): each
+// value goes through torchvision's ToTensor (x / 255) and Normalize ((x - mean[c]) / std[c]) in fp32
+// with IEEE divisions, exactly as code/dataset.py:49-51 runs them on the host, so the bf16 patches
+// equal those of the fp32 path bit for bit -- with a quarter of the bytes over PCIe and from HBM.
+struct ChanNorm {
+  float mean[3], std[3];
+};
+template <int P>
+__global__ void im2col_u8_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out, int n, int S, ChanNorm nm) {
+  const int G = S / P, np = G * G, K = 3 * P * P;
+  const long total = (long)n * np * (K / 8);
+  for (long id = blockIdx.x * (long)blockDim.x + threadIdx.x; id < total; id += (long)gridDim.x * blockDim.x) {
+    const int k8 = (int)(id % (K / 8));
+    const long row = id / (K / 8);
+    const int im = (int)(row / np), pi = (int)(row % np);
+    const int py = pi / G, px = pi % G;
+    const int k = k8 * 8, c = k / (P * P), ky = (k / P) % P, kx = k % P;
+    const uint8_t* src = img + (((size_t)im * 3 + c) * S + py * P + ky) * S + px * P + kx;
+    const uint2 raw = *(const uint2*)src;
+    const float mu = c == 0 ? nm.mean[0] : (c == 1 ? nm.mean[1] : nm.mean[2]);
+    const float sd = c == 0 ? nm.std[0] : (c == 1 ? nm.std[1] : nm.std[2]);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned b = ((j < 4 ? raw.x : raw.y) >> (8 * (j & 3))) & 255u;
+      o[j] = (bf16)(((float)b / 255.0f - mu) / sd);
+    }
+    *(bf16x8*)(out + row * K + k) = o;
+  }
+}
+
 // x[img*T + 0][d] = cls[d] + pos[0][d]
 __global__ void cls_init_kernel(float* __restrict__ x, int ldx, const float* __restrict__ cls,
                                 const float* __restrict__ pos, int n, int T, int D) {
@@ -268,6 +299,18 @@ int es_patch_im2col(const float* img, void* patches, int n, int S, int P, hipStr
   long grid = (total + 255) / 256;
   if (grid > 65536) grid = 65536;
   hipLaunchKernelGGL(im2col_kernel<16>, (int)grid, 256, 0, stream, img, (bf16*)patches, n, S);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_patch_im2col_u8(const void* img, float mean0, float mean1, float mean2, float std0, float std1, float std2,
+                       void* patches, int n, int S, int P, hipStream_t stream) {
+  if (n <= 0 || P != 16 || S % P) return ES_BAD_SHAPE;
+  if (!img || !patches || ((uintptr_t)img & 7)) return ES_BAD_ARG;
+  const long total = (long)n * (S / P) * (S / P) * (3 * P * P / 8);
+  long grid = (total + 255) / 256;
+  if (grid > 65536) grid = 65536;
+  const ChanNorm nm{{mean0, mean1, mean2}, {std0, std1, std2}};
+  hipLaunchKernelGGL(im2col_u8_kernel<16>, (int)grid, 256, 0, stream, (const uint8_t*)img, (bf16*)patches, n, S, nm);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

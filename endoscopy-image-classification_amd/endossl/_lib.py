@@ -34,6 +34,7 @@ SIGNATURES = {
     "es_gelu_fwd": (I, [V, V, L, V]),
     "es_gelu_bwd": (I, [V, V, V, L, V]),
     "es_patch_im2col": (I, [V, V, I, I, I, V]),
+    "es_patch_im2col_u8": (I, [V, F, F, F, F, F, F, V, I, I, I, V]),
     "es_cls_init": (I, [V, I, V, V, I, I, I, V]),
     "es_embed_bwd": (I, [V, I, V, I, V, V, I, I, I, I, V]),
     "es_cls_head_fwd": (I, [V, I, I, V, V, V, V, V, I, V, V, I, I, I, F, V]),

@@ -714,6 +714,9 @@ class NativeConformer(nn.Module):
             raise _lib.EndosslCallError("NativeConformer runs on the MI355X only: move it to a cuda device first")
         if x.dim() != 4 or x.shape[1:] != (3, cfg.img_size, cfg.img_size):
             raise ValueError(f"expected [n, 3, {cfg.img_size}, {cfg.img_size}] images, got {tuple(x.shape)}")
+        if x.dtype == torch.uint8:
+            raise ValueError("NativeConformer takes ImageNet-normalised fp32 images (code/dataset.py:49-51); the "
+                             "uint8 input path is the ViT engine's")
         self._pack()
         x = x.float().contiguous()
         n, S = x.shape[0], cfg.img_size

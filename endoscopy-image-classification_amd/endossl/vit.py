@@ -30,6 +30,11 @@ from ._lib import call, ptr
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT = range(7)
 
 
+# code/dataset.py:21-22 (transforms.Normalize on every ViT input); uint8 batches are normalised on the GPU
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
 def _rup(x, m):
     return (x + m - 1) // m * m
 
@@ -326,11 +331,16 @@ class Engine:
         K0 = 3 * cfg.patch * cfg.patch
         row = 0
         for t in images_list:
-            if t.shape[1:] != (3, cfg.img_size, cfg.img_size) or t.dtype != torch.float32:
-                raise ValueError(f"expected fp32 [n,3,{cfg.img_size},{cfg.img_size}] images, got {tuple(t.shape)}")
+            if t.shape[1:] != (3, cfg.img_size, cfg.img_size) or t.dtype not in (torch.float32, torch.uint8):
+                raise ValueError(f"expected fp32 (normalised) or uint8 (raw) [n,3,{cfg.img_size},{cfg.img_size}] "
+                                 f"images, got {tuple(t.shape)} {t.dtype}")
             t = t.contiguous()
-            call("es_patch_im2col", ptr(t), ptr(A.patches[row * cfg.np:]), int(t.shape[0]), cfg.img_size,
-                 cfg.patch, s)
+            if t.dtype == torch.uint8:  # ToTensor + Normalize fused into the patch gather
+                call("es_patch_im2col_u8", ptr(t), *IMAGENET_MEAN, *IMAGENET_STD, ptr(A.patches[row * cfg.np:]),
+                     int(t.shape[0]), cfg.img_size, cfg.patch, s)
+            else:
+                call("es_patch_im2col", ptr(t), ptr(A.patches[row * cfg.np:]), int(t.shape[0]), cfg.img_size,
+                     cfg.patch, s)
             row += int(t.shape[0])
         x0 = A.x[0]
         pos = self.view(flat, "pos_embed")

@@ -80,6 +80,12 @@ int es_gelu_bwd(const void* x, const void* dy, void* dx, long n, hipStream_t str
 
 /* ---- ViT ends: patches, CLS/pos rows, embedding backward, final LN + head on CLS ------------- */
 int es_patch_im2col(const float* img, void* patches, int n, int S, int P, hipStream_t stream);
+
+// es_patch_im2col from uint8 pixels [n, 3, S, S]: ToTensor (x / 255) then Normalize ((x - mean[c]) /
+// std[c]) in fp32, IEEE divisions (code/dataset.py:21-22,49-51 -- torchvision's transforms on the
+// host), then the same bf16 patch permutation.  img 8-byte aligned.
+int es_patch_im2col_u8(const void* img, float mean0, float mean1, float mean2, float std0, float std1, float std2,
+                       void* patches, int n, int S, int P, hipStream_t stream);
 int es_cls_init(float* x, int ldx, const float* cls, const float* pos, int n, int T, int D, hipStream_t stream);
 int es_embed_bwd(const float* dx, int lddx, void* dpatch, int ldp, float* dpos, float* dcls, int n, int T, int D,
                  int accumulate, hipStream_t stream);

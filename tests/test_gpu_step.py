@@ -304,3 +304,24 @@ def test_two_lane_backward_matches_single_lane():
         worst = max(worst, _rel(a, b))
     _record("two_lane_backward", worst_rel_l2=worst)
     assert worst <= 1e-5, worst
+
+
+def test_uint8_input_path_matches_normalised_fp32():
+    """es_patch_im2col_u8 (ToTensor + Normalize fused into the patch gather, code/dataset.py:21-22,
+    49-51) gives the same logits, bit for bit, as the fp32 images normalised the torchvision way."""
+    from endossl.vit import IMAGENET_MEAN, IMAGENET_STD, NativeViT
+    vcfg, _ = _tiny_cfgs()
+    m = NativeViT(vcfg, seed=2).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    g = torch.Generator().manual_seed(3)
+    u8 = torch.randint(0, 256, (6, 3, 64, 64), generator=g, dtype=torch.uint8)
+    mean = torch.tensor(IMAGENET_MEAN).view(1, 3, 1, 1)
+    std = torch.tensor(IMAGENET_STD).view(1, 3, 1, 1)
+    xf = u8.float().div(255).sub_(mean).div_(std)  # torchvision ToTensor + Normalize
+    a = eng.forward(m.flat, [u8.to(DEV)], train=False).clone()
+    b = eng.forward(m.flat, [xf.to(DEV)], train=False).clone()
+    assert torch.equal(a, b)
+    # mixed list (labeled fp32 + unlabeled uint8) in one train forward
+    c = eng.forward(m.flat, [xf[:2].to(DEV), u8[2:].to(DEV)], train=True).clone()
+    assert torch.equal(c, eng.forward(m.flat, [xf.to(DEV)], train=True))
