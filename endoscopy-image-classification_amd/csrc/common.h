@@ -97,10 +97,19 @@ __device__ __forceinline__ float erf_fast(float x) {
 __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
+// gelu'(x) = Phi(x) + x phi(x).  erf_fast's exp(-z^2), z = x / sqrt(2), IS exp(-x^2 / 2): one v_exp
+// serves both the erf and the density.
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return fmaf(x, pdf, cdf);
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  const float e = __expf(-az * az);
+  const float erfv = copysignf(1.0f - y * t * e, z);
+  return fmaf(x, 0.39894228040143268f * e, 0.5f * (1.0f + erfv));
 }
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):

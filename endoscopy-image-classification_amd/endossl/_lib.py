@@ -61,6 +61,7 @@ SIGNATURES = {
     "es_poly_ce_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, I, V, V]),
     "es_conv2d_fwd": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, I, V]),
     "es_conv2d_bwd_data": (I, [V, L, L, L, V, I, I, I, I, I, I, I, I, I, V, L, L, L, L, I, V]),
+    "es_conv2d_dw_tiles": (I, [I, I, I, I]),
     "es_conv2d_bwd_weight_workspace": (Z, [I, I, I, I, I]),
     "es_conv2d_bwd_weight": (I, [V, I, I, I, I, L, L, L, L, V, L, L, L, I, I, I, I, I, I, V, V, I, V]),
     "es_chan_workspace": (Z, [I, I]),

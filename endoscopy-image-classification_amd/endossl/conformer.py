@@ -206,16 +206,10 @@ class _ConvFn(torch.autograd.Function):
         xp = ptr(x) + 4 * xm.off
         M = xm.N * Ho * Wo
         K = xm.C * k * k
-        # workgroup tiles of es_conv2d_bwd_weight (16x256 / 32x128 / 64x64 by Cout); pixel splits sized
-        # for ~2048 workgroups (8 per CU)
-        if Cout <= 16:
-            tiles = -(-K // 256)
-        elif Cout <= 32:
-            tiles = -(-Cout // 32) * -(-K // 128)
-        else:
-            tiles = -(-Cout // 64) * -(-K // 64)
-        splits = max(1, min(-(-M // 64), -(-2048 // tiles)))
+        # pixel splits sized for ~2048 workgroups (8 per CU) over es_conv2d_bwd_weight's tiles
         lib = _lib.load()
+        tiles = lib.es_conv2d_dw_tiles(Cout, xm.C, k, k)
+        splits = max(1, min(-(-M // 64), -(-2048 // tiles)))
         ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits), device=dy.device)
         call("es_conv2d_bwd_weight", xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy), Ho * Wo * Cout,
              Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0, _s())

@@ -182,6 +182,9 @@ int es_conv2d_fwd(const float* x, int N, int H, int W, int Cin, long sxn, long s
 int es_conv2d_bwd_data(const float* dy, long syn, long syh, long syw, const float* w, int N, int H, int W, int Cin,
                        int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh, long sxw, long sxc,
                        int accumulate, hipStream_t stream);
+// workgroup tiles (Cout x Cin kh kw) one pixel split of es_conv2d_bwd_weight launches: callers size
+// `splits` so that tiles x splits fills the chip
+int es_conv2d_dw_tiles(int Cout, int Cin, int kh, int kw);
 size_t es_conv2d_bwd_weight_workspace(int Cout, int Cin, int kh, int kw, int splits);
 int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
                          const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride, int pad,

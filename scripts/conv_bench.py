@@ -35,7 +35,7 @@ def main():
         dx = torch.empty_like(x)
         M = N * Ho * Ho
         flops = 2.0 * M * Cout * Cin * k * k
-        splits = max(1, min(-(-M // 64), -(-2048 // max(1, (-(-Cout // 64)) * (-(-Cin * k * k // 64))))))
+        splits = max(1, min(-(-M // 64), -(-2048 // _lib.load().es_conv2d_dw_tiles(Cout, Cin, k, k))))
         ws = torch.empty(_lib.load().es_conv2d_bwd_weight_workspace(Cout, Cin, k, k, splits), device=dev)
         dw = torch.empty_like(w)
         ops = {

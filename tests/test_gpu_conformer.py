@@ -72,7 +72,8 @@ def _close(a, b, rtol=1e-4, atol=1e-4):
 @pytest.mark.parametrize("N,Cin,H,Cout,k,s,p", [(3, 5, 11, 7, 3, 2, 1), (2, 64, 16, 16, 1, 1, 0),
                                                 (2, 16, 16, 16, 3, 1, 1), (2, 32, 12, 128, 1, 2, 0),
                                                 (2, 64, 16, 96, 4, 4, 0), (1, 40, 9, 33, 3, 1, 1),
-                                                (2, 3, 13, 20, 7, 2, 3), (2, 8, 10, 12, 2, 3, 0)])
+                                                (2, 3, 13, 20, 7, 2, 3), (2, 8, 10, 12, 2, 3, 0),
+                                                (2, 16, 8, 64, 1, 1, 0), (2, 8, 10, 40, 2, 1, 0)])
 def test_conv2d_fwd_bwd(N, Cin, H, Cout, k, s, p):
     torch.manual_seed(N * 100 + Cin + Cout)
     x = torch.randn(N, Cin, H, H, dtype=torch.float64)
