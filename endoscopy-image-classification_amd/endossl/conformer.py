@@ -158,6 +158,13 @@ def _s():
     return _lib.stream()
 
 
+def _zero_pad(t, rows):
+    """Zero rows [rows, len) of a token-row buffer (the GEMM pad rows) and return it."""
+    if t.shape[0] > rows:
+        t[rows:].zero_()
+    return t
+
+
 class _Map:
     """An NHWC view: tensor t, element offset, (N, H, W, C) and element strides (n, h, w, c)."""
 
@@ -339,7 +346,7 @@ class _FcuTokensFn(torch.autograd.Function):
     def forward(ctx, pooled, xt, m, pre):
         N, h, w, D = pooled.shape
         np_ = h * w
-        out = torch.zeros_like(xt)
+        out = _zero_pad(torch.empty_like(xt), N * (np_ + 1))  # the kernel writes every token row
         mean = torch.empty(N * np_, device=xt.device)
         rstd = torch.empty(N * np_, device=xt.device)
         call("es_fcu_down_tokens_fwd", ptr(pooled.contiguous()), ptr(xt), ptr(m.pview(pre + "ln.weight")),
@@ -355,7 +362,7 @@ class _FcuTokensFn(torch.autograd.Function):
         N, h, w, D = pooled.shape
         np_ = h * w
         dout = dout.contiguous()
-        dxt = torch.zeros_like(dout)
+        dxt = _zero_pad(torch.empty_like(dout), N * (np_ + 1))
         dpooled = torch.empty_like(pooled)
         ws = torch.empty(_lib.load().es_fcu_down_workspace(N, np_, D), device=dout.device)
         call("es_fcu_down_tokens_bwd", ptr(dout), ptr(pooled), ptr(m.pview(pre + "ln.weight")),
@@ -419,13 +426,16 @@ class _BlockFn(torch.autograd.Function):
         s = _s()
         dev = xt.device
         b16 = torch.bfloat16
-        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
-        h1, h2 = z(Mp, D, dt=b16), z(Mp, D, dt=b16)
-        mean1, rstd1, mean2, rstd2 = z(Mp), z(Mp), z(Mp), z(Mp)
-        qkv, o = z(Mp, 3 * D, dt=b16), z(Mp, D, dt=b16)
-        lse = z(n * H * T)
-        xmid, out = z(Mp, D), z(Mp, D)
-        pre_, act = z(Mp, Hd, dt=b16), z(Mp, Hd, dt=b16)
+        # rows [M, Mp) of the weight-gradient GEMM operands (h1, o, h2, act) must read as zero; every
+        # other buffer is read on its first M rows only, so it needs no fill at all
+        e = lambda *sh, dt=torch.float32: torch.empty(*sh, dtype=dt, device=dev)  # noqa: E731
+        zp = lambda *sh, dt=torch.float32: _zero_pad(e(*sh, dt=dt), M)  # noqa: E731
+        h1, h2 = zp(Mp, D, dt=b16), zp(Mp, D, dt=b16)
+        mean1, rstd1, mean2, rstd2 = e(Mp), e(Mp), e(Mp), e(Mp)
+        qkv, o = e(Mp, 3 * D, dt=b16), zp(Mp, D, dt=b16)
+        lse = e(n * H * T)
+        xmid, out = e(Mp, D), zp(Mp, D)
+        pre_, act = e(Mp, Hd, dt=b16), zp(Mp, Hd, dt=b16)
         pv, wb = m.pview, m.wb
         call("es_layernorm_fwd", ptr(xt), D, ptr(pv(pre + "norm1.weight")), ptr(pv(pre + "norm1.bias")), ptr(h1), D,
              ptr(mean1), ptr(rstd1), M, D, LN_EPS, s)
@@ -455,10 +465,12 @@ class _BlockFn(torch.autograd.Function):
         s = _s()
         dev = xt.device
         b16 = torch.bfloat16
-        z = lambda *sh, dt=torch.float32: torch.zeros(*sh, dtype=dt, device=dev)  # noqa: E731
+        # layer-internal scratch, reused by every block's backward (they run one after another on the
+        # stream): allocated zeroed once, so the pad rows the weight-gradient GEMMs read stay zero
+        z = lambda name, *sh, dt=torch.float32: m.bwd_scratch(name, sh, dt)  # noqa: E731
         lib = _lib.load()
         dout = dout.contiguous()
-        dxb = z(Mp, D, dt=b16)
+        dxb = z("dxb", Mp, D, dt=b16)
         call("es_cast_f32_bf16", ptr(dout), ptr(dxb), Mp * D, s)
         wt, pv, gv = m.wt, m.pview, m.gview
         ws_ln = torch.empty(2 * 1024 * D, device=dev)
@@ -468,31 +480,31 @@ class _BlockFn(torch.autograd.Function):
             ws = torch.empty(lib.es_gemm_tn_workspace(N1, N2, sp), device=dev)
             call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, sp, ptr(ws), ptr(gv(wname)), 0, ptr(gv(bname)), s)
 
-        dpre = z(Mp, Hd, dt=b16)
+        dpre = z("dpre", Mp, Hd, dt=b16)
         call("es_gemm_nt", EPI_DGELU, ptr(dxb), D, ptr(wt[pre + "mlp.fc2.weight"]), D, None, ptr(dpre), Hd, None,
              ptr(pre_), Hd, M, Hd, D, 0, s)
         wgrad(dxb, D, act, Hd, pre + "mlp.fc2.weight", pre + "mlp.fc2.bias")
-        dh = z(Mp, D)
+        dh = z("dh", Mp, D)
         call("es_gemm_nt", EPI_F32, ptr(dpre), Hd, ptr(wt[pre + "mlp.fc1.weight"]), Hd, None, ptr(dh), D, None, None,
              0, M, D, Hd, 0, s)
         wgrad(dpre, Hd, h2, D, pre + "mlp.fc1.weight", pre + "mlp.fc1.bias")
-        dxm, dxmb = z(Mp, D), z(Mp, D, dt=b16)
+        dxm, dxmb = z("dxm", Mp, D), z("dxmb", Mp, D, dt=b16)
         call("es_layernorm_bwd", ptr(dh), D, ptr(xmid), D, ptr(mean2), ptr(rstd2), ptr(pv(pre + "norm2.weight")),
              ptr(dout), D, ptr(dxm), D, ptr(dxmb), D, ptr(gv(pre + "norm2.weight")), ptr(gv(pre + "norm2.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
-        do = z(Mp, D, dt=b16)
+        do = z("do", Mp, D, dt=b16)
         call("es_gemm_nt", EPI_BF16, ptr(dxmb), D, ptr(wt[pre + "attn.proj.weight"]), D, None, ptr(do), D, None,
              None, 0, M, D, D, 0, s)
         wgrad(dxmb, D, o, D, pre + "attn.proj.weight", pre + "attn.proj.bias")
-        dqkv = z(Mp, 3 * D, dt=b16)
-        delta = z(n * H * T)
+        dqkv = z("dqkv", Mp, 3 * D, dt=b16)
+        delta = z("delta", n * H * T)
         call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(do), D, ptr(dqkv), 3 * D, n, T, H,
              64 ** -0.5, s)
-        dh2 = z(Mp, D)
+        dh2 = z("dh2", Mp, D)
         call("es_gemm_nt", EPI_F32, ptr(dqkv), 3 * D, ptr(wt[pre + "attn.qkv.weight"]), 3 * D, None, ptr(dh2), D,
              None, None, 0, M, D, 3 * D, 0, s)
         wgrad(dqkv, 3 * D, h1, D, pre + "attn.qkv.weight", pre + "attn.qkv.bias")
-        dx = z(Mp, D)
+        dx = _zero_pad(torch.empty(Mp, D, device=dev), M)  # returned to autograd: fresh
         call("es_layernorm_bwd", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
@@ -585,6 +597,16 @@ class NativeConformer(nn.Module):
         self._build(flat, device=torch.device("cpu"))
         self.version = 0
         self.cur_n = 0
+
+    def bwd_scratch(self, name, shape, dtype):
+        """Zero-initialised scratch for the transformer blocks' backward, allocated once per shape."""
+        if not hasattr(self, "_bwd_scratch"):
+            self._bwd_scratch = {}
+        key = (name, tuple(shape), dtype, self.flat.device)
+        t = self._bwd_scratch.get(key)
+        if t is None:
+            t = self._bwd_scratch[key] = torch.zeros(*shape, dtype=dtype, device=self.flat.device)
+        return t
 
     # ---- parameters: views of one flat buffer; BN running stats: module buffers ------------
     def _resolve(self, name):
