@@ -212,7 +212,6 @@ class _ConvFn(torch.autograd.Function):
         dy = dy.contiguous()
         xp = ptr(x) + 4 * xm.off
         M = xm.N * Ho * Wo
-        K = xm.C * k * k
         # pixel splits sized for ~2048 workgroups (8 per CU) over es_conv2d_bwd_weight's tiles
         lib = _lib.load()
         tiles = lib.es_conv2d_dw_tiles(Cout, xm.C, k, k)
@@ -398,7 +397,7 @@ class _PatchTokensFn(torch.autograd.Function):
         dxt = dxt.contiguous()
         lib = _lib.load()
         M = N * cfg.np
-        splits = max(1, min(-(-M // 16), -(-512 // (-(-D // 64) * -(-(C * dw * dw) // 64)))))
+        splits = max(1, min(-(-M // 64), -(-2048 // lib.es_conv2d_dw_tiles(D, C, dw, dw))))
         ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(D, C, dw, dw, splits), device=dxt.device)
         dyp = ptr(dxt) + 4 * D
         call("es_conv2d_bwd_weight", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, dyp, T * D, g * D, D, D, dw, dw, dw,
@@ -738,8 +737,11 @@ class NativeConformer(nn.Module):
         n, S = x.shape[0], cfg.img_size
         self.cur_n = n
         D = cfg.dim
-        # stem: conv1 7x7/2 (NCHW images read through strides) -> bn1 -> ReLU -> maxpool 3/2
-        img = _Map(x, n, S, S, 3, sn=3 * S * S, sh=S, sw=1, sc=S * S)
+        # stem: conv1 7x7/2 -> bn1 -> ReLU -> maxpool 3/2.  The NCHW images are re-laid NHWC once (a
+        # layout copy): the implicit-GEMM gathers then read the 3 channels of a tap from one 12-byte
+        # run instead of three planes S^2 apart (stem forward / weight gradient 2-3x faster)
+        x = x.permute(0, 2, 3, 1).contiguous()
+        img = _Map(x, n, S, S, 3, sn=3 * S * S, sh=3 * S, sw=3, sc=1)
         # the parameters are not autograd inputs (their gradients go straight to flat_grad): a leaf that
         # requires grad, passed to the stem conv, puts the graph on the tape in training mode
         anchor = self._anchor if (torch.is_grad_enabled() and self.training) else None
