@@ -8,10 +8,10 @@
 // Layout: qkv bf16 [tokens, 3*D] with per-token column order [3][H][64] (the reference reshape);
 // o / dout bf16 [tokens, D] with column h*64+d; lse fp32 [image][head][token].
 //
-// Head tiles are padded to NT16*16 rows (208 for T = 197: 52 KiB for two tiles, so three
-// workgroups share a CU) and staged by LDS-DMA (global_load_lds_dwordx4, 8 rows per
-// wave-instruction); pad rows re-read token T-1, so they hold finite values whose probabilities
-// are exactly zero.  Key (or query) chunks are 32 wide for the P.V-type products; an odd last
+// Head tiles are padded to NT16*16 rows (208 for T = 197: 26 KiB each; the forward stages Q, K and
+// V, 78 KiB, two heads per CU; the backward kernels two tiles, three per CU) and staged by LDS-DMA
+// (global_load_lds_dwordx4, 8 rows per wave-instruction); pad rows re-read token T-1, so they hold
+// finite values whose probabilities are exactly zero.  Key (or query) chunks are 32 wide for the P.V-type products; an odd last
 // 16-row tile uses the K=16 MFMA (v_mfma_f32_16x16x16_bf16), whose operand maps are the first
 // half of the K=32 ones.
 //
@@ -93,8 +93,10 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
   const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
   char* Ks = smem;
   char* Vs = smem + TP * 128;
+  char* Qs = smem + 2 * TP * 128;  // Q staged with K and V: one wait, no per-tile global latency
   stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
   stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  stage_head(Qs, base + h * 64, a.ldqkv, T, TP);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -104,8 +106,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
   for (int qb = w; qb < nqt; qb += 4) {
     const int q = qb * 16 + r;
     const bool qv = q < T;
-    const bf16* qrow = base + (size_t)q * a.ldqkv + h * 64;
-    const bf16x8 qf0 = ld_row8(qrow + 8 * g, qv), qf1 = ld_row8(qrow + 32 + 8 * g, qv);
+    const bf16x8 qf0 = lds_row8(Qs, q, g), qf1 = lds_row8(Qs, q, 4 + g);
 
     // scores in log2 units (scale * log2 e folded in): p = exp2(s - max) is one v_exp_f32; keys
     // are masked only in the partial last tile (the branch is uniform per tile).
@@ -413,7 +414,7 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
   if (!qkv || !o || !lse) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, lse, nullptr, nullptr, nullptr, ldqkv, ldo, 0, 0, T, H, scale};
   const int nt16 = (T + 15) / 16;
-  const size_t lds = 2 * (size_t)nt16 * 16 * 128;
+  const size_t lds = 3 * (size_t)nt16 * 16 * 128;  // K, V, Q head tiles (two heads per CU at T = 197)
   if (g_attn_fwd_occ == 2) {
     FWD_DISPATCH(nt16, 2, nimg * H, lds, stream, a);
   } else {
