@@ -299,70 +299,114 @@ __global__ __launch_bounds__(256) void comatch_da_kernel(const float* __restrict
   (void)colsum;
 }
 
-// Stage 2: memory smoothing partials.  Workgroup (chunk, row group): 64 weak rows x SB bank rows;
-// thread t holds row t/4's embedding in registers and walks every 4th bank row of the chunk:
-// e = exp((z . b) / T), S_e += e, S_p[c] += e * bank_probs[c].  Partials [chunk][row][C+1].
-constexpr int SB = 256;
+// Stage 2: memory smoothing partials on the fp32 matrix cores (v_mfma_f32_16x16x4_f32, a k-ordered
+// fmaf chain, so S is bit-identical to an fp32 dot product).  Workgroup (chunk, row group): SB bank
+// rows staged in LDS (features [SB][L+1], probabilities [SB][32] zero-padded), 4 waves x 16 weak
+// rows.  Per 16-bank-row tile a wave computes S^T = F . Z^T (A = bank features from LDS, B = its
+// rows' embeddings held in registers for the whole chunk), e = exp(S / T), S_e += e, and
+// S_p += E . bank_probs with E straight from the first product's accumulator: lane (g, r) holds
+// S^T[bank 4g + q][row r] = E[row r][bank 4g + q], which is the A operand of k-step q when the
+// B operand (bank_probs, from LDS) uses the same bank order.  Partials [chunk][row][C+1].
+constexpr int SB = 128;
 __global__ __launch_bounds__(256) void comatch_smooth_partial_kernel(const float* __restrict__ zw, int ldz, int nu,
                                                                      int L, const float* __restrict__ bf,
                                                                      const float* __restrict__ bp, int Q, int C,
                                                                      float temperature, float* __restrict__ part) {
-  extern __shared__ float sm[];  // bank feats [SB][L] then probs [SB][C]
-  float* fs = sm;
-  float* ps = sm + SB * L;
+  extern __shared__ float sm[];
+  const int LP = L + 1;
+  float* fs = sm;            // [SB][L + 1]
+  float* ps = sm + SB * LP;  // [SB][32]
   const int chunk = blockIdx.x, j0 = chunk * SB, nb = min(SB, Q - j0);
-  for (int id = threadIdx.x; id < SB * L; id += blockDim.x) fs[id] = id / L < nb ? bf[(size_t)j0 * L + id] : 0.f;
-  for (int id = threadIdx.x; id < SB * C; id += blockDim.x) ps[id] = id / C < nb ? bp[(size_t)j0 * C + id] : 0.f;
+  for (int id = threadIdx.x; id < SB * L; id += blockDim.x) {
+    const int jj = id / L, k = id - jj * L;
+    fs[jj * LP + k] = jj < nb ? bf[(size_t)(j0 + jj) * L + k] : 0.f;
+  }
+  for (int id = threadIdx.x; id < SB * 32; id += blockDim.x) {
+    const int jj = id >> 5, c = id & 31;
+    ps[id] = (jj < nb && c < C) ? bp[(size_t)(j0 + jj) * C + c] : 0.f;
+  }
   __syncthreads();
-  const int r = blockIdx.y * 64 + (threadIdx.x >> 2), sub = threadIdx.x & 3;
-  if (r >= nu) return;
-  float z[64];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, lr = lane & 15, lg = lane >> 4;
+  const int r0 = blockIdx.y * 64 + w * 16;
+  const int ksteps = (L + 3) >> 2;
+  float zb[16];  // B operand of S^T = F . Z^T: zb[s] = Z[r0 + lr][4s + lg]  (L <= 64)
 #pragma unroll
-  for (int c = 0; c < 64; ++c) z[c] = c < L ? zw[(size_t)r * ldz + c] : 0.f;
-  float se = 0.f, sp[32];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) sp[c] = 0.f;
-  for (int j = sub; j < nb; j += 4) {
-    float d = 0.f;
-#pragma unroll
-    for (int c = 0; c < 64; ++c)
-      if (c < L) d = fmaf(z[c], fs[j * L + c], d);
-    const float e = expf(d / temperature);
-    se += e;
-#pragma unroll
-    for (int c = 0; c < 32; ++c)
-      if (c < C) sp[c] = fmaf(e, ps[j * C + c], sp[c]);
+  for (int st = 0; st < 16; ++st) {
+    const int k = 4 * st + lg;
+    zb[st] = (r0 + lr < nu && k < L) ? zw[(size_t)(r0 + lr) * ldz + k] : 0.f;
   }
-  // combine the 4 sub-lanes of a row
+  f32x4 pacc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float se = 0.f;
+  for (int jt = 0; jt * 16 < nb; ++jt) {
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f};
+    const float* frow = fs + (jt * 16 + lr) * LP;
 #pragma unroll
-  for (int o = 1; o < 4; o <<= 1) {
-    se += __shfl_xor(se, o, 64);
+    for (int st = 0; st < 16; ++st) {
+      if (st < ksteps) {
+        const int k = 4 * st + lg;
+        sv = __builtin_amdgcn_mfma_f32_16x16x4f32(k < L ? frow[k] : 0.f, zb[st], sv, 0, 0, 0);
+      }
+    }
+    float e[4];
 #pragma unroll
-    for (int c = 0; c < 32; ++c) sp[c] += __shfl_xor(sp[c], o, 64);
+    for (int q = 0; q < 4; ++q) {
+      e[q] = jt * 16 + 4 * lg + q < nb ? expf(sv[q] / temperature) : 0.f;
+      se += e[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float* prow = ps + (jt * 16 + 4 * lg + q) * 32;
+      pacc[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(e[q], prow[lr], pacc[0], 0, 0, 0);
+      pacc[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(e[q], prow[16 + lr], pacc[1], 0, 0, 0);
+    }
   }
-  if (sub == 0) {
-    float* out = part + ((size_t)chunk * nu + r) * (C + 1);
-    for (int c = 0; c < C; ++c) out[c] = sp[c];
-    out[C] = se;
-  }
+  // S_e of weak row r0 + lr: the 4 lane groups hold disjoint bank rows of it
+  se += __shfl_xor(se, 16, 64);
+  se += __shfl_xor(se, 32, 64);
+  // pacc[nt] lane holds S_p[row r0 + 4 lg + q][class 16 nt + lr]
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = r0 + 4 * lg + q, c = nt * 16 + lr;
+      if (r < nu && c < C) part[((size_t)chunk * nu + r) * (C + 1) + c] = pacc[nt][q];
+    }
+  if (lg == 0 && r0 + lr < nu) part[((size_t)chunk * nu + r0 + lr) * (C + 1) + C] = se;
 }
 
-// Stage 3 (one thread per weak row): p = a p_orig + (1-a) (sum_chunks S_p) / (sum_chunks S_e);
-// score / first-index argmax / mask.
-__global__ void comatch_pseudo_final_kernel(const float* __restrict__ probs_orig, const float* __restrict__ part,
-                                            int nchunks, int nu, int C, float alpha, float thres,
-                                            float* __restrict__ probs, int* __restrict__ pl,
-                                            float* __restrict__ mask) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= nu) return;
-  float se = 0.f;
-  for (int k = 0; k < nchunks; ++k) se += part[((size_t)k * nu + i) * (C + 1) + C];
+// Stage 3 (one workgroup per weak row): the C+1 chunk sums in a fixed-order block reduction, then
+// p = a p_orig + (1-a) S_p / S_e; score / first-index argmax / mask.
+__global__ __launch_bounds__(256) void comatch_pseudo_final_kernel(const float* __restrict__ probs_orig,
+                                                                   const float* __restrict__ part, int nchunks,
+                                                                   int nu, int C, float alpha, float thres,
+                                                                   float* __restrict__ probs, int* __restrict__ pl,
+                                                                   float* __restrict__ mask) {
+  __shared__ float red[33][256];
+  const int i = blockIdx.x, t = threadIdx.x;
+  float acc[33];
+#pragma unroll
+  for (int c = 0; c < 33; ++c) acc[c] = 0.f;
+  for (int k = t; k < nchunks; k += 256) {
+    const float* pr = part + ((size_t)k * nu + i) * (C + 1);
+#pragma unroll
+    for (int c = 0; c < 33; ++c)
+      if (c <= C) acc[c] += pr[c];
+  }
+#pragma unroll
+  for (int c = 0; c < 33; ++c) red[c][t] = acc[c];
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (t < h)
+#pragma unroll
+      for (int c = 0; c < 33; ++c) red[c][t] += red[c][t + h];
+    __syncthreads();
+  }
+  if (t != 0) return;
+  const float se = red[C][0];
   float best = -INFINITY;
   int bi = 0;
   for (int c = 0; c < C; ++c) {
-    float s = 0.f;
-    for (int k = 0; k < nchunks; ++k) s += part[((size_t)k * nu + i) * (C + 1) + c];
-    const float v = alpha * probs_orig[(size_t)i * C + c] + (1.f - alpha) * (s / se);
+    const float v = alpha * probs_orig[(size_t)i * C + c] + (1.f - alpha) * (red[c][0] / se);
     probs[(size_t)i * C + c] = v;
     if (v > best) {  // strict: first index on ties (torch.max)
       best = v;
@@ -683,12 +727,12 @@ int es_comatch_pseudo_ex(const float* logits_w, int ldl, int nu, int C, float* h
   hipLaunchKernelGGL(comatch_da_kernel, 1, 256, 0, stream, logits_w, ldl, nu, C, hist, hist_cap, hist_len, hist_pos,
                      hist_given, probs_orig);
   const int nchunks = (Q + SB - 1) / SB;
-  const size_t lds = (size_t)SB * (L + C) * 4;
+  const size_t lds = (size_t)SB * (L + 1 + 32) * 4;
   allow_lds(comatch_smooth_partial_kernel, lds);
   hipLaunchKernelGGL(comatch_smooth_partial_kernel, dim3(nchunks, (nu + 63) / 64), 256, lds, stream, z_w, ldz, nu, L,
                      bank_feats, bank_probs, Q, C, temperature, workspace);
-  hipLaunchKernelGGL(comatch_pseudo_final_kernel, (nu + 255) / 256, 256, 0, stream, probs_orig, workspace, nchunks, nu,
-                     C, alpha, thres, probs, pl, mask);
+  hipLaunchKernelGGL(comatch_pseudo_final_kernel, nu, 256, 0, stream, probs_orig, workspace, nchunks, nu, C, alpha,
+                     thres, probs, pl, mask);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -144,11 +144,13 @@ def _unit(t):
     return t / t.norm(dim=1, keepdim=True)
 
 
-@pytest.mark.parametrize("Q,zero_bank", [(600, False), (2560, True), (65536, False)])
-def test_comatch_pseudo_vs_reference_formula(Q, zero_bank):
-    """DA over a 3-entry history + memory smoothing (code/comatch.py:167-185) vs torch fp64."""
+@pytest.mark.parametrize("Q,zero_bank,nu,L", [(600, False, 448, 64), (2560, True, 448, 64), (65536, False, 448, 64),
+                                              (300, False, 37, 40)])
+def test_comatch_pseudo_vs_reference_formula(Q, zero_bank, nu, L):
+    """DA over a 3-entry history + memory smoothing (code/comatch.py:167-185) vs torch fp64.
+    (300, 37, 40): bank, weak-row and embedding sizes off the kernel's 128 / 16 / 4 tiles."""
     torch.manual_seed(Q)
-    nu, C, L, T, alpha, thres = 448, 23, 64, 0.2, 0.9, 0.6
+    C, T, alpha, thres = 23, 0.2, 0.9, 0.6
     lw = torch.randn(nu, C, device=DEV) * torch.rand(nu, 1, device=DEV) * 6
     zw = _unit(torch.randn(nu, L, device=DEV))
     bf = torch.zeros(Q, L, device=DEV) if zero_bank else _unit(torch.randn(Q, L, device=DEV))
