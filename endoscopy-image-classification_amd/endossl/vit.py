@@ -198,10 +198,11 @@ class _Grads:
 class Engine:
     """Explicit forward / backward of the ViT over C-ABI kernels.  One per (model, device)."""
 
-    # split-K sizing of the weight-gradient GEMMs: ~6 workgroups per CU (scripts/gemm_bench.py
-    # --tn-blocks sweep on MI355X: 1536 beat 512 by 10-25% on the fc1/fc2/qkv shapes); the split
-    # count is capped so the fp32 slabs stay small for the square 384x384 projection
-    TN_TARGET_BLOCKS = 1536
+    # split-K sizing of the weight-gradient GEMMs: ~3 workgroups per CU (scripts/gemm_bench.py
+    # --tn-blocks sweep 384..3072 on MI355X: 768 is fastest on fc1 / fc2 / qkv, 195-202 / 150 us vs
+    # 219-221 / 160 at 1536 -- fewer fp32 split-K slabs to write and reduce -- and 512 or fewer
+    # starve the chip); the split count is capped so the slabs stay small for the 384x384 projection
+    TN_TARGET_BLOCKS = 768
     TN_MAX_SPLITS = 128
     # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
     # GEMMs beside the data-gradient chain ("bwd"); ENDOSSL_OVERLAP=0 serialises everything on the
