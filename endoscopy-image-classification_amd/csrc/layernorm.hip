@@ -67,9 +67,18 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// two consecutive dy values as float2 (fp32 or bf16 storage)
+__device__ __forceinline__ float2 ld_dy2(const float* p) { return *(const float2*)p; }
+__device__ __forceinline__ float2 ld_dy2(const bf16* p) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  const bf16x2 v = *(const bf16x2*)p;
+  return make_float2((float)v[0], (float)v[1]);
+}
+
 // Each wave walks rows two at a time (both rows' dy / x / dres loads issued before any math).
-template <int V>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ dy, int lddy, const float* __restrict__ x,
+// DY = float or bf16 (the ViT engine's dgrad GEMMs hand over d(LN output) in bf16, half the bytes).
+template <int V, typename DY>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, int lddy, const float* __restrict__ x,
                                                      int ldx, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const float* __restrict__ gamma,
                                                      const float* __restrict__ dres, int ldres, float* __restrict__ dx,
@@ -95,7 +104,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const int c = (j * 64 + lane) * 2;
-        d[q][j] = *(const float2*)(dy + (size_t)row * lddy + c);
+        d[q][j] = ld_dy2(dy + (size_t)row * lddy + c);
         xv[q][j] = *(const float2*)(x + (size_t)row * ldx + c);
         rv[q][j] = dres ? *(const float2*)(dres + (size_t)row * ldres + c) : make_float2(0.f, 0.f);
       }
@@ -161,6 +170,33 @@ extern "C" int es_reduce_partials(const float* P, float* out, int G, int N, int 
     case 6: hipLaunchKernelGGL(KER<6>, GRID, 256, 0, STREAM, __VA_ARGS__); break; \
     default: return ES_BAD_SHAPE;                                              \
   }
+#define LN_BWD_DISPATCH(T_, V_, GRID, STREAM, ...)                                                  \
+  switch (V_) {                                                                                     \
+    case 1: hipLaunchKernelGGL(HIP_KERNEL_NAME(ln_bwd_kernel<1, T_>), GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(ln_bwd_kernel<2, T_>), GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 3: hipLaunchKernelGGL(HIP_KERNEL_NAME(ln_bwd_kernel<3, T_>), GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(ln_bwd_kernel<4, T_>), GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    case 6: hipLaunchKernelGGL(HIP_KERNEL_NAME(ln_bwd_kernel<6, T_>), GRID, 256, 0, STREAM, __VA_ARGS__); break; \
+    default: return ES_BAD_SHAPE;                                                                   \
+  }
+
+template <typename DY>
+static int ln_bwd_launch(const DY* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
+                         float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
+                         hipStream_t stream) {
+  if (M <= 0 || D % 128 || blocks <= 0) return ES_BAD_SHAPE;
+  if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || !workspace) return ES_BAD_ARG;
+  const int grid = blocks < (M + 7) / 8 ? blocks : (M + 7) / 8;
+  float* pg = workspace;
+  float* pb = workspace + (size_t)grid * D;
+  LN_BWD_DISPATCH(DY, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx, (bf16*)dxb,
+                  lddxb, pg, pb, M);
+  if (hipGetLastError() != hipSuccess) return ES_HIP_ERROR;
+  int rc = es_reduce_partials(pg, dgamma, grid, D, accumulate, stream);
+  if (rc) return rc;
+  return es_reduce_partials(pb, dbeta, grid, D, accumulate, stream);
+}
 
 extern "C" {
 
@@ -178,17 +214,17 @@ int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const f
                      const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
                      float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
                      hipStream_t stream) {
-  if (M <= 0 || D % 128 || blocks <= 0) return ES_BAD_SHAPE;
-  if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || !workspace) return ES_BAD_ARG;
-  const int grid = blocks < (M + 7) / 8 ? blocks : (M + 7) / 8;
-  float* pg = workspace;
-  float* pb = workspace + (size_t)grid * D;
-  LN_DISPATCH(ln_bwd_kernel, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx,
-              (bf16*)dxb, lddxb, pg, pb, M);
-  if (hipGetLastError() != hipSuccess) return ES_HIP_ERROR;
-  int rc = es_reduce_partials(pg, dgamma, grid, D, accumulate, stream);
-  if (rc) return rc;
-  return es_reduce_partials(pb, dbeta, grid, D, accumulate, stream);
+  return ln_bwd_launch(dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx, dxb, lddxb, dgamma, dbeta,
+                       workspace, blocks, M, D, accumulate, stream);
+}
+
+// es_layernorm_bwd with dy in bf16 (the dgrad GEMM's output image)
+int es_layernorm_bwd_b16(const void* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
+                         float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
+                         hipStream_t stream) {
+  return ln_bwd_launch((const bf16*)dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx, dxb, lddxb, dgamma,
+                       dbeta, workspace, blocks, M, D, accumulate, stream);
 }
 
 }  // extern "C"

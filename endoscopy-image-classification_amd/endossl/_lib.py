@@ -31,6 +31,7 @@ SIGNATURES = {
     "es_reduce_partials": (I, [V, V, I, I, I, V]),
     "es_layernorm_fwd": (I, [V, I, V, V, V, I, V, V, I, I, F, V]),
     "es_layernorm_bwd": (I, [V, I, V, I, V, V, V, V, I, V, I, V, I, V, V, V, I, I, I, I, V]),
+    "es_layernorm_bwd_b16": (I, [V, I, V, I, V, V, V, V, I, V, I, V, I, V, V, V, I, I, I, I, V]),
     "es_gelu_fwd": (I, [V, V, L, V]),
     "es_gelu_bwd": (I, [V, V, V, L, V]),
     "es_patch_im2col": (I, [V, V, I, I, I, V]),

@@ -483,12 +483,12 @@ class _BlockFn(torch.autograd.Function):
         call("es_gemm_nt", EPI_DGELU, ptr(dxb), D, ptr(wt[pre + "mlp.fc2.weight"]), D, None, ptr(dpre), Hd, None,
              ptr(pre_), Hd, M, Hd, D, 0, s)
         wgrad(dxb, D, act, Hd, pre + "mlp.fc2.weight", pre + "mlp.fc2.bias")
-        dh = z("dh", Mp, D)
-        call("es_gemm_nt", EPI_F32, ptr(dpre), Hd, ptr(wt[pre + "mlp.fc1.weight"]), Hd, None, ptr(dh), D, None, None,
-             0, M, D, Hd, 0, s)
+        dh = z("dh", Mp, D, dt=b16)  # d(LN output) in bf16, as the ViT engine (Engine.DH_BF16)
+        call("es_gemm_nt", EPI_BF16, ptr(dpre), Hd, ptr(wt[pre + "mlp.fc1.weight"]), Hd, None, ptr(dh), D, None,
+             None, 0, M, D, Hd, 0, s)
         wgrad(dpre, Hd, h2, D, pre + "mlp.fc1.weight", pre + "mlp.fc1.bias")
         dxm, dxmb = z("dxm", Mp, D), z("dxmb", Mp, D, dt=b16)
-        call("es_layernorm_bwd", ptr(dh), D, ptr(xmid), D, ptr(mean2), ptr(rstd2), ptr(pv(pre + "norm2.weight")),
+        call("es_layernorm_bwd_b16", ptr(dh), D, ptr(xmid), D, ptr(mean2), ptr(rstd2), ptr(pv(pre + "norm2.weight")),
              ptr(dout), D, ptr(dxm), D, ptr(dxmb), D, ptr(gv(pre + "norm2.weight")), ptr(gv(pre + "norm2.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
         do = z("do", Mp, D, dt=b16)
@@ -499,12 +499,12 @@ class _BlockFn(torch.autograd.Function):
         delta = z("delta", n * H * T)
         call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(do), D, ptr(dqkv), 3 * D, n, T, H,
              64 ** -0.5, s)
-        dh2 = z("dh2", Mp, D)
-        call("es_gemm_nt", EPI_F32, ptr(dqkv), 3 * D, ptr(wt[pre + "attn.qkv.weight"]), 3 * D, None, ptr(dh2), D,
+        dh2 = z("dh2", Mp, D, dt=b16)
+        call("es_gemm_nt", EPI_BF16, ptr(dqkv), 3 * D, ptr(wt[pre + "attn.qkv.weight"]), 3 * D, None, ptr(dh2), D,
              None, None, 0, M, D, 3 * D, 0, s)
         wgrad(dqkv, 3 * D, h1, D, pre + "attn.qkv.weight", pre + "attn.qkv.bias")
         dx = _zero_pad(torch.empty(Mp, D, device=dev), M)  # returned to autograd: fresh
-        call("es_layernorm_bwd", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
+        call("es_layernorm_bwd_b16", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
         return dx, None, None

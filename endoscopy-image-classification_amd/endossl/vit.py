@@ -186,7 +186,7 @@ class _Grads:
         self.n = n
         self.dx, self.dxb = z(Mp, D), z(Mp, D, dt=b16)
         self.dxm, self.dxmb = z(Mp, D), z(Mp, D, dt=b16)
-        self.dh = z(Mp, D)
+        self.dh = z(Mp, D, dt=b16) if Engine.DH_BF16 else z(Mp, D)  # d(LN output) from the dgrad GEMMs
         self.dpre = z(Mp, Hd, dt=b16)
         self.dqkv = z(Mp, 3 * D, dt=b16)
         self.do = z(Mp, D, dt=b16)
@@ -220,6 +220,9 @@ class Engine:
     # vs 39.1 ms -- the chip is throughput-bound, co-running kernels each take ~2x as long, and the
     # single-lane split keeps the weight-gradient GEMMs (the most MFMA-dense work) off the chain.
     LANES = int(os.environ.get("ENDOSSL_LANES", "1"))
+    # d(LN output) from the fc1 / qkv dgrad GEMMs in bf16 (ENDOSSL_DH_BF16=0: fp32) -- every GEMM
+    # operand of the backward is bf16 already; halves those epilogues' writes and the LN-backward reads
+    DH_BF16 = os.environ.get("ENDOSSL_DH_BF16", "1") == "1"
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -405,7 +408,8 @@ class Engine:
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0):
         D = self.cfg.dim
         ws = self.ln_workspace(lane)
-        call("es_layernorm_bwd", ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
+        fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"
+        call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True):
@@ -415,6 +419,7 @@ class Engine:
         final-norm grads are accumulated)."""
         cfg = self.cfg
         s = _lib.stream()
+        EPI_DH = EPI_BF16 if self.DH_BF16 else EPI_F32  # noqa: N806
         top = dfts if cfg.head == "emb" else dlogits
         if top is None:
             raise ValueError("Engine.backward needs dlogits (cls head) or dfts (emb head)")
@@ -468,8 +473,8 @@ class Engine:
             call("es_gemm_nt", EPI_DGELU, ptr(Gi.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre),
                  Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
             wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
-            call("es_gemm_nt", EPI_F32, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh), D,
-                 None, None, 0, M, D, Hd, 0, s)
+            call("es_gemm_nt", EPI_DH, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh),
+                 D, None, None, 0, M, D, Hd, 0, s)
             wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
             self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, Gi.dxmb,
                          gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
@@ -479,7 +484,7 @@ class Engine:
             wgrad_side(Gi.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
             call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
                  ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
-            call("es_gemm_nt", EPI_F32, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+            call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
             wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
             if ov:
@@ -506,6 +511,7 @@ class Engine:
         residual-gradient buffer is its disjoint row range of it.  Issue is interleaved per layer so
         both streams fill from the start."""
         cfg = self.cfg
+        EPI_DH = EPI_BF16 if self.DH_BF16 else EPI_F32  # noqa: N806
         D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
         Ml, Pl = nh * T, nh * cfg.np
         main = torch.cuda.current_stream(self.device)
@@ -542,7 +548,7 @@ class Engine:
                     call("es_gemm_nt", EPI_DGELU, ptr(G.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None,
                          ptr(G.dpre), Hd, None, ptr(pre), Hd, Ml, Hd, D, 0, s)
                     self._wgrad(G.dxb, D, act, Hd, Ml, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"), lane=ln)
-                    call("es_gemm_nt", EPI_F32, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
+                    call("es_gemm_nt", EPI_DH, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
                          ptr(G.dh), D, None, None, 0, Ml, D, Hd, 0, s)
                     self._wgrad(G.dpre, Hd, h2, D, Ml, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"), lane=ln)
                     self._ln_bwd(G.dh, xmid, m2, s2, fv(b + "norm2.weight"), L["dx"], G.dxm, G.dxmb,
@@ -553,7 +559,7 @@ class Engine:
                     self._wgrad(G.dxmb, D, o, D, Ml, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"), lane=ln)
                     call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(G.delta), ptr(G.do), D,
                          ptr(G.dqkv), 3 * D, nh, T, H, 64 ** -0.5, s)
-                    call("es_gemm_nt", EPI_F32, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D,
+                    call("es_gemm_nt", EPI_DH, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D,
                          None, ptr(G.dh), D, None, None, 0, Ml, D, 3 * D, 0, s)
                     self._wgrad(G.dqkv, 3 * D, h1, D, Ml, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"),
                                 lane=ln)

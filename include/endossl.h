@@ -73,6 +73,12 @@ int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const f
                      const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
                      float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
                      hipStream_t stream);
+// es_layernorm_bwd with dy = d(LN output) in bf16 (what the ViT engine's dgrad GEMMs write: the
+// GEMM operands downstream are bf16 already; half the bytes of the fp32 form on both sides)
+int es_layernorm_bwd_b16(const void* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
+                         float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
+                         hipStream_t stream);
 
 /* ---- standalone GELU (nn.GELU, exact erf) ---------------------------------------------------- */
 int es_gelu_fwd(const void* x, void* y, long n, hipStream_t stream);

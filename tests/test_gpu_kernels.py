@@ -257,6 +257,18 @@ def test_layernorm_fwd_bwd(D, M):
     torch.testing.assert_close(dx2, dx, rtol=0, atol=0)
     torch.testing.assert_close(dg2, gr.grad, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(db2, br.grad, rtol=1e-4, atol=1e-3)
+    # bf16 dy (es_layernorm_bwd_b16): the fp32 kernel's result on the same bf16-rounded dy, exactly
+    dyb = dy.bfloat16()
+    dx3, dg3, db3 = torch.zeros_like(dx), torch.zeros_like(dg), torch.zeros_like(db)
+    call("es_layernorm_bwd_b16", ptr(dyb), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx3), D,
+         None, D, ptr(dg3), ptr(db3), ptr(ws), 1024, M, D, 0, S())
+    dyr = dyb.float()
+    dx4, dg4, db4 = torch.zeros_like(dx), torch.zeros_like(dg), torch.zeros_like(db)
+    call("es_layernorm_bwd", ptr(dyr), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx4), D,
+         None, D, ptr(dg4), ptr(db4), ptr(ws), 1024, M, D, 0, S())
+    torch.testing.assert_close(dx3, dx4, rtol=0, atol=0)
+    torch.testing.assert_close(dg3, dg4, rtol=0, atol=0)
+    torch.testing.assert_close(db3, db4, rtol=0, atol=0)
 
 
 # ------------------------------------------------------------------------------------- ViT ends
