@@ -12,10 +12,11 @@ One step = weak forward (448) + train forward/backward (64+448) + fused losses +
 all-reduce + Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.
 
 Reported beside it:
-  roofline      dominant kernel = the fc1 forward GEMM (gemm_nt, GELU epilogue), timed live with
-                HIP events on its launch stream over the timed steps (where it shares the chip with the
-                weak forward on the second stream; "isolated" = the same launch with that stream off).  Its binding roofline is HBM:
-                698.4 MB algorithmic bytes per launch (A [M,384] bf16 read once + pre-activation and
+  roofline      dominant kernel = the fc1 forward GEMM (gemm_nt, GELU epilogue keeping GELU' for the
+                backward), timed live with HIP events on its launch stream over the timed steps (where it
+                shares the chip with the weak forward on the second stream; "isolated" = the same launch
+                with that stream off).  Its binding roofline is HBM:
+                698.4 MB algorithmic bytes per launch (A [M,384] bf16 read once + GELU'(pre) and
                 activation [M,1536] bf16 written once) take 87 us at 8 TB/s, its 119 GFLOP 47 us at
                 the bf16 dense MFMA peak.  achieved = algorithmic bytes / mean launch time; the MFMA
                 view (algorithmic FLOP / time vs 2516.6 TFLOP/s) is reported beside it.
@@ -302,7 +303,8 @@ def main():
     # A read + pre/act written (bf16) + weight image and bias read once
     alg_bytes = 2 * M_tok * K_dim + 2 * 2 * M_tok * N_hid + 2 * N_hid * K_dim + 4 * N_hid
     gbs = alg_bytes / (mean_ms / 1e3) / 1e9
-    traffic = pmc_traffic("gemm_nt_kernel<1,")
+    gelu_d = model.engine().GELU_D
+    traffic = pmc_traffic("gemm_nt_kernel<7," if gelu_d else "gemm_nt_kernel<1,")
 
     if rank == 0:
         ms = T / args.steps * 1e3
@@ -323,8 +325,11 @@ def main():
             "step_tflops": round(STEP_TFLOP_F1 / (ms / 1e3), 1),
             "step_mfma_frac": round(STEP_TFLOP_F1 / (ms / 1e3) / PEAK_BF16_TFLOPS, 4),
             "final_loss": round(loss, 6),
-            "roofline": {"kernel": f"gemm_nt_kernel<EPI_GELU> (train fc1 forward: M={M_tok}, N=1536, K=384, "
-                                   "bias + exact-GELU epilogue writing pre-activation and activation, bf16)",
+            "roofline": {"kernel": (f"gemm_nt_kernel<EPI_GELU_D> (train fc1 forward: M={M_tok}, N=1536, K=384, "
+                                    "bias + exact-GELU epilogue writing GELU'(pre) and the activation, bf16)")
+                         if gelu_d else
+                         (f"gemm_nt_kernel<EPI_GELU> (train fc1 forward: M={M_tok}, N=1536, K=384, "
+                          "bias + exact-GELU epilogue writing pre-activation and activation, bf16)"),
                          "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
                          "algorithmic_bytes": alg_bytes, "mean_launch_ms": round(mean_ms, 4),

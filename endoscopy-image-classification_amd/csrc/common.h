@@ -97,6 +97,21 @@ __device__ __forceinline__ float erf_fast(float x) {
 __device__ __forceinline__ float gelu_f(float x) {
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
+// gelu(x) and gelu'(x) together: one rcp, one exp (the erf's exp(-x^2 / 2) is the density's too)
+__device__ __forceinline__ void gelu_and_grad_f(float x, float& g, float& d) {
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  const float e = __expf(-az * az);
+  const float cdf = 0.5f * (1.0f + copysignf(1.0f - y * t * e, z));
+  g = x * cdf;
+  d = fmaf(x, 0.39894228040143268f * e, cdf);
+}
+
 // gelu'(x) = Phi(x) + x phi(x).  erf_fast's exp(-z^2), z = x / sqrt(2), IS exp(-x^2 / 2): one v_exp
 // serves both the erf and the density.
 __device__ __forceinline__ float gelu_grad_f(float x) {

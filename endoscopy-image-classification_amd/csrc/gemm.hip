@@ -30,6 +30,9 @@ enum Epi {
   EPI_F32 = 4,        // C f32 = acc (+bias)
   EPI_PATCH = 5,      // C f32 at token row (img*(np+1)+1+p) = acc + bias + pos[1+p]
   EPI_GELU_ACT = 6,   // C bf16 = gelu(acc+bias) only (inference: no pre-activation kept)
+  EPI_GELU_D = 7,     // C bf16 = gelu'(acc+bias), C2 bf16 = gelu(acc+bias): the derivative the backward
+                      // needs instead of the pre-activation (it shares the erf's exp; no erf in the backward)
+  EPI_MULAUX = 8,     // C bf16 = acc * aux_bf16 (the backward of EPI_GELU_D: dpre = dact * gelu')
 };
 
 struct NTArgs {
@@ -63,9 +66,9 @@ __device__ __forceinline__ EpiCtx<EPI> epi_ctx(const NTArgs& p) {
   x.esz = f32out ? 4 : 2;
   const unsigned crows = EPI == EPI_PATCH ? (unsigned)(p.M / p.np) * (p.np + 1) : (unsigned)p.M;
   x.c = buf_rsrc(p.C, crows * p.ldc * x.esz);
-  x.c2 = buf_rsrc(EPI == EPI_GELU ? p.C2 : p.C, crows * p.ldc * x.esz);
+  x.c2 = buf_rsrc((EPI == EPI_GELU || EPI == EPI_GELU_D) ? p.C2 : p.C, crows * p.ldc * x.esz);
   if constexpr (EPI == EPI_F32_RESID) x.aux = buf_rsrc(p.aux, (unsigned)p.M * p.ldaux * 4);
-  else if constexpr (EPI == EPI_DGELU) x.aux = buf_rsrc(p.aux, (unsigned)p.M * p.ldaux * 2);
+  else if constexpr (EPI == EPI_DGELU || EPI == EPI_MULAUX) x.aux = buf_rsrc(p.aux, (unsigned)p.M * p.ldaux * 2);
   else if constexpr (EPI == EPI_PATCH) x.aux = buf_rsrc(p.aux, (unsigned)(p.np + 1) * p.ldaux * 4);
   else x.aux = x.c;
   return x;
@@ -86,7 +89,7 @@ __device__ __forceinline__ EpiAuxRegs epi_load_aux(const NTArgs& p, const EpiCtx
     const unsigned off = ok ? (unsigned)((1 + pi) * p.ldaux + n) * 4u : ES_OOB;
     r.a0 = buf_load16(x.aux, off);
     r.a1 = buf_load16(x.aux, off + 16);
-  } else if constexpr (EPI == EPI_DGELU) {
+  } else if constexpr (EPI == EPI_DGELU || EPI == EPI_MULAUX) {
     r.a0 = buf_load16(x.aux, ok ? (unsigned)(m * p.ldaux + n) * 2u : ES_OOB);
   }
   return r;
@@ -113,6 +116,18 @@ __device__ __forceinline__ void epi_store8(const NTArgs& p, const EpiCtx<EPI>& x
   float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
   if constexpr (EPI == EPI_BF16) {
     buf_store16(pack_bf16x8(v), x.c, off);
+  } else if constexpr (EPI == EPI_GELU_D) {
+    float g[8], d[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) gelu_and_grad_f(v[i], g[i], d[i]);
+    buf_store16(pack_bf16x8(d), x.c, off);
+    buf_store16(pack_bf16x8(g), x.c2, off);
+  } else if constexpr (EPI == EPI_MULAUX) {
+    const bf16x8 gp = __builtin_bit_cast(bf16x8, a.a0);
+    float o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = v[i] * (float)gp[i];
+    buf_store16(pack_bf16x8(o), x.c, off);
   } else if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_ACT) {
     float g[8];
 #pragma unroll
@@ -138,43 +153,61 @@ __device__ __forceinline__ void epi_store8(const NTArgs& p, const EpiCtx<EPI>& x
   }
 }
 
+// Per-lane epilogue operands that do not depend on the accumulators -- segment coordinates, the bias
+// of the lane's columns and the first row chunk's aux (residual / GELU' / position rows) -- loaded
+// by epi_prefetch at kernel start, so their HBM latency hides behind the K loop.
+template <int EPI, int NF>
+struct EpiPre {
+  static constexpr int SEGR = NF * 2, SEGS = 16 * SEGR, IT = (SEGS + 63) / 64;
+  int srow[IT], scol[IT];
+  f32x4 b0[IT], b1[IT];
+  EpiAuxRegs aux0[IT];
+};
+
+template <int EPI, int NF>
+__device__ __forceinline__ EpiPre<EPI, NF> epi_prefetch(const NTArgs& p, int mw0, int nw0, int lane) {
+  using E = EpiPre<EPI, NF>;
+  constexpr bool kAux = (EPI == EPI_F32_RESID || EPI == EPI_PATCH || EPI == EPI_DGELU || EPI == EPI_MULAUX);
+  E e;
+  const EpiCtx<EPI> x = epi_ctx<EPI>(p);
+#pragma unroll
+  for (int it = 0; it < E::IT; ++it) {
+    const int sg = it * 64 + lane;
+    const bool valid = (E::SEGS % 64 == 0) || sg < E::SEGS;
+    e.srow[it] = valid ? sg / E::SEGR : (1 << 20);  // an invalid segment lands past M: dropped
+    e.scol[it] = valid ? (sg % E::SEGR) * 8 : 0;
+    e.b0[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+    e.b1[it] = e.b0[it];
+    if (p.bias) {
+      e.b0[it] = *(const f32x4*)(p.bias + nw0 + e.scol[it]);
+      e.b1[it] = *(const f32x4*)(p.bias + nw0 + e.scol[it] + 4);
+    }
+    if constexpr (kAux) e.aux0[it] = epi_load_aux<EPI>(p, x, mw0 + e.srow[it], nw0 + e.scol[it]);
+  }
+  return e;
+}
+
 // A wave's (MF*16) x (NF*16) fp32 accumulator tile goes through its private LDS region 16 rows
 // at a time (rows padded by 16 B so each 16-row ds_write_b128 is conflict-free), read back as
 // 8-column row segments (2 x ds_read_b128) and stored with 16-B accesses (each wave store
-// instruction covers whole row segments).
+// instruction covers whole row segments).  Row chunk mi + 1's aux is loaded during chunk mi.
 template <int NF>
 __host__ __device__ constexpr int epi_wave_bytes() { return 16 * (NF * 64 + 16); }
 constexpr int EPI_WAVE_BYTES = epi_wave_bytes<4>();  // 4352
 
 template <int EPI, int MF, int NF>
 __device__ __forceinline__ void staged_epilogue_g(const NTArgs& p, char* wlds, const f32x4 (&acc)[MF][NF], int mw0,
-                                                  int nw0, int lane) {
+                                                  int nw0, int lane, const EpiPre<EPI, NF>& e) {
+  using E = EpiPre<EPI, NF>;
   constexpr int ROWB = NF * 64 + 16;
-  constexpr int SEGR = NF * 2;          // 8-column segments per row
-  constexpr int SEGS = 16 * SEGR;       // per 16-row chunk
-  constexpr int IT = (SEGS + 63) / 64;  // segments per lane per chunk
-  constexpr bool kAux = (EPI == EPI_F32_RESID || EPI == EPI_PATCH || EPI == EPI_DGELU);
+  constexpr int IT = E::IT;
+  constexpr bool kAux = (EPI == EPI_F32_RESID || EPI == EPI_PATCH || EPI == EPI_DGELU || EPI == EPI_MULAUX);
   const int g = lane >> 4, r = lane & 15;
   const EpiCtx<EPI> x = epi_ctx<EPI>(p);
-  int srow[IT], scol[IT];
-  f32x4 b0[IT], b1[IT];
-#pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int sg = it * 64 + lane;
-    const bool valid = (SEGS % 64 == 0) || sg < SEGS;
-    srow[it] = valid ? sg / SEGR : (1 << 20);  // an invalid segment lands past M: dropped
-    scol[it] = valid ? (sg % SEGR) * 8 : 0;
-    b0[it] = f32x4{0.f, 0.f, 0.f, 0.f};
-    b1[it] = b0[it];
-    if (p.bias) {
-      b0[it] = *(const f32x4*)(p.bias + nw0 + scol[it]);
-      b1[it] = *(const f32x4*)(p.bias + nw0 + scol[it] + 4);
-    }
-  }
   EpiAuxRegs aux[2][IT];
   if constexpr (kAux) {
 #pragma unroll
-    for (int it = 0; it < IT; ++it) aux[0][it] = epi_load_aux<EPI>(p, x, mw0 + srow[it], nw0 + scol[it]);
+    for (int it = 0; it < IT; ++it) aux[0][it] = e.aux0[it];
   }
 #pragma unroll
   for (int mi = 0; mi < MF; ++mi) {
@@ -184,21 +217,21 @@ __device__ __forceinline__ void staged_epilogue_g(const NTArgs& p, char* wlds, c
     f32x4 v[IT][2];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-      const int rr = min(srow[it], 15);
-      v[it][0] = *(const f32x4*)(wlds + rr * ROWB + scol[it] * 4);
-      v[it][1] = *(const f32x4*)(wlds + rr * ROWB + scol[it] * 4 + 16);
+      const int rr = min(e.srow[it], 15);
+      v[it][0] = *(const f32x4*)(wlds + rr * ROWB + e.scol[it] * 4);
+      v[it][1] = *(const f32x4*)(wlds + rr * ROWB + e.scol[it] * 4 + 16);
     }
     __builtin_amdgcn_wave_barrier();
     if constexpr (kAux) {
       if (mi + 1 < MF) {
 #pragma unroll
         for (int it = 0; it < IT; ++it)
-          aux[(mi + 1) & 1][it] = epi_load_aux<EPI>(p, x, mw0 + (mi + 1) * 16 + srow[it], nw0 + scol[it]);
+          aux[(mi + 1) & 1][it] = epi_load_aux<EPI>(p, x, mw0 + (mi + 1) * 16 + e.srow[it], nw0 + e.scol[it]);
       }
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it)
-      epi_store8<EPI>(p, x, mw0 + mi * 16 + srow[it], nw0 + scol[it], v[it][0] + b0[it], v[it][1] + b1[it],
+      epi_store8<EPI>(p, x, mw0 + mi * 16 + e.srow[it], nw0 + e.scol[it], v[it][0] + e.b0[it], v[it][1] + e.b1[it],
                       aux[mi & 1][it]);
   }
 }
@@ -238,6 +271,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int g = lane >> 4, r = lane & 15;
+
+  const EpiPre<EPI, 4> epre = epi_prefetch<EPI, 4>(p, m0 + wm * 64, n0 + wn * 64, lane);
 
   const bf16* ga[4];
   const bf16* gb[2];
@@ -300,7 +335,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
   }
 
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
+  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane, epre);
 }
 
 
@@ -332,6 +367,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w / WN, wn = w % WN;
   const int g = lane >> 4, r = lane & 15;
+
+  const EpiPre<EPI, NF> epre = epi_prefetch<EPI, NF>(p, m0 + wm * MF * 16, n0 + wn * NF * 16, lane);
 
   const bf16* ga[IA];
   const bf16* gb[IBF + IBH];
@@ -409,7 +446,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
 #undef BIG_ISSUE
   __builtin_amdgcn_s_barrier();
   staged_epilogue_g<EPI, MF, NF>(p, smem + w * epi_wave_bytes<NF>(), acc, m0 + wm * MF * 16, n0 + wn * NF * 16,
-                                 lane);
+                                 lane, epre);
 }
 
 // v0 family: 128x128 output tile, 4 waves (2x2, 64x64 each), K step BKT in {32, 64}, NST-stage
@@ -438,6 +475,8 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int g = lane >> 4, r = lane & 15;
+
+  const EpiPre<EPI, 4> epre = epi_prefetch<EPI, 4>(p, m0 + wm * 64, n0 + wn * 64, lane);
 
   const bf16* ga[IPW];
   const bf16* gb[IPW];
@@ -499,7 +538,7 @@ __global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
 
   // ---- epilogue through LDS (stage buffers are free once every wave passed the last MFMA) ----
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane);
+  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane, epre);
 }
 #undef NT_ISSUE
 
@@ -744,6 +783,8 @@ inline void launch_reduce_partials(const float* P, float* out, int G, int N, int
     case EPI_F32: NT_LAUNCH(EPI_F32, BKT_, NST_)         \
     case EPI_PATCH: NT_LAUNCH(EPI_PATCH, BKT_, NST_)     \
     case EPI_GELU_ACT: NT_LAUNCH(EPI_GELU_ACT, BKT_, NST_) \
+    case EPI_GELU_D: NT_LAUNCH(EPI_GELU_D, BKT_, NST_)   \
+    case EPI_MULAUX: NT_LAUNCH(EPI_MULAUX, BKT_, NST_)   \
     default: return ES_BAD_ARG;                          \
   }
 int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
@@ -775,6 +816,8 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
     case EPI_F32: BIG_LAUNCH(EPI_F32, WM_, MF_, NF_, NST_, BKT_)                    \
     case EPI_PATCH: BIG_LAUNCH(EPI_PATCH, WM_, MF_, NF_, NST_, BKT_)                \
     case EPI_GELU_ACT: BIG_LAUNCH(EPI_GELU_ACT, WM_, MF_, NF_, NST_, BKT_)          \
+    case EPI_GELU_D: BIG_LAUNCH(EPI_GELU_D, WM_, MF_, NF_, NST_, BKT_)              \
+    case EPI_MULAUX: BIG_LAUNCH(EPI_MULAUX, WM_, MF_, NF_, NST_, BKT_)              \
     default: return ES_BAD_ARG;                                                     \
   }
 int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
@@ -804,7 +847,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   if (M <= 0 || N <= 0 || K <= 0 || (N % BN) || (K % BK) || (lda % 8) || (ldb % 8) || (ldc % 4))  // NOLINT
     return ES_BAD_SHAPE;
   if (!A || !B || !C) return ES_BAD_ARG;
-  if ((epi == EPI_GELU && !C2) || ((epi == EPI_F32_RESID || epi == EPI_DGELU || epi == EPI_PATCH) && !aux))
+  if (((epi == EPI_GELU || epi == EPI_GELU_D) && !C2) ||
+      ((epi == EPI_F32_RESID || epi == EPI_DGELU || epi == EPI_MULAUX || epi == EPI_PATCH) && !aux))
     return ES_BAD_ARG;
   if (epi == EPI_PATCH && np <= 0) return ES_BAD_ARG;
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
@@ -812,7 +856,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   // (<= 384) is epilogue-bound -> BK32 two-stage at 5 workgroups/CU (BK32 three-stage for the
   // epilogues that read an aux operand: DGELU, residual); long K -> 256x128 three-stage ring.
   int variant = g_gemm_variant;
-  if (variant < 0) variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
+  if (variant < 0)
+    variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
   if (variant == 1) {
     const int grid = ((M + BM2 - 1) / BM2) * (N / BN);
     const size_t lds = 3 * STAGE2;
@@ -825,6 +870,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
       case EPI_F32: L2(EPI_F32)
       case EPI_PATCH: L2(EPI_PATCH)
       case EPI_GELU_ACT: L2(EPI_GELU_ACT)
+      case EPI_GELU_D: L2(EPI_GELU_D)
+      case EPI_MULAUX: L2(EPI_MULAUX)
       default: return ES_BAD_ARG;
     }
 #undef L2

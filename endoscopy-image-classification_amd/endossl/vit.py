@@ -27,7 +27,7 @@ import torch.nn as nn
 from . import _lib
 from ._lib import call, ptr
 
-EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT = range(7)
+EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT, EPI_GELU_D, EPI_MULAUX = range(9)
 
 
 # code/dataset.py:21-22 (transforms.Normalize on every ViT input); uint8 batches are normalised on the GPU
@@ -167,7 +167,7 @@ class _Acts:
         self.qkv = z(Lk, Mp, 3 * D, dt=b16)
         self.o = z(Lk, Mp, D, dt=b16)
         self.lse = z(Lk, n * cfg.heads * cfg.T)
-        self.pre = z(Lk if train else 0, Mp, Hd, dt=b16)
+        self.pre = z(Lk if train else 0, Mp, Hd, dt=b16)  # fc1 pre-activation, or its GELU' (Engine.GELU_D)
         self.act = z(Lk, Mp, Hd, dt=b16)
         self.xhat = z(n, D)
         self.rstd_cls = z(n)
@@ -223,6 +223,10 @@ class Engine:
     # d(LN output) from the fc1 / qkv dgrad GEMMs in bf16 (ENDOSSL_DH_BF16=0: fp32) -- every GEMM
     # operand of the backward is bf16 already; halves those epilogues' writes and the LN-backward reads
     DH_BF16 = os.environ.get("ENDOSSL_DH_BF16", "1") == "1"
+    # the train fc1 forward stores GELU'(pre) instead of the pre-activation (EPI_GELU_D: shares the
+    # erf's exp), so the fc2 dgrad epilogue is one multiply instead of an erf + two exps per element
+    # (EPI_MULAUX); ENDOSSL_GELU_D=0 keeps pre + EPI_DGELU
+    GELU_D = os.environ.get("ENDOSSL_GELU_D", "1") == "1"
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -371,7 +375,8 @@ class Engine:
                  ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
                  cfg.eps, s)
             if train:
-                self._gemm("fc1_fwd", EPI_GELU, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+                self._gemm("fc1_fwd", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(h2), D,
+                           ptr(self.wb[b + "mlp.fc1.weight"]), D,
                            ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.pre[li]), Hd, ptr(A.act[li]), None, 0, M,
                            Hd, D, 0, s)
             else:
@@ -470,8 +475,8 @@ class Engine:
             b = f"blocks.{i}."
             Gi, Gn = GS[i % 2], GS[(i - 1) % 2]
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
-            call("es_gemm_nt", EPI_DGELU, ptr(Gi.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre),
-                 Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
+            call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.dxb), D,
+                 ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre), Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
             wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
             call("es_gemm_nt", EPI_DH, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh),
                  D, None, None, 0, M, D, Hd, 0, s)
@@ -545,7 +550,8 @@ class Engine:
                     m2, s2 = A.mean2[i][r0:r1], A.rstd2[i][r0:r1]
                     lse = A.lse[i][L["lse0"]:]
                     # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
-                    call("es_gemm_nt", EPI_DGELU, ptr(G.dxb), D, ptr(self.wt[b + "mlp.fc2.weight"]), D, None,
+                    call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(G.dxb), D,
+                         ptr(self.wt[b + "mlp.fc2.weight"]), D, None,
                          ptr(G.dpre), Hd, None, ptr(pre), Hd, Ml, Hd, D, 0, s)
                     self._wgrad(G.dxb, D, act, Hd, Ml, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"), lane=ln)
                     call("es_gemm_nt", EPI_DH, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,

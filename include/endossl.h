@@ -35,6 +35,9 @@ int es_abi_version(void);
  *   epi 4: C f32 = acc (+bias)                        (dgrad into LayerNorm backward)
  *   epi 5: C f32 at token row img*(np+1)+1+p = acc + bias + aux[1+p]   (patch embed + pos_embed)
  *   epi 6: C bf16 = GELU(acc+bias) only                (fc1 + act in inference forwards)
+ *   epi 7: C bf16 = GELU'(acc+bias), C2 bf16 = GELU(acc+bias)   (train fc1: keeps the derivative, not the
+ *          pre-activation, so the backward needs no erf; activation bits identical to epi 1)
+ *   epi 8: C bf16 = acc * aux bf16                     (fc2 dgrad times the stored GELU')
  * N % 128 == 0, K % 64 == 0; A readable for round_up(M,256) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);

@@ -18,8 +18,8 @@ from endossl._lib import call, ptr  # noqa: E402
 M_T, M_W = 512 * 197, 448 * 197
 D, HD = 384, 1536
 # (name, epi, M, N, K)  -- NT: C[M,N] = A[M,K] B[N,K]^T
-NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 1, M_T, HD, D),
-      ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 3, M_T, HD, D),
+NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 7, M_T, HD, D),
+      ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 8, M_T, HD, D),
       ("fc1_dgrad", 4, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 4, M_T, D, 3 * D)]
 # (name, M, N1, N2)  -- TN: out[N1,N2] = sum_m A1[m,N1] A2[m,N2]
 TN = [("fc2_wgrad", M_T, D, HD), ("fc1_wgrad", M_T, HD, D), ("proj_wgrad", M_T, D, D), ("qkv_wgrad", M_T, 3 * D, D)]
@@ -63,9 +63,9 @@ def main():
                 if N % {6: 256, 7: 192, 8: 256, 9: 192}.get(v, 128):
                     continue
                 lib.es_set_gemm_variant(v)
-                auxp = aux if epi in (2,) else (aux.bfloat16() if epi == 3 else None)
-                st = [ptr(A), K, ptr(Bw), K, ptr(bias) if epi not in (3, 4) else None, ptr(C), N,
-                      ptr(C2) if epi == 1 else None, ptr(auxp) if auxp is not None else None, N, M, N, K, 0, s]
+                auxp = aux if epi in (2,) else (aux.bfloat16() if epi in (3, 8) else None)
+                st = [ptr(A), K, ptr(Bw), K, ptr(bias) if epi not in (3, 4, 8) else None, ptr(C), N,
+                      ptr(C2) if epi in (1, 7) else None, ptr(auxp) if auxp is not None else None, N, M, N, K, 0, s]
                 call("es_gemm_nt", epi, *st)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()

@@ -14,7 +14,7 @@ from endossl import _lib  # noqa: E402
 from endossl._lib import call, ptr  # noqa: E402
 
 DEV = "cuda"
-EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH = range(6)
+EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT, EPI_GELU_D, EPI_MULAUX = range(9)
 
 
 def S():
@@ -103,6 +103,18 @@ def test_gemm_nt_epilogues_vs_fp32(N, gemm_variant):
     F.gelu(xp).backward(torch.ones_like(xp))
     ref = (A[:M].float() @ B.float().t()) * xp.grad
     torch.testing.assert_close(dpre.float(), ref, rtol=2e-2, atol=2e-2)
+    # GELU_D: gelu'(acc + bias) and the same activation bits as EPI_GELU; MULAUX: acc * aux
+    gd = torch.zeros_like(pre)
+    act2 = torch.zeros_like(pre)
+    call("es_gemm_nt", EPI_GELU_D, ptr(A), K, ptr(B), K, ptr(bias), ptr(gd), N, ptr(act2), None, 0, M, N, K, 0, S())
+    assert torch.equal(act2, act)
+    ac = acc.clone().requires_grad_(True)
+    F.gelu(ac).backward(torch.ones_like(ac))
+    torch.testing.assert_close(gd.float(), ac.grad, rtol=1e-2, atol=1e-2)
+    dmul = torch.zeros_like(pre)
+    call("es_gemm_nt", EPI_MULAUX, ptr(A), K, ptr(B), K, None, ptr(dmul), N, None, ptr(gd), N, M, N, K, 0, S())
+    ref = (A[:M].float() @ B.float().t()) * gd.float()
+    torch.testing.assert_close(dmul.float(), ref, rtol=1e-2, atol=1e-2)
 
 
 @pytest.mark.parametrize("D", [128, 768])
