@@ -355,6 +355,152 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+// ---- CLS-query attention (the last block: only the CLS rows reach the head) ---------------------
+// One wave per (image, head).  Lane (c = lane & 7, jg = lane >> 3) holds dims 8c..8c+7 and walks keys
+// j = jg, jg + 8, ...: each 8-lane group reads whole 128-B K / V rows (coalesced) and completes a
+// dot product with 3 xor-shuffles.  Same rounding points as attn_fwd_kernel / the backward kernels
+// (scores in log2 units, bf16(P) into P.V, bf16(dS) into dQ / dK, bf16(P) into dV); only the fp32
+// summation order differs.  Outputs are compact: o / do [img][D], lse [img][head].
+constexpr int CLS_KMAX = 32;  // keys per lane group: T <= 256
+
+__device__ __forceinline__ float grp8_sum(float v) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  return v;
+}
+
+__device__ __forceinline__ void ld8f(const bf16* p, float* f) {
+  const bf16x8 v = *(const bf16x8*)p;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
+}
+
+__global__ __launch_bounds__(64) void attn_cls_fwd_kernel(const bf16* __restrict__ qkv, int ldqkv, bf16* __restrict__ o,
+                                                          int ldo, float* __restrict__ lse, int T, int H, float scale) {
+  const int bh = blockIdx.x, img = bh / H, h = bh - img * H, D = H * 64;
+  const int lane = threadIdx.x, c = lane & 7, jg = lane >> 3;
+  const bf16* base = qkv + (size_t)img * T * ldqkv;
+  float q[8];
+  ld8f(base + h * 64 + 8 * c, q);
+  const float sl = scale * 1.44269504088896341f;
+  float s[CLS_KMAX];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int it = 0; it < CLS_KMAX; ++it) {
+    const int j = it * 8 + jg;
+    float part = 0.f;
+    if (j < T) {
+      float k[8];
+      ld8f(base + (size_t)j * ldqkv + D + h * 64 + 8 * c, k);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) part = fmaf(q[i], k[i], part);
+    }
+    const float dot = grp8_sum(part);
+    s[it] = j < T ? dot * sl : -INFINITY;
+    mx = fmaxf(mx, s[it]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < CLS_KMAX; ++it) {
+    const int j = it * 8 + jg;
+    if (j < T) {
+      const float p = __builtin_amdgcn_exp2f(s[it] - mx);
+      l += p;
+      const float pb = (float)(bf16)p;
+      float v[8];
+      ld8f(base + (size_t)j * ldqkv + 2 * D + h * 64 + 8 * c, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pb, v[i], acc[i]);
+    }
+  }
+#pragma unroll
+  for (int m = 8; m < 64; m <<= 1) {
+    l += __shfl_xor(l, m, 64);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += __shfl_xor(acc[i], m, 64);
+  }
+  if (jg == 0) {
+    const float inv = 1.0f / l;
+    bf16x8 ov;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ov[i] = (bf16)(acc[i] * inv);
+    *(bf16x8*)(o + (size_t)img * ldo + h * 64 + 8 * c) = ov;
+    if (c == 0) lse[bh] = (mx + __log2f(l)) * 0.69314718055994531f;
+  }
+}
+
+// dQ (CLS row), dK / dV (every key) and zeros for the Q part of the other rows: the whole dqkv of
+// the block's tokens, so the qkv data / weight gradient GEMMs read it as written by es_attn_bwd.
+__global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict__ qkv, int ldqkv,
+                                                          const bf16* __restrict__ o, int ldo,
+                                                          const float* __restrict__ lse,
+                                                          const bf16* __restrict__ dout, int lddo,
+                                                          bf16* __restrict__ dqkv, int lddqkv, int T, int H,
+                                                          float scale) {
+  const int bh = blockIdx.x, img = bh / H, h = bh - img * H, D = H * 64;
+  const int lane = threadIdx.x, c = lane & 7, jg = lane >> 3;
+  const bf16* base = qkv + (size_t)img * T * ldqkv;
+  bf16* dbase = dqkv + (size_t)img * T * lddqkv;
+  float q[8], dq_o[8], ov[8];
+  ld8f(base + h * 64 + 8 * c, q);
+  ld8f(dout + (size_t)img * lddo + h * 64 + 8 * c, dq_o);
+  ld8f(o + (size_t)img * ldo + h * 64 + 8 * c, ov);
+  float dpart = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) dpart += dq_o[i] * ov[i];
+  const float delta = grp8_sum(dpart);
+  const float sl = scale * 1.44269504088896341f;
+  const float lq = lse[bh] * 1.44269504088896341f;
+  float dqa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bf16x8 zero8 = {};
+  for (int it = 0; it < CLS_KMAX; ++it) {
+    const int j = it * 8 + jg;
+    if (it * 8 >= T) break;
+    float k[8], v[8];
+    float sp = 0.f, dpp = 0.f;
+    if (j < T) {
+      ld8f(base + (size_t)j * ldqkv + D + h * 64 + 8 * c, k);
+      ld8f(base + (size_t)j * ldqkv + 2 * D + h * 64 + 8 * c, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        sp = fmaf(q[i], k[i], sp);
+        dpp = fmaf(dq_o[i], v[i], dpp);
+      }
+    }
+    const float sv = grp8_sum(sp), dp = grp8_sum(dpp);
+    if (j < T) {
+      const float p = __builtin_amdgcn_exp2f(sv * sl - lq);
+      const float ds = p * (dp - delta);
+      const float pb = (float)(bf16)p, dsb = (float)(bf16)ds;
+      bf16x8 dk8, dv8;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        dk8[i] = (bf16)(dsb * q[i] * scale);
+        dv8[i] = (bf16)(pb * dq_o[i]);
+        dqa[i] = fmaf(dsb, k[i], dqa[i]);
+      }
+      bf16* drow = dbase + (size_t)j * lddqkv + h * 64 + 8 * c;
+      *(bf16x8*)(drow + D) = dk8;
+      *(bf16x8*)(drow + 2 * D) = dv8;
+      if (j > 0) *(bf16x8*)drow = zero8;
+    }
+  }
+#pragma unroll
+  for (int m = 8; m < 64; m <<= 1)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dqa[i] += __shfl_xor(dqa[i], m, 64);
+  if (jg == 0) {
+    bf16x8 d8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d8[i] = (bf16)(dqa[i] * scale);
+    *(bf16x8*)(dbase + h * 64 + 8 * c) = d8;
+  }
+}
+
 #define ATTN_CASE(KERNEL, N_, GRID, LDS, STREAM, ARGS) \
   case N_: allow_lds(KERNEL<N_>, LDS); hipLaunchKernelGGL(KERNEL<N_>, GRID, 256, LDS, STREAM, ARGS); break;
 
@@ -438,6 +584,33 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
   ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
   ATTN_DISPATCH(attn_bwd_dkv_kernel, nt16, nimg * H, lds_dkv, stream, a);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+
+// CLS-query attention of a block whose non-CLS outputs are unused (the ViT's last block): qkv
+// [nimg*T, ldqkv] -> o [nimg, ldo] (the CLS rows only, compact), lse [nimg*H].
+int es_attn_cls_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
+                    hipStream_t stream) {
+  if (nimg <= 0 || T <= 0 || T > 8 * CLS_KMAX || H <= 0 || ldqkv < 3 * H * 64 || ldo < H * 64 || (ldqkv % 8) ||
+      (ldo % 8))
+    return ES_BAD_SHAPE;
+  if (!qkv || !o || !lse) return ES_BAD_ARG;
+  hipLaunchKernelGGL(attn_cls_fwd_kernel, nimg * H, 64, 0, stream, (const bf16*)qkv, ldqkv, (bf16*)o, ldo, lse, T, H,
+                     scale);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Backward of es_attn_cls_fwd: dout [nimg, lddo] (CLS rows) -> dqkv [nimg*T, lddqkv] for every token
+// (q part zero except the CLS rows).
+int es_attn_cls_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
+                    void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
+  if (nimg <= 0 || T <= 0 || T > 8 * CLS_KMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 ||
+      ldo < H * 64 || lddo < H * 64 || (ldqkv % 8) || (lddqkv % 8) || (ldo % 8) || (lddo % 8))
+    return ES_BAD_SHAPE;
+  if (!qkv || !o || !lse || !dout || !dqkv) return ES_BAD_ARG;
+  hipLaunchKernelGGL(attn_cls_bwd_kernel, nimg * H, 64, 0, stream, (const bf16*)qkv, ldqkv, (const bf16*)o, ldo, lse,
+                     (const bf16*)dout, lddo, (bf16*)dqkv, lddqkv, T, H, scale);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

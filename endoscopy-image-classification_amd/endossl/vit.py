@@ -169,6 +169,13 @@ class _Acts:
         self.lse = z(Lk, n * cfg.heads * cfg.T)
         self.pre = z(Lk if train else 0, Mp, Hd, dt=b16)  # fc1 pre-activation, or its GELU' (Engine.GELU_D)
         self.act = z(Lk, Mp, Hd, dt=b16)
+        # the last block on its CLS rows only (Engine.PRUNE_LAST): compact [n, .] images, rows padded to 256
+        Mc = _rup(n, 256)
+        self.c_o, self.c_lse = z(Mc, D, dt=b16), z(n * cfg.heads)
+        self.c_xmid, self.c_h2 = z(Mc, D), z(Mc, D, dt=b16)
+        self.c_mean2, self.c_rstd2 = z(Mc), z(Mc)
+        self.c_pre = z(Mc, Hd, dt=b16) if train else None
+        self.c_act, self.c_xout = z(Mc, Hd, dt=b16), z(Mc, D)
         self.xhat = z(n, D)
         self.rstd_cls = z(n)
         self.logits = z(n, cfg.num_classes)
@@ -193,6 +200,13 @@ class _Grads:
         self.dpatch = z(_rup(n * cfg.np, 256), D, dt=b16)
         self.dyn = z(n, D)
         self.delta = z(n * cfg.heads * cfg.T)
+        # last block on CLS rows (Engine.PRUNE_LAST): compact gradients, and d(xmid) as a full token
+        # image whose non-CLS rows stay zero (only CLS rows are ever written)
+        Mc = _rup(n, 256)
+        self.c_dx, self.c_dxb = z(Mc, D), z(Mc, D, dt=b16)
+        self.c_dpre, self.c_dxmb, self.c_do = z(Mc, Hd, dt=b16), z(Mc, D, dt=b16), z(Mc, D, dt=b16)
+        self.c_dh = z(Mc, D, dt=b16) if Engine.DH_BF16 else z(Mc, D)
+        self.dxm_cls = z(Mp, D)
 
 
 class Engine:
@@ -227,6 +241,12 @@ class Engine:
     # erf's exp), so the fc2 dgrad epilogue is one multiply instead of an erf + two exps per element
     # (EPI_MULAUX); ENDOSSL_GELU_D=0 keeps pre + EPI_DGELU
     GELU_D = os.environ.get("ENDOSSL_GELU_D", "1") == "1"
+    # the last block on its CLS rows only: timm's head reads x[:, 0] after the last block
+    # (VisionTransformer.forward_features / forward_head), so the last block's attention is needed for
+    # the CLS queries only (over all keys) and its projection, LayerNorm 2 and MLP for the CLS rows
+    # only; in the backward d(loss)/d(non-CLS rows) of the last block's output is exactly zero, so the
+    # skipped rows contribute exactly nothing to any gradient.  ENDOSSL_PRUNE_LAST=0 runs every row.
+    PRUNE_LAST = os.environ.get("ENDOSSL_PRUNE_LAST", "1") == "1"
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -357,6 +377,7 @@ class Engine:
              cfg.np, s)
         call("es_cls_init", ptr(x0), D, ptr(self.view(flat, "cls_token")), ptr(pos), n, T, D, s)
         M = A.M
+        prune = self._prune()
         for i in range(cfg.depth):
             b = f"blocks.{i}."
             li = i if train else 0
@@ -368,6 +389,9 @@ class Engine:
                  cfg.eps, s)
             call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(self.wb[b + "attn.qkv.weight"]), D,
                  ptr(self.view(flat, b + "attn.qkv.bias")), ptr(A.qkv[li]), 3 * D, None, None, 0, M, 3 * D, D, 0, s)
+            if prune and i == cfg.depth - 1:
+                self._last_block_cls_fwd(flat, A, b, li, xin, n, train, s)
+                break
             call("es_attn_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.o[li]), D, ptr(A.lse[li]), n, T, H, 64 ** -0.5, s)
             call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
                  ptr(self.view(flat, b + "attn.proj.bias")), ptr(xmid), D, None, ptr(xin), D, M, D, D, 0, s)
@@ -386,14 +410,44 @@ class Engine:
             call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
                  ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xout), D, None, ptr(xmid), D, M, D, Hd, 0, s)
         xl = A.x[cfg.depth] if train else A.x[cfg.depth & 1]
+        Tl = T  # row stride of the CLS tokens in xl, in tokens
+        if prune:
+            xl, Tl = A.c_xout, 1
         if cfg.head == "emb":  # CLS features for ModelwEmb's heads (comatch_model.py)
-            call("es_cls_ln_fwd", ptr(xl), D, T, ptr(self.view(flat, "norm.weight")),
+            call("es_cls_ln_fwd", ptr(xl), D, Tl, ptr(self.view(flat, "norm.weight")),
                  ptr(self.view(flat, "norm.bias")), ptr(A.fts), D, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.eps, s)
             return A.fts
-        call("es_cls_head_fwd", ptr(xl), D, T, ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")),
+        call("es_cls_head_fwd", ptr(xl), D, Tl, ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")),
              ptr(self.view(flat, "head.weight")), ptr(self.view(flat, "head.bias")), ptr(A.logits),
              cfg.num_classes, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.num_classes, cfg.eps, s)
         return A.logits
+
+    def _prune(self):
+        """PRUNE_LAST in effect (read at each forward / backward: tests override it per instance);
+        the two-lane backward runs every row."""
+        return self.PRUNE_LAST and self.LANES != 2
+
+    def _last_block_cls_fwd(self, flat, A, b, li, xin, n, train, s):
+        """The last block after its qkv GEMM, on the CLS rows only (PRUNE_LAST): CLS-query attention
+        over all keys, then projection (+ the residual read from the CLS rows of xin in place), LN2
+        and the MLP on n compact rows -> A.c_xout."""
+        cfg = self.cfg
+        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
+        fv = lambda name: ptr(self.view(flat, name))  # noqa: E731
+        call("es_attn_cls_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.c_o), D, ptr(A.c_lse), n, T, H, 64 ** -0.5, s)
+        call("es_gemm_nt", EPI_F32_RESID, ptr(A.c_o), D, ptr(self.wb[b + "attn.proj.weight"]), D,
+             fv(b + "attn.proj.bias"), ptr(A.c_xmid), D, None, ptr(xin), T * D, n, D, D, 0, s)
+        call("es_layernorm_fwd", ptr(A.c_xmid), D, fv(b + "norm2.weight"), fv(b + "norm2.bias"), ptr(A.c_h2), D,
+             ptr(A.c_mean2), ptr(A.c_rstd2), n, D, cfg.eps, s)
+        if train:
+            call("es_gemm_nt", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(A.c_h2), D,
+                 ptr(self.wb[b + "mlp.fc1.weight"]), D, fv(b + "mlp.fc1.bias"), ptr(A.c_pre), Hd, ptr(A.c_act), None,
+                 0, n, Hd, D, 0, s)
+        else:
+            call("es_gemm_nt", EPI_GELU_ACT, ptr(A.c_h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+                 fv(b + "mlp.fc1.bias"), ptr(A.c_act), Hd, None, None, 0, n, Hd, D, 0, s)
+        call("es_gemm_nt", EPI_F32_RESID, ptr(A.c_act), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
+             fv(b + "mlp.fc2.bias"), ptr(A.c_xout), D, None, ptr(A.c_xmid), D, n, D, Hd, 0, s)
 
     # -------------------------------------------------------------- backward
     def _tn_splits(self, M, N1, N2):
@@ -410,11 +464,11 @@ class Engine:
         call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
              _lib.stream())
 
-    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0):
+    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None):
         D = self.cfg.dim
         ws = self.ln_workspace(lane)
         fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"
-        call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), D,
+        call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True):
@@ -455,25 +509,58 @@ class Engine:
         done = {}
         if zero_grad:
             grad.zero_()
-        G.dx.zero_()
+        prune = self._prune()
+        GL = GS[(cfg.depth - 1) % 2]
+        # d(loss)/d(CLS tokens after the last block): compact rows (prune) or the CLS rows of G.dx
+        dtop, Tt = (GL.c_dx, 1) if prune else (G.dx, T)
+        if not prune:
+            G.dx.zero_()
         if cfg.head == "emb":
             dfts = dfts.contiguous()
-            call("es_cls_ln_bwd", ptr(dfts), D, ptr(fv("norm.weight")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dx), D, T,
+            call("es_cls_ln_bwd", ptr(dfts), D, ptr(fv("norm.weight")), ptr(A.xhat), ptr(A.rstd_cls), ptr(dtop), D, Tt,
                  ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D, s)
         else:
             dlogits = dlogits.contiguous()
             call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
-                 ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(G.dx), D, T,
+                 ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(dtop), D, Tt,
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
                  cfg.num_classes, s)
         nh = n // 2
-        if (ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0 and (nh * cfg.np) % 256 == 0
-                and grad.numel() % 4 == 0):
+        if (not prune and ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0
+                and (nh * cfg.np) % 256 == 0 and grad.numel() % 4 == 0):
             return self._backward_lanes(flat, grad, A, G.dx, nh)
-        call("es_cast_f32_bf16", ptr(G.dx), ptr(GS[(cfg.depth - 1) % 2].dxb), M * D, s)
+        if prune:
+            call("es_cast_f32_bf16", ptr(GL.c_dx), ptr(GL.c_dxb), n * D, s)
+        else:
+            call("es_cast_f32_bf16", ptr(G.dx), ptr(GL.dxb), M * D, s)
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."
             Gi, Gn = GS[i % 2], GS[(i - 1) % 2]
+            if prune and i == cfg.depth - 1:
+                # ---- the last block on its CLS rows: MLP, LN2 and projection over n compact rows
+                call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.c_dxb), D,
+                     ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.c_dpre), Hd, None, ptr(A.c_pre), Hd, n, Hd,
+                     D, 0, s)
+                wgrad_side(Gi.c_dxb, D, A.c_act, Hd, n, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
+                call("es_gemm_nt", EPI_DH, ptr(Gi.c_dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
+                     ptr(Gi.c_dh), D, None, None, 0, n, D, Hd, 0, s)
+                wgrad_side(Gi.c_dpre, Hd, A.c_h2, D, n, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
+                # d(xmid) lands on the CLS rows of the full token image dxm_cls (zero elsewhere)
+                self._ln_bwd(Gi.c_dh, A.c_xmid, A.c_mean2, A.c_rstd2, fv(b + "norm2.weight"), Gi.c_dx, Gi.dxm_cls,
+                             Gi.c_dxmb, gv(b + "norm2.weight"), gv(b + "norm2.bias"), n, lddx=T * D)
+                call("es_gemm_nt", EPI_BF16, ptr(Gi.c_dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
+                     ptr(Gi.c_do), D, None, None, 0, n, D, D, 0, s)
+                wgrad_side(Gi.c_dxmb, D, A.c_o, D, n, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
+                call("es_attn_cls_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.c_o), D, ptr(A.c_lse), ptr(Gi.c_do), D,
+                     ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
+                call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+                     ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
+                wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
+                if ov:
+                    done[i] = side.record_event()
+                self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), Gi.dxm_cls, G.dx, Gn.dxb,
+                             gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
+                continue
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
             call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.dxb), D,
                  ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre), Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)

@@ -68,6 +68,14 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
 /* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass) */
 int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
                 int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
+/* CLS-query attention for a block whose non-CLS outputs are unused (the last block: only the CLS
+ * token reaches timm's head, VisionTransformer.forward_features x[:, 0]).  o / dout are compact
+ * [nimg, ld] CLS rows, lse [nimg*H]; the backward writes dqkv for every token (q part zero off the
+ * CLS rows), as es_attn_bwd would for a dout that is zero off the CLS rows. */
+int es_attn_cls_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
+                    hipStream_t stream);
+int es_attn_cls_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
+                    void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
 
 /* ---- LayerNorm(eps) (code/models/conformer.py:58,60,65) -------------------------------------- */
 int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,

@@ -232,6 +232,57 @@ def test_attention_bwd(n, T, H):
     assert torch.all(dqkv[n * T:] == 0)
 
 
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1)])
+def test_attention_cls_fwd_bwd(n, T, H):
+    """es_attn_cls_fwd / _bwd (the last block's CLS queries only) against the full-token kernels at
+    the CLS rows -- same rounding points, fp32 summation order only -- and against fp32 torch; the
+    backward equals es_attn_bwd fed a dout that is zero off the CLS rows, over EVERY token's dqkv."""
+    torch.manual_seed(300 + T)
+    D = H * 64
+    qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
+    cls = torch.arange(n, device=DEV) * T
+    # full kernels
+    o = torch.zeros(qkv.shape[0], D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(n * H * T, device=DEV)
+    call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
+    # CLS kernels
+    oc = torch.zeros(n, D, dtype=torch.bfloat16, device=DEV)
+    lc = torch.zeros(n * H, device=DEV)
+    call("es_attn_cls_fwd", ptr(qkv), 3 * D, ptr(oc), D, ptr(lc), n, T, H, 64 ** -0.5, S())
+    torch.cuda.synchronize()
+    torch.testing.assert_close(lc.view(n, H), lse.view(n, H, T)[:, :, 0], rtol=1e-5, atol=1e-5)
+    # the bf16 outputs agree to within one rounding step of the output
+    assert ((oc.float() - o[cls].float()).abs() <= o[cls].float().abs() * 2 ** -7 + 1e-6).all()
+    o_ref, _ = _attn_ref(qkv[:n * T], n, T, H)
+    torch.testing.assert_close(oc.float(), o_ref[cls], rtol=2e-2, atol=2e-2)
+    # backward: dout nonzero on the CLS rows only
+    doc = torch.randn(n, D, device=DEV).bfloat16()
+    dout = torch.zeros(qkv.shape[0], D, dtype=torch.bfloat16, device=DEV)
+    dout[cls] = doc
+    dq_full = torch.zeros_like(qkv)
+    delta = torch.zeros(n * H * T, device=DEV)
+    call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(dout), D, ptr(dq_full), 3 * D, n, T,
+         H, 64 ** -0.5, S())
+    dq_cls = torch.full_like(qkv, float("nan"))  # every token row must be written
+    dq_cls[n * T:] = 0
+    call("es_attn_cls_bwd", ptr(qkv), 3 * D, ptr(oc), D, ptr(lc), ptr(doc), D, ptr(dq_cls), 3 * D, n, T, H,
+         64 ** -0.5, S())
+    torch.cuda.synchronize()
+    assert torch.isfinite(dq_cls).all()
+    x = qkv[:n * T].float().requires_grad_(True)
+    o_r, _ = _attn_ref(x, n, T, H)
+    o_r.backward(dout[:n * T].float())
+    for part in range(3):
+        a = dq_cls[:n * T, part * D:(part + 1) * D].float()
+        b = dq_full[:n * T, part * D:(part + 1) * D].float()
+        r = x.grad[:, part * D:(part + 1) * D]
+        scale = max(r.abs().max().item(), 1e-2)
+        assert (a - b).abs().max().item() / scale < 1e-2, part
+        assert (a - r).abs().max().item() / scale < 3e-2, part
+    qpart = dq_cls[:n * T, :D].view(n, T, D)
+    assert torch.all(qpart[:, 1:] == 0)
+
+
 # ------------------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("D", [128, 384, 768])
 @pytest.mark.parametrize("M", [1000, 1001, 7])

@@ -306,6 +306,47 @@ def test_two_lane_backward_matches_single_lane():
     assert worst <= 1e-5, worst
 
 
+@pytest.mark.parametrize("head", ["cls", "emb"])
+def test_last_block_cls_rows_match_full_rows(head):
+    """Engine.PRUNE_LAST (the last block's attention for the CLS queries only, its projection / LN2 /
+    MLP on the CLS rows only) gives the logits / CLS features and every parameter gradient of the
+    full-row last block: the skipped rows feed nothing downstream, their gradient is exactly zero.
+    Differences come only from the CLS attention's fp32 summation order (bf16 rounding of o / dqkv)."""
+    from endossl.vit import NativeViT
+    vcfg, _ = _tiny_cfgs()
+    if head == "emb":
+        vcfg = type(vcfg)(**{**vcfg.as_dict(), "head": "emb"})
+    m = NativeViT(vcfg, seed=7).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(40, 3, 64, 64, device=DEV, generator=g)
+    outs, grads = {}, {}
+    for prune in (False, True):
+        eng.PRUNE_LAST = prune
+        y = eng.forward(m.flat, [x], train=True).clone()
+        dy = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(9)) * 1e-2
+        gr = torch.zeros_like(m.flat)
+        if head == "emb":
+            eng.backward(m.flat, gr, dfts=dy)
+        else:
+            eng.backward(m.flat, gr, dlogits=dy)
+        yw = eng.forward(m.flat, [x], train=False).clone()
+        torch.cuda.synchronize()
+        outs[prune], grads[prune] = (y, yw), gr.clone()
+    del eng.PRUNE_LAST
+    for a, b in zip(outs[True], outs[False]):
+        assert _rel(a, b) <= 2e-3, _rel(a, b)
+    worst = 0.0
+    for name, _ in eng.layout:
+        a, b = eng.view(grads[True], name), eng.view(grads[False], name)
+        assert torch.isfinite(a).all()
+        if b.abs().max() > 0:
+            worst = max(worst, _rel(a, b))
+    _record(f"last_block_cls_rows_{head}", worst_rel_l2=worst, out_rel=_rel(outs[True][0], outs[False][0]))
+    assert worst <= 1e-2, worst
+
+
 def test_uint8_input_path_matches_normalised_fp32():
     """es_patch_im2col_u8 (ToTensor + Normalize fused into the patch gather, code/dataset.py:21-22,
     49-51) gives the same logits, bit for bit, as the fp32 images normalised the torchvision way."""
