@@ -20,7 +20,9 @@ Reported beside it:
                 activation [M,1536] bf16 written once) take 87 us at 8 TB/s, its 119 GFLOP 47 us at
                 the bf16 dense MFMA peak.  achieved = algorithmic bytes / mean launch time; the MFMA
                 view (algorithmic FLOP / time vs 2516.6 TFLOP/s) is reported beside it.
-  step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.
+  step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.  The engine skips
+                the last block's non-CLS rows after its qkv GEMM (their outputs never reach the head;
+                Engine.PRUNE_LAST), so it executes fewer FLOPs than that: `executed_step_tflop`.
   cpu_baseline  the oracle (CPU fp32 restatement pinned to the reference, kind "port") timed on a
                 bounded sample (B=8, mu=7: 56 unlabeled images/step) on the host cores, rank 0, N=1.
 """
@@ -41,6 +43,15 @@ STD = (0.229, 0.224, 0.225)
 PEAK_BF16_TFLOPS = 256 * 2.4e9 * 4096 / 1e12  # 2516.6 dense (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md §HBM; ~6300 achievable)
 STEP_TFLOP_F1 = 18.247  # fwd 960 imgs + bwd 512 imgs, 9.197 GFLOP/img fwd
+
+
+def vit_s_pruned_tflop(n_fwd, n_bwd):
+    """FLOPs the last block does NOT execute with Engine.PRUNE_LAST (ViT-S/16 at 224^2): for the 196
+    non-CLS tokens of each image, projection + fc1 + fc2 (2*D*(D + 2*Hd)) and their attention
+    queries (4*T*64*H); forward over n_fwd images, backward (2x) over n_bwd."""
+    D, Hd, T, H = 384, 1536, 197, 6
+    per_img = (T - 1) * (2 * D * (D + 2 * Hd) + 4 * T * 64 * H)
+    return per_img * (n_fwd + 2 * n_bwd) / 1e12
 
 
 def synth_u8(n, size, gen, device):
@@ -165,6 +176,9 @@ def run_secondary(args):
         batch = ((x, y), tuple(synth_images(B * MU, 224, g, dev) for _ in range(3)), None)
         batch = (batch[0], (batch[1], None))
         unl, tfl = B * MU, 3 * 9.197e9 * (B + 3 * B * MU) / 1e12 + 2 * (B * MU) * Q * (L + 23) / 1e12
+        from endossl.vit import Engine
+        exe = tfl - (vit_s_pruned_tflop(B + 3 * B * MU, B + 3 * B * MU) if Engine.PRUNE_LAST and Engine.LANES != 2
+                     else 0.0)
         desc = (f"C1: CoMatch ViT-S/16 step, B={B} + 3 x mu*B={B * MU} (weak, strong0, strong1), 224^2, L={L}, "
                 f"bank Q={Q} (memory smoothing over all Q rows), EMA 0.999, lambda_u=lambda_c=2")
     else:
@@ -184,6 +198,7 @@ def run_secondary(args):
         x, y = synth_images(B, 224, g, dev), torch.randint(0, 23, (B,), generator=g, device=dev)
         batch = ((x, y), ((synth_images(B * MU, 224, g, dev), synth_images(B * MU, 224, g, dev)), None))
         unl, tfl = B * MU, conformer_step_tflop(ccfg, B + 2 * B * MU)
+        exe = tfl
         desc = (f"S1: SemiFormer step on Conformer-Ti (code/build.py:135-142: patch 16, embed 384, depth 12, 6 heads, "
                 f"channel_ratio 1), B={B} + 2 x mu*B={B * MU}, 224^2, C=23, tau=0.95, lambda_u=1, EMA 0.999")
     for _ in range(args.warmup):
@@ -208,7 +223,8 @@ def run_secondary(args):
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16 (transformer GEMMs) / fp32", "data": "synthetic (HBM-resident, seed 0)",
             "config": {"workload": desc, "parallelism": f"dp{world}"},
-            "step_tflop": round(tfl, 3), "step_tflops": round(tfl / (ms / 1e3), 1),
+            "step_tflop": round(tfl, 3), "executed_step_tflop": round(exe, 3),
+            "step_tflops": round(tfl / (ms / 1e3), 1),
             "final_loss": round(out["loss"].item(), 6)}), flush=True)
     dist.barrier()
 
@@ -232,7 +248,7 @@ def main():
     from endossl import dist
     from endossl.fixmatch import FixMatch
     from endossl.utils import AttrDict
-    from endossl.vit import NativeViT, ViTConfig
+    from endossl.vit import Engine, NativeViT, ViTConfig
 
     rank, world, local = dist.init_from_env()
     torch.cuda.set_device(local)
@@ -324,6 +340,8 @@ def main():
                        "parallelism": f"dp{world}"},
             "step_tflops": round(STEP_TFLOP_F1 / (ms / 1e3), 1),
             "step_mfma_frac": round(STEP_TFLOP_F1 / (ms / 1e3) / PEAK_BF16_TFLOPS, 4),
+            "executed_step_tflop": round(STEP_TFLOP_F1 - (vit_s_pruned_tflop(B * (1 + 2 * MU), B * (1 + MU))
+                                                          if Engine.PRUNE_LAST and Engine.LANES != 2 else 0.0), 3),
             "final_loss": round(loss, 6),
             "roofline": {"kernel": (f"gemm_nt_kernel<EPI_GELU_D> (train fc1 forward: M={M_tok}, N=1536, K=384, "
                                     "bias + exact-GELU epilogue writing GELU'(pre) and the activation, bf16)")
