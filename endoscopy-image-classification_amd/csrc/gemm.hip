@@ -855,9 +855,16 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py): short K
   // (<= 384) is epilogue-bound -> BK32 two-stage at 5 workgroups/CU (BK32 three-stage for the
   // epilogues that read an aux operand: DGELU, residual); long K -> 256x128 three-stage ring.
+  // The fc2 dgrad (EPI_MULAUX: 310 MB of GELU' read, 310 MB written per launch at F1) runs best on
+  // the 256x256 tile (BK64, 2 stages): 200 vs 228 us for the 128x128 BK32 kernel.  (The fc1
+  // forward, 238 vs 251 us alone, loses with the weak forward co-running: 0.50 vs 0.39 ms.)
   int variant = g_gemm_variant;
-  if (variant < 0)
-    variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
+  if (variant < 0) {
+    if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
+      variant = 6;
+    else
+      variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
+  }
   if (variant == 1) {
     const int grid = ((M + BM2 - 1) / BM2) * (N / BN);
     const size_t lds = 3 * STAGE2;
