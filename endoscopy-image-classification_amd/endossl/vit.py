@@ -247,6 +247,12 @@ class Engine:
     # only; in the backward d(loss)/d(non-CLS rows) of the last block's output is exactly zero, so the
     # skipped rows contribute exactly nothing to any gradient.  ENDOSSL_PRUNE_LAST=0 runs every row.
     PRUNE_LAST = os.environ.get("ENDOSSL_PRUNE_LAST", "1") == "1"
+    # inference rows (the weak forward): fc1 -> GELU -> fc2 + residual in one kernel
+    # (es_mlp_fwd_infer), the [tokens, 4D] activation never written to HBM.  Off by default
+    # (ENDOSSL_FUSED_MLP=1 turns it on): at the F1 weak shape it takes 0.43 ms vs 0.375 ms for the
+    # two GEMMs -- one wave per SIMD (the fc2 accumulators and the register-resident h rows use
+    # ~420 registers) leaves the LDS-fragment latency exposed (scripts/mlp_bench.py)
+    FUSED_MLP = os.environ.get("ENDOSSL_FUSED_MLP", "0") == "1"
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -310,6 +316,14 @@ class Engine:
         if version is not None and version == self._packed_version:
             return
         call("es_pack_weights", ptr(flat), ptr(self._pack_tab), self._nmat, _lib.stream())
+        if self.FUSED_MLP:  # chunk-major fc2 images for es_mlp_fwd_infer
+            cfg = self.cfg
+            if not hasattr(self, "_w2c"):
+                self._w2c = {i: torch.zeros(cfg.hidden // 32, cfg.dim, 32, dtype=torch.bfloat16, device=self.device)
+                             for i in range(cfg.depth)}
+            for i in range(cfg.depth):
+                call("es_pack_chunk32", ptr(self.wb[f"blocks.{i}.mlp.fc2.weight"]), ptr(self._w2c[i]), cfg.dim,
+                     cfg.hidden, _lib.stream())
         self._packed_version = version if version is not None else -1
 
     def acts(self, n, train):
@@ -398,6 +412,11 @@ class Engine:
             call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
                  ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
                  cfg.eps, s)
+            if not train and self.FUSED_MLP and D in (128, 384) and hasattr(self, "_w2c"):
+                call("es_mlp_fwd_infer", ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]),
+                     ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(self._w2c[i]),
+                     ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xmid), D, ptr(xout), D, M, D, Hd, s)
+                continue
             if train:
                 self._gemm("fc1_fwd", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(h2), D,
                            ptr(self.wb[b + "mlp.fc1.weight"]), D,

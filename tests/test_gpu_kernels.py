@@ -283,6 +283,46 @@ def test_attention_cls_fwd_bwd(n, T, H):
     assert torch.all(qpart[:, 1:] == 0)
 
 
+# ------------------------------------------------------------------------------------- fused MLP
+@pytest.mark.parametrize("M,D,Hd", [(1000, 384, 1536), (300, 128, 512), (128, 384, 32), (5, 128, 64),
+                                    (257, 384, 96)])
+def test_mlp_fwd_infer(M, D, Hd):
+    """es_mlp_fwd_infer (fc1 -> GELU -> fc2 + residual, activation kept on chip) against the two
+    unfused GEMMs it replaces in the weak forward (EPI_GELU_ACT, then EPI_F32_RESID) and against
+    fp32 torch with the same bf16 activation rounding.  Rows >= M are never written."""
+    torch.manual_seed(M + D + Hd)
+    hb = _pad_rows(torch.randn(M, D, device=DEV).bfloat16())
+    W1 = (torch.randn(Hd, D, device=DEV) * D ** -0.5).bfloat16()
+    W2 = (torch.randn(D, Hd, device=DEV) * Hd ** -0.5).bfloat16()
+    b1 = torch.randn(Hd, device=DEV) * 0.1
+    b2 = torch.randn(D, device=DEV) * 0.1
+    resid = _pad_rows(torch.randn(M, D, device=DEV))
+    out = torch.full_like(resid, 7.0)
+    W2c = torch.zeros(Hd // 32, D, 32, dtype=torch.bfloat16, device=DEV)
+    call("es_pack_chunk32", ptr(W2), ptr(W2c), D, Hd, S())
+    torch.cuda.synchronize()
+    assert torch.equal(W2c, W2.view(D, Hd // 32, 32).permute(1, 0, 2))
+    call("es_mlp_fwd_infer", ptr(hb), D, ptr(W1), ptr(b1), ptr(W2c), ptr(b2), ptr(resid), D, ptr(out), D, M, D, Hd,
+         S())
+    ref2 = None
+    if Hd % 128 == 0:  # the unfused pair (es_gemm_nt needs N % 128 == 0)
+        act = torch.zeros(hb.shape[0], Hd, dtype=torch.bfloat16, device=DEV)
+        call("es_gemm_nt", EPI_GELU_ACT, ptr(hb), D, ptr(W1), D, ptr(b1), ptr(act), Hd, None, None, 0, M, Hd, D, 0,
+             S())
+        ref2 = torch.zeros_like(resid)
+        call("es_gemm_nt", EPI_F32_RESID, ptr(act), Hd, ptr(W2), Hd, ptr(b2), ptr(ref2), D, None, ptr(resid), D, M,
+             D, Hd, 0, S())
+    torch.cuda.synchronize()
+    pre = hb[:M].float() @ W1.float().t() + b1
+    a32 = F.gelu(pre).bfloat16().float()
+    ref = a32 @ W2.float().t() + b2 + resid[:M]
+    scale = (ref - resid[:M]).abs().max().item()
+    if ref2 is not None:
+        assert (out[:M] - ref2[:M]).abs().max().item() <= 2e-2 * scale, (out[:M] - ref2[:M]).abs().max().item()
+    assert (out[:M] - ref).abs().max().item() <= 2e-2 * scale
+    assert torch.all(out[M:] == 7.0)
+
+
 # ------------------------------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("D", [128, 384, 768])
 @pytest.mark.parametrize("M", [1000, 1001, 7])

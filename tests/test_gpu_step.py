@@ -347,6 +347,32 @@ def test_last_block_cls_rows_match_full_rows(head):
     assert worst <= 1e-2, worst
 
 
+def test_fused_mlp_weak_forward_matches_gemms():
+    """ENDOSSL_FUSED_MLP (opt-in): the inference forward with es_mlp_fwd_infer gives the logits of the
+    two-GEMM MLP within the bf16 rounding of the activation (fp32 summation order only)."""
+    from endossl.vit import NativeViT
+    vcfg, _ = _tiny_cfgs()
+    m = NativeViT(vcfg, seed=11).to(DEV)
+    eng = m.engine()
+    x = torch.randn(24, 3, 64, 64, device=DEV, generator=torch.Generator(device=DEV).manual_seed(2))
+    outs, mids = {}, {}
+    for fused in (False, True):
+        eng.FUSED_MLP = fused
+        eng.pack(m.flat)
+        outs[fused] = eng.forward(m.flat, [x], train=False).clone()
+        mids[fused] = eng.acts(24, False).x[1].clone()  # layer 0's output: through the fused MLP
+    for t in eng._w2c.values():  # the fused path is the one that ran: wrecking its fc2 image shows
+        t.zero_()
+    eng.forward(m.flat, [x], train=False)
+    assert not torch.equal(eng.acts(24, False).x[1], mids[True])
+    del eng.FUSED_MLP
+    torch.cuda.synchronize()
+    _record("fused_mlp_weak_forward", rel=_rel(outs[True], outs[False]), layer0_rel=_rel(mids[True], mids[False]),
+            layer0_maxabs=_maxabs(mids[True], mids[False]))
+    assert _rel(mids[True], mids[False]) <= 5e-3
+    assert _rel(outs[True], outs[False]) <= 5e-3
+
+
 def test_uint8_input_path_matches_normalised_fp32():
     """es_patch_im2col_u8 (ToTensor + Normalize fused into the patch gather, code/dataset.py:21-22,
     49-51) gives the same logits, bit for bit, as the fp32 images normalised the torchvision way."""
