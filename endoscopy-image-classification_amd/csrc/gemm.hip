@@ -118,8 +118,7 @@ __device__ __forceinline__ void epi_store8(const NTArgs& p, const EpiCtx<EPI>& x
     buf_store16(pack_bf16x8(v), x.c, off);
   } else if constexpr (EPI == EPI_GELU_D) {
     float g[8], d[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) gelu_and_grad_f(v[i], g[i], d[i]);
+    gelu_and_grad_f8(v, g, d);
     buf_store16(pack_bf16x8(d), x.c, off);
     buf_store16(pack_bf16x8(g), x.c2, off);
   } else if constexpr (EPI == EPI_MULAUX) {
@@ -129,9 +128,8 @@ __device__ __forceinline__ void epi_store8(const NTArgs& p, const EpiCtx<EPI>& x
     for (int i = 0; i < 8; ++i) o[i] = v[i] * (float)gp[i];
     buf_store16(pack_bf16x8(o), x.c, off);
   } else if constexpr (EPI == EPI_GELU || EPI == EPI_GELU_ACT) {
-    float g[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) g[i] = gelu_f(v[i]);
+    float g[8], d[8];  // d unused: its two ops are dead code
+    gelu_and_grad_f8(v, g, d);
     if constexpr (EPI == EPI_GELU) {
       buf_store16(pack_bf16x8(v), x.c, off);
       buf_store16(pack_bf16x8(g), x.c2, off);
@@ -459,8 +457,13 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
 //            16-row x 16-B fragment reads under the ds_read_b128 lane groups of
 //            MI355X_MICROARCH.md §LDS; the plain c ^ ((r>>2)&3) is 2-way conflicted there)
 
+// GELU epilogues: 4 waves per SIMD (<= 128 VGPRs incl. the 64 accumulators), i.e. 4 workgroups
+// per CU at the 32-KiB two-stage footprint; the packed GELU would otherwise take a few more
+// registers and drop to 3 (measured slower).  The other epilogues fit without the bound.
+template <int EPI>
+constexpr int nt_min_waves() { return (EPI == EPI_GELU || EPI == EPI_GELU_ACT || EPI == EPI_GELU_D) ? 4 : 1; }
 template <int EPI, int BKT, int NST>
-__global__ __launch_bounds__(256) void gemm_nt_kernel(NTArgs p) {
+__global__ __launch_bounds__(256, nt_min_waves<EPI>()) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int ROWB = BKT * 2;              // bytes per LDS row
   constexpr int RPI = 1024 / ROWB;           // rows per 1-KiB glds instruction
