@@ -3,6 +3,7 @@
 
   python scripts/roofline_phases.py gpurun_out/prof_f1 <tag> <bench json line file>
 Steps are delimited by the Adam/EMA sweep (adam_ema_kernel): 2 warm-up, 5 timed, 2 isolated."""
+import collections
 import csv
 import json
 import os
@@ -16,11 +17,18 @@ ends = [int(r["End_Timestamp"]) for r in rows if "adam_ema_kernel" in r["Kernel_
 b = json.loads([ln for ln in open(bench) if ln.startswith("{")][-1])["roofline"]
 
 
+# the full-M launches only (the last block's CLS-row GEMMs use the same kernel on a small grid):
+# the kernel's most frequent grid size
+grids = collections.Counter(r.get("Grid_Size_X", r.get("Grid_Size", "")) for r in rows if kern in r["Kernel_Name"])
+main_grid = grids.most_common(1)[0][0]
+
+
 def avg(a, z):
     lo = ends[a - 1] if a > 0 else 0
     hi = ends[z]
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows
-         if kern in r["Kernel_Name"] and lo < int(r["Start_Timestamp"]) <= hi]
+         if kern in r["Kernel_Name"] and lo < int(r["Start_Timestamp"]) <= hi
+         and r.get("Grid_Size_X", r.get("Grid_Size", "")) == main_grid]
     return sum(d) / len(d) / 1e3, len(d)
 
 
