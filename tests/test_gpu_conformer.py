@@ -194,9 +194,10 @@ def test_bn2d_fwd_bwd(rows_shape, C, relu, with_res):
 
 
 # ------------------------------------------------------------------------------------ pools
-def test_maxpool_avgpool_upsample():
+@pytest.mark.parametrize("C", [24, 6])  # the 4-channel vector kernels, and the scalar ones
+def test_maxpool_avgpool_upsample(C):
     torch.manual_seed(11)
-    N, H, C = 3, 13, 24
+    N, H = 3, 13
     x = torch.randn(N, C, H, H, dtype=torch.float64)
     x[0, 0, 2, 2] = x[0, 0, 2, 3] = 5.0  # a tie inside one window: the first (row-major) wins, as torch
     xr = x.clone().requires_grad_(True)
