@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a) {
 }
 
 // dK, dV: key on the lane; Q and dO of the whole head in LDS with lse / delta per query.
-template <int NT16>
+template <int NT16, bool SELF_DELTA = false>
 __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
@@ -280,9 +280,32 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   // lse in log2 units; padded queries get +inf so their probabilities are exactly 0
   for (int t = threadIdx.x; t < TP; t += blockDim.x)
     lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] * 1.44269504088896341f : INFINITY;
-  for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  if constexpr (!SELF_DELTA) {
+    for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    // delta = rowsum(dO * O) for every query of the head, here instead of in the dQ pass, so the
+    // dQ and dK/dV passes are independent launches (they can run on two streams): dO from its LDS
+    // image, O from HBM, 4 lanes per query
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t0 = 0; t0 < TP; t0 += 64) {
+      const int tq = t0 + (threadIdx.x >> 2), part = threadIdx.x & 3;
+      float dsum = 0.f;
+      if (tq < T) {
+        const bf16* orow = a.o + ((size_t)img * T + tq) * a.ldo + h * 64 + part * 16;
+        const bf16x8 o0 = *(const bf16x8*)orow, o1 = *(const bf16x8*)(orow + 8);
+        const bf16x8 d0 = lds_row8(Ds, tq, 2 * part), d1 = lds_row8(Ds, tq, 2 * part + 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += (float)d0[j] * (float)o0[j] + (float)d1[j] * (float)o1[j];
+      }
+      dsum += __shfl_xor(dsum, 1, 64);
+      dsum += __shfl_xor(dsum, 2, 64);
+      if (part == 0 && tq < TP) del_s[tq] = tq < T ? dsum : 0.f;
+    }
+    __syncthreads();
+  }
   const float sl = a.scale * 1.44269504088896341f;
 
   const int nkt = (T + 15) >> 4;
@@ -587,6 +610,49 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+
+// es_attn_bwd split in two independent launches (run them on two streams): the dQ pass, and the
+// dK/dV pass computing its own delta = rowsum(dO * O).  delta: workspace [nimg*H*T] of the dQ pass.
+int es_attn_bwd_dq(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta,
+                   const void* dout, int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale,
+                   hipStream_t stream) {
+  if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
+      (lddqkv % 8) || (ldo % 8) || (lddo % 8))
+    return ES_BAD_SHAPE;
+  if (!qkv || !o || !lse || !delta || !dout || !dqkv) return ES_BAD_ARG;
+  AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, delta, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
+             lddqkv, T, H, scale};
+  const int nt16 = (T + 15) / 16;
+  const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
+  ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+#define DKV_SELF(N_) attn_bwd_dkv_kernel<N_, true>
+int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
+                    void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
+  if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
+      (lddqkv % 8) || (ldo % 8) || (lddo % 8))
+    return ES_BAD_SHAPE;
+  if (!qkv || !o || !lse || !dout || !dqkv) return ES_BAD_ARG;
+  AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, nullptr, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
+             lddqkv, T, H, scale};
+  const int nt16 = (T + 15) / 16;
+  const size_t lds_dkv = 2 * (size_t)nt16 * 16 * 128 + 2 * (size_t)nt16 * 16 * 4;
+  switch (nt16) {
+#define DKV_CASE(N_)                                                                                   \
+  case N_:                                                                                            \
+    allow_lds(DKV_SELF(N_), lds_dkv);                                                                 \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(DKV_SELF(N_)), nimg * H, 256, lds_dkv, stream, a);             \
+    break;
+    DKV_CASE(1) DKV_CASE(2) DKV_CASE(3) DKV_CASE(4) DKV_CASE(5) DKV_CASE(6) DKV_CASE(7) DKV_CASE(8)
+    DKV_CASE(9) DKV_CASE(10) DKV_CASE(11) DKV_CASE(12) DKV_CASE(13) DKV_CASE(14) DKV_CASE(15) DKV_CASE(16)
+#undef DKV_CASE
+    default: return ES_BAD_SHAPE;
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+#undef DKV_SELF
 
 // CLS-query attention of a block whose non-CLS outputs are unused (the ViT's last block): qkv
 // [nimg*T, ldqkv] -> o [nimg, ldo] (the CLS rows only, compact), lse [nimg*H].

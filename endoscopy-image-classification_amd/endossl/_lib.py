@@ -28,6 +28,8 @@ SIGNATURES = {
     "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
     "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
     "es_attn_bwd": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),
+    "es_attn_bwd_dq": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),
+    "es_attn_bwd_dkv": (I, [V, I, V, I, V, V, I, V, I, I, I, I, F, V]),
     "es_attn_cls_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
     "es_mlp_fwd_infer": (I, [V, I, V, V, V, V, V, I, V, I, I, I, I, V]),
     "es_pack_chunk32": (I, [V, V, I, I, V]),

@@ -253,6 +253,11 @@ class Engine:
     # two GEMMs -- one wave per SIMD (the fc2 accumulators and the register-resident h rows use
     # ~420 registers) leaves the LDS-fragment latency exposed (scripts/mlp_bench.py)
     FUSED_MLP = os.environ.get("ENDOSSL_FUSED_MLP", "0") == "1"
+    # attention backward as two independent launches, dQ on the caller's stream and dK/dV (with its
+    # own delta) on a third stream, joined before the qkv data gradient.  Off by default
+    # (ENDOSSL_ATTN_SPLIT=1): F1 35.00-35.10 vs 34.88-34.95 ms/step in one box -- the chip is already
+    # full with the weight gradients on the side stream
+    ATTN_SPLIT = os.environ.get("ENDOSSL_ATTN_SPLIT", "0") == "1"
 
     def __init__(self, cfg, device):
         self.cfg, self.device = cfg, device
@@ -352,6 +357,12 @@ class Engine:
         if lane not in self._ws_ln:
             self._ws_ln[lane] = torch.empty(2 * 1024 * self.cfg.dim, dtype=torch.float32, device=self.device)
         return self._ws_ln[lane]
+
+    def attn_stream(self):
+        """Third HIP stream: the dK/dV attention-backward pass beside the dQ pass (ATTN_SPLIT)."""
+        if getattr(self, "_attn_s", None) is None:
+            self._attn_s = torch.cuda.Stream(device=self.device)
+        return self._attn_s
 
     def side_stream(self):
         """The second HIP stream (weak forward beside the train forward; weight gradients beside
@@ -593,8 +604,18 @@ class Engine:
             call("es_gemm_nt", EPI_BF16, ptr(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
                  None, None, 0, M, D, D, 0, s)
             wgrad_side(Gi.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
-            call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
-                 ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
+            if ov and self.ATTN_SPLIT:
+                s3 = self.attn_stream()
+                s3.wait_stream(main)
+                with torch.cuda.stream(s3):
+                    call("es_attn_bwd_dkv", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.do), D,
+                         ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, _lib.stream())
+                call("es_attn_bwd_dq", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do),
+                     D, ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
+                main.wait_stream(s3)
+            else:
+                call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
+                     ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
             call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
             wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))

@@ -68,6 +68,13 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
 /* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass) */
 int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
                 int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
+/* es_attn_bwd as two independent launches (two streams): the dQ pass (writes delta) and the dK/dV
+ * pass computing its own delta = rowsum(dO * O); they write disjoint column ranges of dqkv */
+int es_attn_bwd_dq(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta,
+                   const void* dout, int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale,
+                   hipStream_t stream);
+int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
+                    void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
 /* CLS-query attention for a block whose non-CLS outputs are unused (the last block: only the CLS
  * token reaches timm's head, VisionTransformer.forward_features x[:, 0]).  o / dout are compact
  * [nimg, ld] CLS rows, lse [nimg*H]; the backward writes dqkv for every token (q part zero off the

@@ -230,6 +230,18 @@ def test_attention_bwd(n, T, H):
         err = (a - b).abs().max().item() / max(b.abs().max().item(), 1e-2)
         assert err < 3e-2, (part, err)
     assert torch.all(dqkv[n * T:] == 0)
+    # the two-launch form (dQ pass + dK/dV pass with its own delta) gives the same gradients up to the
+    # fp32 summation order of delta
+    dqkv2 = torch.zeros_like(qkv)
+    delta2 = torch.zeros(n * H * T, device=DEV)
+    call("es_attn_bwd_dkv", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(dout), D, ptr(dqkv2), 3 * D, n, T, H,
+         64 ** -0.5, S())
+    call("es_attn_bwd_dq", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta2), ptr(dout), D, ptr(dqkv2), 3 * D, n, T,
+         H, 64 ** -0.5, S())
+    torch.cuda.synchronize()
+    sc = max(dqkv.float().abs().max().item(), 1e-2)
+    assert (dqkv2.float() - dqkv.float()).abs().max().item() <= 1e-2 * sc
+    torch.testing.assert_close(delta2, delta, rtol=0, atol=0)
 
 
 @pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1)])
