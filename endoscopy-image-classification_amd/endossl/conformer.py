@@ -186,7 +186,7 @@ class _Map:
 
 def _tn_splits(M, N1, N2):
     tiles = (N1 // 128) * (N2 // 128)
-    return max(1, min((M + 31) // 32, 128, -(-768 // tiles)))  # Engine.TN_TARGET_BLOCKS
+    return max(1, min((M + 31) // 32, 128, 768 // tiles))  # Engine.TN_TARGET_BLOCKS (floor: see there)
 
 
 class _ConvFn(torch.autograd.Function):

@@ -212,11 +212,16 @@ class _Grads:
 class Engine:
     """Explicit forward / backward of the ViT over C-ABI kernels.  One per (model, device)."""
 
-    # split-K sizing of the weight-gradient GEMMs: ~3 workgroups per CU (scripts/gemm_bench.py
-    # --tn-blocks sweep 384..3072 on MI355X: 768 is fastest on fc1 / fc2 / qkv, 195-202 / 150 us vs
-    # 219-221 / 160 at 1536 -- fewer fp32 split-K slabs to write and reduce -- and 512 or fewer
-    # starve the chip); the split count is capped so the slabs stay small for the 384x384 projection
-    TN_TARGET_BLOCKS = 768
+    # split-K sizing of the weight-gradient GEMMs: floor(TN_TARGET_BLOCKS / tiles) splits, so the grid
+    # never exceeds the target (a ceil left 792 workgroups for 768, and 24 CUs holding one more).
+    # Alone, the whole-chip fill (1024 = 4 workgroups per CU, the kernel's register-limited residency)
+    # is fastest (scripts/gemm_bench.py: fc2 / fc1 / qkv 175 / 169 / 132 us vs 212 / 182 / 138 at
+    # floor 768); inside the F1 step, where the weight gradients share the CUs with the data-gradient
+    # chain on the other stream, 768 leaves the chain room: 35.10-35.13 ms/step vs 35.41-35.43 (1024),
+    # 35.39 (640), 35.99 (512); C1 prefers 1024 (73.9 vs 74.2 ms).  The split count is capped so the
+    # slabs stay small for the 384x384 projection.
+    TN_TARGET_BLOCKS = int(os.environ.get("ENDOSSL_TN_TARGET", "768"))
+    TN_CEIL = os.environ.get("ENDOSSL_TN_CEIL", "0") == "1"  # A/B knob: the earlier ceil sizing
     TN_MAX_SPLITS = 128
     # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
     # GEMMs beside the data-gradient chain ("bwd"); ENDOSSL_OVERLAP=0 serialises everything on the
@@ -483,7 +488,8 @@ class Engine:
     def _tn_splits(self, M, N1, N2):
         tiles = (N1 // 128) * (N2 // 128)
         msteps = (M + 31) // 32
-        return max(1, min(msteps, self.TN_MAX_SPLITS, -(-self.TN_TARGET_BLOCKS // tiles)))
+        sp = -(-self.TN_TARGET_BLOCKS // tiles) if self.TN_CEIL else self.TN_TARGET_BLOCKS // tiles
+        return max(1, min(msteps, self.TN_MAX_SPLITS, sp))
 
     def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0):
         """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy."""

@@ -90,8 +90,10 @@ def main():
         flops = 2.0 * M * N1 * N2
         tiles = (N1 // 128) * (N2 // 128)
         row = {}
-        for tb in [int(x) for x in args.tn_blocks.split(",")]:
-            splits = max(1, min((M + 31) // 32, -(-tb // tiles)))
+        for tbs in args.tn_blocks.split(","):  # "768": ceil(768 / tiles) splits; "f768": floor
+            tb = int(tbs.lstrip("f"))
+            sp = tb // tiles if tbs.startswith("f") else -(-tb // tiles)
+            splits = max(1, min((M + 31) // 32, sp))
             times = {v: [] for v in tn_variants}
             for _ in range(args.rounds):
                 for v in tn_variants:
@@ -108,7 +110,7 @@ def main():
             lib.es_set_tn_variant(-1)
             for v in tn_variants:
                 t = sorted(times[v])[len(times[v]) // 2]
-                row[f"tn{v}_b{tb}"] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}
+                row[f"tn{v}_b{tbs}"] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1), "splits": splits}
         results[name] = row
         print(name, json.dumps(row), flush=True)
     out_dir = os.path.join(ROOT, "gpurun_out")
