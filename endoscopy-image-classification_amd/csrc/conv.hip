@@ -891,7 +891,10 @@ __global__ __launch_bounds__(256) void fcu_down_fwd_kernel(const float* __restri
 // partial gamma / beta gradients partial[block][0..D) / [D..2D).  A wave owns a row at a time with
 // its D/64 columns per lane in registers (D <= 1024): the row's gelu'(z) and xhat are computed once,
 // and the gamma / beta partials stay in registers until one LDS reduction over the 4 waves at the end.
-constexpr int FCU_NJ = 16;
+constexpr int FCU_NJ = 16;  // D <= 1024
+// workgroups of the backward (2048 for large maps: up to 8 waves per SIMD at NJ = 6)
+inline int fcu_bwd_blocks(int rows) { return rows < 8192 ? (rows + 3) / 4 : 2048; }
+template <int NJ>  // 64-column slots per lane: D <= 64 NJ (the unused slots are predicated off)
 __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restrict__ dout, const float* __restrict__ pooled,
                                                            const float* __restrict__ gam, const float* __restrict__ bet,
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -900,9 +903,9 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
                                                            int rows_per_block) {
   extern __shared__ float pg[];  // [4 waves][2 * D]
   const int T = np + 1, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  float ga[FCU_NJ], be[FCU_NJ], pgw[FCU_NJ], pbw[FCU_NJ];
+  float ga[NJ], be[NJ], pgw[NJ], pbw[NJ];
 #pragma unroll
-  for (int j = 0; j < FCU_NJ; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int c = j * 64 + lane;
     ga[j] = c < D ? gam[c] : 0.f;
     be[j] = c < D ? bet[c] : 0.f;
@@ -913,25 +916,25 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
     const int n = row / T, tk = row - n * T;
     const float* dr = dout + (long)row * D;
     float* xr = dxt + (long)row * D;
-    float d[FCU_NJ];
+    float d[NJ];
 #pragma unroll
-    for (int j = 0; j < FCU_NJ; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int c = j * 64 + lane;
       d[j] = c < D ? dr[c] : 0.f;
     }
     if (tk == 0) {
 #pragma unroll
-      for (int j = 0; j < FCU_NJ; ++j)
+      for (int j = 0; j < NJ; ++j)
         if (j * 64 + lane < D) xr[j * 64 + lane] = 2.f * d[j];
       continue;
     }
     const long pi = (long)n * np + tk - 1;
     const float* pr = pooled + pi * D;
     const float mu = mean[pi], rs = rstd[pi];
-    float xh[FCU_NJ], gz[FCU_NJ];
+    float xh[NJ], gz[NJ];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int j = 0; j < FCU_NJ; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int c = j * 64 + lane;
       if (c < D) {
         xr[c] = d[j];
@@ -952,13 +955,13 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
     s2 = warp_sum(s2) / (float)D;
     float* dp = dpooled + pi * D;
 #pragma unroll
-    for (int j = 0; j < FCU_NJ; ++j) {
+    for (int j = 0; j < NJ; ++j) {
       const int c = j * 64 + lane;
       if (c < D) dp[c] = rs * (gz[j] * ga[j] - s1 - xh[j] * s2);
     }
   }
 #pragma unroll
-  for (int j = 0; j < FCU_NJ; ++j) {
+  for (int j = 0; j < NJ; ++j) {
     const int c = j * 64 + lane;
     if (c < D) {
       pg[wv * 2 * D + c] = pgw[j];
@@ -1316,9 +1319,7 @@ int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln
 }
 
 size_t es_fcu_down_workspace(int N, int np, int D) {
-  const int rows = N * (np + 1);
-  const int blocks = rows < 4096 ? (rows + 3) / 4 : 1024;
-  return (size_t)blocks * 2 * D;
+  return (size_t)fcu_bwd_blocks(N * (np + 1)) * 2 * D;
 }
 
 // backward: dxt [N, np+1, D] (overwritten), dpooled [N, np, D] (overwritten), ln_w / ln_b grads (+)=
@@ -1329,11 +1330,20 @@ int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* 
     return ES_BAD_ARG;
   if (N <= 0 || np <= 0 || D <= 0 || D > 64 * FCU_NJ) return ES_BAD_SHAPE;
   const int rows = N * (np + 1);
-  const int blocks = rows < 4096 ? (rows + 3) / 4 : 1024;
+  const int blocks = fcu_bwd_blocks(rows);
   const int per = (rows + blocks - 1) / blocks;
   const size_t lds = (size_t)4 * 2 * D * 4;
-  hipLaunchKernelGGL(fcu_down_bwd_kernel, blocks, 256, lds, stream, dout, pooled, ln_w, ln_b, mean, rstd, dxt, dpooled,
-                     workspace, N, np, D, per);
+  const int nj = (D + 63) / 64;
+#define FCU_BWD(NJ_)                                                                                           \
+  hipLaunchKernelGGL(fcu_down_bwd_kernel<NJ_>, blocks, 256, lds, stream, dout, pooled, ln_w, ln_b, mean, rstd, dxt, \
+                     dpooled, workspace, N, np, D, per)
+  if (nj <= 2) FCU_BWD(2);
+  else if (nj <= 4) FCU_BWD(4);
+  else if (nj <= 6) FCU_BWD(6);
+  else if (nj <= 8) FCU_BWD(8);
+  else if (nj <= 12) FCU_BWD(12);
+  else FCU_BWD(16);
+#undef FCU_BWD
   // partial[b][0..D) = dgamma, [D..2D) = dbeta
   ChanFin f{dln_w, dln_b, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, 0, D, accumulate};
   hipLaunchKernelGGL(chan_final_kernel<3>, (2 * D + 15) / 16, 256, 0, stream, workspace, blocks, 2 * D, f);
