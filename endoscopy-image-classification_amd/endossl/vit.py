@@ -172,6 +172,7 @@ class _Acts:
         # the last block on its CLS rows only (Engine.PRUNE_LAST): compact [n, .] images, rows padded to 256
         Mc = _rup(n, 256)
         self.c_o, self.c_lse = z(Mc, D, dt=b16), z(n * cfg.heads)
+        self.c_h1 = z(Mc, D, dt=b16)  # LN1 output of the CLS rows (the last block's Q projection input)
         self.c_xmid, self.c_h2 = z(Mc, D), z(Mc, D, dt=b16)
         self.c_mean2, self.c_rstd2 = z(Mc), z(Mc)
         self.c_pre = z(Mc, Hd, dt=b16) if train else None
@@ -252,6 +253,9 @@ class Engine:
     # only; in the backward d(loss)/d(non-CLS rows) of the last block's output is exactly zero, so the
     # skipped rows contribute exactly nothing to any gradient.  ENDOSSL_PRUNE_LAST=0 runs every row.
     PRUNE_LAST = os.environ.get("ENDOSSL_PRUNE_LAST", "1") == "1"
+    # ... and its Q projection (forward) and Q weight gradient on the CLS rows only (ENDOSSL_PRUNE_Q=0:
+    # all rows, with a dQ that is zero off the CLS rows)
+    PRUNE_Q = os.environ.get("ENDOSSL_PRUNE_Q", "1") == "1"
     # inference rows (the weak forward): fc1 -> GELU -> fc2 + residual in one kernel
     # (es_mlp_fwd_infer), the [tokens, 4D] activation never written to HBM.  Off by default
     # (ENDOSSL_FUSED_MLP=1 turns it on): at the F1 weak shape it takes 0.43 ms vs 0.375 ms for the
@@ -417,8 +421,18 @@ class Engine:
             call("es_layernorm_fwd", ptr(xin), D, ptr(self.view(flat, b + "norm1.weight")),
                  ptr(self.view(flat, b + "norm1.bias")), ptr(h1), D, ptr(A.mean1[li]), ptr(A.rstd1[li]), M, D,
                  cfg.eps, s)
-            call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(self.wb[b + "attn.qkv.weight"]), D,
-                 ptr(self.view(flat, b + "attn.qkv.bias")), ptr(A.qkv[li]), 3 * D, None, None, 0, M, 3 * D, D, 0, s)
+            if prune and self.PRUNE_Q and i == cfg.depth - 1:
+                # K and V for every token; Q for the CLS rows only, written to their rows of qkv
+                wq, bq = self.wb[b + "attn.qkv.weight"], self.view(flat, b + "attn.qkv.bias")
+                call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(wq[D:]), D, ptr(bq[D:]), ptr(A.qkv[li][:, D:]), 3 * D,
+                     None, None, 0, M, 2 * D, D, 0, s)
+                A.c_h1[:n].copy_(h1[:M].view(n, T, D)[:, 0])
+                call("es_gemm_nt", EPI_BF16, ptr(A.c_h1), D, ptr(wq[:D]), D, ptr(bq[:D]), ptr(A.qkv[li]), T * 3 * D,
+                     None, None, 0, n, D, D, 0, s)
+            else:
+                call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(self.wb[b + "attn.qkv.weight"]), D,
+                     ptr(self.view(flat, b + "attn.qkv.bias")), ptr(A.qkv[li]), 3 * D, None, None, 0, M, 3 * D, D, 0,
+                     s)
             if prune and i == cfg.depth - 1:
                 self._last_block_cls_fwd(flat, A, b, li, xin, n, train, s)
                 break
@@ -491,14 +505,15 @@ class Engine:
         sp = -(-self.TN_TARGET_BLOCKS // tiles) if self.TN_CEIL else self.TN_TARGET_BLOCKS // tiles
         return max(1, min(msteps, self.TN_MAX_SPLITS, sp))
 
-    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0):
-        """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy."""
+    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0, ld1=None, ld2=None):
+        """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy (row strides ld1 / ld2,
+        default N1 / N2)."""
         ws = self.workspace(lane)
         splits = self._tn_splits(M, N1, N2)
         if _lib.load().es_gemm_tn_workspace(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
-        call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
-             _lib.stream())
+        call("es_gemm_tn", ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0,
+             ptr(bias_out), _lib.stream())
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None):
         D = self.cfg.dim
@@ -533,14 +548,14 @@ class Engine:
         main = torch.cuda.current_stream(self.device)
         side = self.side_stream() if ov else None
 
-        def wgrad_side(*args):
+        def wgrad_side(*args, **kw):
             """Weight-gradient GEMM on the side stream once the main stream has produced dY."""
             if not ov:
-                self._wgrad(*args)
+                self._wgrad(*args, **kw)
                 return
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                self._wgrad(*args)
+                self._wgrad(*args, **kw)
 
         done = {}
         if zero_grad:
@@ -591,7 +606,14 @@ class Engine:
                      ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
                 call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                      ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
-                wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
+                gw, gb = gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias")
+                if self.PRUNE_Q and n % 32 == 0:
+                    # K / V weight gradients over every token; the Q part over the CLS rows, the only
+                    # rows with a nonzero dQ (strided views: rows img*T of dqkv and h1)
+                    wgrad_side(Gi.dqkv[:, D:], 2 * D, A.h1[i], D, M, gw[D * D:], gb[D:], ld1=3 * D)
+                    wgrad_side(Gi.dqkv, D, A.h1[i], D, n, gw[:D * D], gb[:D], ld1=T * 3 * D, ld2=T * D)
+                else:
+                    wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gw, gb)
                 if ov:
                     done[i] = side.record_event()
                 self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), Gi.dxm_cls, G.dx, Gn.dxb,

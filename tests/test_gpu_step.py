@@ -306,8 +306,8 @@ def test_two_lane_backward_matches_single_lane():
     assert worst <= 1e-5, worst
 
 
-@pytest.mark.parametrize("head", ["cls", "emb"])
-def test_last_block_cls_rows_match_full_rows(head):
+@pytest.mark.parametrize("head,nimg", [("cls", 40), ("emb", 40), ("cls", 64), ("emb", 64)])
+def test_last_block_cls_rows_match_full_rows(head, nimg):
     """Engine.PRUNE_LAST (the last block's attention for the CLS queries only, its projection / LN2 /
     MLP on the CLS rows only) gives the logits / CLS features and every parameter gradient of the
     full-row last block: the skipped rows feed nothing downstream, their gradient is exactly zero.
@@ -320,7 +320,7 @@ def test_last_block_cls_rows_match_full_rows(head):
     eng = m.engine()
     eng.pack(m.flat, m.version)
     g = torch.Generator(device=DEV).manual_seed(4)
-    x = torch.randn(40, 3, 64, 64, device=DEV, generator=g)
+    x = torch.randn(nimg, 3, 64, 64, device=DEV, generator=g)  # 64: the CLS-row Q weight gradient (n % 32 == 0)
     outs, grads = {}, {}
     for prune in (False, True):
         eng.PRUNE_LAST = prune
@@ -343,7 +343,7 @@ def test_last_block_cls_rows_match_full_rows(head):
         assert torch.isfinite(a).all()
         if b.abs().max() > 0:
             worst = max(worst, _rel(a, b))
-    _record(f"last_block_cls_rows_{head}", worst_rel_l2=worst, out_rel=_rel(outs[True][0], outs[False][0]))
+    _record(f"last_block_cls_rows_{head}_{nimg}", worst_rel_l2=worst, out_rel=_rel(outs[True][0], outs[False][0]))
     assert worst <= 1e-2, worst
 
 
