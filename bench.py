@@ -46,12 +46,16 @@ STEP_TFLOP_F1 = 18.247  # fwd 960 imgs + bwd 512 imgs, 9.197 G
 
 
 def vit_s_pruned_tflop(n_fwd, n_bwd):
-    """FLOPs the last block does NOT execute with Engine.PRUNE_LAST (ViT-S/16 at 224^2): for the 196
-    non-CLS tokens of each image, projection + fc1 + fc2 (2*D*(D + 2*Hd)) and their attention
-    queries (4*T*64*H); forward over n_fwd images, backward (2x) over n_bwd."""
+    """FLOPs the last block does NOT execute with Engine.PRUNE_LAST / PRUNE_Q (ViT-S/16 at 224^2):
+    for the 196 non-CLS tokens of each image, projection + fc1 + fc2 (2*D*(D + 2*Hd)) and their
+    attention queries (4*T*64*H) -- forward over n_fwd images, backward (2x) over n_bwd -- and the Q
+    projection (2*D*D): forward over n_fwd, its weight gradient (1x; the data gradient still runs)
+    over n_bwd."""
+    from endossl.vit import Engine
     D, Hd, T, H = 384, 1536, 197, 6
     per_img = (T - 1) * (2 * D * (D + 2 * Hd) + 4 * T * 64 * H)
-    return per_img * (n_fwd + 2 * n_bwd) / 1e12
+    q = (T - 1) * 2 * D * D
+    return (per_img * (n_fwd + 2 * n_bwd) + (q * (n_fwd + n_bwd) if Engine.PRUNE_Q else 0)) / 1e12
 
 
 def synth_u8(n, size, gen, device):
