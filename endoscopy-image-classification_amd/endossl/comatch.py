@@ -151,8 +151,9 @@ class CoMatch(FixMatch):
         torch.add(stats[0], stats[1], alpha=lam_u, out=stats[4])
         stats[4].add_(stats[2], alpha=lam_c)
 
-        m.backward_from(dl, dz)
-        gscale = dist.allreduce_sum_(m.flat_grad)
+        gb = dist.GradBuckets(m.flat_grad) if world > 1 and self.overlap_allreduce else None
+        m.backward_from(dl, dz, grad_ready=gb.ready if gb is not None else None)
+        gscale = gb.finish() if gb is not None else dist.allreduce_sum_(m.flat_grad)
         ema = self.ema_model
         self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,
                             ema_decay=float(ema.decay) if ema is not None else 0.0, grad_scale=gscale)

@@ -194,9 +194,9 @@ class NativeViTEmb(NativeViT):
         logits, z = self.heads().forward(lambda nm: eng.view(self.flat, nm), self.bn_buffers(), fts, keep, train)
         return logits, fts, z
 
-    def backward_from(self, dlogits, dz, dfts_extra=None):
+    def backward_from(self, dlogits, dz, dfts_extra=None, grad_ready=None):
         """Gradient of the last train forward: dlogits [n, C], dz [n, L] (and optionally a direct
-        dL/dfts) -> flat grad (returned)."""
+        dL/dfts) -> flat grad (returned).  grad_ready: Engine.backward's per-block hook."""
         eng = self.engine()
         g = self.flat_grad
         g.zero_()
@@ -205,7 +205,7 @@ class NativeViTEmb(NativeViT):
                                      self._last_keep, dlogits, dz)
         if dfts_extra is not None:
             dfts.add_(dfts_extra)
-        return eng.backward(self.flat, g, dfts=dfts, zero_grad=False)
+        return eng.backward(self.flat, g, dfts=dfts, zero_grad=False, grad_ready=grad_ready)
 
     def forward(self, x):
         if torch.is_grad_enabled() and self.training and any(p.requires_grad for p in self.parameters()):

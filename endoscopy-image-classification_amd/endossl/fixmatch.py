@@ -13,7 +13,9 @@ benchmark times.  One step (code/fixmatch.py:91-131):
          lu, mask = consistency(logits_w, logits[B:], tau)  fused kernel  (:116)
          losses = lx + LAMBDA_U * lu                                      (:118)
   bwd    flat grads <- explicit backward of d(losses)/d(logits)            (:122)
-  comm   RCCL all-reduce of the flat grad (data-parallel only)
+  comm   RCCL all-reduce of the flat grad (data-parallel only), one bucket per transformer block
+         issued as soon as that block's gradients are final, beside the rest of the reverse pass
+         (dist.GradBuckets; ENDOSSL_OVERLAP_AR=0 for one all-reduce after the backward)
   opt    Adam + EMA in one sweep, then lr_scheduler.step_update           (:123-127)
 
 No `.item()` per step: losses stay on device and the AverageMeter is filled once per epoch.
@@ -38,6 +40,9 @@ def _next(it):
 
 
 class FixMatch:
+    # bucketed all-reduce overlapped with the backward (world > 1)
+    overlap_allreduce = os.environ.get("ENDOSSL_OVERLAP_AR", "1") != "0"
+
     def __init__(self, model, opt_func="Adam", lr=1e-3, device='cpu'):
         self.model = model
         self.opt_func = opt_func
@@ -113,8 +118,9 @@ class FixMatch:
         call("es_fm_consistency_fwd_bwd", ptr(logits_w), C, ptr(logits[B:]), C, nu, C, float(cfg.TRAIN.THRES),
              lam / nu, ptr(self._pl), ptr(self._mask), None, ptr(dl[B:]), C, ptr(stats[1:3]), s)
         torch.add(stats[0], stats[1], alpha=lam, out=stats[3])
-        eng.backward(m.flat, m.flat_grad, dl)
-        gscale = dist.allreduce_sum_(m.flat_grad)
+        gb = dist.GradBuckets(m.flat_grad) if dist.world_size() > 1 and self.overlap_allreduce else None
+        eng.backward(m.flat, m.flat_grad, dl, grad_ready=gb.ready if gb is not None else None)
+        gscale = gb.finish() if gb is not None else dist.allreduce_sum_(m.flat_grad)
         ema = self.ema_model
         self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,
                             ema_decay=float(ema.decay) if ema is not None else 0.0, grad_scale=gscale)

@@ -522,11 +522,14 @@ class Engine:
         call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
-    def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True):
+    def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True, grad_ready=None):
         """dlogits fp32 [n, C] (head "cls") or dfts fp32 [n, D] (head "emb") for the last train
         forward -> grad (flat fp32).  zero_grad=False when the caller already zeroed `grad` and
         wrote the head gradients into it (the trunk's entries are overwritten either way; the
-        final-norm grads are accumulated)."""
+        final-norm grads are accumulated).  grad_ready(lo, hi, events): called once per block as
+        soon as grad[lo:hi] (that block's contiguous parameters) is final -- after the HIP events
+        in `events` -- so the caller can start its all-reduce beside the rest of the reverse pass
+        (dist.GradBuckets); ranges never handed over are the caller's to finish."""
         cfg = self.cfg
         s = _lib.stream()
         EPI_DH = EPI_BF16 if self.DH_BF16 else EPI_F32  # noqa: N806
@@ -558,6 +561,15 @@ class Engine:
                 self._wgrad(*args, **kw)
 
         done = {}
+
+        def block_done(i):
+            if grad_ready is None:
+                return
+            lo = self.offs[f"blocks.{i}.norm1.weight"]
+            hi = self.offs[f"blocks.{i + 1}.norm1.weight" if i + 1 < cfg.depth else "norm.weight"]
+            evs = [main.record_event()] + ([done[i]] if i in done else [])
+            grad_ready(lo, hi, evs)
+
         if zero_grad:
             grad.zero_()
         prune = self._prune()
@@ -618,6 +630,7 @@ class Engine:
                     done[i] = side.record_event()
                 self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), Gi.dxm_cls, G.dx, Gn.dxb,
                              gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
+                block_done(i)
                 continue
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
             call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.dxb), D,
@@ -653,6 +666,7 @@ class Engine:
                     main.wait_event(done.pop(i + 1))
             self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), G.dxm, G.dx, Gn.dxb,
                          gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
+            block_done(i)
         # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
         K0 = 3 * cfg.patch * cfg.patch
         call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,

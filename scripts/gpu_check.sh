@@ -16,6 +16,7 @@ run k 600 $PT tests/test_gpu_kernels.py; rc=$?
 ok $rc && { run s 600 $PT tests/test_gpu_step.py; rc=$?; }
 ok $rc && { run c 600 $PT tests/test_gpu_comatch.py; rc=$?; }
 ok $rc && { run cf 600 $PT tests/test_gpu_conformer.py; rc=$?; }
+ok $rc && { run dist 300 $PT tests/test_gpu_dist.py; rc=$?; }
 ok $rc && { run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; }
 ok $rc && { run bench 600 python bench.py --steps 10 --warmup 3; rc=$?; }
 if ok $rc && [ "${PROFILE:-1}" = 1 ]; then
