@@ -107,28 +107,38 @@ __global__ __launch_bounds__(256) void dense_dx_kernel(const float* __restrict__
   }
 }
 
-// dW[c][k] = sum_i dpre[i][c] X[i][k] (column c per blockIdx.y, k over threads); db[c] = sum_i dpre[i][c]
+// dW[c][k] = sum_i dpre[i][c] X[i][k] (column c per blockIdx.y, k over threads); db[c] = sum_i dpre[i][c],
+// summed in row order beside the dW loop (which loads dpre[i][c] anyway) and written by thread 0 of
+// the first x-block: one serial pass of dependent loads after the loop took ~200 us at n = 960.
 __global__ __launch_bounds__(256) void dense_dw_kernel(const float* __restrict__ dpre, const float* __restrict__ X,
                                                        int ldx, float* __restrict__ dW, float* __restrict__ db, int n,
                                                        int K, int N) {
   const int c = blockIdx.y;
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < K) {
-    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  const bool want_db = db && blockIdx.x == 0 && threadIdx.x == 0;
+  if (k < K || want_db) {
+    const int kk = k < K ? k : 0;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, sb = 0.f;
     int i = 0;
     for (; i + 4 <= n; i += 4) {
-      a0 = fmaf(dpre[(size_t)i * N + c], X[(size_t)i * ldx + k], a0);
-      a1 = fmaf(dpre[(size_t)(i + 1) * N + c], X[(size_t)(i + 1) * ldx + k], a1);
-      a2 = fmaf(dpre[(size_t)(i + 2) * N + c], X[(size_t)(i + 2) * ldx + k], a2);
-      a3 = fmaf(dpre[(size_t)(i + 3) * N + c], X[(size_t)(i + 3) * ldx + k], a3);
+      const float d0 = dpre[(size_t)i * N + c], d1 = dpre[(size_t)(i + 1) * N + c];
+      const float d2 = dpre[(size_t)(i + 2) * N + c], d3 = dpre[(size_t)(i + 3) * N + c];
+      a0 = fmaf(d0, X[(size_t)i * ldx + kk], a0);
+      a1 = fmaf(d1, X[(size_t)(i + 1) * ldx + kk], a1);
+      a2 = fmaf(d2, X[(size_t)(i + 2) * ldx + kk], a2);
+      a3 = fmaf(d3, X[(size_t)(i + 3) * ldx + kk], a3);
+      sb += d0;
+      sb += d1;
+      sb += d2;
+      sb += d3;
     }
-    for (; i < n; ++i) a0 = fmaf(dpre[(size_t)i * N + c], X[(size_t)i * ldx + k], a0);
-    dW[(size_t)c * K + k] = (a0 + a1) + (a2 + a3);
-  }
-  if (db && blockIdx.x == 0 && threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < n; ++i) s += dpre[(size_t)i * N + c];
-    db[c] = s;
+    for (; i < n; ++i) {
+      const float d = dpre[(size_t)i * N + c];
+      a0 = fmaf(d, X[(size_t)i * ldx + kk], a0);
+      sb += d;
+    }
+    if (k < K) dW[(size_t)c * K + k] = (a0 + a1) + (a2 + a3);
+    if (want_db) db[c] = sb;
   }
 }
 

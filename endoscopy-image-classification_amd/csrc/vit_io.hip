@@ -72,7 +72,8 @@ __global__ void cls_init_kernel(float* __restrict__ x, int ldx, const float* __r
 }
 
 // dx fp32 [n*T, D] -> dpatch bf16 [n*(T-1), D]; dpos[t][d] (+)= sum_img dx; dcls[d] (+)= dpos[0][d].
-// Block = 64 features x 4 image groups; the 4 partial sums meet in LDS.
+// Block = 64 features x 4 image groups; the 4 partial sums meet in LDS.  The image loop is unrolled
+// so 8 loads per thread are in flight ahead of the in-order adds.
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict__ dx, int lddx,
                                                         bf16* __restrict__ dpatch, int ldp, float* __restrict__ dpos,
                                                         float* __restrict__ dcls, int n, int T, int D, int accumulate) {
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
     t = id / D;
     d = id % D;
     int im = ig;
+#pragma unroll 4
     for (; im + 4 < n; im += 8) {
       const float v0 = dx[((size_t)im * T + t) * lddx + d];
       const float v1 = dx[((size_t)(im + 4) * T + t) * lddx + d];
