@@ -675,6 +675,8 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restr
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += gridDim.x * blockDim.x) {
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
     int k = 0;
+    // unrolled: 16 slab loads in flight ahead of the four in-order accumulation chains (same sums)
+#pragma unroll 4
     for (; k + 4 <= S; k += 4) {
       s0 += ((const f32x4*)(P + (size_t)k * n))[i];
       s1 += ((const f32x4*)(P + (size_t)(k + 1) * n))[i];
@@ -738,6 +740,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int g = rg;
+#pragma unroll 4
     for (; g + 3 * RG < G; g += 4 * RG) {
       s0 += P[(size_t)g * N + col];
       s1 += P[(size_t)(g + RG) * N + col];
