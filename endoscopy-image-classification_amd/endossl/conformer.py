@@ -21,6 +21,7 @@ MI355X-first layout:
 """
 import ctypes
 import math
+import os
 from copy import deepcopy
 
 import torch
@@ -158,6 +159,46 @@ def _s():
     return _lib.stream()
 
 
+# Conv weight / bias gradients on a side HIP stream beside the data-gradient chain (the S1 backward
+# is otherwise one serial stream of mostly small, latency-bound launches).  Their inputs are
+# record_stream'ed so the caching allocator keeps them until the side stream is done.  The first
+# such launch of a backward pass queues an autograd final callback that makes the backward's stream
+# wait for the side stream, so whatever runs after `backward()` returns (the all-reduce, the
+# optimizer, a test reading .grad) sees complete gradients.
+CONV_DW_SIDE = os.environ.get("ENDOSSL_CONV_DW_SIDE", "1") != "0"
+_wgrad_streams = {}
+_join_queued = set()
+
+
+def _queue_join(main, side):
+    key = (main.device, main.cuda_stream)
+    if key in _join_queued:
+        return
+    _join_queued.add(key)
+
+    def _join():
+        main.wait_stream(side)
+        _join_queued.discard(key)
+    torch.autograd.Variable._execution_engine.queue_callback(_join)
+
+
+def _wgrad_stream(device):
+    st = _wgrad_streams.get(device)
+    if st is None:
+        st = _wgrad_streams[device] = torch.cuda.Stream(device=device)
+    return st
+
+
+def join_wgrad_stream(device=None):
+    """Make the current stream wait for the side-stream weight gradients (no-op if none ran)."""
+    if not torch.cuda.is_available():
+        return
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    st = _wgrad_streams.get(dev)
+    if st is not None:
+        torch.cuda.current_stream(dev).wait_stream(st)
+
+
 def _zero_pad(t, rows):
     """Zero rows [rows, len) of a token-row buffer (the GEMM pad rows) and return it."""
     if t.shape[0] > rows:
@@ -216,12 +257,20 @@ class _ConvFn(torch.autograd.Function):
         lib = _lib.load()
         tiles = lib.es_conv2d_dw_tiles(Cout, xm.C, k, k)
         splits = max(1, min(-(-M // 64), -(-2048 // tiles)))
-        ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits), device=dy.device)
-        call("es_conv2d_bwd_weight", xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy), Ho * Wo * Cout,
-             Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0, _s())
-        if bname:
-            wsb = torch.empty(lib.es_chan_workspace(M, Cout), device=dy.device)
-            call("es_chan_sum", ptr(dy), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(m.gview(bname)), 0, _s())
+        side = _wgrad_stream(dy.device) if CONV_DW_SIDE and dy.is_cuda else None
+        if side is not None:
+            main = torch.cuda.current_stream(dy.device)
+            side.wait_stream(main)
+            _queue_join(main, side)
+            x.record_stream(side)
+            dy.record_stream(side)
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits), device=dy.device)
+            call("es_conv2d_bwd_weight", xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy),
+                 Ho * Wo * Cout, Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0, _s())
+            if bname:
+                wsb = torch.empty(lib.es_chan_workspace(M, Cout), device=dy.device)
+                call("es_chan_sum", ptr(dy), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(m.gview(bname)), 0, _s())
         dx = None
         if ctx.needs_input_grad[0]:
             full = xm.off == 0 and xm.sc == 1 and xm.sn * xm.N == x.numel()
@@ -229,6 +278,14 @@ class _ConvFn(torch.autograd.Function):
             call("es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout, ptr(m.pview(wname)), xm.N, xm.H,
                  xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, 0, _s())
         return dx, None, None, None, None, None, None, None, None, None
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *a):
+        return False
 
 
 def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None):

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib, dist
+from .conformer import join_wgrad_stream
 from ._lib import call, ptr
 from .ema import ModelEMA
 from .fixmatch import _next
@@ -70,6 +71,7 @@ class SemiFormer:
     def _finish(self, out_conv, out_trans, dconv, dtrans):
         self.optimizer.zero_grad()
         torch.autograd.backward([out_conv, out_trans], [dconv, dtrans])
+        join_wgrad_stream(self.model.flat.device)  # (the backward's final callback already did)
         gscale = dist.allreduce_sum_(self.model.flat_grad)
         ema = self.ema_model
         self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,

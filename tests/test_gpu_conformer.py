@@ -467,3 +467,38 @@ def test_semiformer_trainer_vs_reference_train_one(golden):
     rec["max_param_delta"] = worst
     print(json.dumps(rec))
     assert worst <= 2e-3 * steps + 1e-5
+
+
+def test_conv_weight_grads_on_side_stream_match_serial(golden):
+    """conformer.CONV_DW_SIDE: the conv weight / bias gradients run on a side HIP stream beside the
+    data-gradient chain and are joined by an autograd final callback.  Same kernels on the same
+    inputs, so every conv gradient is bit-identical to the single-stream backward, and the rest of
+    the flat gradient agrees within fp32 summation order (head atomics)."""
+    from endossl import conformer as cf
+    d = golden("semiformer_step.npz")
+    m, _ = _model_from_fixture(d)
+    x = torch.cat([torch.tensor(d[k]) for k in ("x0", "uw0", "us0")]).to(DEV)
+    g = torch.Generator().manual_seed(7)
+    m.train()
+    grads, w = {}, None
+    saved = cf.CONV_DW_SIDE
+    try:
+        for side in (False, True):
+            cf.CONV_DW_SIDE = side
+            m.flat_grad.zero_()
+            hc, ht = m(x)
+            if w is None:  # one fixed linear functional of both heads for both passes
+                w = (torch.randn(hc.shape, generator=g).to(DEV), torch.randn(ht.shape, generator=g).to(DEV))
+            (hc * w[0]).sum().add((ht * w[1]).sum()).backward()
+            # read right after backward() returns, on the caller's stream: no explicit synchronize
+            grads[side] = m.flat_grad.clone()
+    finally:
+        cf.CONV_DW_SIDE = saved
+    conv_names = [n for n, _, k in m.layout if k == "p" and (".conv" in n or n.startswith("conv") or "conv_project" in n
+                                                             or "residual_conv" in n or "trans_patch_conv" in n)]
+    assert len(conv_names) > 20
+    for n in conv_names:
+        o, sh = m.offs[n], m.shapes[n]
+        cnt = int(torch.tensor(sh).prod().item()) if len(sh) else 1
+        assert torch.equal(grads[True][o:o + cnt], grads[False][o:o + cnt]), n
+    torch.testing.assert_close(grads[True], grads[False], rtol=1e-5, atol=1e-6)
