@@ -521,9 +521,18 @@ class _BlockFn(torch.autograd.Function):
         s = _s()
         dev = xt.device
         b16 = torch.bfloat16
-        # layer-internal scratch, reused by every block's backward (they run one after another on the
-        # stream): allocated zeroed once, so the pad rows the weight-gradient GEMMs read stay zero
-        z = lambda name, *sh, dt=torch.float32: m.bwd_scratch(name, sh, dt)  # noqa: E731
+        # layer-internal scratch, reused by every other block's backward: allocated zeroed once, so the
+        # pad rows the weight-gradient GEMMs read stay zero.  Two sets alternate by block, because the
+        # weight gradients (side stream, CONV_DW_SIDE) of the block before may still be reading its set;
+        # this block waits for the side-stream event of the last block that used its set.
+        side = _wgrad_stream(dev) if CONV_DW_SIDE and xt.is_cuda else None
+        main = torch.cuda.current_stream(dev) if xt.is_cuda else None
+        k = m._blk_set = getattr(m, "_blk_set", 0) ^ 1
+        z = lambda name, *sh, dt=torch.float32: m.bwd_scratch(f"{name}/{k}", sh, dt)  # noqa: E731
+        if not hasattr(m, "_blk_events"):
+            m._blk_events = {}
+        if side is not None and k in m._blk_events:
+            main.wait_event(m._blk_events.pop(k))
         lib = _lib.load()
         dout = dout.contiguous()
         dxb = z("dxb", Mp, D, dt=b16)
@@ -533,8 +542,12 @@ class _BlockFn(torch.autograd.Function):
 
         def wgrad(dy, N1, x, N2, wname, bname):
             sp = _tn_splits(M, N1, N2)
-            ws = torch.empty(lib.es_gemm_tn_workspace(N1, N2, sp), device=dev)
-            call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, sp, ptr(ws), ptr(gv(wname)), 0, ptr(gv(bname)), s)
+            if side is not None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                ws = torch.empty(lib.es_gemm_tn_workspace(N1, N2, sp), device=dev)
+                call("es_gemm_tn", ptr(dy), N1, ptr(x), N2, M, N1, N2, sp, ptr(ws), ptr(gv(wname)), 0,
+                     ptr(gv(bname)), _s())
 
         dpre = z("dpre", Mp, Hd, dt=b16)
         call("es_gemm_nt", EPI_DGELU, ptr(dxb), D, ptr(wt[pre + "mlp.fc2.weight"]), D, None, ptr(dpre), Hd, None,
@@ -564,6 +577,11 @@ class _BlockFn(torch.autograd.Function):
         call("es_layernorm_bwd_b16", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
+        if side is not None:
+            for t in (act, h2, o, h1):  # saved activations the side stream still reads
+                t.record_stream(side)
+            m._blk_events[k] = side.record_event()
+            _queue_join(main, side)
         return dx, None, None
 
 

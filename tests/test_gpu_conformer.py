@@ -470,10 +470,11 @@ def test_semiformer_trainer_vs_reference_train_one(golden):
 
 
 def test_conv_weight_grads_on_side_stream_match_serial(golden):
-    """conformer.CONV_DW_SIDE: the conv weight / bias gradients run on a side HIP stream beside the
-    data-gradient chain and are joined by an autograd final callback.  Same kernels on the same
-    inputs, so every conv gradient is bit-identical to the single-stream backward, and the rest of
-    the flat gradient agrees within fp32 summation order (head atomics)."""
+    """conformer.CONV_DW_SIDE: the conv and transformer-block weight / bias gradients run on a side
+    HIP stream beside the data-gradient chain (block scratch double-buffered, event-ordered) and are
+    joined by an autograd final callback.  Same kernels on the same inputs, so every conv / Linear
+    gradient is bit-identical to the single-stream backward, and the rest of the flat gradient
+    agrees within fp32 summation order (head atomics)."""
     from endossl import conformer as cf
     d = golden("semiformer_step.npz")
     m, _ = _model_from_fixture(d)
@@ -496,8 +497,9 @@ def test_conv_weight_grads_on_side_stream_match_serial(golden):
         cf.CONV_DW_SIDE = saved
     conv_names = [n for n, _, k in m.layout if k == "p" and (".conv" in n or n.startswith("conv") or "conv_project" in n
                                                              or "residual_conv" in n or "trans_patch_conv" in n)]
-    assert len(conv_names) > 20
-    for n in conv_names:
+    lin_names = [n for n, _, k in m.layout if k == "p" and (".attn." in n or ".mlp." in n)]
+    assert len(conv_names) > 20 and len(lin_names) > 20
+    for n in conv_names + lin_names:
         o, sh = m.offs[n], m.shapes[n]
         cnt = int(torch.tensor(sh).prod().item()) if len(sh) else 1
         assert torch.equal(grads[True][o:o + cnt], grads[False][o:o + cnt]), n
