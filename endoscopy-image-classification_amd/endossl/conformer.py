@@ -182,6 +182,29 @@ def _queue_join(main, side):
     torch.autograd.Variable._execution_engine.queue_callback(_join)
 
 
+# The CNN branch and the transformer branch of each ConvTransBlock run on two HIP streams (forward;
+# autograd then runs each node's backward on its forward stream, so the backward overlaps too):
+# after the cnn_block's conv2 / bn2 produce x2, FCUDown -> transformer block -> FCUUp run on the
+# branch stream while the cnn_block's conv3 / residual / bn3 tail runs on the caller's stream; the
+# fusion block joins them (code/models/conformer.py:334-357 data flow, unchanged arithmetic).
+BRANCH_STREAMS = os.environ.get("ENDOSSL_BRANCH_STREAMS", "1") != "0"
+_branch_streams = {}
+
+
+def _branch_stream(device):
+    st = _branch_streams.get(device)
+    if st is None:
+        st = _branch_streams[device] = torch.cuda.Stream(device=device)
+    return st
+
+
+def _own(t):
+    """Mark a tensor handed across streams (an autograd gradient, a branch output) as used by the
+    current stream, so the caching allocator does not recycle it before this stream's kernels ran."""
+    if t is not None and t.is_cuda:
+        t.record_stream(torch.cuda.current_stream(t.device))
+
+
 def _wgrad_stream(device):
     st = _wgrad_streams.get(device)
     if st is None:
@@ -247,6 +270,7 @@ class _ConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _own(dy)
         (x,) = ctx.saved_tensors
         m, xm = ctx.m, ctx.xmap
         wname, bname, Cout, k, s, p, Ho, Wo = ctx.spec
@@ -317,6 +341,7 @@ class _BNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _own(dy)
         x, y, mean, rstd = ctx.saved_tensors
         m, pre = ctx.m, ctx.pre
         N, H, W, C = x.shape
@@ -350,6 +375,7 @@ class _MaxPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _own(dy)
         (arg,) = ctx.saved_tensors
         N, H, W, C, k, s, p = ctx.geom
         dx = torch.empty(N, H, W, C, device=dy.device)
@@ -368,6 +394,7 @@ class _AvgPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        _own(dy)
         N, H, W, C, k = ctx.geom
         dx = torch.empty(N, H, W, C, device=dy.device)
         call("es_avgpool2d_bwd", ptr(dy.contiguous()), N, H, W, C, k, ptr(dx), 0, _s())
@@ -388,6 +415,7 @@ class _UpsampleAddFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _own(dout)
         N, H, W, C, s = ctx.geom
         dout = dout.contiguous()
         dsrc = torch.empty(N, H // s, W // s, C, device=dout.device)
@@ -413,6 +441,7 @@ class _FcuTokensFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _own(dout)
         pooled, mean, rstd = ctx.saved_tensors
         m, pre = ctx.m, ctx.pre
         N, h, w, D = pooled.shape
@@ -446,6 +475,7 @@ class _PatchTokensFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dxt):
+        _own(dxt)
         (xb,) = ctx.saved_tensors
         m = ctx.m
         cfg = m.cfg
@@ -512,6 +542,7 @@ class _BlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        _own(dout)
         xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, pre_, act = ctx.saved_tensors
         m, pre, n = ctx.m, ctx.pre, ctx.n
         cfg = m.cfg
@@ -603,6 +634,7 @@ class _ConvHeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dl):
+        _own(dl)
         (pooled,) = ctx.saved_tensors
         m = ctx.m
         N, H, W, C = ctx.geom
@@ -637,6 +669,7 @@ class _TransHeadFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dl):
+        _own(dl)
         xhat, rstd = ctx.saved_tensors
         m, n = ctx.m, ctx.n
         cfg = m.cfg
@@ -783,20 +816,28 @@ class NativeConformer(nn.Module):
     # ---- forward (code/models/conformer.py:418-445) ------------------------------------------
     def _conv_block(self, pre, x, stride, res_conv, x_t=None, return_x2=True):
         """ConvBlock.forward (:107-144)."""
+        x2 = self._conv_block_head(pre, x, stride, x_t)
+        out = self._conv_block_tail(pre, x, x2, stride, res_conv)
+        return (out, x2) if return_x2 else out
+
+    def _conv_block_head(self, pre, x, stride, x_t=None):
+        """conv1 -> bn1 -> ReLU (-> + upsampled x_t) -> conv2 -> bn2 -> ReLU: x2 (:118-130)."""
         med = self.shapes[pre + "conv1.weight"][0]
-        outp = self.shapes[pre + "conv3.weight"][0]
-        residual = x
         h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1), pre + "bn1.", relu=True)
         if x_t is not None:
             h = _UpsampleAddFn.apply(h, x_t, h.shape[1] // x_t.shape[1])
         h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1)
-        x2 = bn(self, h, pre + "bn2.", relu=True)
+        return bn(self, h, pre + "bn2.", relu=True)
+
+    def _conv_block_tail(self, pre, x, x2, stride, res_conv):
+        """conv3 -> bn3 (+ residual, via residual_conv / residual_bn) -> ReLU (:132-144)."""
+        outp = self.shapes[pre + "conv3.weight"][0]
         h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1)
+        residual = x
         if res_conv:
-            r = conv(self, residual, _Map.nhwc(residual), pre + "residual_conv.weight", None, outp, 1, stride)
+            r = conv(self, x, _Map.nhwc(x), pre + "residual_conv.weight", None, outp, 1, stride)
             residual = bn(self, r, pre + "residual_bn.")
-        out = bn(self, h, pre + "bn3.", relu=True, res=residual)
-        return (out, x2) if return_x2 else out
+        return bn(self, h, pre + "bn3.", relu=True, res=residual)
 
     def forward(self, x):
         cfg = self.cfg
@@ -822,31 +863,60 @@ class NativeConformer(nn.Module):
         anchor = self._anchor if (torch.is_grad_enabled() and self.training) else None
         h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor)
         x_base = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1)
+        main = torch.cuda.current_stream(x.device)
+        tb = _branch_stream(x.device) if BRANCH_STREAMS else main
+
+        def to_branch(t):  # main-stream tensor read by the branch stream
+            if tb is not main:
+                tb.wait_stream(main)
+                t.record_stream(tb)
+
+        def to_main(t):  # branch-stream tensor read by the main stream
+            if tb is not main:
+                main.wait_stream(tb)
+                t.record_stream(main)
+
+        to_branch(x_base)
+        with torch.cuda.stream(tb):
+            xt = _PatchTokensFn.apply(x_base, self)
+            xt = _BlockFn.apply(xt, self, "trans_1.")
         xc = self._conv_block("conv_1.", x_base, 1, True, return_x2=False)
-        xt = _PatchTokensFn.apply(x_base, self)
-        xt = _BlockFn.apply(xt, self, "trans_1.")
         T, g = cfg.T, cfg.grid
         for name, _, outp, res_conv, stride, dw, last in cfg.stages():
             pre = name + "."
             med = outp // 4
-            xc, x2 = self._conv_block(pre + "cnn_block.", xc, stride, res_conv)
-            # FCUDown (:161-170): 1x1 conv (bias) -> avg-pool dw -> LN -> GELU -> cat(cls), + x_t.
-            # The 1x1 conv and the average pool are both linear maps over different axes (channels /
-            # pixels; the pool averages bias-shifted values to the same bias), so they commute: pooling
-            # the med-channel map first runs the D-channel conv at 1/dw^2 of the pixels (exact in real
-            # arithmetic; fp32 rounding order only)
-            x2p = _AvgPoolFn.apply(x2, dw) if dw > 1 else x2
-            pooled = conv(self, x2p, _Map.nhwc(x2p), pre + "squeeze_block.conv_project.weight",
-                          pre + "squeeze_block.conv_project.bias", D, 1)
-            xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.")
-            xt = _BlockFn.apply(xt, self, pre + "trans_block.")
-            # FCUUp (:187-194): token rows 1.. as a [n, g, g, D] map -> 1x1 conv (bias) -> BN -> ReLU;
-            # the nearest upsampling is fused into the fusion block's conv2 input
-            tok = _Map(xt, n, g, g, D, sn=T * D, sh=g * D, sw=D, sc=1, off=D)
-            up = conv(self, xt, tok, pre + "expand_block.conv_project.weight", pre + "expand_block.conv_project.bias",
-                      med, 1)
-            up = bn(self, up, pre + "expand_block.bn.", relu=True)
+            xin = xc
+            x2 = self._conv_block_head(pre + "cnn_block.", xin, stride)
+            to_branch(x2)
+            with torch.cuda.stream(tb):
+                xt, up = self._trans_branch(pre, x2, xt, dw, med)
+            xc = self._conv_block_tail(pre + "cnn_block.", xin, x2, stride, res_conv)
+            to_main(up)
             xc = self._conv_block(pre + "fusion_block.", xc, 2 if last else 1, last, x_t=up, return_x2=False)
+        to_main(xt)
         conv_cls = _ConvHeadFn.apply(xc, self)
         trans_cls = _TransHeadFn.apply(xt, self)
         return conv_cls, trans_cls
+
+    def _trans_branch(self, pre, x2, xt, dw, med):
+        """FCUDown -> transformer block -> FCUUp of one ConvTransBlock (:334-352); returns the new token
+        buffer and the FCUUp map the fusion block adds."""
+        cfg, n = self.cfg, self.cur_n
+        D, T, g = cfg.dim, cfg.T, cfg.grid
+        # FCUDown (:161-170): 1x1 conv (bias) -> avg-pool dw -> LN -> GELU -> cat(cls), + x_t.
+        # The 1x1 conv and the average pool are both linear maps over different axes (channels /
+        # pixels; the pool averages bias-shifted values to the same bias), so they commute: pooling
+        # the med-channel map first runs the D-channel conv at 1/dw^2 of the pixels (exact in real
+        # arithmetic; fp32 rounding order only)
+        x2p = _AvgPoolFn.apply(x2, dw) if dw > 1 else x2
+        pooled = conv(self, x2p, _Map.nhwc(x2p), pre + "squeeze_block.conv_project.weight",
+                      pre + "squeeze_block.conv_project.bias", D, 1)
+        xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.")
+        xt = _BlockFn.apply(xt, self, pre + "trans_block.")
+        # FCUUp (:187-194): token rows 1.. as a [n, g, g, D] map -> 1x1 conv (bias) -> BN -> ReLU;
+        # the nearest upsampling is fused into the fusion block's conv2 input
+        tok = _Map(xt, n, g, g, D, sn=T * D, sh=g * D, sw=D, sc=1, off=D)
+        up = conv(self, xt, tok, pre + "expand_block.conv_project.weight", pre + "expand_block.conv_project.bias",
+                  med, 1)
+        up = bn(self, up, pre + "expand_block.bn.", relu=True)
+        return xt, up
