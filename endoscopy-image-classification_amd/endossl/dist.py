@@ -17,6 +17,11 @@ def init_from_env(backend=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, gloo over HIP tensors
+    # (RCCL refuses two ranks on one device).  Not for measurement.
+    backend = os.environ.get("ENDOSSL_DIST_BACKEND") or backend
+    if os.environ.get("ENDOSSL_SHARE_DEVICE") == "1":
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:

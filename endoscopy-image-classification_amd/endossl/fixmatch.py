@@ -13,9 +13,9 @@ benchmark times.  One step (code/fixmatch.py:91-131):
          lu, mask = consistency(logits_w, logits[B:], tau)  fused kernel  (:116)
          losses = lx + LAMBDA_U * lu                                      (:118)
   bwd    flat grads <- explicit backward of d(losses)/d(logits)            (:122)
-  comm   RCCL all-reduce of the flat grad (data-parallel only), one bucket per transformer block
-         issued as soon as that block's gradients are final, beside the rest of the reverse pass
-         (dist.GradBuckets; ENDOSSL_OVERLAP_AR=0 for one all-reduce after the backward)
+  comm   RCCL all-reduce of the flat grad (data-parallel only) after the backward; opt-in
+         (ENDOSSL_OVERLAP_AR=1): one bucket per transformer block issued as soon as that block's
+         gradients are final, beside the rest of the reverse pass (dist.GradBuckets)
   opt    Adam + EMA in one sweep, then lr_scheduler.step_update           (:123-127)
 
 No `.item()` per step: losses stay on device and the AverageMeter is filled once per epoch.
@@ -40,8 +40,11 @@ def _next(it):
 
 
 class FixMatch:
-    # bucketed all-reduce overlapped with the backward (world > 1)
-    overlap_allreduce = os.environ.get("ENDOSSL_OVERLAP_AR", "1") != "0"
+    # bucketed all-reduce overlapped with the backward (world > 1): opt-in, ENDOSSL_OVERLAP_AR=1.  Off by
+    # default: unmeasured over RCCL here (one GPU per box), and the two-rank gloo rehearsal on one GPU
+    # ran 1.1-3.7 s/step with it vs 92 ms without whenever the engine's second stream was on
+    # (129 ms with it off) -- DESIGN.md §6
+    overlap_allreduce = os.environ.get("ENDOSSL_OVERLAP_AR", "0") == "1"
 
     def __init__(self, model, opt_func="Adam", lr=1e-3, device='cpu'):
         self.model = model
