@@ -69,6 +69,7 @@ class CoMatch(FixMatch):
         self.queue_feats = torch.zeros(self.queue_size, self.low_dim, device=dev)
         self.queue_probs = torch.zeros(self.queue_size, self.queue_probs.shape[1], device=dev)
         self.queue_ptr = 0
+        self._ws = {}  # the pseudo-label workspace is sized by the queue size
 
     @property
     def prob_list(self):
@@ -77,7 +78,7 @@ class CoMatch(FixMatch):
         return [self.prob_hist[i] for i in idx]
 
     def _workspace(self, bt, btu, C, L):
-        key = (bt, btu)
+        key = (bt, btu, self.queue_size)
         if key not in self._ws:
             dev = self.model.flat.device
             n = bt + 3 * btu

@@ -786,6 +786,10 @@ class NativeConformer(nn.Module):
     def fc(self):  # SemiFormer freezes conv_cls_head / trans_cls_head; FixMatch-style callers ask for .fc
         return self.trans_cls_head
 
+    def no_weight_decay(self):
+        """Conformer.no_weight_decay (code/models/conformer.py:414-415)."""
+        return {"cls_token"}
+
     def _pack(self):
         """bf16 images W [N, K] / W^T [K, N] of every transformer-block matrix (re-packed after
         each optimizer step, es_pack_weights)."""
@@ -849,6 +853,9 @@ class NativeConformer(nn.Module):
             raise ValueError("NativeConformer takes ImageNet-normalised fp32 images (code/dataset.py:49-51); the "
                              "uint8 input path is the ViT engine's")
         self._pack()
+        # a backward that raised after queueing its stream join never ran the callback that clears
+        # its key: every new graph starts with no join pending
+        _join_queued.clear()
         x = x.float().contiguous()
         n, S = x.shape[0], cfg.img_size
         self.cur_n = n

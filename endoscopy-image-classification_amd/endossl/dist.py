@@ -11,17 +11,24 @@ import torch.distributed as dist
 
 
 def init_from_env(backend=None):
-    """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* (127.0.0.1)."""
+    """Initialise from torchrun's RANK / WORLD_SIZE / LOCAL_RANK / MASTER_* (127.0.0.1).  Returns
+    (rank, world, local device index)."""
+    share = os.environ.get("ENDOSSL_SHARE_DEVICE") == "1"
     if dist.is_available() and dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", 0))
+        return dist.get_rank(), dist.get_world_size(), 0 if share else int(os.environ.get("LOCAL_RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, gloo over HIP tensors
     # (RCCL refuses two ranks on one device).  Not for measurement.
     backend = os.environ.get("ENDOSSL_DIST_BACKEND") or backend
-    if os.environ.get("ENDOSSL_SHARE_DEVICE") == "1":
+    if share:
         local = 0
+        if backend is None:
+            backend = "gloo"
+        elif backend == "nccl":
+            raise RuntimeError("ENDOSSL_SHARE_DEVICE=1 puts every rank on device 0, which RCCL refuses: "
+                               "use the gloo backend for the one-GPU rehearsal")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:

@@ -830,6 +830,11 @@ class NativeViT(nn.Module):
     def fc(self):  # code/fixmatch.py:48 freezes `model.fc`; timm ViTs call it `head`
         return self.head
 
+    def no_weight_decay(self):
+        """timm 0.5.4 VisionTransformer.no_weight_decay (the second Adam param group's names,
+        code/optimizer.py:38-41)."""
+        return {"pos_embed", "cls_token", "dist_token"}
+
     def mark_updated(self):
         self.version += 1
 
