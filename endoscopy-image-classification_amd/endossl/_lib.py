@@ -93,6 +93,21 @@ SIGNATURES = {
     "es_pack_weights": (I, [V, V, I, V]),
     "es_cast_f32_bf16": (I, [V, V, L, V]),
     "es_add_f32": (I, [V, V, L, V]),
+    # fp32 parity mode (csrc/parity.hip): the bf16 entry points' signatures, fp32 storage
+    "es_gemm_nt_f32": (I, [I, V, I, V, I, V, V, I, V, V, I, I, I, I, I, V]),
+    "es_gemm_tn_f32_workspace": (Z, [I, I, I]),
+    "es_gemm_tn_f32": (I, [V, I, V, I, I, I, I, I, V, V, I, V, V]),
+    "es_attn_fwd_f32": (I, [V, I, V, I, V, I, I, I, F, V]),
+    "es_attn_bwd_f32": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),
+    "es_attn_cls_fwd_f32": (I, [V, I, V, I, V, I, I, I, F, V]),
+    "es_attn_cls_bwd_f32": (I, [V, I, V, I, V, V, I, V, I, I, I, I, F, V]),
+    "es_layernorm_fwd_f32": (I, [V, I, V, V, V, I, V, V, I, I, F, V]),
+    "es_layernorm_bwd_f32": (I, [V, I, V, I, V, V, V, V, I, V, I, V, I, V, V, V, I, I, I, I, V]),
+    "es_patch_im2col_f32": (I, [V, V, I, I, I, V]),
+    "es_patch_im2col_u8_f32": (I, [V, F, F, F, F, F, F, V, I, I, I, V]),
+    "es_embed_bwd_f32": (I, [V, I, V, I, V, V, I, I, I, I, V]),
+    "es_pack_weights_f32": (I, [V, V, I, V]),
+    "es_copy_f32": (I, [V, V, L, V]),
 }
 
 ABI_VERSION = 1

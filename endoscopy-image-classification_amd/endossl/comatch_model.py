@@ -163,6 +163,7 @@ class NativeViTEmb(NativeViT):
         for a, b in zip(other.bn_buffers(), self.bn_buffers()):
             a.copy_(b)
         other._engine, other._heads = None, None
+        other.precision = self.precision
         other.version = 0
         other.drop_seed, other._drop_counter, other._last_n = self.drop_seed, self._drop_counter, 0
         other.train(self.training)

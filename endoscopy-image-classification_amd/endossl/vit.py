@@ -148,14 +148,14 @@ def timm_init_(flat, cfg, layout, offs, generator=None):
 class _Acts:
     """Token-major activation buffers for one batch size (train keeps every layer's tensors)."""
 
-    def __init__(self, cfg, n, train, device):
+    def __init__(self, cfg, n, train, device, b16=torch.bfloat16):
         D, Hd, L = cfg.dim, cfg.hidden, cfg.depth
         self.n, self.train = n, train
         self.M = n * cfg.T
         Mp = _rup(self.M, 256)
         self.Mp = Mp
         Lk = L if train else 1
-        f32, b16 = torch.float32, torch.bfloat16
+        f32 = torch.float32
         z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
         self.patches = z(_rup(n * cfg.np, 256), 3 * cfg.patch * cfg.patch, dt=b16)
         self.x = z(L + 1 if train else 2, Mp, D)
@@ -186,10 +186,10 @@ class _Acts:
 class _Grads:
     """Backward scratch (one layer's worth, reused top-down)."""
 
-    def __init__(self, cfg, n, device):
+    def __init__(self, cfg, n, device, b16=torch.bfloat16):
         D, Hd = cfg.dim, cfg.hidden
         Mp = _rup(n * cfg.T, 256)
-        f32, b16 = torch.float32, torch.bfloat16
+        f32 = torch.float32
         z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
         self.n = n
         self.dx, self.dxb = z(Mp, D), z(Mp, D, dt=b16)
@@ -268,8 +268,22 @@ class Engine:
     # full with the weight gradients on the side stream
     ATTN_SPLIT = os.environ.get("ENDOSSL_ATTN_SPLIT", "0") == "1"
 
-    def __init__(self, cfg, device):
+    # fp32 parity mode (csrc/parity.hip): the same launch sequence over fp32 operand storage; the
+    # entry points with an fp32 form, by their bf16 names
+    PARITY_NAMES = {n: n + "_f32" for n in (
+        "es_gemm_nt", "es_gemm_tn", "es_attn_fwd", "es_attn_bwd", "es_attn_cls_fwd", "es_attn_cls_bwd",
+        "es_layernorm_fwd", "es_layernorm_bwd", "es_patch_im2col", "es_patch_im2col_u8", "es_embed_bwd",
+        "es_pack_weights")}
+    PARITY_NAMES.update({"es_layernorm_bwd_b16": "es_layernorm_bwd_f32", "es_cast_f32_bf16": "es_copy_f32"})
+
+    def __init__(self, cfg, device, precision="bf16"):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' (production) or 'fp32' (parity mode), got {precision!r}")
         self.cfg, self.device = cfg, device
+        self.precision = precision
+        self.op_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+        if precision == "fp32":  # one lane, the plain launch forms (the opt-in variants have no fp32 form)
+            self.LANES, self.FUSED_MLP, self.ATTN_SPLIT = 1, False, False
         self.layout, self.offs, self.numel = param_layout(cfg)
         self.shapes = dict(self.layout)
         self._acts = {}
@@ -283,7 +297,7 @@ class Engine:
         self.overlap_fwd = self.OVERLAP_FWD
         self._packed_version = -1
         D, Hd = cfg.dim, cfg.hidden
-        b16 = torch.bfloat16
+        b16 = self.op_dtype
         # bf16 weight images: W [N,K] for forward, W^T [K,N] for dgrad
         mats = [("patch_embed.proj.weight", D, 3 * cfg.patch * cfg.patch, False)]
         for i in range(cfg.depth):
@@ -307,18 +321,26 @@ class Engine:
         # optional live timing of one launch site: {"label": str, "events": [(start, end, flops)]}
         self.probe = None
 
+    def _call(self, name, *args):
+        """C-ABI call; in parity mode the fp32 form of the entry point."""
+        if self.precision == "fp32":
+            name = self.PARITY_NAMES.get(name, name)
+            if name in ("es_mlp_fwd_infer", "es_attn_bwd_dq", "es_attn_bwd_dkv", "es_pack_chunk32"):
+                raise RuntimeError(f"{name} has no fp32 parity form")
+        return call(name, *args)
+
     def _gemm(self, label, *args):
         """es_gemm_nt, optionally bracketed by HIP events on the launch stream (bench roofline)."""
         pr = self.probe
         if pr is not None and pr["label"] == label:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            call("es_gemm_nt", *args)
+            self._call("es_gemm_nt", *args)
             e1.record()
             M, N, K = args[11], args[12], args[13]
             pr["events"].append((e0, e1, 2.0 * M * N * K))
         else:
-            call("es_gemm_nt", *args)
+            self._call("es_gemm_nt", *args)
 
     # -------------------------------------------------------------- helpers
     def view(self, flat, name):
@@ -329,21 +351,21 @@ class Engine:
         """Refresh the bf16 weight images from the fp32 master (skipped if `version` unchanged)."""
         if version is not None and version == self._packed_version:
             return
-        call("es_pack_weights", ptr(flat), ptr(self._pack_tab), self._nmat, _lib.stream())
+        self._call("es_pack_weights", ptr(flat), ptr(self._pack_tab), self._nmat, _lib.stream())
         if self.FUSED_MLP:  # chunk-major fc2 images for es_mlp_fwd_infer
             cfg = self.cfg
             if not hasattr(self, "_w2c"):
                 self._w2c = {i: torch.zeros(cfg.hidden // 32, cfg.dim, 32, dtype=torch.bfloat16, device=self.device)
                              for i in range(cfg.depth)}
             for i in range(cfg.depth):
-                call("es_pack_chunk32", ptr(self.wb[f"blocks.{i}.mlp.fc2.weight"]), ptr(self._w2c[i]), cfg.dim,
+                self._call("es_pack_chunk32", ptr(self.wb[f"blocks.{i}.mlp.fc2.weight"]), ptr(self._w2c[i]), cfg.dim,
                      cfg.hidden, _lib.stream())
         self._packed_version = version if version is not None else -1
 
     def acts(self, n, train):
         key = (n, train)
         if key not in self._acts:
-            self._acts[key] = _Acts(self.cfg, n, train, self.device)
+            self._acts[key] = _Acts(self.cfg, n, train, self.device, self.op_dtype)
         return self._acts[key]
 
     def workspace(self, lane=0):
@@ -398,18 +420,18 @@ class Engine:
                                  f"images, got {tuple(t.shape)} {t.dtype}")
             t = t.contiguous()
             if t.dtype == torch.uint8:  # ToTensor + Normalize fused into the patch gather
-                call("es_patch_im2col_u8", ptr(t), *IMAGENET_MEAN, *IMAGENET_STD, ptr(A.patches[row * cfg.np:]),
+                self._call("es_patch_im2col_u8", ptr(t), *IMAGENET_MEAN, *IMAGENET_STD, ptr(A.patches[row * cfg.np:]),
                      int(t.shape[0]), cfg.img_size, cfg.patch, s)
             else:
-                call("es_patch_im2col", ptr(t), ptr(A.patches[row * cfg.np:]), int(t.shape[0]), cfg.img_size,
+                self._call("es_patch_im2col", ptr(t), ptr(A.patches[row * cfg.np:]), int(t.shape[0]), cfg.img_size,
                      cfg.patch, s)
             row += int(t.shape[0])
         x0 = A.x[0]
         pos = self.view(flat, "pos_embed")
-        call("es_gemm_nt", EPI_PATCH, ptr(A.patches), K0, ptr(self.wb["patch_embed.proj.weight"]), K0,
+        self._call("es_gemm_nt", EPI_PATCH, ptr(A.patches), K0, ptr(self.wb["patch_embed.proj.weight"]), K0,
              ptr(self.view(flat, "patch_embed.proj.bias")), ptr(x0), D, None, ptr(pos), D, n * cfg.np, D, K0,
              cfg.np, s)
-        call("es_cls_init", ptr(x0), D, ptr(self.view(flat, "cls_token")), ptr(pos), n, T, D, s)
+        self._call("es_cls_init", ptr(x0), D, ptr(self.view(flat, "cls_token")), ptr(pos), n, T, D, s)
         M = A.M
         prune = self._prune()
         for i in range(cfg.depth):
@@ -418,32 +440,32 @@ class Engine:
             xin = A.x[i] if train else A.x[i & 1]
             xout = A.x[i + 1] if train else A.x[(i + 1) & 1]
             xmid, h1, h2 = A.xmid[li], A.h1[li], A.h2[li]
-            call("es_layernorm_fwd", ptr(xin), D, ptr(self.view(flat, b + "norm1.weight")),
+            self._call("es_layernorm_fwd", ptr(xin), D, ptr(self.view(flat, b + "norm1.weight")),
                  ptr(self.view(flat, b + "norm1.bias")), ptr(h1), D, ptr(A.mean1[li]), ptr(A.rstd1[li]), M, D,
                  cfg.eps, s)
             if prune and self.PRUNE_Q and i == cfg.depth - 1:
                 # K and V for every token; Q for the CLS rows only, written to their rows of qkv
                 wq, bq = self.wb[b + "attn.qkv.weight"], self.view(flat, b + "attn.qkv.bias")
-                call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(wq[D:]), D, ptr(bq[D:]), ptr(A.qkv[li][:, D:]), 3 * D,
+                self._call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(wq[D:]), D, ptr(bq[D:]), ptr(A.qkv[li][:, D:]), 3 * D,
                      None, None, 0, M, 2 * D, D, 0, s)
                 A.c_h1[:n].copy_(h1[:M].view(n, T, D)[:, 0])
-                call("es_gemm_nt", EPI_BF16, ptr(A.c_h1), D, ptr(wq[:D]), D, ptr(bq[:D]), ptr(A.qkv[li]), T * 3 * D,
+                self._call("es_gemm_nt", EPI_BF16, ptr(A.c_h1), D, ptr(wq[:D]), D, ptr(bq[:D]), ptr(A.qkv[li]), T * 3 * D,
                      None, None, 0, n, D, D, 0, s)
             else:
-                call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(self.wb[b + "attn.qkv.weight"]), D,
+                self._call("es_gemm_nt", EPI_BF16, ptr(h1), D, ptr(self.wb[b + "attn.qkv.weight"]), D,
                      ptr(self.view(flat, b + "attn.qkv.bias")), ptr(A.qkv[li]), 3 * D, None, None, 0, M, 3 * D, D, 0,
                      s)
             if prune and i == cfg.depth - 1:
                 self._last_block_cls_fwd(flat, A, b, li, xin, n, train, s)
                 break
-            call("es_attn_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.o[li]), D, ptr(A.lse[li]), n, T, H, 64 ** -0.5, s)
-            call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
+            self._call("es_attn_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.o[li]), D, ptr(A.lse[li]), n, T, H, 64 ** -0.5, s)
+            self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
                  ptr(self.view(flat, b + "attn.proj.bias")), ptr(xmid), D, None, ptr(xin), D, M, D, D, 0, s)
-            call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
+            self._call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
                  ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
                  cfg.eps, s)
             if not train and self.FUSED_MLP and D in (128, 384) and hasattr(self, "_w2c"):
-                call("es_mlp_fwd_infer", ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]),
+                self._call("es_mlp_fwd_infer", ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]),
                      ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(self._w2c[i]),
                      ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xmid), D, ptr(xout), D, M, D, Hd, s)
                 continue
@@ -456,17 +478,17 @@ class Engine:
                 self._gemm("fc1_fwd_weak", EPI_GELU_ACT, ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
                            ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(A.act[li]), Hd, None, None, 0, M, Hd, D, 0,
                            s)
-            call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
+            self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
                  ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xout), D, None, ptr(xmid), D, M, D, Hd, 0, s)
         xl = A.x[cfg.depth] if train else A.x[cfg.depth & 1]
         Tl = T  # row stride of the CLS tokens in xl, in tokens
         if prune:
             xl, Tl = A.c_xout, 1
         if cfg.head == "emb":  # CLS features for ModelwEmb's heads (comatch_model.py)
-            call("es_cls_ln_fwd", ptr(xl), D, Tl, ptr(self.view(flat, "norm.weight")),
+            self._call("es_cls_ln_fwd", ptr(xl), D, Tl, ptr(self.view(flat, "norm.weight")),
                  ptr(self.view(flat, "norm.bias")), ptr(A.fts), D, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.eps, s)
             return A.fts
-        call("es_cls_head_fwd", ptr(xl), D, Tl, ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")),
+        self._call("es_cls_head_fwd", ptr(xl), D, Tl, ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")),
              ptr(self.view(flat, "head.weight")), ptr(self.view(flat, "head.bias")), ptr(A.logits),
              cfg.num_classes, ptr(A.xhat), ptr(A.rstd_cls), n, D, cfg.num_classes, cfg.eps, s)
         return A.logits
@@ -483,19 +505,19 @@ class Engine:
         cfg = self.cfg
         D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
         fv = lambda name: ptr(self.view(flat, name))  # noqa: E731
-        call("es_attn_cls_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.c_o), D, ptr(A.c_lse), n, T, H, 64 ** -0.5, s)
-        call("es_gemm_nt", EPI_F32_RESID, ptr(A.c_o), D, ptr(self.wb[b + "attn.proj.weight"]), D,
+        self._call("es_attn_cls_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.c_o), D, ptr(A.c_lse), n, T, H, 64 ** -0.5, s)
+        self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.c_o), D, ptr(self.wb[b + "attn.proj.weight"]), D,
              fv(b + "attn.proj.bias"), ptr(A.c_xmid), D, None, ptr(xin), T * D, n, D, D, 0, s)
-        call("es_layernorm_fwd", ptr(A.c_xmid), D, fv(b + "norm2.weight"), fv(b + "norm2.bias"), ptr(A.c_h2), D,
+        self._call("es_layernorm_fwd", ptr(A.c_xmid), D, fv(b + "norm2.weight"), fv(b + "norm2.bias"), ptr(A.c_h2), D,
              ptr(A.c_mean2), ptr(A.c_rstd2), n, D, cfg.eps, s)
         if train:
-            call("es_gemm_nt", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(A.c_h2), D,
+            self._call("es_gemm_nt", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(A.c_h2), D,
                  ptr(self.wb[b + "mlp.fc1.weight"]), D, fv(b + "mlp.fc1.bias"), ptr(A.c_pre), Hd, ptr(A.c_act), None,
                  0, n, Hd, D, 0, s)
         else:
-            call("es_gemm_nt", EPI_GELU_ACT, ptr(A.c_h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
+            self._call("es_gemm_nt", EPI_GELU_ACT, ptr(A.c_h2), D, ptr(self.wb[b + "mlp.fc1.weight"]), D,
                  fv(b + "mlp.fc1.bias"), ptr(A.c_act), Hd, None, None, 0, n, Hd, D, 0, s)
-        call("es_gemm_nt", EPI_F32_RESID, ptr(A.c_act), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
+        self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.c_act), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
              fv(b + "mlp.fc2.bias"), ptr(A.c_xout), D, None, ptr(A.c_xmid), D, n, D, Hd, 0, s)
 
     # -------------------------------------------------------------- backward
@@ -512,14 +534,14 @@ class Engine:
         splits = self._tn_splits(M, N1, N2)
         if _lib.load().es_gemm_tn_workspace(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
-        call("es_gemm_tn", ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0,
+        self._call("es_gemm_tn", ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0,
              ptr(bias_out), _lib.stream())
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None):
         D = self.cfg.dim
         ws = self.ln_workspace(lane)
-        fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"
-        call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
+        fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"  # (_f32 in parity mode)
+        self._call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True, grad_ready=None):
@@ -541,7 +563,7 @@ class Engine:
         if n not in self._grads:
             # two sets: layer i's weight-gradient inputs (dY images) live in set i % 2, so the side
             # stream can still read layer i+1's while the main stream writes layer i's
-            self._grads[n] = (_Grads(cfg, n, self.device), _Grads(cfg, n, self.device))
+            self._grads[n] = (_Grads(cfg, n, self.device, self.op_dtype), _Grads(cfg, n, self.device, self.op_dtype))
         G = self._grads[n][0]
         GS = self._grads[n]
         D, Hd, T, H, M = cfg.dim, cfg.hidden, cfg.T, cfg.heads, A.M
@@ -580,11 +602,11 @@ class Engine:
             G.dx.zero_()
         if cfg.head == "emb":
             dfts = dfts.contiguous()
-            call("es_cls_ln_bwd", ptr(dfts), D, ptr(fv("norm.weight")), ptr(A.xhat), ptr(A.rstd_cls), ptr(dtop), D, Tt,
+            self._call("es_cls_ln_bwd", ptr(dfts), D, ptr(fv("norm.weight")), ptr(A.xhat), ptr(A.rstd_cls), ptr(dtop), D, Tt,
                  ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D, s)
         else:
             dlogits = dlogits.contiguous()
-            call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
+            self._call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
                  ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(dtop), D, Tt,
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
                  cfg.num_classes, s)
@@ -593,30 +615,30 @@ class Engine:
                 and (nh * cfg.np) % 256 == 0 and grad.numel() % 4 == 0):
             return self._backward_lanes(flat, grad, A, G.dx, nh)
         if prune:
-            call("es_cast_f32_bf16", ptr(GL.c_dx), ptr(GL.c_dxb), n * D, s)
+            self._call("es_cast_f32_bf16", ptr(GL.c_dx), ptr(GL.c_dxb), n * D, s)
         else:
-            call("es_cast_f32_bf16", ptr(G.dx), ptr(GL.dxb), M * D, s)
+            self._call("es_cast_f32_bf16", ptr(G.dx), ptr(GL.dxb), M * D, s)
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."
             Gi, Gn = GS[i % 2], GS[(i - 1) % 2]
             if prune and i == cfg.depth - 1:
                 # ---- the last block on its CLS rows: MLP, LN2 and projection over n compact rows
-                call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.c_dxb), D,
+                self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.c_dxb), D,
                      ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.c_dpre), Hd, None, ptr(A.c_pre), Hd, n, Hd,
                      D, 0, s)
                 wgrad_side(Gi.c_dxb, D, A.c_act, Hd, n, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
-                call("es_gemm_nt", EPI_DH, ptr(Gi.c_dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
+                self._call("es_gemm_nt", EPI_DH, ptr(Gi.c_dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
                      ptr(Gi.c_dh), D, None, None, 0, n, D, Hd, 0, s)
                 wgrad_side(Gi.c_dpre, Hd, A.c_h2, D, n, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
                 # d(xmid) lands on the CLS rows of the full token image dxm_cls (zero elsewhere)
                 self._ln_bwd(Gi.c_dh, A.c_xmid, A.c_mean2, A.c_rstd2, fv(b + "norm2.weight"), Gi.c_dx, Gi.dxm_cls,
                              Gi.c_dxmb, gv(b + "norm2.weight"), gv(b + "norm2.bias"), n, lddx=T * D)
-                call("es_gemm_nt", EPI_BF16, ptr(Gi.c_dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
+                self._call("es_gemm_nt", EPI_BF16, ptr(Gi.c_dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
                      ptr(Gi.c_do), D, None, None, 0, n, D, D, 0, s)
                 wgrad_side(Gi.c_dxmb, D, A.c_o, D, n, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
-                call("es_attn_cls_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.c_o), D, ptr(A.c_lse), ptr(Gi.c_do), D,
+                self._call("es_attn_cls_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.c_o), D, ptr(A.c_lse), ptr(Gi.c_do), D,
                      ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
-                call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+                self._call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                      ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
                 gw, gb = gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias")
                 if self.PRUNE_Q and n % 32 == 0:
@@ -633,31 +655,31 @@ class Engine:
                 block_done(i)
                 continue
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
-            call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.dxb), D,
+            self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.dxb), D,
                  ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre), Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
             wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
-            call("es_gemm_nt", EPI_DH, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh),
+            self._call("es_gemm_nt", EPI_DH, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh),
                  D, None, None, 0, M, D, Hd, 0, s)
             wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
             self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, Gi.dxmb,
                          gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
             # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
-            call("es_gemm_nt", EPI_BF16, ptr(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
+            self._call("es_gemm_nt", EPI_BF16, ptr(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
                  None, None, 0, M, D, D, 0, s)
             wgrad_side(Gi.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
             if ov and self.ATTN_SPLIT:
                 s3 = self.attn_stream()
                 s3.wait_stream(main)
                 with torch.cuda.stream(s3):
-                    call("es_attn_bwd_dkv", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.do), D,
+                    self._call("es_attn_bwd_dkv", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.do), D,
                          ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, _lib.stream())
-                call("es_attn_bwd_dq", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do),
+                self._call("es_attn_bwd_dq", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do),
                      D, ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
                 main.wait_stream(s3)
             else:
-                call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
+                self._call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
                      ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
-            call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+            self._call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
             wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
             if ov:
@@ -669,7 +691,7 @@ class Engine:
             block_done(i)
         # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
         K0 = 3 * cfg.patch * cfg.patch
-        call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,
+        self._call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,
              s)
         npat = n * cfg.np
         wgrad_side(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
@@ -695,7 +717,8 @@ class Engine:
             self._grad_b = torch.zeros_like(grad)
         key = nh
         if key not in self._lane_state:
-            self._lane_state[key] = [_Grads(cfg, nh, self.device), _Grads(cfg, nh, self.device)]
+            self._lane_state[key] = [_Grads(cfg, nh, self.device, self.op_dtype),
+                                     _Grads(cfg, nh, self.device, self.op_dtype)]
         lanes = []
         for ln, (st, g) in enumerate(((main, grad), (side, self._grad_b))):
             r0 = ln * Ml
@@ -704,7 +727,7 @@ class Engine:
         side.wait_stream(main)  # head backward (dx_full) and the zeroed grad
         for L in lanes:
             with torch.cuda.stream(L["stream"]):
-                call("es_cast_f32_bf16", ptr(L["dx"]), ptr(L["G"].dxb), Ml * D, _lib.stream())
+                self._call("es_cast_f32_bf16", ptr(L["dx"]), ptr(L["G"].dxb), Ml * D, _lib.stream())
         fv = lambda name: self.view(flat, name)  # noqa: E731
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."
@@ -719,22 +742,22 @@ class Engine:
                     m2, s2 = A.mean2[i][r0:r1], A.rstd2[i][r0:r1]
                     lse = A.lse[i][L["lse0"]:]
                     # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
-                    call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(G.dxb), D,
+                    self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(G.dxb), D,
                          ptr(self.wt[b + "mlp.fc2.weight"]), D, None,
                          ptr(G.dpre), Hd, None, ptr(pre), Hd, Ml, Hd, D, 0, s)
                     self._wgrad(G.dxb, D, act, Hd, Ml, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"), lane=ln)
-                    call("es_gemm_nt", EPI_DH, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
+                    self._call("es_gemm_nt", EPI_DH, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
                          ptr(G.dh), D, None, None, 0, Ml, D, Hd, 0, s)
                     self._wgrad(G.dpre, Hd, h2, D, Ml, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"), lane=ln)
                     self._ln_bwd(G.dh, xmid, m2, s2, fv(b + "norm2.weight"), L["dx"], G.dxm, G.dxmb,
                                  gv(b + "norm2.weight"), gv(b + "norm2.bias"), Ml, lane=ln)
                     # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
-                    call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
+                    self._call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
                          ptr(G.do), D, None, None, 0, Ml, D, D, 0, s)
                     self._wgrad(G.dxmb, D, o, D, Ml, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"), lane=ln)
-                    call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(G.delta), ptr(G.do), D,
+                    self._call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(G.delta), ptr(G.do), D,
                          ptr(G.dqkv), 3 * D, nh, T, H, 64 ** -0.5, s)
-                    call("es_gemm_nt", EPI_DH, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D,
+                    self._call("es_gemm_nt", EPI_DH, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D,
                          None, ptr(G.dh), D, None, None, 0, Ml, D, 3 * D, 0, s)
                     self._wgrad(G.dqkv, 3 * D, h1, D, Ml, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"),
                                 lane=ln)
@@ -745,12 +768,12 @@ class Engine:
             with torch.cuda.stream(L["stream"]):
                 G = L["G"]
                 gv = lambda name, _g=L["grad"]: self.view(_g, name)  # noqa: E731
-                call("es_embed_bwd", ptr(L["dx"]), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")),
+                self._call("es_embed_bwd", ptr(L["dx"]), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")),
                      nh, T, D, 0, _lib.stream())
                 self._wgrad(G.dpatch, D, A.patches[L["p0"]:L["p0"] + Pl], K0, Pl, gv("patch_embed.proj.weight"),
                             gv("patch_embed.proj.bias"), lane=L["id"])
         main.wait_stream(side)
-        call("es_add_f32", ptr(grad), ptr(self._grad_b), grad.numel(), _lib.stream())
+        self._call("es_add_f32", ptr(grad), ptr(self._grad_b), grad.numel(), _lib.stream())
         return grad
 
 
@@ -781,6 +804,7 @@ class NativeViT(nn.Module):
         timm_init_(flat, self.cfg, self.layout, self.offs, generator=gen)
         self._set_flat(flat)
         self._engine = None
+        self.precision = "bf16"  # "fp32": parity mode (Engine.PARITY_NAMES)
         self.version = 0  # bumped whenever the fp32 master changes (bf16 images re-packed lazily)
 
     # parameters are views into one flat buffer --------------------------------------------
@@ -815,15 +839,25 @@ class NativeViT(nn.Module):
         other.cfg, other.layout, other.offs, other.numel = self.cfg, self.layout, self.offs, self.numel
         other._set_flat(self.flat.detach().clone())
         other._engine = None
+        other.precision = self.precision
         other.version = 0
         other.train(self.training)
         return other
+
+    def set_precision(self, precision):
+        """"bf16" (production: bf16 MFMA operands, fp32 accumulation / master weights) or "fp32"
+        (parity mode: every operand fp32, csrc/parity.hip)."""
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(precision)
+        if precision != self.precision:
+            self.precision, self._engine = precision, None
+        return self
 
     def engine(self):
         if self._engine is None or self._engine.device != self.flat.device:
             if not self.flat.is_cuda:
                 raise _lib.EndosslCallError("NativeViT runs on the MI355X only: move it to a cuda device first")
-            self._engine = Engine(self.cfg, self.flat.device)
+            self._engine = Engine(self.cfg, self.flat.device, precision=getattr(self, "precision", "bf16"))
         return self._engine
 
     @property

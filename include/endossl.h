@@ -273,6 +273,42 @@ int es_cast_f32_bf16(const float* x, void* y, long n, hipStream_t stream);
 // first (two-lane backward, endossl/vit.py Engine.backward); no reference counterpart (autograd accumulates).
 int es_add_f32(float* y, const float* x, long n, hipStream_t stream);
 
+/* ---- fp32 parity mode (csrc/parity.hip) --------------------------------------------------------
+ * The same arguments as the bf16 entry points above, with fp32 storage wherever those read or write
+ * bf16 (GEMM operands and epilogue outputs, qkv / attention output, LN output, patches, the packed
+ * weight images).  endossl/vit.py's Engine(precision="fp32") runs its one forward / backward sequence
+ * over these, so the 12-layer step is pinned to the fp32 oracle at 1e-3.  Same reference ops as the
+ * bf16 forms (code/models/conformer.py:13-72, timm PatchEmbed); GEMMs on fp32 MFMA, no shape
+ * restrictions beyond head dim 64 and T <= 1024 for attention, D % 64 == 0 for LayerNorm. */
+int es_gemm_nt_f32(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
+                   void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
+size_t es_gemm_tn_f32_workspace(int N1, int N2, int splits);
+int es_gemm_tn_f32(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
+                   float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream);
+int es_attn_fwd_f32(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
+                    hipStream_t stream);
+int es_attn_bwd_f32(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta,
+                    const void* dout, int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale,
+                    hipStream_t stream);
+int es_attn_cls_fwd_f32(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
+                        hipStream_t stream);
+int es_attn_cls_bwd_f32(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout,
+                        int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
+int es_layernorm_fwd_f32(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,
+                         float* rstd, int M, int D, float eps, hipStream_t stream);
+int es_layernorm_bwd_f32(const float* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
+                         const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
+                         float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
+                         hipStream_t stream);
+int es_patch_im2col_f32(const float* img, void* patches, int n, int S, int P, hipStream_t stream);
+int es_patch_im2col_u8_f32(const void* img, float mean0, float mean1, float mean2, float std0, float std1, float std2,
+                           void* patches, int n, int S, int P, hipStream_t stream);
+int es_embed_bwd_f32(const float* dx, int lddx, void* dpatch, int ldp, float* dpos, float* dcls, int n, int T, int D,
+                     int accumulate, hipStream_t stream);
+int es_pack_weights_f32(const float* flat, const void* entries, int nmat, hipStream_t stream);
+/* y = x, n fp32 values (the parity form of es_cast_f32_bf16) */
+int es_copy_f32(const float* x, void* y, long n, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

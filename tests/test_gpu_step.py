@@ -243,7 +243,10 @@ def test_full_size_step_properties():
     import pandas as pd
     from endossl.fixmatch import FixMatch
     from endossl.vit import NativeViT, ViTConfig
-    m = NativeViT(ViTConfig(), seed=0).to(DEV)
+    m = NativeViT(ViTConfig(), seed=0)
+    with torch.no_grad():  # a non-zero head (timm zero-inits it): informative weak logits
+        m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(1)))
+    m = m.to(DEV)
     B, MU = 64, 7
     g = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn(B, 3, 224, 224, device=DEV, generator=g)
@@ -260,11 +263,15 @@ def test_full_size_step_properties():
     df = pd.DataFrame({"target": np.arange(23).repeat(3)})
     tr = FixMatch(m, device=DEV)
     tr.get_dataloader((_DL([], df), _DL([])), None)
-    tr.get_config(_cfg(0.95, 1, B, MU, img=224))
+    # tau = the median weak max-prob: about half the pseudo-labels pass, so the strong branch carries
+    # a consistency gradient (at tau = 0.95 this random model masks every row out)
+    tau = float(torch.softmax(full, -1).max(-1).values.median()) + 1e-4
+    tr.get_config(_cfg(tau, 1, B, MU, img=224))
     w0 = m.flat.clone()
     out = tr.step(((x, y), ((uw, us), None)))
     torch.cuda.synchronize()
     assert torch.isfinite(out["loss"]).item()
+    assert 0.3 < out["mask_mean"].item() < 0.7 and out["lu"].item() > 0
     assert torch.isfinite(m.flat_grad).all().item()
     assert float(m.flat_grad.abs().sum()) > 0
     step = (m.flat - w0).abs()
