@@ -1,30 +1,33 @@
 """Benchmark: unlabeled images/sec of the FixMatch ViT-S/16 SSL step (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling strong|weak]
   (N>1: launched by torch.distributed.run, one rank per GPU, RCCL over xGMI)
 
-Workload F1 (BASELINE configs[1]): FixMatch, ViT-Small/16, B=64 labeled + mu*B = 448 unlabeled
-weak/strong pairs per rank, 224x224x3, 23 classes, bf16 MFMA compute with fp32 master weights.
-Synthetic, HBM-resident inputs (seed 0): uint8 pixels whose ToTensor + ImageNet Normalize
-(code/dataset.py:21-22,49-51) run inside the patch gather (--inputs f32: host-normalised fp32 images).
-Weak scaling: every rank runs the full F1 batch; the gradient all-reduce is the only exchange.
-One step = weak forward (448) + train forward/backward (64+448) + fused losses + grad
-all-reduce + Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.
+Workload F1 (BASELINE configs[1]; configs[2] at N > 1): FixMatch, ViT-Small/16, global batch B=64
+labeled + mu*B = 448 unlabeled weak/strong pairs, 224x224x3, 23 classes, bf16 MFMA compute with
+fp32 master weights.  Synthetic, HBM-resident inputs (seed 0): uint8 pixels whose ToTensor +
+ImageNet Normalize (code/dataset.py:21-22,49-51) run inside the patch gather (--inputs f32:
+host-normalised fp32 images).
+Scaling (north_star / SURVEY.md §8(e)): "strong" (default) shards the global batch over the N ranks
+(64/N labeled + 448/N pairs per GPU: the DDP average of per-rank means is the global-batch gradient);
+"weak" gives every rank the full F1 batch.  The flat fp32 gradient's RCCL all-reduce is the only
+exchange.  One step = weak forward + train forward/backward + fused losses + grad all-reduce +
+Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.  The forward/backward runs as one
+captured hipGraph (FixMatch.use_graph) except where the live roofline probe needs eager launches.
 
 Reported beside it:
-  roofline      dominant kernel = the fc1 forward GEMM (gemm_nt, GELU epilogue keeping GELU' for the
-                backward), timed live with HIP events on its launch stream over the timed steps (where it
-                shares the chip with the weak forward on the second stream; "isolated" = the same launch
-                with that stream off).  Its binding roofline is HBM:
-                698.4 MB algorithmic bytes per launch (A [M,384] bf16 read once + GELU'(pre) and
-                activation [M,1536] bf16 written once) take 87 us at 8 TB/s, its 119 GFLOP 47 us at
-                the bf16 dense MFMA peak.  achieved = algorithmic bytes / mean launch time; the MFMA
-                view (algorithmic FLOP / time vs 2516.6 TFLOP/s) is reported beside it.
+  roofline      the dominant kernel (the most GPU time per step: rocprofv3, profiles/r02*_summary.md)
+                = the weight-gradient GEMM gemm_tn (es_gemm_tn: TN kernel + split-K reduction), timed
+                live with HIP events on its launch stream (the side stream of the backward) at the
+                fc1 weight-gradient site: algorithmic 2*M*1536*384 FLOP per launch (M = train tokens)
+                vs the bf16 dense MFMA peak 2516.6 TFLOP/s.  traffic = HBM bytes per launch from the
+                committed rocprofv3 --pmc summary (profiles/pmc_traffic.json).
   step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.  The engine skips
                 the last block's non-CLS rows after its qkv GEMM (their outputs never reach the head;
                 Engine.PRUNE_LAST), so it executes fewer FLOPs than that: `executed_step_tflop`.
   cpu_baseline  the oracle (CPU fp32 restatement pinned to the reference, kind "port") timed on a
-                bounded sample (B=8, mu=7: 56 unlabeled images/step) on the host cores, rank 0, N=1.
+                bounded sample (B=8, mu=7: 56 unlabeled images/step) with torch.set_num_threads(
+                os.cpu_count()) on the host, rank 0, N=1.
 """
 import argparse
 import json
@@ -71,9 +74,10 @@ def synth_images(n, size, gen, device):
 
 
 def cpu_baseline(B=8, MU=7, steps=2):
-    """Oracle (pinned CPU restatement) FixMatch step on the host cores -- a reported baseline."""
+    """Oracle (pinned CPU restatement) FixMatch step on every host core -- a reported baseline."""
     from oracle import ref
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16")))
+    threads = os.cpu_count() or 1
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     cfg = ref.Cfg()
     params = ref.random_params(cfg, seed=0)
@@ -88,6 +92,8 @@ def cpu_baseline(B=8, MU=7, steps=2):
     for _ in range(steps):
         fm.step(x, y, uw, us)
     dt = (time.perf_counter() - t0) / steps
+    used = torch.get_num_threads()
+    torch.set_num_threads(prev)
     cpu = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -96,10 +102,11 @@ def cpu_baseline(B=8, MU=7, steps=2):
                 break
     except OSError:
         pass
-    return {"value": round(B * MU / dt, 3), "unit": "unlabeled images/s", "cores": torch.get_num_threads(),
+    return {"value": round(B * MU / dt, 3), "unit": "unlabeled images/s", "cores": used,
             "kind": "port",
             "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step), "
-                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', os.cpu_count()={os.cpu_count()}"}
+                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', os.cpu_count()={os.cpu_count()}, "
+                      f"torch.get_num_threads()={used}"}
 
 
 def pmc_traffic(kernel_substr):
@@ -155,6 +162,7 @@ def run_secondary(args):
     from endossl import dist
     from endossl.utils import AttrDict
     rank, world, local = dist.init_from_env()
+    _check_world(args, world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
@@ -233,18 +241,29 @@ def run_secondary(args):
     dist.barrier()
 
 
+def _check_world(args, world):
+    if args.gpus != world:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 under "
+                         f"`python -m torch.distributed.run --nproc-per-node {args.gpus} ... bench.py --gpus "
+                         f"{args.gpus}` (one rank per GPU)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=64, help="global labeled batch B (strong) / per-GPU B (weak)")
     ap.add_argument("--mu", type=int, default=7)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inputs", choices=("u8", "f32"), default="u8",
                     help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")
     ap.add_argument("--workload", choices=("f1", "c1", "s1"), default="f1",
                     help="f1 = the BASELINE metric (default); c1 / s1 = CoMatch / SemiFormer configs")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="hipGraph replay of the step's forward/backward (auto: on for N > 1; at N = 1 the "
+                         "timed steps run eagerly so the roofline probe's HIP events see every launch)")
     args = ap.parse_args()
     if args.workload != "f1":
         return run_secondary(args)
@@ -255,11 +274,19 @@ def main():
     from endossl.vit import Engine, NativeViT, ViTConfig
 
     rank, world, local = dist.init_from_env()
+    _check_world(args, world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    B, MU = args.batch, args.mu
+    if args.scaling == "strong":
+        if args.batch % world:
+            raise SystemExit(f"strong scaling shards B={args.batch} over {world} ranks: B % N must be 0")
+        B, MU = args.batch // world, args.mu  # this rank's shard: B/N labeled + mu*B/N pairs
+    else:
+        B, MU = args.batch, args.mu
     model = NativeViT(ViTConfig(), seed=0)
     tr = FixMatch(model, device=dev)
+    graph = args.graph == "on" or (args.graph == "auto" and world > 1)
+    tr.use_graph = graph
     cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
                    MODEL=AttrDict(NAME="vit_small_patch16_224", NUM_CLASSES=23),
                    TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=1,
@@ -282,10 +309,13 @@ def main():
 
     for _ in range(args.warmup):
         tr.step(batch)
-    torch.cuda.synchronize()
-    dist.barrier()
-    probe = {"label": "fc1_fwd", "events": []}
-    model.engine().probe = probe
+    if graph and tr.static_batch() is not None:
+        batch = tr.static_batch()  # the graph's own input buffers already hold this batch: no copy per step
+    eng = model.engine()
+    probe = {"label": "fc1_wgrad", "events": []}
+    live = not graph  # HIP events bracket eager launches only
+    if live:
+        eng.probe = probe
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
@@ -294,75 +324,80 @@ def main():
     torch.cuda.synchronize()
     dist.barrier()
     t1 = time.perf_counter()
-    model.engine().probe = None
+    eng.probe = None
     elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
     T = elapsed.item()
     loss = out["loss"].item()
 
-    # the same launches with the second stream off (untimed, after the timed region): the kernel's
-    # duration when it has the chip to itself, reported beside the live (co-scheduled) figure
-    eng = model.engine()
+    # untimed steps after the timed region: the probed launch with the second stream off ("isolated"),
+    # and, when the timed steps replayed a graph, the same launch co-scheduled as in the step
+    use_graph, tr.use_graph = tr.use_graph, False
+    if not live:
+        eng.probe = probe
+        for _ in range(2):
+            tr.step(batch)
+        torch.cuda.synchronize()
     ov = (eng.overlap, eng.overlap_fwd)
     eng.overlap = eng.overlap_fwd = False
-    iso = {"label": "fc1_fwd", "events": []}
+    iso = {"label": "fc1_wgrad", "events": []}
     eng.probe = iso
     for _ in range(2):
         tr.step(batch)
     torch.cuda.synchronize()
     eng.probe = None
     eng.overlap, eng.overlap_fwd = ov
+    tr.use_graph = use_graph
     iso_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / len(iso["events"])
-
     ev_ms = [e0.elapsed_time(e1) for e0, e1, _ in probe["events"]]
-    flops = [f for _, _, f in probe["events"]]
+    flop = probe["events"][0][2]
     mean_ms = sum(ev_ms) / len(ev_ms)
-    tflops = sum(flops) / (sum(ev_ms) / 1e3) / 1e12  # TFLOP/s over the probed launches
-    M_tok, N_hid, K_dim = B * (1 + MU) * 197, 1536, 384
-    # A read + pre/act written (bf16) + weight image and bias read once
-    alg_bytes = 2 * M_tok * K_dim + 2 * 2 * M_tok * N_hid + 2 * N_hid * K_dim + 4 * N_hid
-    gbs = alg_bytes / (mean_ms / 1e3) / 1e9
-    gelu_d = model.engine().GELU_D
-    traffic = pmc_traffic("gemm_nt_kernel<7," if gelu_d else "gemm_nt_kernel<1,")
+    tflops = flop / (mean_ms / 1e3) / 1e12
+    M_tok = B * (1 + MU) * 197
+    traffic = pmc_traffic("gemm_tn")
+    lib = __import__("endossl._lib", fromlist=["load"]).load()
+    tn_ws = lib.es_gemm_tn_workspace(1536, 384, 0)
 
     if rank == 0:
         ms = T / args.steps * 1e3
+        glob_unl = world * B * MU  # unlabeled images the whole job processed per step
+        work = STEP_TFLOP_F1 * glob_unl / 448.0
         res = {
             "metric": "unlabeled images/sec/node (FixMatch ViT-S, 224², μ=7)",
-            "value": round(world * B * MU * args.steps / T, 2),
+            "value": round(glob_unl * args.steps / T, 2),
             "unit": "unlabeled images/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None,
             "dtype": "bf16", "data": ("synthetic (HBM-resident uint8 pixels, ImageNet normalisation fused into the "
                                       "patch gather, seed 0)" if args.inputs == "u8" else
                                       "synthetic (HBM-resident uint8->ImageNet-normalised fp32, seed 0)"),
-            "config": {"workload": f"F1: FixMatch ViT-S/16 step, B={B} labeled + mu*B={B * MU} unlabeled "
-                                   f"weak/strong pairs per GPU, 224^2, C=23, tau=0.95, lambda_u=1, Adam 1e-3, "
-                                   f"EMA 0.999", "global_batch": world * B * (1 + 2 * MU), "seq_len": 197,
-                       "parallelism": f"dp{world}"},
-            "step_tflops": round(STEP_TFLOP_F1 / (ms / 1e3), 1),
-            "step_mfma_frac": round(STEP_TFLOP_F1 / (ms / 1e3) / PEAK_BF16_TFLOPS, 4),
-            "executed_step_tflop": round(STEP_TFLOP_F1 - (vit_s_pruned_tflop(B * (1 + 2 * MU), B * (1 + MU))
-                                                          if Engine.PRUNE_LAST and Engine.LANES != 2 else 0.0), 3),
+            "config": {"workload": f"F1: FixMatch ViT-S/16 step, global B={world * B} labeled + mu*B={glob_unl} "
+                                   f"unlabeled weak/strong pairs ({B} + {B * MU} per GPU, {args.scaling} scaling), "
+                                   f"224^2, C=23, tau=0.95, lambda_u=1, Adam 1e-3, EMA 0.999",
+                       "global_batch": world * B * (1 + 2 * MU), "seq_len": 197, "parallelism": f"dp{world}",
+                       "hipgraph": bool(graph)},
+            "step_tflops": round(work / (ms / 1e3), 1),
+            "step_mfma_frac": round(work / (ms / 1e3) / PEAK_BF16_TFLOPS / world, 4),
+            "executed_step_tflop": round((STEP_TFLOP_F1 - (vit_s_pruned_tflop(448 + 512, 512)
+                                                           if Engine.PRUNE_LAST and Engine.LANES != 2 else 0.0))
+                                         * glob_unl / 448.0, 3),
             "final_loss": round(loss, 6),
-            "roofline": {"kernel": (f"gemm_nt_kernel<EPI_GELU_D> (train fc1 forward: M={M_tok}, N=1536, K=384, "
-                                    "bias + exact-GELU epilogue writing GELU'(pre) and the activation, bf16)")
-                         if gelu_d else
-                         (f"gemm_nt_kernel<EPI_GELU> (train fc1 forward: M={M_tok}, N=1536, K=384, "
-                          "bias + exact-GELU epilogue writing pre-activation and activation, bf16)"),
-                         "bound": "hbm", "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": round(gbs / PEAK_HBM_GBS, 4), "traffic": traffic,
-                         "algorithmic_bytes": alg_bytes, "mean_launch_ms": round(mean_ms, 4),
-                         "launches": len(ev_ms), "mfma_tflops": round(tflops, 1),
-                         "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
-                         "streams": 2 if ov[1] else 1,
+            "roofline": {"kernel": (f"es_gemm_tn (weight gradient, fc1 site: out[1536, 384] = dY^T X over M={M_tok} "
+                                    "train tokens, bf16 operands, fp32 split-K slabs + reduction, fused bias "
+                                    "gradient); rocprofv3: gemm_tn_big_kernel + splitk_reduce_kernel"),
+                         "bound": "mfma", "achieved": round(tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
+                         "unit": "TFLOP/s", "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "algorithmic_flop": flop, "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms),
+                         "timed": "live in the timed steps" if live else "2 untimed eager steps after the timed "
+                                                                         "(graph-replayed) steps",
+                         "streams": 2 if ov[0] else 1, "tn_workspace_floats": int(tn_ws),
                          "isolated": {"mean_launch_ms": round(iso_ms, 4),
-                                      "achieved": round(alg_bytes / (iso_ms / 1e3) / 1e9, 1),
-                                      "frac": round(alg_bytes / (iso_ms / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
-                                      "note": "same launch with the second HIP stream off (2 untimed steps); the "
-                                              "live figure above shares the CUs with the weak-forward stream"}},
+                                      "achieved": round(flop / (iso_ms / 1e3) / 1e12, 1),
+                                      "frac": round(flop / (iso_ms / 1e3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                                      "note": "same launch with the engine's second HIP stream off (2 untimed "
+                                              "steps): the live figure shares the CUs with the data-gradient chain"}},
         }
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline()

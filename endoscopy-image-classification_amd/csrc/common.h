@@ -177,9 +177,28 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
-// Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).
+// Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).  Set once per kernel
+// and size (a per-function attribute, remembered per kernel address): the launchers then issue no
+// host-side runtime call beyond the launch itself, which keeps them capturable into a hipGraph
+// (endossl/fixmatch.py).
+inline bool lds_grant_needed(const void* kernel, size_t bytes) {
+  static const void* ks[256];
+  static size_t bs[256];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (ks[i] == kernel) {
+      if (bs[i] >= bytes) return false;
+      bs[i] = bytes;
+      return true;
+    }
+  if (n < 256) {
+    ks[n] = kernel;
+    bs[n++] = bytes;
+  }
+  return true;
+}
 template <typename K>
 inline void allow_lds(K kernel, size_t bytes) {
-  if (bytes > 65536)
+  if (bytes > 65536 && lds_grant_needed((const void*)kernel, bytes))
     (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }

@@ -667,6 +667,143 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(TNArgs p) {
   }
 }
 
+// ---- weight gradient on a 384 x 192 output tile (N1 x N2) per 8-wave workgroup -----------------
+// The 128x128 kernel above brings 16 KiB into LDS per 32-token step for 1 MFLOP: at 64 FLOP/B the
+// L2 -> LDS stream, not the matrix cores, sets its pace (rocprofv3: 63 % of wave cycles parked in
+// s_waitcnt, no LDS bank conflicts).  Here a workgroup owns a 384 (N1, from A1 = dY) x 192 (N2,
+// from A2 = X) tile -- 128 FLOP/B -- as 8 waves of 96 x 96 (4 along N1 x 2 along N2), each 6 x 6
+// v_mfma_f32_16x16x32_bf16 per 32 tokens from 12 A2 + 12 A1 transposed fragment reads (0.67
+// ds_read_b64_tr_b16 per MFMA, was 1.0).  Every ViT-S / ViT-B Linear satisfies N1 % 384 == 0 and
+// N2 % 192 == 0.  Operand rows are 768 B (A1) and 384 B (A2) of 16-B chunks, written by LDS-DMA
+// pieces that cross rows; conflict-free transposed reads via source-side XOR swizzles:
+//   A1 (row stride = 0 mod 64 banks): chunk c of row r at c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3))
+//   A2 (row stride = 32 mod 64 banks: odd rows shift by half the banks):
+//                                     chunk c of row r at c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2))
+// The bias gradient (column sums of A1) rides on the matrix cores: the N2-tile-0 workgroups' w2 = 0
+// waves issue one extra MFMA per A1 fragment against an all-ones A operand.
+constexpr int TB1 = 384, TB2 = 192;
+__device__ __forceinline__ int swz384(int r, int c) { return c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2)); }
+
+template <int BKM, int NST>
+__global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int R1B = TB1 * 2, R2B = TB2 * 2;          // LDS row bytes: 768, 384
+  constexpr int C1 = R1B / 16, C2 = R2B / 16;           // 16-B chunks per row: 48, 24
+  constexpr int T1B = BKM * R1B, T2B = BKM * R2B;
+  constexpr int STAGE = T1B + T2B;
+  constexpr int F1 = T1B / 1024 / 8;                    // full 1-KiB pieces per wave, A1
+  constexpr int F2 = T2B / 1024 / 8;                    // ... A2
+  constexpr int H2 = ((T2B / 1024) % 8) ? 1 : 0;        // plus one half piece (lanes 0..31)
+  static_assert((T1B / 1024) % 8 == 0 && ((T2B / 1024) % 8 == 0 || (T2B / 1024) % 8 == 4), "pieces");
+  constexpr int PER = F1 + F2 + H2;
+  const int nt2 = p.N2 / TB2, ntiles = (p.N1 / TB1) * nt2;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / ntiles, tile = wg - split * ntiles;
+  const int n1_0 = (tile / nt2) * TB1, n2_0 = (tile % nt2) * TB2;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int w1 = w >> 1, w2 = w & 1;
+  const bool do_bias = p.PB != nullptr && (tile % nt2) == 0 && w2 == 0;
+  const int mbeg = split * p.mchunk;
+  const int mend = min(mbeg + p.mchunk, (p.M + BKM - 1) / BKM * BKM);
+  const int g = lane >> 4, t = lane & 15, q = t >> 2, p4 = t & 3;
+
+  // per-lane byte offsets of the DMA sources within one token step (row-major tile, swizzled chunk)
+  unsigned o1[F1], o2[F2 + H2];
+#pragma unroll
+  for (int j = 0; j < F1; ++j) {
+    const int L = (j * 8 + w) * 64 + lane, row = L / C1;
+    o1[j] = (unsigned)row * p.ld1 * 2u + (unsigned)swz256(row, L - row * C1) * 16u;
+  }
+#pragma unroll
+  for (int j = 0; j < F2 + H2; ++j) {
+    const int L = j < F2 ? (j * 8 + w) * 64 + lane : F2 * 512 + w * 32 + (lane & 31), row = L / C2;
+    o2[j] = (unsigned)row * p.ld2 * 2u + (unsigned)swz384(row, L - row * C2) * 16u;
+  }
+  const char* b1 = (const char*)(p.A1 + (size_t)mbeg * p.ld1 + n1_0);
+  const char* b2 = (const char*)(p.A2 + (size_t)mbeg * p.ld2 + n2_0);
+  const size_t s1 = (size_t)BKM * p.ld1 * 2, s2 = (size_t)BKM * p.ld2 * 2;
+#define TNB_ISSUE(BUF, KT)                                                                       \
+  {                                                                                              \
+    char* S_ = smem + (BUF) * STAGE;                                                             \
+    const char* x1 = b1 + (size_t)(KT) * s1;                                                     \
+    const char* x2 = b2 + (size_t)(KT) * s2;                                                     \
+    _Pragma("unroll") for (int j = 0; j < F1; ++j) glds16(x1 + o1[j], S_ + (j * 8 + w) * 1024);  \
+    _Pragma("unroll") for (int j = 0; j < F2; ++j) glds16(x2 + o2[j], S_ + T1B + (j * 8 + w) * 1024); \
+    if constexpr (H2) {                                                                          \
+      if (lane < 32) glds16(x2 + o2[F2], S_ + T1B + F2 * 8192 + w * 512);                        \
+    }                                                                                            \
+  }
+
+  f32x4 acc[6][6], bacc[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ones[i] = (bf16)1.0f;
+
+  const int nk = (mend - mbeg) / BKM;
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) TNB_ISSUE(st, st)
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_vmcnt(min(NST - 2, nk - 1 - kt) * PER);
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nk) {
+      int nb = buf + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
+      TNB_ISSUE(nb, kt + NST - 1)
+    }
+    const char* T1 = smem + buf * STAGE;
+    const char* T2 = T1 + T1B;
+#pragma unroll
+    for (int hh = 0; hh < BKM / 32; ++hh) {
+      const int r1 = hh * 32 + 8 * g + q, r2 = r1 + 4;
+      const int off = (p4 & 1) * 8;
+      bf16x8 bfr[6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int cb = (w1 * 96 + i * 16) / 8 + (p4 >> 1);
+        bfr[i] = cat8(lds_tr4(T1 + r1 * R1B + swz256(r1, cb) * 16 + off),
+                      lds_tr4(T1 + r2 * R1B + swz256(r2, cb) * 16 + off));
+      }
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) bacc[i] = mfma16(ones, bfr[i], bacc[i]);
+      }
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const int ca = (w2 * 96 + a * 16) / 8 + (p4 >> 1);
+        const bf16x8 af = cat8(lds_tr4(T2 + r1 * R2B + swz384(r1, ca) * 16 + off),
+                               lds_tr4(T2 + r2 * R2B + swz384(r2, ca) * 16 + off));
+#pragma unroll
+        for (int i = 0; i < 6; ++i) acc[a][i] = mfma16(af, bfr[i], acc[a][i]);
+      }
+    }
+    buf = buf + 1 == NST ? 0 : buf + 1;
+  }
+#undef TNB_ISSUE
+  // lane holds D[n2 = .. + 4g + e][n1 = .. + t]  ->  P[split][n1][n2 .. n2+3]
+  float* P = p.P + (size_t)split * p.N1 * p.N2;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int n1 = n1_0 + w1 * 96 + i * 16 + t;
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      const int n2 = n2_0 + w2 * 96 + a * 16 + 4 * g;
+      *(f32x4*)(P + (size_t)n1 * p.N2 + n2) = acc[a][i];
+    }
+  }
+  if (do_bias && g == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) p.PB[(size_t)split * p.N1 + n1_0 + w1 * 96 + i * 16 + t] = bacc[i][0];
+  }
+}
+
 // out[i] = (accumulate ? out[i] : 0) + sum_s P[s][i]   (n % 4 == 0); 4 independent partial sums
 // per thread keep 4 slab loads in flight.
 __global__ void splitk_reduce_kernel(const float* __restrict__ P, float* __restrict__ out, int S, int n,
@@ -913,37 +1050,83 @@ int es_set_gemm_variant(int v) {
   return old;
 }
 
-// Tuning knob for es_gemm_tn: -1 = default, 0..4 = (token step, ring depth) in
-// {32x2, 32x3, 32x4, 64x2, 64x3}.  Returns the previous value.
+// Tuning knob for es_gemm_tn: -1 = default, 0..4 = 128x128 tile with (token step, ring depth) in
+// {32x2, 32x3, 32x4, 64x2, 64x3}, 5..7 = 384x192 tile with 32x2, 32x3, 64x2 (shapes that do not
+// tile fall back to 0).  Returns the previous value.
 int es_set_tn_variant(int v) {
   const int old = g_tn_variant;
   g_tn_variant = v;
   return old;
 }
 
-// workspace floats needed by es_gemm_tn for `splits` splits (slabs + bias partials)
-size_t es_gemm_tn_workspace(int N1, int N2, int splits) { return (size_t)splits * N1 * N2 + (size_t)splits * N1; }
+// es_gemm_tn kernel choice and split-K sizing (splits <= 0: auto).  Kernels: 0..4 the 128 x 128
+// four-wave tile, 5..8 the 384 x 192 eight-wave tile (where the shape tiles).  Auto: the big tile
+// for long token axes (M >= 65536: 15-25 % faster alone at the F1 shapes, scripts/gemm_bench.py),
+// the 128 x 128 tile below that (more tiles to spread a short axis over).  Splits: enough
+// workgroups to fill the chip (target), but at least TN_MIN_SPLIT_TOKENS tokens per split -- each
+// split writes and the reduction re-reads a full fp32 N1 x N2 slab.  Measured at a per-GPU shard of
+// 64 images (M = 12,608, scripts/gemm_bench.py --m-train): 16-24 splits of the 128 x 128 kernel are
+// fastest (fc1 / fc2 / qkv / proj weight gradients 44 / 44 / 38 / 28 us; 64 splits of the big tile
+// 48 + 26 us of reduction; 4 splits 108 us).
+constexpr int TN_MIN_SPLIT_TOKENS = 512;
+static bool tn_big_ok(int N1, int N2, int ld1, int ld2) {
+  return N1 % TB1 == 0 && N2 % TB2 == 0 && ld1 % 8 == 0 && ld2 % 8 == 0;
+}
+static int tn_pick(int M, int N1, int N2, int ld1, int ld2) {
+  const int v = g_tn_variant;
+  if (!(N1 % BM == 0 && N2 % BN == 0)) return 7;  // only the big tile covers N2 = 192 (caller checked)
+  if (v >= 5 && v <= 8) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
+  if (v >= 0) return v;
+  return (tn_big_ok(N1, N2, ld1, ld2) && M >= 65536) ? 7 : 0;
+}
+static int tn_target(int v) { return v == 5 ? 512 : (v >= 6 ? 256 : 768); }
+static int tn_tiles(int v, int N1, int N2) { return v >= 5 ? (N1 / TB1) * (N2 / TB2) : (N1 / BM) * (N2 / BN); }
+static int tn_auto_splits(int v, int M, int N1, int N2) {
+  const int by_fill = std::max(1, tn_target(v) / tn_tiles(v, N1, N2));
+  const int by_len = std::max(1, M / TN_MIN_SPLIT_TOKENS);
+  return std::min(by_fill, by_len);
+}
+
+// workspace floats needed by es_gemm_tn for `splits` splits (slabs + bias partials); splits <= 0:
+// the most any kernel choice's automatic split count can use
+size_t es_gemm_tn_workspace(int N1, int N2, int splits) {
+  if (splits <= 0) {
+    splits = std::max(1, 768 / std::max(1, (N1 / BM) * (N2 / BN)));
+    if (N1 % TB1 == 0 && N2 % TB2 == 0) splits = std::max(splits, 512 / std::max(1, (N1 / TB1) * (N2 / TB2)));
+  }
+  return (size_t)splits * N1 * N2 + (size_t)splits * N1;
+}
 
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream) {
-  if (M <= 0 || (N1 % BM) || (N2 % BN) || splits <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
+  if (M <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
+  if (!tn_big_ok(N1, N2, ld1, ld2) && ((N1 % BM) || (N2 % BN))) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
-  // variant: token step BKM and ring depth NST (0 = 32x2, 1 = 32x3, 2 = 32x4, 3 = 64x2, 4 = 64x3)
-  const int v = g_tn_variant < 0 ? 0 : g_tn_variant;  // 32x2 measured fastest (deeper rings cost occupancy)
-  const int BKM = v >= 3 ? 64 : 32;
+  // variant: 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3;
+  // 5..7 = 384x192 tile with 32x2 (72 KiB: two workgroups per CU), 32x3, 64x2
+  const int v = tn_pick(M, N1, N2, ld1, ld2);
+  const int BKM = (v == 3 || v == 4 || v == 7) ? 64 : 32;  // (8: 384x192, 32x4)
   const int msteps = (M + BKM - 1) / BKM;
+  if (splits <= 0) splits = tn_auto_splits(v, M, N1, N2);
+  splits = std::min(splits, msteps);
   const int per = (msteps + splits - 1) / splits;
   const int S = (msteps + per - 1) / per;
   const bool direct = (S == 1 && !accumulate);
   float* P = direct ? out : workspace;
   float* PB = bias_out ? workspace + (size_t)S * N1 * N2 : nullptr;
   TNArgs a{(const bf16*)A1, (const bf16*)A2, P, PB, M, N1, N2, ld1, ld2, per * BKM};
-  const int grid = S * (N1 / BM) * (N2 / BN);
+  const int grid = S * tn_tiles(v, N1, N2);
 #define TN_LAUNCH(BKM_, NST_)                                                                           \
   {                                                                                                   \
     const size_t lds = (size_t)NST_ * 2 * BKM_ * BM * 2;                                              \
     allow_lds(gemm_tn_kernel<BKM_, NST_>, lds);                                                       \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_kernel<BKM_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
+  }
+#define TNB_LAUNCH(BKM_, NST_)                                                                          \
+  {                                                                                                   \
+    const size_t lds = (size_t)NST_ * BKM_ * (TB1 + TB2) * 2;                                         \
+    allow_lds(gemm_tn_big_kernel<BKM_, NST_>, lds);                                                   \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_kernel<BKM_, NST_>), dim3(grid), dim3(512), lds, stream, a); \
   }
   switch (v) {
     case 0: TN_LAUNCH(32, 2) break;
@@ -951,9 +1134,14 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
     case 3: TN_LAUNCH(64, 2) break;
     case 4: TN_LAUNCH(64, 3) break;
     case 2: TN_LAUNCH(32, 4) break;
+    case 5: TNB_LAUNCH(32, 2) break;
+    case 6: TNB_LAUNCH(32, 3) break;
+    case 7: TNB_LAUNCH(64, 2) break;
+    case 8: TNB_LAUNCH(32, 4) break;
     default: TN_LAUNCH(32, 2) break;
   }
 #undef TN_LAUNCH
+#undef TNB_LAUNCH
   if (!direct) {
     const int n = N1 * N2;
     int rg = (n / 4 + 255) / 256;

@@ -249,8 +249,8 @@ class _Map:
 
 
 def _tn_splits(M, N1, N2):
-    tiles = (N1 // 128) * (N2 // 128)
-    return max(1, min((M + 31) // 32, 128, 768 // tiles))  # Engine.TN_TARGET_BLOCKS (floor: see there)
+    """0: es_gemm_tn sizes the split-K for the kernel it picks (as the ViT engine, Engine._tn_splits)."""
+    return 0
 
 
 class _ConvFn(torch.autograd.Function):

@@ -83,18 +83,21 @@ class FixMatch:
             self.class_weights = None
 
     # ------------------------------------------------------------------ the hot step
-    def step(self, batch):
-        """batch = ((x, y), ((u_w, u_s), idx)) -> dict of device scalars / tensors."""
-        (inputs_x, targets_x), ((inputs_u_w, inputs_u_s), _) = batch
-        dev = self.model.flat.device
-        inputs_x = inputs_x.to(dev, non_blocking=True)
-        targets_x = targets_x.to(dev, non_blocking=True).to(torch.int64)
-        inputs_u_w = inputs_u_w.to(dev, non_blocking=True)
-        inputs_u_s = inputs_u_s.to(dev, non_blocking=True)
+    # The forward / losses / backward of a step as one hipGraph (torch.cuda.CUDAGraph over the C-ABI
+    # launches, both HIP streams): ~600 kernel launches replayed without the host walking the
+    # engine, which matters once a rank's share of the batch is small (strong scaling: 8 + 56 pairs
+    # per GPU at N = 8).  Captured on the first step of a shape after one eager step; inputs are
+    # copied into the graph's own static buffers (static_batch() hands them out for zero-copy use).
+    # The optimizer, the all-reduce and the LR schedule stay outside (their scalars change per step).
+    # ENDOSSL_GRAPH=0 runs everything eagerly.
+    use_graph = os.environ.get("ENDOSSL_GRAPH", "1") == "1"
+
+    def _compute(self, inputs_x, targets_x, inputs_u_w, inputs_u_s):
+        """Weak forward, train forward, fused losses, backward into model.flat_grad (no host sync)."""
         cfg = self.config
         m = self.model
         eng = m.engine()
-        eng.pack(m.flat, m.version)
+        dev = m.flat.device
         B, nu = int(inputs_x.shape[0]), int(inputs_u_w.shape[0])
         C = m.cfg.num_classes
         s = _lib.stream()
@@ -103,7 +106,6 @@ class FixMatch:
             self._pl = torch.empty(nu, dtype=torch.int32, device=dev)
             self._mask = torch.empty(nu, dtype=torch.uint8, device=dev)
         stats = torch.empty(4, dtype=torch.float32, device=dev)  # lx, lu, mask_mean, total
-
         if eng.overlap_fwd:  # weak forward on the side stream, beside the train forward
             main, side = torch.cuda.current_stream(dev), eng.side_stream()
             side.wait_stream(main)
@@ -123,6 +125,50 @@ class FixMatch:
         torch.add(stats[0], stats[1], alpha=lam, out=stats[3])
         gb = dist.GradBuckets(m.flat_grad) if dist.world_size() > 1 and self.overlap_allreduce else None
         eng.backward(m.flat, m.flat_grad, dl, grad_ready=gb.ready if gb is not None else None)
+        return stats, gb
+
+    def _graphable(self):
+        eng = self.model.engine()
+        return (self.use_graph and eng.probe is None and not (dist.world_size() > 1 and self.overlap_allreduce))
+
+    def static_batch(self):
+        """The captured graph's input buffers as a batch (fill them in place to skip the copy)."""
+        if getattr(self, "_graph", None) is None:
+            return None
+        x, y, uw, us = self._gin
+        return ((x, y), ((uw, us), None))
+
+    def _run_graph(self, inputs):
+        key = tuple((tuple(t.shape), t.dtype) for t in inputs)
+        if getattr(self, "_graph", None) is None or self._gkey != key:
+            self._graph = None
+            stats, _ = self._compute(*inputs)  # eager step (warms every launch path on this shape)
+            gin = [t.clone() for t in inputs]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                gstats, _ = self._compute(*gin)
+            self._graph, self._gkey, self._gin, self._gstats = g, key, gin, gstats
+            return stats
+        for dst, src in zip(self._gin, inputs):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src, non_blocking=True)
+        self._graph.replay()
+        return self._gstats
+
+    def step(self, batch):
+        """batch = ((x, y), ((u_w, u_s), idx)) -> dict of device scalars / tensors."""
+        (inputs_x, targets_x), ((inputs_u_w, inputs_u_s), _) = batch
+        dev = self.model.flat.device
+        inputs = (inputs_x.to(dev, non_blocking=True), targets_x.to(dev, non_blocking=True).to(torch.int64),
+                  inputs_u_w.to(dev, non_blocking=True), inputs_u_s.to(dev, non_blocking=True))
+        m = self.model
+        eng = m.engine()
+        eng.pack(m.flat, m.version)
+        gb = None
+        if self._graphable():
+            stats = self._run_graph(inputs)
+        else:
+            stats, gb = self._compute(*inputs)
         gscale = gb.finish() if gb is not None else dist.allreduce_sum_(m.flat_grad)
         ema = self.ema_model
         self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,

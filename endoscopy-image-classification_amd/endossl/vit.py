@@ -221,6 +221,7 @@ class Engine:
     # chain on the other stream, 768 leaves the chain room: 35.10-35.13 ms/step vs 35.41-35.43 (1024),
     # 35.39 (640), 35.99 (512); C1 prefers 1024 (73.9 vs 74.2 ms).  The split count is capped so the
     # slabs stay small for the 384x384 projection.
+    TN_TARGET_SET = "ENDOSSL_TN_TARGET" in os.environ
     TN_TARGET_BLOCKS = int(os.environ.get("ENDOSSL_TN_TARGET", "768"))
     TN_CEIL = os.environ.get("ENDOSSL_TN_CEIL", "0") == "1"  # A/B knob: the earlier ceil sizing
     TN_MAX_SPLITS = 128
@@ -522,20 +523,33 @@ class Engine:
 
     # -------------------------------------------------------------- backward
     def _tn_splits(self, M, N1, N2):
+        """0 = the library's automatic split-K sizing for the kernel it picks (es_gemm_tn); with
+        ENDOSSL_TN_TARGET set, floor(target / 128x128 tiles) splits (the round-1 sizing)."""
+        if not self.TN_TARGET_SET:
+            return 0
         tiles = (N1 // 128) * (N2 // 128)
         msteps = (M + 31) // 32
         sp = -(-self.TN_TARGET_BLOCKS // tiles) if self.TN_CEIL else self.TN_TARGET_BLOCKS // tiles
         return max(1, min(msteps, self.TN_MAX_SPLITS, sp))
 
-    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0, ld1=None, ld2=None):
+    def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0, ld1=None, ld2=None, label=None):
         """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy (row strides ld1 / ld2,
-        default N1 / N2)."""
+        default N1 / N2).  `label`: a launch site the bench can time with HIP events (self.probe)."""
         ws = self.workspace(lane)
         splits = self._tn_splits(M, N1, N2)
         if _lib.load().es_gemm_tn_workspace(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
-        self._call("es_gemm_tn", ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0,
-             ptr(bias_out), _lib.stream())
+        args = (ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
+                _lib.stream())
+        pr = self.probe
+        if pr is not None and label is not None and pr["label"] == label:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self._call("es_gemm_tn", *args)
+            e1.record()
+            pr["events"].append((e0, e1, 2.0 * M * N1 * N2))
+        else:
+            self._call("es_gemm_tn", *args)
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None):
         D = self.cfg.dim
@@ -660,7 +674,7 @@ class Engine:
             wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
             self._call("es_gemm_nt", EPI_DH, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh),
                  D, None, None, 0, M, D, Hd, 0, s)
-            wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
+            wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"), label="fc1_wgrad")
             self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, Gi.dxmb,
                          gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
             # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))

@@ -32,8 +32,13 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="", help="comma-separated shape names (default: all)")
     ap.add_argument("--tn-variants", default="0,2")
-    ap.add_argument("--tn-blocks", default="512", help="target workgroup counts (split-K sizing) to sweep")
+    ap.add_argument("--tn-blocks", default="512", help="target workgroup counts (split-K sizing) to sweep; "
+                    "'auto' = the library's sizing, 's<N>' = N splits")
+    ap.add_argument("--m-train", type=int, default=0, help="token rows of the TN shapes (default 512 x 197)")
     args = ap.parse_args()
+    global TN
+    if args.m_train:
+        TN = [(n, args.m_train, a, b) for n, _, a, b in TN]
     lib = _lib.load()
     lib.es_set_gemm_variant.restype = _lib.I
     lib.es_set_gemm_variant.argtypes = [_lib.I]
@@ -91,9 +96,14 @@ def main():
         tiles = (N1 // 128) * (N2 // 128)
         row = {}
         for tbs in args.tn_blocks.split(","):  # "768": ceil(768 / tiles) splits; "f768": floor
-            tb = int(tbs.lstrip("f"))
-            sp = tb // tiles if tbs.startswith("f") else -(-tb // tiles)
-            splits = max(1, min((M + 31) // 32, sp))
+            if tbs == "auto":  # es_gemm_tn sizes the split-K for the kernel it picks
+                splits = 0
+            elif tbs.startswith("s"):
+                splits = int(tbs[1:])
+            else:
+                tb = int(tbs.lstrip("f"))
+                sp = tb // tiles if tbs.startswith("f") else -(-tb // tiles)
+                splits = max(1, min((M + 31) // 32, sp))
             times = {v: [] for v in tn_variants}
             for _ in range(args.rounds):
                 for v in tn_variants:

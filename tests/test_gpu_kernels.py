@@ -136,7 +136,7 @@ def test_gemm_nt_patch_epilogue(D, gemm_variant):
 
 
 # ------------------------------------------------------------------------------------- GEMM TN
-@pytest.fixture(params=[-1, 0, 1, 2, 3, 4], ids=["auto", "t0", "t1", "t2", "t3", "t4"])
+@pytest.fixture(params=[-1, 0, 1, 2, 3, 4, 5, 6, 7], ids=["auto", "t0", "t1", "t2", "t3", "t4", "b5", "b6", "b7"])
 def tn_variant(request):
     old = _lib.load().es_set_tn_variant(request.param)
     yield request.param
@@ -144,7 +144,8 @@ def tn_variant(request):
 
 
 @pytest.mark.parametrize("M,N1,N2,splits", [(1000, 128, 256, 1), (1000, 384, 128, 5), (4096, 256, 384, 17),
-                                            (3000, 128, 128, 2)])
+                                            (3000, 128, 128, 2), (1000, 384, 192, 1), (5000, 1152, 384, 0),
+                                            (3000, 384, 1536, 7), (2500, 768, 384, 3)])
 def test_gemm_tn_exact_integers(M, N1, N2, splits, tn_variant):
     g = torch.Generator().manual_seed(M + splits)
     A1 = _pad_rows(_int_bf16(M, N1, lo=-2, hi=3, gen=g))

@@ -399,3 +399,44 @@ def test_uint8_input_path_matches_normalised_fp32():
     # mixed list (labeled fp32 + unlabeled uint8) in one train forward
     c = eng.forward(m.flat, [xf[:2].to(DEV), u8[2:].to(DEV)], train=True).clone()
     assert torch.equal(c, eng.forward(m.flat, [xf.to(DEV)], train=True))
+
+
+def test_graph_replay_matches_eager_step():
+    """FixMatch.use_graph: the forward / losses / backward replayed from a captured hipGraph give the
+    eager step's losses, pseudo-labels and gradients (the same launches in the same order; only the
+    head's fp32-atomic reductions may differ in the last bits), step after step."""
+    from endossl.vit import NativeViT, ViTConfig
+    vcfg = ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23)
+    g = torch.Generator().manual_seed(12)
+    batches = []
+    for _ in range(3):
+        x, y = torch.randn(4, 3, 64, 64, generator=g), torch.randint(0, 23, (4,), generator=g)
+        batches.append(((x.to(DEV), y.to(DEV)), ((torch.randn(8, 3, 64, 64, generator=g).to(DEV),
+                                                  torch.randn(8, 3, 64, 64, generator=g).to(DEV)), None)))
+    res = {}
+    for graph in (False, True):
+        from endossl.fixmatch import FixMatch
+        m = NativeViT(vcfg, seed=3)
+        with torch.no_grad():
+            m.head.weight.normal_(0, 0.5, generator=torch.Generator().manual_seed(2))
+        m = m.to(DEV)
+        tr = FixMatch(m, device=DEV)
+        tr.use_graph = graph
+        tr.get_dataloader((None, None), None)
+        c = _cfg(0.3, 1, 4, 2)
+        c.TRAIN.CLS_WEIGHT = False
+        tr.get_config(c)
+        outs = []
+        for b in batches:
+            o = tr.step(b)
+            torch.cuda.synchronize()
+            outs.append(({k: o[k].detach().clone() for k in ("lx", "lu", "mask_mean", "pseudo_label")},
+                         m.flat_grad.clone(), m.flat.clone()))
+        assert (getattr(tr, "_graph", None) is not None) == graph
+        res[graph] = outs
+    for (oe, ge, we), (og, gg, wg) in zip(res[False], res[True]):
+        for k in ("lx", "lu", "mask_mean"):
+            assert abs(oe[k].item() - og[k].item()) <= 1e-6 * max(1.0, abs(oe[k].item())), k
+        assert torch.equal(oe["pseudo_label"], og["pseudo_label"])
+        assert _rel(gg, ge) <= 1e-6
+        assert (wg - we).abs().max().item() <= 1e-6
