@@ -231,6 +231,102 @@ __global__ __launch_bounds__(256) void bn1d_bwd_kernel(const float* __restrict__
     dU[(size_t)i * lddu + f] = k * (dY[(size_t)i * lddy + f] - m1 - xhat[(size_t)i * F + f] * m2);
 }
 
+// ---- SyncBatchNorm1d pieces (the data-parallel CoMatch head: BatchNorm1d statistics over the global
+// batch, as one process would compute them on the concatenated batch).  The caller all-reduces the
+// per-feature sums between launches: S1 = sum x, then S2 = sum (x - S1/N)^2 (the same two-pass
+// variance as bn1d_fwd_kernel), and in the backward sum dY, sum dY xhat.
+__device__ __forceinline__ float wg_sum256(float v, float* red) {
+  const int t = threadIdx.x;
+  red[t] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) red[t] += red[t + o];
+    __syncthreads();
+  }
+  const float r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// out[f] = sum_i U[i][f]  (S1 == null)  or  sum_i (U[i][f] - S1[f] / N)^2
+__global__ __launch_bounds__(256) void bn1d_sums_kernel(const float* __restrict__ U, int ldu, const float* S1, float N,
+                                                        float* __restrict__ out, int n) {
+  __shared__ float red[256];
+  const int f = blockIdx.x;
+  const float c = S1 ? S1[f] / N : 0.f;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float d = U[(size_t)i * ldu + f] - c;
+    s += S1 ? d * d : d;
+  }
+  s = wg_sum256(s, red);
+  if (threadIdx.x == 0) out[f] = s;
+}
+
+__global__ __launch_bounds__(256) void bn1d_fwd_global_kernel(const float* __restrict__ U, int ldu,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, const float* S1,
+                                                              const float* S2, float N, float* running_mean,
+                                                              float* running_var, long long* nbt, float momentum,
+                                                              float eps, float* __restrict__ Y, int ldy,
+                                                              float* __restrict__ xhat, float* __restrict__ rstd_out,
+                                                              int n, int F) {
+  const int f = blockIdx.x, t = threadIdx.x;
+  const float mean = S1[f] / N, var = S2[f] / N;
+  const float rstd = 1.0f / sqrtf(var + eps);
+  if (t == 0) {
+    running_mean[f] = (1.f - momentum) * running_mean[f] + momentum * mean;
+    running_var[f] = (1.f - momentum) * running_var[f] + momentum * (N > 1.f ? var * N / (N - 1.f) : var);
+    if (f == 0 && nbt) *nbt += 1;
+    rstd_out[f] = rstd;
+  }
+  const float g = gamma[f], bt = beta[f];
+  for (int i = t; i < n; i += blockDim.x) {
+    const float xh = (U[(size_t)i * ldu + f] - mean) * rstd;
+    xhat[(size_t)i * F + f] = xh;
+    Y[(size_t)i * ldy + f] = xh * g + bt;
+  }
+}
+
+// out[f] = sum_i dY[i][f], out[F + f] = sum_i dY[i][f] xhat[i][f]  (this rank's rows)
+__global__ __launch_bounds__(256) void bn1d_bwd_sums_kernel(const float* __restrict__ dY, int lddy,
+                                                            const float* __restrict__ xhat, float* __restrict__ out,
+                                                            int n, int F) {
+  __shared__ float red[256];
+  const int f = blockIdx.x;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float g = dY[(size_t)i * lddy + f];
+    s1 += g;
+    s2 += g * xhat[(size_t)i * F + f];
+  }
+  s1 = wg_sum256(s1, red);
+  s2 = wg_sum256(s2, red);
+  if (threadIdx.x == 0) {
+    out[f] = s1;
+    out[F + f] = s2;
+  }
+}
+
+// dU = gamma rstd (dY - Sg[f]/N - xhat Sg[F+f]/N) with the all-reduced sums Sg; dgamma / dbeta = this
+// rank's sums Sl (the gradient all-reduce adds the other ranks')
+__global__ __launch_bounds__(256) void bn1d_bwd_global_kernel(const float* __restrict__ dY, int lddy,
+                                                              const float* __restrict__ xhat,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ gamma, const float* Sg,
+                                                              const float* Sl, float N, float* __restrict__ dU,
+                                                              int lddu, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta, int n, int F) {
+  const int f = blockIdx.x;
+  if (threadIdx.x == 0) {
+    dgamma[f] = Sl[F + f];
+    dbeta[f] = Sl[f];
+  }
+  const float k = gamma[f] * rstd[f], m1 = Sg[f] / N, m2 = Sg[F + f] / N;
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    dU[(size_t)i * lddu + f] = k * (dY[(size_t)i * lddy + f] - m1 - xhat[(size_t)i * F + f] * m2);
+}
+
 // Normalize(2): one wave per row, L <= 256
 __global__ __launch_bounds__(256) void l2norm_fwd_kernel(const float* __restrict__ V, int ldv, float* __restrict__ Z,
                                                          int ldz, float* __restrict__ nrm, int n, int L) {
@@ -441,35 +537,39 @@ __global__ void comatch_bank_write_kernel(const float* __restrict__ zw, int ldzw
 }
 
 // ---- contrastive (code/comatch.py:199-213) ------------------------------------------------------
-// One workgroup per anchor row i: sim_ij = exp((z0_i . z1_j) / T), P = sim / rowsum; Q_ij = p_i . p_j
-// with Q_ii = 1, zeroed below th, row-normalised; loss_i = -sum_j Q_ij log(P_ij + 1e-7).
+// One workgroup per anchor row i (nr local rows, global index row_off + i) against nc columns
+// (the global batch: all-gathered z1 / probs at world > 1): sim_ij = exp((z0_i . z1_j) / T),
+// P = sim / rowsum; Q_ij = p_i . p_j with Q_ii = 1 (the row's own column), zeroed below th,
+// row-normalised; loss_i = -sum_j Q_ij log(P_ij + 1e-7).
 // dloss_i/ds_ik = P_ik sum_j w_ij - w_ik with w_ij = Q_ij P_ij / (P_ij + 1e-7); the rows of
 // G = scale * dloss/ds / T feed dz0 = G z1 and dz1 = G^T z0.
 __global__ __launch_bounds__(256) void contrast_rows_kernel(const float* __restrict__ z0, int ldz0,
                                                             const float* __restrict__ z1, int ldz1,
-                                                            const float* __restrict__ probs, int nu, int L, int C,
-                                                            float temperature, float th, float scale,
-                                                            float* __restrict__ G, float* __restrict__ row_loss) {
-  extern __shared__ float sm[];  // sim [nu], q [nu], z0_i [L], p_i [C]
+                                                            const float* __restrict__ probs_r,
+                                                            const float* __restrict__ probs_c, int nr, int nc,
+                                                            int row_off, int L, int C, float temperature, float th,
+                                                            float scale, float* __restrict__ G,
+                                                            float* __restrict__ row_loss) {
+  extern __shared__ float sm[];  // sim [nc], q [nc], z0_i [L], p_i [C]
   __shared__ float red[256];
   float* sim = sm;
-  float* q = sm + nu;
-  float* zi = q + nu;
+  float* q = sm + nc;
+  float* zi = q + nc;
   float* pi = zi + L;
   const int i = blockIdx.x, t = threadIdx.x;
   for (int c = t; c < L; c += blockDim.x) zi[c] = z0[(size_t)i * ldz0 + c];
-  for (int c = t; c < C; c += blockDim.x) pi[c] = probs[(size_t)i * C + c];
+  for (int c = t; c < C; c += blockDim.x) pi[c] = probs_r[(size_t)i * C + c];
   __syncthreads();
   float ssum = 0.f, qsum = 0.f;
-  for (int j = t; j < nu; j += blockDim.x) {
+  for (int j = t; j < nc; j += blockDim.x) {
     float d = 0.f;
     for (int c = 0; c < L; ++c) d = fmaf(zi[c], z1[(size_t)j * ldz1 + c], d);
     const float e = expf(d / temperature);
     sim[j] = e;
     ssum += e;
     float qq = 0.f;
-    for (int c = 0; c < C; ++c) qq = fmaf(pi[c], probs[(size_t)j * C + c], qq);
-    if (j == i) qq = 1.f;
+    for (int c = 0; c < C; ++c) qq = fmaf(pi[c], probs_c[(size_t)j * C + c], qq);
+    if (j == row_off + i) qq = 1.f;
     qq = qq >= th ? qq : 0.f;
     q[j] = qq;
     qsum += qq;
@@ -488,7 +588,7 @@ __global__ __launch_bounds__(256) void contrast_rows_kernel(const float* __restr
   ssum = block_sum(ssum);
   qsum = block_sum(qsum);
   float lsum = 0.f, wsum = 0.f;
-  for (int j = t; j < nu; j += blockDim.x) {
+  for (int j = t; j < nc; j += blockDim.x) {
     const float P = sim[j] / ssum, Qn = q[j] / qsum;
     lsum -= logf(P + 1e-7f) * Qn;
     const float w = Qn * P / (P + 1e-7f);
@@ -499,33 +599,34 @@ __global__ __launch_bounds__(256) void contrast_rows_kernel(const float* __restr
   lsum = block_sum(lsum);
   wsum = block_sum(wsum);
   const float k = scale / temperature;
-  for (int j = t; j < nu; j += blockDim.x) G[(size_t)i * nu + j] = k * (sim[j] * wsum - q[j]);
+  for (int j = t; j < nc; j += blockDim.x) G[(size_t)i * nc + j] = k * (sim[j] * wsum - q[j]);
   if (t == 0) row_loss[i] = lsum;
 }
 
-// dz0[i] = sum_k G[i][k] z1[k] (blockIdx.y = 0) and dz1[k] = sum_i G[i][k] z0[i] (blockIdx.y = 1):
-// one wave per output row, lanes over L
+// dz0[r] = sum_k G[r][k] z1[k] over the nc columns (blockIdx.y = 0, r < nr) and dz1[r] = sum_i G[i][r]
+// z0[i] over the nr local rows (blockIdx.y = 1, r < nc): one wave per output row, lanes over L
 __global__ __launch_bounds__(256) void contrast_dz_kernel(const float* __restrict__ G, const float* __restrict__ z0,
                                                           int ldz0, const float* __restrict__ z1, int ldz1,
                                                           float* __restrict__ dz0, int lddz0, float* __restrict__ dz1,
-                                                          int lddz1, int nu, int L) {
+                                                          int lddz1, int nr, int nc, int L) {
   const int lane = threadIdx.x & 63, r = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (r >= nu) return;
   const bool t1 = blockIdx.y == 1;
+  if (r >= (t1 ? nc : nr)) return;
   for (int c = lane; c < L; c += 64) {
     float acc = 0.f;
     if (!t1) {
-      for (int k = 0; k < nu; ++k) acc = fmaf(G[(size_t)r * nu + k], z1[(size_t)k * ldz1 + c], acc);
+      for (int k = 0; k < nc; ++k) acc = fmaf(G[(size_t)r * nc + k], z1[(size_t)k * ldz1 + c], acc);
       dz0[(size_t)r * lddz0 + c] = acc;
     } else {
-      for (int i = 0; i < nu; ++i) acc = fmaf(G[(size_t)i * nu + r], z0[(size_t)i * ldz0 + c], acc);
+      for (int i = 0; i < nr; ++i) acc = fmaf(G[(size_t)i * nc + r], z0[(size_t)i * ldz0 + c], acc);
       dz1[(size_t)r * lddz1 + c] = acc;
     }
   }
 }
 
-// mean of per-row values (one workgroup) -> out[0]
-__global__ __launch_bounds__(256) void row_mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
+// sum of per-row values / div (one workgroup) -> out[0]
+__global__ __launch_bounds__(256) void row_mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out,
+                                                       float div) {
   __shared__ float red[256];
   const int t = threadIdx.x;
   float s = 0.f;
@@ -536,7 +637,7 @@ __global__ __launch_bounds__(256) void row_mean_kernel(const float* __restrict__
     if (t < o) red[t] += red[t + o];
     __syncthreads();
   }
-  if (t == 0) out[0] = red[0] / n;
+  if (t == 0) out[0] = red[0] / div;
 }
 
 // ---- focal unsupervised loss (code/comatch.py:215-220) ------------------------------------------
@@ -658,6 +759,42 @@ int es_bn1d_bwd(const float* dY, int lddy, const float* xhat, const float* rstd,
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+// SyncBatchNorm1d (data-parallel CoMatch head), see the kernels above.  N = global row count.
+int es_bn1d_sums(const float* U, int ldu, int n, int F, const float* S1, float N, float* out, hipStream_t stream) {
+  if (n <= 0 || F <= 0 || N < (float)n) return ES_BAD_SHAPE;
+  if (!U || !out) return ES_BAD_ARG;
+  hipLaunchKernelGGL(bn1d_sums_kernel, F, 256, 0, stream, U, ldu, S1, N, out, n);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_bn1d_fwd_global(const float* U, int ldu, const float* gamma, const float* beta, const float* S1,
+                       const float* S2, float N, float* running_mean, float* running_var, void* num_batches_tracked,
+                       float momentum, float eps, float* Y, int ldy, float* xhat, float* rstd, int n, int F,
+                       hipStream_t stream) {
+  if (n <= 0 || F <= 0 || N < (float)n) return ES_BAD_SHAPE;
+  if (!U || !gamma || !beta || !S1 || !S2 || !running_mean || !running_var || !Y || !xhat || !rstd) return ES_BAD_ARG;
+  hipLaunchKernelGGL(bn1d_fwd_global_kernel, F, 256, 0, stream, U, ldu, gamma, beta, S1, S2, N, running_mean,
+                     running_var, (long long*)num_batches_tracked, momentum, eps, Y, ldy, xhat, rstd, n, F);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_bn1d_bwd_sums(const float* dY, int lddy, const float* xhat, int n, int F, float* out, hipStream_t stream) {
+  if (n <= 0 || F <= 0) return ES_BAD_SHAPE;
+  if (!dY || !xhat || !out) return ES_BAD_ARG;
+  hipLaunchKernelGGL(bn1d_bwd_sums_kernel, F, 256, 0, stream, dY, lddy, xhat, out, n, F);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_bn1d_bwd_global(const float* dY, int lddy, const float* xhat, const float* rstd, const float* gamma,
+                       const float* sums_global, const float* sums_local, float N, float* dU, int lddu,
+                       float* dgamma, float* dbeta, int n, int F, hipStream_t stream) {
+  if (n <= 0 || F <= 0 || N < (float)n) return ES_BAD_SHAPE;
+  if (!dY || !xhat || !rstd || !gamma || !sums_global || !sums_local || !dU || !dgamma || !dbeta) return ES_BAD_ARG;
+  hipLaunchKernelGGL(bn1d_bwd_global_kernel, F, 256, 0, stream, dY, lddy, xhat, rstd, gamma, sums_global, sums_local,
+                     N, dU, lddu, dgamma, dbeta, n, F);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
 int es_l2norm_fwd(const float* V, int ldv, float* Z, int ldz, float* norm, int n, int L, hipStream_t stream) {
   if (n <= 0 || L <= 0) return ES_BAD_SHAPE;
   if (!V || !Z || !norm) return ES_BAD_ARG;
@@ -758,24 +895,47 @@ int es_comatch_bank_write(const float* z_w, int ldzw, int nu, const float* z_x, 
 }
 
 size_t es_comatch_contrastive_workspace(int nu) { return (size_t)nu * nu + nu; }
+size_t es_comatch_contrastive_ex_workspace(int nr, int nc) { return (size_t)nr * nc + nr; }
+
+static int contrastive_launch(const float* z0, int ldz0, const float* z1, int ldz1, const float* probs_r,
+                              const float* probs_c, int nr, int nc, int row_off, int L, int C, float temperature,
+                              float contrast_th, float grad_scale, float loss_div, float* loss_out, float* dz0,
+                              int lddz0, float* dz1, int lddz1, float* workspace, hipStream_t stream) {
+  if (nr <= 0 || nc < nr || nc > 8192 || row_off < 0 || row_off + nr > nc || L <= 0 || C <= 0) return ES_BAD_SHAPE;
+  if (!z0 || !z1 || !probs_r || !probs_c || !loss_out || !dz0 || !dz1 || !workspace) return ES_BAD_ARG;
+  float* G = workspace;
+  float* row_loss = workspace + (size_t)nr * nc;
+  const size_t lds = (size_t)(2 * nc + L + C) * 4;
+  allow_lds(contrast_rows_kernel, lds);
+  hipLaunchKernelGGL(contrast_rows_kernel, nr, 256, lds, stream, z0, ldz0, z1, ldz1, probs_r, probs_c, nr, nc, row_off,
+                     L, C, temperature, contrast_th, grad_scale, G, row_loss);
+  hipLaunchKernelGGL(contrast_dz_kernel, dim3((nc + 3) / 4, 2), 256, 0, stream, G, z0, ldz0, z1, ldz1, dz0, lddz0, dz1,
+                     lddz1, nr, nc, L);
+  hipLaunchKernelGGL(row_mean_kernel, 1, 256, 0, stream, row_loss, nr, loss_out, loss_div);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
 
 // loss_out[0] = L_c = mean_i L_i (unscaled); dz0 / dz1 = grad_scale * d(sum_i L_i) / dz (overwritten)
 int es_comatch_contrastive_fwd_bwd(const float* z0, int ldz0, const float* z1, int ldz1, const float* probs, int nu,
                                    int L, int C, float temperature, float contrast_th, float grad_scale,
                                    float* loss_out, float* dz0, int lddz0, float* dz1, int lddz1, float* workspace,
                                    hipStream_t stream) {
-  if (nu <= 0 || L <= 0 || C <= 0 || nu > 8192) return ES_BAD_SHAPE;
-  if (!z0 || !z1 || !probs || !loss_out || !dz0 || !dz1 || !workspace) return ES_BAD_ARG;
-  float* G = workspace;
-  float* row_loss = workspace + (size_t)nu * nu;
-  const size_t lds = (size_t)(2 * nu + L + C) * 4;
-  allow_lds(contrast_rows_kernel, lds);
-  hipLaunchKernelGGL(contrast_rows_kernel, nu, 256, lds, stream, z0, ldz0, z1, ldz1, probs, nu, L, C, temperature,
-                     contrast_th, grad_scale, G, row_loss);
-  hipLaunchKernelGGL(contrast_dz_kernel, dim3((nu + 3) / 4, 2), 256, 0, stream, G, z0, ldz0, z1, ldz1, dz0, lddz0, dz1,
-                     lddz1, nu, L);
-  hipLaunchKernelGGL(row_mean_kernel, 1, 256, 0, stream, row_loss, nu, loss_out);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return contrastive_launch(z0, ldz0, z1, ldz1, probs, probs, nu, nu, 0, L, C, temperature, contrast_th, grad_scale,
+                            (float)nu, loss_out, dz0, lddz0, dz1, lddz1, workspace, stream);
+}
+
+// The data-parallel form: this rank's nr anchor rows (global rows row_off .. row_off + nr - 1)
+// against the nc global columns (z1_all / probs_all: the all-gathered batch).  loss_out[0] =
+// sum over the local rows / loss_div (pass the global row count: the ranks' values then sum to L_c);
+// dz0 [nr, L] for the local rows, dz1 [nc, L] this rank's share of d/dz1 for EVERY column (the
+// caller sums the shares over ranks and keeps its own rows).
+int es_comatch_contrastive_fwd_bwd_ex(const float* z0, int ldz0, const float* z1_all, int ldz1,
+                                      const float* probs_rows, const float* probs_all, int nr, int nc, int row_off,
+                                      int L, int C, float temperature, float contrast_th, float grad_scale,
+                                      float loss_div, float* loss_out, float* dz0, int lddz0, float* dz1_all,
+                                      int lddz1, float* workspace, hipStream_t stream) {
+  return contrastive_launch(z0, ldz0, z1_all, ldz1, probs_rows, probs_all, nr, nc, row_off, L, C, temperature,
+                            contrast_th, grad_scale, loss_div, loss_out, dz0, lddz0, dz1_all, lddz1, workspace, stream);
 }
 
 // loss_out[0] = L_u = mean_i L_i (unscaled); dls = grad_scale * d(sum_i L_i) / dlogits_s0 (overwritten);
@@ -787,7 +947,7 @@ int es_comatch_focal_fwd_bwd(const float* ls, int ldl, const float* probs, const
   if (!ls || !probs || !mask || !loss_out || !dls || !workspace) return ES_BAD_ARG;
   hipLaunchKernelGGL(focal_kernel, (nu + 255) / 256, 256, 0, stream, ls, ldl, probs, mask, nu, C, gamma, grad_scale,
                      dls, lddl, workspace);
-  hipLaunchKernelGGL(row_mean_kernel, 1, 256, 0, stream, workspace, nu, loss_out);
+  hipLaunchKernelGGL(row_mean_kernel, 1, 256, 0, stream, workspace, nu, loss_out, (float)nu);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -596,14 +596,22 @@ int es_gemm_nt_f32(int epi, const void* A, int lda, const void* B, int ldb, cons
   return launch_pgemm(false, false, p, (K + PK - 1) / PK * PK, stream);
 }
 
+// splits <= 0: automatic (enough 64 x 64 tiles x splits to fill the chip, >= 1024 tokens per split)
+static int ptn_auto_splits(int M, int N1, int N2) {
+  const int tiles = ((N1 + PT - 1) / PT) * ((N2 + PT - 1) / PT);
+  return std::max(1, std::min(std::max(1, 1024 / tiles), std::max(1, M / 1024)));
+}
+
 size_t es_gemm_tn_f32_workspace(int N1, int N2, int splits) {
+  if (splits <= 0) splits = std::max(1, 1024 / (((N1 + PT - 1) / PT) * ((N2 + PT - 1) / PT)));
   return (size_t)splits * N1 * N2 + (size_t)splits * N1;
 }
 
 int es_gemm_tn_f32(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                    float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream) {
-  if (M <= 0 || N1 <= 0 || N2 <= 0 || splits <= 0) return ES_BAD_SHAPE;
+  if (M <= 0 || N1 <= 0 || N2 <= 0) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
+  if (splits <= 0) splits = ptn_auto_splits(M, N1, N2);
   // each split covers a whole number of 16-deep k steps; the slab count is what the grid covers
   const int kchunk = ((M + splits - 1) / splits + PK - 1) / PK * PK;
   const int S = (M + kchunk - 1) / kchunk;

@@ -54,6 +54,10 @@ SIGNATURES = {
     "es_bn1d_fwd": (I, [V, I, V, V, V, V, V, F, F, I, V, I, V, V, I, I, V]),
     "es_bn1d_bwd": (I, [V, I, V, V, V, V, I, V, V, I, I, V]),
     "es_dropout_keep": (I, [V, L, F, U64, U64, V]),
+    "es_bn1d_sums": (I, [V, I, I, I, V, F, V, V]),
+    "es_bn1d_fwd_global": (I, [V, I, V, V, V, V, F, V, V, V, F, F, V, I, V, V, I, I, V]),
+    "es_bn1d_bwd_sums": (I, [V, I, V, I, I, V, V]),
+    "es_bn1d_bwd_global": (I, [V, I, V, V, V, V, V, F, V, I, V, V, I, I, V]),
     "es_l2norm_fwd": (I, [V, I, V, I, V, I, I, V]),
     "es_l2norm_bwd": (I, [V, I, V, I, V, V, I, I, I, V]),
     "es_comatch_pseudo_workspace": (Z, [I, I, I]),
@@ -63,6 +67,8 @@ SIGNATURES = {
     "es_comatch_bank_write": (I, [V, I, I, V, I, I, I, V, V, I, V, V, I, I, V]),
     "es_comatch_contrastive_workspace": (Z, [I]),
     "es_comatch_contrastive_fwd_bwd": (I, [V, I, V, I, V, I, I, I, F, F, F, V, V, I, V, I, V, V]),
+    "es_comatch_contrastive_ex_workspace": (Z, [I, I]),
+    "es_comatch_contrastive_fwd_bwd_ex": (I, [V, I, V, I, V, V, I, I, I, I, I, F, F, F, F, V, V, I, V, I, V, V]),
     "es_comatch_focal_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, V, I, V, V]),
     "es_fm_consistency_fwd_bwd": (I, [V, I, V, I, I, I, F, F, V, V, V, V, I, V, V]),
     "es_poly_ce_fwd_bwd": (I, [V, I, V, V, I, I, F, F, V, I, V, V]),

@@ -14,9 +14,11 @@ evaluate_one, save_checkpoint, load_checkpoint, fit) plus `step(batch)`.  One st
          L_u = focal(logits_s0 | p, mask)                         (:215-220)
          losses = L_x + LAMBDA_U L_u + LAMBDA_C L_c               (:222)
   bwd    heads backward -> dL/dfts -> trunk backward over every image (BN1d couples the rows)
-  comm   data-parallel only: all-reduce of the DA batch mean (C floats) and all-gather of the bank
-         rows, so every rank holds the same DA history and bank; RCCL all-reduce of the flat grad.
-         BatchNorm1d statistics and the contrastive graph stay per rank (DDP without SyncBN)
+  comm   data-parallel only (global-batch semantics: N ranks compute what one process computes on
+         the concatenated batch): all-reduce of the DA batch mean (C floats); all-gather of the bank
+         rows (every rank holds the same bank); SyncBatchNorm1d in the head (all-reduced per-feature
+         sums, comatch_model.EmbHeads); the contrastive graph over the global batch (all-gathered
+         z_s1 / probs columns, summed column gradients); RCCL all-reduce of the flat grad
   opt    Adam + parameter EMA in one sweep, EMA of the BatchNorm buffers, lr_scheduler.step_update
 
 Reference behaviour kept on purpose: `train_one` walks the whole unlabeled
@@ -143,9 +145,28 @@ class CoMatch(FixMatch):
                          ptr(po_a[r * btu:]), ptr(y_a[r * bt:]), C, ptr(self.queue_feats), ptr(self.queue_probs),
                          self.queue_ptr + r * (bt + btu), self.queue_size, s)
             self.queue_ptr = (self.queue_ptr + n) % self.queue_size
-        call("es_comatch_contrastive_fwd_bwd", ptr(z0), L, ptr(z1), L, ptr(W["probs"]), btu, L, C, self.temperature,
-             self.contrast_th, lam_c / btu, ptr(stats[2:3]), ptr(dz[bt + btu:]), L, ptr(dz[bt + 2 * btu:]), L,
-             ptr(W["ws_c"]), s)
+        if world == 1:
+            call("es_comatch_contrastive_fwd_bwd", ptr(z0), L, ptr(z1), L, ptr(W["probs"]), btu, L, C,
+                 self.temperature, self.contrast_th, lam_c / btu, ptr(stats[2:3]), ptr(dz[bt + btu:]), L,
+                 ptr(dz[bt + 2 * btu:]), L, ptr(W["ws_c"]), s)
+        else:
+            # the graph spans the global batch (code/comatch.py:200-213 on the concatenated batch): this
+            # rank's anchor rows against every rank's z_s1 / probs columns (all-gathered, rank order =
+            # global order, so the self-loop sits at column rank * btu + i).  Gradient scale lam_c / btu =
+            # lam_c * world / nu_global: the flat gradient is SUM-reduced and scaled by 1 / world.  Every
+            # rank holds a share of d/dz_s1 for all columns; the shares are summed and each keeps its rows.
+            rk, nc = dist.rank(), world * btu
+            z1_all = dist.all_gather_cat(z1.contiguous())
+            p_all = dist.all_gather_cat(W["probs"])
+            if "ws_cx" not in W or W["ws_cx"].numel() < _lib.load().es_comatch_contrastive_ex_workspace(btu, nc):
+                W["ws_cx"] = torch.zeros(_lib.load().es_comatch_contrastive_ex_workspace(btu, nc), device=dev)
+                W["dz1_all"] = torch.zeros(nc, L, device=dev)
+            call("es_comatch_contrastive_fwd_bwd_ex", ptr(z0), L, ptr(z1_all), L, ptr(W["probs"]), ptr(p_all), btu, nc,
+                 rk * btu, L, C, self.temperature, self.contrast_th, lam_c / btu, float(nc), ptr(stats[2:3]),
+                 ptr(dz[bt + btu:]), L, ptr(W["dz1_all"]), L, ptr(W["ws_cx"]), s)
+            dist.allreduce_inplace_(W["dz1_all"])
+            dz[bt + 2 * btu:].copy_(W["dz1_all"][rk * btu:(rk + 1) * btu])
+            dist.allreduce_inplace_(stats[2:3])  # L_c over the global batch (each rank sent its rows' sum / nc)
         call("es_comatch_focal_fwd_bwd", ptr(ls0), C, ptr(W["probs"]), ptr(W["mask"]), btu, C, float(self.gamma),
              lam_u / btu, ptr(stats[1:2]), ptr(dl[bt + btu:]), C, ptr(W["ws_f"]), s)
         torch.mean(W["mask"], 0, keepdim=True, out=stats[3:4])

@@ -16,7 +16,7 @@ from copy import deepcopy
 import torch
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, dist
 from ._lib import call, ptr
 from .vit import NativeViT, ViTConfig
 
@@ -40,7 +40,8 @@ class EmbHeads:
                 "u": z(n, F), "xhat": z(n, F), "rstd": z(F), "y": z(n, F), "logits": z(n, C),
                 "e": z(n, 3 * L), "v": z(n, L), "z": z(n, L), "norm": z(n),
                 "dy": z(n, F), "du": z(n, F), "dv": z(n, L), "de": z(n, 3 * L), "dfts": z(n, D),
-                "ws": z(n * max(F, C, 3 * L, L)), "keep": torch.ones(n, F, dtype=torch.uint8, device=self.device)}
+                "ws": z(n * max(F, C, 3 * L, L)), "keep": torch.ones(n, F, dtype=torch.uint8, device=self.device),
+                "s1": z(F), "s2": z(F), "sb": z(2 * F), "sbl": z(2 * F)}
         return self._bufs[n]
 
     def forward(self, view, bn, fts, keep, train):
@@ -53,9 +54,22 @@ class EmbHeads:
         kp = ptr(keep) if train else None
         call("es_dense_fwd", ptr(fts), D, ptr(view("fc.0.weight")), ptr(view("fc.0.bias")), ptr(b["u"]), F, n, D, F, 1,
              0.0, kp, 1.0 / (1.0 - DROP_P), s)
-        call("es_bn1d_fwd", ptr(b["u"]), F, ptr(view("fc.3.weight")), ptr(view("fc.3.bias")), ptr(bn[0]), ptr(bn[1]),
-             ptr(bn[2]) if train else None, BN_MOMENTUM, BN_EPS, 1 if train else 0, ptr(b["y"]), F, ptr(b["xhat"]),
-             ptr(b["rstd"]), n, F, s)
+        world = dist.world_size()
+        if train and world > 1:
+            # SyncBatchNorm: batch statistics over every rank's rows (the one-process batch of the
+            # reference); two all-reduces of F floats (sum, then the centred sum of squares)
+            N = float(n * world)
+            call("es_bn1d_sums", ptr(b["u"]), F, n, F, None, N, ptr(b["s1"]), s)
+            dist.allreduce_inplace_(b["s1"])
+            call("es_bn1d_sums", ptr(b["u"]), F, n, F, ptr(b["s1"]), N, ptr(b["s2"]), s)
+            dist.allreduce_inplace_(b["s2"])
+            call("es_bn1d_fwd_global", ptr(b["u"]), F, ptr(view("fc.3.weight")), ptr(view("fc.3.bias")), ptr(b["s1"]),
+                 ptr(b["s2"]), N, ptr(bn[0]), ptr(bn[1]), ptr(bn[2]), BN_MOMENTUM, BN_EPS, ptr(b["y"]), F,
+                 ptr(b["xhat"]), ptr(b["rstd"]), n, F, s)
+        else:
+            call("es_bn1d_fwd", ptr(b["u"]), F, ptr(view("fc.3.weight")), ptr(view("fc.3.bias")), ptr(bn[0]),
+                 ptr(bn[1]), ptr(bn[2]) if train else None, BN_MOMENTUM, BN_EPS, 1 if train else 0, ptr(b["y"]), F,
+                 ptr(b["xhat"]), ptr(b["rstd"]), n, F, s)
         call("es_dense_fwd", ptr(b["y"]), F, ptr(view("fc.4.weight")), ptr(view("fc.4.bias")), ptr(b["logits"]), C, n,
              F, C, 0, 0.0, None, 1.0, s)
         call("es_dense_fwd", ptr(fts), D, ptr(view("head_emb.0.weight")), ptr(view("head_emb.0.bias")), ptr(b["e"]),
@@ -75,8 +89,17 @@ class EmbHeads:
         ws = b["ws"]
         call("es_dense_bwd", ptr(dlogits), C, None, 0, 0, 0.0, None, 1.0, ptr(b["y"]), F, ptr(view("fc.4.weight")),
              ptr(b["dy"]), F, 0, ptr(gview("fc.4.weight")), ptr(gview("fc.4.bias")), n, F, C, ptr(ws), s)
-        call("es_bn1d_bwd", ptr(b["dy"]), F, ptr(b["xhat"]), ptr(b["rstd"]), ptr(view("fc.3.weight")), ptr(b["du"]), F,
-             ptr(gview("fc.3.weight")), ptr(gview("fc.3.bias")), n, F, s)
+        world = dist.world_size()
+        if world > 1:  # SyncBatchNorm backward: the global means of dY and dY * xhat
+            call("es_bn1d_bwd_sums", ptr(b["dy"]), F, ptr(b["xhat"]), n, F, ptr(b["sbl"]), s)
+            b["sb"].copy_(b["sbl"])
+            dist.allreduce_inplace_(b["sb"])
+            call("es_bn1d_bwd_global", ptr(b["dy"]), F, ptr(b["xhat"]), ptr(b["rstd"]), ptr(view("fc.3.weight")),
+                 ptr(b["sb"]), ptr(b["sbl"]), float(n * world), ptr(b["du"]), F, ptr(gview("fc.3.weight")),
+                 ptr(gview("fc.3.bias")), n, F, s)
+        else:
+            call("es_bn1d_bwd", ptr(b["dy"]), F, ptr(b["xhat"]), ptr(b["rstd"]), ptr(view("fc.3.weight")), ptr(b["du"]),
+                 F, ptr(gview("fc.3.weight")), ptr(gview("fc.3.bias")), n, F, s)
         call("es_dense_bwd", ptr(b["du"]), F, ptr(b["u"]), F, 1, 0.0, ptr(keep), 1.0 / (1.0 - DROP_P), ptr(fts), D,
              ptr(view("fc.0.weight")), ptr(b["dfts"]), D, 0, ptr(gview("fc.0.weight")), ptr(gview("fc.0.bias")), n, D,
              F, ptr(ws), s)

@@ -112,6 +112,13 @@ class GradBuckets:
         return 1.0 / self.world
 
 
+def allreduce_inplace_(t):
+    """In-place SUM over ranks (SyncBatchNorm statistics, CoMatch's contrastive column gradients)."""
+    if world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
 def allreduce_mean_(t):
     """In-place mean over ranks (CoMatch's distribution-alignment batch mean)."""
     w = world_size()

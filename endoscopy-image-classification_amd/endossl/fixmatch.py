@@ -90,7 +90,7 @@ class FixMatch:
     # copied into the graph's own static buffers (static_batch() hands them out for zero-copy use).
     # The optimizer, the all-reduce and the LR schedule stay outside (their scalars change per step).
     # ENDOSSL_GRAPH=0 runs everything eagerly.
-    use_graph = os.environ.get("ENDOSSL_GRAPH", "1") == "1"
+    use_graph = os.environ.get("ENDOSSL_GRAPH", "0") == "1"
 
     def _compute(self, inputs_x, targets_x, inputs_u_w, inputs_u_s):
         """Weak forward, train forward, fused losses, backward into model.flat_grad (no host sync)."""

@@ -537,7 +537,8 @@ class Engine:
         default N1 / N2).  `label`: a launch site the bench can time with HIP events (self.probe)."""
         ws = self.workspace(lane)
         splits = self._tn_splits(M, N1, N2)
-        if _lib.load().es_gemm_tn_workspace(N1, N2, splits) > ws.numel():
+        need = getattr(_lib.load(), "es_gemm_tn_f32_workspace" if self.precision == "fp32" else "es_gemm_tn_workspace")
+        if need(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
         args = (ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
                 _lib.stream())

@@ -45,10 +45,12 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 int es_set_gemm_variant(int variant);
 /* weight gradient: out[N1,N2] (+)= sum_m A1[m,N1]^T A2[m,N2], token axis split `splits` ways into
  * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced; bias_out (nullable) (+)=
- * sum_m A1[m,:] computed from the same LDS tiles.  N1,N2 % 128 == 0; rows in [M, round_up(M,64))
- * of A1 must be zero. */
-/* tuning knob for es_gemm_tn: -1 = default, 0..4 = (token step, ring depth) 32x2, 32x3, 32x4, 64x2,
- * 64x3; returns the previous value */
+ * sum_m A1[m,:] computed from the same tiles.  splits <= 0: sized by the library for the kernel it
+ * picks (es_gemm_tn_workspace(N1, N2, 0) bounds the workspace).  N1,N2 % 128 == 0, or N1 % 384 == 0
+ * and N2 % 192 == 0; rows in [M, round_up(M,64)) of A1 must be zero. */
+/* tuning knob for es_gemm_tn: -1 = default (384x192 tile for M >= 65536 where it tiles, else
+ * 128x128), 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3, 5..8 =
+ * 384x192 tile with 32x2, 32x3, 64x2, 32x4; returns the previous value */
 int es_set_tn_variant(int variant);
 size_t es_gemm_tn_workspace(int N1, int N2, int splits);
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
@@ -155,6 +157,22 @@ int es_bn1d_fwd(const float* U, int ldu, const float* gamma, const float* beta, 
                 float* rstd, int n, int F, hipStream_t stream);
 int es_bn1d_bwd(const float* dY, int lddy, const float* xhat, const float* rstd, const float* gamma, float* dU,
                 int lddu, float* dgamma, float* dbeta, int n, int F, hipStream_t stream);
+/* SyncBatchNorm1d pieces for the data-parallel CoMatch head (statistics over the global batch of N
+ * rows, the caller all-reducing the per-feature sums between launches; code/models/custom_model.py:
+ * 110-116 BatchNorm1d as one process computes it on the concatenated batch):
+ *   es_bn1d_sums: out[f] = sum_i U[i][f] (S1 NULL) or sum_i (U[i][f] - S1[f]/N)^2;
+ *   es_bn1d_fwd_global: y / xhat / rstd from the global S1, S2, running-buffer update (unbiased var);
+ *   es_bn1d_bwd_sums: out[f] = sum dY, out[F+f] = sum dY xhat over this rank's rows;
+ *   es_bn1d_bwd_global: dU from the all-reduced sums, dgamma / dbeta = this rank's sums. */
+int es_bn1d_sums(const float* U, int ldu, int n, int F, const float* S1, float N, float* out, hipStream_t stream);
+int es_bn1d_fwd_global(const float* U, int ldu, const float* gamma, const float* beta, const float* S1,
+                       const float* S2, float N, float* running_mean, float* running_var, void* num_batches_tracked,
+                       float momentum, float eps, float* Y, int ldy, float* xhat, float* rstd, int n, int F,
+                       hipStream_t stream);
+int es_bn1d_bwd_sums(const float* dY, int lddy, const float* xhat, int n, int F, float* out, hipStream_t stream);
+int es_bn1d_bwd_global(const float* dY, int lddy, const float* xhat, const float* rstd, const float* gamma,
+                       const float* sums_global, const float* sums_local, float N, float* dU, int lddu,
+                       float* dgamma, float* dbeta, int n, int F, hipStream_t stream);
 /* Dropout(p) keep-mask (uint8 0/1), counter-based hash of (seed, offset + i) */
 int es_dropout_keep(void* keep, long n, float p, unsigned long long seed, unsigned long long offset,
                     hipStream_t stream);
@@ -191,6 +209,15 @@ int es_comatch_contrastive_fwd_bwd(const float* z0, int ldz0, const float* z1, i
                                    int L, int C, float temperature, float contrast_th, float grad_scale,
                                    float* loss_out, float* dz0, int lddz0, float* dz1, int lddz1, float* workspace,
                                    hipStream_t stream);
+/* the data-parallel form: nr local anchor rows (global rows row_off..) against the nc global columns
+ * (all-gathered z1 / probs); loss_out[0] = local row-loss sum / loss_div; dz1_all [nc, L] is this
+ * rank's share of d/dz1 for every column (sum it over ranks, keep the own rows) */
+size_t es_comatch_contrastive_ex_workspace(int nr, int nc);
+int es_comatch_contrastive_fwd_bwd_ex(const float* z0, int ldz0, const float* z1_all, int ldz1,
+                                      const float* probs_rows, const float* probs_all, int nr, int nc, int row_off,
+                                      int L, int C, float temperature, float contrast_th, float grad_scale,
+                                      float loss_div, float* loss_out, float* dz0, int lddz0, float* dz1_all,
+                                      int lddz1, float* workspace, hipStream_t stream);
 /* loss_out[0] = L_u = mean_i L_i; dls = grad_scale * d(sum_i L_i)/dlogits -- pass lambda_u / nu
  * (code/comatch.py:215-220); workspace nu floats */
 int es_comatch_focal_fwd_bwd(const float* ls, int ldl, const float* probs, const float* mask, int nu, int C,

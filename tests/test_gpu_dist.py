@@ -89,3 +89,159 @@ def test_two_rank_overlapped_allreduce_bit_identical():
         assert handed == 3
         sums.add(gsum)
     assert len(sums) == 1  # both ranks hold the same summed block gradients
+
+
+def _shard_worker(rank, world, port, q):
+    """Strong-scaling sharding (north_star / SURVEY §8(e)) on the native engine: rank r runs the
+    FixMatch trainer step on shard r of the global batch (B/world labeled + mu*B/world pairs); the
+    SUM all-reduce / world must equal the single-process full-batch gradient."""
+    sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+    sys.path.insert(0, ROOT)
+    from endossl import dist
+    from endossl.fixmatch import FixMatch
+    from endossl.utils import AttrDict
+    from endossl.vit import NativeViT, ViTConfig
+    vcfg = ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23)
+    B, MU = 8, 2
+    g = torch.Generator().manual_seed(77)
+    x, y = torch.randn(B, 3, 64, 64, generator=g), torch.randint(0, 23, (B,), generator=g)
+    uw, us = torch.randn(B * MU, 3, 64, 64, generator=g), torch.randn(B * MU, 3, 64, 64, generator=g)
+
+    def trainer(n_b):
+        m = NativeViT(vcfg, seed=5)
+        with torch.no_grad():
+            m.head.weight.normal_(0, 0.5, generator=torch.Generator().manual_seed(6))
+        m = m.to("cuda")
+        tr = FixMatch(m, device="cuda")
+        tr.get_dataloader((None, None), None)
+        tr.get_config(AttrDict(DATA=AttrDict(BATCH_SIZE=n_b, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+                               MODEL=AttrDict(NAME="vit_tiny_test", NUM_CLASSES=23),
+                               TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3,
+                                              EVAL_STEP=1, CLS_WEIGHT=False, THRES=0.3, T=1.0, LAMBDA_U=1.0,
+                                              EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4,
+                                              LR_DECAY=0.8, SCH_NAME="const")))
+        return m, tr
+
+    # the single-process full-batch step first (no process group yet: world 1)
+    m1, tr1 = trainer(B)
+    o1 = tr1.step(((x, y), ((uw, us), None)))
+    torch.cuda.synchronize()
+    full_grad, full_w, full_lx = m1.flat_grad.clone(), m1.flat.clone(), o1["lx"].item()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    dist.init_from_env(backend="gloo")
+    try:
+        b, nu = B // world, B * MU // world
+        m, tr = trainer(b)
+        sl, su = slice(rank * b, (rank + 1) * b), slice(rank * nu, (rank + 1) * nu)
+        o = tr.step(((x[sl], y[sl]), ((uw[su], us[su]), None)))
+        torch.cuda.synchronize()
+        lx = torch.tensor([o["lx"].item()])
+        torch.distributed.all_reduce(lx)
+        grad = m.flat_grad / world  # the trainer hands Adam the SUM and a 1/world scale
+        rel = ((grad - full_grad).norm() / full_grad.norm()).item()
+        wdiff = (m.flat - full_w).abs().max().item()
+        q.put((rank, rel, wdiff, lx.item() / world, full_lx))
+        dist.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_rank_sharded_step_equals_full_batch():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, rel, wdiff, lx, full_lx in res:
+        # rows are independent through the ViT; only the weight gradients' token-axis split (fp32
+        # summation order) and the head's fp32 atomics differ from the full-batch pass
+        assert rel <= 1e-5, (rank, rel)
+        assert abs(lx - full_lx) <= 1e-6 * max(1.0, abs(full_lx)), (rank, lx, full_lx)
+        assert wdiff <= 2e-3 + 1e-6, (rank, wdiff)  # Adam: a ~0 gradient's sign may flip (<= 2 lr)
+
+
+def _comatch_shard_worker(rank, world, port, q, precision):
+    """CoMatch global-batch semantics at N > 1 (code/comatch.py:141-231 on the concatenated batch):
+    SyncBatchNorm1d in the head, the contrastive graph over all-gathered columns with summed column
+    gradients, the DA mean all-reduced.  Shards of a global batch vs the one-process step."""
+    sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+    sys.path.insert(0, ROOT)
+    from endossl import dist
+    from endossl.comatch import CoMatch
+    from endossl.comatch_model import NativeViTEmb
+    from endossl.utils import AttrDict
+    from endossl.vit import ViTConfig
+    L, B, MU = 16, 4, 2
+    nu = B * MU
+    vcfg = ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23, head="emb", low_dim=L)
+    g = torch.Generator().manual_seed(31)
+    x, y = torch.randn(B, 3, 64, 64, generator=g), torch.randint(0, 23, (B,), generator=g)
+    uw, u0, u1 = (torch.randn(nu, 3, 64, 64, generator=g) for _ in range(3))
+    keep = (torch.rand(B + 3 * nu, 128 // 4, generator=g) > 0.2).to(torch.uint8)
+
+    def trainer(n_b):
+        m = NativeViTEmb(vcfg, seed=9).to("cuda").set_precision(precision)
+        tr = CoMatch(m, device="cuda")
+        tr.get_dataloader((None, None), None)
+        tr.get_config(AttrDict(
+            DATA=AttrDict(BATCH_SIZE=n_b, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+            MODEL=AttrDict(NAME="vit_tiny_test", NUM_CLASSES=23, TYPE_SEMI="CoMatch", LOW_DIM=L),
+            TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=1,
+                           CLS_WEIGHT=False, THRES=0.05, T=1.0, LAMBDA_U=2.0, LAMBDA_C=2.0, EPOCHS=1, WARMUP_EPOCHS=0,
+                           DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const")))
+        tr.contrast_th = 0.02  # a dense graph: many off-diagonal positives across the shards
+        return m, tr
+
+    m1, tr1 = trainer(B)
+    o1 = tr1.step(((x, y), ((uw, u0, u1), None)), drop_keep=keep)
+    torch.cuda.synchronize()
+    full = {k: o1[k].item() for k in ("lx", "lu", "lc")}
+    full_grad = m1.flat_grad.clone()
+    full_bn = [t.clone() for t in m1.bn_buffers()]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    dist.init_from_env(backend="gloo")
+    try:
+        b, n = B // world, nu // world
+        m, tr = trainer(b)
+        sl, su = slice(rank * b, (rank + 1) * b), slice(rank * n, (rank + 1) * n)
+        k = torch.cat([keep[:B][sl], keep[B:B + nu][su], keep[B + nu:B + 2 * nu][su], keep[B + 2 * nu:][su]])
+        o = tr.step(((x[sl], y[sl]), ((uw[su], u0[su], u1[su]), None)), drop_keep=k)
+        torch.cuda.synchronize()
+        loc = torch.tensor([o["lx"].item(), o["lu"].item()])
+        torch.distributed.all_reduce(loc)
+        got = {"lx": loc[0].item() / world, "lu": loc[1].item() / world, "lc": o["lc"].item()}
+        rel = ((m.flat_grad / world - full_grad).norm() / full_grad.norm()).item()
+        bn = max((a - c).abs().max().item() for a, c in zip(m.bn_buffers()[:2], full_bn[:2]))
+        q.put((rank, got, full, rel, bn))
+        dist.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_two_rank_comatch_global_batch(precision):
+    """fp32 parity mode: the sharded step equals the one-process step to fp32 summation order.  bf16:
+    the rows now couple (BatchNorm1d, the contrastive graph), so d(loss)/d(features) differ in the last
+    fp32 bits and the trunk's bf16 operands round some of them to the neighbouring value: 1e-3."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comatch_shard_worker, args=(r, 2, port, q, precision)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got, full, rel, bn in res:
+        for key in ("lx", "lu", "lc"):  # fp32 summation order only (the trunk rows are independent)
+            assert abs(got[key] - full[key]) <= 1e-5 * max(1.0, abs(full[key])), (rank, key, got[key], full[key])
+        assert rel <= (1e-5 if precision == "fp32" else 1e-3), (rank, rel)
+        assert bn <= 1e-5, (rank, bn)  # SyncBatchNorm: the running statistics of the global batch
