@@ -48,6 +48,10 @@ class CoMatch(FixMatch):
         self.gamma = 2
         self._ws = {}
 
+    def _trainable_when_frozen(self):
+        """code/comatch.py:64-73: `model.fc` and `model.head_emb`."""
+        return [self.model.fc, self.model.head_emb]
+
     def get_config(self, config):
         super().get_config(config)
         dev = self.model.flat.device
@@ -109,7 +113,8 @@ class CoMatch(FixMatch):
         s = _lib.stream()
         W = self._workspace(bt, btu, C, L)
         keep = None if drop_keep is None else drop_keep.to(dev, torch.uint8).contiguous()
-        logits, fts, z = m._run([inputs_x, u_w, u_s0, u_s1], train=True, keep=keep)
+        frozen = getattr(self, "frozen", False)  # IS_FREEZE: the trunk in inference form, heads trained
+        logits, fts, z = m._run([inputs_x, u_w, u_s0, u_s1], train=True, keep=keep, trunk_train=not frozen)
         lw, ls0 = logits[bt:bt + btu], logits[bt + btu:bt + 2 * btu]
         zx, zw, z0, z1 = z[:bt], z[bt:bt + btu], z[bt + btu:bt + 2 * btu], z[bt + 2 * btu:]
         dl, dz = W["dl"], W["dz"]
@@ -174,7 +179,7 @@ class CoMatch(FixMatch):
         stats[4].add_(stats[2], alpha=lam_c)
 
         gb = dist.GradBuckets(m.flat_grad) if world > 1 and self.overlap_allreduce else None
-        m.backward_from(dl, dz, grad_ready=gb.ready if gb is not None else None)
+        m.backward_from(dl, dz, grad_ready=gb.ready if gb is not None else None, trunk=not frozen)
         gscale = gb.finish() if gb is not None else dist.allreduce_sum_(m.flat_grad)
         ema = self.ema_model
         self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,

@@ -204,12 +204,15 @@ class NativeViTEmb(NativeViT):
         self._drop_counter += keep.numel()
         return keep
 
-    def _run(self, images, train, keep=None):
-        """Trunk features + heads.  images: tensor or list of tensors (one batch, no concat)."""
+    def _run(self, images, train, keep=None, trunk_train=None):
+        """Trunk features + heads.  images: tensor or list of tensors (one batch, no concat).
+        trunk_train=False: the trunk in inference form (no saved activations; a frozen trunk)."""
         eng = self.engine()
         eng.pack(self.flat, self.version)
         imgs = images if isinstance(images, (list, tuple)) else [images]
-        fts = eng.forward(self.flat, imgs, train=train)
+        trunk_train = train if trunk_train is None else trunk_train
+        self._last_trunk_train = trunk_train
+        fts = eng.forward(self.flat, imgs, train=trunk_train)
         n = int(fts.shape[0])
         self._last_n = n
         if train and keep is None:
@@ -218,17 +221,20 @@ class NativeViTEmb(NativeViT):
         logits, z = self.heads().forward(lambda nm: eng.view(self.flat, nm), self.bn_buffers(), fts, keep, train)
         return logits, fts, z
 
-    def backward_from(self, dlogits, dz, dfts_extra=None, grad_ready=None):
+    def backward_from(self, dlogits, dz, dfts_extra=None, grad_ready=None, trunk=True):
         """Gradient of the last train forward: dlogits [n, C], dz [n, L] (and optionally a direct
-        dL/dfts) -> flat grad (returned).  grad_ready: Engine.backward's per-block hook."""
+        dL/dfts) -> flat grad (returned).  grad_ready: Engine.backward's per-block hook.
+        trunk=False (IS_FREEZE): the heads' parameter gradients only, the trunk's stay zero."""
         eng = self.engine()
         g = self.flat_grad
         g.zero_()
-        fts = eng.acts(self._last_n, True).fts
+        fts = eng.acts(self._last_n, getattr(self, "_last_trunk_train", True)).fts
         dfts = self.heads().backward(lambda nm: eng.view(self.flat, nm), lambda nm: eng.view(g, nm), fts,
                                      self._last_keep, dlogits, dz)
         if dfts_extra is not None:
             dfts.add_(dfts_extra)
+        if not trunk:
+            return g
         return eng.backward(self.flat, g, dfts=dfts, zero_grad=False, grad_ready=grad_ready)
 
     def forward(self, x):

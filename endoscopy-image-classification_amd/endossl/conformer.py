@@ -620,7 +620,7 @@ class _ConvHeadFn(torch.autograd.Function):
     """AdaptiveAvgPool2d(1) + flatten + conv_cls_head Linear (Conformer.forward :438-439)."""
 
     @staticmethod
-    def forward(ctx, x, m):
+    def forward(ctx, x, m, anchor=None):
         N, H, W, C = x.shape
         ncls = m.cfg.num_classes
         pooled = torch.empty(N, C, device=x.device)
@@ -645,16 +645,18 @@ class _ConvHeadFn(torch.autograd.Function):
         call("es_dense_bwd", ptr(dl), ncls, None, 0, 0, 0.0, None, 1.0, ptr(pooled), C,
              ptr(m.pview("conv_cls_head.weight")), ptr(dpooled), C, 0, ptr(m.gview("conv_cls_head.weight")),
              ptr(m.gview("conv_cls_head.bias")), N, C, ncls, ptr(ws), _s())
+        if getattr(m, "frozen_trunk", False):  # IS_FREEZE: the head's parameters only
+            return None, None, None
         dx = torch.empty(N, H, W, C, device=dl.device)
         call("es_avgpool2d_bwd", ptr(dpooled), N, H, W, C, H, ptr(dx), 0, _s())
-        return dx, None
+        return dx, None, None
 
 
 class _TransHeadFn(torch.autograd.Function):
     """trans_norm (LayerNorm eps 1e-5) + trans_cls_head on the CLS token (Conformer.forward :441-443)."""
 
     @staticmethod
-    def forward(ctx, xt, m):
+    def forward(ctx, xt, m, anchor=None):
         cfg = m.cfg
         n, D, ncls = m.cur_n, cfg.dim, cfg.num_classes
         logits = torch.empty(n, ncls, device=xt.device)
@@ -674,13 +676,16 @@ class _TransHeadFn(torch.autograd.Function):
         m, n = ctx.m, ctx.n
         cfg = m.cfg
         D, ncls = cfg.dim, cfg.num_classes
-        dx = torch.zeros(ctx.Mp, D, device=dl.device)
+        frozen = getattr(m, "frozen_trunk", False)  # IS_FREEZE: trans_norm frozen, no input gradient
+        dx = torch.zeros(ctx.Mp if not frozen else n, D, device=dl.device)
         dyn = torch.empty(n, D, device=dl.device)
+        gn = (m.gview("trans_norm.weight"), m.gview("trans_norm.bias")) if not frozen else \
+            (torch.zeros(D, device=dl.device), torch.zeros(D, device=dl.device))
         call("es_cls_head_bwd", ptr(dl.contiguous()), ncls, ptr(m.pview("trans_cls_head.weight")),
              ptr(m.pview("trans_norm.weight")), ptr(m.pview("trans_norm.bias")), ptr(xhat), ptr(rstd), ptr(dyn),
-             ptr(dx), D, cfg.T, ptr(m.gview("trans_cls_head.weight")), ptr(m.gview("trans_cls_head.bias")),
-             ptr(m.gview("trans_norm.weight")), ptr(m.gview("trans_norm.bias")), n, D, ncls, _s())
-        return dx, None
+             ptr(dx), D, cfg.T if not frozen else 1, ptr(m.gview("trans_cls_head.weight")),
+             ptr(m.gview("trans_cls_head.bias")), ptr(gn[0]), ptr(gn[1]), n, D, ncls, _s())
+        return (dx if not frozen else None), None, None
 
 
 # ------------------------------------------------------------------------------------ model
@@ -866,8 +871,11 @@ class NativeConformer(nn.Module):
         x = x.permute(0, 2, 3, 1).contiguous()
         img = _Map(x, n, S, S, 3, sn=3 * S * S, sh=3 * S, sw=3, sc=1)
         # the parameters are not autograd inputs (their gradients go straight to flat_grad): a leaf that
-        # requires grad, passed to the stem conv, puts the graph on the tape in training mode
-        anchor = self._anchor if (torch.is_grad_enabled() and self.training) else None
+        # requires grad, passed to the stem conv, puts the graph on the tape in training mode.  With a
+        # frozen trunk (IS_FREEZE) the leaf goes to the two heads instead: only they run a backward
+        on_tape = torch.is_grad_enabled() and self.training
+        frozen = getattr(self, "frozen_trunk", False)
+        anchor = self._anchor if (on_tape and not frozen) else None
         h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor)
         x_base = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1)
         main = torch.cuda.current_stream(x.device)
@@ -901,8 +909,9 @@ class NativeConformer(nn.Module):
             to_main(up)
             xc = self._conv_block(pre + "fusion_block.", xc, 2 if last else 1, last, x_t=up, return_x2=False)
         to_main(xt)
-        conv_cls = _ConvHeadFn.apply(xc, self)
-        trans_cls = _TransHeadFn.apply(xt, self)
+        head_anchor = self._anchor if (on_tape and frozen) else None
+        conv_cls = _ConvHeadFn.apply(xc, self, head_anchor)
+        trans_cls = _TransHeadFn.apply(xt, self, head_anchor)
         return conv_cls, trans_cls
 
     def _trans_branch(self, pre, x2, xt, dw, med):

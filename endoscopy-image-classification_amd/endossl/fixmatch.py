@@ -61,12 +61,21 @@ class FixMatch:
         self.valid_dl = valid_dl
         self.test_dl = test_dl
 
+    def _trainable_when_frozen(self):
+        """The modules IS_FREEZE keeps trainable (code/fixmatch.py:45-48: `model.fc`)."""
+        return [self.model.fc]
+
     def get_config(self, config):
         self.config = config
-        if config.TRAIN.IS_FREEZE:
-            raise NotImplementedError("IS_FREEZE (head-only training) is not on the native SSL path yet")
+        # code/fixmatch.py:40-52: IS_FREEZE trains `model.fc` only (timm ViT: the classifier head).  The
+        # native step then runs both forwards in inference form (no saved activations) and the head's
+        # backward alone (Engine.head_backward): the trunk gets exactly zero gradient and no update
+        self.frozen = bool(config.TRAIN.IS_FREEZE)
         for p in self.model.parameters():
-            p.requires_grad = True
+            p.requires_grad = not self.frozen
+        if self.frozen:
+            for mod in self._trainable_when_frozen():
+                mod.requires_grad_(True)
         # identical replicas on every rank before the first step
         dist.broadcast_(self.model.flat)
         self.model.mark_updated()
@@ -106,16 +115,17 @@ class FixMatch:
             self._pl = torch.empty(nu, dtype=torch.int32, device=dev)
             self._mask = torch.empty(nu, dtype=torch.uint8, device=dev)
         stats = torch.empty(4, dtype=torch.float32, device=dev)  # lx, lu, mask_mean, total
+        frozen = getattr(self, "frozen", False)
         if eng.overlap_fwd:  # weak forward on the side stream, beside the train forward
             main, side = torch.cuda.current_stream(dev), eng.side_stream()
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 logits_w = eng.forward(m.flat, [inputs_u_w], train=False)
-            logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=True)
+            logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=not frozen)
             main.wait_stream(side)
         else:
             logits_w = eng.forward(m.flat, [inputs_u_w], train=False)
-            logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=True)
+            logits = eng.forward(m.flat, [inputs_x, inputs_u_s], train=not frozen)
         dl = self._dlogits
         call("es_poly_ce_fwd_bwd", ptr(logits), C, ptr(targets_x), ptr(self.class_weights), B, C, 2.0, 1.0 / B,
              ptr(dl), C, ptr(stats[0:1]), s)
@@ -123,6 +133,9 @@ class FixMatch:
         call("es_fm_consistency_fwd_bwd", ptr(logits_w), C, ptr(logits[B:]), C, nu, C, float(cfg.TRAIN.THRES),
              lam / nu, ptr(self._pl), ptr(self._mask), None, ptr(dl[B:]), C, ptr(stats[1:3]), s)
         torch.add(stats[0], stats[1], alpha=lam, out=stats[3])
+        if frozen:
+            eng.head_backward(m.flat, m.flat_grad, dl, train=False)
+            return stats, None
         gb = dist.GradBuckets(m.flat_grad) if dist.world_size() > 1 and self.overlap_allreduce else None
         eng.backward(m.flat, m.flat_grad, dl, grad_ready=gb.ready if gb is not None else None)
         return stats, gb
@@ -249,8 +262,12 @@ class FixMatch:
     def load_checkpoint(self, checkpoint_dir, is_train=False):
         checkpoint = torch.load(checkpoint_dir, map_location='cpu', weights_only=True)
         self.model.load_state_dict(checkpoint['model_state_dict'])
+        # code/fixmatch.py:204-216: is_train -> trainable again (the IS_FREEZE split re-applied), else frozen
         for p in self.model.parameters():
-            p.requires_grad = bool(is_train)
+            p.requires_grad = bool(is_train) and not getattr(self, "frozen", False)
+        if is_train and getattr(self, "frozen", False):
+            for mod in self._trainable_when_frozen():
+                mod.requires_grad_(True)
         if self.config.TRAIN.USE_EMA:
             self.ema_model.ema.load_state_dict(checkpoint['ema_state_dict'])
         self.epoch_start = checkpoint['epoch']

@@ -50,8 +50,16 @@ class SemiFormer:
         self.model.mark_updated()
         self.ema_model = ModelEMA(model=self.model, decay=config.TRAIN.EMA_DECAY, device=self.device) \
             if config.TRAIN.USE_EMA else None
-        if config.TRAIN.IS_FREEZE:
-            raise NotImplementedError("IS_FREEZE (heads-only training) is not on the native SSL path")
+        # code/semiformer.py:50-56: IS_FREEZE trains conv_cls_head and trans_cls_head only; the native
+        # forward then keeps the trunk off the autograd tape (NativeConformer.frozen_trunk) so only the
+        # heads' backward runs, and the trunk's gradient stays exactly zero
+        self.frozen = bool(config.TRAIN.IS_FREEZE)
+        self.model.frozen_trunk = self.frozen
+        if self.frozen:
+            for p in self.model.parameters():
+                p.requires_grad = False
+            self.model.conv_cls_head.requires_grad_(True)
+            self.model.trans_cls_head.requires_grad_(True)
         self.optimizer = build_optimizer(self.model, opt_func=self.opt_func, lr=config.TRAIN.BASE_LR)
         self.lr_scheduler = build_scheduler(config=config, optimizer=self.optimizer,
                                             n_iter_per_epoch=config.TRAIN.EVAL_STEP)

@@ -715,6 +715,28 @@ class Engine:
         return grad
 
 
+    def head_backward(self, flat, grad, dlogits, train=False):
+        """IS_FREEZE (code/fixmatch.py:40-48: every parameter frozen but `model.fc`, timm's `head`):
+        grad <- d(loss)/d(head.weight, head.bias) only, from the CLS features the forward (train or
+        inference form) normalised; every other entry of grad is zero, so the fused Adam sweep leaves
+        the frozen parameters exactly unchanged (zero gradient, zero moments)."""
+        cfg = self.cfg
+        if cfg.head != "cls":
+            raise ValueError("head_backward is the classifier-head model's; the emb-head model runs its heads' "
+                             "backward in comatch_model.EmbHeads")
+        n, D, C = int(dlogits.shape[0]), cfg.dim, cfg.num_classes
+        A = self.acts(n, train)
+        if getattr(self, "_hb", None) is None or self._hb[0].shape[0] < n:
+            z = lambda *sh: torch.zeros(*sh, dtype=torch.float32, device=self.device)  # noqa: E731
+            self._hb = (z(n, D), z(n, D), z(D), z(D))  # dyn, dx (CLS rows), frozen-norm gradients
+        dyn, dx, gnw, gnb = self._hb
+        grad.zero_()
+        self._call("es_cls_head_bwd", ptr(dlogits.contiguous()), C, ptr(self.view(flat, "head.weight")),
+                   ptr(self.view(flat, "norm.weight")), ptr(self.view(flat, "norm.bias")), ptr(A.xhat),
+                   ptr(A.rstd_cls), ptr(dyn), ptr(dx), D, 1, ptr(self.view(grad, "head.weight")),
+                   ptr(self.view(grad, "head.bias")), ptr(gnw), ptr(gnb), n, D, C, _lib.stream())
+        return grad
+
     def _backward_lanes(self, flat, grad, A, dx_full, nh):
         """Two-lane reverse pass (see LANES): lane 0 = images [0, nh) on the caller's stream into
         `grad`, lane 1 = images [nh, 2 nh) on the side stream into a second flat gradient.  dx_full
