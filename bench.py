@@ -73,10 +73,40 @@ def synth_images(n, size, gen, device):
     return x.sub_(m).div_(s)
 
 
+def host_cpus():
+    """CPUs this process may actually use: os.cpu_count() capped by the affinity mask and the cgroup
+    CPU quota (a GPU box shows the whole machine's 256 threads but grants a share of them)."""
+    n = os.cpu_count() or 1
+    info = {"os.cpu_count": n}
+    try:
+        aff = len(os.sched_getaffinity(0))
+        info["affinity"] = aff
+        n = min(n, aff)
+    except (AttributeError, OSError):
+        pass
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            txt = open(path).read().split()
+            if path.endswith("cpu.max") and txt[0] != "max":
+                q = int(txt[0]) / int(txt[1])
+            elif path.endswith("quota_us") and int(txt[0]) > 0:
+                q = int(txt[0]) / int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            else:
+                continue
+            info["cgroup_quota"] = q
+            n = min(n, max(1, int(q)))
+            break
+        except (OSError, ValueError, IndexError):
+            continue
+    return n, info
+
+
 def cpu_baseline(B=8, MU=7, steps=2):
-    """Oracle (pinned CPU restatement) FixMatch step on every host core -- a reported baseline."""
+    """Oracle (pinned CPU restatement) FixMatch step on every host core this process may use -- a
+    reported baseline (torch.set_num_threads(os.cpu_count()), capped by the CPU share the
+    box grants: more threads than cores only oversubscribes)."""
     from oracle import ref
-    threads = os.cpu_count() or 1
+    threads, cpu_info = host_cpus()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     cfg = ref.Cfg()
@@ -88,9 +118,11 @@ def cpu_baseline(B=8, MU=7, steps=2):
     uw = synth_images(B * MU, 224, g, "cpu")
     us = synth_images(B * MU, 224, g, "cpu")
     fm.step(x, y, uw, us)  # warm-up
+    print(f"cpu_baseline: warm-up step done on {threads} threads", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for i in range(steps):
         fm.step(x, y, uw, us)
+        print(f"cpu_baseline: step {i + 1}/{steps}", file=sys.stderr, flush=True)
     dt = (time.perf_counter() - t0) / steps
     used = torch.get_num_threads()
     torch.set_num_threads(prev)
@@ -105,7 +137,7 @@ def cpu_baseline(B=8, MU=7, steps=2):
     return {"value": round(B * MU / dt, 3), "unit": "unlabeled images/s", "cores": used,
             "kind": "port",
             "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step), "
-                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', os.cpu_count()={os.cpu_count()}, "
+                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', host CPUs {cpu_info}, "
                       f"torch.get_num_threads()={used}"}
 
 
