@@ -172,6 +172,119 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
   }
 }
 
+// ---- long sequences (256 < T <= 640: ViT/16 at 384^2, T = 577) ------------------------------------
+// K and V of the head staged in LDS (2 x 74 KiB at T = 577; Q can no longer ride along), Q fragments
+// straight from HBM, eight waves per workgroup.  The scores of a 16-query block are taken over key
+// chunks of FCH 16-key tiles with an online softmax (running max / sum, the output rescaled when the
+// max grows), so the registers hold FCH tiles instead of all NT16.  Rounding points as the short
+// kernel: scores in log2 units, bf16(P) into P.V, fp32 accumulation; P is exp2(s - running max).
+constexpr int FCH = 8;
+
+template <int NT>
+__device__ __forceinline__ void fwd_long_chunk(const char* Ks, const char* Vs, int t0, int T, float sl, int g, int r,
+                                               const bf16x8& qf0, const bf16x8& qf1, float& m, float& l, f32x4* o) {
+  f32x4 s[NT];
+  float cm = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int kt = t0 + t;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = mfma16(lds_row8(Ks, kt * 16 + r, g), qf0, acc);
+    acc = mfma16(lds_row8(Ks, kt * 16 + r, 4 + g), qf1, acc);
+    acc *= sl;
+    if (kt * 16 + 16 > T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (kt * 16 + 4 * g + i >= T) acc[i] = -INFINITY;
+    }
+    cm = fmaxf(cm, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
+    s[t] = acc;
+  }
+  cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
+  cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
+  const float mn = fmaxf(m, cm);
+  const float alpha = __builtin_amdgcn_exp2f(m - mn);  // 0 on the first chunk (m = -inf)
+  l *= alpha;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+  m = mn;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float pv = __builtin_amdgcn_exp2f(s[t][i] - mn);
+      s[t][i] = pv;
+      l += pv;
+    }
+#pragma unroll
+  for (int sc = 0; sc < NT / 2; ++sc) {
+    bf16x8 pf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pf[i] = (bf16)s[2 * sc][i];
+      pf[4 + i] = (bf16)s[2 * sc + 1][i];
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16(lds_trT(Vs, (t0 + 2 * sc) * 16, dt * 16, g, r), pf, o[dt]);
+  }
+  if constexpr (NT & 1) {
+    const bf16x4 pf = {(bf16)s[NT - 1][0], (bf16)s[NT - 1][1], (bf16)s[NT - 1][2], (bf16)s[NT - 1][3]};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16k16(lds_trT4(Vs, (t0 + NT - 1) * 16, dt * 16, g, r), pf, o[dt]);
+  }
+}
+
+template <int NT16>
+__global__ __launch_bounds__(512) void attn_fwd_long_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TP = NT16 * 16;
+  const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
+  const int D = a.H * 64, T = a.T;
+  const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
+  char* Ks = smem;
+  char* Vs = smem + TP * 128;
+  {  // stage K and V with all eight waves (stage_head assumes four)
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int i = w; i < 2 * (TP / 8); i += 8) {
+      const int which = i >= TP / 8, ii = which ? i - TP / 8 : i;
+      const int row = ii * 8 + (lane >> 3);
+      const int sr = row < T ? row : T - 1;
+      glds16(base + (which ? 2 * D : D) + h * 64 + (size_t)sr * a.ldqkv + aswz(row, lane & 7) * 8,
+             (which ? Vs : Ks) + ii * 1024);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  const int nqt = (T + 15) >> 4;
+  const float sl = a.scale * 1.44269504088896341f;
+  for (int qb = w; qb < nqt; qb += 8) {
+    const int q = qb * 16 + r;
+    const bool qv = q < T;
+    const bf16* qrow = base + (size_t)(qv ? q : T - 1) * a.ldqkv + h * 64;
+    const bf16x8 qf0 = *(const bf16x8*)(qrow + 8 * g), qf1 = *(const bf16x8*)(qrow + 32 + 8 * g);
+    float m = -INFINITY, l = 0.f;
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int c = 0; c < NT16 / FCH; ++c) fwd_long_chunk<FCH>(Ks, Vs, c * FCH, T, sl, g, r, qf0, qf1, m, l, o);
+    if constexpr (NT16 % FCH) fwd_long_chunk<NT16 % FCH>(Ks, Vs, NT16 - NT16 % FCH, T, sl, g, r, qf0, qf1, m, l, o);
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    if (qv) {
+      const float inv = 1.0f / l;
+      bf16* orow = a.o + (size_t)(img * T + q) * a.ldo + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 v = {(bf16)(o[dt][0] * inv), (bf16)(o[dt][1] * inv), (bf16)(o[dt][2] * inv), (bf16)(o[dt][3] * inv)};
+        *(bf16x4*)(orow + dt * 16 + 4 * g) = v;
+      }
+      if (g == 0) a.lse[(size_t)bh * T + q] = (m + __log2f(l)) * 0.69314718055994531f;  // natural log
+    }
+  }
+}
+
 // dQ: query on the lane; delta = rowsum(dO * O) computed in-register for the wave's queries.
 template <int NT16>
 __global__ __launch_bounds__(256, 3) void attn_bwd_dq_kernel(AttnArgs a) {
@@ -384,7 +497,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
 // dot product with 3 xor-shuffles.  Same rounding points as attn_fwd_kernel / the backward kernels
 // (scores in log2 units, bf16(P) into P.V, bf16(dS) into dQ / dK, bf16(P) into dV); only the fp32
 // summation order differs.  Outputs are compact: o / do [img][D], lse [img][head].
-constexpr int CLS_KMAX = 32;  // keys per lane group: T <= 256
+constexpr int CLS_KMAX = 32;       // keys per lane group: T <= 256
+constexpr int CLS_KMAX_LONG = 80;  // T <= 640 (ViT/16 at 384^2: 577)
 
 __device__ __forceinline__ float grp8_sum(float v) {
   v += __shfl_xor(v, 1, 64);
@@ -399,6 +513,7 @@ __device__ __forceinline__ void ld8f(const bf16* p, float* f) {
   for (int i = 0; i < 8; ++i) f[i] = (float)v[i];
 }
 
+template <int KMAX>
 __global__ __launch_bounds__(64) void attn_cls_fwd_kernel(const bf16* __restrict__ qkv, int ldqkv, bf16* __restrict__ o,
                                                           int ldo, float* __restrict__ lse, int T, int H, float scale) {
   const int bh = blockIdx.x, img = bh / H, h = bh - img * H, D = H * 64;
@@ -407,10 +522,10 @@ __global__ __launch_bounds__(64) void attn_cls_fwd_kernel(const bf16* __restrict
   float q[8];
   ld8f(base + h * 64 + 8 * c, q);
   const float sl = scale * 1.44269504088896341f;
-  float s[CLS_KMAX];
+  float s[KMAX];
   float mx = -INFINITY;
 #pragma unroll
-  for (int it = 0; it < CLS_KMAX; ++it) {
+  for (int it = 0; it < KMAX; ++it) {
     const int j = it * 8 + jg;
     float part = 0.f;
     if (j < T) {
@@ -428,7 +543,7 @@ __global__ __launch_bounds__(64) void attn_cls_fwd_kernel(const bf16* __restrict
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float l = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int it = 0; it < CLS_KMAX; ++it) {
+  for (int it = 0; it < KMAX; ++it) {
     const int j = it * 8 + jg;
     if (j < T) {
       const float p = __builtin_amdgcn_exp2f(s[it] - mx);
@@ -458,6 +573,7 @@ __global__ __launch_bounds__(64) void attn_cls_fwd_kernel(const bf16* __restrict
 
 // dQ (CLS row), dK / dV (every key) and zeros for the Q part of the other rows: the whole dqkv of
 // the block's tokens, so the qkv data / weight gradient GEMMs read it as written by es_attn_bwd.
+template <int KMAX>
 __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict__ qkv, int ldqkv,
                                                           const bf16* __restrict__ o, int ldo,
                                                           const float* __restrict__ lse,
@@ -480,7 +596,7 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
   const float lq = lse[bh] * 1.44269504088896341f;
   float dqa[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const bf16x8 zero8 = {};
-  for (int it = 0; it < CLS_KMAX; ++it) {
+  for (int it = 0; it < KMAX; ++it) {
     const int j = it * 8 + jg;
     if (it * 8 >= T) break;
     float k[8], v[8];
@@ -537,6 +653,7 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
     ATTN_CASE(KERNEL, 11, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 12, GRID, LDS, STREAM, ARGS)          \
     ATTN_CASE(KERNEL, 13, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 14, GRID, LDS, STREAM, ARGS)          \
     ATTN_CASE(KERNEL, 15, GRID, LDS, STREAM, ARGS) ATTN_CASE(KERNEL, 16, GRID, LDS, STREAM, ARGS)          \
+    ATTN_CASE(KERNEL, 37, GRID, LDS, STREAM, ARGS)                                                        \
     default: return ES_BAD_SHAPE;                                                                         \
   }
 
@@ -575,13 +692,25 @@ int es_set_attn_variant(int occ) {
 }
 
 
-// qkv [nimg*T, ldqkv] -> o [nimg*T, ldo], lse [nimg*H*T]; head dim 64, T <= 256.
+// 16-key tiles of a head: exact for T <= 256; one 37-tile instantiation (592 rows: two staged heads
+// fit the 160 KiB of LDS) covers 256 < T <= 592 (ViT/16 at 384^2, T = 577), rows past T masked
+static int attn_tiles(int T) { return T <= 256 ? (T + 15) / 16 : 37; }
+constexpr int ATTN_TMAX = 592;
+
+// qkv [nimg*T, ldqkv] -> o [nimg*T, ldo], lse [nimg*H*T]; head dim 64, T <= 592.
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || ldo < H * 64 || (ldqkv % 8) || (ldo % 8))
+  if (nimg <= 0 || T <= 0 || T > ATTN_TMAX || H <= 0 || ldqkv < 3 * H * 64 || ldo < H * 64 || (ldqkv % 8) ||
+      (ldo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, lse, nullptr, nullptr, nullptr, ldqkv, ldo, 0, 0, T, H, scale};
+  if (T > 256) {  // online softmax over key chunks, K / V staged, eight waves
+    const size_t lds = 2 * (size_t)37 * 16 * 128;
+    allow_lds(attn_fwd_long_kernel<37>, lds);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_fwd_long_kernel<37>), nimg * H, 512, lds, stream, a);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   const int nt16 = (T + 15) / 16;
   const size_t lds = 3 * (size_t)nt16 * 16 * 128;  // K, V, Q head tiles (two heads per CU at T = 197)
   if (g_attn_fwd_occ == 2) {
@@ -596,13 +725,13 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
 // delta: workspace [nimg*H*T] fp32 (rowsum(dO*O), written by the dQ pass, read by the dK/dV pass).
 int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
                 int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
+  if (nimg <= 0 || T <= 0 || T > ATTN_TMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
       (lddqkv % 8) || (ldo % 8) || (lddo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse || !delta || !dout || !dqkv) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, delta, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
              lddqkv, T, H, scale};
-  const int nt16 = (T + 15) / 16;
+  const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
   ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
@@ -616,13 +745,13 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
 int es_attn_bwd_dq(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta,
                    const void* dout, int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale,
                    hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
+  if (nimg <= 0 || T <= 0 || T > ATTN_TMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
       (lddqkv % 8) || (ldo % 8) || (lddo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse || !delta || !dout || !dqkv) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, delta, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
              lddqkv, T, H, scale};
-  const int nt16 = (T + 15) / 16;
+  const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -631,13 +760,13 @@ int es_attn_bwd_dq(const void* qkv, int ldqkv, const void* o, int ldo, const flo
 #define DKV_SELF(N_) attn_bwd_dkv_kernel<N_, true>
 int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
                     void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > 256 || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
+  if (nimg <= 0 || T <= 0 || T > ATTN_TMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
       (lddqkv % 8) || (ldo % 8) || (lddo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse || !dout || !dqkv) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, nullptr, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
              lddqkv, T, H, scale};
-  const int nt16 = (T + 15) / 16;
+  const int nt16 = attn_tiles(T);
   const size_t lds_dkv = 2 * (size_t)nt16 * 16 * 128 + 2 * (size_t)nt16 * 16 * 4;
   switch (nt16) {
 #define DKV_CASE(N_)                                                                                   \
@@ -646,7 +775,7 @@ int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const fl
     hipLaunchKernelGGL(HIP_KERNEL_NAME(DKV_SELF(N_)), nimg * H, 256, lds_dkv, stream, a);             \
     break;
     DKV_CASE(1) DKV_CASE(2) DKV_CASE(3) DKV_CASE(4) DKV_CASE(5) DKV_CASE(6) DKV_CASE(7) DKV_CASE(8)
-    DKV_CASE(9) DKV_CASE(10) DKV_CASE(11) DKV_CASE(12) DKV_CASE(13) DKV_CASE(14) DKV_CASE(15) DKV_CASE(16)
+    DKV_CASE(9) DKV_CASE(10) DKV_CASE(11) DKV_CASE(12) DKV_CASE(13) DKV_CASE(14) DKV_CASE(15) DKV_CASE(16) DKV_CASE(37)
 #undef DKV_CASE
     default: return ES_BAD_SHAPE;
   }
@@ -658,12 +787,16 @@ int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const fl
 // [nimg*T, ldqkv] -> o [nimg, ldo] (the CLS rows only, compact), lse [nimg*H].
 int es_attn_cls_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                     hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > 8 * CLS_KMAX || H <= 0 || ldqkv < 3 * H * 64 || ldo < H * 64 || (ldqkv % 8) ||
+  if (nimg <= 0 || T <= 0 || T > 8 * CLS_KMAX_LONG || H <= 0 || ldqkv < 3 * H * 64 || ldo < H * 64 || (ldqkv % 8) ||
       (ldo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse) return ES_BAD_ARG;
-  hipLaunchKernelGGL(attn_cls_fwd_kernel, nimg * H, 64, 0, stream, (const bf16*)qkv, ldqkv, (bf16*)o, ldo, lse, T, H,
-                     scale);
+  if (T <= 8 * CLS_KMAX)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_cls_fwd_kernel<CLS_KMAX>), nimg * H, 64, 0, stream, (const bf16*)qkv, ldqkv,
+                       (bf16*)o, ldo, lse, T, H, scale);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_cls_fwd_kernel<CLS_KMAX_LONG>), nimg * H, 64, 0, stream, (const bf16*)qkv,
+                       ldqkv, (bf16*)o, ldo, lse, T, H, scale);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -671,12 +804,16 @@ int es_attn_cls_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, in
 // (q part zero except the CLS rows).
 int es_attn_cls_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
                     void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > 8 * CLS_KMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 ||
+  if (nimg <= 0 || T <= 0 || T > 8 * CLS_KMAX_LONG || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 ||
       ldo < H * 64 || lddo < H * 64 || (ldqkv % 8) || (lddqkv % 8) || (ldo % 8) || (lddo % 8))
     return ES_BAD_SHAPE;
   if (!qkv || !o || !lse || !dout || !dqkv) return ES_BAD_ARG;
-  hipLaunchKernelGGL(attn_cls_bwd_kernel, nimg * H, 64, 0, stream, (const bf16*)qkv, ldqkv, (const bf16*)o, ldo, lse,
-                     (const bf16*)dout, lddo, (bf16*)dqkv, lddqkv, T, H, scale);
+  if (T <= 8 * CLS_KMAX)
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_cls_bwd_kernel<CLS_KMAX>), nimg * H, 64, 0, stream, (const bf16*)qkv, ldqkv,
+                       (const bf16*)o, ldo, lse, (const bf16*)dout, lddo, (bf16*)dqkv, lddqkv, T, H, scale);
+  else
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_cls_bwd_kernel<CLS_KMAX_LONG>), nimg * H, 64, 0, stream, (const bf16*)qkv,
+                       ldqkv, (const bf16*)o, ldo, lse, (const bf16*)dout, lddo, (bf16*)dqkv, lddqkv, T, H, scale);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

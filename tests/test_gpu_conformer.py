@@ -314,6 +314,27 @@ def test_conformer_forward_backward_vs_oracle(golden):
     m, state = _model_from_fixture(d)
     _, ocfg = _tiny_cfgs()
     x = torch.cat([torch.tensor(d[k]) for k in ("x0", "uw0", "us0")])
+    _check_model_vs_oracle(m, state, ocfg, x, ("bn1.running_mean", "conv_trans_4.fusion_block.bn2.running_var",
+                                              "conv_trans_6.expand_block.bn.running_mean"))
+
+
+def test_conformer_vit_b_384_forward_backward_vs_oracle():
+    """The SemiFormer stress shape (BASELINE configs[4]: a ViT-Base/16 transformer branch at 384^2):
+    D = 768, 12 heads, T = 577 tokens (the long-sequence attention kernels, online softmax), on a
+    CNN branch narrowed to base 16 channels and depth 3 so the CPU oracle finishes in seconds."""
+    from endossl.conformer import ConformerConfig, NativeConformer
+    kw = dict(img_size=384, patch=16, base_channel=16, channel_ratio=1, embed_dim=768, depth=3, heads=12,
+              num_classes=23)
+    ncfg, ocfg = ConformerConfig(**kw), cr.ConformerCfg(**kw)
+    assert ncfg.T == 577
+    m = NativeConformer(ncfg, seed=5)
+    state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    x = torch.randn(3, 3, 384, 384, generator=torch.Generator().manual_seed(8))
+    _check_model_vs_oracle(m, state, ocfg, x, ("bn1.running_mean", "conv_trans_2.fusion_block.bn2.running_var"))
+
+
+def _check_model_vs_oracle(m, state, ocfg, x, bn_keys):
     rec = {}
     res = {}
     for bf in (True, False):
@@ -332,7 +353,7 @@ def test_conformer_forward_backward_vs_oracle(golden):
         rec[name] = {"hip_vs_bf16_contract": e16, "bf16_envelope": env, "scale": sc}
         assert e16 <= 1e-3 * sc + 0.25 * env, rec
     # BatchNorm running statistics after the train-mode forward
-    for k in ("bn1.running_mean", "conv_trans_4.fusion_block.bn2.running_var", "conv_trans_6.expand_block.bn.running_mean"):
+    for k in bn_keys:
         _close(m.get_buffer(k).cpu(), res[True][3][k], atol=2e-3)
     assert int(m.get_buffer("bn1.num_batches_tracked").item()) == int(state["bn1.num_batches_tracked"].item()) + 1
     # gradients of a fixed random linear functional of both heads

@@ -193,7 +193,8 @@ def attn_occ(request):
     _lib.load().es_set_attn_variant(old)
 
 
-@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 64, 1), (2, 250, 2), (3, 40, 2), (2, 1, 1)])
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 64, 1), (2, 250, 2), (3, 40, 2), (2, 1, 1),
+                                   (2, 577, 3), (1, 300, 1)])
 def test_attention_fwd(n, T, H, attn_occ):
     torch.manual_seed(T)
     D = H * 64
@@ -207,7 +208,8 @@ def test_attention_fwd(n, T, H, attn_occ):
     assert torch.all(o[n * T:] == 0)
 
 
-@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 17, 2), (3, 40, 2), (2, 250, 1), (2, 1, 1)])
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 17, 2), (3, 40, 2), (2, 250, 1), (2, 1, 1), (2, 577, 3),
+                                   (1, 300, 1)])
 def test_attention_bwd(n, T, H):
     torch.manual_seed(100 + T)
     D = H * 64
@@ -245,7 +247,8 @@ def test_attention_bwd(n, T, H):
     torch.testing.assert_close(delta2, delta, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1)])
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1),
+                                   (2, 577, 2), (1, 300, 1)])
 def test_attention_cls_fwd_bwd(n, T, H):
     """es_attn_cls_fwd / _bwd (the last block's CLS queries only) against the full-token kernels at
     the CLS rows -- same rounding points, fp32 summation order only -- and against fp32 torch; the
@@ -264,8 +267,13 @@ def test_attention_cls_fwd_bwd(n, T, H):
     call("es_attn_cls_fwd", ptr(qkv), 3 * D, ptr(oc), D, ptr(lc), n, T, H, 64 ** -0.5, S())
     torch.cuda.synchronize()
     torch.testing.assert_close(lc.view(n, H), lse.view(n, H, T)[:, :, 0], rtol=1e-5, atol=1e-5)
-    # the bf16 outputs agree to within one rounding step of the output
-    assert ((oc.float() - o[cls].float()).abs() <= o[cls].float().abs() * 2 ** -7 + 1e-6).all()
+    # the bf16 outputs agree to within one rounding step of the output (past T = 256 the long kernel's
+    # online softmax rounds P against the running, not the final, row max: a bound relative to the
+    # row's scale)
+    if T <= 256:
+        assert ((oc.float() - o[cls].float()).abs() <= o[cls].float().abs() * 2 ** -7 + 1e-6).all()
+    else:
+        assert (oc.float() - o[cls].float()).abs().max() <= 1e-2 * o[cls].float().abs().max()
     o_ref, _ = _attn_ref(qkv[:n * T], n, T, H)
     torch.testing.assert_close(oc.float(), o_ref[cls], rtol=2e-2, atol=2e-2)
     # backward: dout nonzero on the CLS rows only
