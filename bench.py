@@ -228,23 +228,35 @@ def run_secondary(args):
     else:
         from endossl.conformer import ConformerConfig, NativeConformer
         from endossl.semiformer import SemiFormer
-        B, MU = 24, 7
-        ccfg = ConformerConfig()
+        MU = 7
+        if args.s1_model == "b384":
+            # BASELINE configs[4] "ViT-Base/16 at 384^2": the reference's Conformer class defaults
+            # (code/models/conformer.py:308-309: channel_ratio 4, embed_dim 768, depth 12, 12 heads) at
+            # 384^2 (577 tokens), qkv_bias as build.py builds it.  Per GPU: B labeled + 2 mu B
+            # unlabeled (B defaults to 8: ~0.75 GB of saved activations per image at this size)
+            B = args.batch if args.batch != 64 else 8
+            ccfg = ConformerConfig(img_size=384, channel_ratio=4, embed_dim=768, depth=12, heads=12)
+            name = "Conformer-B (channel_ratio 4, embed 768, depth 12, 12 heads; code/models/conformer.py:308-309)"
+        else:  # build.py's Conformer-Ti at 224^2, the B of kaggle_semisupervised_real_2.yaml:7
+            B = args.batch if args.batch != 64 else 24
+            ccfg = ConformerConfig()
+            name = "Conformer-Ti (code/build.py:135-142: patch 16, embed 384, depth 12, 6 heads, channel_ratio 1)"
+        S = ccfg.img_size
         model = NativeConformer(ccfg, seed=0)
         tr = SemiFormer(model, device=dev)
-        cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
+        cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=S, TARGET_NAME="target"),
                        MODEL=AttrDict(NAME="conformer", NUM_CLASSES=23),
                        TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, EVAL_STEP=1,
                                       EVAL_STEP_SUP=0, CLS_WEIGHT=False, THRES=0.95, T=1.0, LAMBDA_U=1.0, EPOCHS=1,
                                       WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const"))
         tr.get_dataloader((None, None), None)
         tr.get_config(cfg)
-        x, y = synth_images(B, 224, g, dev), torch.randint(0, 23, (B,), generator=g, device=dev)
-        batch = ((x, y), ((synth_images(B * MU, 224, g, dev), synth_images(B * MU, 224, g, dev)), None))
+        x, y = synth_images(B, S, g, dev), torch.randint(0, 23, (B,), generator=g, device=dev)
+        batch = ((x, y), ((synth_images(B * MU, S, g, dev), synth_images(B * MU, S, g, dev)), None))
         unl, tfl = B * MU, conformer_step_tflop(ccfg, B + 2 * B * MU)
         exe = tfl
-        desc = (f"S1: SemiFormer step on Conformer-Ti (code/build.py:135-142: patch 16, embed 384, depth 12, 6 heads, "
-                f"channel_ratio 1), B={B} + 2 x mu*B={B * MU}, 224^2, C=23, tau=0.95, lambda_u=1, EMA 0.999")
+        desc = (f"S1: SemiFormer step on {name}, {S}^2 ({ccfg.T} tokens), B={B} + 2 x mu*B={B * MU} per GPU, C=23, "
+                f"tau=0.95, lambda_u=1, EMA 0.999; convs fp32 MFMA, transformer GEMMs bf16 MFMA")
     for _ in range(args.warmup):
         tr.step(batch)
     torch.cuda.synchronize()
@@ -293,6 +305,8 @@ def main():
                     help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")
     ap.add_argument("--workload", choices=("f1", "c1", "s1"), default="f1",
                     help="f1 = the BASELINE metric (default); c1 / s1 = CoMatch / SemiFormer configs")
+    ap.add_argument("--s1-model", choices=("b384", "ti224"), default="b384",
+                    help="s1: the ViT-Base/16 384^2 stress Conformer (BASELINE configs[4]) or build.py's Conformer-Ti")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="hipGraph replay of the step's forward/backward (auto: on for N > 1; at N = 1 the "
                          "timed steps run eagerly so the roofline probe's HIP events see every launch)")
