@@ -256,7 +256,8 @@ def run_secondary(args):
         unl, tfl = B * MU, conformer_step_tflop(ccfg, B + 2 * B * MU)
         exe = tfl
         desc = (f"S1: SemiFormer step on {name}, {S}^2 ({ccfg.T} tokens), B={B} + 2 x mu*B={B * MU} per GPU, C=23, "
-                f"tau=0.95, lambda_u=1, EMA 0.999; convs fp32 MFMA, transformer GEMMs bf16 MFMA")
+                f"tau=0.95, lambda_u=1, EMA 0.999; transformer GEMMs and convs with channels % 32 == 0 on bf16 "
+                f"MFMA ({'on' if model.conv_bf16 else 'off: ENDOSSL_CONV_BF16=0'}), BatchNorm / maps fp32")
     for _ in range(args.warmup):
         tr.step(batch)
     torch.cuda.synchronize()
@@ -277,8 +278,8 @@ def run_secondary(args):
             "metric": f"unlabeled images/sec/node ({args.workload.upper()})", "value": round(world * unl * args.steps / T, 2),
             "unit": "unlabeled images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 (transformer GEMMs) / fp32", "data": "synthetic (HBM-resident, seed 0)",
-            "config": {"workload": desc, "parallelism": f"dp{world}"},
+            "dtype": "bf16 operands (GEMMs, convs) / fp32 accumulate, maps, BatchNorm",
+            "data": "synthetic (HBM-resident, seed 0)", "config": {"workload": desc, "parallelism": f"dp{world}"},
             "step_tflop": round(tfl, 3), "executed_step_tflop": round(exe, 3),
             "step_tflops": round(tfl / (ms / 1e3), 1),
             "final_loss": round(out["loss"].item(), 6)}), flush=True)

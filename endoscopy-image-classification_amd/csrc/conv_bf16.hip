@@ -1,0 +1,534 @@
+// bf16-operand MFMA convolutions for the Conformer CNN branch at ViT-B scale (SURVEY.md §8(a) a20;
+// code/models/conformer.py:75-200 ConvBlock / FCUDown / FCUUp / trans_patch_conv Conv2d calls).
+//
+//  es_conv2d_pack_bf16              weights [Cout][Cin][kh][kw] fp32 -> wp [Cout][kh kw][Cin] bf16
+//                                   (forward operand) and / or wt [Cin][kh kw][Cout] bf16 (data grad)
+//  es_conv2d_fwd_bf16               y (+)= conv(x)              implicit GEMM, rows = output pixels
+//  es_conv2d_bwd_data_bf16          dx (+)= conv^T(dy)          implicit GEMM per stride phase
+//  es_conv2d_bwd_weight_bf16        dw (+)= sum_pixels dy x im2col(x)   split over pixels + reduce
+//
+// Numerical contract (the transformer GEMMs' one): the maps stay fp32 in HBM (BatchNorm statistics,
+// residual sums and ReLU masks are fp32); the conv OPERANDS -- the gathered activation / gradient
+// tile and the weights -- are rounded to bf16 as they are staged into LDS, products accumulate in
+// fp32 on v_mfma_f32_16x16x32_bf16 (8x the fp32 MFMA rate conv.hip's kernels run at).  The fp32
+// kernels of conv.hip remain the parity mode and the path for convs these do not take (channel
+// counts not multiples of 32: the 3-channel stem, Conformer-Ti's 16-channel bottlenecks).
+//
+// Tiling.  Forward / data grad: 128 output pixels x BN (64 | 128) output channels per 256-thread
+// workgroup, 4 waves 2 x 2 (64 x BN/2 each), 32-deep K steps that each cover ONE kernel tap and 32
+// consecutive channels (C % 32 == 0), so a step's gather is one 128-byte channel run per pixel:
+// two threads per pixel, four 16-byte loads each, converted to bf16 and written to a 64-byte LDS
+// row (XOR-swizzled 16-byte chunks: conflict-free ds_read_b128 fragment reads).  The next step's
+// gathers are issued before this step's MFMAs (register double buffering, two LDS stages, one
+// barrier per step).  Weight gradient: a TN product over pixels -- 32-pixel steps, dy and im2col(x)
+// tiles stored pixel-major ([32 rows][256 B], the TN GEMM's swizzle) and read as transposed
+// fragments (ds_read_b64_tr_b16); fp32 partial slabs per pixel split, reduced in a fixed order.
+#include "common.h"
+
+namespace {
+
+// 64-byte rows (32 bf16): chunk c of row r at c ^ ((-(r >> 2)) & 3) (gemm.hip swz64)
+__device__ __forceinline__ int cswz64(int r, int c) { return c ^ ((4 - ((r >> 2) & 3)) & 3); }
+// 256-byte rows read transposed (gemm.hip swz256)
+__device__ __forceinline__ int cswz256(int r, int c) { return c ^ (((r & 3) << 1) | (((r >> 3) & 1) << 3)); }
+
+__device__ __forceinline__ u32x4 f8_to_bf16x8(f32x4 a, f32x4 b) {
+  bf16x8 o;
+  o[0] = (bf16)a[0]; o[1] = (bf16)a[1]; o[2] = (bf16)a[2]; o[3] = (bf16)a[3];
+  o[4] = (bf16)b[0]; o[5] = (bf16)b[1]; o[6] = (bf16)b[2]; o[7] = (bf16)b[3];
+  return __builtin_bit_cast(u32x4, o);
+}
+
+struct NTConv {
+  const float* src;   // gathered operand: x (forward) or dy (data grad), channel stride 1
+  const bf16* wp;     // packed weights [Ncol][kh kw][C]
+  const float* bias;  // [Ncol] or null
+  float* out;
+  int N, C, Ncol, Hs, Ws;  // C = gathered channels (Cin | Cout), Ncol = output channels (Cout | Cin)
+  long ssn, ssh, ssw;
+  int kh, kw, s, p;
+  int Ho, Wo;  // output map dims: forward y (Ho, Wo); data grad x (H, W)
+  long osn, osh, osw;
+  int accumulate;
+};
+
+constexpr int NT_BM = 128, NT_BK = 32;
+
+// out[pixel][col] (+)= bias[col] + sum_{tap, c} src[gathered pixel(tap)][c] . wp[col][tap][c]
+// DX = false: pixels (n, ho, wo); source (n, ho s - p + ky, wo s - p + kx).
+// DX = true:  blockIdx.z = stride phase (py, px); pixels (n, hq, wq) -> x pixel (hq s + py, wq s + px);
+//             taps ky = ky0 + s kyq (the only ones that reach this phase); source dy pixel
+//             (hq + qh - kyq, wq + qw - kxq) (conv.hip conv_dx_kernel's decomposition).
+template <int BN, bool DX>
+__global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
+  constexpr int NF = BN / 32;       // 16-col fragments per wave (wave covers BN / 2 cols)
+  constexpr int BJ = BN / 64;       // 16-byte weight loads per thread per step
+  constexpr int ABYTES = NT_BM * 64, BBYTES = BN * 64, STAGE = ABYTES + BBYTES;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+
+  int Hm, Wm, ra, ca, cb, sy, twx, twy, by0, bx0, bs, om, oa0, ob0;
+  if constexpr (!DX) {
+    Hm = a.Ho; Wm = a.Wo; ra = a.s; ca = -a.p; cb = -a.p; sy = 1; twy = a.kh; twx = a.kw;
+    by0 = 0; bx0 = 0; bs = 1; om = 1; oa0 = 0; ob0 = 0;
+  } else {
+    const int s = a.s, py = blockIdx.z / s, px = blockIdx.z - py * s;
+    Hm = (a.Ho - py + s - 1) / s;
+    Wm = (a.Wo - px + s - 1) / s;
+    const int ky0 = (py + a.p) % s, kx0 = (px + a.p) % s;
+    twy = a.kh > ky0 ? (a.kh - ky0 + s - 1) / s : 0;
+    twx = a.kw > kx0 ? (a.kw - kx0 + s - 1) / s : 0;
+    ca = (py + a.p - ky0) / s; cb = (px + a.p - kx0) / s; ra = 1; sy = -1;
+    by0 = ky0; bx0 = kx0; bs = s; om = s; oa0 = py; ob0 = px;
+  }
+  const int M = a.N * Hm * Wm;
+  const int m0 = blockIdx.x * NT_BM, n0 = blockIdx.y * BN;
+  if (m0 >= M) return;  // a smaller stride phase (block-uniform)
+  const int nk = twy * twx * (a.C / NT_BK);
+  const int Kfull = a.kh * a.kw * a.C;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+
+  // gather slots: pixel row arow (2 threads per pixel, 16 channels each)
+  const int arow = tid >> 1, ahalf = tid & 1;
+  const int am = m0 + arow;
+  const bool am_ok = am < M;
+  long abase = 0;
+  int ahb = -(1 << 28), awb = 0;
+  if (am_ok) {
+    const int bb = am % Wm, t = am / Wm, aa = t % Hm, n = t / Hm;
+    abase = (long)n * a.ssn + ahalf * 16;
+    ahb = aa * ra + ca;
+    awb = bb * ra + cb;
+  }
+  const int bchunk = tid & 3, brow0 = tid >> 2;
+
+  f32x4 ra4[4];
+  u32x4 rb[BJ];
+  auto load = [&](int kt) {
+    const int k0 = kt * NT_BK;
+    const int tq = k0 / a.C, c0 = k0 - tq * a.C;
+    const int tyq = tq / twx, txq = tq - tyq * twx;
+    const int h = ahb + sy * tyq, ww = awb + sy * txq;
+    const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
+    if (ok) {
+      const f32x4* src = (const f32x4*)(a.src + abase + (long)h * a.ssh + (long)ww * a.ssw + c0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ra4[e] = src[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) ra4[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int btap = (by0 + tyq * bs) * a.kw + bx0 + txq * bs;
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const int col = n0 + brow0 + 64 * j;
+      rb[j] = col < a.Ncol ? *(const u32x4*)(a.wp + (long)col * Kfull + btap * a.C + c0 + bchunk * 8)
+                           : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&](int buf) {
+    char* As = smem + buf * STAGE;
+    char* Bs = As + ABYTES;
+    *(u32x4*)(As + arow * 64 + cswz64(arow, ahalf * 2) * 16) = f8_to_bf16x8(ra4[0], ra4[1]);
+    *(u32x4*)(As + arow * 64 + cswz64(arow, ahalf * 2 + 1) * 16) = f8_to_bf16x8(ra4[2], ra4[3]);
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const int br = brow0 + 64 * j;
+      *(u32x4*)(Bs + br * 64 + cswz64(br, bchunk) * 16) = rb[j];
+    }
+  };
+
+  const int wm = w >> 1, wn = w & 1;
+  f32x4 acc[4][NF];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    load(0);  // a pixel row past M gathers zeros (its h base is far out of range)
+    store(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load(kt + 1);
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + ABYTES;
+    bf16x8 af[4], bfr[NF];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = wm * 64 + i * 16 + r;
+      af[i] = *(const bf16x8*)(As + rr * 64 + cswz64(rr, g) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int rr = wn * (BN / 2) + j * 16 + r;
+      bfr[j] = *(const bf16x8*)(Bs + rr * 64 + cswz64(rr, g) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // lane holds out[pixel m0 + wm 64 + 16 i + r][col n0 + wn BN/2 + 16 j + 4 g .. + 3]
+  f32x4 bv[NF];
+#pragma unroll
+  for (int j = 0; j < NF; ++j) {
+    const int col = n0 + wn * (BN / 2) + j * 16 + 4 * g;
+    bv[j] = (a.bias && col < a.Ncol) ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm * 64 + i * 16 + r;
+    if (m >= M) continue;
+    const int bb = m % Wm, t = m / Wm, aa = t % Hm, n = t / Hm;
+    float* orow = a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int col = n0 + wn * (BN / 2) + j * 16 + 4 * g;
+      if (col < a.Ncol) {
+        f32x4 v = acc[i][j] + bv[j];
+        if (a.accumulate) v += *(const f32x4*)(orow + col);
+        *(f32x4*)(orow + col) = v;
+      }
+    }
+  }
+}
+
+// ---- weight gradient -------------------------------------------------------------------------
+struct DWConv {
+  const float* x;   // [N, H, W, Cin] at (sxn, sxh, sxw), channel stride 1
+  const float* dy;  // [N, Ho, Wo, Cout] at (syn, syh, syw), channel stride 1
+  float* P;         // [splits][Cout][kh kw Cin] partials, column k' = tap Cin + ci
+  int N, H, W, Cin, Ho, Wo, Cout, kh, kw, s, p;
+  long sxn, sxh, sxw, syn, syh, syw;
+  int M, mchunk;
+};
+
+// pixel index -> (n, ho, wo), advanced without division
+struct PixWalk {
+  int n, ho, wo;
+  __device__ void init(int m, int Ho, int Wo) {
+    wo = m % Wo;
+    const int t = m / Wo;
+    ho = t % Ho;
+    n = t / Ho;
+  }
+  __device__ void advance(int d, int Ho, int Wo) {
+    wo += d;
+    while (wo >= Wo) {
+      wo -= Wo;
+      if (++ho == Ho) {
+        ho = 0;
+        ++n;
+      }
+    }
+  }
+};
+
+// P[split][co][k'] = sum_{pixels m of the split} dy[m][co] . im2col(x)[m][k'], tile B1 (co) x B2 (k')
+template <int B1, int B2>
+__global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
+  constexpr int WA = (B1 == 128 && B2 == 64) ? 4 : (B1 == 64 && B2 == 128) ? 1 : 2, WB = 4 / WA;
+  constexpr int F1 = B1 / WA / 16, F2 = B2 / WB / 16;  // fragments per wave along co / k'
+  constexpr int QP1 = B1 / 4, RP1 = 256 / QP1, J1 = 32 / RP1;  // dy tile: quads per row, rows per pass
+  constexpr int QP2 = B2 / 4, RP2 = 256 / QP2, J2 = 32 / RP2;  // im2col tile
+  constexpr int TILE = 32 * 256, STAGE = 2 * TILE;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  const int K = a.kh * a.kw * a.Cin;
+  const int co0 = blockIdx.x * B1, k0 = blockIdx.y * B2, split = blockIdx.z;
+  const int mbeg = split * a.mchunk, mend = min(mbeg + a.mchunk, a.M);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, t16 = lane & 15, q = t16 >> 2, p4 = t16 & 3;
+
+  // dy slots: channel quad q1, rows r1 + RP1 j
+  const int q1 = tid % QP1, r1 = tid / QP1;
+  const int co = co0 + 4 * q1;
+  const bool co_ok = co < a.Cout;
+  // im2col slots: column quad q2 -> (tap, ci) fixed for the kernel
+  const int q2 = tid % QP2, r2 = tid / QP2;
+  const int kc = k0 + 4 * q2;
+  const bool kc_ok = kc < K;
+  int ky = 0, kx = 0, ci = 0;
+  if (kc_ok) {
+    const int tap = kc / a.Cin;
+    ci = kc - tap * a.Cin;
+    ky = tap / a.kw;
+    kx = tap - ky * a.kw;
+  }
+  PixWalk pw1[J1], pw2[J2];
+#pragma unroll
+  for (int j = 0; j < J1; ++j) pw1[j].init(mbeg + r1 + RP1 * j, a.Ho, a.Wo);
+#pragma unroll
+  for (int j = 0; j < J2; ++j) pw2[j].init(mbeg + r2 + RP2 * j, a.Ho, a.Wo);
+
+  f32x4 v1[J1], v2[J2];
+  auto load = [&](int mm) {
+#pragma unroll
+    for (int j = 0; j < J1; ++j) {
+      const int m = mm + r1 + RP1 * j;
+      v1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < mend && co_ok)
+        v1[j] = *(const f32x4*)(a.dy + (long)pw1[j].n * a.syn + (long)pw1[j].ho * a.syh + (long)pw1[j].wo * a.syw + co);
+      pw1[j].advance(32, a.Ho, a.Wo);
+    }
+#pragma unroll
+    for (int j = 0; j < J2; ++j) {
+      const int m = mm + r2 + RP2 * j;
+      v2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < mend && kc_ok) {
+        const int h = pw2[j].ho * a.s - a.p + ky, ww = pw2[j].wo * a.s - a.p + kx;
+        if ((unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
+          v2[j] = *(const f32x4*)(a.x + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
+      }
+      pw2[j].advance(32, a.Ho, a.Wo);
+    }
+  };
+  auto store = [&](int buf) {
+    char* T1 = smem + buf * STAGE;
+    char* T2 = T1 + TILE;
+#pragma unroll
+    for (int j = 0; j < J1; ++j) {
+      const int row = r1 + RP1 * j;
+      bf16x4 o = {(bf16)v1[j][0], (bf16)v1[j][1], (bf16)v1[j][2], (bf16)v1[j][3]};
+      *(bf16x4*)(T1 + row * 256 + cswz256(row, q1 >> 1) * 16 + (q1 & 1) * 8) = o;
+    }
+#pragma unroll
+    for (int j = 0; j < J2; ++j) {
+      const int row = r2 + RP2 * j;
+      bf16x4 o = {(bf16)v2[j][0], (bf16)v2[j][1], (bf16)v2[j][2], (bf16)v2[j][3]};
+      *(bf16x4*)(T2 + row * 256 + cswz256(row, q2 >> 1) * 16 + (q2 & 1) * 8) = o;
+    }
+  };
+
+  const int wa = w / WB, wb = w % WB;
+  f32x4 acc[F2][F1];
+#pragma unroll
+  for (int i = 0; i < F2; ++i)
+#pragma unroll
+    for (int j = 0; j < F1; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = mend > mbeg ? (mend - mbeg + 31) / 32 : 0;
+  if (nk > 0) {
+    load(mbeg);
+    store(0);
+    __syncthreads();
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load(mbeg + (kt + 1) * 32);
+    const char* T1 = smem + buf * STAGE;
+    const char* T2 = T1 + TILE;
+    const int ra_ = 8 * g + q, rb_ = ra_ + 4;
+    const int off = (p4 & 1) * 8;
+    bf16x8 af[F2], bfr[F1];
+#pragma unroll
+    for (int i = 0; i < F2; ++i) {
+      const int c = (wb * (B2 / WB) + i * 16) / 8 + (p4 >> 1);
+      af[i] = cat8(lds_tr4(T2 + ra_ * 256 + cswz256(ra_, c) * 16 + off),
+                   lds_tr4(T2 + rb_ * 256 + cswz256(rb_, c) * 16 + off));
+    }
+#pragma unroll
+    for (int j = 0; j < F1; ++j) {
+      const int c = (wa * (B1 / WA) + j * 16) / 8 + (p4 >> 1);
+      bfr[j] = cat8(lds_tr4(T1 + ra_ * 256 + cswz256(ra_, c) * 16 + off),
+                    lds_tr4(T1 + rb_ * 256 + cswz256(rb_, c) * 16 + off));
+    }
+#pragma unroll
+    for (int i = 0; i < F2; ++i)
+#pragma unroll
+      for (int j = 0; j < F1; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+    if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // lane holds D[k' = .. + 4 g + e][co = .. + t16] -> P[split][co][k' .. k'+3]
+  float* P = a.P + (long)split * a.Cout * K;
+#pragma unroll
+  for (int j = 0; j < F1; ++j) {
+    const int c = co0 + wa * (B1 / WA) + j * 16 + t16;
+    if (c >= a.Cout) continue;
+#pragma unroll
+    for (int i = 0; i < F2; ++i) {
+      const int kk = k0 + wb * (B2 / WB) + i * 16 + 4 * g;
+      if (kk < K) *(f32x4*)(P + (long)c * K + kk) = acc[i][j];
+    }
+  }
+}
+
+// dw[co][ci][tap] (+)= sum_s P[s][co][tap Cin + ci]: 64 column quads x 4 split lanes per workgroup,
+// lanes combined in a fixed order (deterministic)
+__global__ __launch_bounds__(256) void convb_dw_reduce_kernel(const float* __restrict__ P, int S, int Cout, int Cin,
+                                                              int T, float* __restrict__ dw, int accumulate) {
+  __shared__ f32x4 red[4][64];
+  const long n = (long)Cout * T * Cin;
+  const int nq = (int)(n / 4);
+  const int cq = blockIdx.x * 64 + (threadIdx.x & 63), sl = threadIdx.x >> 6;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (cq < nq) {
+#pragma unroll 4
+    for (int k = sl; k < S; k += 4) s += *(const f32x4*)(P + (long)k * n + (long)cq * 4);
+  }
+  red[sl][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (sl != 0 || cq >= nq) return;
+  s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+  const int K = T * Cin;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long idx = (long)cq * 4 + e;
+    const int c = (int)(idx / K), kk = (int)(idx - (long)c * K);
+    const int tap = kk / Cin, cc = kk - tap * Cin;
+    float* o = dw + (long)c * K + (long)cc * T + tap;
+    *o = accumulate ? *o + s[e] : s[e];
+  }
+}
+
+// wp[co][tap][ci] = bf16(w[co][ci][tap]); wt[ci][tap][co] = bf16(w[co][ci][tap])
+__global__ void convb_pack_kernel(const float* __restrict__ w, int Cout, int Cin, int T, bf16* __restrict__ wp,
+                                  bf16* __restrict__ wt) {
+  const long n = (long)Cout * Cin * T;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int tap = (int)(i % T);
+    const long t2 = i / T;
+    const int ci = (int)(t2 % Cin), co = (int)(t2 / Cin);
+    const bf16 v = (bf16)w[i];
+    if (wp) wp[((long)co * T + tap) * Cin + ci] = v;
+    if (wt) wt[((long)ci * T + tap) * Cout + co] = v;
+  }
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+inline bool st4(long a, long b, long c) { return a % 4 == 0 && b % 4 == 0 && c % 4 == 0; }
+
+constexpr int DW_TARGET_WG = 1024;  // ~4 workgroups per CU over the pixel splits
+constexpr int DW_MAX_SPLITS = 256;
+
+inline void dw_tile(int Cout, int K, int& b1, int& b2) {
+  b1 = Cout <= 64 ? 64 : 128;
+  b2 = K <= 64 ? 64 : 128;
+}
+inline int dw_tiles(int Cout, int K) {
+  int b1, b2;
+  dw_tile(Cout, K, b1, b2);
+  return ((Cout + b1 - 1) / b1) * ((K + b2 - 1) / b2);
+}
+inline int dw_splits(int M, int Cout, int K, int splits) {
+  if (splits <= 0) {
+    const int tiles = dw_tiles(Cout, K);
+    splits = (DW_TARGET_WG + tiles - 1) / tiles;
+    const int maxs = (M + 255) / 256;  // at least 8 pixel steps per split
+    splits = splits < maxs ? splits : maxs;
+  }
+  if (splits > DW_MAX_SPLITS) splits = DW_MAX_SPLITS;
+  return splits < 1 ? 1 : splits;
+}
+
+}  // namespace
+
+extern "C" {
+
+// 1 if the bf16 kernels take a conv of these channel counts (both multiples of 32)
+int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw) {
+  return Cin > 0 && Cout > 0 && Cin % 32 == 0 && Cout % 32 == 0 && kh > 0 && kw > 0 && kh * kw <= 64;
+}
+
+int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream) {
+  if (!w || (!wp && !wt)) return ES_BAD_ARG;
+  if (Cout <= 0 || Cin <= 0 || kh <= 0 || kw <= 0) return ES_BAD_SHAPE;
+  const long n = (long)Cout * Cin * kh * kw;
+  long b = (n + 255) / 256;
+  hipLaunchKernelGGL(convb_pack_kernel, (unsigned)(b > 4096 ? 4096 : b), 256, 0, stream, w, Cout, Cin, kh * kw, (bf16*)wp,
+                     (bf16*)wt);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// y[n, ho, wo, co] (+)= bias[co] + conv(x) with wp = es_conv2d_pack_bf16's forward image.  Same
+// geometry arguments as es_conv2d_fwd; requires es_conv2d_bf16_eligible, sxc == 1, 16-byte aligned
+// pixel rows (strides % 4 == 0) and pointers.
+int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                       const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
+                       long syn, long syh, long syw, int accumulate, hipStream_t stream) {
+  if (!x || !wp || !y) return ES_BAD_ARG;
+  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
+    return ES_BAD_SHAPE;
+  const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
+  if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(x) || !al16(y) || !al16(wp) ||
+      (bias && !al16(bias)))
+    return ES_BAD_SHAPE;
+  NTConv a{x, (const bf16*)wp, bias, y, N, Cin, Cout, H, W, sxn, sxh, sxw, kh, kw, stride, pad, Ho, Wo, syn, syh, syw,
+           accumulate};
+  const int M = N * Ho * Wo;
+  if (Cout % 128 == 0)
+    hipLaunchKernelGGL((convb_nt_kernel<128, false>), dim3((M + 127) / 128, Cout / 128), 256, 0, stream, a);
+  else
+    hipLaunchKernelGGL((convb_nt_kernel<64, false>), dim3((M + 127) / 128, (Cout + 63) / 64), 256, 0, stream, a);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// dx[n, h, w, ci] (+)= conv^T(dy) with wt = es_conv2d_pack_bf16's transposed image.  Same geometry
+// arguments as es_conv2d_bwd_data.
+int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
+                            int Cin, int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh,
+                            long sxw, long sxc, int accumulate, hipStream_t stream) {
+  if (!dy || !wt || !dx) return ES_BAD_ARG;
+  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
+    return ES_BAD_SHAPE;
+  const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
+  if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(dy) || !al16(dx) ||
+      !al16(wt))
+    return ES_BAD_SHAPE;
+  NTConv a{dy, (const bf16*)wt, nullptr, dx, N, Cout, Cin, Ho, Wo, syn, syh, syw, kh, kw, stride, pad, H, W, sxn, sxh,
+           sxw, accumulate};
+  const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
+  const unsigned ph = (unsigned)(stride * stride);
+  if (Cin % 128 == 0)
+    hipLaunchKernelGGL((convb_nt_kernel<128, true>), dim3((Mq + 127) / 128, Cin / 128, ph), 256, 0, stream, a);
+  else
+    hipLaunchKernelGGL((convb_nt_kernel<64, true>), dim3((Mq + 127) / 128, (Cin + 63) / 64, ph), 256, 0, stream, a);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// fp32 workspace floats of es_conv2d_bwd_weight_bf16 for M = N Ho Wo output pixels (splits <= 0: auto)
+size_t es_conv2d_bwd_weight_bf16_workspace(int M, int Cout, int Cin, int kh, int kw, int splits) {
+  if (M <= 0 || Cout <= 0 || Cin <= 0 || kh <= 0 || kw <= 0) return 0;
+  const int K = Cin * kh * kw;
+  return (size_t)dw_splits(M, Cout, K, splits) * Cout * K;
+}
+
+// dw[co, ci, ky, kx] (+)= sum over output pixels of dy x im2col(x) (bf16 operands, fp32 sums); same
+// geometry arguments as es_conv2d_bwd_weight; splits <= 0 sizes the pixel split for the chip.
+int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                              const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
+                              int pad, int splits, float* workspace, float* dw, int accumulate, hipStream_t stream) {
+  if (!x || !dy || !dw || !workspace) return ES_BAD_ARG;
+  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
+    return ES_BAD_SHAPE;
+  const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
+  if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(x) || !al16(dy) ||
+      !al16(workspace))
+    return ES_BAD_SHAPE;
+  const int M = N * Ho * Wo, K = Cin * kh * kw;
+  const int S0 = dw_splits(M, Cout, K, splits);
+  int chunk = (M + S0 - 1) / S0;
+  chunk = (chunk + 31) / 32 * 32;
+  const int S = (M + chunk - 1) / chunk;
+  DWConv a{x, dy, workspace, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, sxn, sxh, sxw, syn, syh, syw, M, chunk};
+  int b1, b2;
+  dw_tile(Cout, K, b1, b2);
+  const dim3 grid((Cout + b1 - 1) / b1, (K + b2 - 1) / b2, S);
+  if (b1 == 128 && b2 == 128) hipLaunchKernelGGL((convb_dw_kernel<128, 128>), grid, 256, 0, stream, a);
+  else if (b1 == 64 && b2 == 128) hipLaunchKernelGGL((convb_dw_kernel<64, 128>), grid, 256, 0, stream, a);
+  else if (b1 == 128) hipLaunchKernelGGL((convb_dw_kernel<128, 64>), grid, 256, 0, stream, a);
+  else hipLaunchKernelGGL((convb_dw_kernel<64, 64>), grid, 256, 0, stream, a);
+  const long n = (long)Cout * K;
+  hipLaunchKernelGGL(convb_dw_reduce_kernel, (unsigned)((n / 4 + 63) / 64), 256, 0, stream, workspace, S, Cout, Cin,
+                     kh * kw, dw, accumulate);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+}  // extern "C"

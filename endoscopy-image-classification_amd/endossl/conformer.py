@@ -9,8 +9,10 @@ MI355X-first layout:
   * parameters live in ONE fp32 flat buffer in the reference's state_dict order (checkpoints
     interchange; the fused Adam + EMA sweep of optim.hip updates all of them in one pass); the
     BatchNorm running statistics are ordinary buffers of the BN submodules;
-  * the CNN branch keeps NHWC fp32 maps and runs on conv.hip (fp32 implicit-GEMM convolutions,
-    BatchNorm2d with fused residual + ReLU, pools, nearest upsampling); the transformer branch is a
+  * the CNN branch keeps NHWC fp32 maps and runs on conv.hip (BatchNorm2d with fused residual +
+    ReLU, pools, nearest upsampling, fp32 implicit-GEMM convolutions) and conv_bf16.hip (the convs
+    whose channel counts are multiples of 32, on bf16 operands: every conv of Conformer-B but the
+    3-channel stem; set_conv_precision("fp32") is the parity mode); the transformer branch is a
     [tokens, D] fp32 residual stream padded to 256 rows (zero pad) and runs on the same bf16 MFMA
     kernels as the ViT (gemm / attention / layernorm); the FCU bridges read and write token rows
     in place through element strides (no transposes);
@@ -253,6 +255,18 @@ def _tn_splits(M, N1, N2):
     return 0
 
 
+# CNN-branch conv operands in bf16 (csrc/conv_bf16.hip: v_mfma_f32_16x16x32_bf16, fp32 maps and
+# accumulation) wherever both channel counts are multiples of 32; ENDOSSL_CONV_BF16=0 (or
+# NativeConformer.set_conv_precision("fp32")) keeps every conv on conv.hip's fp32 MFMA kernels.
+CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
+
+
+def _conv_bf16(m, xmap, Cout, k):
+    if not getattr(m, "conv_bf16", False) or xmap.sc != 1 or (xmap.sn | xmap.sh | xmap.sw) % 4 or xmap.p() % 16:
+        return False
+    return bool(_lib.load().es_conv2d_bf16_eligible(xmap.C, Cout, k, k))
+
+
 class _ConvFn(torch.autograd.Function):
     """Conv2d (groups 1, optional bias) on an NHWC view -> new NHWC map (code/models/conformer.py
     ConvBlock / FCU convs, Conformer.conv1)."""
@@ -261,11 +275,16 @@ class _ConvFn(torch.autograd.Function):
     def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None):
         Ho, Wo = (xmap.H + 2 * p - k) // s + 1, (xmap.W + 2 * p - k) // s + 1
         y = torch.empty(xmap.N, Ho, Wo, Cout, dtype=torch.float32, device=x.device)
-        call("es_conv2d_fwd", xmap.p(), xmap.N, xmap.H, xmap.W, xmap.C, xmap.sn, xmap.sh, xmap.sw, xmap.sc,
-             ptr(m.pview(wname)), ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout,
-             Wo * Cout, Cout, 0, _s())
+        b16 = _conv_bf16(m, xmap, Cout, k)
+        args = (xmap.p(), xmap.N, xmap.H, xmap.W, xmap.C, xmap.sn, xmap.sh, xmap.sw, xmap.sc)
+        tail = (ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout, Wo * Cout, Cout, 0,
+                _s())
+        if b16:
+            call("es_conv2d_fwd_bf16", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail)
+        else:
+            call("es_conv2d_fwd", *args, ptr(m.pview(wname)), *tail)
         ctx.save_for_backward(x)
-        ctx.m, ctx.xmap, ctx.spec = m, xmap, (wname, bname, Cout, k, s, p, Ho, Wo)
+        ctx.m, ctx.xmap, ctx.spec, ctx.b16 = m, xmap, (wname, bname, Cout, k, s, p, Ho, Wo), b16
         return y
 
     @staticmethod
@@ -277,10 +296,15 @@ class _ConvFn(torch.autograd.Function):
         dy = dy.contiguous()
         xp = ptr(x) + 4 * xm.off
         M = xm.N * Ho * Wo
-        # pixel splits sized for ~2048 workgroups (8 per CU) over es_conv2d_bwd_weight's tiles
         lib = _lib.load()
-        tiles = lib.es_conv2d_dw_tiles(Cout, xm.C, k, k)
-        splits = max(1, min(-(-M // 64), -(-2048 // tiles)))
+        b16 = ctx.b16
+        if b16:  # the bf16 weight gradient sizes its own pixel split (splits = 0)
+            splits, dwfn = 0, "es_conv2d_bwd_weight_bf16"
+            wsn = lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, xm.C, k, k, 0)
+        else:  # pixel splits sized for ~2048 workgroups (8 per CU) over es_conv2d_bwd_weight's tiles
+            tiles = lib.es_conv2d_dw_tiles(Cout, xm.C, k, k)
+            splits, dwfn = max(1, min(-(-M // 64), -(-2048 // tiles))), "es_conv2d_bwd_weight"
+            wsn = lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits)
         side = _wgrad_stream(dy.device) if CONV_DW_SIDE and dy.is_cuda else None
         if side is not None:
             main = torch.cuda.current_stream(dy.device)
@@ -289,8 +313,8 @@ class _ConvFn(torch.autograd.Function):
             x.record_stream(side)
             dy.record_stream(side)
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, xm.C, k, k, splits), device=dy.device)
-            call("es_conv2d_bwd_weight", xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy),
+            ws = torch.empty(wsn, device=dy.device)
+            call(dwfn, xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy),
                  Ho * Wo * Cout, Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0, _s())
             if bname:
                 wsb = torch.empty(lib.es_chan_workspace(M, Cout), device=dy.device)
@@ -299,8 +323,10 @@ class _ConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             full = xm.off == 0 and xm.sc == 1 and xm.sn * xm.N == x.numel()
             dx = torch.empty_like(x) if full else torch.zeros_like(x)
-            call("es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout, ptr(m.pview(wname)), xm.N, xm.H,
-                 xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, 0, _s())
+            wimg = m.conv_pack(wname, Cout, xm.C, k)[1] if b16 else m.pview(wname)
+            call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
+                 ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, 0,
+                 _s())
         return dx, None, None, None, None, None, None, None, None, None
 
 
@@ -466,11 +492,13 @@ class _PatchTokensFn(torch.autograd.Function):
         N, H, W, C = xb.shape
         D, T, g, dw = cfg.dim, cfg.T, cfg.grid, cfg.dw
         xt = torch.zeros(_rup(N * T, 256), D, device=xb.device)
-        call("es_conv2d_fwd", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, ptr(m.pview("trans_patch_conv.weight")),
+        b16 = _conv_bf16(m, _Map.nhwc(xb), D, dw)
+        wimg = m.conv_pack("trans_patch_conv.weight", D, C, dw)[0] if b16 else m.pview("trans_patch_conv.weight")
+        call("es_conv2d_fwd_bf16" if b16 else "es_conv2d_fwd", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, ptr(wimg),
              ptr(m.pview("trans_patch_conv.bias")), D, dw, dw, dw, 0, ptr(xt) + 4 * D, T * D, g * D, D, 0, _s())
         call("es_tokens_cls_set", ptr(xt), N, T, D, ptr(m.pview("cls_token")), _s())
         ctx.save_for_backward(xb)
-        ctx.m = m
+        ctx.m, ctx.b16 = m, b16
         return xt
 
     @staticmethod
@@ -484,17 +512,23 @@ class _PatchTokensFn(torch.autograd.Function):
         dxt = dxt.contiguous()
         lib = _lib.load()
         M = N * cfg.np
-        splits = max(1, min(-(-M // 64), -(-2048 // lib.es_conv2d_dw_tiles(D, C, dw, dw))))
-        ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(D, C, dw, dw, splits), device=dxt.device)
+        b16 = ctx.b16
+        if b16:
+            splits = 0
+            ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, D, C, dw, dw, 0), device=dxt.device)
+        else:
+            splits = max(1, min(-(-M // 64), -(-2048 // lib.es_conv2d_dw_tiles(D, C, dw, dw))))
+            ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(D, C, dw, dw, splits), device=dxt.device)
         dyp = ptr(dxt) + 4 * D
-        call("es_conv2d_bwd_weight", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, dyp, T * D, g * D, D, D, dw, dw, dw,
+        call("es_conv2d_bwd_weight_bf16" if b16 else "es_conv2d_bwd_weight", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, dyp, T * D, g * D, D, D, dw, dw, dw,
              0, splits, ptr(ws), ptr(m.gview("trans_patch_conv.weight")), 0, _s())
         wsb = torch.empty(lib.es_chan_workspace(M, D), device=dxt.device)
         call("es_chan_sum", dyp, M, D, T * D, D, cfg.np, ptr(wsb), ptr(m.gview("trans_patch_conv.bias")), 0, _s())
         call("es_chan_sum", ptr(dxt), N, D, T * D, 0, 1, ptr(wsb), ptr(m.gview("cls_token")), 0, _s())
         dxb = torch.empty_like(xb)
-        call("es_conv2d_bwd_data", dyp, T * D, g * D, D, ptr(m.pview("trans_patch_conv.weight")), N, H, W, C, D, dw,
-             dw, dw, 0, ptr(dxb), H * W * C, W * C, C, 1, 0, _s())
+        wimg = m.conv_pack("trans_patch_conv.weight", D, C, dw)[1] if b16 else m.pview("trans_patch_conv.weight")
+        call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", dyp, T * D, g * D, D, ptr(wimg), N, H, W, C,
+             D, dw, dw, dw, 0, ptr(dxb), H * W * C, W * C, C, 1, 0, _s())
         return dxb, None
 
 
@@ -709,6 +743,28 @@ class NativeConformer(nn.Module):
         self._build(flat, device=torch.device("cpu"))
         self.version = 0
         self.cur_n = 0
+        self.conv_bf16 = CONV_BF16
+
+    def set_conv_precision(self, precision):
+        """"bf16": convs with channel counts % 32 == 0 on bf16 operands (default); "fp32": all on
+        conv.hip's fp32 MFMA kernels (the parity mode of the CNN branch)."""
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(precision)
+        self.conv_bf16 = precision == "bf16"
+        return self
+
+    def conv_pack(self, name, Cout, Cin, k):
+        """bf16 images of conv weight `name` -- wp [Cout][k k][Cin] and wt [Cin][k k][Cout] -- packed
+        once per parameter version (es_conv2d_pack_bf16)."""
+        ent = self._cpack.get(name)
+        if ent is None:
+            n = Cout * Cin * k * k
+            ent = self._cpack[name] = [-1, torch.empty(n, dtype=torch.bfloat16, device=self.flat.device),
+                                       torch.empty(n, dtype=torch.bfloat16, device=self.flat.device)]
+        if ent[0] != self.version:
+            call("es_conv2d_pack_bf16", ptr(self.pview(name)), Cout, Cin, k, k, ptr(ent[1]), ptr(ent[2]), _s())
+            ent[0] = self.version
+        return ent[1], ent[2]
 
     def bwd_scratch(self, name, shape, dtype):
         """Zero-initialised scratch for the transformer blocks' backward, allocated once per shape."""
@@ -750,6 +806,7 @@ class NativeConformer(nn.Module):
                 mod._buffers[attr] = t
         self._packed_version = -1
         self._wtab = None
+        self._cpack = {}
         self._anchor = torch.zeros((), device=device, requires_grad=True)
 
     def _apply(self, fn, recurse=True):
@@ -766,6 +823,7 @@ class NativeConformer(nn.Module):
         bufs = {name: self.get_buffer(name).detach().clone() for name, _, kind in self.layout if kind != "p"}
         other._build(self.flat.detach().clone(), device=self.flat.device, buffers=bufs)
         other.version, other.cur_n = 0, 0
+        other.conv_bf16 = self.conv_bf16
         other.train(self.training)
         return other
 

@@ -64,7 +64,7 @@ int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate,
 
 /* tuning knob: forward attention occupancy target (2 or 3 workgroups per CU); returns previous */
 int es_set_attn_variant(int occ);
-/* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 256 --------------- */
+/* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 592 (384^2 / 16) ------ */
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream);
 /* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass) */
@@ -250,6 +250,25 @@ size_t es_conv2d_bwd_weight_workspace(int Cout, int Cin, int kh, int kw, int spl
 int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
                          const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride, int pad,
                          int splits, float* workspace, float* dw, int accumulate, hipStream_t stream);
+/* bf16-operand forms of the three convs above (csrc/conv_bf16.hip): the same fp32 maps and
+ * geometry arguments, operands rounded to bf16 as they are staged, fp32 accumulation on
+ * v_mfma_f32_16x16x32_bf16.  Taken for eligible convs (Cin, Cout multiples of 32) when
+ * the maps have channel stride 1 with 16-byte aligned pixel rows.  Weights go through
+ * es_conv2d_pack_bf16 first: wp [Cout][kh kw][Cin] (forward), wt [Cin][kh kw][Cout] (data grad),
+ * Cout Cin kh kw bf16 each, either pointer may be null. */
+int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw);
+int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);
+int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                       const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
+                       long syn, long syh, long syw, int accumulate, hipStream_t stream);
+int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
+                            int Cin, int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh,
+                            long sxw, long sxc, int accumulate, hipStream_t stream);
+/* workspace floats for M = N Ho Wo output pixels; splits <= 0 sizes the pixel split automatically */
+size_t es_conv2d_bwd_weight_bf16_workspace(int M, int Cout, int Cin, int kh, int kw, int splits);
+int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                              const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
+                              int pad, int splits, float* workspace, float* dw, int accumulate, hipStream_t stream);
 size_t es_chan_workspace(int rows, int C);
 /* out[c] (+)= sum_r v[(r / HW) * sn + (r % HW) * sp + c]  (bias gradients) */
 int es_chan_sum(const float* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,

@@ -4,7 +4,8 @@ Kernels (conv.hip, es_ce_weighted_fwd_bwd) against plain torch fp64 CPU restatem
 (autograd for the gradients): fp32 tolerances.  The native Conformer against the oracle
 (oracle/conformer_ref.py, pinned bit-exact to the reference's SemiFormer.train_one fixture): forward
 logits within 1e-3 * scale of the bf16-contract emulation (the transformer blocks round their GEMM
-operands to bf16, the CNN branch is fp32); the SemiFormer trainer against the reference fixture over
+operands to bf16; with fp32 convs) or within twice the contract's envelope of the fp32 reference
+(bf16 convs, csrc/conv_bf16.hip, vs fp64 of rounded operands above); the SemiFormer trainer against the reference fixture over
 two steps within the bf16 envelope, pseudo-labels / masks bit-exact on decidable rows, parameters
 within 2 * lr * steps.
 """
@@ -105,6 +106,91 @@ def test_conv2d_fwd_bwd(N, Cin, H, Cout, k, s, p):
     dbd = torch.full((Cout,), 3.0, device=DEV)
     call("es_chan_sum", ptr(dyd), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(dbd), 1, S())
     _close(dbd.cpu() - 3.0, br.grad)
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(t.dtype)
+
+
+@pytest.mark.parametrize("N,Cin,H,Cout,k,s,p", [(2, 64, 16, 64, 1, 1, 0), (2, 32, 13, 96, 3, 1, 1),
+                                                (3, 64, 15, 128, 3, 2, 1), (2, 128, 12, 256, 1, 2, 0),
+                                                (2, 64, 16, 384, 4, 4, 0), (1, 96, 9, 32, 3, 1, 1),
+                                                (2, 256, 8, 64, 1, 1, 0)])
+def test_conv2d_bf16_fwd_bwd(N, Cin, H, Cout, k, s, p):
+    """csrc/conv_bf16.hip against fp64 convs of the bf16-rounded operands (the kernels' contract:
+    operands rounded to bf16, fp32 accumulation): forward, data gradient, weight gradient (pixel
+    splits 1, 3 and automatic), accumulate mode."""
+    lib = _lib.load()
+    assert lib.es_conv2d_bf16_eligible(Cin, Cout, k, k) == 1
+    torch.manual_seed(N * 100 + Cin + Cout + k)
+    x = torch.randn(N, Cin, H, H, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, dtype=torch.float64) * 0.2
+    b = torch.randn(Cout, dtype=torch.float64)
+    xr, wr = _bf(x).requires_grad_(True), _bf(w).requires_grad_(True)
+    y = F.conv2d(xr, wr, b, stride=s, padding=p)
+    Ho = y.shape[2]
+    xd, wd, bd = _nhwc(x).float().to(DEV), w.float().to(DEV), b.float().to(DEV)
+    n = Cout * Cin * k * k
+    wp, wt = torch.empty(n, dtype=torch.bfloat16, device=DEV), torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    call("es_conv2d_pack_bf16", ptr(wd), Cout, Cin, k, k, ptr(wp), ptr(wt), S())
+    torch.cuda.synchronize()
+    assert torch.equal(wp.view(Cout, k * k, Cin).cpu(), w.float().bfloat16().view(Cout, Cin, k * k).transpose(1, 2))
+    yd = torch.full((N, Ho, Ho, Cout), 0.5, device=DEV)
+    call("es_conv2d_fwd_bf16", ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(wp), ptr(bd), Cout, k, k, s,
+         p, ptr(yd), Ho * Ho * Cout, Ho * Cout, Cout, 1, S())
+    _close(_nchw(yd.cpu()) - 0.5, y, atol=2e-5)
+    dy = torch.randn_like(y)
+    y.backward(_bf(dy))
+    dyd = _nhwc(dy).float().to(DEV)
+    dxd = torch.empty(N, H, H, Cin, device=DEV)
+    call("es_conv2d_bwd_data_bf16", ptr(dyd), Ho * Ho * Cout, Ho * Cout, Cout, ptr(wt), N, H, H, Cin, Cout, k, k, s,
+         p, ptr(dxd), H * H * Cin, H * Cin, Cin, 1, 0, S())
+    _close(_nchw(dxd.cpu()), xr.grad, atol=2e-5)
+    M = N * Ho * Ho
+    for splits in (1, 3, 0):
+        ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, Cin, k, k, splits), device=DEV)
+        dwd = torch.full_like(wd, 2.0)
+        call("es_conv2d_bwd_weight_bf16", ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(dyd),
+             Ho * Ho * Cout, Ho * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(dwd), 1, S())
+        _close(dwd.cpu() - 2.0, wr.grad, atol=2e-5)
+
+
+def test_conv2d_bf16_token_rows():
+    """bf16 convs over token-row views: a 4x4/4 patch conv written into rows 1.. of [N, T, D]
+    (trans_patch_conv), and a 1x1 conv reading them back with its data gradient written into token
+    rows (FCUUp conv_project), row 0 untouched."""
+    torch.manual_seed(5)
+    N, C, H, D, k = 2, 64, 24, 128, 4
+    g = H // k
+    T = g * g + 1
+    x = torch.randn(N, C, H, H)
+    w = torch.randn(D, C, k, k) * 0.1
+    wp = torch.empty(D * C * k * k, dtype=torch.bfloat16, device=DEV)
+    call("es_conv2d_pack_bf16", ptr(dv(w)), D, C, k, k, ptr(wp), None, S())
+    tok = torch.full((N * T, D), 9.0, device=DEV)
+    call("es_conv2d_fwd_bf16", ptr(dv(_nhwc(x))), N, H, H, C, H * H * C, H * C, C, 1, ptr(wp), None, D, k, k, k, 0,
+         ptr(tok) + 4 * D, T * D, g * D, D, 0, S())
+    t = tok.view(N, T, D).cpu()
+    assert torch.all(t[:, 0] == 9.0)
+    _close(t[:, 1:].reshape(N, g, g, D), _nhwc(F.conv2d(_bf(x.double()), _bf(w.double()), stride=k)), atol=2e-5)
+    C2 = 64
+    w2 = torch.randn(C2, D, 1, 1) * 0.1
+    wp2 = torch.empty(C2 * D, dtype=torch.bfloat16, device=DEV)
+    wt2 = torch.empty(C2 * D, dtype=torch.bfloat16, device=DEV)
+    call("es_conv2d_pack_bf16", ptr(dv(w2)), C2, D, 1, 1, ptr(wp2), ptr(wt2), S())
+    out = torch.empty(N, g, g, C2, device=DEV)
+    call("es_conv2d_fwd_bf16", ptr(tok) + 4 * D, N, g, g, D, T * D, g * D, D, 1, ptr(wp2), None, C2, 1, 1, 1, 0,
+         ptr(out), g * g * C2, g * C2, C2, 0, S())
+    xin = _nchw(t[:, 1:].reshape(N, g, g, D)).double()
+    _close(_nchw(out.cpu()), F.conv2d(_bf(xin), _bf(w2.double())), atol=2e-5)
+    dy = torch.randn(N, g, g, C2)
+    dtok = torch.zeros(N * T, D, device=DEV)
+    call("es_conv2d_bwd_data_bf16", ptr(dv(dy)), g * g * C2, g * C2, C2, ptr(wt2), N, g, g, D, C2, 1, 1, 1, 0,
+         ptr(dtok) + 4 * D, T * D, g * D, D, 1, 0, S())
+    ref = torch.einsum("nhwo,oc->nhwc", _bf(dy.double()), _bf(w2.double()).view(C2, D))
+    d = dtok.view(N, T, D).cpu()
+    assert torch.all(d[:, 0] == 0)
+    _close(d[:, 1:].reshape(N, g, g, D), ref, atol=2e-5)
 
 
 def test_conv2d_strided_views():
@@ -307,11 +393,14 @@ def _model_from_fixture(d):
     return m.to(DEV), state
 
 
-def test_conformer_forward_backward_vs_oracle(golden):
+@pytest.mark.parametrize("conv", ["fp32", "bf16"])
+def test_conformer_forward_backward_vs_oracle(golden, conv):
     """One train-mode forward + backward of the native Conformer vs the oracle (bf16-contract mode:
-    the transformer blocks' GEMM operands rounded like the MFMA kernels)."""
+    the transformer blocks' GEMM operands rounded like the MFMA kernels; with conv = "bf16" also the
+    operands of the convs the device runs on conv_bf16.hip -- stages 2 and 3 of this fixture)."""
     d = golden("semiformer_step.npz")
     m, state = _model_from_fixture(d)
+    m.set_conv_precision(conv)
     _, ocfg = _tiny_cfgs()
     x = torch.cat([torch.tensor(d[k]) for k in ("x0", "uw0", "us0")])
     _check_model_vs_oracle(m, state, ocfg, x, ("bn1.running_mean", "conv_trans_4.fusion_block.bn2.running_var",
@@ -334,13 +423,39 @@ def test_conformer_vit_b_384_forward_backward_vs_oracle():
     _check_model_vs_oracle(m, state, ocfg, x, ("bn1.running_mean", "conv_trans_2.fusion_block.bn2.running_var"))
 
 
+def test_conformer_b_cnn_branch_bf16_vs_oracle():
+    """Conformer-B's CNN branch (channel_ratio 4: stages of 256 / 512 / 1024 channels, bottlenecks of
+    64 / 128 / 256) -- every conv but the stem on the bf16 kernels (csrc/conv_bf16.hip) -- at 64^2 so
+    the CPU oracle stays fast; the oracle's bf16 mode rounds the same conv operands."""
+    from endossl.conformer import ConformerConfig, NativeConformer
+    kw = dict(img_size=64, patch=16, base_channel=64, channel_ratio=4, embed_dim=128, depth=3, heads=2,
+              num_classes=23)
+    ncfg, ocfg = ConformerConfig(**kw), cr.ConformerCfg(**kw)
+    m = NativeConformer(ncfg, seed=11)
+    assert m.conv_bf16
+    state = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(DEV)
+    x = torch.randn(6, 3, 64, 64, generator=torch.Generator().manual_seed(12))
+    _check_model_vs_oracle(m, state, ocfg, x, ("bn1.running_mean", "conv_trans_2.fusion_block.bn2.running_var",
+                                              "conv_trans_3.cnn_block.bn1.running_mean"))
+
+
 def _check_model_vs_oracle(m, state, ocfg, x, bn_keys):
-    rec = {}
+    """Train-mode forward + backward vs the oracle in fp32 and in the device's bf16 contract.
+
+    fp32 convs: the device tracks the contract emulation to within a quarter of the bf16 envelope
+    (|contract - fp32|).  bf16 convs: the device rounds its OWN fp32 conv inputs, which differ from the
+    emulation's in the last bits (summation order upstream); a rounding flip there is a bf16 ulp that
+    the batch-statistics BatchNorms pass on, so the two bf16 computations are independent samples of
+    the same error distribution.  The test then asks for the property that matters -- the device is as
+    close to the fp32 reference as the contract emulation is: |device - fp32| <= 2 x envelope."""
+    conv16 = m.conv_bf16
+    rec = {"conv_bf16": conv16}
     res = {}
     for bf in (True, False):
         p = {k: v.clone().float().requires_grad_(True) for k, v in state.items() if not cr.is_buffer(k)}
         bufs = {k: v.clone() for k, v in state.items() if cr.is_buffer(k)}
-        oc, ot = cr.conformer_forward(p, bufs, x, ocfg, train=True, bf16=bf)
+        oc, ot = cr.conformer_forward(p, bufs, x, ocfg, train=True, bf16=bf, bf16_conv=bf and conv16)
         res[bf] = (oc, ot, p, bufs)
     m.train()
     m.flat_grad.zero_()
@@ -349,12 +464,16 @@ def _check_model_vs_oracle(m, state, ocfg, x, bn_keys):
         r16, r32 = res[True][i].detach().double(), res[False][i].detach().double()
         sc = max(1.0, r32.abs().max().item())
         e16 = (h.detach().cpu().double() - r16).abs().max().item()
+        e32 = (h.detach().cpu().double() - r32).abs().max().item()
         env = (r16 - r32).abs().max().item()
-        rec[name] = {"hip_vs_bf16_contract": e16, "bf16_envelope": env, "scale": sc}
-        assert e16 <= 1e-3 * sc + 0.25 * env, rec
+        rec[name] = {"hip_vs_bf16_contract": e16, "hip_vs_fp32": e32, "bf16_envelope": env, "scale": sc}
+        if conv16:
+            assert e32 <= 2 * env + 1e-3 * sc, rec
+        else:
+            assert e16 <= 1e-3 * sc + 0.25 * env, rec
     # BatchNorm running statistics after the train-mode forward
     for k in bn_keys:
-        _close(m.get_buffer(k).cpu(), res[True][3][k], atol=2e-3)
+        _close(m.get_buffer(k).cpu(), res[True][3][k], atol=2e-2 if conv16 else 2e-3)
     assert int(m.get_buffer("bn1.num_batches_tracked").item()) == int(state["bn1.num_batches_tracked"].item()) + 1
     # gradients of a fixed random linear functional of both heads
     g = torch.Generator().manual_seed(4)
@@ -375,6 +494,9 @@ def _check_model_vs_oracle(m, state, ocfg, x, bn_keys):
         g16, g32 = grads[True][k].double(), grads[False][k].double()
         nrm = g32.norm().item()
         e, env = (gh - g16).norm().item(), (g16 - g32).norm().item()
+        if conv16:  # as the logits: the device within twice the contract's distance from fp32
+            e = (gh - g32).norm().item()
+            env = 2 * env
         worst.append((e / (nrm + 1e-12), env / (nrm + 1e-12), k))
         if e > 2e-3 * nrm + env + 1e-4 * gmax:
             bad.append((k, e, env, nrm))
@@ -401,12 +523,19 @@ class _DL:
         return len(self.items)
 
 
-def test_semiformer_trainer_vs_reference_train_one(golden):
+@pytest.mark.parametrize("conv", ["fp32", "bf16"])
+def test_semiformer_trainer_vs_reference_train_one(golden, conv):
+    """The SemiFormer trainer over the fixture's steps.  kc / kr / kd: the tolerance factors on the
+    bf16 envelope; with bf16 convs the device is an independent bf16 sample (see
+    _check_model_vs_oracle), so it is held to the envelope itself rather than a fraction of it."""
     import pandas as pd
     from endossl.semiformer import SemiFormer
     from endossl.utils import AttrDict
     d = golden("semiformer_step.npz")
     m, state = _model_from_fixture(d)
+    m.set_conv_precision(conv)
+    c16 = conv == "bf16"
+    kc, kr, kd = (2.0, 3.0, 4.0) if c16 else (0.25, 1.5, 2.0)
     _, ocfg = _tiny_cfgs()
     B, MU, steps, thres = int(d["B"]), int(d["MU"]), int(d["steps"]), float(d["thres"])
     C = 23
@@ -423,14 +552,14 @@ def test_semiformer_trainer_vs_reference_train_one(golden):
                        WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const", FREQ_EVAL=1)))
     np.testing.assert_allclose(tr.class_weights.cpu().numpy(), d["class_weights"], rtol=1e-6)
     cw = torch.tensor(d["class_weights"]).float()
-    emu = cr.SemiFormerRef(state, ocfg, class_weights=cw, thres=thres, bf16=True)
+    emu = cr.SemiFormerRef(state, ocfg, class_weights=cw, thres=thres, bf16=True, bf16_conv=c16)
     rec = {}
     for i in range(steps):
         # the oracle at the HIP path's own pre-step state (parameters + BN buffers): every step is checked
         # tightly against the bf16-contract emulation of that state, not against a diverging trajectory
         # (Adam turns bf16 noise on near-zero gradients into +-lr moves, which BatchNorm then amplifies)
         snap = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-        ref16 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=True)
+        ref16 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=True, bf16_conv=c16)
         ref32 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=False)
         o = tr.step((lab[i], unl[i]))
         r16, r32 = ref16.step(*lab[i], *unl[i][0]), ref32.step(*lab[i], *unl[i][0])
@@ -441,19 +570,19 @@ def test_semiformer_trainer_vs_reference_train_one(golden):
             sc = max(1.0, a32.abs().max().item())
             e, env = (h - a16).abs().max().item(), (a16 - a32).abs().max().item()
             rec[f"step{i}_{head}_vs_contract_at_hip_state"] = {"err": e, "bf16_envelope": env}
-            assert e <= 1e-3 * sc + 0.25 * env, rec
+            assert e <= 1e-3 * sc + kc * env, rec
             if i == 0:  # same initial state as the reference fixture
                 ref = torch.tensor(d[f"{head}{i}"]).double()
                 err, envr = (h - ref).abs().max().item(), (r[head].double() - ref).abs().max().item()
                 rec[f"step0_{head}_vs_reference"] = {"err": err, "bf16_envelope": envr}
-                assert err <= 1.5 * envr + 1e-3 * sc, rec
+                assert err <= kr * envr + 1e-3 * sc, rec
         for k in ("lx", "lu", "loss"):
             hip, a16, a32 = o[k].item(), r16[k], r32[k]
             rec[f"step{i}_{k}"] = {"hip": hip, "bf16_contract": a16, "fp32": a32}
-            assert abs(hip - a16) <= 1e-3 * max(1.0, abs(a32)) + 0.25 * abs(a16 - a32), rec
+            assert abs(hip - a16) <= 1e-3 * max(1.0, abs(a32)) + kc * abs(a16 - a32), rec
         if i == 0:
             for k, ref_v in (("lx", float(d["lx"][0] + d["lx"][1])), ("lu", float(d["lu"][0] + d["lu"][1]))):
-                assert abs(o[k].item() - ref_v) <= 1.5 * abs(r[k] - ref_v) + 1e-3 * max(1.0, abs(ref_v)), rec
+                assert abs(o[k].item() - ref_v) <= kr * abs(r[k] - ref_v) + 1e-3 * max(1.0, abs(ref_v)), rec
         # pseudo-labels / masks of the conv head's weak rows, on decidable rows of the fp32 oracle at
         # the same state (the reference's own at step 0)
         wk32 = r32["out_conv"][B:B + B * MU].double()
@@ -461,8 +590,8 @@ def test_semiformer_trainer_vs_reference_train_one(golden):
         p32, p16 = torch.softmax(wk32, -1), torch.softmax(wk16, -1)
         envp = (p32 - p16).abs().max().item()
         top2 = p32.topk(2, -1).values
-        ok = ((top2[:, 0] - top2[:, 1]) > 2 * envp + 1e-6).numpy()
-        okm = ((p32.max(-1).values - thres).abs() > 2 * envp + 1e-6).numpy()
+        ok = ((top2[:, 0] - top2[:, 1]) > kd * envp + 1e-6).numpy()
+        okm = ((p32.max(-1).values - thres).abs() > kd * envp + 1e-6).numpy()
         np.testing.assert_array_equal(o["pseudo_label"].cpu().numpy()[ok], r32["pseudo_label"].numpy()[ok])
         np.testing.assert_array_equal(o["mask"].cpu().numpy().astype(bool)[okm], r32["mask"].numpy().astype(bool)[okm])
         if i == 0:
@@ -478,7 +607,7 @@ def test_semiformer_trainer_vs_reference_train_one(golden):
             else:
                 fx = torch.tensor(d["final/" + k])
                 e, ev = (v.cpu() - fx).abs().max().item(), (emu.bufs[k] - fx).abs().max().item()
-                assert e <= 1.5 * ev + 2e-3, (k, e, ev)
+                assert e <= kr * ev + 2e-3, (k, e, ev)
             continue
         if "final/" + k in d.files:
             worst = max(worst, (v.cpu() - torch.tensor(d["final/" + k])).abs().max().item())
