@@ -88,17 +88,23 @@ __global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
 
-  // gather slots: pixel row arow (2 threads per pixel, 16 channels each)
-  const int arow = tid >> 1, ahalf = tid & 1;
-  const int am = m0 + arow;
-  const bool am_ok = am < M;
-  long abase = 0;
-  int ahb = -(1 << 28), awb = 0;
-  if (am_ok) {
-    const int bb = am % Wm, t = am / Wm, aa = t % Hm, n = t / Hm;
-    abase = (long)n * a.ssn + ahalf * 16;
-    ahb = aa * ra + ca;
-    awb = bb * ra + cb;
+  // gather slots: 8 lanes per pixel (one 16-byte channel quad each: a wave instruction reads 8
+  // whole 128-byte channel runs), pixel rows arow0 + 32 j
+  const int ac = tid & 7, arow0 = tid >> 3;
+  long abase[4];
+  int ahb[4], awb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int am = m0 + arow0 + 32 * j;
+    abase[j] = 0;
+    ahb[j] = -(1 << 28);  // a pixel row past M gathers zeros (its h is far out of range)
+    awb[j] = 0;
+    if (am < M) {
+      const int bb = am % Wm, t = am / Wm, aa = t % Hm, n = t / Hm;
+      abase[j] = (long)n * a.ssn + ac * 4;
+      ahb[j] = aa * ra + ca;
+      awb[j] = bb * ra + cb;
+    }
   }
   const int bchunk = tid & 3, brow0 = tid >> 2;
 
@@ -108,15 +114,12 @@ __global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
     const int k0 = kt * NT_BK;
     const int tq = k0 / a.C, c0 = k0 - tq * a.C;
     const int tyq = tq / twx, txq = tq - tyq * twx;
-    const int h = ahb + sy * tyq, ww = awb + sy * txq;
-    const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
-    if (ok) {
-      const f32x4* src = (const f32x4*)(a.src + abase + (long)h * a.ssh + (long)ww * a.ssw + c0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) ra4[e] = src[e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) ra4[e] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) {
+      const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
+      ra4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if ((unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws)
+        ra4[j] = *(const f32x4*)(a.src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
     }
     const int btap = (by0 + tyq * bs) * a.kw + bx0 + txq * bs;
 #pragma unroll
@@ -129,8 +132,12 @@ __global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
   auto store = [&](int buf) {
     char* As = smem + buf * STAGE;
     char* Bs = As + ABYTES;
-    *(u32x4*)(As + arow * 64 + cswz64(arow, ahalf * 2) * 16) = f8_to_bf16x8(ra4[0], ra4[1]);
-    *(u32x4*)(As + arow * 64 + cswz64(arow, ahalf * 2 + 1) * 16) = f8_to_bf16x8(ra4[2], ra4[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = arow0 + 32 * j;
+      const bf16x4 o = {(bf16)ra4[j][0], (bf16)ra4[j][1], (bf16)ra4[j][2], (bf16)ra4[j][3]};
+      *(bf16x4*)(As + row * 64 + cswz64(row, ac >> 1) * 16 + (ac & 1) * 8) = o;
+    }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
       const int br = brow0 + 64 * j;
@@ -174,28 +181,35 @@ __global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
     __syncthreads();
   }
 
-  // lane holds out[pixel m0 + wm 64 + 16 i + r][col n0 + wn BN/2 + 16 j + 4 g .. + 3]
-  f32x4 bv[NF];
-#pragma unroll
-  for (int j = 0; j < NF; ++j) {
-    const int col = n0 + wn * (BN / 2) + j * 16 + 4 * g;
-    bv[j] = (a.bias && col < a.Ncol) ? *(const f32x4*)(a.bias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-  }
+  // Epilogue through LDS (the stage buffers are free after the loop's last barrier): lane holds
+  // out[pixel m0 + wm 64 + 16 i + r][col wn BN/2 + 16 j + 4 g .. + 3]; per 16-pixel chunk the wave
+  // writes its [16][BN/2] tile to its LDS region and reads it back as whole-row quads, so every store
+  // instruction covers RPI pixel rows x BN/2 contiguous channels (256 B per row at BN = 128).
+  constexpr int NCOL = BN / 2, QPR = NCOL / 4, RPI = 64 / QPR, ROWF = NCOL + 4;
+  float* wl = (float*)smem + w * 16 * ROWF;
+  const int eq = lane % QPR, er = lane / QPR;
+  const int ecol = n0 + wn * NCOL + eq * 4;
+  const bool ecol_ok = ecol < a.Ncol;
+  const f32x4 bv = (a.bias && ecol_ok) ? *(const f32x4*)(a.bias + ecol) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int m = m0 + wm * 64 + i * 16 + r;
-    if (m >= M) continue;
-    const int bb = m % Wm, t = m / Wm, aa = t % Hm, n = t / Hm;
-    float* orow = a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw;
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      const int col = n0 + wn * (BN / 2) + j * 16 + 4 * g;
-      if (col < a.Ncol) {
-        f32x4 v = acc[i][j] + bv[j];
-        if (a.accumulate) v += *(const f32x4*)(orow + col);
-        *(f32x4*)(orow + col) = v;
+    for (int j = 0; j < NF; ++j) *(f32x4*)(wl + r * ROWF + j * 16 + 4 * g) = acc[i][j];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 16 / RPI; ++it) {
+      const int row = er + it * RPI;
+      const f32x4 v0 = *(const f32x4*)(wl + row * ROWF + eq * 4);
+      const int m = m0 + wm * 64 + i * 16 + row;
+      if (m < M && ecol_ok) {
+        const int bb = m % Wm, t = m / Wm, aa = t % Hm, n = t / Hm;
+        float* o = a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw + ecol;
+        f32x4 v = v0 + bv;
+        if (a.accumulate) v += *(const f32x4*)o;
+        *(f32x4*)o = v;
       }
     }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -405,8 +419,8 @@ __global__ void convb_pack_kernel(const float* __restrict__ w, int Cout, int Cin
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool st4(long a, long b, long c) { return a % 4 == 0 && b % 4 == 0 && c % 4 == 0; }
 
-constexpr int DW_TARGET_WG = 1024;  // ~4 workgroups per CU over the pixel splits
-constexpr int DW_MAX_SPLITS = 256;
+constexpr int DW_TARGET_WG = 2048;  // ~8 workgroups per CU over the pixel splits (the small-tile
+constexpr int DW_MAX_SPLITS = 1024;  // shapes are load-latency bound: occupancy hides it)
 
 inline void dw_tile(int Cout, int K, int& b1, int& b2) {
   b1 = Cout <= 64 ? 64 : 128;
@@ -421,7 +435,7 @@ inline int dw_splits(int M, int Cout, int K, int splits) {
   if (splits <= 0) {
     const int tiles = dw_tiles(Cout, K);
     splits = (DW_TARGET_WG + tiles - 1) / tiles;
-    const int maxs = (M + 255) / 256;  // at least 8 pixel steps per split
+    const int maxs = (M + 127) / 128;  // at least 4 pixel steps per split
     splits = splits < maxs ? splits : maxs;
   }
   if (splits > DW_MAX_SPLITS) splits = DW_MAX_SPLITS;

@@ -1,0 +1,89 @@
+"""bf16 conv kernels (csrc/conv_bf16.hip) in isolation over the Conformer-B/384 CNN-branch shapes
+(SemiFormer S1: B=8, mu=7 -> 120 images).  Per shape and pass: HIP-event time of one launch
+(+ its reduce for dW), algorithmic TFLOP/s (2 Cout Cin k^2 per output pixel) and GB/s of the
+algorithmic bytes (fp32 maps read / written once, bf16 weights).
+  python scripts/convb_bench.py [--n 120] [--iters 5]"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+import torch  # noqa: E402
+
+from endossl import _lib  # noqa: E402
+from endossl._lib import call, ptr  # noqa: E402
+
+# (name, H (input), Cin, Cout, k, s, p)
+SHAPES = [("st1_conv1_256to64", 96, 256, 64, 1, 1, 0), ("st1_conv2_64_3x3", 96, 64, 64, 3, 1, 1),
+          ("st1_conv3_64to256", 96, 64, 256, 1, 1, 0), ("st2_conv1_512to128", 48, 512, 128, 1, 1, 0),
+          ("st2_conv2_128_3x3", 48, 128, 128, 3, 1, 1), ("st2_conv3_128to512", 48, 128, 512, 1, 1, 0),
+          ("st3_conv2_256_3x3", 24, 256, 256, 3, 1, 1), ("st3_conv3_256to1024", 24, 256, 1024, 1, 1, 0),
+          ("patch_64to768_k4s4", 96, 64, 768, 4, 4, 0), ("st2_res_256to512_s2", 96, 256, 512, 1, 2, 0),
+          ("fcu_up_768to64", 24, 768, 64, 1, 1, 0)]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=120)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    lib = _lib.load()
+    s = _lib.stream()
+    dev = "cuda"
+    out = []
+    for name, H, Cin, Cout, k, st, p in SHAPES:
+        N = a.n
+        Ho = (H + 2 * p - k) // st + 1
+        M = N * Ho * Ho
+        x = torch.randn(N, H, H, Cin, device=dev)
+        w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
+        y = torch.empty(N, Ho, Ho, Cout, device=dev)
+        dy = torch.randn_like(y)
+        dx = torch.empty_like(x)
+        n = Cout * Cin * k * k
+        wp = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        wt = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        dw = torch.empty_like(w)
+        ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, Cin, k, k, 0), device=dev)
+        call("es_conv2d_pack_bf16", ptr(w), Cout, Cin, k, k, ptr(wp), ptr(wt), s)
+        xs = (H * H * Cin, H * Cin, Cin, 1)
+        ys = (Ho * Ho * Cout, Ho * Cout, Cout)
+
+        def fwd():
+            call("es_conv2d_fwd_bf16", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k, st, p, ptr(y), *ys, 0, s)
+
+        def dgrad():
+            call("es_conv2d_bwd_data_bf16", ptr(dy), *ys, ptr(wt), N, H, H, Cin, Cout, k, k, st, p, ptr(dx), *xs, 0, s)
+
+        def wgrad():
+            call("es_conv2d_bwd_weight_bf16", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys, Cout, k, k, st, p, 0, ptr(ws),
+                 ptr(dw), 0, s)
+
+        flop = 2.0 * M * Cout * Cin * k * k
+        xb, yb = 4.0 * N * H * H * Cin, 4.0 * M * Cout
+        rec = {"shape": name, "M": M, "GFLOP": round(flop / 1e9, 1)}
+        for pas, fn, byts in (("fwd", fwd, xb + yb), ("dgrad", dgrad, xb + yb), ("wgrad", wgrad, xb + yb)):
+            fn()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ts = []
+            for _ in range(a.iters):
+                e0.record(torch.cuda.current_stream())
+                fn()
+                e1.record(torch.cuda.current_stream())
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            t = sorted(ts)[len(ts) // 2] * 1e-3
+            rec[pas] = {"us": round(t * 1e6, 1), "TFLOPs": round(flop / t / 1e12, 1), "GBs": round(byts / t / 1e9)}
+        print(json.dumps(rec), flush=True)
+        out.append(rec)
+        del x, y, dy, dx, ws
+        torch.cuda.empty_cache()
+    tot = {p: sum(r[p]["us"] for r in out) for p in ("fwd", "dgrad", "wgrad")}
+    print(json.dumps({"total_us": tot}))
+
+
+if __name__ == "__main__":
+    main()
