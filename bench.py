@@ -12,8 +12,10 @@ Scaling (north_star / SURVEY.md §8(e)): "strong" (default) shards the global ba
 (64/N labeled + 448/N pairs per GPU: the DDP average of per-rank means is the global-batch gradient);
 "weak" gives every rank the full F1 batch.  The flat fp32 gradient's RCCL all-reduce is the only
 exchange.  One step = weak forward + train forward/backward + fused losses + grad all-reduce +
-Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.  The forward/backward runs as one
-captured hipGraph (FixMatch.use_graph) except where the live roofline probe needs eager launches.
+Adam/EMA sweep (code/fixmatch.py:91-131) -- nothing skipped.  Eager launches (--graph on replays
+the forward/backward as one captured hipGraph, FixMatch.use_graph: measured slower here).  At N > 1
+with strong scaling the line also carries `weak_scaling`: the same step timed with a full batch per
+rank (configs[2] as DDP would run it).
 
 Reported beside it:
   roofline      the dominant kernel (the most GPU time per step: rocprofv3, profiles/r02*_summary.md)
@@ -332,7 +334,9 @@ def main():
         B, MU = args.batch, args.mu
     model = NativeViT(ViTConfig(), seed=0)
     tr = FixMatch(model, device=dev)
-    graph = args.graph == "on" or (args.graph == "auto" and world > 1)
+    # eager by default: the captured-graph replay measured slower than eager launches at both the
+    # per-rank shard of N = 8 (B = 8: 7.11 vs 6.40 ms/step) and the full batch (r02)
+    graph = args.graph == "on"
     tr.use_graph = graph
     cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
                    MODEL=AttrDict(NAME="vit_small_patch16_224", NUM_CLASSES=23),
@@ -396,6 +400,28 @@ def main():
     eng.probe = None
     eng.overlap, eng.overlap_fwd = ov
     tr.use_graph = use_graph
+    weak = None
+    if world > 1 and args.scaling == "strong":
+        # configs[2] as the reference would run it under DDP: every rank a full B, mu batch (weak
+        # scaling), timed the same way; reported beside the strong-scaling value (not the headline)
+        xw, yw = make(args.batch, 224, g, dev), torch.randint(0, 23, (args.batch,), generator=g, device=dev)
+        bw = ((xw, yw), ((make(args.batch * MU, 224, g, dev), make(args.batch * MU, 224, g, dev)), None))
+        for _ in range(2):
+            tr.step(bw)
+        torch.cuda.synchronize()
+        dist.barrier()
+        w0 = time.perf_counter()
+        for _ in range(args.steps):
+            tr.step(bw)
+        torch.cuda.synchronize()
+        dist.barrier()
+        we = torch.tensor([time.perf_counter() - w0], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(we, op=torch.distributed.ReduceOp.MAX)
+        weak = {"per_gpu_batch": f"{args.batch} + {args.batch * MU} pairs",
+                "value": round(world * args.batch * MU * args.steps / we.item(), 2),
+                "ms_per_step": round(we.item() / args.steps * 1e3, 3),
+                "note": "same step with every rank on a full B=64, mu=7 batch (DDP weak scaling)"}
+        del xw, yw, bw
     iso_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / len(iso["events"])
     ev_ms = [e0.elapsed_time(e1) for e0, e1, _ in probe["events"]]
     flop = probe["events"][0][2]
@@ -446,6 +472,8 @@ def main():
                                       "note": "same launch with the engine's second HIP stream off (2 untimed "
                                               "steps): the live figure shares the CUs with the data-gradient chain"}},
         }
+        if weak is not None:
+            res["weak_scaling"] = weak
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline()
         print(json.dumps(res), flush=True)
