@@ -560,15 +560,12 @@ struct TNArgs {
 // workgroups of the first N2 tile also sum their A1 (= dY) tile columns from LDS: the bias
 // gradient of the same Linear, written as per-split partials PB[split][N1].
 template <int BKM, int NST>
-__global__ __launch_bounds__(256) void gemm_tn_kernel(TNArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void gemm_tn_body(const TNArgs& p, int split, int tile, char* smem) {
   constexpr int IPW = (BKM / 4) / 4;    // 1-KiB glds (4 rows of 256 B) per wave per operand per stage
   constexpr int PER = 2 * IPW;
   constexpr int TILE = BKM * BM * 2;     // bytes per operand tile
   constexpr int STAGE = 2 * TILE;
-  const int nt2 = p.N2 / BN, ntiles = (p.N1 / BM) * nt2;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = wg / ntiles, tile = wg - split * ntiles;
+  const int nt2 = p.N2 / BN;
   const int n1_0 = (tile / nt2) * BM, n2_0 = (tile % nt2) * BN;
   const bool do_bias = p.PB != nullptr && (tile % nt2) == 0;
   const int mbeg = split * p.mchunk;
@@ -665,6 +662,32 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(TNArgs p) {
     __syncthreads();
     if (bh == 0) p.PB[(size_t)split * p.N1 + n1_0 + bc] = bsum + red[bc];
   }
+}
+
+template <int BKM, int NST>
+__global__ __launch_bounds__(256) void gemm_tn_kernel(TNArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntiles = (p.N1 / BM) * (p.N2 / BN);
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / ntiles;
+  gemm_tn_body<BKM, NST>(p, split, wg - split * ntiles, smem);
+}
+
+// Grouped weight gradients: one launch over many independent TN problems, each tile over its
+// problem's whole token axis (no split-K: no fp32 slabs, no reduction launches).  Entry g's tiles
+// are the global tile indices [tile0_g, tile0_g + tiles_g); entries sorted by tile0.
+struct TNGroupEntry {
+  TNArgs a;
+  int tile0, pad;
+};
+template <int BKM, int NST>
+__global__ __launch_bounds__(256) void gemm_tn_grouped_kernel(const TNGroupEntry* __restrict__ grp, int ng) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int e = 0;
+  while (e + 1 < ng && grp[e + 1].tile0 <= wg) ++e;
+  const TNArgs a = grp[e].a;
+  gemm_tn_body<BKM, NST>(a, 0, wg - grp[e].tile0, smem);
 }
 
 // ---- weight gradient on a 384 x 192 output tile (N1 x N2) per 8-wave workgroup -----------------
@@ -1150,6 +1173,39 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
   }
   if (bias_out)
     launch_reduce_partials(PB, bias_out, S, N1, accumulate, stream);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// ---- grouped weight gradients (es_tn_problem, include/endossl.h) ----
+static_assert(sizeof(TNGroupEntry) == 64, "es_tn_problem layout");
+size_t es_tn_problem_size(void) { return sizeof(TNGroupEntry); }
+
+// Validate a host copy of the table and fill its tile0 / mchunk fields; returns the total tile
+// count (the grid), or a negative status.
+int es_gemm_tn_grouped_prepare(void* host_table, int count) {
+  if (!host_table || count <= 0) return ES_BAD_ARG;
+  TNGroupEntry* t = (TNGroupEntry*)host_table;
+  int tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    TNArgs& a = t[i].a;
+    if (!a.A1 || !a.A2 || !a.P) return ES_BAD_ARG;
+    if (a.M <= 0 || a.N1 % BM || a.N2 % BN || a.ld1 % 8 || a.ld2 % 8) return ES_BAD_SHAPE;
+    a.mchunk = (a.M + 31) / 32 * 32;
+    t[i].tile0 = tiles;
+    t[i].pad = 0;
+    tiles += (a.N1 / BM) * (a.N2 / BN);
+  }
+  return tiles;
+}
+
+// out_g = dY_g^T X_g (+ bias_g = column sums of dY_g) for every entry of a device table prepared by
+// es_gemm_tn_grouped_prepare (same count, total_tiles its return value).  Outputs overwritten.
+int es_gemm_tn_grouped(const void* device_table, int count, int total_tiles, hipStream_t stream) {
+  if (!device_table || count <= 0 || total_tiles <= 0) return ES_BAD_ARG;
+  const size_t lds = (size_t)2 * 2 * 32 * BM * 2;
+  allow_lds(gemm_tn_grouped_kernel<32, 2>, lds);
+  hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_grouped_kernel<32, 2>), dim3(total_tiles), dim3(256), lds, stream,
+                     (const TNGroupEntry*)device_table, count);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

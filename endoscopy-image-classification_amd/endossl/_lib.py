@@ -25,6 +25,9 @@ SIGNATURES = {
     "es_set_tn_variant": (I, [I]),
     "es_set_attn_variant": (I, [I]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),
+    "es_tn_problem_size": (Z, []),
+    "es_gemm_tn_grouped_prepare": (I, [V, I]),
+    "es_gemm_tn_grouped": (I, [V, I, I, V]),
     "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
     "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
     "es_attn_bwd": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),

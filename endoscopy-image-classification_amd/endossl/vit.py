@@ -210,6 +210,14 @@ class _Grads:
         self.dxm_cls = z(Mp, D)
 
 
+class _TNProblem(ctypes.Structure):
+    """es_tn_problem (include/endossl.h): one GEMM of a grouped weight-gradient launch."""
+    _fields_ = [("dy", ctypes.c_void_p), ("x", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("bias_out", ctypes.c_void_p), ("M", ctypes.c_int), ("N1", ctypes.c_int), ("N2", ctypes.c_int),
+                ("ld1", ctypes.c_int), ("ld2", ctypes.c_int), ("mchunk", ctypes.c_int), ("tile0", ctypes.c_int),
+                ("pad", ctypes.c_int)]
+
+
 class Engine:
     """Explicit forward / backward of the ViT over C-ABI kernels.  One per (model, device)."""
 
@@ -228,6 +236,17 @@ class Engine:
     # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
     # GEMMs beside the data-gradient chain ("bwd"); ENDOSSL_OVERLAP=0 serialises everything on the
     # caller's stream
+    # Weight gradients of a small shard (strong scaling: M = 12,608 train tokens per rank at N = 8) as ONE
+    # grouped launch after the data-gradient chain (es_gemm_tn_grouped: every 128x128 tile over its
+    # GEMM's whole token axis -- no split-K slabs, no per-GEMM reductions) instead of split-K launches
+    # on the side stream; the first half of the layers' launch overlaps the rest of the chain.
+    # Measured (bench.py --batch B, one MI355X, ms/step grouped vs split-K): B=8 6.11-6.15 vs 6.35;
+    # B=16 10.44 vs 10.34; B=32 19.41 vs 18.79; launches every 2 / 4 / 6 / 12 layers at B=8: 6.88 /
+    # 6.36 / 6.14 / 6.22.  "auto": when the train tokens M < GROUP_WGRAD_MAX_M (the N=8 shard of F1,
+    # M = 12,608); "1" always; "0" never.  bf16 engines only (no fp32 twin).
+    GROUP_WGRAD = os.environ.get("ENDOSSL_GROUP_WGRAD", "auto")
+    GROUP_WGRAD_MAX_M = 16384
+    GROUP_LAYERS = int(os.environ.get("ENDOSSL_GROUP_LAYERS", "6"))  # layers per grouped launch
     _OV = os.environ.get("ENDOSSL_OVERLAP", "1")
     OVERLAP_FWD = _OV in ("1", "fwd")
     OVERLAP = _OV in ("1", "bwd")
@@ -587,19 +606,43 @@ class Engine:
         ov = self.overlap
         main = torch.cuda.current_stream(self.device)
         side = self.side_stream() if ov else None
+        grouped = self._grouped_wgrad(M, grad_ready)
+        if grouped:
+            # one dY set per layer (+ a spare for layer 0's unused dY of the embedding): the grouped launch
+            # at the end reads every layer's weight-gradient inputs
+            key = (n, "grouped")
+            if key not in self._grads:
+                self._grads[key] = [G] + [_Grads(cfg, n, self.device, self.op_dtype) for _ in range(cfg.depth)]
+            GS = self._grads[key]
+        ovw = ov and not grouped
+        problems = []
 
-        def wgrad_side(*args, **kw):
-            """Weight-gradient GEMM on the side stream once the main stream has produced dY."""
+        def wgrad_side(dy, N1, x, N2, Mw, out, bias_out=None, ld1=None, ld2=None, label=None):
+            """Weight-gradient GEMM on the side stream once the main stream has produced dY (or, grouped,
+            recorded for the one launch after the chain)."""
+            if grouped:
+                problems.append((dy, N1, x, N2, Mw, out, bias_out, ld1 or N1, ld2 or N2))
+                return
             if not ov:
-                self._wgrad(*args, **kw)
+                self._wgrad(dy, N1, x, N2, Mw, out, bias_out, ld1=ld1, ld2=ld2, label=label)
                 return
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                self._wgrad(*args, **kw)
+                self._wgrad(dy, N1, x, N2, Mw, out, bias_out, ld1=ld1, ld2=ld2, label=label)
 
         done = {}
 
         def block_done(i):
+            if grouped and i > 0 and i % self.GROUP_LAYERS == 0 and problems:
+                # these layers' weight gradients as one grouped launch on the side stream, beside the
+                # rest of the data-gradient chain (their dY sets are never rewritten within the step)
+                if ov:
+                    side.wait_stream(main)
+                    with torch.cuda.stream(side):
+                        self._launch_grouped(problems, i)
+                else:
+                    self._launch_grouped(problems, i)
+                problems.clear()
             if grad_ready is None:
                 return
             lo = self.offs[f"blocks.{i}.norm1.weight"]
@@ -610,7 +653,7 @@ class Engine:
         if zero_grad:
             grad.zero_()
         prune = self._prune()
-        GL = GS[(cfg.depth - 1) % 2]
+        GL = GS[cfg.depth - 1] if grouped else GS[(cfg.depth - 1) % 2]
         # d(loss)/d(CLS tokens after the last block): compact rows (prune) or the CLS rows of G.dx
         dtop, Tt = (GL.c_dx, 1) if prune else (G.dx, T)
         if not prune:
@@ -626,7 +669,7 @@ class Engine:
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
                  cfg.num_classes, s)
         nh = n // 2
-        if (not prune and ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0
+        if (not grouped and not prune and ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0
                 and (nh * cfg.np) % 256 == 0 and grad.numel() % 4 == 0):
             return self._backward_lanes(flat, grad, A, G.dx, nh)
         if prune:
@@ -635,7 +678,10 @@ class Engine:
             self._call("es_cast_f32_bf16", ptr(G.dx), ptr(GL.dxb), M * D, s)
         for i in reversed(range(cfg.depth)):
             b = f"blocks.{i}."
-            Gi, Gn = GS[i % 2], GS[(i - 1) % 2]
+            if grouped:
+                Gi, Gn = GS[i], GS[i - 1] if i > 0 else GS[cfg.depth]
+            else:
+                Gi, Gn = GS[i % 2], GS[(i - 1) % 2]
             if prune and i == cfg.depth - 1:
                 # ---- the last block on its CLS rows: MLP, LN2 and projection over n compact rows
                 self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.c_dxb), D,
@@ -663,7 +709,7 @@ class Engine:
                     wgrad_side(Gi.dqkv, D, A.h1[i], D, n, gw[:D * D], gb[:D], ld1=T * 3 * D, ld2=T * D)
                 else:
                     wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gw, gb)
-                if ov:
+                if ovw:
                     done[i] = side.record_event()
                 self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), Gi.dxm_cls, G.dx, Gn.dxb,
                              gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
@@ -697,7 +743,7 @@ class Engine:
             self._call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
             wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
-            if ov:
+            if ovw:
                 done[i] = side.record_event()
                 if i + 1 in done:  # set (i-1) % 2 was layer i+1's: its weight gradients must be done
                     main.wait_event(done.pop(i + 1))
@@ -710,9 +756,48 @@ class Engine:
              s)
         npat = n * cfg.np
         wgrad_side(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
+        if grouped:
+            self._launch_grouped(problems, 0)
         if ov:
             main.wait_stream(side)
         return grad
+
+    def _grouped_wgrad(self, M, grad_ready):
+        if self.precision != "bf16" or grad_ready is not None:  # per-block hand-over needs per-layer launches
+            return False
+        return self.GROUP_WGRAD == "1" or (self.GROUP_WGRAD == "auto" and M < self.GROUP_WGRAD_MAX_M)
+
+    def _launch_grouped(self, problems, slot):
+        """One es_gemm_tn_grouped launch over the recorded weight-gradient GEMMs (longest token axis
+        first).  The table's pointers are stable for a batch size (cached buffers), so the device copy
+        (one per launch slot of the step) is re-made only when its bytes change."""
+        problems = sorted(problems, key=lambda q: -q[4])
+        tab = (_TNProblem * len(problems))()
+        for e, (dy, N1, x, N2, Mw, out, bias, ld1, ld2) in zip(tab, problems):
+            e.dy, e.x, e.out, e.bias_out = ptr(dy), ptr(x), ptr(out), ptr(bias) if bias is not None else None
+            e.M, e.N1, e.N2, e.ld1, e.ld2 = Mw, N1, N2, ld1, ld2
+        lib = _lib.load()
+        tiles = lib.es_gemm_tn_grouped_prepare(ctypes.byref(tab), len(problems))
+        if tiles <= 0:
+            raise _lib.EndosslLibraryError(f"es_gemm_tn_grouped_prepare: status {tiles}")
+        raw = bytes(tab)
+        if not hasattr(self, "_gtab"):
+            self._gtab = {}
+        cache = self._gtab.get(slot)
+        if cache is None or cache[0] != raw:
+            dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device, non_blocking=False)
+            self._gtab[slot] = cache = (raw, dev)
+        pr = self.probe
+        flop = sum(2.0 * q[4] * q[1] * q[3] for q in problems)
+        if pr is not None and pr["label"] == "fc1_wgrad":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            call("es_gemm_tn_grouped", ptr(cache[1]), len(problems), tiles, _lib.stream())
+            e1.record()
+            pr["events"].append((e0, e1, flop))
+            pr["kernel"] = f"es_gemm_tn_grouped ({len(problems)} weight-gradient GEMMs, {tiles} tiles)"
+        else:
+            call("es_gemm_tn_grouped", ptr(cache[1]), len(problems), tiles, _lib.stream())
 
 
     def head_backward(self, flat, grad, dlogits, train=False):

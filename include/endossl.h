@@ -56,6 +56,23 @@ size_t es_gemm_tn_workspace(int N1, int N2, int splits);
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream);
 int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream);
+/* Grouped weight gradients: many independent es_gemm_tn problems in ONE launch, each 128x128 tile
+ * over its problem's whole token axis (no split-K slabs, no reduction launches) -- the small-shard
+ * backward (strong scaling: M = 12,608 tokens per rank at N = 8), where split-K slabs and per-GEMM
+ * reductions cost more than the products.  N1, N2 % 128 == 0; rows [M, round_up(M, 32)) of dy zero;
+ * out / bias_out overwritten.  es_gemm_tn_grouped_prepare fills mchunk / tile0 of a HOST table and
+ * returns the total tile count; the caller copies the table to the device and launches. */
+typedef struct {
+  const void* dy;     /* A1 [M, N1] bf16, row stride ld1 */
+  const void* x;      /* A2 [M, N2] bf16, row stride ld2 */
+  float* out;         /* [N1, N2] fp32 */
+  float* bias_out;    /* [N1] fp32 column sums of dy, nullable */
+  int M, N1, N2, ld1, ld2;
+  int mchunk, tile0, pad;  /* filled by es_gemm_tn_grouped_prepare */
+} es_tn_problem;
+size_t es_tn_problem_size(void);
+int es_gemm_tn_grouped_prepare(void* host_table, int count);
+int es_gemm_tn_grouped(const void* device_table, int count, int total_tiles, hipStream_t stream);
 /* bias gradient: out[n] (+)= sum_m Y[m][n]  (workspace >= blocks*N floats) */
 int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
               hipStream_t stream);

@@ -445,3 +445,38 @@ def test_comatch_trainer_vs_reference_train_one(golden, tag):
     print(json.dumps(rec))
     assert worst <= 2e-3 * steps + 1e-5
     assert worst_e <= 1e-3 * 2e-3 * steps * (steps + 1) / 2 + 1e-6
+
+
+def test_comatch_bank_resize_between_steps():
+    """set_queue_size after a step (the C1 65,536-entry bank is set this way): the pseudo-label
+    workspace is sized by the queue size, so it must be re-made -- a step at the larger bank runs,
+    smooths against the new bank and writes into it without touching memory past its end."""
+    from endossl.comatch import CoMatch
+    from endossl.comatch_model import NativeViTEmb
+    from endossl.vit import ViTConfig
+    L, B, MU = 16, 2, 2
+    m = NativeViTEmb(ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23, head="emb", low_dim=L),
+                     seed=3).to(DEV)
+    tr = CoMatch(m, opt_func="Adam", lr=1e-3, device=DEV)
+    g = torch.Generator().manual_seed(9)
+    batches = [((torch.randn(B, 3, 64, 64, generator=g), torch.randint(0, 23, (B,), generator=g)),
+                (tuple(torch.randn(B * MU, 3, 64, 64, generator=g) for _ in range(3)), None)) for _ in range(3)]
+    tr.get_dataloader((_DL([b[0] for b in batches]), _DL([b[1] for b in batches])), None)
+    tr.get_config(_cfg(0.3, 3, B, MU, L))
+    tr.step(batches[0])
+    q0 = tr.queue_size
+    tr.set_queue_size(4 * q0 + 64)
+    guard = torch.full((1 << 20,), 7.0, device=DEV)  # allocated after the resize: a stale workspace would be
+    out = tr.step(batches[1])                         # smaller than the new bank's and overrun such blocks
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["loss"]).item() and torch.all(guard == 7.0)
+    assert tr.queue_feats.shape[0] == 4 * q0 + 64
+    # a bank of exactly the batch's rows opens the reference's write gate (code/comatch.py:192)
+    n = B + B * MU
+    tr.set_queue_size(n)
+    out = tr.step(batches[2])
+    torch.cuda.synchronize()
+    assert torch.isfinite(out["loss"]).item() and torch.all(guard == 7.0)
+    assert tr.queue_ptr == 0 and tr.queue_feats.abs().sum(1).gt(0).all().item()
+    norms = tr.queue_feats.norm(dim=1)
+    torch.testing.assert_close(norms, torch.ones_like(norms), rtol=1e-4, atol=1e-4)  # L2-normalised z rows

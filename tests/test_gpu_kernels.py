@@ -161,6 +161,42 @@ def test_gemm_tn_exact_integers(M, N1, N2, splits, tn_variant):
     torch.testing.assert_close(out, 2 * ref, rtol=0, atol=0)
 
 
+def test_gemm_tn_grouped_exact_integers():
+    """es_gemm_tn_grouped: several weight-gradient GEMMs (different M, N1, N2, row strides, with and
+    without the bias) in one launch, each tile over its whole token axis -- exact on integer data,
+    outputs and biases overwritten."""
+    import ctypes
+    from endossl.vit import _TNProblem
+    lib = _lib.load()
+    assert lib.es_tn_problem_size() == ctypes.sizeof(_TNProblem) == 64
+    g = torch.Generator().manual_seed(11)
+    shapes = [(3008, 384, 1536, None), (3008, 1536, 384, None), (992, 1152, 384, None), (3008, 384, 384, 640),
+              (64, 768, 384, None), (2000, 128, 128, None)]
+    keep, tab, refs = [], (_TNProblem * len(shapes))(), []
+    for e, (M, N1, N2, ld1) in zip(tab, shapes):
+        ld1 = ld1 or N1
+        A1 = _pad_rows(_int_bf16(M, ld1, lo=-2, hi=3, gen=g))
+        A2 = _pad_rows(_int_bf16(M, N2, lo=-2, hi=3, gen=g))
+        out = torch.full((N1, N2), 3.0, device=DEV)
+        bias = torch.full((N1,), 5.0, device=DEV) if N1 != 128 else None
+        keep += [A1, A2, out, bias]
+        e.dy, e.x, e.out, e.bias_out = ptr(A1), ptr(A2), ptr(out), ptr(bias) if bias is not None else None
+        e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, ld1, N2
+        refs.append((out, bias, A1[:M, :N1].float().t() @ A2[:M].float(), A1[:M, :N1].float().sum(0)))
+    tiles = lib.es_gemm_tn_grouped_prepare(ctypes.byref(tab), len(shapes))
+    assert tiles == sum((N1 // 128) * (N2 // 128) for _, N1, N2, _ in shapes)
+    dtab = torch.frombuffer(bytearray(bytes(tab)), dtype=torch.uint8).to(DEV)
+    call("es_gemm_tn_grouped", ptr(dtab), len(shapes), tiles, S())
+    torch.cuda.synchronize()
+    for out, bias, ref, bref in refs:
+        torch.testing.assert_close(out, ref, rtol=0, atol=0)
+        if bias is not None:
+            torch.testing.assert_close(bias, bref, rtol=0, atol=0)
+    bad = (_TNProblem * 1)()
+    bad[0].dy, bad[0].x, bad[0].out, bad[0].M, bad[0].N1, bad[0].N2, bad[0].ld1, bad[0].ld2 = 1, 1, 1, 10, 100, 128, 100, 128
+    assert lib.es_gemm_tn_grouped_prepare(ctypes.byref(bad), 1) == -1  # N1 % 128
+
+
 def test_colsum():
     torch.manual_seed(2)
     M, N = 5000, 1152

@@ -313,6 +313,40 @@ def test_two_lane_backward_matches_single_lane():
     assert worst <= 1e-5, worst
 
 
+@pytest.mark.parametrize("nimg", [40, 64])
+def test_grouped_weight_gradients_match_split_k(nimg):
+    """Engine.GROUP_WGRAD (the small-shard backward): every weight gradient from ONE grouped launch
+    after the data-gradient chain, one dY set per layer, gives the split-K side-stream gradients up to
+    fp32 summation order (split-K slabs vs whole-axis tiles); the rest of the step is the same launch
+    sequence.  nimg 64: the last block's CLS-row Q weight gradient (strided rows) is in the group."""
+    from endossl.vit import NativeViT
+    vcfg, _ = _tiny_cfgs()
+    m = NativeViT(vcfg, seed=6).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(nimg, 3, 64, 64, device=DEV, generator=g)
+    dl = torch.randn(nimg, 23, device=DEV, generator=g) * 1e-2
+    grads = {}
+    for mode in ("0", "1"):
+        eng.GROUP_WGRAD = mode
+        for _ in range(2):  # the second pass reuses the cached device table
+            eng.forward(m.flat, [x], train=True)
+            gr = torch.full_like(m.flat, 9.0)
+            eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        grads[mode] = gr.clone()
+    del eng.GROUP_WGRAD
+    worst = 0.0
+    for name, _ in eng.layout:
+        a, b = eng.view(grads["1"], name), eng.view(grads["0"], name)
+        assert torch.isfinite(a).all()
+        if b.abs().max() > 0:
+            worst = max(worst, _rel(a, b))
+    _record(f"grouped_wgrad_{nimg}", worst_rel_l2=worst)
+    assert worst <= 1e-5, worst
+
+
 @pytest.mark.parametrize("head,nimg", [("cls", 40), ("emb", 40), ("cls", 64), ("emb", 64)])
 def test_last_block_cls_rows_match_full_rows(head, nimg):
     """Engine.PRUNE_LAST (the last block's attention for the CLS queries only, its projection / LN2 /
