@@ -12,13 +12,11 @@ run() {  # name limit cmd...
 }
 ok() { [ "$1" -le 1 ]; }
 PT="python -u -m pytest -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread"
-run k 600 $PT tests/test_gpu_kernels.py; rc=$?
-ok $rc && { run s 600 $PT tests/test_gpu_step.py; rc=$?; }
-ok $rc && { run c 600 $PT tests/test_gpu_comatch.py; rc=$?; }
-ok $rc && { run cf 600 $PT tests/test_gpu_conformer.py; rc=$?; }
-ok $rc && { run dist 300 $PT tests/test_gpu_dist.py; rc=$?; }
+run t 1100 $PT -m gpu -x tests/; rc=$?   # the driver's round-end GPU tier: every gpu test, one process
 ok $rc && { run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; }
 ok $rc && { run bench 600 python bench.py --steps 10 --warmup 3; rc=$?; }
+ok $rc && { run c1 300 python bench.py --workload c1 --steps 5 --warmup 2; rc=$?; }
+ok $rc && { run s1 400 python bench.py --workload s1 --steps 3 --warmup 2; rc=$?; }
 if ok $rc && [ "${PROFILE:-1}" = 1 ]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; rc=$?
