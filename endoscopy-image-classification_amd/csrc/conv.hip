@@ -1044,6 +1044,34 @@ int launch_conv_dx(const float* dy, const float* w, float* dx, const ConvGeom& g
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+// ---- BatchNorm2d over the global batch (SyncBatchNorm across ranks) -------------------------
+__global__ void bn_mean_from_sum_kernel(const float* __restrict__ sum_g, float rows_g, int C, float* __restrict__ mean) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) mean[c] = sum_g[c] / rows_g;
+}
+// mean / biased var from the global sums; running stats with the unbiased var; rstd saved
+__global__ void bn_finalize_global_kernel(const float* __restrict__ sum_g, const float* __restrict__ sq_g, float rows_g,
+                                          int C, float eps, float momentum, float* __restrict__ mean,
+                                          float* __restrict__ rstd, float* __restrict__ run_mean,
+                                          float* __restrict__ run_var) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mu = sum_g[c] / rows_g, var = sq_g[c] / rows_g;
+  mean[c] = mu;
+  rstd[c] = 1.0f / sqrtf(var + eps);
+  const float unb = rows_g > 1.f ? sq_g[c] / (rows_g - 1.f) : var;
+  run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+  run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+}
+// dbeta (+)= local sum g, dgamma (+)= local sum g xhat (sums_local = [sum g | sum g xhat])
+__global__ void bn_param_grads_kernel(const float* __restrict__ sums_local, int C, float* __restrict__ dgamma,
+                                      float* __restrict__ dbeta, int accumulate) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  dbeta[c] = accumulate ? dbeta[c] + sums_local[c] : sums_local[c];
+  dgamma[c] = accumulate ? dgamma[c] + sums_local[C + c] : sums_local[C + c];
+}
+
 }  // namespace
 
 extern "C" {
@@ -1236,6 +1264,105 @@ int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows, mean, rstd,
                        gamma, sums, dx, gout);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// ---- SyncBatchNorm2d (the Conformer's BatchNorm2d over the global batch at N > 1) ------------
+// Per-channel sums of an NHWC map [rows, C] (contiguous):  mode 0: out[c] = sum x;  mode 1:
+// out[c] = sum (x - sum_g[c] / rows_g)^2, centred on the GLOBAL mean (sum_g = the all-reduced mode-0
+// sums).  workspace: es_chan_workspace(rows, C) floats.
+int es_bn2d_sums(const float* x, int rows, int C, int mode, const float* sum_g, int rows_g, float* out,
+                 float* workspace, hipStream_t stream) {
+  if (!x || !out || !workspace || (mode == 1 && !sum_g)) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || (mode != 0 && mode != 1) || (mode == 1 && rows_g <= 0)) return ES_BAD_SHAPE;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  float* mean = workspace + (size_t)G * 2 * C;  // [C] (the tail es_bn2d_bwd keeps for its sums)
+  const bool v4 = C % 4 == 0 && al16(x) && al16(mean);
+  if (mode == 1)
+    hipLaunchKernelGGL(bn_mean_from_sum_kernel, (C + 255) / 256, 256, 0, stream, sum_g, (float)rows_g, C, mean);
+#define BN_SUMS(MODE_, V_)                                                                                      \
+  hipLaunchKernelGGL((chan_partial_kernel<MODE_, V_>), G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr, \
+                     nullptr, 0, workspace)
+  if (mode == 0) {
+    if (v4) BN_SUMS(0, 4); else BN_SUMS(0, 1);
+  } else {
+    if (v4) BN_SUMS(1, 4); else BN_SUMS(1, 1);
+  }
+#undef BN_SUMS
+  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
+  hipLaunchKernelGGL(chan_final_kernel<0>, (C + 15) / 16, 256, 0, stream, workspace, G, C, f);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Train-mode BatchNorm2d from the global sums (sum_g, centred sq_g over rows_g rows): mean / rstd
+// saved, running stats updated (unbiased variance over rows_g), num_batches_tracked += 1 (nullable),
+// y = bn(x) (+ res) then ReLU if relu -- es_bn2d_fwd with the statistics of every rank's rows.
+int es_bn2d_fwd_global(const float* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                       float* running_var, void* num_batches_tracked, float momentum, float eps, const float* sum_g,
+                       const float* sq_g, int rows_g, const float* res, int relu, float* y, float* mean, float* rstd,
+                       hipStream_t stream) {
+  if (!x || !gamma || !beta || !running_mean || !running_var || !sum_g || !sq_g || !y || !mean || !rstd)
+    return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || rows_g < rows) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(bn_finalize_global_kernel, (C + 255) / 256, 256, 0, stream, sum_g, sq_g, (float)rows_g, C, eps,
+                     momentum, mean, rstd, running_mean, running_var);
+  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+  const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) && al16(mean) &&
+                  al16(rstd);
+  if (v4)
+    hipLaunchKernelGGL(bn_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mean, rstd, nullptr,
+                       eps, gamma, beta, res, relu, y);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<1>, grid1d(n), 256, 0, stream, x, (int)n, C, mean, rstd, nullptr, eps, gamma,
+                       beta, res, relu, y);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Backward, local half: out[0..C) = sum g, out[C..2C) = sum g xhat over this rank's rows
+// (g = dy * [y > 0 if relu]).  workspace: es_chan_workspace(rows, C) floats.
+int es_bn2d_bwd_sums(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* mean,
+                     const float* rstd, float* out, float* workspace, hipStream_t stream) {
+  if (!x || !dy || !mean || !rstd || !out || !workspace || (relu && !y)) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  const bool v4 = C % 4 == 0 && al16(x) && al16(dy) && (!y || al16(y)) && al16(mean) && al16(rstd);
+  if (v4)
+    hipLaunchKernelGGL((chan_partial_kernel<2, 4>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
+                       workspace);
+  else
+    hipLaunchKernelGGL((chan_partial_kernel<2, 1>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
+                       workspace);
+  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
+  hipLaunchKernelGGL(chan_final_kernel<0>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Backward, global half: dx = rstd gamma (g - sum_g g / rows_g - xhat sum_g (g xhat) / rows_g) with the
+// all-reduced sums (so dx is d(sum of every rank's loss)/dx), gout = g (nullable: the residual
+// input's gradient); dgamma / dbeta (+)= this rank's LOCAL sums (the gradient all-reduce averages them).
+int es_bn2d_bwd_global(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
+                       const float* mean, const float* rstd, const float* sums_local, const float* sums_g, int rows_g,
+                       float* dx, float* gout, float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
+  if (!x || !dy || !gamma || !mean || !rstd || !sums_local || !sums_g || !dx || !dgamma || !dbeta || (relu && !y))
+    return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || rows_g < rows) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(bn_param_grads_kernel, (C + 255) / 256, 256, 0, stream, sums_local, C, dgamma, dbeta, accumulate);
+  const bool v4 = C % 4 == 0 && al16(x) && al16(dy) && (!y || al16(y)) && al16(dx) && (!gout || al16(gout)) &&
+                  al16(mean) && al16(rstd) && al16(gamma) && al16(sums_g);
+  if (v4)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
+                       rows_g, mean, rstd, gamma, sums_g, dx, gout);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows_g, mean,
+                       rstd, gamma, sums_g, dx, gout);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

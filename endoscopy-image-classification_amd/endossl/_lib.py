@@ -90,6 +90,10 @@ SIGNATURES = {
     "es_chan_sum": (I, [V, I, I, L, L, I, V, V, I, V]),
     "es_bn2d_fwd": (I, [V, I, I, V, V, V, V, V, F, F, I, V, I, V, V, V, V, V]),
     "es_bn2d_bwd": (I, [V, V, V, I, I, I, V, V, V, I, V, F, V, V, V, V, I, V, V]),
+    "es_bn2d_sums": (I, [V, I, I, I, V, I, V, V, V]),
+    "es_bn2d_fwd_global": (I, [V, I, I, V, V, V, V, V, F, F, V, V, I, V, I, V, V, V, V]),
+    "es_bn2d_bwd_sums": (I, [V, V, V, I, I, I, V, V, V, V, V]),
+    "es_bn2d_bwd_global": (I, [V, V, V, I, I, I, V, V, V, V, V, I, V, V, V, V, I, V]),
     "es_maxpool2d_fwd": (I, [V, I, I, I, I, I, I, I, V, V, V]),
     "es_maxpool2d_bwd": (I, [V, V, I, I, I, I, I, I, I, V, V]),
     "es_avgpool2d_fwd": (I, [V, I, I, I, I, I, V, V]),

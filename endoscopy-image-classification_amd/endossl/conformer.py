@@ -29,7 +29,7 @@ from copy import deepcopy
 import torch
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, dist
 from ._lib import call, ptr
 
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32 = 0, 1, 2, 3, 4
@@ -358,11 +358,25 @@ class _BNFn(torch.autograd.Function):
         ws = torch.empty(_lib.load().es_chan_workspace(rows, C), device=x.device)
         rm, rv, nbt = m.bn_buffers(pre)
         res_c = res.contiguous() if res is not None else None  # keep temporaries alive across the launch
-        call("es_bn2d_fwd", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")), ptr(rm),
-             ptr(rv), ptr(nbt) if train else None, BN_MOMENTUM, eps, 1 if train else 0, ptr(res_c),
-             1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), _s())
+        world = dist.world_size() if train and getattr(m, "sync_bn", True) else 1
+        if world > 1:
+            # SyncBatchNorm over every rank's rows (the single-process statistics)
+            rows_g = rows * world
+            sums = torch.empty(2, C, device=x.device)
+            call("es_bn2d_sums", ptr(x), rows, C, 0, None, 0, ptr(sums[0]), ptr(ws), _s())
+            dist.allreduce_inplace_(sums[0])
+            call("es_bn2d_sums", ptr(x), rows, C, 1, ptr(sums[0]), rows_g, ptr(sums[1]), ptr(ws), _s())
+            dist.allreduce_inplace_(sums[1])
+            call("es_bn2d_fwd_global", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")),
+                 ptr(rm), ptr(rv), ptr(nbt), BN_MOMENTUM, eps, ptr(sums[0]), ptr(sums[1]), rows_g, ptr(res_c),
+                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), _s())
+        else:
+            call("es_bn2d_fwd", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")), ptr(rm),
+                 ptr(rv), ptr(nbt) if train else None, BN_MOMENTUM, eps, 1 if train else 0, ptr(res_c),
+                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), _s())
         ctx.save_for_backward(x, y, mean, rstd)
         ctx.m, ctx.pre, ctx.eps, ctx.relu, ctx.train, ctx.has_res = m, pre, eps, relu, train, res is not None
+        ctx.world = world
         return y
 
     @staticmethod
@@ -377,6 +391,15 @@ class _BNFn(torch.autograd.Function):
         gout = torch.empty_like(x) if ctx.has_res else None
         ws = torch.empty(_lib.load().es_chan_workspace(rows, C), device=x.device)
         _, rv, _ = m.bn_buffers(pre)
+        if ctx.world > 1:
+            loc = torch.empty(2 * C, device=x.device)
+            call("es_bn2d_bwd_sums", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(mean), ptr(rstd),
+                 ptr(loc), ptr(ws), _s())
+            glob = dist.allreduce_inplace_(loc.clone())
+            call("es_bn2d_bwd_global", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0,
+                 ptr(m.pview(pre + "weight")), ptr(mean), ptr(rstd), ptr(loc), ptr(glob), rows * ctx.world, ptr(dx),
+                 ptr(gout), ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, _s())
+            return dx, gout, None, None, None, None
         call("es_bn2d_bwd", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(m.pview(pre + "weight")),
              ptr(mean), ptr(rstd), 1 if ctx.train else 0, ptr(rv), ctx.eps, ptr(dx), ptr(gout),
              ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(ws), _s())

@@ -298,6 +298,23 @@ int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float
 int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
                 const float* mean, const float* rstd, int train, const float* running_var, float eps, float* dx,
                 float* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t stream);
+/* SyncBatchNorm2d: the Conformer's BatchNorm2d over the global batch at N > 1 (SURVEY.md §8(e):
+ * exact parity with the single-process step needs the statistics of every rank's rows).  Flow per
+ *  BatchNorm: es_bn2d_sums [mode 0] -> all-reduce -> es_bn2d_sums [mode 1: centred on the global mean]
+ * -> all-reduce -> es_bn2d_fwd_global; backward: es_bn2d_bwd_sums -> all-reduce of a copy ->
+ * es_bn2d_bwd_global [dx from the global sums, dgamma / dbeta from the local ones].  rows_g = the
+ * rows of every rank together; workspace = es_chan_workspace(rows, C) floats. */
+int es_bn2d_sums(const float* x, int rows, int C, int mode, const float* sum_g, int rows_g, float* out,
+                 float* workspace, hipStream_t stream);
+int es_bn2d_fwd_global(const float* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                       float* running_var, void* num_batches_tracked, float momentum, float eps, const float* sum_g,
+                       const float* sq_g, int rows_g, const float* res, int relu, float* y, float* mean, float* rstd,
+                       hipStream_t stream);
+int es_bn2d_bwd_sums(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* mean,
+                     const float* rstd, float* out, float* workspace, hipStream_t stream);
+int es_bn2d_bwd_global(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
+                       const float* mean, const float* rstd, const float* sums_local, const float* sums_g, int rows_g,
+                       float* dx, float* gout, float* dgamma, float* dbeta, int accumulate, hipStream_t stream);
 int es_maxpool2d_fwd(const float* x, int N, int H, int W, int C, int k, int s, int p, float* y, void* arg,
                      hipStream_t stream);
 int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,

@@ -38,6 +38,7 @@ def _worker(rank, world, port, q):
         cfg = ViTConfig(img_size=64, dim=128, depth=3, heads=2, num_classes=23)
         m = NativeViT(cfg, seed=3).to("cuda")
         eng = m.engine()
+        eng.GROUP_WGRAD = "0"  # the same split-K weight-gradient launches in both reverse passes
         eng.pack(m.flat, m.version)
         g = torch.Generator(device="cuda").manual_seed(10 + rank)
         x = torch.randn(64, 3, 64, 64, device="cuda", generator=g)
@@ -245,3 +246,83 @@ def test_two_rank_comatch_global_batch(precision):
             assert abs(got[key] - full[key]) <= 1e-5 * max(1.0, abs(full[key])), (rank, key, got[key], full[key])
         assert rel <= (1e-5 if precision == "fp32" else 1e-3), (rank, rel)
         assert bn <= 1e-5, (rank, bn)  # SyncBatchNorm: the running statistics of the global batch
+
+
+def _semiformer_shard_worker(rank, world, port, q):
+    """SemiFormer at N > 1 (BN backbones need SyncBN for the single-process result): the
+    Conformer's BatchNorm2d statistics over every rank's rows (es_bn2d_sums -> all-reduce ->
+    es_bn2d_fwd_global; backward es_bn2d_bwd_sums -> all-reduce -> es_bn2d_bwd_global).  Shards of a
+    global batch vs the one-process step."""
+    sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+    sys.path.insert(0, ROOT)
+    from endossl import dist
+    from endossl.conformer import ConformerConfig, NativeConformer
+    from endossl.semiformer import SemiFormer
+    from endossl.utils import AttrDict
+    ccfg = ConformerConfig(img_size=64, patch=16, base_channel=64, channel_ratio=1, embed_dim=128, depth=3, heads=2,
+                           num_classes=23)
+    B, MU = 4, 2
+    g = torch.Generator().manual_seed(41)
+    x, y = torch.randn(B, 3, 64, 64, generator=g), torch.randint(0, 23, (B,), generator=g)
+    uw, us = torch.randn(B * MU, 3, 64, 64, generator=g), torch.randn(B * MU, 3, 64, 64, generator=g)
+
+    def trainer(n_b):
+        m = NativeConformer(ccfg, seed=4).to("cuda").set_conv_precision("fp32")
+        tr = SemiFormer(m, device="cuda")
+        tr.get_dataloader((None, None), None)
+        tr.get_config(AttrDict(DATA=AttrDict(BATCH_SIZE=n_b, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
+                               MODEL=AttrDict(NAME="conformer", NUM_CLASSES=23),
+                               TRAIN=AttrDict(IS_FREEZE=False, USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3,
+                                              EVAL_STEP=1, CLS_WEIGHT=False, THRES=0.05, T=1.0, LAMBDA_U=1.0,
+                                              EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4,
+                                              LR_DECAY=0.8, SCH_NAME="const")))
+        return m, tr
+
+    m1, tr1 = trainer(B)
+    o1 = tr1.step(((x, y), ((uw, us), None)))
+    torch.cuda.synchronize()
+    full = {k: o1[k].item() for k in ("lx", "lu")}
+    full_grad = m1.flat_grad.clone()
+    bn_names = [n for n, _, kind in m1.layout if kind in ("rm", "rv")]
+    full_bn = {n: m1.get_buffer(n).clone() for n in bn_names}
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    dist.init_from_env(backend="gloo")
+    try:
+        b, n = B // world, B * MU // world
+        m, tr = trainer(b)
+        sl, su = slice(rank * b, (rank + 1) * b), slice(rank * n, (rank + 1) * n)
+        o = tr.step(((x[sl], y[sl]), ((uw[su], us[su]), None)))
+        torch.cuda.synchronize()
+        loc = torch.tensor([o["lx"].item(), o["lu"].item()])
+        torch.distributed.all_reduce(loc)
+        got = {"lx": loc[0].item() / world, "lu": loc[1].item() / world}
+        rel = ((m.flat_grad / world - full_grad).norm() / full_grad.norm()).item()
+        bn = max((m.get_buffer(k) - v).abs().max().item() / max(1.0, v.abs().max().item()) for k, v in full_bn.items())
+        nbt = int(m.get_buffer("bn1.num_batches_tracked").item())
+        q.put((rank, got, full, rel, bn, nbt))
+        dist.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_rank_semiformer_sync_batchnorm():
+    """The transformer blocks stay bf16 (their shard-sized GEMMs round in a different order), the convs
+    fp32: losses to 1e-3, the flat gradient to 1e-2 relative L2, every running statistic of the global
+    batch to 1e-4 relative -- without SyncBN the per-rank statistics differ at the 1e-1 level."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_semiformer_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got, full, rel, bn, nbt in res:
+        for key in ("lx", "lu"):
+            assert abs(got[key] - full[key]) <= 1e-3 * max(1.0, abs(full[key])), (rank, key, got[key], full[key])
+        assert rel <= 1e-2, (rank, rel)
+        assert bn <= 1e-4, (rank, bn)
+        assert nbt == 1
