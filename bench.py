@@ -227,6 +227,32 @@ def run_secondary(args):
                      else 0.0)
         desc = (f"C1: CoMatch ViT-S/16 step, B={B} + 3 x mu*B={B * MU} (weak, strong0, strong1), 224^2, L={L}, "
                 f"bank Q={Q} (memory smoothing over all Q rows), EMA 0.999, lambda_u=lambda_c=2")
+    elif args.workload == "p0":
+        # BASELINE configs[0]: the supervised baseline (code/supervised.py:111-138 plain path) -- the
+        # reference runs it on CPU as plumbing; here the native ResNet-18 step on the GPU
+        from endossl.resnet import NativeResNet, ResNetConfig
+        from endossl.supervised import SupLearning
+        B = args.batch if args.batch != 64 else 16
+        model = NativeResNet(ResNetConfig(num_classes=23), seed=0)
+        tr = SupLearning(model, device=dev)
+
+        class _DS:
+            df = None
+        tr.get_dataloader(type("DL", (list,), {"dataset": _DS()})(), None, None)
+        tr.get_config(AttrDict(DATA=AttrDict(BATCH_SIZE=B, IMG_SIZE=224, TARGET_NAME="target"),
+                               MODEL=AttrDict(NAME="resnet18", NUM_CLASSES=23, MARGIN="None", IS_TRIPLET=False),
+                               TRAIN=AttrDict(USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, CLS_WEIGHT=False, EPOCHS=1,
+                                              WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4, LR_DECAY=0.8,
+                                              SCH_NAME="const")))
+        tr.class_weights = torch.linspace(0.5, 2.0, 23, device=dev)
+        x, y = synth_images(B, 224, g, dev), torch.randint(0, 23, (B,), generator=g, device=dev)
+        batch = (x, y)
+        unl = B  # labeled images per step (the metric's unit for this workload)
+        tfl = 3 * 2 * 1.8186e9 * B / 1e12  # resnet18 at 224^2: 1.8186 GMAC forward per image
+        exe = tfl
+        desc = (f"P0: supervised ResNet-18 step (timm resnet18, 23 classes; code/supervised.py:111-138), B={B}, "
+                f"224^2, weighted CE, Adam 1e-3, EMA 0.999; convs with channels % 32 == 0 on bf16 MFMA "
+                f"({'on' if model.conv_bf16 else 'off'}), the stem fp32")
     else:
         from endossl.conformer import ConformerConfig, NativeConformer
         from endossl.semiformer import SemiFormer
@@ -277,8 +303,10 @@ def run_secondary(args):
     if rank == 0:
         ms = T / args.steps * 1e3
         print(json.dumps({
-            "metric": f"unlabeled images/sec/node ({args.workload.upper()})", "value": round(world * unl * args.steps / T, 2),
-            "unit": "unlabeled images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "metric": (f"labeled images/sec/node (P0)" if args.workload == "p0" else
+                       f"unlabeled images/sec/node ({args.workload.upper()})"),
+            "value": round(world * unl * args.steps / T, 2),
+            "unit": "labeled images/s" if args.workload == "p0" else "unlabeled images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "bf16 operands (GEMMs, convs) / fp32 accumulate, maps, BatchNorm",
             "data": "synthetic (HBM-resident, seed 0)", "config": {"workload": desc, "parallelism": f"dp{world}"},
@@ -306,7 +334,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inputs", choices=("u8", "f32"), default="u8",
                     help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")
-    ap.add_argument("--workload", choices=("f1", "c1", "s1"), default="f1",
+    ap.add_argument("--workload", choices=("f1", "c1", "s1", "p0"), default="f1",
                     help="f1 = the BASELINE metric (default); c1 / s1 = CoMatch / SemiFormer configs")
     ap.add_argument("--s1-model", choices=("b384", "ti224"), default="b384",
                     help="s1: the ViT-Base/16 384^2 stress Conformer (BASELINE configs[4]) or build.py's Conformer-Ti")

@@ -16,6 +16,7 @@ import torch
 
 from .comatch_model import NativeViTEmb
 from .conformer import ConformerConfig, NativeConformer
+from .resnet import NativeResNet, ResNetConfig
 from .vit import VIT_CONFIGS, NativeViT, ViTConfig
 
 
@@ -34,6 +35,13 @@ def build_model(config, is_pathology=True, seed=0):
                   or v.shape[0] == C}
             model.load_state_dict(sd, strict=False)
         return model
+    if name == "resnet18":
+        # the supervised baseline (BASELINE configs[0]; code/build.py:218-220 timm.create_model('resnet18',
+        # num_classes=C): ImageNet weights are a download, unavailable here -- timm's random init)
+        if getattr(config.MODEL, "PRE_TRAIN_PATH", "None") not in (None, "None", ""):
+            raise NotImplementedError("resnet18 + PRE_TRAIN_PATH swaps fc for build_head's MLP "
+                                      "(code/build.py:202-211): outside the native scope")
+        return NativeResNet(ResNetConfig(num_classes=C), seed=seed)
     if name not in VIT_CONFIGS:
         raise NotImplementedError(f"backbone {name!r}: native builds exist for {sorted(VIT_CONFIGS)}")
     comatch = getattr(config.MODEL, "TYPE_SEMI", "FixMatch") == "CoMatch" and getattr(config.TRAIN, "IS_SSL", True)

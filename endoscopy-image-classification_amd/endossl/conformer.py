@@ -674,19 +674,22 @@ class _BlockFn(torch.autograd.Function):
 
 
 class _ConvHeadFn(torch.autograd.Function):
-    """AdaptiveAvgPool2d(1) + flatten + conv_cls_head Linear (Conformer.forward :438-439)."""
+    """AdaptiveAvgPool2d(1) + flatten + conv_cls_head Linear (Conformer.forward :438-439; also
+    ResNet's global pool + fc, pre="fc.")."""
 
     @staticmethod
-    def forward(ctx, x, m, anchor=None):
+    def forward(ctx, x, m, anchor=None, pre="conv_cls_head."):
         N, H, W, C = x.shape
+        if H != W:
+            raise ValueError(f"the global-pool head expects square maps, got {H}x{W}")
         ncls = m.cfg.num_classes
         pooled = torch.empty(N, C, device=x.device)
         call("es_avgpool2d_fwd", ptr(x.contiguous()), N, H, W, C, H, ptr(pooled), _s())
         logits = torch.empty(N, ncls, device=x.device)
-        call("es_dense_fwd", ptr(pooled), C, ptr(m.pview("conv_cls_head.weight")), ptr(m.pview("conv_cls_head.bias")),
+        call("es_dense_fwd", ptr(pooled), C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")),
              ptr(logits), ncls, N, C, ncls, 0, 0.0, None, 1.0, _s())
         ctx.save_for_backward(pooled)
-        ctx.m, ctx.geom = m, (N, H, W, C)
+        ctx.m, ctx.geom, ctx.pre = m, (N, H, W, C), pre
         return logits
 
     @staticmethod
@@ -699,14 +702,15 @@ class _ConvHeadFn(torch.autograd.Function):
         dl = dl.contiguous()
         dpooled = torch.empty(N, C, device=dl.device)
         ws = torch.empty(_lib.load().es_dense_bwd_workspace(N, ncls), device=dl.device)
+        pre = ctx.pre
         call("es_dense_bwd", ptr(dl), ncls, None, 0, 0, 0.0, None, 1.0, ptr(pooled), C,
-             ptr(m.pview("conv_cls_head.weight")), ptr(dpooled), C, 0, ptr(m.gview("conv_cls_head.weight")),
-             ptr(m.gview("conv_cls_head.bias")), N, C, ncls, ptr(ws), _s())
+             ptr(m.pview(pre + "weight")), ptr(dpooled), C, 0, ptr(m.gview(pre + "weight")),
+             ptr(m.gview(pre + "bias")), N, C, ncls, ptr(ws), _s())
         if getattr(m, "frozen_trunk", False):  # IS_FREEZE: the head's parameters only
-            return None, None, None
+            return None, None, None, None
         dx = torch.empty(N, H, W, C, device=dl.device)
         call("es_avgpool2d_bwd", ptr(dpooled), N, H, W, C, H, ptr(dx), 0, _s())
-        return dx, None, None
+        return dx, None, None, None
 
 
 class _TransHeadFn(torch.autograd.Function):
@@ -839,7 +843,7 @@ class NativeConformer(nn.Module):
         return self
 
     def __deepcopy__(self, memo):
-        other = NativeConformer.__new__(NativeConformer)
+        other = type(self).__new__(type(self))
         nn.Module.__init__(other)
         other.cfg, other.layout, other.offs, other.numel, other.shapes = (self.cfg, self.layout, self.offs,
                                                                           self.numel, self.shapes)

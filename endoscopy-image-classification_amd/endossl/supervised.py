@@ -1,0 +1,191 @@
+"""Supervised trainer with the reference's API (`SupLearning`, code/supervised.py:23-360) over the
+native models -- BASELINE configs[0] (ResNet-18, 23 classes, B=16, 224²) as a GPU step.
+
+Same constructor and methods -- get_dataloader(train_dl, valid_dl, mixup_fn, test_dl), get_config,
+train_one, evaluate_one, save_checkpoint, load_checkpoint, fit -- plus `step(batch)`.  One step
+(:111-138, the plain path: MODEL.MARGIN 'None', no triplet, no mixup):
+
+  fwd    logits = model(images)
+  loss   F.cross_entropy(logits, y, weight=class_weights, reduction='mean')   (ce_loss type 'none',
+         code/loss.py:118) -- value and d(loss)/d(logits) in one kernel (es_ce_weighted_fwd_bwd)
+  bwd    autograd over the HIP ops
+  opt    Adam + EMA of the parameters in one sweep, EMA of the BatchNorm buffers, LR update
+
+The margin (AngularPenaltySMLoss), triplet and mixup paths are out of the §8 scope
+and raise NotImplementedError.
+"""
+import os
+from datetime import date, datetime
+
+import numpy as np
+import torch
+
+from . import _lib, dist
+from ._lib import call, ptr
+from .conformer import join_wgrad_stream
+from .ema import ModelEMA
+from .lr_scheduler import build_scheduler
+from .optimizer import build_optimizer
+from .utils import AverageMeter, balanced_class_weights, calculate_metrics
+
+
+class SupLearning:
+    def __init__(self, model, opt_func="Adam", lr=1e-3, device='cpu', wandb=None):
+        self.model = model
+        self.opt_func = opt_func
+        self.device = device
+        self.model.to(self.device)
+        self.epoch_start = 0
+        self.best_valid_loss = None
+        self.best_valid_score = None
+        self.wandb = wandb
+
+    def get_dataloader(self, train_dl, valid_dl, mixup_fn=None, test_dl=None):
+        self.train_dl = train_dl
+        self.valid_dl = valid_dl
+        self.test_dl = test_dl
+        if mixup_fn is not None:
+            raise NotImplementedError("mixup (code/supervised.py:112-113) is outside the native step's scope")
+        self.mixup_fn = None
+
+    def get_config(self, config):
+        self.config = config
+        print('Training mode: Supervised Learning')
+        if getattr(config.MODEL, "IS_TRIPLET", False) or str(getattr(config.MODEL, "MARGIN", "None")) != "None":
+            raise NotImplementedError("the triplet / angular-margin losses are outside the native step's scope")
+        dist.broadcast_(self.model.flat)
+        self.model.mark_updated()
+        self.ema_model = ModelEMA(model=self.model, decay=config.TRAIN.EMA_DECAY, device=self.device) \
+            if config.TRAIN.USE_EMA else None
+        self.optimizer = build_optimizer(self.model, opt_func=self.opt_func, lr=config.TRAIN.BASE_LR)
+        n_iter = len(self.train_dl) if self.train_dl is not None else 1
+        self.lr_scheduler = build_scheduler(config=config, optimizer=self.optimizer, n_iter_per_epoch=n_iter)
+        if config.TRAIN.CLS_WEIGHT:
+            df = self.train_dl.dataset.df
+            self.class_weights = torch.tensor(balanced_class_weights(df[config.DATA.TARGET_NAME]),
+                                              dtype=torch.float).to(self.device)
+        else:
+            self.class_weights = None
+
+    def step(self, batch):
+        """batch = (images [n, 3, H, W], targets [n]) -> {"loss", "logits"} (device tensors)."""
+        images, targets = batch
+        dev = self.model.flat.device
+        targets = targets.to(dev, non_blocking=True).to(torch.int64).contiguous()
+        self.model.train()
+        logits = self.model(images.to(dev, non_blocking=True))
+        n, C = logits.shape
+        stats = torch.zeros(1, dtype=torch.float32, device=dev)
+        dl = torch.empty_like(logits)
+        call("es_ce_weighted_fwd_bwd", ptr(logits.detach()), C, ptr(targets), ptr(self.class_weights), n, C, 1.0,
+             ptr(dl), C, ptr(stats), _lib.stream())
+        self.optimizer.zero_grad()
+        torch.autograd.backward([logits], [dl])
+        join_wgrad_stream(dev)
+        gscale = dist.allreduce_sum_(self.model.flat_grad)
+        ema = self.ema_model
+        self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,
+                            ema_decay=float(ema.decay) if ema is not None else 0.0, grad_scale=gscale)
+        if ema is not None:
+            ema.update_buffers(self.model)
+            ema.ema.mark_updated()
+        return {"loss": stats[0], "logits": logits.detach()}
+
+    def train_one(self, epoch):
+        self.model.train()
+        summary_loss = AverageMeter()
+        num_steps = len(self.train_dl)
+        pending = []
+        for step, batch in enumerate(self.train_dl):
+            out = self.step(batch)
+            self.lr_scheduler.step_update(epoch * num_steps + step)
+            pending.append(out["loss"].detach().clone())
+        for v in pending:  # one host sync per epoch
+            summary_loss.update(v.item(), self.config.DATA.BATCH_SIZE)
+        return summary_loss
+
+    def evaluate_one(self, epoch=None, show_metric=False, show_report=False, show_cf_matrix=False):
+        """code/supervised.py:148-196: unweighted CE mean, prediction = argmax softmax(logits)."""
+        eval_model = self.ema_model.ema if self.config.TRAIN.USE_EMA else self.model
+        eval_model.eval()
+        summary_loss = AverageMeter()
+        outs, tgts = [], []
+        dev = self.model.flat.device
+        with torch.no_grad():
+            for images, targets in self.valid_dl:
+                logits = eval_model(images.to(dev))
+                targets = targets.to(dev).to(torch.int64).contiguous()
+                st = torch.zeros(1, device=dev)
+                scratch = torch.empty_like(logits)
+                call("es_ce_weighted_fwd_bwd", ptr(logits), logits.shape[1], ptr(targets), None, logits.shape[0],
+                     logits.shape[1], 1.0, ptr(scratch), logits.shape[1], ptr(st), _lib.stream())
+                summary_loss.update(st.item(), self.config.DATA.BATCH_SIZE)
+                outs.append(logits.argmax(1).cpu().numpy())
+                tgts.append(targets.cpu().numpy())
+        pred, tgt = np.concatenate(outs), np.concatenate(tgts)
+        metric = calculate_metrics(pred, tgt, self.config)
+        if show_metric:
+            print('Metric:')
+            print(metric)
+        if show_report:
+            from sklearn.metrics import classification_report
+            print(classification_report(tgt, pred))
+        return summary_loss, metric
+
+    def save_checkpoint(self, foldname):
+        """Same dict keys and filename scheme as code/supervised.py:271-293."""
+        checkpoint = {}
+        if self.config.TRAIN.USE_EMA:
+            checkpoint['ema_state_dict'] = self.ema_model.ema.state_dict()
+        d = date.today().strftime("%m_%d_%Y")
+        h = datetime.now().strftime("%H_%M_%S").split('_')
+        h[0] = str(int(h[0]) + 2)
+        filename = d + '_' + '_'.join(h) + '_epoch_' + str(self.epoch)
+        checkpoint['epoch'] = self.epoch
+        checkpoint['best_valid_loss'] = self.best_valid_loss
+        checkpoint['best_valid_score'] = self.best_valid_score
+        checkpoint['model_state_dict'] = self.model.state_dict()
+        checkpoint['optimizer'] = self.optimizer.state_dict()
+        checkpoint['scheduler'] = self.lr_scheduler.state_dict()
+        f = os.path.join(foldname, filename + '.pth')
+        torch.save(checkpoint, f)
+        return f
+
+    def load_checkpoint(self, checkpoint_dir, is_train=False):
+        checkpoint = torch.load(checkpoint_dir, map_location='cpu', weights_only=True)
+        self.model.load_state_dict(checkpoint['model_state_dict'])
+        for p in self.model.parameters():
+            p.requires_grad = bool(is_train)
+        if self.config.TRAIN.USE_EMA:
+            self.ema_model.ema.load_state_dict(checkpoint['ema_state_dict'])
+        self.epoch_start = checkpoint['epoch']
+        self.optimizer.load_state_dict(checkpoint['optimizer'])
+        self.lr_scheduler.load_state_dict(checkpoint['scheduler'])
+
+    def fit(self):
+        count_early_stop = 0
+        for epoch in range(self.epoch_start, self.config.TRAIN.EPOCHS):
+            if count_early_stop > 5:
+                print('Early stopping')
+                break
+            self.epoch = epoch
+            train_loss = self.train_one(self.epoch)
+            print(f'\tTrain Loss: {train_loss.avg:.3f}')
+            if epoch % self.config.TRAIN.FREQ_EVAL == 0 and self.valid_dl is not None:
+                valid_loss, valid_metric = self.evaluate_one(self.epoch)
+                f1 = float(valid_metric['macro/f1'])
+                # code/supervised.py:344-358: save on a better loss AND score, count the epochs that
+                # are worse in either (never reset, as in the reference)
+                if self.best_valid_loss and self.best_valid_score:
+                    if self.best_valid_loss > valid_loss.avg and self.best_valid_score < f1:
+                        self.best_valid_loss, self.best_valid_score = valid_loss.avg, f1
+                        if dist.rank() == 0:
+                            self.save_checkpoint(self.config.TRAIN.SAVE_CP)
+                    elif self.best_valid_loss < valid_loss.avg or self.best_valid_score > f1:
+                        count_early_stop += 1
+                else:
+                    self.best_valid_loss, self.best_valid_score = valid_loss.avg, f1
+                    if dist.rank() == 0:
+                        self.save_checkpoint(self.config.TRAIN.SAVE_CP)
+                print(f'\tValid Loss: {valid_loss.avg:.3f}')
+                print(f'\tMetric: {valid_metric}')
