@@ -286,13 +286,20 @@ def run_secondary(args):
         desc = (f"S1: SemiFormer step on {name}, {S}^2 ({ccfg.T} tokens), B={B} + 2 x mu*B={B * MU} per GPU, C=23, "
                 f"tau=0.95, lambda_u=1, EMA 0.999; transformer GEMMs and convs with channels % 32 == 0 on bf16 "
                 f"MFMA ({'on' if model.conv_bf16 else 'off: ENDOSSL_CONV_BF16=0'}), BatchNorm / maps fp32")
+    steplog = os.environ.get("ENDOSSL_BENCH_STEPLOG") == "1"  # diagnostics: synchronises every step
     for _ in range(args.warmup):
         tr.step(batch)
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         out = tr.step(batch)
+        if steplog:
+            torch.cuda.synchronize()
+            print(f"step {i}: {1e3 * (time.perf_counter() - t0):.1f} ms cumulative, allocated "
+                  f"{torch.cuda.memory_allocated(dev) / 2**30:.1f} GiB, reserved "
+                  f"{torch.cuda.memory_reserved(dev) / 2**30:.1f} GiB, retries "
+                  f"{torch.cuda.memory_stats(dev).get('num_alloc_retries', 0)}", file=sys.stderr, flush=True)
     torch.cuda.synchronize()
     dist.barrier()
     T = time.perf_counter() - t0
@@ -312,6 +319,12 @@ def run_secondary(args):
             "data": "synthetic (HBM-resident, seed 0)", "config": {"workload": desc, "parallelism": f"dp{world}"},
             "step_tflop": round(tfl, 3), "executed_step_tflop": round(exe, 3),
             "step_tflops": round(tfl / (ms / 1e3), 1),
+            # caching-allocator retries (a full cache flush + re-allocation each) slow a step by
+            # orders of magnitude when HBM runs short: reported so such a run reads as one
+            "hbm_peak_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 1),
+            "alloc_retries": int(torch.cuda.memory_stats(dev).get("num_alloc_retries", 0)),
+            "device_allocs": int(torch.cuda.memory_stats(dev).get("num_device_alloc", 0)),
+            "hbm_reserved_peak_gib": round(torch.cuda.max_memory_reserved(dev) / 2**30, 1),
             "final_loss": round(out["loss"].item(), 6)}), flush=True)
     dist.barrier()
 

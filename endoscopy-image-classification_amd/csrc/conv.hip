@@ -1063,6 +1063,58 @@ __global__ void bn_finalize_global_kernel(const float* __restrict__ sum_g, const
   run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
   run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
 }
+// Batch statistics from per-block partials P[b][0][c] = block sum, P[b][1][c] = block M2 over blocks of
+// `bsz` rows (the last one rows - (nblk-1) bsz), block b at P + b stride 2C: mean = sum / n, M2 =
+// sum_b M2_b + n_b (mean_b - mean)^2 (Chan et al.).  64 channels x 4 block lanes per workgroup, lanes
+// combined in a fixed order.  !FINAL: workgroup y combines blocks [y G, y G + G) and writes the group's
+// (sum, M2) over its first block's slot (read only by this workgroup, before its last barrier) -- the
+// first of two levels, so no thread walks more than ~G / 4 blocks at any pixel count.
+template <bool FINAL>
+__global__ __launch_bounds__(256) void bn_stats_from_partials_kernel(float* __restrict__ P, int nblk, int bsz,
+                                                                     int stride, int G, int rows, int C, float eps,
+                                                                     float momentum, float* __restrict__ mean,
+                                                                     float* __restrict__ rstd,
+                                                                     float* __restrict__ run_mean,
+                                                                     float* __restrict__ run_var) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, bl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const bool ok = c < C;
+  const int b0 = blockIdx.y * G, b1 = min(nblk, b0 + G);
+  const long bs = (long)stride * 2 * C;
+  const int rows_y = min(rows - b0 * bsz, (b1 - b0) * bsz);
+  float s = 0.f;
+  if (ok)
+    for (int b = b0 + bl; b < b1; b += 4) s += P[b * bs + c];
+  red[bl][cl] = s;
+  __syncthreads();
+  const float sum = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+  const float mu = sum / (float)rows_y;
+  __syncthreads();
+  float m2 = 0.f;
+  if (ok)
+    for (int b = b0 + bl; b < b1; b += 4) {
+      const float nb = (float)(b + 1 < nblk ? bsz : rows - (nblk - 1) * bsz);
+      const float d = P[b * bs + c] / nb - mu;
+      m2 += P[b * bs + C + c] + nb * d * d;
+    }
+  red[bl][cl] = m2;
+  __syncthreads();
+  if (bl != 0 || !ok) return;
+  const float M2 = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+  if constexpr (!FINAL) {
+    P[b0 * bs + c] = sum;
+    P[b0 * bs + C + c] = M2;
+  } else {
+    const float var = M2 / (float)rows;
+    mean[c] = mu;
+    rstd[c] = 1.0f / sqrtf(var + eps);
+    const float unb = rows > 1 ? M2 / (float)(rows - 1) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+}
+
 // dbeta (+)= local sum g, dgamma (+)= local sum g xhat (sums_local = [sum g | sum g xhat])
 __global__ void bn_param_grads_kernel(const float* __restrict__ sums_local, int C, float* __restrict__ dgamma,
                                       float* __restrict__ dbeta, int accumulate) {
@@ -1310,6 +1362,41 @@ int es_bn2d_fwd_global(const float* x, int rows, int C, const float* gamma, cons
   if (n >= (1L << 31)) return ES_BAD_SHAPE;
   hipLaunchKernelGGL(bn_finalize_global_kernel, (C + 255) / 256, 256, 0, stream, sum_g, sq_g, (float)rows_g, C, eps,
                      momentum, mean, rstd, running_mean, running_var);
+  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+  const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) && al16(mean) &&
+                  al16(rstd);
+  if (v4)
+    hipLaunchKernelGGL(bn_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mean, rstd, nullptr,
+                       eps, gamma, beta, res, relu, y);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<1>, grid1d(n), 256, 0, stream, x, (int)n, C, mean, rstd, nullptr, eps, gamma,
+                       beta, res, relu, y);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// Train-mode BatchNorm2d whose batch statistics come from the producing conv's per-block partials
+// (es_conv2d_fwd_bf16_bnstats: blocks of 128 rows): no statistics pass over x.  Running stats,
+// num_batches_tracked, mean / rstd and y = bn(x) (+ res) (relu) as es_bn2d_fwd.
+int es_bn2d_fwd_partials(const float* x, int rows, int C, float* partials, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var, void* num_batches_tracked,
+                         float momentum, float eps, const float* res, int relu, float* y, float* mean, float* rstd,
+                         hipStream_t stream) {
+  if (!x || !partials || !gamma || !beta || !running_mean || !running_var || !y || !mean || !rstd) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  const int nblk = (rows + 127) / 128, G = 64;
+  float* P = (float*)partials;  // level 1 overwrites group-leading slots in place
+  if (nblk > G) {
+    const int ng = (nblk + G - 1) / G;
+    hipLaunchKernelGGL(bn_stats_from_partials_kernel<false>, dim3((C + 63) / 64, ng), 256, 0, stream, P, nblk, 128, 1,
+                       G, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+    hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, ng, 128 * G, G,
+                       ng, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+  } else {
+    hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, nblk, 128, 1,
+                       nblk, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+  }
   if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
   const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) && al16(mean) &&
                   al16(rstd);

@@ -50,6 +50,7 @@ struct NTConv {
   int Ho, Wo;  // output map dims: forward y (Ho, Wo); data grad x (H, W)
   long osn, osh, osw;
   int accumulate;
+  float* stats;  // forward only, nullable: per 128-pixel block [sum | M2] of every output channel
 };
 
 constexpr int NT_BM = 128, NT_BK = 32;
@@ -59,8 +60,8 @@ constexpr int NT_BM = 128, NT_BK = 32;
 // DX = true:  blockIdx.z = stride phase (py, px); pixels (n, hq, wq) -> x pixel (hq s + py, wq s + px);
 //             taps ky = ky0 + s kyq (the only ones that reach this phase); source dy pixel
 //             (hq + qh - kyq, wq + qw - kxq) (conv.hip conv_dx_kernel's decomposition).
-template <int BN, bool DX>
-__global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
+template <int BN, bool DX, bool STATS = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void convb_nt_kernel(NTConv a) {
   constexpr int NF = BN / 32;       // 16-col fragments per wave (wave covers BN / 2 cols)
   constexpr int BJ = BN / 64;       // 16-byte weight loads per thread per step
   constexpr int ABYTES = NT_BM * 64, BBYTES = BN * 64, STAGE = ABYTES + BBYTES;
@@ -178,6 +179,60 @@ __global__ __launch_bounds__(256) void convb_nt_kernel(NTConv a) {
 #pragma unroll
       for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
     if (kt + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // BatchNorm statistics of this tile (forward, STATS: a separate instantiation, so the plain
+  // forward keeps its registers): per output channel the block's sum and its
+  // centred sum of squares M2 over the valid pixels of the 128-pixel block (Chan's parallel form;
+  // es_bn2d_fwd_partials combines the blocks).  Lane (g, r) holds rows wm 64 + 16 i + r of the 4
+  // channels wn BN/2 + 16 j + 4 g + q: sums over i in-lane, over r by xor shuffles within each
+  // 16-lane group, over the two row waves (wm) through LDS.
+  if constexpr (STATS && !DX) {
+    // the bias shifts a channel's values uniformly: M2 is computed on the accumulators alone and the
+    // sum gets nb bias[col] added once (no per-lane bias registers: the plain instantiation's occupancy)
+    float* red = (float*)smem;  // [2 (wm)][BN] partial sums, then [2][BN] partial M2
+    const int nb = min(NT_BM, M - m0);
+    bool rv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rv[i] = m0 + wm * 64 + i * 16 + r < M;
+    float mu[NF][4];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float t = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = pass == 0 ? acc[i][j][q] : acc[i][j][q] - mu[j][q];
+            t += rv[i] ? (pass == 0 ? d : d * d) : 0.f;
+          }
+          t += __shfl_xor(t, 1, 64);
+          t += __shfl_xor(t, 2, 64);
+          t += __shfl_xor(t, 4, 64);
+          t += __shfl_xor(t, 8, 64);
+          if (r == 0) red[wm * BN + wn * (BN / 2) + j * 16 + 4 * g + q] = t;
+        }
+      __syncthreads();
+      const bool wr = tid < BN && n0 + tid < a.Ncol;
+      if (pass == 0) {
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cl = wn * (BN / 2) + j * 16 + 4 * g + q;
+            mu[j][q] = (red[cl] + red[BN + cl]) / (float)nb;
+          }
+        if (wr)
+          a.stats[(long)blockIdx.x * 2 * a.Ncol + n0 + tid] =
+              red[tid] + red[BN + tid] + (a.bias ? (float)nb * a.bias[n0 + tid] : 0.f);
+        __syncthreads();
+      } else if (wr) {
+        a.stats[(long)blockIdx.x * 2 * a.Ncol + a.Ncol + n0 + tid] = red[tid] + red[BN + tid];
+      }
+    }
     __syncthreads();
   }
 
@@ -464,9 +519,10 @@ int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void*
 // y[n, ho, wo, co] (+)= bias[co] + conv(x) with wp = es_conv2d_pack_bf16's forward image.  Same
 // geometry arguments as es_conv2d_fwd; requires es_conv2d_bf16_eligible, sxc == 1, 16-byte aligned
 // pixel rows (strides % 4 == 0) and pointers.
-int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
-                       const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
-                       long syn, long syh, long syw, int accumulate, hipStream_t stream) {
+static int conv_fwd_bf16_impl(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                              const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
+                              float* y, long syn, long syh, long syw, int accumulate, float* bn_partials,
+                              hipStream_t stream) {
   if (!x || !wp || !y) return ES_BAD_ARG;
   if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
     return ES_BAD_SHAPE;
@@ -475,13 +531,45 @@ int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, l
       (bias && !al16(bias)))
     return ES_BAD_SHAPE;
   NTConv a{x, (const bf16*)wp, bias, y, N, Cin, Cout, H, W, sxn, sxh, sxw, kh, kw, stride, pad, Ho, Wo, syn, syh, syw,
-           accumulate};
+           accumulate, bn_partials};
+  if (bn_partials && accumulate) return ES_BAD_ARG;
   const int M = N * Ho * Wo;
-  if (Cout % 128 == 0)
-    hipLaunchKernelGGL((convb_nt_kernel<128, false>), dim3((M + 127) / 128, Cout / 128), 256, 0, stream, a);
-  else
-    hipLaunchKernelGGL((convb_nt_kernel<64, false>), dim3((M + 127) / 128, (Cout + 63) / 64), 256, 0, stream, a);
+  const dim3 g128((M + 127) / 128, Cout / 128), g64((M + 127) / 128, (Cout + 63) / 64);
+  if (Cout % 128 == 0) {
+    if (bn_partials)
+      hipLaunchKernelGGL((convb_nt_kernel<128, false, true>), g128, 256, 0, stream, a);
+    else
+      hipLaunchKernelGGL((convb_nt_kernel<128, false>), g128, 256, 0, stream, a);
+  } else {
+    if (bn_partials)
+      hipLaunchKernelGGL((convb_nt_kernel<64, false, true>), g64, 256, 0, stream, a);
+    else
+      hipLaunchKernelGGL((convb_nt_kernel<64, false>), g64, 256, 0, stream, a);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                       const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
+                       long syn, long syh, long syw, int accumulate, hipStream_t stream) {
+  return conv_fwd_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh, syw,
+                            accumulate, nullptr, stream);
+}
+
+// floats of es_conv2d_fwd_bf16_bnstats' partials for M = N Ho Wo output pixels
+size_t es_conv2d_bnstats_size(int M, int Cout) {
+  return M > 0 && Cout > 0 ? (size_t)((M + NT_BM - 1) / NT_BM) * 2 * Cout : 0;
+}
+
+// es_conv2d_fwd_bf16 (accumulate 0) that also writes the BatchNorm statistics of y: per 128-pixel
+// block b, partials[b][0][c] = sum of y[., c] and partials[b][1][c] = sum of (y - block mean)^2 over
+// the block's pixels -- es_bn2d_fwd_partials turns them into the batch statistics without re-reading y.
+int es_conv2d_fwd_bf16_bnstats(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                               const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
+                               float* y, long syn, long syh, long syw, float* partials, hipStream_t stream) {
+  if (!partials) return ES_BAD_ARG;
+  return conv_fwd_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh, syw,
+                            0, partials, stream);
 }
 
 // dx[n, h, w, ci] (+)= conv^T(dy) with wt = es_conv2d_pack_bf16's transposed image.  Same geometry
@@ -497,7 +585,7 @@ int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const
       !al16(wt))
     return ES_BAD_SHAPE;
   NTConv a{dy, (const bf16*)wt, nullptr, dx, N, Cout, Cin, Ho, Wo, syn, syh, syw, kh, kw, stride, pad, H, W, sxn, sxh,
-           sxw, accumulate};
+           sxw, accumulate, nullptr};
   const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
   const unsigned ph = (unsigned)(stride * stride);
   if (Cin % 128 == 0)

@@ -84,6 +84,9 @@ SIGNATURES = {
     "es_conv2d_pack_bf16": (I, [V, I, I, I, I, V, V, V]),
     "es_conv2d_fwd_bf16": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, I, V]),
     "es_conv2d_bwd_data_bf16": (I, [V, L, L, L, V, I, I, I, I, I, I, I, I, I, V, L, L, L, L, I, V]),
+    "es_conv2d_bnstats_size": (Z, [I, I]),
+    "es_conv2d_fwd_bf16_bnstats": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, V, V]),
+    "es_bn2d_fwd_partials": (I, [V, I, I, V, V, V, V, V, V, F, F, V, I, V, V, V, V]),
     "es_conv2d_bwd_weight_bf16_workspace": (Z, [I, I, I, I, I, I]),
     "es_conv2d_bwd_weight_bf16": (I, [V, I, I, I, I, L, L, L, L, V, L, L, L, I, I, I, I, I, I, V, V, I, V]),
     "es_chan_workspace": (Z, [I, I]),

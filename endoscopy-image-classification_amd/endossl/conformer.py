@@ -224,6 +224,36 @@ def join_wgrad_stream(device=None):
         torch.cuda.current_stream(dev).wait_stream(st)
 
 
+# How many steps the host may queue ahead of the GPU.  The conv weight-gradient side stream and the
+# branch streams record_stream() their operands, so the caching allocator can recycle a step's
+# activations only once the GPU has passed that step's events: a host queueing step i+1 while the
+# GPU still runs step i's backward allocates step i+1's maps fresh, and at Conformer-B/384 sizes
+# (~85 GB allocated per step) the reserved pool then reaches the whole HBM, where each allocation
+# retry flushes the cache and stalls (S1 measured 5x slower).  1 = the next step starts its host
+# work once the previous step's last kernel (the Adam + EMA sweep) has finished; 0 = unbounded.
+MAX_INFLIGHT_STEPS = int(os.environ.get("ENDOSSL_MAX_INFLIGHT_STEPS", "1"))
+
+
+class StepThrottle:
+    """Bounds a trainer's queued steps to MAX_INFLIGHT_STEPS (record() after a step's last launch,
+    wait() before the next step's first)."""
+
+    def __init__(self, depth=None):
+        self.depth = MAX_INFLIGHT_STEPS if depth is None else depth
+        self.events = []
+
+    def record(self):
+        if self.depth <= 0 or not torch.cuda.is_available():
+            return
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream())
+        self.events.append(ev)
+
+    def wait(self):
+        while self.depth > 0 and len(self.events) >= self.depth:
+            self.events.pop(0).synchronize()
+
+
 def _zero_pad(t, rows):
     """Zero rows [rows, len) of a token-row buffer (the GEMM pad rows) and return it."""
     if t.shape[0] > rows:
@@ -259,6 +289,9 @@ def _tn_splits(M, N1, N2):
 # accumulation) wherever both channel counts are multiples of 32; ENDOSSL_CONV_BF16=0 (or
 # NativeConformer.set_conv_precision("fp32")) keeps every conv on conv.hip's fp32 MFMA kernels.
 CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
+# train-mode BatchNorm statistics of a bf16 conv's output computed in the conv's epilogue
+# (es_conv2d_fwd_bf16_bnstats -> es_bn2d_fwd_partials): no two statistics passes over the map
+BN_STATS_FUSED = os.environ.get("ENDOSSL_BN_STATS_FUSED", "1") != "0"
 
 
 def _conv_bf16(m, xmap, Cout, k):
@@ -272,14 +305,21 @@ class _ConvFn(torch.autograd.Function):
     ConvBlock / FCU convs, Conformer.conv1)."""
 
     @staticmethod
-    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None):
+    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None, stats=False):
         Ho, Wo = (xmap.H + 2 * p - k) // s + 1, (xmap.W + 2 * p - k) // s + 1
         y = torch.empty(xmap.N, Ho, Wo, Cout, dtype=torch.float32, device=x.device)
         b16 = _conv_bf16(m, xmap, Cout, k)
         args = (xmap.p(), xmap.N, xmap.H, xmap.W, xmap.C, xmap.sn, xmap.sh, xmap.sw, xmap.sc)
         tail = (ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout, Wo * Cout, Cout, 0,
                 _s())
-        if b16:
+        if b16 and stats and m.training and BN_STATS_FUSED:
+            # the BatchNorm that follows takes its batch statistics from these per-block partials
+            lib = _lib.load()
+            part = torch.empty(lib.es_conv2d_bnstats_size(xmap.N * Ho * Wo, Cout), device=x.device)
+            call("es_conv2d_fwd_bf16_bnstats", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail[:-2],
+                 ptr(part), _s())
+            m._bn_partials[y.data_ptr()] = (part, y.shape)
+        elif b16:
             call("es_conv2d_fwd_bf16", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail)
         else:
             call("es_conv2d_fwd", *args, ptr(m.pview(wname)), *tail)
@@ -327,7 +367,7 @@ class _ConvFn(torch.autograd.Function):
             call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
                  ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, 0,
                  _s())
-        return dx, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None
 
 
 class _nullctx:
@@ -338,8 +378,10 @@ class _nullctx:
         return False
 
 
-def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None):
-    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor)
+def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None, stats=False):
+    """stats=True: the output feeds a train-mode BatchNorm, which then takes its batch statistics
+    from the conv's epilogue (BN_STATS_FUSED)."""
+    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor, stats)
 
 
 class _BNFn(torch.autograd.Function):
@@ -359,7 +401,12 @@ class _BNFn(torch.autograd.Function):
         rm, rv, nbt = m.bn_buffers(pre)
         res_c = res.contiguous() if res is not None else None  # keep temporaries alive across the launch
         world = dist.world_size() if train and getattr(m, "sync_bn", True) else 1
-        if world > 1:
+        part = m._bn_partials.pop(x.data_ptr(), None) if train and world == 1 else None
+        if part is not None and part[1] == x.shape:
+            call("es_bn2d_fwd_partials", ptr(x), rows, C, ptr(part[0]), ptr(m.pview(pre + "weight")),
+                 ptr(m.pview(pre + "bias")), ptr(rm), ptr(rv), ptr(nbt), BN_MOMENTUM, eps, ptr(res_c),
+                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), _s())
+        elif world > 1:
             # SyncBatchNorm over every rank's rows (the single-process statistics)
             rows_g = rows * world
             sums = torch.empty(2, C, device=x.device)
@@ -834,6 +881,7 @@ class NativeConformer(nn.Module):
         self._packed_version = -1
         self._wtab = None
         self._cpack = {}
+        self._bn_partials = {}
         self._anchor = torch.zeros((), device=device, requires_grad=True)
 
     def _apply(self, fn, recurse=True):
@@ -917,19 +965,20 @@ class NativeConformer(nn.Module):
     def _conv_block_head(self, pre, x, stride, x_t=None):
         """conv1 -> bn1 -> ReLU (-> + upsampled x_t) -> conv2 -> bn2 -> ReLU: x2 (:118-130)."""
         med = self.shapes[pre + "conv1.weight"][0]
-        h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1), pre + "bn1.", relu=True)
+        h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1, stats=True), pre + "bn1.",
+               relu=True)
         if x_t is not None:
             h = _UpsampleAddFn.apply(h, x_t, h.shape[1] // x_t.shape[1])
-        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1)
+        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1, stats=True)
         return bn(self, h, pre + "bn2.", relu=True)
 
     def _conv_block_tail(self, pre, x, x2, stride, res_conv):
         """conv3 -> bn3 (+ residual, via residual_conv / residual_bn) -> ReLU (:132-144)."""
         outp = self.shapes[pre + "conv3.weight"][0]
-        h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1)
+        h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1, stats=True)
         residual = x
         if res_conv:
-            r = conv(self, x, _Map.nhwc(x), pre + "residual_conv.weight", None, outp, 1, stride)
+            r = conv(self, x, _Map.nhwc(x), pre + "residual_conv.weight", None, outp, 1, stride, stats=True)
             residual = bn(self, r, pre + "residual_bn.")
         return bn(self, h, pre + "bn3.", relu=True, res=residual)
 
@@ -946,6 +995,7 @@ class NativeConformer(nn.Module):
         # a backward that raised after queueing its stream join never ran the callback that clears
         # its key: every new graph starts with no join pending
         _join_queued.clear()
+        self._bn_partials.clear()
         x = x.float().contiguous()
         n, S = x.shape[0], cfg.img_size
         self.cur_n = n
@@ -1018,6 +1068,6 @@ class NativeConformer(nn.Module):
         # the nearest upsampling is fused into the fusion block's conv2 input
         tok = _Map(xt, n, g, g, D, sn=T * D, sh=g * D, sw=D, sc=1, off=D)
         up = conv(self, xt, tok, pre + "expand_block.conv_project.weight", pre + "expand_block.conv_project.bias",
-                  med, 1)
+                  med, 1, stats=True)
         up = bn(self, up, pre + "expand_block.bn.", relu=True)
         return xt, up

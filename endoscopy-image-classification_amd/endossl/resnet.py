@@ -113,11 +113,11 @@ class NativeResNet(NativeConformer):
 
     def _block(self, x, pre, inp, planes, stride, ds):
         """timm BasicBlock.forward: relu(bn2(conv2(relu(bn1(conv1(x))))) + shortcut)."""
-        h = conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, planes, 3, stride, 1)
+        h = conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, planes, 3, stride, 1, stats=True)
         h = bn(self, h, pre + "bn1.", eps=BN_EPS, relu=True)
-        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, planes, 3, 1, 1)
+        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, planes, 3, 1, 1, stats=True)
         if ds:
-            sc = conv(self, x, _Map.nhwc(x), pre + "downsample.0.weight", None, planes, 1, stride, 0)
+            sc = conv(self, x, _Map.nhwc(x), pre + "downsample.0.weight", None, planes, 1, stride, 0, stats=True)
             sc = bn(self, sc, pre + "downsample.1.", eps=BN_EPS)
         else:
             sc = x
@@ -130,6 +130,7 @@ class NativeResNet(NativeConformer):
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected [n, 3, H, W] images, got {tuple(x.shape)}")
         _join_queued.clear()
+        self._bn_partials.clear()
         n, H, W = x.shape[0], x.shape[2], x.shape[3]
         self.cur_n = n
         x = x.float().permute(0, 2, 3, 1).contiguous()  # NHWC once (the stem's 3-channel gathers)

@@ -20,7 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib, dist
-from .conformer import join_wgrad_stream
+from .conformer import StepThrottle, join_wgrad_stream
 from ._lib import call, ptr
 from .ema import ModelEMA
 from .fixmatch import _next
@@ -37,6 +37,7 @@ class SemiFormer:
         self.model.to(self.device)
         self.epoch_start = 0
         self.best_valid_perf = None
+        self._inflight = StepThrottle()
 
     def get_dataloader(self, train_dl, valid_dl, test_dl=None):
         self.train_labeled_dl, self.train_unlabeled_dl = train_dl
@@ -87,11 +88,13 @@ class SemiFormer:
         if ema is not None:
             ema.update_buffers(self.model)
             ema.ema.mark_updated()
+        self._inflight.record()
 
     def step(self, batch):
         """batch = ((x, y), ((u_w, u_s), idx)) -> dict of device scalars / tensors."""
         (inputs_x, targets_x), ((inputs_u_w, inputs_u_s), _) = batch
         dev = self.model.flat.device
+        self._inflight.wait()
         bs, nu = int(inputs_x.shape[0]), int(inputs_u_w.shape[0])
         targets_x = targets_x.to(dev, non_blocking=True).to(torch.int64).contiguous()
         inputs = torch.cat((inputs_x.to(dev), inputs_u_w.to(dev), inputs_u_s.to(dev)))
@@ -124,6 +127,7 @@ class SemiFormer:
         """Supervised warm-up step (code/semiformer.py:75-101): CE on both heads."""
         images, targets = batch
         dev = self.model.flat.device
+        self._inflight.wait()
         targets = targets.to(dev).to(torch.int64).contiguous()
         self.model.train()
         out_conv, out_trans = self.model(images.to(dev))

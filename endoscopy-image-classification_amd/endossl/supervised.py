@@ -22,7 +22,7 @@ import torch
 
 from . import _lib, dist
 from ._lib import call, ptr
-from .conformer import join_wgrad_stream
+from .conformer import StepThrottle, join_wgrad_stream
 from .ema import ModelEMA
 from .lr_scheduler import build_scheduler
 from .optimizer import build_optimizer
@@ -39,6 +39,7 @@ class SupLearning:
         self.best_valid_loss = None
         self.best_valid_score = None
         self.wandb = wandb
+        self._inflight = StepThrottle()
 
     def get_dataloader(self, train_dl, valid_dl, mixup_fn=None, test_dl=None):
         self.train_dl = train_dl
@@ -71,6 +72,7 @@ class SupLearning:
         """batch = (images [n, 3, H, W], targets [n]) -> {"loss", "logits"} (device tensors)."""
         images, targets = batch
         dev = self.model.flat.device
+        self._inflight.wait()
         targets = targets.to(dev, non_blocking=True).to(torch.int64).contiguous()
         self.model.train()
         logits = self.model(images.to(dev, non_blocking=True))
@@ -89,6 +91,7 @@ class SupLearning:
         if ema is not None:
             ema.update_buffers(self.model)
             ema.ema.mark_updated()
+        self._inflight.record()
         return {"loss": stats[0], "logits": logits.detach()}
 
     def train_one(self, epoch):

@@ -281,6 +281,13 @@ int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, l
 int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
                             int Cin, int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh,
                             long sxw, long sxc, int accumulate, hipStream_t stream);
+/* es_conv2d_fwd_bf16 (overwrite) that also writes y's BatchNorm statistics per 128-pixel block:
+ * partials[b][0][c] = block sum, partials[b][1][c] = block-centred sum of squares
+ * (es_conv2d_bnstats_size floats) -- es_bn2d_fwd_partials needs no statistics pass over y. */
+size_t es_conv2d_bnstats_size(int M, int Cout);
+int es_conv2d_fwd_bf16_bnstats(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                               const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
+                               float* y, long syn, long syh, long syw, float* partials, hipStream_t stream);
 /* workspace floats for M = N Ho Wo output pixels; splits <= 0 sizes the pixel split automatically */
 size_t es_conv2d_bwd_weight_bf16_workspace(int M, int Cout, int Cin, int kh, int kw, int splits);
 int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
@@ -298,6 +305,14 @@ int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float
 int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
                 const float* mean, const float* rstd, int train, const float* running_var, float eps, float* dx,
                 float* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t stream);
+/* Train-mode BatchNorm2d with the batch statistics from es_conv2d_fwd_bf16_bnstats' partials of x
+ * (128-row blocks, combined as Chan et al. in two levels of 64 blocks; the first level overwrites
+ * partials in place): running stats, num_batches_tracked, mean / rstd and y = bn(x) (+ res) (relu)
+ * as es_bn2d_fwd. */
+int es_bn2d_fwd_partials(const float* x, int rows, int C, float* partials, const float* gamma,
+                         const float* beta, float* running_mean, float* running_var, void* num_batches_tracked,
+                         float momentum, float eps, const float* res, int relu, float* y, float* mean, float* rstd,
+                         hipStream_t stream);
 /* SyncBatchNorm2d: the Conformer's BatchNorm2d over the global batch at N > 1 (SURVEY.md §8(e):
  * exact parity with the single-process step needs the statistics of every rank's rows).  Flow per
  *  BatchNorm: es_bn2d_sums [mode 0] -> all-reduce -> es_bn2d_sums [mode 1: centred on the global mean]

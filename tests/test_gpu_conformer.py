@@ -155,6 +155,58 @@ def test_conv2d_bf16_fwd_bwd(N, Cin, H, Cout, k, s, p):
         _close(dwd.cpu() - 2.0, wr.grad, atol=2e-5)
 
 
+@pytest.mark.parametrize("N,Cin,H,Cout,k,s,p", [(3, 64, 15, 64, 3, 1, 1), (2, 32, 20, 128, 1, 2, 0),
+                                                (2, 64, 9, 256, 3, 1, 1), (5, 32, 45, 64, 1, 1, 0)])
+def test_conv_bf16_fused_bn_statistics(N, Cin, H, Cout, k, s, p):
+    """es_conv2d_fwd_bf16_bnstats (per-128-pixel-block sum / centred M2 in the conv epilogue) +
+    es_bn2d_fwd_partials (Chan combination) give es_bn2d_fwd's statistics of the same conv output:
+    the same y (bit-identical conv), mean / rstd / running stats within fp32 summation order, the
+    normalised output too; pixel counts that are not multiples of 128 (a partial last block), and
+    10,125 pixels = 80 blocks (the two-level combine with a partial last group)."""
+    lib = _lib.load()
+    torch.manual_seed(N + Cin + Cout)
+    x = _nhwc(torch.randn(N, Cin, H, H)).to(DEV)
+    w = (torch.randn(Cout, Cin, k, k) * 0.2).to(DEV)
+    b = torch.randn(Cout).to(DEV) * 3.0  # a bias shifts the mean: the centring must follow it
+    Ho = (H + 2 * p - k) // s + 1
+    M = N * Ho * Ho
+    wp = torch.empty(Cout * Cin * k * k, dtype=torch.bfloat16, device=DEV)
+    call("es_conv2d_pack_bf16", ptr(w), Cout, Cin, k, k, ptr(wp), None, S())
+    y1, y2 = torch.empty(M, Cout, device=DEV), torch.empty(M, Cout, device=DEV)
+    geo = (H * H * Cin, H * Cin, Cin, 1)
+    call("es_conv2d_fwd_bf16", ptr(x), N, H, H, Cin, *geo, ptr(wp), ptr(b), Cout, k, k, s, p, ptr(y1),
+         Ho * Ho * Cout, Ho * Cout, Cout, 0, S())
+    part = torch.empty(lib.es_conv2d_bnstats_size(M, Cout), device=DEV)
+    call("es_conv2d_fwd_bf16_bnstats", ptr(x), N, H, H, Cin, *geo, ptr(wp), ptr(b), Cout, k, k, s, p, ptr(y2),
+         Ho * Ho * Cout, Ho * Cout, Cout, ptr(part), S())
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    gam, bet = dv(torch.rand(Cout) + 0.5), dv(torch.randn(Cout))
+    rm0, rv0 = torch.randn(Cout), torch.rand(Cout) + 0.5  # the same running stats entering both paths
+    outs = []
+    for fused in (False, True):
+        rm, rvv, nbt = dv(rm0.clone()), dv(rv0.clone()), torch.zeros((), dtype=torch.int64, device=DEV)
+        yo, mean, rstd = torch.empty_like(y1), torch.empty(Cout, device=DEV), torch.empty(Cout, device=DEV)
+        if fused:
+            call("es_bn2d_fwd_partials", ptr(y2), M, Cout, ptr(part), ptr(gam), ptr(bet), ptr(rm), ptr(rvv), ptr(nbt),
+                 0.1, 1e-6, None, 1, ptr(yo), ptr(mean), ptr(rstd), S())
+        else:
+            ws = torch.empty(lib.es_chan_workspace(M, Cout), device=DEV)
+            call("es_bn2d_fwd", ptr(y1), M, Cout, ptr(gam), ptr(bet), ptr(rm), ptr(rvv), ptr(nbt), 0.1, 1e-6, 1, None,
+                 1, ptr(yo), ptr(mean), ptr(rstd), ptr(ws), S())
+        torch.cuda.synchronize()
+        outs.append((yo.cpu(), mean.cpu(), rstd.cpu(), rm.cpu(), rvv.cpu(), int(nbt.item())))
+    ref = y1.double().cpu()
+    mu, var = ref.mean(0), ref.var(0, unbiased=False)
+    for i, (a, c) in enumerate(zip(outs[0], outs[1])):
+        if isinstance(a, int):
+            assert a == c == 1
+        else:
+            _close(c, a, atol=2e-5)
+    _close(outs[1][1], mu, atol=1e-5)
+    _close(outs[1][2], 1.0 / (var + 1e-6).sqrt(), atol=1e-4)
+
+
 def test_conv2d_bf16_token_rows():
     """bf16 convs over token-row views: a 4x4/4 patch conv written into rows 1.. of [N, T, D]
     (trans_patch_conv), and a 1x1 conv reading them back with its data gradient written into token
