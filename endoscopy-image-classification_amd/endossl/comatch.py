@@ -104,6 +104,7 @@ class CoMatch(FixMatch):
         drop_keep: optional uint8 [B + 3muB, D/4] Dropout keep-mask to replay (parity tests)."""
         (inputs_x, targets_x), ((u_w, u_s0, u_s1), _) = batch
         dev = self.model.flat.device
+        self._inflight.wait()
         inputs_x = inputs_x.to(dev, non_blocking=True)
         targets_x = targets_x.to(dev, non_blocking=True).to(torch.int64)
         u_w, u_s0, u_s1 = (t.to(dev, non_blocking=True) for t in (u_w, u_s0, u_s1))
@@ -187,6 +188,7 @@ class CoMatch(FixMatch):
         if ema is not None:
             ema.update_buffers(m)
             ema.ema.mark_updated()
+        self._inflight.record()
         return {"loss": stats[4], "lx": stats[0], "lu": stats[1], "lc": stats[2], "mask_mean": stats[3],
                 "pseudo_label": W["pl"], "mask": W["mask"], "probs": W["probs"], "probs_orig": W["probs_orig"],
                 "logits": logits, "fts": fts, "z": z}

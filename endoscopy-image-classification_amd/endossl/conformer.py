@@ -224,36 +224,6 @@ def join_wgrad_stream(device=None):
         torch.cuda.current_stream(dev).wait_stream(st)
 
 
-# How many steps the host may queue ahead of the GPU.  The conv weight-gradient side stream and the
-# branch streams record_stream() their operands, so the caching allocator can recycle a step's
-# activations only once the GPU has passed that step's events: a host queueing step i+1 while the
-# GPU still runs step i's backward allocates step i+1's maps fresh, and at Conformer-B/384 sizes
-# (~85 GB allocated per step) the reserved pool then reaches the whole HBM, where each allocation
-# retry flushes the cache and stalls (S1 measured 5x slower).  1 = the next step starts its host
-# work once the previous step's last kernel (the Adam + EMA sweep) has finished; 0 = unbounded.
-MAX_INFLIGHT_STEPS = int(os.environ.get("ENDOSSL_MAX_INFLIGHT_STEPS", "1"))
-
-
-class StepThrottle:
-    """Bounds a trainer's queued steps to MAX_INFLIGHT_STEPS (record() after a step's last launch,
-    wait() before the next step's first)."""
-
-    def __init__(self, depth=None):
-        self.depth = MAX_INFLIGHT_STEPS if depth is None else depth
-        self.events = []
-
-    def record(self):
-        if self.depth <= 0 or not torch.cuda.is_available():
-            return
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream())
-        self.events.append(ev)
-
-    def wait(self):
-        while self.depth > 0 and len(self.events) >= self.depth:
-            self.events.pop(0).synchronize()
-
-
 def _zero_pad(t, rows):
     """Zero rows [rows, len) of a token-row buffer (the GEMM pad rows) and return it."""
     if t.shape[0] > rows:

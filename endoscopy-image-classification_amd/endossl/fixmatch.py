@@ -32,6 +32,7 @@ from .ema import ModelEMA
 from .loss import ce_loss
 from .lr_scheduler import build_scheduler
 from .optimizer import build_optimizer
+from .throttle import StepThrottle
 from .utils import AverageMeter, balanced_class_weights, calculate_metrics
 
 
@@ -55,6 +56,7 @@ class FixMatch:
         self.best_valid_perf = None
         self._dlogits = None
         self._stats = None
+        self._inflight = StepThrottle(2)
 
     def get_dataloader(self, train_dl, valid_dl, test_dl=None):
         self.train_labeled_dl, self.train_unlabeled_dl = train_dl
@@ -172,6 +174,7 @@ class FixMatch:
         """batch = ((x, y), ((u_w, u_s), idx)) -> dict of device scalars / tensors."""
         (inputs_x, targets_x), ((inputs_u_w, inputs_u_s), _) = batch
         dev = self.model.flat.device
+        self._inflight.wait()
         inputs = (inputs_x.to(dev, non_blocking=True), targets_x.to(dev, non_blocking=True).to(torch.int64),
                   inputs_u_w.to(dev, non_blocking=True), inputs_u_s.to(dev, non_blocking=True))
         m = self.model
@@ -188,6 +191,7 @@ class FixMatch:
                             ema_decay=float(ema.decay) if ema is not None else 0.0, grad_scale=gscale)
         if ema is not None:
             ema.ema.mark_updated()
+        self._inflight.record()
         return {"loss": stats[3], "lx": stats[0], "lu": stats[1], "mask_mean": stats[2],
                 "pseudo_label": self._pl, "mask": self._mask}
 

@@ -20,12 +20,13 @@ import numpy as np
 import torch
 
 from . import _lib, dist
-from .conformer import StepThrottle, join_wgrad_stream
+from .conformer import join_wgrad_stream
 from ._lib import call, ptr
 from .ema import ModelEMA
 from .fixmatch import _next
 from .lr_scheduler import build_scheduler
 from .optimizer import build_optimizer
+from .throttle import StepThrottle
 from .utils import AverageMeter, balanced_class_weights, calculate_metrics
 
 

@@ -22,10 +22,11 @@ import torch
 
 from . import _lib, dist
 from ._lib import call, ptr
-from .conformer import StepThrottle, join_wgrad_stream
+from .conformer import join_wgrad_stream
 from .ema import ModelEMA
 from .lr_scheduler import build_scheduler
 from .optimizer import build_optimizer
+from .throttle import StepThrottle
 from .utils import AverageMeter, balanced_class_weights, calculate_metrics
 
 
