@@ -35,10 +35,19 @@ def main():
     ap.add_argument("--tn-blocks", default="512", help="target workgroup counts (split-K sizing) to sweep; "
                     "'auto' = the library's sizing, 's<N>' = N splits")
     ap.add_argument("--m-train", type=int, default=0, help="token rows of the TN shapes (default 512 x 197)")
+    ap.add_argument("--s1", action="store_true", help="the Conformer-B/384 transformer-branch shapes of S1 "
+                    "(D 768, hidden 3072, 120 images x 577 tokens)")
     args = ap.parse_args()
-    global TN
+    global TN, NT
+    if args.s1:
+        m, d, hd = 120 * 577, 768, 3072
+        NT = [("qkv_fwd", 0, m, 3 * d, d), ("proj_fwd", 2, m, d, d), ("fc1_fwd", 7, m, hd, d), ("fc2_fwd", 2, m, d, hd),
+              ("fc2_dgrad", 8, m, hd, d), ("fc1_dgrad", 0, m, d, hd), ("proj_dgrad", 0, m, d, d),
+              ("qkv_dgrad", 0, m, d, 3 * d)]
+        TN = [("fc2_wgrad", m, d, hd), ("fc1_wgrad", m, hd, d), ("proj_wgrad", m, d, d), ("qkv_wgrad", m, 3 * d, d)]
     if args.m_train:
         TN = [(n, args.m_train, a, b) for n, _, a, b in TN]
+    WX = max(max(n, k) for _, _, _, n, k in NT)  # widest operand / output row
     lib = _lib.load()
     lib.es_set_gemm_variant.restype = _lib.I
     lib.es_set_gemm_variant.argtypes = [_lib.I]
@@ -49,13 +58,13 @@ def main():
     dev = "cuda"
     torch.manual_seed(0)
     s = _lib.stream()
-    Mp = (M_T + 255) // 256 * 256
-    A = torch.randn(Mp, HD * 2, device=dev).bfloat16()
-    Bw = (torch.randn(HD * 2, HD * 2, device=dev) * 0.05).bfloat16()
-    bias = torch.randn(HD * 2, device=dev)
-    C = torch.empty(Mp, HD * 2, device=dev)  # big enough for f32 [M, 1536]
-    C2 = torch.empty(Mp, HD, device=dev, dtype=torch.bfloat16)
-    aux = torch.randn(Mp, HD, device=dev)
+    Mp = (max(M for _, _, M, _, _ in NT) + 255) // 256 * 256
+    A = torch.randn(Mp, max(WX, HD * 2), device=dev).bfloat16()
+    Bw = (torch.randn(max(WX, HD * 2), max(WX, HD * 2), device=dev) * 0.05).bfloat16()
+    bias = torch.randn(max(WX, HD * 2), device=dev)
+    C = torch.empty(Mp, WX, device=dev)  # f32 [M, widest N]
+    C2 = torch.empty(Mp, WX, device=dev, dtype=torch.bfloat16)
+    aux = torch.randn(Mp, WX, device=dev)
     results = {}
     only = set(args.only.split(",")) if args.only else None
     for name, epi, M, N, K in NT:
@@ -87,8 +96,8 @@ def main():
             row[v] = {"ms": round(t, 4), "tflops": round(flops / t / 1e9, 1)}
         results[name] = row
         print(name, json.dumps(row), flush=True)
-    ws = torch.empty(160 * HD * D, device=dev)
-    out = torch.empty(HD, HD, device=dev)
+    ws = torch.empty(160 * max(n1 * n2 for _, _, n1, n2 in TN), device=dev)
+    out = torch.empty(max(n1 * n2 for _, _, n1, n2 in TN), device=dev)
     for name, M, N1, N2 in TN:
         if only and name not in only:
             continue
