@@ -22,8 +22,10 @@ Reported beside it:
                 = the weight-gradient GEMM gemm_tn (es_gemm_tn: TN kernel + split-K reduction), timed
                 live with HIP events on its launch stream (the side stream of the backward) at the
                 fc1 weight-gradient site: algorithmic 2*M*1536*384 FLOP per launch (M = train tokens)
-                vs the bf16 dense MFMA peak 2516.6 TFLOP/s.  traffic = HBM bytes per launch from the
-                committed rocprofv3 --pmc summary (profiles/pmc_traffic.json).
+                vs the bf16 dense MFMA peak 2516.6 TFLOP/s.  traffic = HBM bytes of that same site
+                inside the F1 step (kernel + split-K and bias reductions), from rocprofv3 --pmc
+                FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes over this bench (scripts/gpu_pmc_step.sh,
+                scripts/pmc_site_bytes.py -> profiles/pmc_traffic.json).
   step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.  The engine skips
                 the last block's non-CLS rows after its qkv GEMM (their outputs never reach the head;
                 Engine.PRUNE_LAST), so it executes fewer FLOPs than that: `executed_step_tflop`.
