@@ -262,6 +262,8 @@ CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
 # train-mode BatchNorm statistics of a bf16 conv's output computed in the conv's epilogue
 # (es_conv2d_fwd_bf16_bnstats -> es_bn2d_fwd_partials): no two statistics passes over the map
 BN_STATS_FUSED = os.environ.get("ENDOSSL_BN_STATS_FUSED", "1") != "0"
+# a ConvBlock input's two gradient contributions (conv1, residual) summed in place (_GradSink)
+GRAD_SINKS = os.environ.get("ENDOSSL_GRAD_SINKS", "1") != "0"
 
 
 def _conv_bf16(m, xmap, Cout, k):
@@ -270,12 +272,25 @@ def _conv_bf16(m, xmap, Cout, k):
     return bool(_lib.load().es_conv2d_bf16_eligible(xmap.C, Cout, k, k))
 
 
+class _GradSink:
+    """The gradient of a map with two consumers on one stream -- a ConvBlock's input feeds conv1 and
+    the residual (identity into bn3, or residual_conv) -- summed in place instead of by autograd's
+    add (a full extra read-read-write pass over the map): the first consumer's backward writes the
+    buffer and returns None for the map, the second accumulates into it (the conv data-gradient
+    kernels' accumulate mode) and returns it.  bn3's backward always runs before conv1's (conv1's
+    output gradient depends on it)."""
+    __slots__ = ("buf",)
+
+    def __init__(self):
+        self.buf = None
+
+
 class _ConvFn(torch.autograd.Function):
     """Conv2d (groups 1, optional bias) on an NHWC view -> new NHWC map (code/models/conformer.py
     ConvBlock / FCU convs, Conformer.conv1)."""
 
     @staticmethod
-    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None, stats=False):
+    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None, stats=False, sink=None):
         Ho, Wo = (xmap.H + 2 * p - k) // s + 1, (xmap.W + 2 * p - k) // s + 1
         y = torch.empty(xmap.N, Ho, Wo, Cout, dtype=torch.float32, device=x.device)
         b16 = _conv_bf16(m, xmap, Cout, k)
@@ -295,6 +310,7 @@ class _ConvFn(torch.autograd.Function):
             call("es_conv2d_fwd", *args, ptr(m.pview(wname)), *tail)
         ctx.save_for_backward(x)
         ctx.m, ctx.xmap, ctx.spec, ctx.b16 = m, xmap, (wname, bname, Cout, k, s, p, Ho, Wo), b16
+        ctx.sink = sink
         return y
 
     @staticmethod
@@ -332,12 +348,19 @@ class _ConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             full = xm.off == 0 and xm.sc == 1 and xm.sn * xm.N == x.numel()
-            dx = torch.empty_like(x) if full else torch.zeros_like(x)
+            sink = ctx.sink if full else None
+            acc = 1 if (sink is not None and sink.buf is not None) else 0
+            if acc:
+                dx = sink.buf
+            else:
+                dx = torch.empty_like(x) if full else torch.zeros_like(x)
             wimg = m.conv_pack(wname, Cout, xm.C, k)[1] if b16 else m.pview(wname)
             call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
-                 ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, 0,
+                 ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, acc,
                  _s())
-        return dx, None, None, None, None, None, None, None, None, None, None
+            if sink is not None:  # first consumer: hand the buffer over; second: return the sum
+                sink.buf, dx = (None, dx) if acc else (dx, None)
+        return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _nullctx:
@@ -348,10 +371,10 @@ class _nullctx:
         return False
 
 
-def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None, stats=False):
+def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None, stats=False, sink=None):
     """stats=True: the output feeds a train-mode BatchNorm, which then takes its batch statistics
-    from the conv's epilogue (BN_STATS_FUSED)."""
-    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor, stats)
+    from the conv's epilogue (BN_STATS_FUSED).  sink: a _GradSink shared with x's other consumer."""
+    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor, stats, sink)
 
 
 class _BNFn(torch.autograd.Function):
@@ -359,7 +382,7 @@ class _BNFn(torch.autograd.Function):
     residual_bn, FCUUp bn, Conformer.bn1)."""
 
     @staticmethod
-    def forward(ctx, x, res, m, pre, eps, relu):
+    def forward(ctx, x, res, m, pre, eps, relu, res_sink=None):
         x = x.contiguous()
         N, H, W, C = x.shape
         rows = N * H * W
@@ -394,6 +417,7 @@ class _BNFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, mean, rstd)
         ctx.m, ctx.pre, ctx.eps, ctx.relu, ctx.train, ctx.has_res = m, pre, eps, relu, train, res is not None
         ctx.world = world
+        ctx.res_sink = res_sink if res is not None else None
         return y
 
     @staticmethod
@@ -416,15 +440,28 @@ class _BNFn(torch.autograd.Function):
             call("es_bn2d_bwd_global", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0,
                  ptr(m.pview(pre + "weight")), ptr(mean), ptr(rstd), ptr(loc), ptr(glob), rows * ctx.world, ptr(dx),
                  ptr(gout), ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, _s())
-            return dx, gout, None, None, None, None
+            return dx, _BNFn._res_grad(ctx, gout), None, None, None, None, None
         call("es_bn2d_bwd", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(m.pview(pre + "weight")),
              ptr(mean), ptr(rstd), 1 if ctx.train else 0, ptr(rv), ctx.eps, ptr(dx), ptr(gout),
              ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(ws), _s())
-        return dx, gout, None, None, None, None
+        return dx, _BNFn._res_grad(ctx, gout), None, None, None, None, None
+
+    @staticmethod
+    def _res_grad(ctx, gout):
+        """The residual's gradient, or None with it handed to the residual map's _GradSink."""
+        sink = ctx.res_sink
+        if gout is None or sink is None:
+            return gout
+        if sink.buf is None:
+            sink.buf = gout
+            return None
+        sink.buf.add_(gout)  # (not reached in the Conformer / ResNet graphs: bn3 runs first)
+        out, sink.buf = sink.buf, None
+        return out
 
 
-def bn(m, x, pre, eps=BN_EPS_BLOCK, relu=False, res=None):
-    return _BNFn.apply(x, res, m, pre, eps, relu)
+def bn(m, x, pre, eps=BN_EPS_BLOCK, relu=False, res=None, res_sink=None):
+    return _BNFn.apply(x, res, m, pre, eps, relu, res_sink)
 
 
 class _MaxPoolFn(torch.autograd.Function):
@@ -928,29 +965,33 @@ class NativeConformer(nn.Module):
     # ---- forward (code/models/conformer.py:418-445) ------------------------------------------
     def _conv_block(self, pre, x, stride, res_conv, x_t=None, return_x2=True):
         """ConvBlock.forward (:107-144)."""
-        x2 = self._conv_block_head(pre, x, stride, x_t)
-        out = self._conv_block_tail(pre, x, x2, stride, res_conv)
+        sink = _GradSink() if GRAD_SINKS else None
+        x2 = self._conv_block_head(pre, x, stride, x_t, sink=sink)
+        out = self._conv_block_tail(pre, x, x2, stride, res_conv, sink=sink)
         return (out, x2) if return_x2 else out
 
-    def _conv_block_head(self, pre, x, stride, x_t=None):
-        """conv1 -> bn1 -> ReLU (-> + upsampled x_t) -> conv2 -> bn2 -> ReLU: x2 (:118-130)."""
+    def _conv_block_head(self, pre, x, stride, x_t=None, sink=None):
+        """conv1 -> bn1 -> ReLU (-> + upsampled x_t) -> conv2 -> bn2 -> ReLU: x2 (:118-130).  sink: the
+        _GradSink x shares with the tail's residual."""
         med = self.shapes[pre + "conv1.weight"][0]
-        h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1, stats=True), pre + "bn1.",
-               relu=True)
+        h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1, stats=True, sink=sink),
+               pre + "bn1.", relu=True)
         if x_t is not None:
             h = _UpsampleAddFn.apply(h, x_t, h.shape[1] // x_t.shape[1])
         h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1, stats=True)
         return bn(self, h, pre + "bn2.", relu=True)
 
-    def _conv_block_tail(self, pre, x, x2, stride, res_conv):
+    def _conv_block_tail(self, pre, x, x2, stride, res_conv, sink=None):
         """conv3 -> bn3 (+ residual, via residual_conv / residual_bn) -> ReLU (:132-144)."""
         outp = self.shapes[pre + "conv3.weight"][0]
         h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1, stats=True)
         residual = x
         if res_conv:
-            r = conv(self, x, _Map.nhwc(x), pre + "residual_conv.weight", None, outp, 1, stride, stats=True)
+            r = conv(self, x, _Map.nhwc(x), pre + "residual_conv.weight", None, outp, 1, stride, stats=True,
+                     sink=sink)
             residual = bn(self, r, pre + "residual_bn.")
-        return bn(self, h, pre + "bn3.", relu=True, res=residual)
+            return bn(self, h, pre + "bn3.", relu=True, res=residual)
+        return bn(self, h, pre + "bn3.", relu=True, res=residual, res_sink=sink)
 
     def forward(self, x):
         cfg = self.cfg
@@ -1006,11 +1047,12 @@ class NativeConformer(nn.Module):
             pre = name + "."
             med = outp // 4
             xin = xc
-            x2 = self._conv_block_head(pre + "cnn_block.", xin, stride)
+            sink = _GradSink() if GRAD_SINKS else None
+            x2 = self._conv_block_head(pre + "cnn_block.", xin, stride, sink=sink)
             to_branch(x2)
             with torch.cuda.stream(tb):
                 xt, up = self._trans_branch(pre, x2, xt, dw, med)
-            xc = self._conv_block_tail(pre + "cnn_block.", xin, x2, stride, res_conv)
+            xc = self._conv_block_tail(pre + "cnn_block.", xin, x2, stride, res_conv, sink=sink)
             to_main(up)
             xc = self._conv_block(pre + "fusion_block.", xc, 2 if last else 1, last, x_t=up, return_x2=False)
         to_main(xt)

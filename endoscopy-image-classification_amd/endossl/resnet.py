@@ -18,8 +18,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .conformer import (BN_EPS_STEM, CONV_BF16, NativeConformer, _ConvHeadFn, _Map, _MaxPoolFn, _join_queued, _rup,
-                        bn, conv)
+from .conformer import (BN_EPS_STEM, CONV_BF16, GRAD_SINKS, NativeConformer, _ConvHeadFn, _GradSink, _Map, _MaxPoolFn,
+                        _join_queued, _rup, bn, conv)
 
 BN_EPS = 1e-5  # timm BasicBlock norm_layer = nn.BatchNorm2d (default eps)
 
@@ -113,15 +113,16 @@ class NativeResNet(NativeConformer):
 
     def _block(self, x, pre, inp, planes, stride, ds):
         """timm BasicBlock.forward: relu(bn2(conv2(relu(bn1(conv1(x))))) + shortcut)."""
-        h = conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, planes, 3, stride, 1, stats=True)
+        sink = _GradSink() if GRAD_SINKS else None  # x's two gradient contributions summed in place
+        h = conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, planes, 3, stride, 1, stats=True, sink=sink)
         h = bn(self, h, pre + "bn1.", eps=BN_EPS, relu=True)
         h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, planes, 3, 1, 1, stats=True)
         if ds:
-            sc = conv(self, x, _Map.nhwc(x), pre + "downsample.0.weight", None, planes, 1, stride, 0, stats=True)
+            sc = conv(self, x, _Map.nhwc(x), pre + "downsample.0.weight", None, planes, 1, stride, 0, stats=True,
+                      sink=sink)
             sc = bn(self, sc, pre + "downsample.1.", eps=BN_EPS)
-        else:
-            sc = x
-        return bn(self, h, pre + "bn2.", eps=BN_EPS, relu=True, res=sc)
+            return bn(self, h, pre + "bn2.", eps=BN_EPS, relu=True, res=sc)
+        return bn(self, h, pre + "bn2.", eps=BN_EPS, relu=True, res=x, res_sink=sink)
 
     def forward(self, x):
         cfg = self.cfg
