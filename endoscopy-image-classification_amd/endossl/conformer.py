@@ -273,16 +273,37 @@ def _conv_bf16(m, xmap, Cout, k):
 
 
 class _GradSink:
-    """The gradient of a map with two consumers on one stream -- a ConvBlock's input feeds conv1 and
-    the residual (identity into bn3, or residual_conv) -- summed in place instead of by autograd's
-    add (a full extra read-read-write pass over the map): the first consumer's backward writes the
-    buffer and returns None for the map, the second accumulates into it (the conv data-gradient
-    kernels' accumulate mode) and returns it.  bn3's backward always runs before conv1's (conv1's
-    output gradient depends on it)."""
-    __slots__ = ("buf",)
+    """The gradient of a map with two consumers summed in place instead of by autograd's add (a full
+    extra read-read-write pass over the map): a ConvBlock's input feeds conv1 and the residual
+    (identity into bn3, or residual_conv).  (Its x2, which feeds conv3 and the transformer branch's
+    FCUDown on the branch stream, keeps autograd's add: the cross-stream wait cost what the add
+    saved, S1 195.5 vs 194.7 ms.)  The first consumer's backward writes the buffer (take -> a
+    fresh map, accumulate 0) and returns None for the map (give); the second waits for the first's
+    event, accumulates into the buffer (the data-gradient kernels' accumulate mode) and returns it.
+    bn3's backward always runs before conv1's (conv1's output gradient depends on it)."""
+    __slots__ = ("buf", "ev")
 
     def __init__(self):
-        self.buf = None
+        self.buf, self.ev = None, None
+
+    def take(self, alloc):
+        """(dx buffer, accumulate flag) for the consumer whose backward runs now; alloc() makes the
+        buffer when it is the first."""
+        if self.buf is None:
+            return alloc(), 0
+        cur = torch.cuda.current_stream(self.buf.device)
+        cur.wait_event(self.ev)
+        self.buf.record_stream(cur)
+        return self.buf, 1
+
+    def give(self, dx, acc):
+        """What the backward returns for the map after writing dx (acc as take returned it)."""
+        if acc:
+            self.buf, self.ev = None, None
+            return dx
+        self.buf, self.ev = dx, torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream(dx.device))
+        return None
 
 
 class _ConvFn(torch.autograd.Function):
@@ -348,18 +369,15 @@ class _ConvFn(torch.autograd.Function):
         dx = None
         if ctx.needs_input_grad[0]:
             full = xm.off == 0 and xm.sc == 1 and xm.sn * xm.N == x.numel()
-            sink = ctx.sink if full else None
-            acc = 1 if (sink is not None and sink.buf is not None) else 0
-            if acc:
-                dx = sink.buf
-            else:
-                dx = torch.empty_like(x) if full else torch.zeros_like(x)
+            sink = ctx.sink
+            alloc = (lambda: torch.empty_like(x)) if full else (lambda: torch.zeros_like(x))  # noqa: E731
+            dx, acc = sink.take(alloc) if sink is not None else (alloc(), 0)
             wimg = m.conv_pack(wname, Cout, xm.C, k)[1] if b16 else m.pview(wname)
             call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
                  ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, acc,
                  _s())
             if sink is not None:  # first consumer: hand the buffer over; second: return the sum
-                sink.buf, dx = (None, dx) if acc else (dx, None)
+                dx = sink.give(dx, acc)
         return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
@@ -453,11 +471,10 @@ class _BNFn(torch.autograd.Function):
         if gout is None or sink is None:
             return gout
         if sink.buf is None:
-            sink.buf = gout
-            return None
-        sink.buf.add_(gout)  # (not reached in the Conformer / ResNet graphs: bn3 runs first)
-        out, sink.buf = sink.buf, None
-        return out
+            return sink.give(gout, 0)
+        buf, _ = sink.take(None)  # (not reached in the Conformer / ResNet graphs: bn3 runs first)
+        buf.add_(gout)
+        return sink.give(buf, 1)
 
 
 def bn(m, x, pre, eps=BN_EPS_BLOCK, relu=False, res=None, res_sink=None):
