@@ -1025,12 +1025,14 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   // the 256x256 tile (BK64, 2 stages): 200 vs 228 us for the 128x128 BK32 kernel.  (The fc1
   // forward, 238 vs 251 us alone, loses with the weak forward co-running: 0.50 vs 0.39 ms.)
   // ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
-  // tile, 710-930 vs 620-900 TF/s for the 256x128 ring in isolation (scripts/gemm_bench.py --s1).
+  // tile, 710-930 vs 620-900 TF/s for the 256x128 ring in isolation (scripts/gemm_bench.py --s1) --
+  // except the erf-per-element EPI_DGELU epilogue, serial behind the 8 waves' K loop at one
+  // workgroup per CU (S1 fc2 data gradient 1.97 vs 1.65 ms on the 256x128 ring)
   int variant = g_gemm_variant;
   if (variant < 0) {
     if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
       variant = 6;
-    else if (K >= 768 && N % 256 == 0)
+    else if (K >= 768 && N % 256 == 0 && epi != EPI_DGELU)
       variant = 6;
     else
       variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
