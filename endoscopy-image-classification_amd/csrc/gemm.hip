@@ -1018,24 +1018,32 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     return ES_BAD_ARG;
   if (epi == EPI_PATCH && np <= 0) return ES_BAD_ARG;
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
-  // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py): short K
-  // (<= 384) is epilogue-bound -> BK32 two-stage at 5 workgroups/CU (BK32 three-stage for the
-  // epilogues that read an aux operand: DGELU, residual); long K -> 256x128 three-stage ring.
-  // The fc2 dgrad (EPI_MULAUX: 310 MB of GELU' read, 310 MB written per launch at F1) runs best on
-  // the 256x256 tile (BK64, 2 stages): 200 vs 228 us for the 128x128 BK32 kernel.  (The fc1
-  // forward, 238 vs 251 us alone, loses with the weak forward co-running: 0.50 vs 0.39 ms.)
-  // ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
-  // tile, 710-930 vs 620-900 TF/s for the 256x128 ring in isolation (scripts/gemm_bench.py --s1) --
-  // except the erf-per-element EPI_DGELU epilogue, serial behind the 8 waves' K loop at one
-  // workgroup per CU (S1 fc2 data gradient 1.97 vs 1.65 ms on the 256x128 ring)
+  // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py, isolated launches
+  // at the F1 shapes and at 1/2, 1/4, 1/8 of the batch -- a rank's share at N GPUs, --shard):
+  //  * the GELU epilogues (fc1 forward): 128x128 BK32 two-stage at 4-5 workgroups/CU for K <= 384;
+  //  * the other K <= 384 GEMMs: 128x128 BK64 two-stage (variant 0) for the N = 384 outputs (proj
+  //    forward / dgrad: 0.91-0.96x the BK32 kernels' time at every batch share) and for M < 32768
+  //    (qkv forward 0.90x at 1/4, 0.85x at 1/8), else BK32 (three-stage for DGELU);
+  //  * fc2 dgrad (EPI_MULAUX: 310 MB of GELU' read at F1) on the 256x256 tile (200 vs 228 us), on
+  //    variant 0 below M = 32768 (0.90x at 1/4, 0.78x at 1/8);
+  //  * long K (fc2 forward, fc1 / qkv dgrad): the 256x128 three-stage ring, variant 0 below
+  //    M = 65536 (0.81x for the two dgrads at 1/2);
+  //  * ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
+  //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
+  //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
   int variant = g_gemm_variant;
   if (variant < 0) {
+    const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
     if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
-      variant = 6;
+      variant = M < 32768 ? 0 : 6;
     else if (K >= 768 && N % 256 == 0 && epi != EPI_DGELU)
       variant = 6;
+    else if (gelu)
+      variant = K <= 384 ? 5 : 1;
+    else if (K <= 384)
+      variant = (epi == EPI_F32_RESID || N <= 384 || M < 32768) ? 0 : (epi == EPI_DGELU ? 2 : 5);
     else
-      variant = K <= 384 ? ((epi == EPI_DGELU || epi == EPI_F32_RESID) ? 2 : 5) : 1;
+      variant = M < 65536 ? 0 : 1;
   }
   if (variant == 1) {
     const int grid = ((M + BM2 - 1) / BM2) * (N / BN);

@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--tn-blocks", default="512", help="target workgroup counts (split-K sizing) to sweep; "
                     "'auto' = the library's sizing, 's<N>' = N splits")
     ap.add_argument("--m-train", type=int, default=0, help="token rows of the TN shapes (default 512 x 197)")
+    ap.add_argument("--shard", type=int, default=1, help="F1 shapes at 1/N of the batch (a rank's share of the "
+                    "global batch at N GPUs, strong scaling)")
     ap.add_argument("--s1", action="store_true", help="the Conformer-B/384 transformer-branch shapes of S1 "
                     "(D 768, hidden 3072, 120 images x 577 tokens)")
     args = ap.parse_args()
@@ -45,6 +47,9 @@ def main():
               ("fc2_dgrad", 8, m, hd, d), ("fc1_dgrad", 0, m, d, hd), ("proj_dgrad", 0, m, d, d),
               ("qkv_dgrad", 0, m, d, 3 * d)]
         TN = [("fc2_wgrad", m, d, hd), ("fc1_wgrad", m, hd, d), ("proj_wgrad", m, d, d), ("qkv_wgrad", m, 3 * d, d)]
+    if args.shard > 1 and not args.s1:
+        NT = [(n, e, M // args.shard, N, K) for n, e, M, N, K in NT]
+        TN = [(n, M // args.shard, a, b) for n, M, a, b in TN]
     if args.m_train:
         TN = [(n, args.m_train, a, b) for n, _, a, b in TN]
     WX = max(max(n, k) for _, _, _, n, k in NT)  # widest operand / output row
