@@ -105,6 +105,42 @@ def host_cpus():
     return n, info
 
 
+def host_input_run(tr, B, MU, steps, dev):
+    """F1 steps whose batches come from the native host input path: decoded
+    RGB frames -> the reference's TransformFixMatch / labeled transforms on the granted host threads
+    (csrc/host_aug.cpp) -> pinned uint8 -> side-stream H2D copy, double-buffered against the step."""
+    import numpy as np
+
+    from endossl import host_aug
+    threads, _ = host_cpus()
+    g = np.random.default_rng(7)
+    base = g.integers(0, 256, (60, 80, 3), dtype=np.uint8)
+    srcs = [host_aug.resize_bilinear(base ^ np.uint8(i * 29 % 256), (500, 375)) for i in range(64)]
+    lab = host_aug.HostBatcher(srcs, batch=B, size=224, kind="labeled", seed=1, threads=threads, device=dev)
+    unl = host_aug.HostBatcher(srcs, batch=B * MU, size=224, kind="fixmatch", seed=2, threads=threads, device=dev)
+    y = torch.randint(0, 23, (B,), device=dev)
+
+    def one():
+        x, _ = lab.next()
+        uw, us = unl.next()
+        return tr.step(((x, y), ((uw, us), None)))
+
+    for _ in range(2):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        one()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t1 = time.perf_counter()  # the host transforms alone, same threads (what bounds the fed step)
+    host_aug.transform_batch(srcs[:32] * 4, 224, "fixmatch", seed=3, threads=threads)
+    pairs = 128 / (time.perf_counter() - t1)
+    return {"value": round(B * MU * steps / dt, 2), "unit": "unlabeled images/s", "ms_per_step": round(dt / steps * 1e3, 3),
+            "host_threads": threads, "host_fixmatch_pairs_per_s": round(pairs, 1),
+            "source": "synthetic decoded RGB 500x375 frames (64), IS_CROP, S=224; decode not timed"}
+
+
 def cpu_baseline(B=8, MU=7, steps=2):
     """Oracle (pinned CPU restatement) FixMatch step on every host core this process may use -- a
     reported baseline (torch.set_num_threads(os.cpu_count()), capped by the CPU share the
@@ -353,6 +389,11 @@ def main():
                     help="f1 = the BASELINE metric (default); c1 / s1 = CoMatch / SemiFormer configs")
     ap.add_argument("--s1-model", choices=("b384", "ti224"), default="b384",
                     help="s1: the ViT-Base/16 384^2 stress Conformer (BASELINE configs[4]) or build.py's Conformer-Ti")
+    ap.add_argument("--host-input", action="store_true",
+                    help="also time F1 steps fed by the native host input path (endossl.host_aug.HostBatcher: "
+                         "the reference's transforms on the granted host threads from decoded 500x375 RGB "
+                         "frames, pinned uint8 batches copied on a side stream); reported as 'host_input', "
+                         "never as value")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="hipGraph replay of the step's forward/backward (auto: on for N > 1; at N = 1 the "
                          "timed steps run eagerly so the roofline probe's HIP events see every launch)")
@@ -465,6 +506,7 @@ def main():
                 "ms_per_step": round(we.item() / args.steps * 1e3, 3),
                 "note": "same step with every rank on a full B=64, mu=7 batch (DDP weak scaling)"}
         del xw, yw, bw
+    host_input = host_input_run(tr, B, MU, args.steps, dev) if args.host_input else None
     iso_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / len(iso["events"])
     iso_tflops = (sum(f for _, _, f in iso["events"]) / (sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / 1e3)
                   / 1e12)
@@ -525,6 +567,8 @@ def main():
         }
         if weak is not None:
             res["weak_scaling"] = weak
+        if host_input is not None:
+            res["host_input"] = host_input
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline()
         print(json.dumps(res), flush=True)

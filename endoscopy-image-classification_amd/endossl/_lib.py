@@ -164,8 +164,10 @@ def load(path=None):
         fn.argtypes = args
     if lib.es_abi_version() != ABI_VERSION:
         raise EndosslLibraryError(f"ABI mismatch: library {lib.es_abi_version()} != python {ABI_VERSION}")
-    # kernel-family knobs for A/B runs (scripts/, bench.py): ENDOSSL_TN_VARIANT / ENDOSSL_GEMM_VARIANT
-    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant")):
+    # kernel-family knobs for A/B runs (scripts/, bench.py): ENDOSSL_TN_VARIANT / ENDOSSL_GEMM_VARIANT /
+    # ENDOSSL_ATTN_VARIANT
+    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"),
+                    ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant")):
         if os.environ.get(env):
             getattr(lib, fn)(int(os.environ[env]))
     if path is None:

@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU pass incl. the host input path: new tests first, then the driver's tiers, the F1 bench with the
+# host-fed measurement, secondary workloads and the rocprofv3 kernel trace.
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; OUT="$GRAFT_REPO_ROOT/gpurun_out"
+run() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1; local rc=$?
+  echo "$name rc=$rc"; tail -3 "$OUT/$name.log"
+  return $rc
+}
+ok() { [ "$1" -le 1 ]; }
+PT="python -u -m pytest -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread"
+run th 300 $PT -m gpu -x tests/test_gpu_host_input.py; rc=$?
+ok $rc && { run t 1100 $PT -m gpu -x tests/; rc=$?; }
+ok $rc && { run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; }
+ok $rc && { run bench 600 python bench.py --steps 10 --warmup 3 --host-input; rc=$?; }
+ok $rc && { run hab 300 python scripts/host_aug_bench.py --threads 1,8,16 --n 512; rc=$?; }
+if ok $rc && [ "${PROFILE:-1}" = 1 ]; then
+  export TMPDIR=/tmp
+  run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; rc=$?
+fi
+exit 0

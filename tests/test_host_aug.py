@@ -1,0 +1,214 @@
+"""Host input path (csrc/host_aug.cpp via endossl.host_aug) pinned bit-exact to PIL, the library the
+reference's transforms call (code/randaugment.py ops at fixed magnitudes and signs; torchvision's
+Resize / CenterCrop / RandomCrop(reflect) on PIL images, code/dataset.py:24-56).  PIL is the oracle
+here (Pillow as installed in this image; the reference pins no version).  CPU only."""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+PIL = pytest.importorskip("PIL")
+from PIL import Image, ImageDraw, ImageEnhance, ImageOps  # noqa: E402
+
+from endossl import host_aug  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "endoscopy-image-classification_amd", "csrc")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _built():
+    if not os.path.exists(host_aug.LIB_PATH):  # plain g++, seconds
+        subprocess.run(["make", "-C", CSRC, os.path.relpath(host_aug.LIB_PATH, CSRC)], check=True,
+                       capture_output=True)
+    host_aug.load()
+
+
+def _images():
+    g = np.random.default_rng(0)
+    out = [g.integers(0, 256, (37, 53, 3), dtype=np.uint8),  # ragged, odd sizes
+           g.integers(0, 256, (64, 64, 3), dtype=np.uint8)]
+    # smooth + low-contrast content (autocontrast / equalize / contrast see narrow histograms)
+    yy, xx = np.mgrid[0:70, 0:90]
+    sm = np.stack([(xx * 1.3 + yy) % 97 + 60, (yy * 2) % 80 + 90, (xx + 3 * yy) % 50 + 100], -1)
+    out.append(sm.astype(np.uint8))
+    out.append(np.full((20, 30, 3), 77, np.uint8))  # flat image (degenerate histograms)
+    return out
+
+
+IMGS = _images()
+
+
+def _f(v, max_v):  # the reference's _float_parameter / _int_parameter (code/randaugment.py:139-144)
+    return float(v) * max_v / 10
+
+
+def _i(v, max_v):
+    return int(v * max_v / 10)
+
+
+def _pil_op(im, name, v, neg):
+    """The reference's pool op at magnitude v, sign draw `neg`, written against PIL directly."""
+    s = -1 if neg else 1
+    if name == "AutoContrast":
+        return ImageOps.autocontrast(im)
+    if name == "Brightness":
+        return ImageEnhance.Brightness(im).enhance(_f(v, 0.9) + 0.05)
+    if name == "Color":
+        return ImageEnhance.Color(im).enhance(_f(v, 0.9) + 0.05)
+    if name == "Contrast":
+        return ImageEnhance.Contrast(im).enhance(_f(v, 0.9) + 0.05)
+    if name == "Equalize":
+        return ImageOps.equalize(im)
+    if name == "Identity":
+        return im
+    if name == "Posterize":
+        return ImageOps.posterize(im, _i(v, 4) + 4)
+    if name == "Rotate":
+        return im.rotate(s * _i(v, 30))
+    if name == "Sharpness":
+        return ImageEnhance.Sharpness(im).enhance(_f(v, 0.9) + 0.05)
+    if name == "ShearX":
+        return im.transform(im.size, Image.AFFINE, (1, s * _f(v, 0.3), 0, 0, 1, 0))
+    if name == "ShearY":
+        return im.transform(im.size, Image.AFFINE, (1, 0, 0, s * _f(v, 0.3), 1, 0))
+    if name == "Solarize":
+        return ImageOps.solarize(im, 256 - _i(v, 256))
+    if name == "TranslateX":
+        return im.transform(im.size, Image.AFFINE, (1, 0, int(s * _f(v, 0.3) * im.size[0]), 0, 1, 0))
+    if name == "TranslateY":
+        return im.transform(im.size, Image.AFFINE, (1, 0, 0, 0, 1, int(s * _f(v, 0.3) * im.size[1])))
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("name", host_aug.POOL)
+def test_pool_ops_bit_exact_vs_pil(name):
+    for a in IMGS:
+        im = Image.fromarray(a)
+        for v in range(1, 11):
+            for neg in (False, True):
+                want = np.asarray(_pil_op(im, name, v, neg).convert("RGB"))
+                got = host_aug.aug_op(a, name, v, neg)
+                assert np.array_equal(got, want), (name, a.shape, v, neg, int((got != want).sum()))
+
+
+@pytest.mark.parametrize("kind", ["brightness", "color", "contrast", "sharpness"])
+def test_enhance_factors_bit_exact(kind):
+    cls = {"brightness": ImageEnhance.Brightness, "color": ImageEnhance.Color, "contrast": ImageEnhance.Contrast,
+           "sharpness": ImageEnhance.Sharpness}[kind]
+    g = np.random.default_rng(1)
+    for a in IMGS:
+        for f in [0.0, 1.0, 0.8, 1.2, 0.05, 0.95, 1.85, 2.7] + list(g.uniform(0.0, 2.0, 6)):
+            want = np.asarray(cls(Image.fromarray(a)).enhance(f))
+            assert np.array_equal(host_aug.enhance(a, kind, f), want), (kind, a.shape, f)
+
+
+def test_rotate_float_and_special_angles():
+    """Image.rotate at RandomRotation(20)'s float angles and Pillow's transpose shortcuts."""
+    g = np.random.default_rng(2)
+    for a in IMGS:
+        for ang in [0, 90, 180, 270, -90, 360, 27, -27, 3] + list(g.uniform(-20, 20, 8)):
+            want = np.asarray(Image.fromarray(a).rotate(ang))
+            assert np.array_equal(host_aug.rotate(a, ang), want), (a.shape, ang)
+
+
+@pytest.mark.parametrize("src,dst", [((37, 53), (268, 268)), ((64, 64), (224, 224)), ((500, 375), (268, 268)),
+                                     ((268, 268), (112, 134)), ((90, 70), (90, 70)), ((1, 5), (7, 3))])
+def test_resize_bilinear_bit_exact(src, dst):
+    g = np.random.default_rng(sum(src) + sum(dst))
+    a = g.integers(0, 256, (src[1], src[0], 3), dtype=np.uint8)
+    want = np.asarray(Image.fromarray(a).resize(dst, Image.BILINEAR))
+    assert np.array_equal(host_aug.resize_bilinear(a, dst), want)
+
+
+def test_cutout_rectangle_and_reflect_crop():
+    a = IMGS[1]
+    for xy in [(10, 5, 26, 21), (50, 50, 64, 64), (0, 0, 0, 0), (-3, 60, 5, 70)]:
+        im = Image.fromarray(a.copy())
+        ImageDraw.Draw(im).rectangle(tuple(max(0, t) if i < 2 else t for i, t in enumerate(xy)), (127, 127, 127))
+        assert np.array_equal(host_aug.fill_rect(a, (max(0, xy[0]), max(0, xy[1]), xy[2], xy[3])), np.asarray(im))
+    # RandomCrop(S, padding=pad, padding_mode='reflect') == numpy reflect pad + crop (torchvision, PIL input)
+    b = IMGS[0]
+    pad, S = 6, 30
+    padded = np.pad(b, ((pad, pad), (pad, pad), (0, 0)), mode="reflect")
+    for top, left in [(0, 0), (2 * pad + b.shape[0] - S, 2 * pad + b.shape[1] - S), (5, 17)]:
+        assert np.array_equal(host_aug.pad_reflect_crop(b, pad, top, left, S), padded[top:top + S, left:left + S])
+
+
+def test_fixmatch_weak_is_resize_center_crop():
+    """TransformFixMatch's weak view (IS_CROP): Resize((1.2 S, 1.2 S)) -> CenterCrop(S), deterministic."""
+    S = 64
+    R = int(S * 1.2)
+    weak, strong = host_aug.transform_batch(IMGS[:3], S, "fixmatch", is_crop=True, seed=5, threads=2)
+    for i, a in enumerate(IMGS[:3]):
+        r = Image.fromarray(a).resize((R, R), Image.BILINEAR)
+        top = int(round((R - S) / 2.0))
+        want = np.asarray(r)[top:top + S, top:top + S].transpose(2, 0, 1)
+        assert np.array_equal(weak[i].numpy(), want)
+    assert strong.shape == weak.shape and strong.dtype == torch.uint8
+
+
+def test_batch_deterministic_across_threads_and_matches_single():
+    imgs = IMGS * 3
+    a = host_aug.transform_batch(imgs, 48, "fixmatch", seed=11, threads=1)
+    b = host_aug.transform_batch(imgs, 48, "fixmatch", seed=11, threads=8)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    c = host_aug.transform_batch(imgs, 48, "fixmatch", seed=12, threads=8)
+    assert not torch.equal(a[1], c[1])  # the strong view depends on the seed
+    lab = host_aug.transform_batch(imgs, 48, "labeled", seed=3, threads=4)[0]
+    lab1 = host_aug.transform_batch(imgs, 48, "labeled", seed=3, threads=1)[0]
+    assert torch.equal(lab, lab1) and lab.shape == (len(imgs), 3, 48, 48)
+
+
+def test_strong_view_statistics():
+    """RandAugmentMC's draws follow the reference's distributions: over many images the strong view
+    differs from the weak one (flip / crop / ops), and its Cutout leaves a 16 x 16 gray (127) square
+    in every image whose centre lands inside (code/randaugment.py:47-60, 221)."""
+    flat = [np.full((80, 80, 3), 200, np.uint8)] * 64
+    weak, strong = host_aug.transform_batch(flat, 64, "fixmatch", is_crop=True, seed=1, threads=4)
+    gray = (strong == 127).all(1)  # [n, S, S]
+    counts = gray.flatten(1).sum(1)
+    assert (counts > 0).float().mean() > 0.9
+    assert counts.max() <= 17 * 17
+
+
+def test_batcher_cpu_double_buffer():
+    hb = host_aug.HostBatcher(IMGS, batch=5, size=32, seed=4, threads=2, device="cpu")
+    w0, s0 = hb.next()
+    w1, s1 = hb.next()
+    assert w0.shape == (5, 3, 32, 32) and s1.dtype == torch.uint8
+    hb2 = host_aug.HostBatcher(IMGS, batch=5, size=32, seed=4, threads=7, device="cpu")
+    v0, t0 = hb2.next()
+    assert torch.equal(w0, v0) and torch.equal(s0, t0)  # per-(seed, step, index) streams
+
+
+def test_native_transform_object_signature():
+    class D:
+        IMG_SIZE = 40
+        IS_CROP = True
+
+    class C:
+        DATA = D
+
+    t = host_aug.TransformFixMatchNative(C)
+    w, s = t(Image.fromarray(IMGS[2]))
+    assert w.shape == (3, 40, 40) and s.shape == (3, 40, 40)
+    assert not math.isnan(float(w.float().mean()))
+
+
+def test_host_library_exports_every_declared_symbol():
+    """libendossl_host.so exports exactly what include/endossl_host.h declares, with matching arity."""
+    import re
+    txt = open(os.path.join(ROOT, "include", "endossl_host.h")).read()
+    decl = sorted(set(re.findall(r"^\s*int\s+(esh_\w+)\s*\(", txt, flags=re.M)))
+    assert set(decl) == set(host_aug._SIG)
+    flat = txt.replace("\n", " ")
+    lib = host_aug.load()
+    for name, (_, args) in host_aug._SIG.items():
+        assert hasattr(lib, name), name
+        params = [p for p in re.search(r"\b" + name + r"\s*\(([^)]*)\)", flat).group(1).split(",")
+                  if p.strip() and p.strip() != "void"]
+        assert len(params) == len(args), name
