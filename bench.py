@@ -121,7 +121,7 @@ def host_input_run(tr, B, MU, steps, dev):
     y = torch.randint(0, 23, (B,), device=dev)
 
     def one():
-        x, _ = lab.next()
+        (x,) = lab.next()
         uw, us = unl.next()
         return tr.step(((x, y), ((uw, us), None)))
 

@@ -670,6 +670,125 @@ void labeled_train(const View& src, int S, bool is_crop, uint64_t seed, Img& out
   out = std::move(im);
 }
 
+// ---- ColorJitter hue / RandomGrayscale (TransformCoMatch's strong_1) ------------------------------
+// PIL's convert("HSV") / convert("RGB") from HSV (Convert.c, "following colorsys.py"): float / double
+// arithmetic exactly as Pillow evaluates it, pinned by tests/test_host_aug.py.
+inline void rgb2hsv_px(const u8* in, u8* out) {
+  const u8 r = in[0], g = in[1], b = in[2];
+  const u8 maxc = std::max(r, std::max(g, b)), minc = std::min(r, std::min(g, b));
+  u8 uh = 0, us = 0;
+  if (minc != maxc) {
+    const float cr = (float)(maxc - minc);
+    const float sat = cr / (float)maxc;
+    const float rc = (float)(maxc - r) / cr, gc = (float)(maxc - g) / cr, bc = (float)(maxc - b) / cr;
+    float h;
+    if (r == maxc) h = bc - gc;
+    else if (g == maxc) h = (float)(2.0 + rc - bc);
+    else h = (float)(4.0 + gc - rc);
+    h = (float)std::fmod(h / 6.0 + 1.0, 1.0);
+    const int ih = (int)(h * 255.0), is = (int)(sat * 255.0);
+    uh = (u8)(ih < 0 ? 0 : (ih > 255 ? 255 : ih));
+    us = (u8)(is < 0 ? 0 : (is > 255 ? 255 : is));
+  }
+  out[0] = uh;
+  out[1] = us;
+  out[2] = maxc;
+}
+
+inline u8 clip_i(int v) { return (u8)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+
+inline void hsv2rgb_px(const u8* in, u8* out) {
+  const u8 h = in[0], s = in[1], v = in[2];
+  if (s == 0) {
+    out[0] = out[1] = out[2] = v;
+    return;
+  }
+  const int i = (int)std::floor((float)h * 6.0 / 255.0);
+  const float f = (float)((float)h * 6.0 / 255.0 - (float)i);
+  const float fs = (float)((float)s / 255.0);
+  const u8 up = clip_i((int)std::round((float)v * (1.0 - fs)));
+  const u8 uq = clip_i((int)std::round((float)v * (1.0 - fs * f)));
+  const u8 ut = clip_i((int)std::round((float)v * (1.0 - fs * (1.0 - f))));
+  switch (i % 6) {
+    case 0: out[0] = v; out[1] = ut; out[2] = up; break;
+    case 1: out[0] = uq; out[1] = v; out[2] = up; break;
+    case 2: out[0] = up; out[1] = v; out[2] = ut; break;
+    case 3: out[0] = up; out[1] = uq; out[2] = v; break;
+    case 4: out[0] = ut; out[1] = up; out[2] = v; break;
+    default: out[0] = v; out[1] = up; out[2] = uq; break;
+  }
+}
+
+// torchvision adjust_hue on a PIL image: HSV, h += int8(hue_factor * 255) with uint8 wraparound, back
+void adjust_hue(Img& im, double hue_factor) {
+  const int shift = (int)(hue_factor * 255.0);  // np.int8(hue_factor * 255): truncation toward zero
+  const size_t n = (size_t)im.w * im.h;
+  u8 hsv[3];
+  for (size_t i = 0; i < n; ++i) {
+    u8* q = &im.px[i * 3];
+    rgb2hsv_px(q, hsv);
+    hsv[0] = (u8)((hsv[0] + shift) & 255);
+    hsv2rgb_px(hsv, q);
+  }
+}
+
+// rgb_to_grayscale(img, 3) on PIL: convert("L"), the gray replicated into three channels
+void grayscale3(Img& im) {
+  const size_t n = (size_t)im.w * im.h;
+  for (size_t i = 0; i < n; ++i) {
+    u8* q = &im.px[i * 3];
+    q[0] = q[1] = q[2] = (u8)luma(q);
+  }
+}
+
+void to_chw(const Img& im, u8* dst);
+
+// TransformCoMatch (code/dataset.py:58-110, IS_CROP): weak = Resize -> CenterCrop -> HFlip; strong_0 =
+// Resize -> CenterCrop -> HFlip -> RandAugmentMC(2, 10); strong_1 = Resize -> CenterCrop ->
+// RandomApply([ColorJitter(0.4, 0.4, 0.4, 0.1)], p=0.8) -> RandomGrayscale(0.2) -> HFlip
+void comatch_triplet(const View& src, int S, bool is_crop, uint64_t seed, u8* w_chw, u8* s0_chw, u8* s1_chw) {
+  const int R = is_crop ? (int)(S * 1.2) : S;
+  Img base = resize_bilinear(src, R, R);
+  if (is_crop) base = center_crop(base, S);
+  Rng rng(seed);
+  {
+    Img w = base;
+    if (rng.uniform() < 0.5) hflip(w);
+    to_chw(w, w_chw);
+  }
+  {
+    Img s0 = base;
+    if (rng.uniform() < 0.5) hflip(s0);
+    randaugment_mc(s0, 2, 10, rng);
+    to_chw(s0, s0_chw);
+  }
+  Img& s1 = base;
+  if (rng.uniform() < 0.8) {  // ColorJitter: the four adjustments in a random order
+    int order[4] = {0, 1, 2, 3};
+    for (int i = 3; i > 0; --i) std::swap(order[i], order[rng.randint(0, i + 1)]);
+    const float fb = (float)(0.6 + 0.8 * rng.uniform()), fc = (float)(0.6 + 0.8 * rng.uniform());
+    const float fsat = (float)(0.6 + 0.8 * rng.uniform());
+    const double fh = -0.1 + 0.2 * rng.uniform();
+    for (int k = 0; k < 4; ++k) {
+      if (order[k] == 0) brightness(s1, fb);
+      else if (order[k] == 1) contrast(s1, fc);
+      else if (order[k] == 2) color(s1, fsat);
+      else adjust_hue(s1, fh);
+    }
+  }
+  if (rng.uniform() < 0.2) grayscale3(s1);
+  if (rng.uniform() < 0.5) hflip(s1);
+  to_chw(s1, s1_chw);
+}
+
+// the validation / evaluation transform (code/dataset.py:217-231): Resize -> CenterCrop
+void eval_view(const View& src, int S, bool is_crop, u8* chw) {
+  const int R = is_crop ? (int)(S * 1.2) : S;
+  Img base = resize_bilinear(src, R, R);
+  if (is_crop) base = center_crop(base, S);
+  to_chw(base, chw);
+}
+
 void to_chw(const Img& im, u8* dst) {  // planar [3][S][S]
   const size_t n = (size_t)im.w * im.h;
   for (size_t i = 0; i < n; ++i)
@@ -701,7 +820,7 @@ extern "C" {
 // status codes shared with the device library (include/endossl.h)
 enum { ESH_OK = 0, ESH_BAD_ARG = 2, ESH_BAD_SHAPE = 3 };
 
-int esh_abi_version(void) { return 1; }
+int esh_abi_version(void) { return 2; }
 
 // One RandAugmentMC pool op on an RGB HWC image (src may equal dst): op index in
 // fixmatch_augment_pool() order, magnitude v (1..10), neg = the op's sign draw.
@@ -728,6 +847,18 @@ int esh_enhance(int kind, const uint8_t* src, uint8_t* dst, int w, int h, float 
 }
 
 // Image.rotate(angle_deg) (NEAREST, no expand, fill 0)
+// ColorJitter's hue adjustment (torchvision adjust_hue on PIL) and RandomGrayscale's 3-channel gray:
+// kind 0 hue (factor in [-0.5, 0.5]), 1 grayscale (factor unused)
+int esh_color_op(int kind, const uint8_t* src, uint8_t* dst, int w, int h, double factor) {
+  if (bad_img(src, w, h) || !dst || kind < 0 || kind > 1 || (kind == 0 && !(factor >= -0.5 && factor <= 0.5)))
+    return ESH_BAD_ARG;
+  Img im = from_ptr(src, w, h);
+  if (kind == 0) adjust_hue(im, factor);
+  else grayscale3(im);
+  std::memcpy(dst, im.px.data(), im.px.size());
+  return ESH_OK;
+}
+
 int esh_rotate(const uint8_t* src, uint8_t* dst, int w, int h, double angle_deg) {
   if (bad_img(src, w, h) || !dst) return ESH_BAD_ARG;
   Img im = from_ptr(src, w, h);
@@ -768,8 +899,9 @@ int esh_pad_reflect_crop(const uint8_t* src, int w, int h, int pad, int top, int
 //  kind 0: TransformFixMatch -> weak (out0) and strong (out1)      code/dataset.py:24-56
 //  kind 1: the labeled train transform -> out0 (out1 unused)      code/dataset.py:185-207
 int esh_transform_batch(int kind, const uint8_t* const* srcs, const int* ws, const int* hs, int n, int S,
-                        int is_crop, uint64_t seed, int nthreads, uint8_t* out0, uint8_t* out1) {
-  if (!srcs || !ws || !hs || n <= 0 || S <= 0 || !out0 || (kind == 0 && !out1) || kind < 0 || kind > 1)
+                        int is_crop, uint64_t seed, int nthreads, uint8_t* out0, uint8_t* out1, uint8_t* out2) {
+  if (!srcs || !ws || !hs || n <= 0 || S <= 0 || !out0 || kind < 0 || kind > 3 || ((kind == 0 || kind == 2) && !out1) ||
+      (kind == 2 && !out2))
     return ESH_BAD_ARG;
   const int R = is_crop ? (int)(S * 1.2) : S;
   for (int i = 0; i < n; ++i)
@@ -779,6 +911,11 @@ int esh_transform_batch(int kind, const uint8_t* const* srcs, const int* ws, con
     const View src{srcs[i], ws[i], hs[i]};
     if (kind == 0) {
       fixmatch_pair(src, S, is_crop != 0, image_seed(seed, (uint64_t)i, 0), out0 + per * i, out1 + per * i);
+    } else if (kind == 2) {
+      comatch_triplet(src, S, is_crop != 0, image_seed(seed, (uint64_t)i, 2), out0 + per * i, out1 + per * i,
+                      out2 + per * i);
+    } else if (kind == 3) {
+      eval_view(src, S, is_crop != 0, out0 + per * i);
     } else {
       Img out;
       labeled_train(src, S, is_crop != 0, image_seed(seed, (uint64_t)i, 1), out);

@@ -25,7 +25,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ENDOSSL_HOST_LIB", os.path.join(_HERE, "lib", "libendossl_host.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # fixmatch_augment_pool() order (code/randaugment.py:147-163)
 POOL = ("AutoContrast", "Brightness", "Color", "Contrast", "Equalize", "Identity", "Posterize", "Rotate",
@@ -38,12 +38,13 @@ _SIG = {
     "esh_abi_version": (_I, []),
     "esh_aug_op": (_I, [_I, _P, _P, _I, _I, _I, _I]),
     "esh_enhance": (_I, [_I, _P, _P, _I, _I, ctypes.c_float]),
+    "esh_color_op": (_I, [_I, _P, _P, _I, _I, ctypes.c_double]),
     "esh_rotate": (_I, [_P, _P, _I, _I, ctypes.c_double]),
     "esh_resize_bilinear": (_I, [_P, _I, _I, _P, _I, _I]),
     "esh_fill_rect": (_I, [_P, _I, _I, _I, _I, _I, _I, _I]),
     "esh_pad_reflect_crop": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
     "esh_transform_batch": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_I), ctypes.POINTER(_I), _I, _I, _I,
-                                 ctypes.c_uint64, _I, _P, _P]),
+                                 ctypes.c_uint64, _I, _P, _P, _P]),
 }
 _lib = None
 _lock = threading.Lock()
@@ -104,6 +105,20 @@ def enhance(img, kind, factor):
     return out
 
 
+def adjust_hue(img, factor):
+    a = _hwc(img)
+    out = np.empty_like(a)
+    _check(load().esh_color_op(0, _ptr(a), _ptr(out), a.shape[1], a.shape[0], float(factor)), "esh_color_op")
+    return out
+
+
+def grayscale3(img):
+    a = _hwc(img)
+    out = np.empty_like(a)
+    _check(load().esh_color_op(1, _ptr(a), _ptr(out), a.shape[1], a.shape[0], 0.0), "esh_color_op")
+    return out
+
+
 def rotate(img, angle):
     a = _hwc(img)
     out = np.empty_like(a)
@@ -135,30 +150,36 @@ def pad_reflect_crop(img, pad, top, left, size):
 
 
 # ---- batches --------------------------------------------------------------------------------------
-def transform_batch(images, size, kind="fixmatch", is_crop=True, seed=0, threads=None, out0=None, out1=None):
-    """Run the reference's transform over a list of RGB images on `threads` host threads.
+KINDS = {"fixmatch": (0, 2), "labeled": (1, 1), "comatch": (2, 3), "eval": (3, 1)}  # kind -> (id, outputs)
 
-    kind 'fixmatch': TransformFixMatch (code/dataset.py:24-56) -> (weak, strong), each uint8
-    [n, 3, S, S]; kind 'labeled': the labeled train transform (:185-207) -> (x, None).  out0 / out1 may
-    be preallocated (e.g. pinned) uint8 tensors; image i's randomness is keyed on (seed, i) only."""
+
+def transform_batch(images, size, kind="fixmatch", is_crop=True, seed=0, threads=None, outs=None):
+    """Run one of the reference's transforms over a list of RGB images on `threads` host threads.
+
+    kind 'fixmatch': TransformFixMatch (code/dataset.py:24-56) -> (weak, strong); 'comatch':
+    TransformCoMatch (:58-110) -> (weak, strong_0, strong_1); 'labeled': the labeled train transform
+    (:185-207) -> (x,); 'eval': Resize -> CenterCrop (:217-231) -> (x,).  Each output uint8
+    [n, 3, S, S]; `outs` may hold preallocated (e.g. pinned) CPU tensors.  Image i's randomness is
+    keyed on (seed, i) only."""
     arrs = [_hwc(im) for im in images]
     n = len(arrs)
-    k = {"fixmatch": 0, "labeled": 1}[kind]
+    k, nout = KINDS[kind]
     shape = (n, 3, size, size)
-    out0 = torch.empty(shape, dtype=torch.uint8) if out0 is None else out0
-    if k == 0 and out1 is None:
-        out1 = torch.empty(shape, dtype=torch.uint8)
-    for t in (out0, out1) if k == 0 else (out0,):
+    outs = list(outs) if outs is not None else [torch.empty(shape, dtype=torch.uint8) for _ in range(nout)]
+    if len(outs) != nout:
+        raise ValueError(f"kind {kind!r} writes {nout} outputs")
+    for t in outs:
         if tuple(t.shape) != shape or t.dtype != torch.uint8 or not t.is_contiguous() or t.device.type != "cpu":
             raise ValueError(f"output must be a contiguous CPU uint8 tensor of shape {shape}")
     ptrs = (_P * n)(*[a.ctypes.data for a in arrs])
     ws = (_I * n)(*[a.shape[1] for a in arrs])
     hs = (_I * n)(*[a.shape[0] for a in arrs])
     threads = threads or min(16, os.cpu_count() or 1)
+    op = [t.data_ptr() for t in outs] + [None] * (3 - nout)
     rc = load().esh_transform_batch(k, ptrs, ws, hs, n, size, int(bool(is_crop)), int(seed) & (2 ** 64 - 1),
-                                    int(threads), out0.data_ptr(), out1.data_ptr() if k == 0 else None)
+                                    int(threads), *op)
     _check(rc, "esh_transform_batch")
-    return out0, (out1 if k == 0 else None)
+    return tuple(outs)
 
 
 class TransformFixMatchNative:
@@ -182,20 +203,23 @@ class HostBatcher:
     consumed, and copies it to the device on a side stream (code/dataset.py's DataLoader role).
 
     images: list of RGB images (PIL or HWC uint8); each batch draws `batch` of them uniformly (with a
-    fresh per-batch seed) and returns (weak, strong) device uint8 [batch, 3, S, S] (kind 'fixmatch')
-    or (x, None) (kind 'labeled'), ready for es_patch_im2col_u8."""
+    fresh per-batch seed) and next() returns the kind's views as device uint8 [batch, 3, S, S] tensors
+    ('fixmatch': (weak, strong), 'comatch': (weak, strong_0, strong_1), 'labeled' / 'eval': (x,)),
+    ready for es_patch_im2col_u8."""
 
     def __init__(self, images, batch, size, kind="fixmatch", is_crop=True, seed=0, threads=None, device="cuda"):
         self.images = [_hwc(im) for im in images]
         self.batch, self.size, self.kind, self.is_crop = batch, size, kind, is_crop
         self.seed, self.threads, self.device = seed, threads, device
         self.step = 0
+        nout = KINDS[kind][1]
         pin = torch.cuda.is_available() and str(device).startswith("cuda")
         shape = (batch, 3, size, size)
-        self._host = [[torch.empty(shape, dtype=torch.uint8, pin_memory=pin) for _ in range(2)] for _ in range(2)]
+        self._host = [[torch.empty(shape, dtype=torch.uint8, pin_memory=pin) for _ in range(nout)] for _ in range(2)]
         self._stream = torch.cuda.Stream(device=device) if pin else None
         self._events = [None, None]
         self._worker = None
+        self._error = None
         self._submit(0)
 
     def _indices(self, step):
@@ -203,14 +227,15 @@ class HostBatcher:
         return g.integers(0, len(self.images), self.batch)
 
     def _build(self, step):
-        slot = step & 1
-        if self._events[slot] is not None:  # the copy out of this slot two batches ago must be done
-            self._events[slot].synchronize()
-        idx = self._indices(step)
-        bufs = self._host[slot]
-        transform_batch([self.images[i] for i in idx], self.size, self.kind, self.is_crop,
-                        seed=(self.seed << 32) ^ step, threads=self.threads, out0=bufs[0],
-                        out1=bufs[1] if self.kind == "fixmatch" else None)
+        try:
+            slot = step & 1
+            if self._events[slot] is not None:  # the copy out of this slot two batches ago must be done
+                self._events[slot].synchronize()
+            idx = self._indices(step)
+            transform_batch([self.images[i] for i in idx], self.size, self.kind, self.is_crop,
+                            seed=(self.seed << 32) ^ step, threads=self.threads, outs=self._host[slot])
+        except BaseException as e:  # surfaced by next()
+            self._error = e
 
     def _submit(self, step):
         self._worker = threading.Thread(target=self._build, args=(step,), daemon=True)  # ctypes drops the GIL
@@ -219,22 +244,23 @@ class HostBatcher:
     def next(self):
         """The next batch on the device (the copy is ordered before any later work on the caller's stream)."""
         self._worker.join()
-        step, slot = self.step, self.step & 1
+        if self._error is not None:
+            raise self._error
+        slot = self.step & 1
         bufs = self._host[slot]
         if self._stream is None:
-            out = tuple(b.clone() for b in bufs) if self.kind == "fixmatch" else (bufs[0].clone(), None)
+            out = tuple(b.clone() for b in bufs)
         else:
             cur = torch.cuda.current_stream(self.device)
             self._stream.wait_stream(cur)
             with torch.cuda.stream(self._stream):
-                dev = [b.to(self.device, non_blocking=True) for b in (bufs if self.kind == "fixmatch" else bufs[:1])]
+                out = tuple(b.to(self.device, non_blocking=True) for b in bufs)
                 ev = torch.cuda.Event()
                 ev.record(self._stream)
             self._events[slot] = ev
             cur.wait_stream(self._stream)
-            for d in dev:
+            for d in out:
                 d.record_stream(cur)
-            out = (dev[0], dev[1]) if self.kind == "fixmatch" else (dev[0], None)
         self.step += 1
         self._submit(self.step)
         return out

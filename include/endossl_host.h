@@ -2,7 +2,9 @@
  *
  * Replaces the reference's DataLoader-worker transforms (torchvision on PIL images):
  *   TransformFixMatch            code/dataset.py:24-56     (weak / strong views; also SemiFormer's)
- *   the labeled train transform  code/dataset.py:185-207   (IS_CROP branch, without ToTensor/Normalize)
+ *   TransformCoMatch             code/dataset.py:58-110    (weak / strong_0 / strong_1 views)
+ *   the labeled train transform  code/dataset.py:185-207   (without ToTensor/Normalize)
+ *   the evaluation transform     code/dataset.py:217-231   (Resize -> CenterCrop)
  *   RandAugmentMC + its pool     code/randaugment.py:20-163,207-222
  * ToTensor + Normalize (code/dataset.py:49-51) are NOT here: the device applies them inside the patch
  * gather (es_patch_im2col_u8, include/endossl.h), so batches stay uint8 [n][3][S][S] end to end.
@@ -29,6 +31,11 @@ int esh_aug_op(int op, const uint8_t* src, uint8_t* dst, int w, int h, int v, in
  * (code/randaugment.py:24-36,87-89; torchvision ColorJitter's brightness / contrast / saturation). */
 int esh_enhance(int kind, const uint8_t* src, uint8_t* dst, int w, int h, float factor);
 
+/* ColorJitter's hue (torchvision adjust_hue on a PIL image: HSV, hue += int8(factor * 255) mod 256,
+ * back to RGB; factor in [-0.5, 0.5]) as kind 0, RandomGrayscale's 3-channel gray as kind 1
+ * (code/dataset.py:76-79). */
+int esh_color_op(int kind, const uint8_t* src, uint8_t* dst, int w, int h, double factor);
+
 /* Image.rotate(angle_deg), NEAREST, no expand, fill 0 (code/randaugment.py:80-84; RandomRotation). */
 int esh_rotate(const uint8_t* src, uint8_t* dst, int w, int h, double angle_deg);
 
@@ -45,11 +52,13 @@ int esh_pad_reflect_crop(const uint8_t* src, int w, int h, int pad, int top, int
 
 /* Batch builder on nthreads host threads; image i's randomness keyed on (seed, i) only, so the result
  * does not depend on nthreads.  Outputs planar uint8 [n][3][S][S] (es_patch_im2col_u8's input).
- *   kind 0: TransformFixMatch -> out0 = weak, out1 = strong   (code/dataset.py:24-56)
- *   kind 1: labeled train transform -> out0                   (code/dataset.py:185-207)
- * is_crop: config.DATA.IS_CROP (Resize to int(1.2 S), then CenterCrop(S)). */
+ *   kind 0: TransformFixMatch -> out0 = weak, out1 = strong                    (code/dataset.py:24-56)
+ *   kind 1: labeled train transform -> out0                                    (code/dataset.py:185-207)
+ *   kind 2: TransformCoMatch -> out0 = weak, out1 = strong_0, out2 = strong_1  (code/dataset.py:58-110)
+ *   kind 3: evaluation transform -> out0                                       (code/dataset.py:217-231)
+ * is_crop: config.DATA.IS_CROP (Resize to int(1.2 S), then CenterCrop(S)); unused outputs may be NULL. */
 int esh_transform_batch(int kind, const uint8_t* const* srcs, const int* ws, const int* hs, int n, int S,
-                        int is_crop, uint64_t seed, int nthreads, uint8_t* out0, uint8_t* out1);
+                        int is_crop, uint64_t seed, int nthreads, uint8_t* out0, uint8_t* out1, uint8_t* out2);
 
 #ifdef __cplusplus
 }

@@ -73,7 +73,7 @@ def test_fixmatch_step_on_host_batches():
     lab = host_aug.HostBatcher(srcs, batch=B, size=224, kind="labeled", seed=1, threads=2)
     unl = host_aug.HostBatcher(srcs, batch=B * MU, size=224, kind="fixmatch", seed=2, threads=2)
     for _ in range(2):
-        x, _ = lab.next()
+        (x,) = lab.next()
         uw, us = unl.next()
         y = torch.randint(0, 23, (B,), device="cuda")
         out = tr.step(((x, y), ((uw, us), None)))

@@ -212,3 +212,41 @@ def test_host_library_exports_every_declared_symbol():
         params = [p for p in re.search(r"\b" + name + r"\s*\(([^)]*)\)", flat).group(1).split(",")
                   if p.strip() and p.strip() != "void"]
         assert len(params) == len(args), name
+
+
+def _tv_adjust_hue(a, f):
+    """torchvision's adjust_hue on a PIL image: HSV, hue + int8(f * 255) with uint8 wraparound, RGB."""
+    h, s, v = Image.fromarray(a).convert("HSV").split()
+    nh = ((np.array(h, dtype=np.int64) + int(np.trunc(f * 255))) % 256).astype(np.uint8)
+    return np.asarray(Image.merge("HSV", (Image.fromarray(nh, "L"), s, v)).convert("RGB"))
+
+
+def test_hue_and_grayscale_bit_exact():
+    g = np.random.default_rng(5)
+    for a in IMGS + [g.integers(0, 256, (48, 48, 3), dtype=np.uint8)]:
+        for f in [0.0, 0.1, -0.1, 0.5, -0.5, 0.0392, -0.0785] + list(g.uniform(-0.1, 0.1, 6)):
+            assert np.array_equal(host_aug.adjust_hue(a, f), _tv_adjust_hue(a, f)), (a.shape, f)
+        gray = np.asarray(Image.fromarray(a).convert("L"))
+        assert np.array_equal(host_aug.grayscale3(a), np.dstack([gray] * 3))
+    # every RGB triple through PIL's HSV round trip (hue shift 0 is not the identity in PIL either)
+    cube = np.stack(np.meshgrid(np.arange(0, 256, 5), np.arange(0, 256, 3), np.arange(0, 256, 7), indexing="ij"), -1)
+    cube = cube.reshape(-1, 3)[: (cube.reshape(-1, 3).shape[0] // 64) * 64].reshape(64, -1, 3).astype(np.uint8)
+    cube = np.ascontiguousarray(cube)
+    assert np.array_equal(host_aug.adjust_hue(cube, 0.0), _tv_adjust_hue(cube, 0.0))
+    assert np.array_equal(host_aug.adjust_hue(cube, 0.07), _tv_adjust_hue(cube, 0.07))
+
+
+def test_comatch_and_eval_kinds():
+    S = 56
+    R = int(S * 1.2)
+    w, s0, s1 = host_aug.transform_batch(IMGS, S, "comatch", is_crop=True, seed=2, threads=3)
+    (ev,) = host_aug.transform_batch(IMGS, S, "eval", is_crop=True, threads=2)
+    for i, a in enumerate(IMGS):
+        r = np.asarray(Image.fromarray(a).resize((R, R), Image.BILINEAR))
+        top = int(round((R - S) / 2.0))
+        crop = r[top:top + S, top:top + S].transpose(2, 0, 1)
+        assert np.array_equal(ev[i].numpy(), crop)  # eval: Resize -> CenterCrop
+        # weak: the same crop, possibly mirrored
+        assert np.array_equal(w[i].numpy(), crop) or np.array_equal(w[i].numpy(), crop[:, :, ::-1])
+    w2, s02, s12 = host_aug.transform_batch(IMGS, S, "comatch", is_crop=True, seed=2, threads=1)
+    assert torch.equal(w, w2) and torch.equal(s0, s02) and torch.equal(s1, s12)
