@@ -109,7 +109,9 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
     const bf16x8 qf0 = lds_row8(Qs, q, g), qf1 = lds_row8(Qs, q, 4 + g);
 
     // scores in log2 units (scale * log2 e folded in): p = exp2(s - max) is one v_exp_f32; keys
-    // are masked only in the partial last tile (the branch is uniform per tile).
+    // are masked only in the last tile, the only one that can be partial (the launcher picks
+    // NT16 = ceil(T / 16)): a compile-time choice -- a runtime test per tile made the compiler
+    // precompute all 4 x NT16 key masks into SGPR pairs spilled to VGPR lanes.
     f32x4 s[NT16];
     float mx = -INFINITY;
 #pragma unroll
@@ -118,7 +120,7 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
       acc = mfma16(lds_row8(Ks, t * 16 + r, g), qf0, acc);
       acc = mfma16(lds_row8(Ks, t * 16 + r, 4 + g), qf1, acc);
       acc *= sl;
-      if (t * 16 + 16 > T) {
+      if (t == NT16 - 1) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
           if (t * 16 + 4 * g + i >= T) acc[i] = -INFINITY;
