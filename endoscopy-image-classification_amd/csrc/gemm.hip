@@ -345,8 +345,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
 // instead of 16 KiB for 64x64 tiles.  With BKT = 32 the B tile may need a half glds instruction
 // per wave (BN = 192: 24 rows per wave); the instruction count per wave stays uniform so the
 // vmcnt arithmetic holds for every wave.
-template <int EPI, int WM, int MF, int NF, int NST, int BKT>
-__global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
+// OCC: waves per SIMD the register budget is sized for (launch_bounds' second argument; 4: <= 128
+// VGPRs, so two 8-wave workgroups share a CU and one's epilogue runs beside the other's main loop).
+template <int EPI, int WM, int MF, int NF, int NST, int BKT, int OCC = 1>
+__global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int WN = 8 / WM;
   constexpr int TBM = WM * MF * 16, TBN = WN * NF * 16;
@@ -366,7 +368,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
   const int wm = w / WN, wn = w % WN;
   const int g = lane >> 4, r = lane & 15;
 
-  const EpiPre<EPI, NF> epre = epi_prefetch<EPI, NF>(p, m0 + wm * MF * 16, n0 + wn * NF * 16, lane);
+  // bias / first aux chunk prefetched at kernel start (one workgroup per CU: nothing else hides their
+  // latency); at two per CU they are loaded after the K loop instead, keeping 32 registers out of it
+  EpiPre<EPI, NF> epre;
+  if constexpr (OCC < 4) epre = epi_prefetch<EPI, NF>(p, m0 + wm * MF * 16, n0 + wn * NF * 16, lane);
 
   const bf16* ga[IA];
   const bf16* gb[IBF + IBH];
@@ -442,6 +447,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_big_kernel(NTArgs p) {
     buf = buf + 1 == NST ? 0 : buf + 1;
   }
 #undef BIG_ISSUE
+  if constexpr (OCC >= 4) epre = epi_prefetch<EPI, NF>(p, m0 + wm * MF * 16, n0 + wn * NF * 16, lane);
   __builtin_amdgcn_s_barrier();
   staged_epilogue_g<EPI, MF, NF>(p, smem + w * epi_wave_bytes<NF>(), acc, m0 + wm * MF * 16, n0 + wn * NF * 16,
                                  lane, epre);
@@ -965,29 +971,31 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
 #undef NT_EPIS
 #undef NT_LAUNCH
 
-#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_, BKT_)                                                   \
+#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_, BKT_, OCC_)                                             \
   {                                                                                                 \
     const size_t lds = (size_t)NST_ * (WM_ * MF_ * 16 + (8 / WM_) * NF_ * 16) * BKT_ * 2;            \
-    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_>, lds);                               \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_>), dim3(grid), dim3(512), \
-                       lds, stream, a);                                                             \
+    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_, OCC_>, lds);                         \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_, OCC_>), dim3(grid), \
+                       dim3(512), lds, stream, a);                                                  \
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;                                  \
   }
-#define BIG_EPIS(WM_, MF_, NF_, NST_, BKT_)                                         \
-  switch (epi) {                                                                    \
-    case EPI_BF16: BIG_LAUNCH(EPI_BF16, WM_, MF_, NF_, NST_, BKT_)                  \
-    case EPI_GELU: BIG_LAUNCH(EPI_GELU, WM_, MF_, NF_, NST_, BKT_)                  \
-    case EPI_F32_RESID: BIG_LAUNCH(EPI_F32_RESID, WM_, MF_, NF_, NST_, BKT_)        \
-    case EPI_DGELU: BIG_LAUNCH(EPI_DGELU, WM_, MF_, NF_, NST_, BKT_)                \
-    case EPI_F32: BIG_LAUNCH(EPI_F32, WM_, MF_, NF_, NST_, BKT_)                    \
-    case EPI_PATCH: BIG_LAUNCH(EPI_PATCH, WM_, MF_, NF_, NST_, BKT_)                \
-    case EPI_GELU_ACT: BIG_LAUNCH(EPI_GELU_ACT, WM_, MF_, NF_, NST_, BKT_)          \
-    case EPI_GELU_D: BIG_LAUNCH(EPI_GELU_D, WM_, MF_, NF_, NST_, BKT_)              \
-    case EPI_MULAUX: BIG_LAUNCH(EPI_MULAUX, WM_, MF_, NF_, NST_, BKT_)              \
-    default: return ES_BAD_ARG;                                                     \
+#define BIG_EPIS2(WM_, MF_, NF_, NST_, BKT_, OCC_)                                        \
+  switch (epi) {                                                                          \
+    case EPI_BF16: BIG_LAUNCH(EPI_BF16, WM_, MF_, NF_, NST_, BKT_, OCC_)                  \
+    case EPI_GELU: BIG_LAUNCH(EPI_GELU, WM_, MF_, NF_, NST_, BKT_, OCC_)                  \
+    case EPI_F32_RESID: BIG_LAUNCH(EPI_F32_RESID, WM_, MF_, NF_, NST_, BKT_, OCC_)        \
+    case EPI_DGELU: BIG_LAUNCH(EPI_DGELU, WM_, MF_, NF_, NST_, BKT_, OCC_)                \
+    case EPI_F32: BIG_LAUNCH(EPI_F32, WM_, MF_, NF_, NST_, BKT_, OCC_)                    \
+    case EPI_PATCH: BIG_LAUNCH(EPI_PATCH, WM_, MF_, NF_, NST_, BKT_, OCC_)                \
+    case EPI_GELU_ACT: BIG_LAUNCH(EPI_GELU_ACT, WM_, MF_, NF_, NST_, BKT_, OCC_)          \
+    case EPI_GELU_D: BIG_LAUNCH(EPI_GELU_D, WM_, MF_, NF_, NST_, BKT_, OCC_)              \
+    case EPI_MULAUX: BIG_LAUNCH(EPI_MULAUX, WM_, MF_, NF_, NST_, BKT_, OCC_)              \
+    default: return ES_BAD_ARG;                                                           \
   }
+#define BIG_EPIS(WM_, MF_, NF_, NST_, BKT_) BIG_EPIS2(WM_, MF_, NF_, NST_, BKT_, 1)
 int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   switch (cfg) {
+    case 10: BIG_EPIS2(4, 4, 4, 3, 32, 4)  // 256x128, BK32, 3 stages (72 KiB), two workgroups per CU
     case 6: BIG_EPIS(2, 8, 4, 2, 64)   // 256x256, BK64, 2 stages (128 KiB)
     case 7: BIG_EPIS(2, 8, 3, 2, 64)   // 256x192, BK64, 2 stages (112 KiB)
     case 9: BIG_EPIS(2, 8, 3, 4, 32)   // 256x192, BK32, 4 stages
@@ -995,6 +1003,7 @@ int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) 
   }
 }
 #undef BIG_EPIS
+#undef BIG_EPIS2
 #undef BIG_LAUNCH
 
 }  // namespace es_gemm
@@ -1031,10 +1040,18 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //  * ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
   //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
   //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
+  //  * (variant -1 only; -2 keeps the rules above) the 256 x 128 two-workgroups-per-CU kernel
+  //    (variant 10) for the plain / residual epilogues at F1's long token axis: the qkv and proj
+  //    forwards (K = 384) and the N = 384 data gradients of fc1 / qkv: 0.96-0.97x the time of the
+  //    kernels above at those shapes (scripts/gemm_bench.py, r02d).
   int variant = g_gemm_variant;
+  const bool two_wg = variant == -1;
   if (variant < 0) {
     const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
-    if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
+    const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID;
+    if (two_wg && plain && M >= 65536 && ((K <= 384 && N >= 384) || (K >= 768 && N == 384)))
+      variant = 10;
+    else if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
       variant = M < 32768 ? 0 : 6;
     else if (K >= 768 && N % 256 == 0 && epi != EPI_DGELU)
       variant = 6;
@@ -1064,8 +1081,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
-  if (variant >= 6 && variant <= 9) {
-    const int tbn = (variant == 6 || variant == 8) ? 256 : 192;
+  if (variant >= 6 && variant <= 10) {
+    const int tbn = (variant == 6 || variant == 8) ? 256 : (variant == 10 ? 128 : 192);
     if (N % tbn) return ES_BAD_SHAPE;
     return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
   }
@@ -1079,7 +1096,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 // BK64 2-stage, 1 = 256x128 BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage,
 // 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage; 8 waves, one workgroup per CU, 128x64 or
 // 128x48 per wave: 6 = 256x256 BK64 2-stage, 7 = 256x192 BK64 2-stage, 8 = 256x256 BK32
-// 4-stage, 9 = 256x192 BK32 4-stage; 6/8 need N % 256 == 0, 7/9 N % 192 == 0).
+// 4-stage, 9 = 256x192 BK32 4-stage; 6/8 need N % 256 == 0, 7/9 N % 192 == 0; 10 = 256x128 BK32
+// 3-stage, 64x64 per wave, two workgroups per CU).
 // Returns the previous value.
 int es_set_gemm_variant(int v) {
   const int old = g_gemm_variant;
