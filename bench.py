@@ -345,9 +345,40 @@ def run_secondary(args):
     if world > 1:
         torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
     T = elapsed.item()
+    host = None
+    if args.host_input and args.workload == "c1":
+        # C1 fed by the native host input path: TransformCoMatch's weak / strong_0 / strong_1 views and
+        # the labeled transform on the granted host threads (csrc/host_aug.cpp), uint8 into the engine
+        import numpy as np
+
+        from endossl import host_aug
+        threads, _ = host_cpus()
+        gh = np.random.default_rng(7)
+        base = gh.integers(0, 256, (60, 80, 3), dtype=np.uint8)
+        srcs = [host_aug.resize_bilinear(base ^ np.uint8(i * 29 % 256), (500, 375)) for i in range(64)]
+        lab = host_aug.HostBatcher(srcs, batch=B, size=224, kind="labeled", seed=1, threads=threads, device=dev)
+        ub = host_aug.HostBatcher(srcs, batch=B * MU, size=224, kind="comatch", seed=2, threads=threads, device=dev)
+        yh = torch.randint(0, 23, (B,), device=dev)
+
+        def one():
+            (xh,) = lab.next()
+            return tr.step(((xh, yh), (ub.next(), None)))
+
+        for _ in range(2):
+            one()
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(args.steps):
+            one()
+        torch.cuda.synchronize()
+        hd = time.perf_counter() - h0
+        host = {"value": round(unl * args.steps / hd, 2), "unit": "unlabeled images/s",
+                "ms_per_step": round(hd / args.steps * 1e3, 3), "host_threads": threads,
+                "source": "synthetic decoded RGB 500x375 frames (64), IS_CROP, S=224; decode not timed"}
     if rank == 0:
         ms = T / args.steps * 1e3
-        print(json.dumps({
+        host_line = {"host_input": host} if host is not None else {}
+        print(json.dumps({**{
             "metric": (f"labeled images/sec/node (P0)" if args.workload == "p0" else
                        f"unlabeled images/sec/node ({args.workload.upper()})"),
             "value": round(world * unl * args.steps / T, 2),
@@ -363,7 +394,7 @@ def run_secondary(args):
             "alloc_retries": int(torch.cuda.memory_stats(dev).get("num_alloc_retries", 0)),
             "device_allocs": int(torch.cuda.memory_stats(dev).get("num_device_alloc", 0)),
             "hbm_reserved_peak_gib": round(torch.cuda.max_memory_reserved(dev) / 2**30, 1),
-            "final_loss": round(out["loss"].item(), 6)}), flush=True)
+            "final_loss": round(out["loss"].item(), 6)}, **host_line}), flush=True)
     dist.barrier()
 
 

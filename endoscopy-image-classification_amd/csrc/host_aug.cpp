@@ -83,8 +83,10 @@ std::vector<u8> take_buf(size_t n) {
   return v;
 }
 
+constexpr size_t MAX_CACHED_BYTES = (size_t)4 << 20;  // larger temporaries (huge sources) go back to malloc
+
 void give_buf(std::vector<u8>&& v) {
-  if (!v.capacity()) return;
+  if (!v.capacity() || v.capacity() > MAX_CACHED_BYTES) return;
   std::lock_guard<std::mutex> lk(g_buf_mu);
   if (g_bufs.size() < MAX_CACHED_BUFS) g_bufs.push_back(std::move(v));
 }

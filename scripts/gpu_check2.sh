@@ -15,6 +15,9 @@ ok $rc && { run t 1100 $PT -m gpu -x tests/; rc=$?; }
 ok $rc && { run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; }
 ok $rc && { run bench 600 python bench.py --steps 10 --warmup 3 --host-input; rc=$?; }
 ok $rc && { run hab 300 python scripts/host_aug_bench.py --threads 1,8,16 --n 512; rc=$?; }
+ok $rc && { run c1 300 python bench.py --workload c1 --steps 5 --warmup 2 --host-input; rc=$?; }
+ok $rc && { run s1 400 python bench.py --workload s1 --steps 3 --warmup 2; rc=$?; }
+ok $rc && { run p0 200 python bench.py --workload p0 --steps 10 --warmup 3; rc=$?; }
 if ok $rc && [ "${PROFILE:-1}" = 1 ]; then
   export TMPDIR=/tmp
   run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline; rc=$?
