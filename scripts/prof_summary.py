@@ -29,7 +29,8 @@ tr = os.path.join(src, "run_kernel_trace.csv")
 if os.path.exists(tr):
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in csv.DictReader(open(tr)):
-        m = re.search(r"(gemm_nt\w*<[^>]*>|gemm_tn_kernel|attn_\w+<\d>)", r["Kernel_Name"])
+        m = re.search(r"(gemm_nt\w*<[^>]*>|gemm_tn_kernel|gemm_tn_big_kernel|splitk_reduce_kernel|attn_\w+<\d+>)",
+                      r["Kernel_Name"])
         if not m:
             continue
         k = (m.group(1), int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
@@ -39,5 +40,10 @@ if os.path.exists(tr):
               "|---:|---:|---:|---|---:|"]
     for (n, g), (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
         lines.append(f"| {t / steps / 1e3:.3f} | {c / steps:.1f} | {t / c:.1f} | `{n}` | {g} |")
+    lines += ["", "The bench's roofline site (fc1 weight gradient, N1 x N2 = 1536 x 384 over M = 100,864 tokens) is "
+              "the `gemm_tn_big_kernel` launch of 256 workgroups (8 tiles x 32 splits; the fc2 site has the same "
+              "grid) plus its `splitk_reduce_kernel` of 576 workgroups (1536 x 384 / 4 / 256). Durations under "
+              "the profiler run longer than the bench's live HIP-event figure (lower clocks while profiling, "
+              "MI355X_MICROARCH.md 'DVFS give-back' item 2)."]
 open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines[:20]))
