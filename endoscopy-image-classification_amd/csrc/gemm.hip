@@ -1045,10 +1045,10 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //    forwards (K = 384) and the N = 384 data gradients of fc1 / qkv: 0.96-0.97x the time of the
   //    kernels above at those shapes (scripts/gemm_bench.py, r02d).
   int variant = g_gemm_variant;
-  const bool two_wg = variant == -1;
+  const bool two_wg = variant == -1 || variant == -3;
   if (variant < 0) {
     const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
-    const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID;
+    const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || (variant == -3 && epi == EPI_MULAUX);
     if (two_wg && plain && M >= 65536 && ((K <= 384 && N >= 384) || (K >= 768 && N == 384)))
       variant = 10;
     else if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
