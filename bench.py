@@ -346,9 +346,10 @@ def run_secondary(args):
         torch.distributed.all_reduce(elapsed, op=torch.distributed.ReduceOp.MAX)
     T = elapsed.item()
     host = None
-    if args.host_input and args.workload == "c1":
-        # C1 fed by the native host input path: TransformCoMatch's weak / strong_0 / strong_1 views and
-        # the labeled transform on the granted host threads (csrc/host_aug.cpp), uint8 into the engine
+    if args.host_input and args.workload in ("c1", "s1"):
+        # C1 / S1 fed by the native host input path: TransformCoMatch's weak / strong_0 / strong_1 views
+        # (C1) or TransformFixMatch's weak / strong pair (S1) and the labeled transform on the granted host
+        # threads (csrc/host_aug.cpp), uint8 into the model (normalised on the device)
         import numpy as np
 
         from endossl import host_aug
@@ -356,8 +357,10 @@ def run_secondary(args):
         gh = np.random.default_rng(7)
         base = gh.integers(0, 256, (60, 80, 3), dtype=np.uint8)
         srcs = [host_aug.resize_bilinear(base ^ np.uint8(i * 29 % 256), (500, 375)) for i in range(64)]
-        lab = host_aug.HostBatcher(srcs, batch=B, size=224, kind="labeled", seed=1, threads=threads, device=dev)
-        ub = host_aug.HostBatcher(srcs, batch=B * MU, size=224, kind="comatch", seed=2, threads=threads, device=dev)
+        side = 224 if args.workload == "c1" else S
+        lab = host_aug.HostBatcher(srcs, batch=B, size=side, kind="labeled", seed=1, threads=threads, device=dev)
+        ub = host_aug.HostBatcher(srcs, batch=B * MU, size=side, kind="comatch" if args.workload == "c1" else "fixmatch",
+                                  seed=2, threads=threads, device=dev)
         yh = torch.randint(0, 23, (B,), device=dev)
 
         def one():
@@ -374,7 +377,7 @@ def run_secondary(args):
         hd = time.perf_counter() - h0
         host = {"value": round(unl * args.steps / hd, 2), "unit": "unlabeled images/s",
                 "ms_per_step": round(hd / args.steps * 1e3, 3), "host_threads": threads,
-                "source": "synthetic decoded RGB 500x375 frames (64), IS_CROP, S=224; decode not timed"}
+                "source": f"synthetic decoded RGB 500x375 frames (64), IS_CROP, S={side}; decode not timed"}
     if rank == 0:
         ms = T / args.steps * 1e3
         host_line = {"host_input": host} if host is not None else {}

@@ -1041,14 +1041,15 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
   //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
   //  * (variant -1 only; -2 keeps the rules above) the 256 x 128 two-workgroups-per-CU kernel
-  //    (variant 10) for the plain / residual epilogues at F1's long token axis: the qkv and proj
-  //    forwards (K = 384) and the N = 384 data gradients of fc1 / qkv: 0.96-0.97x the time of the
-  //    kernels above at those shapes (scripts/gemm_bench.py, r02d).
+  //    (variant 10) for the plain / residual / MULAUX epilogues at F1's long token axis: the qkv and
+  //    proj forwards (K = 384), the fc2 data gradient and the N = 384 data gradients of fc1 / qkv:
+  //    0.96-0.97x the time of the kernels above at those shapes (scripts/gemm_bench.py, r02d); F1
+  //    35.41 -> 35.21 ms, and 34.58 -> 34.48 ms with the fc2 data gradient too (same-box A/Bs).
   int variant = g_gemm_variant;
-  const bool two_wg = variant == -1 || variant == -3;
+  const bool two_wg = variant == -1;
   if (variant < 0) {
     const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
-    const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || (variant == -3 && epi == EPI_MULAUX);
+    const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || epi == EPI_MULAUX;
     if (two_wg && plain && M >= 65536 && ((K <= 384 && N >= 384) || (K >= 768 && N == 384)))
       variant = 10;
     else if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)

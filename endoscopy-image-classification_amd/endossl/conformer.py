@@ -31,6 +31,7 @@ import torch.nn as nn
 
 from . import _lib, dist
 from ._lib import call, ptr
+from .vit import IMAGENET_MEAN, IMAGENET_STD
 
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32 = 0, 1, 2, 3, 4
 BN_EPS_BLOCK, BN_EPS_STEM, LN_EPS, LN_EPS_TRANS_NORM = 1e-6, 1e-5, 1e-6, 1e-5
@@ -1017,8 +1018,11 @@ class NativeConformer(nn.Module):
         if x.dim() != 4 or x.shape[1:] != (3, cfg.img_size, cfg.img_size):
             raise ValueError(f"expected [n, 3, {cfg.img_size}, {cfg.img_size}] images, got {tuple(x.shape)}")
         if x.dtype == torch.uint8:
-            raise ValueError("NativeConformer takes ImageNet-normalised fp32 images (code/dataset.py:49-51); the "
-                             "uint8 input path is the ViT engine's")
+            # raw pixels (the host input path's batches): ToTensor + Normalize (code/dataset.py:21-22,49-51)
+            # on the device, the same fp32 operations in the same order as torchvision's on the host
+            mean = torch.tensor(IMAGENET_MEAN, device=x.device).view(1, 3, 1, 1)
+            std = torch.tensor(IMAGENET_STD, device=x.device).view(1, 3, 1, 1)
+            x = x.float().div_(255.0).sub_(mean).div_(std)
         self._pack()
         # a backward that raised after queueing its stream join never ran the callback that clears
         # its key: every new graph starts with no join pending

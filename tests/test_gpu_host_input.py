@@ -79,3 +79,22 @@ def test_fixmatch_step_on_host_batches():
         out = tr.step(((x, y), ((uw, us), None)))
     torch.cuda.synchronize()
     assert torch.isfinite(out["loss"]).item()
+
+
+def test_conformer_uint8_input_equals_host_normalised():
+    """NativeConformer fed raw uint8 pixels (the host input path's batches) normalises them on the
+    device with torchvision's fp32 operations: the same logits as the host-normalised fp32 images."""
+    from endossl.conformer import ConformerConfig, NativeConformer
+    kw = dict(img_size=64, patch=16, base_channel=64, channel_ratio=1, embed_dim=128, depth=3, heads=2, num_classes=23)
+    m = NativeConformer(ConformerConfig(**kw), seed=3).to("cuda")
+    m.eval()
+    srcs = _sources(3)
+    (x8,) = host_aug.transform_batch(srcs, 64, "eval", True, threads=2)
+    mean = torch.tensor(MEAN).view(1, 3, 1, 1)
+    std = torch.tensor(STD).view(1, 3, 1, 1)
+    xf = (x8.float() / 255.0 - mean) / std  # ToTensor + Normalize on the host (code/dataset.py:49-51)
+    with torch.no_grad():
+        a = [t.clone() for t in m(x8.cuda())]
+        b = [t.clone() for t in m(xf.cuda())]
+    torch.cuda.synchronize()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
