@@ -1020,9 +1020,11 @@ class NativeConformer(nn.Module):
         if x.dtype == torch.uint8:
             # raw pixels (the host input path's batches): ToTensor + Normalize (code/dataset.py:21-22,49-51)
             # on the device, the same fp32 operations in the same order as torchvision's on the host
+            # (divisors as device tensors: torch divides by a Python scalar as a multiply by its
+            # reciprocal on the GPU, which is not the host's x / 255 to the last bit)
             mean = torch.tensor(IMAGENET_MEAN, device=x.device).view(1, 3, 1, 1)
             std = torch.tensor(IMAGENET_STD, device=x.device).view(1, 3, 1, 1)
-            x = x.float().div_(255.0).sub_(mean).div_(std)
+            x = x.float().div_(torch.tensor(255.0, device=x.device)).sub_(mean).div_(std)
         self._pack()
         # a backward that raised after queueing its stream join never ran the callback that clears
         # its key: every new graph starts with no join pending
