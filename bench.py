@@ -550,6 +550,7 @@ def main():
     flop = sum(f for _, _, f in probe["events"]) / len(ev_ms)  # per launch (uniform at the fc1 site)
     tflops = sum(f for _, _, f in probe["events"]) / (sum(ev_ms) / 1e3) / 1e12
     M_tok = B * (1 + MU) * 197
+    share = (Engine.TN_SHARE if (ov[0] and not grouped and Engine.TN_SHARE < 1.0 and M_tok >= 65536) else 1.0)
     traffic = None if grouped else pmc_traffic("gemm_tn")
     lib = __import__("endossl._lib", fromlist=["load"]).load()
     tn_ws = lib.es_gemm_tn_workspace(1536, 384, 0)
@@ -593,6 +594,11 @@ def main():
                          "timed": "live in the timed steps" if live else "2 untimed eager steps after the timed "
                                                                          "(graph-replayed) steps",
                          "streams": 2 if ov[0] else 1, "tn_workspace_floats": int(tn_ws),
+                         "cu_share": share,
+                         "frac_of_share": round(tflops / (PEAK_BF16_TFLOPS * share), 4),
+                         "share_note": ("the live launch is sized to this share of the CUs (Engine.TN_SHARE: "
+                                        "the rest run the data-gradient chain beside it); frac is against the "
+                                        "whole chip's peak, frac_of_share against the granted CUs' peak"),
                          "isolated": {"mean_launch_ms": round(iso_ms, 4),
                                       "achieved": round(iso_tflops, 1),
                                       "frac": round(iso_tflops / PEAK_BF16_TFLOPS, 4),

@@ -231,6 +231,11 @@ class Engine:
     # slabs stay small for the 384x384 projection.
     TN_TARGET_SET = "ENDOSSL_TN_TARGET" in os.environ
     TN_TARGET_BLOCKS = int(os.environ.get("ENDOSSL_TN_TARGET", "768"))
+    # share of the CUs the overlapped long-axis weight-gradient launches are sized to (1 = the whole
+    # chip, the library's sizing).  Half: the 384 x 192 tile's 147-KiB workgroups otherwise hold every
+    # CU's LDS and the data-gradient chain's launches wait for CUs; F1 34.43 / 34.36 -> 33.66 / 33.84
+    # ms (same-box A/B, 0.375 of the CUs: 35.03 / 35.11)
+    TN_SHARE = float(os.environ.get("ENDOSSL_TN_SHARE", "0.5"))
     TN_CEIL = os.environ.get("ENDOSSL_TN_CEIL", "0") == "1"  # A/B knob: the earlier ceil sizing
     TN_MAX_SPLITS = 128
     # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
@@ -311,6 +316,7 @@ class Engine:
         self._ws = None
         self._ws_ln = None
         self._side = None
+        self._ncu = None
         self._lane_state = {}
         self._grad_b = None
         self.overlap = self.OVERLAP
@@ -543,8 +549,16 @@ class Engine:
     # -------------------------------------------------------------- backward
     def _tn_splits(self, M, N1, N2):
         """0 = the library's automatic split-K sizing for the kernel it picks (es_gemm_tn); with
-        ENDOSSL_TN_TARGET set, floor(target / 128x128 tiles) splits (the round-1 sizing)."""
+        ENDOSSL_TN_TARGET set, floor(target / 128x128 tiles) splits (the round-1 sizing).  With the
+        weight gradients overlapped on the side stream and TN_SHARE < 1, the 384 x 192 tile's launches
+        are sized to that share of the CUs (the rest stay free for the data-gradient chain)."""
         if not self.TN_TARGET_SET:
+            if (self.TN_SHARE < 1.0 and self.overlap and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0
+                    and self.precision == "bf16"):
+                if self._ncu is None:
+                    self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+                tiles = (N1 // 384) * (N2 // 192)
+                return max(1, int(self._ncu * self.TN_SHARE) // tiles)
             return 0
         tiles = (N1 // 128) * (N2 // 128)
         msteps = (M + 31) // 32
