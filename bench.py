@@ -550,7 +550,7 @@ def main():
     flop = sum(f for _, _, f in probe["events"]) / len(ev_ms)  # per launch (uniform at the fc1 site)
     tflops = sum(f for _, _, f in probe["events"]) / (sum(ev_ms) / 1e3) / 1e12
     M_tok = B * (1 + MU) * 197
-    share = (Engine.TN_SHARE if (ov[0] and not grouped and Engine.TN_SHARE < 1.0 and M_tok >= 65536) else 1.0)
+    share = (Engine.TN_SHARE if (ov[0] and not grouped and Engine.TN_SHARE < 1.0 and M_tok >= 16384) else 1.0)
     traffic = None if grouped else pmc_traffic("gemm_tn")
     lib = __import__("endossl._lib", fromlist=["load"]).load()
     tn_ws = lib.es_gemm_tn_workspace(1536, 384, 0)

@@ -553,8 +553,7 @@ class Engine:
         weight gradients overlapped on the side stream and TN_SHARE < 1, the 384 x 192 tile's launches
         are sized to that share of the CUs (the rest stay free for the data-gradient chain)."""
         if not self.TN_TARGET_SET:
-            if (self.TN_SHARE < 1.0 and self.overlap and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0
-                    and self.precision == "bf16"):
+            if self._tn_shared(M, N1, N2):
                 if self._ncu is None:
                     self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
                 tiles = (N1 // 384) * (N2 // 192)
@@ -564,6 +563,14 @@ class Engine:
         msteps = (M + 31) // 32
         sp = -(-self.TN_TARGET_BLOCKS // tiles) if self.TN_CEIL else self.TN_TARGET_BLOCKS // tiles
         return max(1, min(msteps, self.TN_MAX_SPLITS, sp))
+
+    def _tn_shared(self, M, N1, N2):
+        """The overlapped weight gradient on the 384 x 192 tile sized to TN_SHARE of the CUs: from the
+        F1 batch down to a rank's share at N = 4 (M = 25,216 tokens; the library alone picks that tile
+        from M = 65,536).  Same-box A/Bs: N = 2 shard 19.01-19.26 -> 18.15-18.32 ms, N = 4 shard
+        10.07-10.09 -> 9.73-9.74 ms (the whole-chip big tile: 18.80-18.96 / 10.25-10.27)."""
+        return (self.TN_SHARE < 1.0 and self.overlap and M >= 16384 and N1 % 384 == 0 and N2 % 192 == 0
+                and self.precision == "bf16")
 
     def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0, ld1=None, ld2=None, label=None):
         """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy (row strides ld1 / ld2,
@@ -575,6 +582,20 @@ class Engine:
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
         args = (ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
                 _lib.stream())
+        if splits and not self.TN_TARGET_SET and self._tn_shared(M, N1, N2):
+            lib = _lib.load()
+            old = lib.es_set_tn_variant(7)  # the 384 x 192 tile (unless an A/B run pinned a variant)
+            if old != -1:
+                lib.es_set_tn_variant(old)
+            try:
+                self._wgrad_launch(args, M, N1, N2, label)
+            finally:
+                if old == -1:
+                    lib.es_set_tn_variant(-1)
+            return
+        self._wgrad_launch(args, M, N1, N2, label)
+
+    def _wgrad_launch(self, args, M, N1, N2, label):
         pr = self.probe
         if pr is not None and label is not None and pr["label"] == label:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
