@@ -31,7 +31,7 @@ import torch.nn as nn
 
 from . import _lib, dist
 from ._lib import call, ptr
-from .vit import IMAGENET_MEAN, IMAGENET_STD, Engine
+from .vit import IMAGENET_MEAN, IMAGENET_STD
 
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32 = 0, 1, 2, 3, 4
 BN_EPS_BLOCK, BN_EPS_STEM, LN_EPS, LN_EPS_TRANS_NORM = 1e-6, 1e-5, 1e-6, 1e-5
@@ -249,6 +249,11 @@ class _Map:
     def nhwc(t):
         N, H, W, C = t.shape
         return _Map(t, N, H, W, C)
+
+
+# share of the CUs the transformer blocks' overlapped weight gradients are sized to (Engine.TN_SHARE's
+# counterpart; 1 = the library's whole-chip sizing, kept until measured at S1)
+CONF_TN_SHARE = float(os.environ.get("ENDOSSL_CONF_TN_SHARE", "1.0"))
 
 
 def _tn_splits(M, N1, N2):
@@ -702,10 +707,10 @@ class _BlockFn(torch.autograd.Function):
 
         def wgrad(dy, N1, x, N2, wname, bname):
             sp = _tn_splits(M, N1, N2)
-            if side is not None and Engine.TN_SHARE < 1.0 and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
-                # beside the branch streams: the 384 x 192 tile on a share of the CUs (Engine.TN_SHARE)
+            if side is not None and CONF_TN_SHARE < 1.0 and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
+                # beside the branch streams: the 384 x 192 tile on a share of the CUs (as Engine.TN_SHARE)
                 ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-                sp = max(1, int(ncu * Engine.TN_SHARE) // ((N1 // 384) * (N2 // 192)))
+                sp = max(1, int(ncu * CONF_TN_SHARE) // ((N1 // 384) * (N2 // 192)))
             if side is not None:
                 side.wait_stream(main)
             with torch.cuda.stream(side) if side is not None else _nullctx():
