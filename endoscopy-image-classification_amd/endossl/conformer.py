@@ -252,8 +252,8 @@ class _Map:
 
 
 # share of the CUs the transformer blocks' overlapped weight gradients are sized to (Engine.TN_SHARE's
-# counterpart; 1 = the library's whole-chip sizing, kept until measured at S1)
-CONF_TN_SHARE = float(os.environ.get("ENDOSSL_CONF_TN_SHARE", "1.0"))
+# counterpart; 1 = the library's whole-chip sizing): S1 195.46 / 195.46 -> 193.26 / 193.38 ms same-box A/B)
+CONF_TN_SHARE = float(os.environ.get("ENDOSSL_CONF_TN_SHARE", "0.5"))
 
 
 def _tn_splits(M, N1, N2):
