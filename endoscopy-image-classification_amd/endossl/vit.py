@@ -236,6 +236,7 @@ class Engine:
     # CU's LDS and the data-gradient chain's launches wait for CUs; F1 34.43 / 34.36 -> 33.66 / 33.84
     # ms (same-box A/B, 0.375 of the CUs: 35.03 / 35.11)
     TN_SHARE = float(os.environ.get("ENDOSSL_TN_SHARE", "0.5"))
+    TN_SHARE_MIN_M = int(os.environ.get("ENDOSSL_TN_SHARE_MIN_M", "16384"))  # shortest token axis it applies to
     TN_CEIL = os.environ.get("ENDOSSL_TN_CEIL", "0") == "1"  # A/B knob: the earlier ceil sizing
     TN_MAX_SPLITS = 128
     # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
@@ -569,8 +570,8 @@ class Engine:
         F1 batch down to a rank's share at N = 4 (M = 25,216 tokens; the library alone picks that tile
         from M = 65,536).  Same-box A/Bs: N = 2 shard 19.01-19.26 -> 18.15-18.32 ms, N = 4 shard
         10.07-10.09 -> 9.73-9.74 ms (the whole-chip big tile: 18.80-18.96 / 10.25-10.27)."""
-        return (self.TN_SHARE < 1.0 and self.overlap and M >= 16384 and N1 % 384 == 0 and N2 % 192 == 0
-                and self.precision == "bf16")
+        return (self.TN_SHARE < 1.0 and self.overlap and M >= self.TN_SHARE_MIN_M and N1 % 384 == 0
+                and N2 % 192 == 0 and self.precision == "bf16")
 
     def _wgrad(self, dy, N1, x, N2, M, out, bias_out=None, lane=0, ld1=None, ld2=None, label=None):
         """out = dy^T x (weight grad) and, fused, bias_out = column sums of dy (row strides ld1 / ld2,
