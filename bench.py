@@ -401,6 +401,33 @@ def run_secondary(args):
     dist.barrier()
 
 
+def launcher_cmd(argv, nproc, port, script=None):
+    """The torch.distributed.run command that runs this script once per GPU (one rank per GPU, RCCL
+    over xGMI), with the same arguments, and the environment it needs."""
+    script = script or os.path.abspath(__file__)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    return cmd, env
+
+
+def _self_launch(args, argv):
+    """`python bench.py --gpus N` (N > 1) with no WORLD_SIZE in the environment: start the N ranks as
+    ONE child process (torch.distributed.run) before anything touches the GPU, let rank 0's JSON line
+    pass through on the shared stdout, and exit with the child's status (no exec)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd, env = launcher_cmd(argv, args.gpus, port)
+    print(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
+
+
 def _check_world(args, world):
     if args.gpus != world:
         raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 under "
@@ -429,9 +456,11 @@ def main():
                          "frames, pinned uint8 batches copied on a side stream); reported as 'host_input', "
                          "never as value")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
-                    help="hipGraph replay of the step's forward/backward (auto: on for N > 1; at N = 1 the "
-                         "timed steps run eagerly so the roofline probe's HIP events see every launch)")
+                    help="hipGraph replay of the step's forward/backward (on); auto = off = eager launches "
+                         "(measured faster than the replay at N = 1 and at the N = 8 shard, DESIGN.md §5)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_self_launch(args, sys.argv[1:]))
     if args.workload != "f1":
         return run_secondary(args)
 
@@ -452,8 +481,8 @@ def main():
         B, MU = args.batch, args.mu
     model = NativeViT(ViTConfig(), seed=0)
     tr = FixMatch(model, device=dev)
-    # eager by default: the captured-graph replay measured slower than eager launches at both the
-    # per-rank shard of N = 8 (B = 8: 7.11 vs 6.40 ms/step) and the full batch (r02)
+    # eager by default ("auto" = "off"): the captured-graph replay measured slower than eager launches
+    # at both the per-rank shard of N = 8 (B = 8: 7.11 vs 6.40 ms/step) and the full batch (r02)
     graph = args.graph == "on"
     tr.use_graph = graph
     cfg = AttrDict(DATA=AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=224, TARGET_NAME="target"),
@@ -540,6 +569,28 @@ def main():
                 "ms_per_step": round(we.item() / args.steps * 1e3, 3),
                 "note": "same step with every rank on a full B=64, mu=7 batch (DDP weak scaling)"}
         del xw, yw, bw
+    ar_overlap = None
+    if world > 1:
+        # the same step with the gradient all-reduce bucketed per block and overlapped with the reverse pass
+        # (FixMatch.overlap_allreduce / dist.GradBuckets, opt-in) -- reported beside the headline, which runs
+        # the default single post-backward all-reduce, so one multi-GPU run measures both forms
+        prev_ov, tr.overlap_allreduce = tr.overlap_allreduce, not tr.overlap_allreduce
+        for _ in range(2):
+            tr.step(batch)
+        torch.cuda.synchronize()
+        dist.barrier()
+        a0 = time.perf_counter()
+        for _ in range(args.steps):
+            tr.step(batch)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ae = torch.tensor([time.perf_counter() - a0], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(ae, op=torch.distributed.ReduceOp.MAX)
+        tr.overlap_allreduce = prev_ov
+        ar_overlap = {"overlap_allreduce": not prev_ov, "value": round(world * B * MU * args.steps / ae.item(), 2),
+                      "ms_per_step": round(ae.item() / args.steps * 1e3, 3),
+                      "note": "same step and batch with the other all-reduce form (per-block buckets overlapped "
+                              "with the backward vs one all-reduce after it)"}
     host_input = host_input_run(tr, B, MU, args.steps, dev) if args.host_input else None
     iso_ms = sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / len(iso["events"])
     iso_tflops = (sum(f for _, _, f in iso["events"]) / (sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / 1e3)
@@ -607,6 +658,9 @@ def main():
         }
         if weak is not None:
             res["weak_scaling"] = weak
+        if ar_overlap is not None:
+            res["allreduce_form"] = "overlapped per-block buckets" if tr.overlap_allreduce else "one after the backward"
+            res["allreduce_other_form"] = ar_overlap
         if host_input is not None:
             res["host_input"] = host_input
         if world == 1 and not args.no_cpu_baseline:

@@ -1016,6 +1016,9 @@ static int g_tn_variant = -1;
 
 extern "C" {
 
+int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
+                  float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream);
+
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C,
                int ldc, void* C2, const void* aux, int ldaux, int M, int N, int K, int np,
                hipStream_t stream) {
@@ -1128,8 +1131,7 @@ constexpr int TN_MIN_SPLIT_TOKENS = 512;
 static bool tn_big_ok(int N1, int N2, int ld1, int ld2) {
   return N1 % TB1 == 0 && N2 % TB2 == 0 && ld1 % 8 == 0 && ld2 % 8 == 0;
 }
-static int tn_pick(int M, int N1, int N2, int ld1, int ld2) {
-  const int v = g_tn_variant;
+static int tn_pick(int M, int N1, int N2, int ld1, int ld2, int v) {
   if (!(N1 % BM == 0 && N2 % BN == 0)) return 7;  // only the big tile covers N2 = 192 (caller checked)
   if (v >= 5 && v <= 8) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
   if (v >= 0) return v;
@@ -1155,12 +1157,21 @@ size_t es_gemm_tn_workspace(int N1, int N2, int splits) {
 
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream) {
+  return es_gemm_tn_ex(A1, ld1, A2, ld2, M, N1, N2, splits, workspace, out, accumulate, bias_out, -1, stream);
+}
+
+// es_gemm_tn with the kernel chosen by the caller (variant >= 0, as es_set_tn_variant; shapes the
+// chosen tile does not cover fall back as there) instead of the process-wide knob (variant -1):
+// no global state changes, so concurrent launchers never see each other's choice.
+int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
+                  float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream) {
   if (M <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!tn_big_ok(N1, N2, ld1, ld2) && ((N1 % BM) || (N2 % BN))) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
+  if (variant > 8) return ES_BAD_ARG;
   // variant: 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3;
   // 5..7 = 384x192 tile with 32x2 (72 KiB: two workgroups per CU), 32x3, 64x2
-  const int v = tn_pick(M, N1, N2, ld1, ld2);
+  const int v = tn_pick(M, N1, N2, ld1, ld2, variant >= 0 ? variant : g_tn_variant);
   const int BKM = (v == 3 || v == 4 || v == 7) ? 64 : 32;  // (8: 384x192, 32x4)
   const int msteps = (M + BKM - 1) / BKM;
   if (splits <= 0) splits = tn_auto_splits(v, M, N1, N2);

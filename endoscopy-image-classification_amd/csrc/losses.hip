@@ -118,16 +118,18 @@ __global__ __launch_bounds__(256) void poly_ce_kernel(const float* __restrict__ 
 // (code/loss.py:118, the SemiFormer heads' loss, code/semiformer.py:125-126); one workgroup.
 __global__ __launch_bounds__(256) void ce_weighted_kernel(const float* __restrict__ l, int ldl,
                                                           const int64_t* __restrict__ y, const float* __restrict__ w,
-                                                          int n, int C, float grad_scale, float* __restrict__ dl,
-                                                          int lddl, float* __restrict__ out) {
+                                                          const float* __restrict__ wsum_global, int n, int C,
+                                                          float grad_scale, float* __restrict__ dl, int lddl,
+                                                          float* __restrict__ out) {
   __shared__ float red[16];
   float ws = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int yi = (int)y[i];
     ws += (unsigned)yi >= (unsigned)C ? __int_as_float(0x7fc00000) : (w ? w[yi] : 1.f);
   }
-  const float W = block_sum(ws, red);
+  float W = block_sum(ws, red);
   __syncthreads();
+  if (wsum_global) W = *wsum_global;  // the whole batch's weight sum over every rank (data-parallel step)
   const float invW = 1.0f / W;
   float sum = 0.f;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -154,6 +156,18 @@ __global__ __launch_bounds__(256) void ce_weighted_kernel(const float* __restric
   if (threadIdx.x == 0) out[0] = sum * invW;
 }
 
+__global__ __launch_bounds__(256) void ce_weight_sum_kernel(const int64_t* __restrict__ y, const float* __restrict__ w,
+                                                            int n, int C, float* __restrict__ out) {
+  __shared__ float red[16];
+  float ws = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int yi = (int)y[i];
+    ws += (unsigned)yi >= (unsigned)C ? __int_as_float(0x7fc00000) : (w ? w[yi] : 1.f);
+  }
+  ws = block_sum(ws, red);
+  if (threadIdx.x == 0) out[0] = ws;
+}
+
 }  // namespace
 
 extern "C" {
@@ -163,8 +177,29 @@ int es_ce_weighted_fwd_bwd(const float* logits, int ldl, const int64_t* targets,
                            float grad_scale, float* dlogits, int lddl, float* out, hipStream_t stream) {
   if (n <= 0 || C <= 0) return ES_BAD_SHAPE;
   if (!logits || !targets || !dlogits || !out) return ES_BAD_ARG;
-  hipLaunchKernelGGL(ce_weighted_kernel, 1, 256, 0, stream, logits, ldl, targets, weights, n, C, grad_scale, dlogits,
-                     lddl, out);
+  hipLaunchKernelGGL(ce_weighted_kernel, 1, 256, 0, stream, logits, ldl, targets, weights, nullptr, n, C, grad_scale,
+                     dlogits, lddl, out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// out[0] = sum_i w[y_i] (the local weight sum of the weighted mean; weights nullable -> n)
+int es_ce_weight_sum(const int64_t* targets, const float* weights, int n, int C, float* out, hipStream_t stream) {
+  if (n <= 0 || C <= 0) return ES_BAD_SHAPE;
+  if (!targets || !out) return ES_BAD_ARG;
+  hipLaunchKernelGGL(ce_weight_sum_kernel, 1, 256, 0, stream, targets, weights, n, C, out);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// The data-parallel form: the rows are this rank's shard, *wsum_global the weight sum over every
+// rank's rows (es_ce_weight_sum + a SUM all-reduce), so out[0] = this shard's share of the global
+// weighted mean, sum_{i in shard} w l_i / W_global, and dl = grad_scale * d(out[0])/d logits.
+int es_ce_weighted_fwd_bwd_global(const float* logits, int ldl, const int64_t* targets, const float* weights,
+                                  const float* wsum_global, int n, int C, float grad_scale, float* dlogits, int lddl,
+                                  float* out, hipStream_t stream) {
+  if (n <= 0 || C <= 0) return ES_BAD_SHAPE;
+  if (!logits || !targets || !dlogits || !out || !wsum_global) return ES_BAD_ARG;
+  hipLaunchKernelGGL(ce_weighted_kernel, 1, 256, 0, stream, logits, ldl, targets, weights, wsum_global, n, C,
+                     grad_scale, dlogits, lddl, out);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -22,6 +22,7 @@ SIGNATURES = {
     "es_set_gemm_variant": (I, [I]),
     "es_gemm_tn_workspace": (Z, [I, I, I]),
     "es_gemm_tn": (I, [V, I, V, I, I, I, I, I, V, V, I, V, V]),
+    "es_gemm_tn_ex": (I, [V, I, V, I, I, I, I, I, V, V, I, V, I, V]),
     "es_set_tn_variant": (I, [I]),
     "es_set_attn_variant": (I, [I]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),
@@ -108,6 +109,8 @@ SIGNATURES = {
     "es_fcu_down_tokens_bwd": (I, [V, V, V, V, V, V, V, V, V, V, I, I, I, I, V, V]),
     "es_tokens_cls_set": (I, [V, I, I, I, V, V]),
     "es_ce_weighted_fwd_bwd": (I, [V, I, V, V, I, I, F, V, I, V, V]),
+    "es_ce_weight_sum": (I, [V, V, I, I, V, V]),
+    "es_ce_weighted_fwd_bwd_global": (I, [V, I, V, V, V, I, I, F, V, I, V, V]),
     "es_adam_ema_step": (I, [V, V, V, V, V, L, F, F, F, F, F, F, F, F, V]),
     "es_ema_entry_size": (I, []),
     "es_ema_update_multi": (I, [V, V, I, F, F, V]),

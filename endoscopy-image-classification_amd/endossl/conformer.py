@@ -324,8 +324,11 @@ class _ConvFn(torch.autograd.Function):
         args = (xmap.p(), xmap.N, xmap.H, xmap.W, xmap.C, xmap.sn, xmap.sh, xmap.sw, xmap.sc)
         tail = (ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout, Wo * Cout, Cout, 0,
                 _s())
-        if b16 and stats and m.training and BN_STATS_FUSED:
-            # the BatchNorm that follows takes its batch statistics from these per-block partials
+        if b16 and stats and m.training and BN_STATS_FUSED and not (getattr(m, "sync_bn", True)
+                                                                    and dist.world_size() > 1):
+            # the BatchNorm that follows takes its batch statistics from these per-block partials (one
+            # rank's rows only: a SyncBatchNorm at N > 1 sums global statistics itself, _BNFn, so the
+            # partials are requested only when they will be consumed)
             lib = _lib.load()
             part = torch.empty(lib.es_conv2d_bnstats_size(xmap.N * Ho * Wo, Cout), device=x.device)
             call("es_conv2d_fwd_bf16_bnstats", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail[:-2],

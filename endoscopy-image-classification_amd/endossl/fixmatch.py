@@ -100,7 +100,9 @@ class FixMatch:
     # per GPU at N = 8).  Captured on the first step of a shape after one eager step; inputs are
     # copied into the graph's own static buffers (static_batch() hands them out for zero-copy use).
     # The optimizer, the all-reduce and the LR schedule stay outside (their scalars change per step).
-    # ENDOSSL_GRAPH=0 runs everything eagerly.
+    # Off by default (eager launches measured faster); ENDOSSL_GRAPH=1 turns capture on.
+    # The grouped weight-gradient launches of a small shard (Engine.GROUP_WGRAD) are captured too: their
+    # device-side problem tables are uploaded by the eager step and only read inside the graph.
     use_graph = os.environ.get("ENDOSSL_GRAPH", "0") == "1"
 
     def _compute(self, inputs_x, targets_x, inputs_u_w, inputs_u_s):

@@ -87,3 +87,31 @@ def consistency_loss(logits_w, logits_s, name='ce', T=1.0, p_cutoff=0.0, use_har
 def consistency_loss_full(logits_w, logits_s, p_cutoff):
     """Same as consistency_loss, also returning int32 pseudo-labels and the uint8 mask."""
     return _Consistency.apply(logits_w, logits_s, p_cutoff)
+
+
+def weighted_ce_fwd_bwd(logits, targets, weights, dlogits, out):
+    """F.cross_entropy(logits, y, weight=w, reduction='mean') = sum_i w[y_i] l_i / sum_i w[y_i]
+    (code/loss.py:118: the supervised step, code/supervised.py:127-130, and the SemiFormer heads,
+    code/semiformer.py:125-126): out[0] and dlogits = d(out[0])/d(logits) in one launch.
+
+    Data-parallel (world > 1) with class weights, the rows are this rank's shard of the global batch:
+    the denominator is the weight sum over EVERY rank's rows (es_ce_weight_sum + one SUM all-reduce of
+    a float, no host sync), so the rank writes its share sum_{own} w l / W_global and the gradient of
+    that share times `world`; the optimizer's SUM all-reduce of the flat gradient times 1/world then
+    yields d(global weighted mean) -- what the single-process reference computes over the whole batch.
+    A per-rank weighted mean would instead average sum_r W_r-normalised means, which differs whenever
+    the shards' weight sums differ.  out[0] is all-reduced too, so every rank logs the global loss.
+    Without weights the shards are equal-sized plain means and the DDP average is already exact."""
+    from . import dist
+    n, C = logits.shape
+    world = dist.world_size()
+    if weights is None or world == 1:
+        call("es_ce_weighted_fwd_bwd", ptr(logits), C, ptr(targets), ptr(weights), n, C, 1.0, ptr(dlogits), C, ptr(out),
+             _lib.stream())
+        return
+    wsum = torch.empty(1, dtype=torch.float32, device=logits.device)
+    call("es_ce_weight_sum", ptr(targets), ptr(weights), n, C, ptr(wsum), _lib.stream())
+    dist.allreduce_inplace_(wsum)
+    call("es_ce_weighted_fwd_bwd_global", ptr(logits), C, ptr(targets), ptr(weights), ptr(wsum), n, C, float(world),
+         ptr(dlogits), C, ptr(out), _lib.stream())
+    dist.allreduce_inplace_(out[:1])

@@ -24,6 +24,7 @@ from .conformer import join_wgrad_stream
 from ._lib import call, ptr
 from .ema import ModelEMA
 from .fixmatch import _next
+from .loss import weighted_ce_fwd_bwd
 from .lr_scheduler import build_scheduler
 from .optimizer import build_optimizer
 from .throttle import StepThrottle
@@ -74,9 +75,7 @@ class SemiFormer:
 
     # ------------------------------------------------------------------ steps
     def _ce(self, logits, y, dl, out):
-        n, C = logits.shape
-        call("es_ce_weighted_fwd_bwd", ptr(logits), C, ptr(y), ptr(self.class_weights), n, C, 1.0, ptr(dl), C,
-             ptr(out), _lib.stream())
+        weighted_ce_fwd_bwd(logits, y, self.class_weights, dl, out)
 
     def _finish(self, out_conv, out_trans, dconv, dtrans):
         self.optimizer.zero_grad()

@@ -24,6 +24,7 @@ from . import _lib, dist
 from ._lib import call, ptr
 from .conformer import join_wgrad_stream
 from .ema import ModelEMA
+from .loss import weighted_ce_fwd_bwd
 from .lr_scheduler import build_scheduler
 from .optimizer import build_optimizer
 from .throttle import StepThrottle
@@ -77,11 +78,9 @@ class SupLearning:
         targets = targets.to(dev, non_blocking=True).to(torch.int64).contiguous()
         self.model.train()
         logits = self.model(images.to(dev, non_blocking=True))
-        n, C = logits.shape
         stats = torch.zeros(1, dtype=torch.float32, device=dev)
         dl = torch.empty_like(logits)
-        call("es_ce_weighted_fwd_bwd", ptr(logits.detach()), C, ptr(targets), ptr(self.class_weights), n, C, 1.0,
-             ptr(dl), C, ptr(stats), _lib.stream())
+        weighted_ce_fwd_bwd(logits.detach(), targets, self.class_weights, dl, stats)
         self.optimizer.zero_grad()
         torch.autograd.backward([logits], [dl])
         join_wgrad_stream(dev)

@@ -70,10 +70,34 @@ def count_parameters(model):
     return sum(p.numel() for p in model.parameters() if p.requires_grad)
 
 
+def sen_spec(pred, target, num_classes):
+    """Per-class sensitivity / specificity (code/utils.py:41-46): class l's one-vs-rest problem
+    (target == l, pred == l) through precision_recall_fscore_support(average=None); the recall of
+    the positive label is the sensitivity, that of the negative label the specificity.  labels=
+    [False, True] is passed explicitly: the reference's call infers the labels, so a class absent
+    from both target and pred yields one label and its recall[1] raises IndexError; here that class
+    reads sensitivity 0, specificity 1."""
+    import pandas as pd
+    from sklearn.metrics import precision_recall_fscore_support
+    pred, target = np.asarray(pred), np.asarray(target)
+    rows = []
+    for c in range(num_classes):
+        _, recall, _, _ = precision_recall_fscore_support(target == c, pred == c, labels=[False, True], average=None,
+                                                          zero_division=0)
+        rows.append([c, recall[1], recall[0]])
+    return pd.DataFrame(rows, columns=["class", "sensitivity", "specificity"])
+
+
 def calculate_metrics(pred, target, config=None):
-    """Micro/macro P/R/F1 (code/utils.py:38-55); host-side, evaluation only."""
+    """Micro/macro P/R/F1 and the per-class sensitivity / specificity table (code/utils.py:38-55);
+    host-side, evaluation only.  config.MODEL.NUM_CLASSES sets the table's classes (config None:
+    max label + 1)."""
     from sklearn.metrics import f1_score, precision_score, recall_score
     pred, target = np.asarray(pred), np.asarray(target)
+    try:
+        ncls = int(config.MODEL.NUM_CLASSES)
+    except (AttributeError, KeyError, TypeError):
+        ncls = int(max(pred.max(initial=-1), target.max(initial=-1))) + 1
     return {
         "micro/precision": precision_score(target, pred, average="micro", zero_division=0),
         "micro/recall": recall_score(target, pred, average="micro", zero_division=0),
@@ -81,6 +105,7 @@ def calculate_metrics(pred, target, config=None):
         "macro/precision": precision_score(target, pred, average="macro", zero_division=0),
         "macro/recall": recall_score(target, pred, average="macro", zero_division=0),
         "macro/f1": f1_score(target, pred, average="macro", zero_division=0),
+        "sen/spec": sen_spec(pred, target, ncls),
     }
 
 

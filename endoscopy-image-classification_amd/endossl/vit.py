@@ -347,6 +347,12 @@ class Engine:
         self._nmat = len(mats)
         # optional live timing of one launch site: {"label": str, "events": [(start, end, flops)]}
         self.probe = None
+        # optional test hook (tests/test_gpu_blocks.py, teacher-forced per-block parity): called as
+        # capture(kind, train, layer, *tensors) on the launch stream with the engine's own buffers --
+        # "fwd" (block input, block output), "fwd_cls" (input, compact CLS-row output of the pruned last
+        # block), "dtop" (d loss / d final-block output: compact CLS rows or full token rows), "bwd"
+        # (d loss / d block input, after the block's reverse pass); the callee clones what it keeps
+        self.capture = None
 
     def _call(self, name, *args):
         """C-ABI call; in parity mode the fp32 form of the entry point."""
@@ -484,6 +490,8 @@ class Engine:
                      s)
             if prune and i == cfg.depth - 1:
                 self._last_block_cls_fwd(flat, A, b, li, xin, n, train, s)
+                if self.capture is not None:
+                    self.capture("fwd_cls", train, i, xin[:M], A.c_xout[:n])
                 break
             self._call("es_attn_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.o[li]), D, ptr(A.lse[li]), n, T, H, 64 ** -0.5, s)
             self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
@@ -495,6 +503,8 @@ class Engine:
                 self._call("es_mlp_fwd_infer", ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]),
                      ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(self._w2c[i]),
                      ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xmid), D, ptr(xout), D, M, D, Hd, s)
+                if self.capture is not None:
+                    self.capture("fwd", train, i, xin[:M], xout[:M])
                 continue
             if train:
                 self._gemm("fc1_fwd", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(h2), D,
@@ -507,6 +517,8 @@ class Engine:
                            s)
             self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.act[li]), Hd, ptr(self.wb[b + "mlp.fc2.weight"]), Hd,
                  ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xout), D, None, ptr(xmid), D, M, D, Hd, 0, s)
+            if self.capture is not None:
+                self.capture("fwd", train, i, xin[:M], xout[:M])
         xl = A.x[cfg.depth] if train else A.x[cfg.depth & 1]
         Tl = T  # row stride of the CLS tokens in xl, in tokens
         if prune:
@@ -581,31 +593,29 @@ class Engine:
         need = getattr(_lib.load(), "es_gemm_tn_f32_workspace" if self.precision == "fp32" else "es_gemm_tn_workspace")
         if need(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
-        args = (ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out),
-                _lib.stream())
-        if splits and not self.TN_TARGET_SET and self._tn_shared(M, N1, N2):
-            lib = _lib.load()
-            old = lib.es_set_tn_variant(7)  # the 384 x 192 tile (unless an A/B run pinned a variant)
-            if old != -1:
-                lib.es_set_tn_variant(old)
-            try:
-                self._wgrad_launch(args, M, N1, N2, label)
-            finally:
-                if old == -1:
-                    lib.es_set_tn_variant(-1)
-            return
-        self._wgrad_launch(args, M, N1, N2, label)
+        # the CU-share-sized launches name the 384 x 192 tile explicitly (es_gemm_tn_ex); an A/B pin of
+        # the process-wide knob (ENDOSSL_TN_VARIANT) still wins, as before
+        variant = -1
+        if (splits and not self.TN_TARGET_SET and self._tn_shared(M, N1, N2)
+                and not os.environ.get("ENDOSSL_TN_VARIANT")):
+            variant = 7
+        args = (ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out))
+        self._wgrad_launch(args, variant, M, N1, N2, label)
 
-    def _wgrad_launch(self, args, M, N1, N2, label):
+    def _wgrad_launch(self, args, variant, M, N1, N2, label):
+        if self.precision == "fp32":  # parity mode: the fp32 twin (no kernel variants)
+            fn, args = "es_gemm_tn", args + (_lib.stream(),)
+        else:
+            fn, args = "es_gemm_tn_ex", args + (variant, _lib.stream())
         pr = self.probe
         if pr is not None and label is not None and pr["label"] == label:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            self._call("es_gemm_tn", *args)
+            self._call(fn, *args)
             e1.record()
             pr["events"].append((e0, e1, 2.0 * M * N1 * N2))
         else:
-            self._call("es_gemm_tn", *args)
+            self._call(fn, *args)
 
     def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None):
         D = self.cfg.dim
@@ -669,6 +679,8 @@ class Engine:
         done = {}
 
         def block_done(i):
+            if self.capture is not None:
+                self.capture("bwd", True, i, G.dx[:M])
             if grouped and i > 0 and i % self.GROUP_LAYERS == 0 and problems:
                 # these layers' weight gradients as one grouped launch on the side stream, beside the
                 # rest of the data-gradient chain (their dY sets are never rewritten within the step)
@@ -704,6 +716,8 @@ class Engine:
                  ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(dtop), D, Tt,
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
                  cfg.num_classes, s)
+        if self.capture is not None:
+            self.capture("dtop", True, cfg.depth - 1, dtop[:n] if prune else G.dx[:M])
         nh = n // 2
         if (not grouped and not prune and ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0
                 and (nh * cfg.np) % 256 == 0 and grad.numel() % 4 == 0):
@@ -821,6 +835,12 @@ class Engine:
             self._gtab = {}
         cache = self._gtab.get(slot)
         if cache is None or cache[0] != raw:
+            if torch.cuda.is_current_stream_capturing():
+                # a blocking host->device copy cannot be captured: the eager step that precedes every
+                # capture (FixMatch._run_graph) uploads the identical table, so a miss here means the
+                # buffers moved between that step and the capture
+                raise RuntimeError("grouped weight-gradient table changed during hipGraph capture; run one eager "
+                                   "step of this shape first")
             dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device, non_blocking=False)
             self._gtab[slot] = cache = (raw, dev)
         pr = self.probe

@@ -55,6 +55,11 @@ int es_set_tn_variant(int variant);
 size_t es_gemm_tn_workspace(int N1, int N2, int splits);
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream);
+/* es_gemm_tn with an explicit kernel choice (variant >= 0, the es_set_tn_variant numbering; -1 = the
+ * process-wide setting): the engine passes the 384x192 tile for its CU-share-sized launches this way
+ * instead of toggling the global knob around each call */
+int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
+                  float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream);
 int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream);
 /* Grouped weight gradients: many independent es_gemm_tn problems in ONE launch, each 128x128 tile
  * over its problem's whole token axis (no split-K slabs, no reduction launches) -- the small-shard
@@ -352,6 +357,13 @@ int es_tokens_cls_set(float* xt, int N, int T, int D, const float* cls, hipStrea
  * dlogits = grad_scale * d(out[0]) / d logits */
 int es_ce_weighted_fwd_bwd(const float* logits, int ldl, const int64_t* targets, const float* weights, int n, int C,
                            float grad_scale, float* dlogits, int lddl, float* out, hipStream_t stream);
+/* out[0] = sum_i w[y_i] over this rank's rows (weights nullable -> n) */
+int es_ce_weight_sum(const int64_t* targets, const float* weights, int n, int C, float* out, hipStream_t stream);
+/* the data-parallel weighted mean (code/loss.py:118 over the GLOBAL batch): *wsum_global = the weight sum over every
+ * rank's rows; out[0] = sum_{own rows} w_y l / W_global; dlogits = grad_scale * d(out[0]) / d logits */
+int es_ce_weighted_fwd_bwd_global(const float* logits, int ldl, const int64_t* targets, const float* weights,
+                                  const float* wsum_global, int n, int C, float grad_scale, float* dlogits, int lddl,
+                                  float* out, hipStream_t stream);
 
 /* ---- optimizer / EMA (code/optimizer.py:50-51, code/ema.py:51-62) ----------------------------- */
 int es_adam_ema_step(float* p, const float* g, float* m, float* v, float* ema, long n, float beta1, float beta2,

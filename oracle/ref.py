@@ -284,3 +284,123 @@ class CoMatchRef:
         loss = loss_x + self.lambda_u * loss_u + self.lambda_c * loss_contrast
         return {"lx": loss_x.item(), "lu": loss_u.item(), "lc": loss_contrast.item(), "loss": loss.item(),
                 "probs": probs, "probs_orig": probs_orig, "mask": mask, "pseudo_label": lbs, "loss_t": loss}
+
+
+# ------------------------------------------------------------------ one ViT block, bf16 contract
+# The per-block restatement the teacher-forced parity test (tests/test_gpu_blocks.py) holds the
+# production kernels to.  Arithmetic: code/models/conformer.py:8-72 (Mlp :13-23 with exact GELU,
+# Attention :35-50 with scale hd^-0.5, Block :53-72 pre-norm residual, LN eps 1e-6).  Rounding points
+# (the numerical contract of the bf16 kernels, forward and backward): every GEMM / attention operand
+# is a bf16 value (LN outputs, qkv, the unnormalised softmax numerators bf16(e) in P.V, the attention
+# output, GELU output, every weight, and in the backward the output gradients bf16(dY), bf16(dY*GELU'),
+# bf16(d LN-output), bf16(d attention-output), bf16(P) / bf16(dS) inside the attention backward and the
+# attention input gradient dqkv); GELU'(pre) is kept as a bf16 value; accumulation, LN / softmax
+# statistics, the residual stream and its gradient, biases and their gradients stay fp32.  The
+# functions keep the dtype of their inputs: float32 on the CPU is the oracle as specified; float64
+# (e.g. on a device, for BASELINE-size batches) only removes accumulation-order noise.
+ROUND = True  # tests switch the rounding points off to check the reverse pass against autograd
+
+
+def _rb(t):
+    """Round to bf16, keep the dtype (identity when ROUND is off)."""
+    return t.to(torch.bfloat16).to(t.dtype) if ROUND else t
+
+
+def _gelu_exact(x):
+    return 0.5 * x * (1.0 + torch.erf(x * 0.7071067811865476))
+
+
+def _gelu_grad(x):
+    return 0.5 * (1.0 + torch.erf(x * 0.7071067811865476)) + x * torch.exp(-0.5 * x * x) * 0.3989422804014327
+
+
+def _ln_stats(x, eps):
+    mean = x.mean(-1, keepdim=True)
+    var = ((x - mean) ** 2).mean(-1, keepdim=True)
+    rstd = torch.rsqrt(var + eps)
+    return (x - mean) * rstd, rstd
+
+
+def _ln_bwd(dy, xhat, rstd, w):
+    """d LayerNorm: dx from dy (the bf16 values the kernel reads), xhat, rstd; dw, db as column sums."""
+    g = dy * w
+    dx = rstd * (g - g.mean(-1, keepdim=True) - xhat * (g * xhat).mean(-1, keepdim=True))
+    return dx, (dy * xhat).sum(0), dy.sum(0)
+
+
+def block_fwd_bf16(p, i, x, n, cfg):
+    """Block i of the ViT (code/models/conformer.py:70-72: x + attn(norm1(x)), then + mlp(norm2(.)))
+    over n images of cfg.T tokens, x [n*T, D] (residual stream, fp32 / fp64).  Returns (out, cache)."""
+    b = f"blocks.{i}."
+    D, H, T = cfg.dim, cfg.heads, cfg.T
+    xh1, r1 = _ln_stats(x, cfg.eps)
+    h1 = _rb(xh1 * p[b + "norm1.weight"] + p[b + "norm1.bias"])
+    qkv = _rb(h1 @ _rb(p[b + "attn.qkv.weight"]).T + p[b + "attn.qkv.bias"])
+    q, k, v = qkv.view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-2, -1)) * 64 ** -0.5
+    mx = s.amax(-1, keepdim=True)
+    e = torch.exp(s - mx)
+    l = e.sum(-1, keepdim=True)
+    lse = mx + torch.log(l)
+    o = _rb(((_rb(e) @ v) / l).transpose(1, 2).reshape(n * T, D))
+    xmid = x + (o @ _rb(p[b + "attn.proj.weight"]).T + p[b + "attn.proj.bias"])
+    xh2, r2 = _ln_stats(xmid, cfg.eps)
+    h2 = _rb(xh2 * p[b + "norm2.weight"] + p[b + "norm2.bias"])
+    pre = h2 @ _rb(p[b + "mlp.fc1.weight"]).T + p[b + "mlp.fc1.bias"]
+    act = _rb(_gelu_exact(pre))
+    out = xmid + (act @ _rb(p[b + "mlp.fc2.weight"]).T + p[b + "mlp.fc2.bias"])
+    cache = dict(xh1=xh1, r1=r1, h1=h1, qkv=qkv, lse=lse, o=o, xh2=xh2, r2=r2, h2=h2, gd=_rb(_gelu_grad(pre)),
+                 act=act)
+    return out, cache
+
+
+def block_bwd_bf16(p, i, cache, dy, n, cfg):
+    """Reverse pass of block_fwd_bf16 given dy = d(loss)/d(out) [n*T, D] (fp32 values), at the bf16
+    kernels' rounding points (see above; attention backward as flash-style recomputation from lse:
+    P = exp(s - lse), delta = rowsum(dO * O)).  Returns (dx, {parameter name: gradient})."""
+    b = f"blocks.{i}."
+    D, H, T = cfg.dim, cfg.heads, cfg.T
+    c = cache
+    g = {}
+    dyb = _rb(dy)
+    dpre = _rb((dyb @ _rb(p[b + "mlp.fc2.weight"])) * c["gd"])
+    g[b + "mlp.fc2.weight"], g[b + "mlp.fc2.bias"] = dyb.T @ c["act"], dyb.sum(0)
+    dh2 = _rb(dpre @ _rb(p[b + "mlp.fc1.weight"]))
+    g[b + "mlp.fc1.weight"], g[b + "mlp.fc1.bias"] = dpre.T @ c["h2"], dpre.sum(0)
+    dx2, g[b + "norm2.weight"], g[b + "norm2.bias"] = _ln_bwd(dh2, c["xh2"], c["r2"], p[b + "norm2.weight"])
+    dxm = dx2 + dy
+    dxmb = _rb(dxm)
+    do = _rb(dxmb @ _rb(p[b + "attn.proj.weight"]))
+    g[b + "attn.proj.weight"], g[b + "attn.proj.bias"] = dxmb.T @ c["o"], dxmb.sum(0)
+    # attention backward (per image-head); o / do in [n*T, D] with column h*64 + d
+    q, k, v = c["qkv"].view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    o4 = c["o"].view(n, T, H, 64).transpose(1, 2)
+    do4 = do.view(n, T, H, 64).transpose(1, 2)
+    scale = 64 ** -0.5
+    P = torch.exp((q @ k.transpose(-2, -1)) * scale - c["lse"])
+    delta = (do4 * o4).sum(-1, keepdim=True)
+    dS = P * (do4 @ v.transpose(-2, -1) - delta)
+    dSb = _rb(dS)
+    dq = _rb((dSb @ k) * scale)
+    dk = _rb((dSb.transpose(-2, -1) @ q) * scale)
+    dv = _rb(_rb(P).transpose(-2, -1) @ do4)
+    dqkv = torch.stack((dq, dk, dv)).permute(1, 3, 0, 2, 4).reshape(n * T, 3 * D)
+    dh1 = _rb(dqkv @ _rb(p[b + "attn.qkv.weight"]))
+    g[b + "attn.qkv.weight"], g[b + "attn.qkv.bias"] = dqkv.T @ c["h1"], dqkv.sum(0)
+    dx1, g[b + "norm1.weight"], g[b + "norm1.bias"] = _ln_bwd(dh1, c["xh1"], c["r1"], p[b + "norm1.weight"])
+    return dx1 + dxm, g
+
+
+def embed_fwd_bf16(p, x, cfg):
+    """PatchEmbed Conv2d(3, D, 16, 16) on bf16 pixels and weights + cat(cls) + pos_embed (timm
+    VisionTransformer.forward_features; code/models/conformer.py:420,430) -> [n*T, D]."""
+    n = x.shape[0]
+    t = F.conv2d(_rb(x), _rb(p["patch_embed.proj.weight"]), p["patch_embed.proj.bias"], stride=cfg.patch)
+    t = torch.cat((p["cls_token"].expand(n, -1, -1), t.flatten(2).transpose(1, 2)), dim=1) + p["pos_embed"]
+    return t.reshape(n * cfg.T, cfg.dim)
+
+
+def head_fwd(p, x_cls, cfg):
+    """Final LayerNorm + Linear head on the CLS rows (fp32; code/models/conformer.py:442-443)."""
+    return F.linear(F.layer_norm(x_cls, (cfg.dim,), p["norm.weight"], p["norm.bias"], cfg.eps), p["head.weight"],
+                    p["head.bias"])

@@ -326,3 +326,58 @@ def test_two_rank_semiformer_sync_batchnorm():
         assert rel <= 1e-2, (rank, rel)
         assert bn <= 1e-4, (rank, bn)
         assert nbt == 1
+
+
+def _wce_worker(rank, world, port, q):
+    """Weighted CE (code/loss.py:118) over the global batch at N = 2: the shards' weight sums differ
+    (rank 0 holds the heavy classes), so per-rank weighted means would average to the wrong loss."""
+    sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
+    from endossl import dist
+    from endossl.loss import weighted_ce_fwd_bwd
+    g = torch.Generator().manual_seed(5)
+    n, C = 64, 23
+    logits = (torch.randn(n, C, generator=g) * 2).cuda()
+    y = torch.cat([torch.randint(0, 5, (n // 2,), generator=g), torch.randint(5, C, (n // 2,), generator=g)]).cuda()
+    w = torch.linspace(3.0, 0.2, C).cuda()
+    full_out, full_dl = torch.zeros(1, device="cuda"), torch.empty_like(logits)
+    weighted_ce_fwd_bwd(logits, y, w, full_dl, full_out)  # no process group yet: the one-process form
+    ref = torch.nn.functional.cross_entropy(logits.double(), y, weight=w.double())
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0")
+    dist.init_from_env(backend="gloo")
+    try:
+        b = n // world
+        sl = slice(rank * b, (rank + 1) * b)
+        out, dl = torch.zeros(1, device="cuda"), torch.empty(b, C, device="cuda")
+        weighted_ce_fwd_bwd(logits[sl].contiguous(), y[sl].contiguous(), w, dl, out)
+        torch.cuda.synchronize()
+        parts = [torch.empty_like(dl) for _ in range(world)]
+        torch.distributed.all_gather(parts, dl)
+        glob = torch.cat(parts) / world  # the optimizer's SUM all-reduce x 1/world, per row
+        local_mean = torch.nn.functional.cross_entropy(logits[sl].double(), y[sl], weight=w.double())
+        q.put((rank, out.item(), full_out.item(), ref.item(), (glob - full_dl).abs().max().item(),
+               full_dl.abs().max().item(), local_mean.item()))
+        dist.barrier()
+    finally:
+        torch.distributed.destroy_process_group()
+
+
+def test_two_rank_weighted_ce_global_batch():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_wce_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    means = []
+    for rank, out, full, ref, dmax, dscale, local_mean in res:
+        assert abs(full - ref) <= 1e-5 * abs(ref), (full, ref)
+        assert abs(out - ref) <= 1e-5 * abs(ref), f"rank {rank}: all-reduced loss {out} vs global {ref}"
+        assert dmax <= 1e-6 * dscale + 1e-8, f"rank {rank}: gradient off by {dmax}"
+        means.append(local_mean)
+    # the test is sensitive: the average of per-rank weighted means is not the global weighted mean
+    assert abs(sum(means) / 2 - res[0][3]) > 1e-2 * abs(res[0][3])

@@ -435,10 +435,13 @@ def test_uint8_input_path_matches_normalised_fp32():
     assert torch.equal(c, eng.forward(m.flat, [xf.to(DEV)], train=True))
 
 
-def test_graph_replay_matches_eager_step():
+@pytest.mark.parametrize("group", ["0", "1"])
+def test_graph_replay_matches_eager_step(group):
     """FixMatch.use_graph: the forward / losses / backward replayed from a captured hipGraph give the
     eager step's losses, pseudo-labels and gradients (the same launches in the same order; only the
-    head's fp32-atomic reductions may differ in the last bits), step after step."""
+    head's fp32-atomic reductions may differ in the last bits), step after step -- with the weight
+    gradients as split-K launches (group "0") and as the small shard's grouped launches ("1", whose
+    device problem tables the eager step uploads and the graph only reads)."""
     from endossl.vit import NativeViT, ViTConfig
     vcfg = ViTConfig(img_size=64, dim=128, depth=2, heads=2, num_classes=23)
     g = torch.Generator().manual_seed(12)
@@ -454,6 +457,7 @@ def test_graph_replay_matches_eager_step():
         with torch.no_grad():
             m.head.weight.normal_(0, 0.5, generator=torch.Generator().manual_seed(2))
         m = m.to(DEV)
+        m.engine().GROUP_WGRAD = group
         tr = FixMatch(m, device=DEV)
         tr.use_graph = graph
         tr.get_dataloader((None, None), None)
@@ -467,6 +471,7 @@ def test_graph_replay_matches_eager_step():
             outs.append(({k: o[k].detach().clone() for k in ("lx", "lu", "mask_mean", "pseudo_label")},
                          m.flat_grad.clone(), m.flat.clone()))
         assert (getattr(tr, "_graph", None) is not None) == graph
+        assert (len(getattr(m.engine(), "_gtab", {})) > 0) == (group == "1")
         res[graph] = outs
     for (oe, ge, we), (og, gg, wg) in zip(res[False], res[True]):
         for k in ("lx", "lu", "mask_mean"):
