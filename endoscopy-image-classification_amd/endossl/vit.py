@@ -766,18 +766,27 @@ class Engine:
                 block_done(i)
                 continue
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
+            cap = self.capture  # test hook: each reverse-pass intermediate as the next op reads it
+            if cap is not None:
+                cap("b_dxb", True, i, Gi.dxb[:M])
             self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(Gi.dxb), D,
                  ptr(self.wt[b + "mlp.fc2.weight"]), D, None, ptr(Gi.dpre), Hd, None, ptr(A.pre[i]), Hd, M, Hd, D, 0, s)
             wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
             self._call("es_gemm_nt", EPI_DH, ptr(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None, ptr(G.dh),
                  D, None, None, 0, M, D, Hd, 0, s)
             wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"), label="fc1_wgrad")
+            if cap is not None:
+                cap("b_dpre", True, i, Gi.dpre[:M])
+                cap("b_dh2", True, i, G.dh[:M])
             self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, Gi.dxmb,
                          gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
             # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
             self._call("es_gemm_nt", EPI_BF16, ptr(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
                  None, None, 0, M, D, D, 0, s)
             wgrad_side(Gi.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
+            if cap is not None:
+                cap("b_dxm", True, i, G.dxm[:M], Gi.dxmb[:M])
+                cap("b_do", True, i, G.do[:M])
             if ov and self.ATTN_SPLIT:
                 s3 = self.attn_stream()
                 s3.wait_stream(main)
@@ -793,6 +802,9 @@ class Engine:
             self._call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
             wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
+            if cap is not None:
+                cap("b_dqkv", True, i, Gi.dqkv[:M])
+                cap("b_dh1", True, i, G.dh[:M])
             if ovw:
                 done[i] = side.record_event()
                 if i + 1 in done:  # set (i-1) % 2 was layer i+1's: its weight gradients must be done

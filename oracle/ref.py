@@ -328,6 +328,39 @@ def _ln_bwd(dy, xhat, rstd, w):
     return dx, (dy * xhat).sum(0), dy.sum(0)
 
 
+def attn_fwd_bf16(qkv, n, T, H):
+    """softmax(q k^T hd^-0.5) v per image-head (code/models/conformer.py:41-50) at the kernels'
+    rounding points: qkv bf16 values [n*T, 3*H*64] (column order [3][H][64]); the unnormalised
+    numerators e = exp(s - max) enter P.V as bf16(e), the sum l in full precision; o = bf16(P.V / l)
+    [n*T, H*64]; lse = max + log(l) [n, H, T, 1] (what the reverse pass recomputes P from)."""
+    q, k, v = qkv.view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-2, -1)) * 64 ** -0.5
+    mx = s.amax(-1, keepdim=True)
+    e = torch.exp(s - mx)
+    l = e.sum(-1, keepdim=True)
+    o = _rb(((_rb(e) @ v) / l).transpose(1, 2).reshape(n * T, H * 64))
+    return o, mx + torch.log(l)
+
+
+def attn_bwd_bf16(qkv, o, lse, do, n, T, H):
+    """Reverse pass of attn_fwd_bf16 (flash-style recomputation): P = exp(s - lse), delta =
+    rowsum(dO * O), dS = P (dO v^T - delta); dV = bf16(bf16(P)^T dO), dK = bf16(bf16(dS)^T q * scale),
+    dQ = bf16(bf16(dS) k * scale) -> dqkv [n*T, 3*H*64] in qkv's column order."""
+    D = H * 64
+    q, k, v = qkv.view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    o4 = o.view(n, T, H, 64).transpose(1, 2)
+    do4 = do.view(n, T, H, 64).transpose(1, 2)
+    scale = 64 ** -0.5
+    P = torch.exp((q @ k.transpose(-2, -1)) * scale - lse)
+    delta = (do4 * o4).sum(-1, keepdim=True)
+    dS = P * (do4 @ v.transpose(-2, -1) - delta)
+    dSb = _rb(dS)
+    dq = _rb((dSb @ k) * scale)
+    dk = _rb((dSb.transpose(-2, -1) @ q) * scale)
+    dv = _rb(_rb(P).transpose(-2, -1) @ do4)
+    return torch.stack((dq, dk, dv)).permute(1, 3, 0, 2, 4).reshape(n * T, 3 * D)
+
+
 def block_fwd_bf16(p, i, x, n, cfg):
     """Block i of the ViT (code/models/conformer.py:70-72: x + attn(norm1(x)), then + mlp(norm2(.)))
     over n images of cfg.T tokens, x [n*T, D] (residual stream, fp32 / fp64).  Returns (out, cache)."""
@@ -336,13 +369,7 @@ def block_fwd_bf16(p, i, x, n, cfg):
     xh1, r1 = _ln_stats(x, cfg.eps)
     h1 = _rb(xh1 * p[b + "norm1.weight"] + p[b + "norm1.bias"])
     qkv = _rb(h1 @ _rb(p[b + "attn.qkv.weight"]).T + p[b + "attn.qkv.bias"])
-    q, k, v = qkv.view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
-    s = (q @ k.transpose(-2, -1)) * 64 ** -0.5
-    mx = s.amax(-1, keepdim=True)
-    e = torch.exp(s - mx)
-    l = e.sum(-1, keepdim=True)
-    lse = mx + torch.log(l)
-    o = _rb(((_rb(e) @ v) / l).transpose(1, 2).reshape(n * T, D))
+    o, lse = attn_fwd_bf16(qkv, n, T, H)
     xmid = x + (o @ _rb(p[b + "attn.proj.weight"]).T + p[b + "attn.proj.bias"])
     xh2, r2 = _ln_stats(xmid, cfg.eps)
     h2 = _rb(xh2 * p[b + "norm2.weight"] + p[b + "norm2.bias"])
@@ -372,19 +399,7 @@ def block_bwd_bf16(p, i, cache, dy, n, cfg):
     dxmb = _rb(dxm)
     do = _rb(dxmb @ _rb(p[b + "attn.proj.weight"]))
     g[b + "attn.proj.weight"], g[b + "attn.proj.bias"] = dxmb.T @ c["o"], dxmb.sum(0)
-    # attention backward (per image-head); o / do in [n*T, D] with column h*64 + d
-    q, k, v = c["qkv"].view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
-    o4 = c["o"].view(n, T, H, 64).transpose(1, 2)
-    do4 = do.view(n, T, H, 64).transpose(1, 2)
-    scale = 64 ** -0.5
-    P = torch.exp((q @ k.transpose(-2, -1)) * scale - c["lse"])
-    delta = (do4 * o4).sum(-1, keepdim=True)
-    dS = P * (do4 @ v.transpose(-2, -1) - delta)
-    dSb = _rb(dS)
-    dq = _rb((dSb @ k) * scale)
-    dk = _rb((dSb.transpose(-2, -1) @ q) * scale)
-    dv = _rb(_rb(P).transpose(-2, -1) @ do4)
-    dqkv = torch.stack((dq, dk, dv)).permute(1, 3, 0, 2, 4).reshape(n * T, 3 * D)
+    dqkv = attn_bwd_bf16(c["qkv"], c["o"], c["lse"], do, n, T, H)
     dh1 = _rb(dqkv @ _rb(p[b + "attn.qkv.weight"]))
     g[b + "attn.qkv.weight"], g[b + "attn.qkv.bias"] = dqkv.T @ c["h1"], dqkv.sum(0)
     dx1, g[b + "norm1.weight"], g[b + "norm1.bias"] = _ln_bwd(dh1, c["xh1"], c["r1"], p[b + "norm1.weight"])
