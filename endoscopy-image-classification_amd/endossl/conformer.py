@@ -312,6 +312,18 @@ class _GradSink:
         return None
 
 
+# test hook (tests/test_gpu_convs.py, teacher-forced per-conv parity): called as CAPTURE("fwd", wname, x, y,
+# spec) after each convolution's forward and CAPTURE("bwd", wname, dy, dx_before, dx) after its input
+# gradient, on the launch stream, with the conv's own NHWC views (x: the input map as the kernel reads it;
+# dx_before: what a gradient sink's buffer held before this conv accumulated into it, else None); the callee
+# clones what it keeps.  spec = (bias name, Cout, k, stride, padding, bf16 kernels?)
+CAPTURE = None
+
+
+def _map_view(t, xm):
+    return torch.as_strided(t, (xm.N, xm.H, xm.W, xm.C), (xm.sn, xm.sh, xm.sw, xm.sc), xm.off)
+
+
 class _ConvFn(torch.autograd.Function):
     """Conv2d (groups 1, optional bias) on an NHWC view -> new NHWC map (code/models/conformer.py
     ConvBlock / FCU convs, Conformer.conv1)."""
@@ -341,6 +353,8 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x)
         ctx.m, ctx.xmap, ctx.spec, ctx.b16 = m, xmap, (wname, bname, Cout, k, s, p, Ho, Wo), b16
         ctx.sink = sink
+        if CAPTURE is not None:
+            CAPTURE("fwd", wname, _map_view(xmap.t, xmap), y, (bname, Cout, k, s, p, b16))
         return y
 
     @staticmethod
@@ -382,11 +396,16 @@ class _ConvFn(torch.autograd.Function):
             alloc = (lambda: torch.empty_like(x)) if full else (lambda: torch.zeros_like(x))  # noqa: E731
             dx, acc = sink.take(alloc) if sink is not None else (alloc(), 0)
             wimg = m.conv_pack(wname, Cout, xm.C, k)[1] if b16 else m.pview(wname)
+            before = _map_view(dx, xm).clone() if CAPTURE is not None and acc else None
             call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
                  ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, acc,
                  _s())
+            if CAPTURE is not None:
+                CAPTURE("bwd", wname, dy, before, _map_view(dx, xm))
             if sink is not None:  # first consumer: hand the buffer over; second: return the sum
                 dx = sink.give(dx, acc)
+        elif CAPTURE is not None:  # no input gradient (the stem reads the images): dy for the weight gradient
+            CAPTURE("bwd", wname, dy, None, None)
         return dx, None, None, None, None, None, None, None, None, None, None, None
 
 
