@@ -12,7 +12,9 @@ the step.  Each conv is then re-computed by its oracle from THOSE operands, in f
       db = sum dy (csrc/conv_bf16.hip header);
   conv.hip (the 3-channel stem): plain fp32 operands.
 One rounding point per output, so device and oracle differ by fp32 summation order only: every conv's
-y, dx, dw (and db) within 1e-4 relative L2 (measured ~1e-6 .. 1e-5) -- this replaces the model-level
+y, dx, dw within 1e-4 relative L2 (measured 3e-7, 3e-7, 2e-6 over the 96 convs of the step), db within 1e-4
+of the per-channel sum of |dy| (a bias feeding a BatchNorm has a true gradient of exactly zero, so a relative
+bar would measure cancellation noise) -- this replaces the model-level
 "|device - fp32| <= 2 x envelope" bar of test_gpu_conformer.py for the bf16 convs.
 """
 import json
@@ -90,7 +92,10 @@ def test_s1_per_conv_teacher_forced():
             dwr = torch.nn.grad.conv2d_weight(xr, w.shape, _rb(dyc, b16), stride=s, padding=p)
             rec[f"{wname}.dw"] = _rel(m.gview(wname).view(w.shape), dwr)
             if bname:
-                rec[f"{wname}.db"] = _rel(m.gview(bname), dyc.sum((0, 2, 3)))
+                # relative to sum |dy| per channel: a conv bias in front of a BatchNorm (FCUUp's
+                # conv_project) has an exactly-zero true gradient, so its sum is pure cancellation noise
+                dbr = dyc.sum((0, 2, 3))
+                rec[f"{wname}.db"] = ((m.gview(bname).double() - dbr).norm() / dyc.abs().sum((0, 2, 3)).norm()).item()
             del xc, xr, yr, dyc, dwr
     root = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
