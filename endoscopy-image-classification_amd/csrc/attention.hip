@@ -493,6 +493,271 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(AttnArgs a) {
   }
 }
 
+// dK, dV with the query-pair loop software-pipelined: the LDS fragments of pair sc+1 (Q and dO rows
+// for the S / dP products, lse / delta) and the transposed dO / Q fragments of pair sc are issued
+// before pair sc's MFMAs and VALU, into separate registers, so every ds_read's latency hides behind
+// the previous pair's work (the straight loop waited lgkmcnt(0) in front of each of its 16 MFMAs:
+// one register set, each LDS round trip exposed).  Same operands, same MFMAs, same rounding points
+// (bf16(P) into dV, bf16(dS) into dK) and the same fp32 accumulation order as attn_bwd_dkv_kernel.
+struct DkvPair {
+  bf16x8 qa0, qa1, da0, da1, qb0, qb1, db0, db1;  // rows of query tiles u = 2sc (a) and 2sc+1 (b)
+  f32x4 la, dla, lb, dlb;                          // lse (log2 units) and delta of those queries
+};
+
+template <int NT16, bool SELF_DELTA = false>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv_pipe_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TP = NT16 * 16;
+  constexpr int NP = NT16 / 2;  // full query-tile pairs
+  const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
+  const int D = a.H * 64, T = a.T;
+  const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
+  char* Qs = smem;
+  char* Ds = smem + TP * 128;
+  float* lse_s = (float*)(smem + 2 * TP * 128);
+  float* del_s = lse_s + TP;
+  stage_head(Qs, base + h * 64, a.ldqkv, T, TP);
+  stage_head(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  for (int t = threadIdx.x; t < TP; t += blockDim.x)
+    lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] * 1.44269504088896341f : INFINITY;
+  if constexpr (!SELF_DELTA) {
+    for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t0 = 0; t0 < TP; t0 += 64) {
+      const int tq = t0 + (threadIdx.x >> 2), part = threadIdx.x & 3;
+      float dsum = 0.f;
+      if (tq < T) {
+        const bf16* orow = a.o + ((size_t)img * T + tq) * a.ldo + h * 64 + part * 16;
+        const bf16x8 o0 = *(const bf16x8*)orow, o1 = *(const bf16x8*)(orow + 8);
+        const bf16x8 d0 = lds_row8(Ds, tq, 2 * part), d1 = lds_row8(Ds, tq, 2 * part + 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += (float)d0[j] * (float)o0[j] + (float)d1[j] * (float)o1[j];
+      }
+      dsum += __shfl_xor(dsum, 1, 64);
+      dsum += __shfl_xor(dsum, 2, 64);
+      if (part == 0 && tq < TP) del_s[tq] = tq < T ? dsum : 0.f;
+    }
+    __syncthreads();
+  }
+  const float sl = a.scale * 1.44269504088896341f;
+
+  auto load_pair = [&](int sc) {
+    DkvPair o;
+    const int ua = 2 * sc * 16 + r, ub = ua + 16;
+    o.qa0 = lds_row8(Qs, ua, g); o.qa1 = lds_row8(Qs, ua, 4 + g);
+    o.da0 = lds_row8(Ds, ua, g); o.da1 = lds_row8(Ds, ua, 4 + g);
+    o.qb0 = lds_row8(Qs, ub, g); o.qb1 = lds_row8(Qs, ub, 4 + g);
+    o.db0 = lds_row8(Ds, ub, g); o.db1 = lds_row8(Ds, ub, 4 + g);
+    o.la = *(const f32x4*)(lse_s + 2 * sc * 16 + 4 * g);
+    o.dla = *(const f32x4*)(del_s + 2 * sc * 16 + 4 * g);
+    o.lb = *(const f32x4*)(lse_s + 2 * sc * 16 + 16 + 4 * g);
+    o.dlb = *(const f32x4*)(del_s + 2 * sc * 16 + 16 + 4 * g);
+    return o;
+  };
+
+  const int nkt = (T + 15) >> 4;
+  for (int kb = w; kb < nkt; kb += 4) {
+    const int key = kb * 16 + r;
+    const bool kv = key < T;
+    const bf16* krow = base + (size_t)key * a.ldqkv + D + h * 64;
+    const bf16* vrow = krow + D;
+    const bf16x8 kf0 = ld_row8(krow + 8 * g, kv), kf1 = ld_row8(krow + 32 + 8 * g, kv);
+    const bf16x8 vf0 = ld_row8(vrow + 8 * g, kv), vf1 = ld_row8(vrow + 32 + 8 * g, kv);
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dk[dt] = dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // P and dS of one query tile from its operands (query rows on the B side, this lane's key)
+    auto p_ds = [&](bf16x8 q0, bf16x8 q1, bf16x8 d0, bf16x8 d1, f32x4 l4, f32x4 d4, f32x4& p, f32x4& ds) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      sv = mfma16(q0, kf0, sv);
+      sv = mfma16(q1, kf1, sv);
+      dp = mfma16(d0, vf0, dp);
+      dp = mfma16(d1, vf1, dp);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        p[i] = __builtin_amdgcn_exp2f(sv[i] * sl - l4[i]);
+        ds[i] = p[i] * (dp[i] - d4[i]);
+      }
+    };
+    DkvPair cur = load_pair(0);
+#pragma unroll 2
+    for (int sc = 0; sc < NP; ++sc) {
+      DkvPair nxt = cur;
+      if (sc + 1 < NP) nxt = load_pair(sc + 1);
+      // this pair's transposed dO / Q fragments (the A operands of dV^T / dK^T)
+      bf16x8 tdo[4], tq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        tdo[dt] = lds_trT(Ds, sc * 32, dt * 16, g, r);
+        tq[dt] = lds_trT(Qs, sc * 32, dt * 16, g, r);
+      }
+      f32x4 p0, p1, s0, s1;
+      p_ds(cur.qa0, cur.qa1, cur.da0, cur.da1, cur.la, cur.dla, p0, s0);
+      p_ds(cur.qb0, cur.qb1, cur.db0, cur.db1, cur.lb, cur.dlb, p1, s1);
+      bf16x8 pf, dsf;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pf[i] = (bf16)p0[i];
+        pf[4 + i] = (bf16)p1[i];
+        dsf[i] = (bf16)s0[i];
+        dsf[4 + i] = (bf16)s1[i];
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16(tdo[dt], pf, dv[dt]);
+        dk[dt] = mfma16(tq[dt], dsf, dk[dt]);
+      }
+      cur = nxt;
+    }
+    if constexpr (NT16 & 1) {
+      const int u = NT16 - 1;
+      f32x4 p0, s0;
+      p_ds(lds_row8(Qs, u * 16 + r, g), lds_row8(Qs, u * 16 + r, 4 + g), lds_row8(Ds, u * 16 + r, g),
+           lds_row8(Ds, u * 16 + r, 4 + g), *(const f32x4*)(lse_s + u * 16 + 4 * g),
+           *(const f32x4*)(del_s + u * 16 + 4 * g), p0, s0);
+      const bf16x4 pf = {(bf16)p0[0], (bf16)p0[1], (bf16)p0[2], (bf16)p0[3]};
+      const bf16x4 dsf = {(bf16)s0[0], (bf16)s0[1], (bf16)s0[2], (bf16)s0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16k16(lds_trT4(Ds, u * 16, dt * 16, g, r), pf, dv[dt]);
+        dk[dt] = mfma16k16(lds_trT4(Qs, u * 16, dt * 16, g, r), dsf, dk[dt]);
+      }
+    }
+    if (kv) {
+      bf16* drow = a.dqkv + ((size_t)img * T + key) * a.lddqkv + D + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 vk = {(bf16)(dk[dt][0] * a.scale), (bf16)(dk[dt][1] * a.scale), (bf16)(dk[dt][2] * a.scale),
+                     (bf16)(dk[dt][3] * a.scale)};
+        bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
+        *(bf16x4*)(drow + dt * 16 + 4 * g) = vk;
+        *(bf16x4*)(drow + D + dt * 16 + 4 * g) = vv;
+      }
+    }
+  }
+}
+
+// dQ with the key-pair loop software-pipelined (as attn_bwd_dkv_pipe_kernel): pair sc+1's K / V row
+// fragments and pair sc's transposed K fragments are in flight while pair sc's MFMAs and VALU run.
+// Same operands, MFMAs, rounding points and fp32 accumulation order as attn_bwd_dq_kernel.
+struct DqPair {
+  bf16x8 ka0, ka1, va0, va1, kb0, kb1, vb0, vb1;  // rows of key tiles 2sc (a) and 2sc+1 (b)
+};
+
+template <int NT16>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq_pipe_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TP = NT16 * 16;
+  constexpr int NP = NT16 / 2;
+  const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
+  const int D = a.H * 64, T = a.T;
+  const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
+  char* Ks = smem;
+  char* Vs = smem + TP * 128;
+  stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
+  stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  const int nqt = (T + 15) >> 4;
+  const float sl = a.scale * 1.44269504088896341f;
+  auto load_pair = [&](int sc) {
+    DqPair o;
+    const int ta = 2 * sc * 16 + r, tb = ta + 16;
+    o.ka0 = lds_row8(Ks, ta, g); o.ka1 = lds_row8(Ks, ta, 4 + g);
+    o.va0 = lds_row8(Vs, ta, g); o.va1 = lds_row8(Vs, ta, 4 + g);
+    o.kb0 = lds_row8(Ks, tb, g); o.kb1 = lds_row8(Ks, tb, 4 + g);
+    o.vb0 = lds_row8(Vs, tb, g); o.vb1 = lds_row8(Vs, tb, 4 + g);
+    return o;
+  };
+  for (int qb = w; qb < nqt; qb += 4) {
+    const int q = qb * 16 + r;
+    const bool qv = q < T;
+    const size_t tok = (size_t)img * T + q;
+    const bf16* qrow = base + (size_t)q * a.ldqkv + h * 64;
+    const bf16* dorow = a.dout + tok * a.lddo + h * 64;
+    const bf16* orow = a.o + tok * a.ldo + h * 64;
+    const bf16x8 qf0 = ld_row8(qrow + 8 * g, qv), qf1 = ld_row8(qrow + 32 + 8 * g, qv);
+    const bf16x8 df0 = ld_row8(dorow + 8 * g, qv), df1 = ld_row8(dorow + 32 + 8 * g, qv);
+    const bf16x8 of0 = ld_row8(orow + 8 * g, qv), of1 = ld_row8(orow + 32 + 8 * g, qv);
+    float delta = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) delta += (float)df0[j] * (float)of0[j] + (float)df1[j] * (float)of1[j];
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    if (qv && g == 0) a.delta[(size_t)bh * T + q] = delta;  // consumed by the dK/dV pass
+    const float lq = qv ? a.lse[(size_t)bh * T + q] * 1.44269504088896341f : 0.f;  // log2 units
+
+    // dS^T tile t (keys 16t + 4g + i on this lane's query), in fp32
+    auto ds_tile = [&](int t, bf16x8 k0, bf16x8 k1, bf16x8 v0, bf16x8 v1) {
+      f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      sv = mfma16(k0, qf0, sv);
+      sv = mfma16(k1, qf1, sv);
+      dp = mfma16(v0, df0, dp);
+      dp = mfma16(v1, df1, dp);
+      f32x4 pv;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sv[i] * sl - lq);
+      if (t * 16 + 16 > T) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (t * 16 + 4 * g + i >= T) pv[i] = 0.f;
+      }
+      f32x4 ds;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ds[i] = pv[i] * (dp[i] - delta);
+      return ds;
+    };
+
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    DqPair cur = load_pair(0);
+#pragma unroll 2
+    for (int sc = 0; sc < NP; ++sc) {
+      DqPair nxt = cur;
+      if (sc + 1 < NP) nxt = load_pair(sc + 1);
+      bf16x8 tk[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) tk[dt] = lds_trT(Ks, sc * 32, dt * 16, g, r);
+      const f32x4 d0 = ds_tile(2 * sc, cur.ka0, cur.ka1, cur.va0, cur.va1);
+      const f32x4 d1 = ds_tile(2 * sc + 1, cur.kb0, cur.kb1, cur.vb0, cur.vb1);
+      bf16x8 dsf;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        dsf[i] = (bf16)d0[i];
+        dsf[4 + i] = (bf16)d1[i];
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tk[dt], dsf, dq[dt]);
+      cur = nxt;
+    }
+    if constexpr (NT16 & 1) {
+      const int t = NT16 - 1;
+      const f32x4 d0 = ds_tile(t, lds_row8(Ks, t * 16 + r, g), lds_row8(Ks, t * 16 + r, 4 + g),
+                               lds_row8(Vs, t * 16 + r, g), lds_row8(Vs, t * 16 + r, 4 + g));
+      const bf16x4 dsf = {(bf16)d0[0], (bf16)d0[1], (bf16)d0[2], (bf16)d0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16k16(lds_trT4(Ks, t * 16, dt * 16, g, r), dsf, dq[dt]);
+    }
+    if (qv) {
+      bf16* drow = a.dqkv + tok * a.lddqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 v = {(bf16)(dq[dt][0] * a.scale), (bf16)(dq[dt][1] * a.scale), (bf16)(dq[dt][2] * a.scale),
+                    (bf16)(dq[dt][3] * a.scale)};
+        *(bf16x4*)(drow + dt * 16 + 4 * g) = v;
+      }
+    }
+  }
+}
+
 // ---- CLS-query attention (the last block: only the CLS rows reach the head) ---------------------
 // One wave per (image, head).  Lane (c = lane & 7, jg = lane >> 3) holds dims 8c..8c+7 and walks keys
 // j = jg, jg + 8, ...: each 8-lane group reads whole 128-B K / V rows (coalesced) and completes a
@@ -681,6 +946,8 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
 // (measured faster: 108 vs 150 us at the F1 shape, scripts/attn_bench.py),
 // 3 = 168 VGPRs (three 52-KiB heads per CU, small spill)
 int g_attn_fwd_occ = 2;
+// backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 0 = the plain loops
+int g_attn_bwd_pipe = 1;
 
 }  // namespace
 
@@ -690,6 +957,13 @@ extern "C" {
 int es_set_attn_variant(int occ) {
   const int old = g_attn_fwd_occ;
   g_attn_fwd_occ = occ;
+  return old;
+}
+
+// tuning knob: attention backward loops, 1 = software-pipelined (default), 0 = plain; returns the previous value
+int es_set_attn_bwd_variant(int v) {
+  const int old = g_attn_bwd_pipe;
+  g_attn_bwd_pipe = v;
   return old;
 }
 
@@ -736,6 +1010,13 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
+  if (g_attn_bwd_pipe && nt16 == 13) {  // ViT/16 at 224^2 (T = 197): the pipelined loops
+    allow_lds(attn_bwd_dq_pipe_kernel<13>, lds_dq);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<13>), nimg * H, 256, lds_dq, stream, a);
+    allow_lds(attn_bwd_dkv_pipe_kernel<13>, lds_dkv);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<13>), nimg * H, 256, lds_dkv, stream, a);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
   ATTN_DISPATCH(attn_bwd_dkv_kernel, nt16, nimg * H, lds_dkv, stream, a);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;

@@ -25,6 +25,24 @@ __device__ __forceinline__ void glds16(const void* src, char* lds) {
   __builtin_amdgcn_global_load_lds(src, LDS_PTR(lds), 16, 0, 0);
 }
 
+// The same DMA as inline asm (cdna_hip_programming.md §5.7 LDS-DMA recipe: M0 written and restored in the
+// statement).  For loops that keep LDS-DMA in flight while they read other ring stages with
+// ds_read_b64_tr_b16: hipcc cannot prove that such a transposed read does not alias a pending
+// global_load_lds and drains every one of them (s_waitcnt vmcnt(0)) in front of the first read -- measured
+// in the weight-gradient kernels, where it serialised each stage's load with the previous stage's MFMAs.
+// An asm DMA is invisible to hipcc's waitcnt bookkeeping, so the CALLER retires it: a counted
+// s_waitcnt vmcnt(N) and a barrier before any wave reads the stage (extra compiler-counted VMEM ops only
+// make hipcc's own waits stricter, never looser).  No VGPR destination: register-safe.
+__device__ __forceinline__ void glds16_asm(const void* src, char* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
 // Raw buffer access (range-checked by the resource: out-of-range loads return 0, out-of-range
 // stores are dropped).  Epilogues map rows past M to an out-of-range offset with a select instead
 // of branching, which keeps the code straight-line so the waitcnt pass can count (a divergent

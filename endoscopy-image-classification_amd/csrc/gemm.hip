@@ -562,7 +562,8 @@ struct TNArgs {
   int M, N1, N2, ld1, ld2, mchunk;
 };
 
-// BKM-deep token steps (32 or 64), NST-stage glds ring, counted vmcnt.  With PB != null the
+// BKM-deep token steps (32 or 64), NST-stage glds ring (asm DMA: glds16_asm, retired by the counted
+// vmcnt + barrier at the top of each step), counted vmcnt.  With PB != null the
 // workgroups of the first N2 tile also sum their A1 (= dY) tile columns from LDS: the bias
 // gradient of the same Linear, written as per-split partials PB[split][N1].
 template <int BKM, int NST>
@@ -593,8 +594,8 @@ __device__ __forceinline__ void gemm_tn_body(const TNArgs& p, int split, int til
   {                                                                              \
     char* T1_ = smem + (BUF) * STAGE;                                            \
     _Pragma("unroll") for (int j = 0; j < IPW; ++j) {                            \
-      glds16(g1[j] + (size_t)(MO) * p.ld1, T1_ + (w * IPW + j) * 1024);          \
-      glds16(g2[j] + (size_t)(MO) * p.ld2, T1_ + TILE + (w * IPW + j) * 1024);   \
+      glds16_asm(g1[j] + (size_t)(MO) * p.ld1, T1_ + (w * IPW + j) * 1024);      \
+      glds16_asm(g2[j] + (size_t)(MO) * p.ld2, T1_ + TILE + (w * IPW + j) * 1024); \
     }                                                                            \
   }
 
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(256) void gemm_tn_grouped_kernel(const TNGroupEntry
 constexpr int TB1 = 384, TB2 = 192;
 __device__ __forceinline__ int swz384(int r, int c) { return c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2)); }
 
-template <int BKM, int NST>
+template <int BKM, int NST, bool ASM = true>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int R1B = TB1 * 2, R2B = TB2 * 2;          // LDS row bytes: 768, 384
@@ -756,13 +757,19 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
     char* S_ = smem + (BUF) * STAGE;                                                             \
     const char* x1 = b1 + (size_t)(KT) * s1;                                                     \
     const char* x2 = b2 + (size_t)(KT) * s2;                                                     \
-    _Pragma("unroll") for (int j = 0; j < F1; ++j) glds16(x1 + o1[j], S_ + (j * 8 + w) * 1024);  \
-    _Pragma("unroll") for (int j = 0; j < F2; ++j) glds16(x2 + o2[j], S_ + T1B + (j * 8 + w) * 1024); \
+    _Pragma("unroll") for (int j = 0; j < F1; ++j) GLDS(x1 + o1[j], S_ + (j * 8 + w) * 1024);  \
+    _Pragma("unroll") for (int j = 0; j < F2; ++j) GLDS(x2 + o2[j], S_ + T1B + (j * 8 + w) * 1024); \
     if constexpr (H2) {                                                                          \
-      if (lane < 32) glds16(x2 + o2[F2], S_ + T1B + F2 * 8192 + w * 512);                        \
+      if (lane < 32) GLDS(x2 + o2[F2], S_ + T1B + F2 * 8192 + w * 512);                          \
     }                                                                                            \
   }
 
+  // ASM: the ring's DMA as inline asm (glds16_asm), so the transposed reads of the current stage are
+  // not preceded by a compiler drain of the next stage's DMA; retired by the counted waits below
+  auto GLDS = [](const char* src, char* dst) {
+    if constexpr (ASM) glds16_asm(src, dst);
+    else glds16(src, dst);
+  };
   f32x4 acc[6][6], bacc[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
@@ -1133,7 +1140,7 @@ static bool tn_big_ok(int N1, int N2, int ld1, int ld2) {
 }
 static int tn_pick(int M, int N1, int N2, int ld1, int ld2, int v) {
   if (!(N1 % BM == 0 && N2 % BN == 0)) return 7;  // only the big tile covers N2 = 192 (caller checked)
-  if (v >= 5 && v <= 8) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
+  if (v >= 5 && v <= 9) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
   if (v >= 0) return v;
   return (tn_big_ok(N1, N2, ld1, ld2) && M >= 65536) ? 7 : 0;
 }
@@ -1168,11 +1175,11 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
   if (M <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!tn_big_ok(N1, N2, ld1, ld2) && ((N1 % BM) || (N2 % BN))) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
-  if (variant > 8) return ES_BAD_ARG;
+  if (variant > 9) return ES_BAD_ARG;
   // variant: 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3;
   // 5..7 = 384x192 tile with 32x2 (72 KiB: two workgroups per CU), 32x3, 64x2
   const int v = tn_pick(M, N1, N2, ld1, ld2, variant >= 0 ? variant : g_tn_variant);
-  const int BKM = (v == 3 || v == 4 || v == 7) ? 64 : 32;  // (8: 384x192, 32x4)
+  const int BKM = (v == 3 || v == 4 || v == 7 || v == 9) ? 64 : 32;  // (8: 384x192, 32x4)
   const int msteps = (M + BKM - 1) / BKM;
   if (splits <= 0) splits = tn_auto_splits(v, M, N1, N2);
   splits = std::min(splits, msteps);
@@ -1189,11 +1196,11 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
     allow_lds(gemm_tn_kernel<BKM_, NST_>, lds);                                                       \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_kernel<BKM_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
   }
-#define TNB_LAUNCH(BKM_, NST_)                                                                          \
+#define TNB_LAUNCH(BKM_, NST_, ASM_)                                                                    \
   {                                                                                                   \
     const size_t lds = (size_t)NST_ * BKM_ * (TB1 + TB2) * 2;                                         \
-    allow_lds(gemm_tn_big_kernel<BKM_, NST_>, lds);                                                   \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_kernel<BKM_, NST_>), dim3(grid), dim3(512), lds, stream, a); \
+    allow_lds(gemm_tn_big_kernel<BKM_, NST_, ASM_>, lds);                                             \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_kernel<BKM_, NST_, ASM_>), dim3(grid), dim3(512), lds, stream, a); \
   }
   switch (v) {
     case 0: TN_LAUNCH(32, 2) break;
@@ -1201,10 +1208,11 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
     case 3: TN_LAUNCH(64, 2) break;
     case 4: TN_LAUNCH(64, 3) break;
     case 2: TN_LAUNCH(32, 4) break;
-    case 5: TNB_LAUNCH(32, 2) break;
-    case 6: TNB_LAUNCH(32, 3) break;
-    case 7: TNB_LAUNCH(64, 2) break;
-    case 8: TNB_LAUNCH(32, 4) break;
+    case 5: TNB_LAUNCH(32, 2, true) break;
+    case 6: TNB_LAUNCH(32, 3, true) break;
+    case 7: TNB_LAUNCH(64, 2, true) break;
+    case 8: TNB_LAUNCH(32, 4, true) break;
+    case 9: TNB_LAUNCH(64, 2, false) break;  // A/B: the builtin transposed reads (compiler-drained prefetch)
     default: TN_LAUNCH(32, 2) break;
   }
 #undef TN_LAUNCH

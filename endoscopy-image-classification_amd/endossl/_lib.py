@@ -25,6 +25,7 @@ SIGNATURES = {
     "es_gemm_tn_ex": (I, [V, I, V, I, I, I, I, I, V, V, I, V, I, V]),
     "es_set_tn_variant": (I, [I]),
     "es_set_attn_variant": (I, [I]),
+    "es_set_attn_bwd_variant": (I, [I]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),
     "es_tn_problem_size": (Z, []),
     "es_gemm_tn_grouped_prepare": (I, [V, I]),
@@ -170,7 +171,8 @@ def load(path=None):
     # kernel-family knobs for A/B runs (scripts/, bench.py): ENDOSSL_TN_VARIANT / ENDOSSL_GEMM_VARIANT /
     # ENDOSSL_ATTN_VARIANT
     for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"),
-                    ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant")):
+                    ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant"),
+                    ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant")):
         if os.environ.get(env):
             getattr(lib, fn)(int(os.environ[env]))
     if path is None:

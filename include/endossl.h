@@ -86,6 +86,8 @@ int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate,
 
 /* tuning knob: forward attention occupancy target (2 or 3 workgroups per CU); returns previous */
 int es_set_attn_variant(int occ);
+/* attention backward loops: 1 = software-pipelined (default), 0 = plain; returns the previous value */
+int es_set_attn_bwd_variant(int v);
 /* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 592 (384^2 / 16) ------ */
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream);

@@ -283,6 +283,33 @@ def test_attention_bwd(n, T, H):
     torch.testing.assert_close(delta2, delta, rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("n", [3, 64])
+def test_attention_bwd_pipelined_matches_plain(n):
+    """The software-pipelined dQ / dK-dV loops (es_set_attn_bwd_variant 1, the default at T = 197) issue the
+    same MFMAs on the same operands in the same order as the plain loops: dqkv and delta bit-identical."""
+    T, H = 197, 6
+    D = H * 64
+    torch.manual_seed(7 + n)
+    qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
+    dout = _pad_rows(torch.randn(n * T, D, device=DEV).bfloat16())
+    o = torch.zeros(qkv.shape[0], D, dtype=torch.bfloat16, device=DEV)
+    lse = torch.zeros(n * H * T, device=DEV)
+    call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
+    res = {}
+    lib = _lib.load()
+    for v in (0, 1):
+        old = lib.es_set_attn_bwd_variant(v)
+        dqkv = torch.full_like(qkv, 3.0)
+        delta = torch.zeros(n * H * T, device=DEV)
+        call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(dout), D, ptr(dqkv), 3 * D, n, T, H,
+             64 ** -0.5, S())
+        torch.cuda.synchronize()
+        lib.es_set_attn_bwd_variant(old)
+        res[v] = (dqkv[:n * T].clone(), delta)
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
 @pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1),
                                    (2, 577, 2), (1, 300, 1)])
 def test_attention_cls_fwd_bwd(n, T, H):
