@@ -758,6 +758,327 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_pipe_kernel(AttnArgs a) {
   }
 }
 
+// dK, dV with TWO key tiles per wave item (32 keys): every Q / dO row fragment, lse / delta vector and
+// transposed dO / Q fragment read from LDS feeds both tiles' MFMAs, halving the LDS bytes per MFMA -- the
+// one-tile form (attn_bwd_dkv_pipe_kernel) moves ~17 KiB through LDS per 16 MFMAs, more than the 256 B/clk
+// a CU's LDS delivers beside two waves per SIMD of matrix work.  Items: key-tile pairs (2kp, 2kp+1); a
+// second tile past the head (odd tile count) computes on zero K / V rows and stores nothing.  Per key
+// tile the operands, MFMAs, rounding points and fp32 accumulation order are those of
+// attn_bwd_dkv_kernel: bit-identical dK / dV.
+template <int NT16, bool SELF_DELTA = false>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TP = NT16 * 16;
+  constexpr int NP = NT16 / 2;
+  const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
+  const int D = a.H * 64, T = a.T;
+  const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
+  char* Qs = smem;
+  char* Ds = smem + TP * 128;
+  float* lse_s = (float*)(smem + 2 * TP * 128);
+  float* del_s = lse_s + TP;
+  stage_head(Qs, base + h * 64, a.ldqkv, T, TP);
+  stage_head(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  for (int t = threadIdx.x; t < TP; t += blockDim.x)
+    lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] * 1.44269504088896341f : INFINITY;
+  if constexpr (!SELF_DELTA) {
+    for (int t = threadIdx.x; t < TP; t += blockDim.x) del_s[t] = t < T ? a.delta[(size_t)bh * T + t] : 0.f;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t0 = 0; t0 < TP; t0 += 64) {
+      const int tq = t0 + (threadIdx.x >> 2), part = threadIdx.x & 3;
+      float dsum = 0.f;
+      if (tq < T) {
+        const bf16* orow = a.o + ((size_t)img * T + tq) * a.ldo + h * 64 + part * 16;
+        const bf16x8 o0 = *(const bf16x8*)orow, o1 = *(const bf16x8*)(orow + 8);
+        const bf16x8 d0 = lds_row8(Ds, tq, 2 * part), d1 = lds_row8(Ds, tq, 2 * part + 1);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dsum += (float)d0[j] * (float)o0[j] + (float)d1[j] * (float)o1[j];
+      }
+      dsum += __shfl_xor(dsum, 1, 64);
+      dsum += __shfl_xor(dsum, 2, 64);
+      if (part == 0 && tq < TP) del_s[tq] = tq < T ? dsum : 0.f;
+    }
+    __syncthreads();
+  }
+  const float sl = a.scale * 1.44269504088896341f;
+
+  // P and dS of one query tile (operands q0, q1, d0, d1 = its Q / dO rows, l4 / d4 its lse / delta)
+  // against one key tile (kf0, kf1, vf0, vf1)
+  auto p_ds = [&](bf16x8 q0, bf16x8 q1, bf16x8 d0, bf16x8 d1, f32x4 l4, f32x4 d4, bf16x8 kf0, bf16x8 kf1,
+                  bf16x8 vf0, bf16x8 vf1, f32x4& p, f32x4& ds) {
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+    sv = mfma16(q0, kf0, sv);
+    sv = mfma16(q1, kf1, sv);
+    dp = mfma16(d0, vf0, dp);
+    dp = mfma16(d1, vf1, dp);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      p[i] = __builtin_amdgcn_exp2f(sv[i] * sl - l4[i]);
+      ds[i] = p[i] * (dp[i] - d4[i]);
+    }
+  };
+
+  const int nkt = (T + 15) >> 4;
+  const int nitems = (nkt + 1) >> 1;
+  for (int kp = w; kp < nitems; kp += 4) {
+    const int keyA = kp * 32 + r, keyB = keyA + 16;
+    const bool kvA = keyA < T, kvB = keyB < T;
+    const bf16* krA = base + (size_t)keyA * a.ldqkv + D + h * 64;
+    const bf16* krB = base + (size_t)keyB * a.ldqkv + D + h * 64;
+    const bf16x8 kA0 = ld_row8(krA + 8 * g, kvA), kA1 = ld_row8(krA + 32 + 8 * g, kvA);
+    const bf16x8 vA0 = ld_row8(krA + D + 8 * g, kvA), vA1 = ld_row8(krA + D + 32 + 8 * g, kvA);
+    const bf16x8 kB0 = ld_row8(krB + 8 * g, kvB), kB1 = ld_row8(krB + 32 + 8 * g, kvB);
+    const bf16x8 vB0 = ld_row8(krB + D + 8 * g, kvB), vB1 = ld_row8(krB + D + 32 + 8 * g, kvB);
+    f32x4 dkA[4], dvA[4], dkB[4], dvB[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dkA[dt] = dvA[dt] = dkB[dt] = dvB[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int sc = 0; sc < NP; ++sc) {
+      const int ua = 2 * sc * 16 + r, ub = ua + 16;
+      const bf16x8 qa0 = lds_row8(Qs, ua, g), qa1 = lds_row8(Qs, ua, 4 + g);
+      const bf16x8 da0 = lds_row8(Ds, ua, g), da1 = lds_row8(Ds, ua, 4 + g);
+      const bf16x8 qb0 = lds_row8(Qs, ub, g), qb1 = lds_row8(Qs, ub, 4 + g);
+      const bf16x8 db0 = lds_row8(Ds, ub, g), db1 = lds_row8(Ds, ub, 4 + g);
+      const f32x4 la = *(const f32x4*)(lse_s + 2 * sc * 16 + 4 * g);
+      const f32x4 dla = *(const f32x4*)(del_s + 2 * sc * 16 + 4 * g);
+      const f32x4 lb = *(const f32x4*)(lse_s + 2 * sc * 16 + 16 + 4 * g);
+      const f32x4 dlb = *(const f32x4*)(del_s + 2 * sc * 16 + 16 + 4 * g);
+      bf16x8 tdo[4], tq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        tdo[dt] = lds_trT(Ds, sc * 32, dt * 16, g, r);
+        tq[dt] = lds_trT(Qs, sc * 32, dt * 16, g, r);
+      }
+      {  // key tile A
+        f32x4 p0, p1, s0, s1;
+        p_ds(qa0, qa1, da0, da1, la, dla, kA0, kA1, vA0, vA1, p0, s0);
+        p_ds(qb0, qb1, db0, db1, lb, dlb, kA0, kA1, vA0, vA1, p1, s1);
+        bf16x8 pf, dsf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pf[i] = (bf16)p0[i];
+          pf[4 + i] = (bf16)p1[i];
+          dsf[i] = (bf16)s0[i];
+          dsf[4 + i] = (bf16)s1[i];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dvA[dt] = mfma16(tdo[dt], pf, dvA[dt]);
+          dkA[dt] = mfma16(tq[dt], dsf, dkA[dt]);
+        }
+      }
+      {  // key tile B
+        f32x4 p0, p1, s0, s1;
+        p_ds(qa0, qa1, da0, da1, la, dla, kB0, kB1, vB0, vB1, p0, s0);
+        p_ds(qb0, qb1, db0, db1, lb, dlb, kB0, kB1, vB0, vB1, p1, s1);
+        bf16x8 pf, dsf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pf[i] = (bf16)p0[i];
+          pf[4 + i] = (bf16)p1[i];
+          dsf[i] = (bf16)s0[i];
+          dsf[4 + i] = (bf16)s1[i];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dvB[dt] = mfma16(tdo[dt], pf, dvB[dt]);
+          dkB[dt] = mfma16(tq[dt], dsf, dkB[dt]);
+        }
+      }
+    }
+    if constexpr (NT16 & 1) {
+      const int u = NT16 - 1;
+      const bf16x8 q0 = lds_row8(Qs, u * 16 + r, g), q1 = lds_row8(Qs, u * 16 + r, 4 + g);
+      const bf16x8 d0 = lds_row8(Ds, u * 16 + r, g), d1 = lds_row8(Ds, u * 16 + r, 4 + g);
+      const f32x4 l4 = *(const f32x4*)(lse_s + u * 16 + 4 * g), d4 = *(const f32x4*)(del_s + u * 16 + 4 * g);
+      bf16x4 tdo4[4], tq4[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        tdo4[dt] = lds_trT4(Ds, u * 16, dt * 16, g, r);
+        tq4[dt] = lds_trT4(Qs, u * 16, dt * 16, g, r);
+      }
+      f32x4 p0, s0;
+      p_ds(q0, q1, d0, d1, l4, d4, kA0, kA1, vA0, vA1, p0, s0);
+      bf16x4 pf = {(bf16)p0[0], (bf16)p0[1], (bf16)p0[2], (bf16)p0[3]};
+      bf16x4 dsf = {(bf16)s0[0], (bf16)s0[1], (bf16)s0[2], (bf16)s0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dvA[dt] = mfma16k16(tdo4[dt], pf, dvA[dt]);
+        dkA[dt] = mfma16k16(tq4[dt], dsf, dkA[dt]);
+      }
+      p_ds(q0, q1, d0, d1, l4, d4, kB0, kB1, vB0, vB1, p0, s0);
+      pf = bf16x4{(bf16)p0[0], (bf16)p0[1], (bf16)p0[2], (bf16)p0[3]};
+      dsf = bf16x4{(bf16)s0[0], (bf16)s0[1], (bf16)s0[2], (bf16)s0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dvB[dt] = mfma16k16(tdo4[dt], pf, dvB[dt]);
+        dkB[dt] = mfma16k16(tq4[dt], dsf, dkB[dt]);
+      }
+    }
+    auto store = [&](int key, bool kv, const f32x4* dk, const f32x4* dv) {
+      if (!kv) return;
+      bf16* drow = a.dqkv + ((size_t)img * T + key) * a.lddqkv + D + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 vk = {(bf16)(dk[dt][0] * a.scale), (bf16)(dk[dt][1] * a.scale), (bf16)(dk[dt][2] * a.scale),
+                     (bf16)(dk[dt][3] * a.scale)};
+        bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
+        *(bf16x4*)(drow + dt * 16 + 4 * g) = vk;
+        *(bf16x4*)(drow + D + dt * 16 + 4 * g) = vv;
+      }
+    };
+    store(keyA, kvA, dkA, dvA);
+    store(keyB, kvB, dkB, dvB);
+  }
+}
+
+// dQ with TWO query tiles per wave item (32 queries): the K / V row fragments and transposed K fragments
+// read from LDS for a key pair feed both query tiles' MFMAs (half the LDS bytes per MFMA of
+// attn_bwd_dq_kernel).  A second tile past the head (odd tile count) runs on zero rows and stores nothing.
+// Per query tile: the operands, MFMAs, rounding points and fp32 order of attn_bwd_dq_kernel (bit-identical).
+template <int NT16>
+__global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TP = NT16 * 16;
+  constexpr int NP = NT16 / 2;
+  const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
+  const int D = a.H * 64, T = a.T;
+  const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
+  char* Ks = smem;
+  char* Vs = smem + TP * 128;
+  stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
+  stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  const int nqt = (T + 15) >> 4;
+  const int nitems = (nqt + 1) >> 1;
+  const float sl = a.scale * 1.44269504088896341f;
+  struct QOps {
+    bf16x8 qf0, qf1, df0, df1;
+    float delta, lq;
+    int q;
+    bool qv;
+  };
+  auto load_q = [&](int qb) {
+    QOps o;
+    o.q = qb * 16 + r;
+    o.qv = o.q < T;
+    const size_t tok = (size_t)img * T + o.q;
+    const bf16* qrow = base + (size_t)o.q * a.ldqkv + h * 64;
+    const bf16* dorow = a.dout + tok * a.lddo + h * 64;
+    const bf16* orow = a.o + tok * a.ldo + h * 64;
+    o.qf0 = ld_row8(qrow + 8 * g, o.qv);
+    o.qf1 = ld_row8(qrow + 32 + 8 * g, o.qv);
+    o.df0 = ld_row8(dorow + 8 * g, o.qv);
+    o.df1 = ld_row8(dorow + 32 + 8 * g, o.qv);
+    const bf16x8 of0 = ld_row8(orow + 8 * g, o.qv), of1 = ld_row8(orow + 32 + 8 * g, o.qv);
+    float delta = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) delta += (float)o.df0[j] * (float)of0[j] + (float)o.df1[j] * (float)of1[j];
+    delta += __shfl_xor(delta, 16, 64);
+    delta += __shfl_xor(delta, 32, 64);
+    o.delta = delta;
+    if (o.qv && g == 0) a.delta[(size_t)bh * T + o.q] = delta;  // consumed by the dK/dV pass
+    o.lq = o.qv ? a.lse[(size_t)bh * T + o.q] * 1.44269504088896341f : 0.f;  // log2 units
+    return o;
+  };
+  // dS^T tile t (keys 16t + 4g + i on this lane's query) from the key tile's K / V rows
+  auto ds_tile = [&](const QOps& Q, int t, bf16x8 k0, bf16x8 k1, bf16x8 v0, bf16x8 v1) {
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+    sv = mfma16(k0, Q.qf0, sv);
+    sv = mfma16(k1, Q.qf1, sv);
+    dp = mfma16(v0, Q.df0, dp);
+    dp = mfma16(v1, Q.df1, dp);
+    f32x4 pv;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sv[i] * sl - Q.lq);
+    if (t * 16 + 16 > T) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (t * 16 + 4 * g + i >= T) pv[i] = 0.f;
+    }
+    f32x4 ds;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ds[i] = pv[i] * (dp[i] - Q.delta);
+    return ds;
+  };
+  auto store = [&](const QOps& Q, const f32x4* dq) {
+    if (!Q.qv) return;
+    bf16* drow = a.dqkv + ((size_t)img * T + Q.q) * a.lddqkv + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 v = {(bf16)(dq[dt][0] * a.scale), (bf16)(dq[dt][1] * a.scale), (bf16)(dq[dt][2] * a.scale),
+                  (bf16)(dq[dt][3] * a.scale)};
+      *(bf16x4*)(drow + dt * 16 + 4 * g) = v;
+    }
+  };
+
+  for (int it = w; it < nitems; it += 4) {
+    const QOps QA = load_q(2 * it), QB = load_q(2 * it + 1);
+    f32x4 dqA[4], dqB[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dqA[dt] = dqB[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int sc = 0; sc < NP; ++sc) {
+      const int ta = 2 * sc * 16 + r, tb = ta + 16;
+      const bf16x8 ka0 = lds_row8(Ks, ta, g), ka1 = lds_row8(Ks, ta, 4 + g);
+      const bf16x8 va0 = lds_row8(Vs, ta, g), va1 = lds_row8(Vs, ta, 4 + g);
+      const bf16x8 kb0 = lds_row8(Ks, tb, g), kb1 = lds_row8(Ks, tb, 4 + g);
+      const bf16x8 vb0 = lds_row8(Vs, tb, g), vb1 = lds_row8(Vs, tb, 4 + g);
+      bf16x8 tk[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) tk[dt] = lds_trT(Ks, sc * 32, dt * 16, g, r);
+      {
+        const f32x4 d0 = ds_tile(QA, 2 * sc, ka0, ka1, va0, va1), d1 = ds_tile(QA, 2 * sc + 1, kb0, kb1, vb0, vb1);
+        bf16x8 dsf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dsf[i] = (bf16)d0[i];
+          dsf[4 + i] = (bf16)d1[i];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dqA[dt] = mfma16(tk[dt], dsf, dqA[dt]);
+      }
+      {
+        const f32x4 d0 = ds_tile(QB, 2 * sc, ka0, ka1, va0, va1), d1 = ds_tile(QB, 2 * sc + 1, kb0, kb1, vb0, vb1);
+        bf16x8 dsf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dsf[i] = (bf16)d0[i];
+          dsf[4 + i] = (bf16)d1[i];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dqB[dt] = mfma16(tk[dt], dsf, dqB[dt]);
+      }
+    }
+    if constexpr (NT16 & 1) {
+      const int t = NT16 - 1;
+      const bf16x8 k0 = lds_row8(Ks, t * 16 + r, g), k1 = lds_row8(Ks, t * 16 + r, 4 + g);
+      const bf16x8 v0 = lds_row8(Vs, t * 16 + r, g), v1 = lds_row8(Vs, t * 16 + r, 4 + g);
+      bf16x4 tk4[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) tk4[dt] = lds_trT4(Ks, t * 16, dt * 16, g, r);
+      f32x4 d0 = ds_tile(QA, t, k0, k1, v0, v1);
+      bf16x4 dsf = {(bf16)d0[0], (bf16)d0[1], (bf16)d0[2], (bf16)d0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dqA[dt] = mfma16k16(tk4[dt], dsf, dqA[dt]);
+      d0 = ds_tile(QB, t, k0, k1, v0, v1);
+      dsf = bf16x4{(bf16)d0[0], (bf16)d0[1], (bf16)d0[2], (bf16)d0[3]};
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dqB[dt] = mfma16k16(tk4[dt], dsf, dqB[dt]);
+    }
+    store(QA, dqA);
+    store(QB, dqB);
+  }
+}
+
 // ---- CLS-query attention (the last block: only the CLS rows reach the head) ---------------------
 // One wave per (image, head).  Lane (c = lane & 7, jg = lane >> 3) holds dims 8c..8c+7 and walks keys
 // j = jg, jg + 8, ...: each 8-lane group reads whole 128-B K / V rows (coalesced) and completes a
@@ -946,7 +1267,9 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
 // (measured faster: 108 vs 150 us at the F1 shape, scripts/attn_bench.py),
 // 3 = 168 VGPRs (three 52-KiB heads per CU, small spill)
 int g_attn_fwd_occ = 2;
-// backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 0 = the plain loops
+// backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 2 = the pipelined dQ
+// and the two-key-tiles-per-wave dK / dV (attn_bwd_dkv2_kernel), 3 = two query tiles per wave for dQ
+// (attn_bwd_dq2_kernel) and dkv2, 0 = the plain loops (all bit-identical)
 int g_attn_bwd_pipe = 1;
 
 }  // namespace
@@ -1011,10 +1334,20 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
   if (g_attn_bwd_pipe && nt16 == 13) {  // ViT/16 at 224^2 (T = 197): the pipelined loops
-    allow_lds(attn_bwd_dq_pipe_kernel<13>, lds_dq);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<13>), nimg * H, 256, lds_dq, stream, a);
-    allow_lds(attn_bwd_dkv_pipe_kernel<13>, lds_dkv);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<13>), nimg * H, 256, lds_dkv, stream, a);
+    if (g_attn_bwd_pipe == 3) {
+      allow_lds(attn_bwd_dq2_kernel<13>, lds_dq);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<13>), nimg * H, 256, lds_dq, stream, a);
+    } else {
+      allow_lds(attn_bwd_dq_pipe_kernel<13>, lds_dq);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<13>), nimg * H, 256, lds_dq, stream, a);
+    }
+    if (g_attn_bwd_pipe >= 2) {
+      allow_lds(attn_bwd_dkv2_kernel<13>, lds_dkv);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<13>), nimg * H, 256, lds_dkv, stream, a);
+    } else {
+      allow_lds(attn_bwd_dkv_pipe_kernel<13>, lds_dkv);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<13>), nimg * H, 256, lds_dkv, stream, a);
+    }
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);

@@ -47,7 +47,7 @@ def main():
     fwd = lambda: call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 0.125, s)  # noqa: E731
     bwd = lambda: call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(do), D, ptr(dqkv),  # noqa
                        3 * D, n, T, H, 0.125, s)
-    res = {"fwd_occ2": [], "fwd_occ3": [], "bwd_plain": [], "bwd_pipe": []}
+    res = {"fwd_occ2": [], "fwd_occ3": [], "bwd_plain": [], "bwd_pipe": [], "bwd_dkv2": [], "bwd_dq2_dkv2": []}
     outs = {}
     for _ in range(args.rounds):
         for occ in (2, 3):
@@ -55,12 +55,14 @@ def main():
             res[f"fwd_occ{occ}"].append(timed(fwd, args.iters))
         lib.es_set_attn_variant(2)
         fwd()
-        for v, name in ((0, "bwd_plain"), (1, "bwd_pipe")):
+        for v, name in ((0, "bwd_plain"), (1, "bwd_pipe"), (2, "bwd_dkv2"), (3, "bwd_dq2_dkv2")):
             lib.es_set_attn_bwd_variant(v)
             res[name].append(timed(bwd, args.iters))
             outs[name] = dqkv.clone()
     lib.es_set_attn_bwd_variant(1)
-    print("bwd pipe == plain (bit-exact):", torch.equal(outs["bwd_pipe"], outs["bwd_plain"]), flush=True)
+    print("bwd pipe == plain (bit-exact):", torch.equal(outs["bwd_pipe"], outs["bwd_plain"]),
+          "dkv2 == plain:", torch.equal(outs["bwd_dkv2"], outs["bwd_plain"]),
+          "dq2 + dkv2 == plain:", torch.equal(outs["bwd_dq2_dkv2"], outs["bwd_plain"]), flush=True)
     flops_f = 4.0 * n * H * T * T * 64
     out = {}
     for k, v in res.items():

@@ -285,8 +285,9 @@ def test_attention_bwd(n, T, H):
 
 @pytest.mark.parametrize("n", [3, 64])
 def test_attention_bwd_pipelined_matches_plain(n):
-    """The software-pipelined dQ / dK-dV loops (es_set_attn_bwd_variant 1, the default at T = 197) issue the
-    same MFMAs on the same operands in the same order as the plain loops: dqkv and delta bit-identical."""
+    """The software-pipelined dQ / dK-dV loops (es_set_attn_bwd_variant 1) and the two-key-tiles-per-wave
+    dK / dV (2) issue the same MFMAs on the same operands in the same order per key tile as the plain loops
+    (0): dqkv and delta bit-identical."""
     T, H = 197, 6
     D = H * 64
     torch.manual_seed(7 + n)
@@ -297,7 +298,7 @@ def test_attention_bwd_pipelined_matches_plain(n):
     call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
     res = {}
     lib = _lib.load()
-    for v in (0, 1):
+    for v in (0, 1, 2, 3):
         old = lib.es_set_attn_bwd_variant(v)
         dqkv = torch.full_like(qkv, 3.0)
         delta = torch.zeros(n * H * T, device=DEV)
@@ -306,8 +307,9 @@ def test_attention_bwd_pipelined_matches_plain(n):
         torch.cuda.synchronize()
         lib.es_set_attn_bwd_variant(old)
         res[v] = (dqkv[:n * T].clone(), delta)
-    assert torch.equal(res[0][0], res[1][0])
-    assert torch.equal(res[0][1], res[1][1])
+    for v in (1, 2, 3):
+        assert torch.equal(res[0][0], res[v][0]), v
+        assert torch.equal(res[0][1], res[v][1]), v
 
 
 @pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1),
