@@ -1269,8 +1269,9 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
 int g_attn_fwd_occ = 2;
 // backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 2 = the pipelined dQ
 // and the two-key-tiles-per-wave dK / dV (attn_bwd_dkv2_kernel), 3 = two query tiles per wave for dQ
-// (attn_bwd_dq2_kernel) and dkv2, 0 = the plain loops (all bit-identical)
-int g_attn_bwd_pipe = 1;
+// (attn_bwd_dq2_kernel) and dkv2, 0 = the plain loops (all bit-identical).  Default 3: 0.257 ms vs 0.269 (1) and
+// 0.289 (0) for the F1 head batch in isolation, F1 32.51-32.56 vs 32.69-32.72 ms (scripts/attn_bench.py, same box)
+int g_attn_bwd_pipe = 3;
 
 }  // namespace
 
@@ -1283,7 +1284,8 @@ int es_set_attn_variant(int occ) {
   return old;
 }
 
-// tuning knob: attention backward loops, 1 = software-pipelined (default), 0 = plain; returns the previous value
+// tuning knob: attention backward loops (0 plain, 1 pipelined, 2 pipelined dQ + dkv2, 3 dq2 + dkv2 = default);
+// returns the previous value
 int es_set_attn_bwd_variant(int v) {
   const int old = g_attn_bwd_pipe;
   g_attn_bwd_pipe = v;
