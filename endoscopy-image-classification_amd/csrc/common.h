@@ -84,6 +84,33 @@ __device__ __forceinline__ bf16x8 cat8(bf16x4 lo, bf16x4 hi) {
   return r;
 }
 
+// ---- activation-map element types (the CNN branch keeps its NHWC maps in fp32 or in bf16) ----------
+// Q4<T>::t: 4 consecutive map elements as loaded (16 bytes of fp32, 8 of bf16); q4_f32 widens them,
+// q4_b16 rounds them to the bf16 operand form (exact for bf16 maps), q4_store rounds fp32 values to T.
+template <typename T> struct Q4;
+template <> struct Q4<float> { typedef f32x4 t; };
+template <> struct Q4<bf16> { typedef bf16x4 t; };
+template <typename T> __device__ __forceinline__ typename Q4<T>::t q4_zero();
+template <> __device__ __forceinline__ f32x4 q4_zero<float>() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+template <> __device__ __forceinline__ bf16x4 q4_zero<bf16>() {
+  const bf16 z = (bf16)0.f;
+  return bf16x4{z, z, z, z};
+}
+__device__ __forceinline__ f32x4 q4_f32(f32x4 v) { return v; }
+__device__ __forceinline__ f32x4 q4_f32(bf16x4 v) { return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]}; }
+__device__ __forceinline__ bf16x4 q4_b16(bf16x4 v) { return v; }
+__device__ __forceinline__ bf16x4 q4_b16(f32x4 v) { return bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]}; }
+template <typename T> __device__ __forceinline__ typename Q4<T>::t q4_load(const T* p) {
+  return *(const typename Q4<T>::t*)p;
+}
+__device__ __forceinline__ void q4_store(float* p, f32x4 v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void q4_store(bf16* p, f32x4 v) { *(bf16x4*)p = q4_b16(v); }
+// scalar forms
+__device__ __forceinline__ float m_f32(float v) { return v; }
+__device__ __forceinline__ float m_f32(bf16 v) { return (float)v; }
+__device__ __forceinline__ void m_store(float* p, float v) { *p = v; }
+__device__ __forceinline__ void m_store(bf16* p, float v) { *p = (bf16)v; }
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

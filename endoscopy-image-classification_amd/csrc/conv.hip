@@ -432,16 +432,37 @@ __device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[VEC]
     for (int j = 0; j < VEC; ++j) p[j] = v[j];
   }
 }
+// bf16 maps: VEC consecutive elements widened to fp32 (VEC = 4: one 8-byte load) / rounded once on store
+template <int VEC>
+__device__ __forceinline__ void ldv(const bf16* __restrict__ p, float (&o)[VEC]) {
+  if constexpr (VEC == 4) {
+    const bf16x4 t = *(const bf16x4*)p;
+    o[0] = (float)t[0]; o[1] = (float)t[1]; o[2] = (float)t[2]; o[3] = (float)t[3];
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = (float)p[j];
+  }
+}
+template <int VEC>
+__device__ __forceinline__ void stv(bf16* __restrict__ p, const float (&v)[VEC]) {
+  if constexpr (VEC == 4) {
+    *(bf16x4*)p = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) p[j] = (bf16)v[j];
+  }
+}
 
 // MODE 0: sum v;  MODE 1: sum (v - mean[c])^2;  MODE 2: sum g, sum g * xhat  (g = dy * [y > 0 if relu],
 // xhat = (x - mean) * rstd), written as partial[block][c] and partial[block][C + c].
 // A thread owns VEC channels and walks every rp-th row of the block's chunk; contiguous views
 // (sn = HW * sp, every BatchNorm) take 4 rows per iteration so 4 (MODE 2: 12) loads are in flight.
-template <int MODE, int VEC>
-__global__ __launch_bounds__(256) void chan_partial_kernel(const float* __restrict__ v, RowMap rm, int rows, int C,
+// T: element type of the maps v, dy, y (fp32 or bf16); sums in fp32.
+template <int MODE, int VEC, typename T = float>
+__global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__ v, RowMap rm, int rows, int C,
                                                            int rows_per, const float* __restrict__ mean,
-                                                           const float* __restrict__ rstd, const float* __restrict__ dy,
-                                                           const float* __restrict__ y, int relu,
+                                                           const float* __restrict__ rstd, const T* __restrict__ dy,
+                                                           const T* __restrict__ y, int relu,
                                                            float* __restrict__ partial) {
   __shared__ float red[256 * VEC];
   __shared__ float red2[MODE == 2 ? 256 * VEC : 1];
@@ -581,11 +602,12 @@ __global__ void nbt_inc_kernel(int64_t* nbt) { *nbt += 1; }
 
 // y = (x - mean) * rstd * gamma + beta (+ res) (relu); eval: rstd from the running variance.
 // nv = elements / VEC, CV = C / VEC (32-bit index arithmetic: the host checks nv < 2^31)
-template <int VEC>
-__global__ void bn_apply_kernel(const float* __restrict__ x, int nv, int CV, const float* __restrict__ mean,
+// T: element type of the maps x, res, y (bf16 maps: widened on load, the result rounded once)
+template <int VEC, typename T = float>
+__global__ void bn_apply_kernel(const T* __restrict__ x, int nv, int CV, const float* __restrict__ mean,
                                 const float* __restrict__ rstd, const float* __restrict__ rvar, float eps,
                                 const float* __restrict__ gamma, const float* __restrict__ beta,
-                                const float* __restrict__ res, int relu, float* __restrict__ y) {
+                                const T* __restrict__ res, int relu, T* __restrict__ y) {
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
     const int c = (int)((unsigned)i % (unsigned)CV) * VEC;
     float xv[VEC], mu[VEC], ga[VEC], be[VEC], rs[VEC], rv[VEC], o[VEC];
@@ -618,12 +640,12 @@ __global__ void bn_apply_kernel(const float* __restrict__ x, int nv, int CV, con
 
 // dx = rstd * gamma * (g - sum(g)/P - xhat * sum(g xhat)/P); g = dy [* (y > 0)] (written to gout
 // when given: the residual branch's gradient)
-template <int VEC>
-__global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __restrict__ dy,
-                                    const float* __restrict__ y, int relu, int nv, int CV, int rows,
+template <int VEC, typename T = float>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                    const T* __restrict__ y, int relu, int nv, int CV, int rows,
                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                     const float* __restrict__ gamma, const float* __restrict__ sums,
-                                    float* __restrict__ dx, float* __restrict__ gout) {
+                                    T* __restrict__ dx, T* __restrict__ gout) {
   const float inv = 1.0f / (float)rows;
   const int C = CV * VEC;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
@@ -654,21 +676,23 @@ __global__ void bn_bwd_apply_kernel(const float* __restrict__ x, const float* __
 
 // eval-mode BatchNorm backward is an affine map: dx = g * gamma * rstd_running (not on the training
 // path; kept for completeness of the autograd surface)
-__global__ void bn_bwd_eval_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu, long n, int C,
+template <typename T = float>
+__global__ void bn_bwd_eval_kernel(const T* __restrict__ dy, const T* __restrict__ y, int relu, long n, int C,
                                    const float* __restrict__ rvar, float eps, const float* __restrict__ gamma,
-                                   float* __restrict__ dx, float* __restrict__ gout) {
+                                   T* __restrict__ dx, T* __restrict__ gout) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C);
-    float gg = dy[i];
-    if (relu && !(y[i] > 0.f)) gg = 0.f;
-    if (gout) gout[i] = gg;
-    dx[i] = gg * gamma[c] / sqrtf(rvar[c] + eps);
+    float gg = m_f32(dy[i]);
+    if (relu && !(m_f32(y[i]) > 0.f)) gg = 0.f;
+    if (gout) m_store(gout + i, gg);
+    m_store(dx + i, gg * gamma[c] / sqrtf(rvar[c] + eps));
   }
 }
 
 // ---- pooling / upsampling (NHWC contiguous)
+template <typename TO = float>
 __global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, int W, int C, int k, int s, int p,
-                                   int Ho, int Wo, float* __restrict__ y, int8_t* __restrict__ arg) {
+                                   int Ho, int Wo, TO* __restrict__ y, int8_t* __restrict__ arg) {
   const unsigned n_out = (unsigned)((long)N * Ho * Wo * C);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
     const int c = (int)(i % (unsigned)C);
@@ -692,12 +716,13 @@ __global__ void maxpool_fwd_kernel(const float* __restrict__ x, int N, int H, in
         }
       }
     }
-    y[i] = best;
+    m_store(y + i, best);
     arg[i] = (int8_t)bi;
   }
 }
 
-__global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int8_t* __restrict__ arg, int N, int H, int W,
+template <typename TI = float>
+__global__ void maxpool_bwd_kernel(const TI* __restrict__ dy, const int8_t* __restrict__ arg, int N, int H, int W,
                                    int C, int k, int s, int p, int Ho, int Wo, float* __restrict__ dx) {
   const unsigned n_in = (unsigned)((long)N * H * W * C);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
@@ -716,7 +741,7 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int8_t* _
         const int kx = w + p - wo * s;
         if (kx < 0 || kx >= k) continue;
         const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
-        if (arg[o] == ky * k + kx) acc += dy[o];
+        if (arg[o] == ky * k + kx) acc += m_f32(dy[o]);
       }
     }
     dx[i] = acc;
@@ -727,8 +752,9 @@ __global__ void maxpool_bwd_kernel(const float* __restrict__ dy, const int8_t* _
 // (the stem max-pool at S1 moves 1.2 GB in and 0.3 GB out per launch; the scalar forms ran at ~1.5
 // and ~0.9 TB/s)
 typedef char char4v __attribute__((ext_vector_type(4)));
+template <typename TO = float>
 __global__ void maxpool_fwd4_kernel(const float* __restrict__ x, int N, int H, int W, int C4, int k, int s, int p,
-                                    int Ho, int Wo, float* __restrict__ y, int8_t* __restrict__ arg) {
+                                    int Ho, int Wo, TO* __restrict__ y, int8_t* __restrict__ arg) {
   const unsigned n_out = (unsigned)((long)N * Ho * Wo * C4);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
     const int c4 = (int)(i % (unsigned)C4);
@@ -753,13 +779,14 @@ __global__ void maxpool_fwd4_kernel(const float* __restrict__ x, int N, int H, i
           }
       }
     }
-    *(f32x4*)(y + (size_t)i * 4) = best;
+    q4_store(y + (size_t)i * 4, best);  // (rounding commutes with the max: bf16 maps store bf16(max))
     const char4v a = {(char)bi[0], (char)bi[1], (char)bi[2], (char)bi[3]};
     *(char4v*)(arg + (size_t)i * 4) = a;
   }
 }
 
-__global__ void maxpool_bwd4_kernel(const float* __restrict__ dy, const int8_t* __restrict__ arg, int N, int H, int W,
+template <typename TI = float>
+__global__ void maxpool_bwd4_kernel(const TI* __restrict__ dy, const int8_t* __restrict__ arg, int N, int H, int W,
                                     int C4, int k, int s, int p, int Ho, int Wo, float* __restrict__ dx) {
   const unsigned n_in = (unsigned)((long)N * H * W * C4);
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
@@ -779,7 +806,7 @@ __global__ void maxpool_bwd4_kernel(const float* __restrict__ dy, const int8_t* 
         if (kx < 0 || kx >= k) continue;
         const long o = (((long)n * Ho + ho) * Wo + wo) * C4 + c4;
         const char4v a = *(const char4v*)(arg + o * 4);
-        const f32x4 g = *(const f32x4*)(dy + o * 4);
+        const f32x4 g = q4_f32(q4_load(dy + o * 4));
         const int tap = ky * k + kx;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -819,6 +846,74 @@ __global__ void avgpool_bwd_kernel(const float* __restrict__ dy, int N, int H, i
     const int h = (int)(t % (unsigned)H), n = (int)(t / (unsigned)H);
     const float v = dy[(((long)n * Ho + h / k) * Wo + w / k) * C + c] * inv;
     dx[i] = accumulate ? dx[i] + v : v;
+  }
+}
+
+// 4-channel forms over fp32 or bf16 maps (C % 4 == 0): TI / TO = input / output element type
+template <typename TI, typename TO>
+__global__ void avgpool_fwd4_kernel(const TI* __restrict__ x, int N, int H, int W, int C4, int k, int Ho, int Wo,
+                                    TO* __restrict__ y) {
+  const unsigned n_out = (unsigned)((long)N * Ho * Wo * C4);
+  const float inv = 1.0f / (float)(k * k);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_out; i += gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % (unsigned)C4);
+    unsigned t = i / (unsigned)C4;
+    const int wo = (int)(t % (unsigned)Wo);
+    t /= (unsigned)Wo;
+    const int ho = (int)(t % (unsigned)Ho), n = (int)(t / (unsigned)Ho);
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    for (int ky = 0; ky < k; ++ky)
+      for (int kx = 0; kx < k; ++kx)
+        s += q4_f32(q4_load(x + ((((long)n * H + ho * k + ky) * W + wo * k + kx) * C4 + c4) * 4));
+    q4_store(y + (size_t)i * 4, s * inv);
+  }
+}
+template <typename TI, typename TO>
+__global__ void avgpool_bwd4_kernel(const TI* __restrict__ dy, int N, int H, int W, int C4, int k, int Ho, int Wo,
+                                    TO* __restrict__ dx, int accumulate) {
+  const unsigned n_in = (unsigned)((long)N * H * W * C4);
+  const float inv = 1.0f / (float)(k * k);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n_in; i += gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % (unsigned)C4);
+    unsigned t = i / (unsigned)C4;
+    const int w = (int)(t % (unsigned)W);
+    t /= (unsigned)W;
+    const int h = (int)(t % (unsigned)H), n = (int)(t / (unsigned)H);
+    f32x4 v = q4_f32(q4_load(dy + ((((long)n * Ho + h / k) * Wo + w / k) * C4 + c4) * 4)) * inv;
+    if (accumulate) v += q4_f32(q4_load(dx + (size_t)i * 4));
+    q4_store(dx + (size_t)i * 4, v);
+  }
+}
+template <typename T>
+__global__ void upsample_add_fwd4_kernel(const T* __restrict__ base, const T* __restrict__ src, int N, int H, int W,
+                                         int C4, int s, T* __restrict__ out) {
+  const int h2 = H / s, w2 = W / s;
+  const unsigned n = (unsigned)((long)N * H * W * C4);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % (unsigned)C4);
+    unsigned t = i / (unsigned)C4;
+    const int w = (int)(t % (unsigned)W);
+    t /= (unsigned)W;
+    const int h = (int)(t % (unsigned)H), nn = (int)(t / (unsigned)H);
+    q4_store(out + (size_t)i * 4, q4_f32(q4_load(base + (size_t)i * 4)) +
+                                      q4_f32(q4_load(src + ((((long)nn * h2 + h / s) * w2 + w / s) * C4 + c4) * 4)));
+  }
+}
+template <typename T>
+__global__ void upsample_bwd4_kernel(const T* __restrict__ dout, int N, int H, int W, int C4, int s,
+                                     T* __restrict__ dsrc) {
+  const int h2 = H / s, w2 = W / s;
+  const unsigned n = (unsigned)((long)N * h2 * w2 * C4);
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % (unsigned)C4);
+    unsigned t = i / (unsigned)C4;
+    const int ws = (int)(t % (unsigned)w2);
+    t /= (unsigned)w2;
+    const int hs = (int)(t % (unsigned)h2), nn = (int)(t / (unsigned)h2);
+    f32x4 a = {0.f, 0.f, 0.f, 0.f};
+    for (int dy = 0; dy < s; ++dy)
+      for (int dx = 0; dx < s; ++dx) a += q4_f32(q4_load(dout + ((((long)nn * H + hs * s + dy) * W + ws * s + dx) * C4 + c4) * 4));
+    q4_store(dsrc + (size_t)i * 4, a);
   }
 }
 
@@ -1124,6 +1219,219 @@ __global__ void bn_param_grads_kernel(const float* __restrict__ sums_local, int 
   dgamma[c] = accumulate ? dgamma[c] + sums_local[C + c] : sums_local[C + c];
 }
 
+
+// ---- host launchers templated on the map element type T (float or bf16); the extern "C" entry points
+// below pick T from their flags (bit 0: the maps are bf16) -------------------------------------------
+template <typename T>
+bool map_v4(int C, const void* a, const void* b = nullptr, const void* c = nullptr, const void* d = nullptr,
+            const void* e = nullptr) {
+  return C % 4 == 0 && al16(a) && (!b || al16(b)) && (!c || al16(c)) && (!d || al16(d)) && (!e || al16(e));
+}
+
+template <typename T>
+void bn_apply_launch(bool v4, const T* x, long n, int C, const float* mu, const float* rs, const float* rv, float eps,
+                     const float* gamma, const float* beta, const T* res, int relu, T* y, hipStream_t stream) {
+  if (v4)
+    hipLaunchKernelGGL((bn_apply_kernel<4, T>), grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mu, rs, rv, eps,
+                       gamma, beta, res, relu, y);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<1, T>), grid1d(n), 256, 0, stream, x, (int)n, C, mu, rs, rv, eps, gamma, beta,
+                       res, relu, y);
+}
+
+template <int MODE, typename T>
+void chan_partial_launch(bool v4, int G, const T* v, RowMap rm, int rows, int C, int per, const float* mean,
+                         const float* rstd, const T* dy, const T* y, int relu, float* ws, hipStream_t stream) {
+  if (v4)
+    hipLaunchKernelGGL((chan_partial_kernel<MODE, 4, T>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd, dy, y, relu,
+                       ws);
+  else
+    hipLaunchKernelGGL((chan_partial_kernel<MODE, 1, T>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd, dy, y, relu,
+                       ws);
+}
+
+template <typename T>
+int chan_sum_impl(const T* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out, int accumulate,
+                  hipStream_t stream) {
+  if (!v || !out || !workspace) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || HW <= 0) return ES_BAD_SHAPE;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{sn, sp, HW};
+  chan_partial_launch<0, T>(C % 4 == 0 && sn % 4 == 0 && sp % 4 == 0 && al16(v), G, v, rm, rows, C, per, nullptr,
+                            nullptr, nullptr, nullptr, 0, workspace, stream);
+  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, accumulate};
+  hipLaunchKernelGGL(chan_final_kernel<0>, (C + 15) / 16, 256, 0, stream, workspace, G, C, f);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_fwd_impl(const T* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                  float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const T* res,
+                  int relu, T* y, float* mean, float* rstd, float* workspace, hipStream_t stream) {
+  if (!x || !gamma || !beta || !y || !running_mean || !running_var) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(running_mean) && al16(running_var) &&
+                  (!mean || al16(mean)) && (!rstd || al16(rstd));
+  if (!train) {
+    bn_apply_launch<T>(v4, x, n, C, running_mean, nullptr, running_var, eps, gamma, beta, res, relu, y, stream);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
+  if (!mean || !rstd || !workspace) return ES_BAD_ARG;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  const dim3 fg((C + 15) / 16);
+  ChanFin fm{mean, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
+  ChanFin fv{rstd, nullptr, nullptr, mean, running_mean, running_var, eps, momentum, rows, 0, 0};
+  chan_partial_launch<0, T>(v4, G, x, rm, rows, C, per, nullptr, nullptr, nullptr, nullptr, 0, workspace, stream);
+  hipLaunchKernelGGL(chan_final_kernel<1>, fg, 256, 0, stream, workspace, G, C, fm);
+  chan_partial_launch<1, T>(v4, G, x, rm, rows, C, per, mean, nullptr, nullptr, nullptr, 0, workspace, stream);
+  hipLaunchKernelGGL(chan_final_kernel<2>, fg, 256, 0, stream, workspace, G, C, fv);
+  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+  bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_bwd_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu, const float* gamma, const float* mean,
+                  const float* rstd, int train, const float* running_var, float eps, T* dx, T* gout, float* dgamma,
+                  float* dbeta, int accumulate, float* workspace, hipStream_t stream) {
+  if (!x || !dy || !dx || !gamma || (relu && !y)) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  if (!train) {
+    if (!running_var) return ES_BAD_ARG;
+    hipLaunchKernelGGL(bn_bwd_eval_kernel<T>, grid1d(n), 256, 0, stream, dy, y, relu, n, C, running_var, eps, gamma, dx,
+                       gout);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
+  if (!mean || !rstd || !workspace || !dgamma || !dbeta) return ES_BAD_ARG;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  float* sums = workspace + (size_t)G * 2 * C;  // [2C]: sum g, sum g xhat
+  const bool v4 = map_v4<T>(C, x, dy, y, dx, gout) && al16(mean) && al16(rstd) && al16(gamma) && al16(sums);
+  chan_partial_launch<2, T>(v4, G, x, rm, rows, C, per, mean, rstd, dy, y, relu, workspace, stream);
+  // sums[0..C) = sum g -> dbeta, sums[C..2C) = sum g xhat -> dgamma
+  ChanFin f{dbeta, dgamma, sums, nullptr, nullptr, nullptr, 0.f, 0.f, rows, C, accumulate};
+  hipLaunchKernelGGL(chan_final_kernel<3>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
+  if (v4)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
+                       rows, mean, rstd, gamma, sums, dx, gout);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows, mean,
+                       rstd, gamma, sums, dx, gout);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_sums_impl(const T* x, int rows, int C, int mode, const float* sum_g, int rows_g, float* out, float* workspace,
+                   hipStream_t stream) {
+  if (!x || !out || !workspace || (mode == 1 && !sum_g)) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || (mode != 0 && mode != 1) || (mode == 1 && rows_g <= 0)) return ES_BAD_SHAPE;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  float* mean = workspace + (size_t)G * 2 * C;  // [C] (the tail es_bn2d_bwd keeps for its sums)
+  const bool v4 = C % 4 == 0 && al16(x) && al16(mean);
+  if (mode == 1)
+    hipLaunchKernelGGL(bn_mean_from_sum_kernel, (C + 255) / 256, 256, 0, stream, sum_g, (float)rows_g, C, mean);
+  if (mode == 0)
+    chan_partial_launch<0, T>(v4, G, x, rm, rows, C, per, mean, nullptr, nullptr, nullptr, 0, workspace, stream);
+  else
+    chan_partial_launch<1, T>(v4, G, x, rm, rows, C, per, mean, nullptr, nullptr, nullptr, 0, workspace, stream);
+  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
+  hipLaunchKernelGGL(chan_final_kernel<0>, (C + 15) / 16, 256, 0, stream, workspace, G, C, f);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_fwd_global_impl(const T* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                         float* running_var, void* num_batches_tracked, float momentum, float eps, const float* sum_g,
+                         const float* sq_g, int rows_g, const T* res, int relu, T* y, float* mean, float* rstd,
+                         hipStream_t stream) {
+  if (!x || !gamma || !beta || !running_mean || !running_var || !sum_g || !sq_g || !y || !mean || !rstd)
+    return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || rows_g < rows) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(bn_finalize_global_kernel, (C + 255) / 256, 256, 0, stream, sum_g, sq_g, (float)rows_g, C, eps,
+                     momentum, mean, rstd, running_mean, running_var);
+  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+  const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
+  bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_fwd_partials_impl(const T* x, int rows, int C, float* partials, const float* gamma, const float* beta,
+                           float* running_mean, float* running_var, void* num_batches_tracked, float momentum, float eps,
+                           const T* res, int relu, T* y, float* mean, float* rstd, hipStream_t stream) {
+  if (!x || !partials || !gamma || !beta || !running_mean || !running_var || !y || !mean || !rstd) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  const int nblk = (rows + 127) / 128, G = 64;
+  float* P = partials;  // level 1 overwrites group-leading slots in place
+  if (nblk > G) {
+    const int ng = (nblk + G - 1) / G;
+    hipLaunchKernelGGL(bn_stats_from_partials_kernel<false>, dim3((C + 63) / 64, ng), 256, 0, stream, P, nblk, 128, 1,
+                       G, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+    hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, ng, 128 * G, G,
+                       ng, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+  } else {
+    hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, nblk, 128, 1,
+                       nblk, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+  }
+  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+  const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
+  bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_bwd_sums_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu, const float* mean,
+                       const float* rstd, float* out, float* workspace, hipStream_t stream) {
+  if (!x || !dy || !mean || !rstd || !out || !workspace || (relu && !y)) return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
+  const int G = chan_groups(rows);
+  const int per = (rows + G - 1) / G;
+  const RowMap rm{(long)rows * C, (long)C, rows};
+  const bool v4 = map_v4<T>(C, x, dy, y) && al16(mean) && al16(rstd);
+  chan_partial_launch<2, T>(v4, G, x, rm, rows, C, per, mean, rstd, dy, y, relu, workspace, stream);
+  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
+  hipLaunchKernelGGL(chan_final_kernel<0>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+template <typename T>
+int bn2d_bwd_global_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu, const float* gamma,
+                         const float* mean, const float* rstd, const float* sums_local, const float* sums_g, int rows_g,
+                         T* dx, T* gout, float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
+  if (!x || !dy || !gamma || !mean || !rstd || !sums_local || !sums_g || !dx || !dgamma || !dbeta || (relu && !y))
+    return ES_BAD_ARG;
+  if (rows <= 0 || C <= 0 || rows_g < rows) return ES_BAD_SHAPE;
+  const long n = (long)rows * C;
+  if (n >= (1L << 31)) return ES_BAD_SHAPE;
+  hipLaunchKernelGGL(bn_param_grads_kernel, (C + 255) / 256, 256, 0, stream, sums_local, C, dgamma, dbeta, accumulate);
+  const bool v4 = map_v4<T>(C, x, dy, y, dx, gout) && al16(mean) && al16(rstd) && al16(gamma) && al16(sums_g);
+  if (v4)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
+                       rows_g, mean, rstd, gamma, sums_g, dx, gout);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows_g, mean,
+                       rstd, gamma, sums_g, dx, gout);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// flags of the map entry points: bit 0 = the (input) maps are bf16; pools / upsampling: bit 1 = the output
+// map is bf16 (bit 0 the input)
+constexpr int MAPS_BF16 = 1, OUT_BF16 = 2;
+
 }  // namespace
 
 extern "C" {
@@ -1212,20 +1520,14 @@ size_t es_chan_workspace(int rows, int C) {
 // out[c] (+)= sum over rows of v; row r at (r / HW) * sn + (r % HW) * sp (bias gradients)
 int es_chan_sum(const float* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
                 int accumulate, hipStream_t stream) {
-  if (!v || !out || !workspace) return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0 || HW <= 0) return ES_BAD_SHAPE;
-  const int G = chan_groups(rows);
-  const int per = (rows + G - 1) / G;
-  const RowMap rm{sn, sp, HW};
-  if (C % 4 == 0 && sn % 4 == 0 && sp % 4 == 0 && al16(v))
-    hipLaunchKernelGGL((chan_partial_kernel<0, 4>), G, 256, 0, stream, v, rm, rows, C, per, nullptr, nullptr, nullptr,
-                       nullptr, 0, workspace);
-  else
-    hipLaunchKernelGGL((chan_partial_kernel<0, 1>), G, 256, 0, stream, v, rm, rows, C, per, nullptr, nullptr, nullptr,
-                       nullptr, 0, workspace);
-  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, accumulate};
-  hipLaunchKernelGGL(chan_final_kernel<0>, (C + 15) / 16, 256, 0, stream, workspace, G, C, f);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return chan_sum_impl<float>(v, rows, C, sn, sp, HW, workspace, out, accumulate, stream);
+}
+// es_chan_sum over an fp32 (flags 0) or bf16 (flags 1) map
+int es_chan_sum_ex(const void* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
+                   int accumulate, int flags, hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  return flags ? chan_sum_impl<bf16>((const bf16*)v, rows, C, sn, sp, HW, workspace, out, accumulate, stream)
+               : chan_sum_impl<float>((const float*)v, rows, C, sn, sp, HW, workspace, out, accumulate, stream);
 }
 
 // BatchNorm2d over x [rows = N*H*W, C] (NHWC contiguous).  train: batch mean / biased variance,
@@ -1234,48 +1536,20 @@ int es_chan_sum(const float* v, int rows, int C, long sn, long sp, int HW, float
 int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
                 float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const float* res,
                 int relu, float* y, float* mean, float* rstd, float* workspace, hipStream_t stream) {
-  if (!x || !gamma || !beta || !y || !running_mean || !running_var) return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
-  const long n = (long)rows * C;
-  if (n >= (1L << 31)) return ES_BAD_SHAPE;
-  const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) &&
-                  al16(running_mean) && al16(running_var) && (!mean || al16(mean)) && (!rstd || al16(rstd));
-  auto apply = [&](const float* mu, const float* rs, const float* rv) {
-    if (v4)
-      hipLaunchKernelGGL(bn_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mu, rs, rv, eps,
-                         gamma, beta, res, relu, y);
-    else
-      hipLaunchKernelGGL(bn_apply_kernel<1>, grid1d(n), 256, 0, stream, x, (int)n, C, mu, rs, rv, eps, gamma, beta,
-                         res, relu, y);
-  };
-  if (!train) {
-    apply(running_mean, nullptr, running_var);
-    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-  }
-  if (!mean || !rstd || !workspace) return ES_BAD_ARG;
-  const int G = chan_groups(rows);
-  const int per = (rows + G - 1) / G;
-  const RowMap rm{(long)rows * C, (long)C, rows};
-  const dim3 fg((C + 15) / 16);
-  ChanFin fm{mean, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
-  ChanFin fv{rstd, nullptr, nullptr, mean, running_mean, running_var, eps, momentum, rows, 0, 0};
-  if (v4) {
-    hipLaunchKernelGGL((chan_partial_kernel<0, 4>), G, 256, 0, stream, x, rm, rows, C, per, nullptr, nullptr, nullptr,
-                       nullptr, 0, workspace);
-    hipLaunchKernelGGL(chan_final_kernel<1>, fg, 256, 0, stream, workspace, G, C, fm);
-    hipLaunchKernelGGL((chan_partial_kernel<1, 4>), G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr,
-                       nullptr, 0, workspace);
-  } else {
-    hipLaunchKernelGGL((chan_partial_kernel<0, 1>), G, 256, 0, stream, x, rm, rows, C, per, nullptr, nullptr, nullptr,
-                       nullptr, 0, workspace);
-    hipLaunchKernelGGL(chan_final_kernel<1>, fg, 256, 0, stream, workspace, G, C, fm);
-    hipLaunchKernelGGL((chan_partial_kernel<1, 1>), G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr,
-                       nullptr, 0, workspace);
-  }
-  hipLaunchKernelGGL(chan_final_kernel<2>, fg, 256, 0, stream, workspace, G, C, fv);
-  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
-  apply(mean, rstd, nullptr);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_fwd_impl<float>(x, rows, C, gamma, beta, running_mean, running_var, num_batches_tracked, momentum, eps,
+                              train, res, relu, y, mean, rstd, workspace, stream);
+}
+// es_bn2d_fwd with x / res / y as fp32 (flags 0) or bf16 (flags 1) maps: statistics and the affine map in
+// fp32, y rounded once
+int es_bn2d_fwd_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                   float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const void* res,
+                   int relu, void* y, float* mean, float* rstd, float* workspace, int flags, hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_fwd_impl<bf16>((const bf16*)x, rows, C, gamma, beta, running_mean, running_var, num_batches_tracked,
+                               momentum, eps, train, (const bf16*)res, relu, (bf16*)y, mean, rstd, workspace, stream);
+  return bn2d_fwd_impl<float>((const float*)x, rows, C, gamma, beta, running_mean, running_var, num_batches_tracked,
+                              momentum, eps, train, (const float*)res, relu, (float*)y, mean, rstd, workspace, stream);
 }
 
 // Backward of es_bn2d_fwd (train mode): g = dy * [y > 0 if relu] (written to gout when non-null: the
@@ -1284,39 +1558,21 @@ int es_bn2d_fwd(const float* x, int rows, int C, const float* gamma, const float
 int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
                 const float* mean, const float* rstd, int train, const float* running_var, float eps, float* dx,
                 float* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t stream) {
-  if (!x || !dy || !dx || !gamma || (relu && !y)) return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
-  const long n = (long)rows * C;
-  if (n >= (1L << 31)) return ES_BAD_SHAPE;
-  if (!train) {
-    if (!running_var) return ES_BAD_ARG;
-    hipLaunchKernelGGL(bn_bwd_eval_kernel, grid1d(n), 256, 0, stream, dy, y, relu, n, C, running_var, eps, gamma, dx,
-                       gout);
-    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-  }
-  if (!mean || !rstd || !workspace || !dgamma || !dbeta) return ES_BAD_ARG;
-  const int G = chan_groups(rows);
-  const int per = (rows + G - 1) / G;
-  const RowMap rm{(long)rows * C, (long)C, rows};
-  float* sums = workspace + (size_t)G * 2 * C;  // [2C]: sum g, sum g xhat
-  const bool v4 = C % 4 == 0 && al16(x) && al16(dy) && (!y || al16(y)) && al16(dx) && (!gout || al16(gout)) &&
-                  al16(mean) && al16(rstd) && al16(gamma) && al16(sums);
-  if (v4)
-    hipLaunchKernelGGL((chan_partial_kernel<2, 4>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       workspace);
-  else
-    hipLaunchKernelGGL((chan_partial_kernel<2, 1>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       workspace);
-  // sums[0..C) = sum g -> dbeta, sums[C..2C) = sum g xhat -> dgamma
-  ChanFin f{dbeta, dgamma, sums, nullptr, nullptr, nullptr, 0.f, 0.f, rows, C, accumulate};
-  hipLaunchKernelGGL(chan_final_kernel<3>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
-  if (v4)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
-                       rows, mean, rstd, gamma, sums, dx, gout);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows, mean, rstd,
-                       gamma, sums, dx, gout);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_bwd_impl<float>(x, y, dy, rows, C, relu, gamma, mean, rstd, train, running_var, eps, dx, gout, dgamma,
+                              dbeta, accumulate, workspace, stream);
+}
+// es_bn2d_bwd with x / y / dy / dx / gout as fp32 (flags 0) or bf16 (flags 1) maps (sums in fp32)
+int es_bn2d_bwd_ex(const void* x, const void* y, const void* dy, int rows, int C, int relu, const float* gamma,
+                   const float* mean, const float* rstd, int train, const float* running_var, float eps, void* dx,
+                   void* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, int flags,
+                   hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_bwd_impl<bf16>((const bf16*)x, (const bf16*)y, (const bf16*)dy, rows, C, relu, gamma, mean, rstd, train,
+                               running_var, eps, (bf16*)dx, (bf16*)gout, dgamma, dbeta, accumulate, workspace, stream);
+  return bn2d_bwd_impl<float>((const float*)x, (const float*)y, (const float*)dy, rows, C, relu, gamma, mean, rstd,
+                              train, running_var, eps, (float*)dx, (float*)gout, dgamma, dbeta, accumulate, workspace,
+                              stream);
 }
 
 // ---- SyncBatchNorm2d (the Conformer's BatchNorm2d over the global batch at N > 1) ------------
@@ -1325,27 +1581,13 @@ int es_bn2d_bwd(const float* x, const float* y, const float* dy, int rows, int C
 // sums).  workspace: es_chan_workspace(rows, C) floats.
 int es_bn2d_sums(const float* x, int rows, int C, int mode, const float* sum_g, int rows_g, float* out,
                  float* workspace, hipStream_t stream) {
-  if (!x || !out || !workspace || (mode == 1 && !sum_g)) return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0 || (mode != 0 && mode != 1) || (mode == 1 && rows_g <= 0)) return ES_BAD_SHAPE;
-  const int G = chan_groups(rows);
-  const int per = (rows + G - 1) / G;
-  const RowMap rm{(long)rows * C, (long)C, rows};
-  float* mean = workspace + (size_t)G * 2 * C;  // [C] (the tail es_bn2d_bwd keeps for its sums)
-  const bool v4 = C % 4 == 0 && al16(x) && al16(mean);
-  if (mode == 1)
-    hipLaunchKernelGGL(bn_mean_from_sum_kernel, (C + 255) / 256, 256, 0, stream, sum_g, (float)rows_g, C, mean);
-#define BN_SUMS(MODE_, V_)                                                                                      \
-  hipLaunchKernelGGL((chan_partial_kernel<MODE_, V_>), G, 256, 0, stream, x, rm, rows, C, per, mean, nullptr, nullptr, \
-                     nullptr, 0, workspace)
-  if (mode == 0) {
-    if (v4) BN_SUMS(0, 4); else BN_SUMS(0, 1);
-  } else {
-    if (v4) BN_SUMS(1, 4); else BN_SUMS(1, 1);
-  }
-#undef BN_SUMS
-  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
-  hipLaunchKernelGGL(chan_final_kernel<0>, (C + 15) / 16, 256, 0, stream, workspace, G, C, f);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_sums_impl<float>(x, rows, C, mode, sum_g, rows_g, out, workspace, stream);
+}
+int es_bn2d_sums_ex(const void* x, int rows, int C, int mode, const float* sum_g, int rows_g, float* out,
+                    float* workspace, int flags, hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  return flags ? bn2d_sums_impl<bf16>((const bf16*)x, rows, C, mode, sum_g, rows_g, out, workspace, stream)
+               : bn2d_sums_impl<float>((const float*)x, rows, C, mode, sum_g, rows_g, out, workspace, stream);
 }
 
 // Train-mode BatchNorm2d from the global sums (sum_g, centred sq_g over rows_g rows): mean / rstd
@@ -1355,23 +1597,21 @@ int es_bn2d_fwd_global(const float* x, int rows, int C, const float* gamma, cons
                        float* running_var, void* num_batches_tracked, float momentum, float eps, const float* sum_g,
                        const float* sq_g, int rows_g, const float* res, int relu, float* y, float* mean, float* rstd,
                        hipStream_t stream) {
-  if (!x || !gamma || !beta || !running_mean || !running_var || !sum_g || !sq_g || !y || !mean || !rstd)
-    return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0 || rows_g < rows) return ES_BAD_SHAPE;
-  const long n = (long)rows * C;
-  if (n >= (1L << 31)) return ES_BAD_SHAPE;
-  hipLaunchKernelGGL(bn_finalize_global_kernel, (C + 255) / 256, 256, 0, stream, sum_g, sq_g, (float)rows_g, C, eps,
-                     momentum, mean, rstd, running_mean, running_var);
-  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
-  const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) && al16(mean) &&
-                  al16(rstd);
-  if (v4)
-    hipLaunchKernelGGL(bn_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mean, rstd, nullptr,
-                       eps, gamma, beta, res, relu, y);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<1>, grid1d(n), 256, 0, stream, x, (int)n, C, mean, rstd, nullptr, eps, gamma,
-                       beta, res, relu, y);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_fwd_global_impl<float>(x, rows, C, gamma, beta, running_mean, running_var, num_batches_tracked, momentum,
+                                     eps, sum_g, sq_g, rows_g, res, relu, y, mean, rstd, stream);
+}
+int es_bn2d_fwd_global_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, void* num_batches_tracked, float momentum, float eps, const float* sum_g,
+                          const float* sq_g, int rows_g, const void* res, int relu, void* y, float* mean, float* rstd,
+                          int flags, hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_fwd_global_impl<bf16>((const bf16*)x, rows, C, gamma, beta, running_mean, running_var,
+                                      num_batches_tracked, momentum, eps, sum_g, sq_g, rows_g, (const bf16*)res, relu,
+                                      (bf16*)y, mean, rstd, stream);
+  return bn2d_fwd_global_impl<float>((const float*)x, rows, C, gamma, beta, running_mean, running_var,
+                                     num_batches_tracked, momentum, eps, sum_g, sq_g, rows_g, (const float*)res, relu,
+                                     (float*)y, mean, rstd, stream);
 }
 
 // Train-mode BatchNorm2d whose batch statistics come from the producing conv's per-block partials
@@ -1381,53 +1621,37 @@ int es_bn2d_fwd_partials(const float* x, int rows, int C, float* partials, const
                          const float* beta, float* running_mean, float* running_var, void* num_batches_tracked,
                          float momentum, float eps, const float* res, int relu, float* y, float* mean, float* rstd,
                          hipStream_t stream) {
-  if (!x || !partials || !gamma || !beta || !running_mean || !running_var || !y || !mean || !rstd) return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
-  const long n = (long)rows * C;
-  if (n >= (1L << 31)) return ES_BAD_SHAPE;
-  const int nblk = (rows + 127) / 128, G = 64;
-  float* P = (float*)partials;  // level 1 overwrites group-leading slots in place
-  if (nblk > G) {
-    const int ng = (nblk + G - 1) / G;
-    hipLaunchKernelGGL(bn_stats_from_partials_kernel<false>, dim3((C + 63) / 64, ng), 256, 0, stream, P, nblk, 128, 1,
-                       G, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
-    hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, ng, 128 * G, G,
-                       ng, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
-  } else {
-    hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, nblk, 128, 1,
-                       nblk, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
-  }
-  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
-  const bool v4 = C % 4 == 0 && al16(x) && al16(y) && (!res || al16(res)) && al16(gamma) && al16(beta) && al16(mean) &&
-                  al16(rstd);
-  if (v4)
-    hipLaunchKernelGGL(bn_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mean, rstd, nullptr,
-                       eps, gamma, beta, res, relu, y);
-  else
-    hipLaunchKernelGGL(bn_apply_kernel<1>, grid1d(n), 256, 0, stream, x, (int)n, C, mean, rstd, nullptr, eps, gamma,
-                       beta, res, relu, y);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_fwd_partials_impl<float>(x, rows, C, partials, gamma, beta, running_mean, running_var,
+                                       num_batches_tracked, momentum, eps, res, relu, y, mean, rstd, stream);
+}
+int es_bn2d_fwd_partials_ex(const void* x, int rows, int C, float* partials, const float* gamma, const float* beta,
+                            float* running_mean, float* running_var, void* num_batches_tracked, float momentum,
+                            float eps, const void* res, int relu, void* y, float* mean, float* rstd, int flags,
+                            hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_fwd_partials_impl<bf16>((const bf16*)x, rows, C, partials, gamma, beta, running_mean, running_var,
+                                        num_batches_tracked, momentum, eps, (const bf16*)res, relu, (bf16*)y, mean,
+                                        rstd, stream);
+  return bn2d_fwd_partials_impl<float>((const float*)x, rows, C, partials, gamma, beta, running_mean, running_var,
+                                       num_batches_tracked, momentum, eps, (const float*)res, relu, (float*)y, mean,
+                                       rstd, stream);
 }
 
 // Backward, local half: out[0..C) = sum g, out[C..2C) = sum g xhat over this rank's rows
 // (g = dy * [y > 0 if relu]).  workspace: es_chan_workspace(rows, C) floats.
 int es_bn2d_bwd_sums(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* mean,
                      const float* rstd, float* out, float* workspace, hipStream_t stream) {
-  if (!x || !dy || !mean || !rstd || !out || !workspace || (relu && !y)) return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
-  const int G = chan_groups(rows);
-  const int per = (rows + G - 1) / G;
-  const RowMap rm{(long)rows * C, (long)C, rows};
-  const bool v4 = C % 4 == 0 && al16(x) && al16(dy) && (!y || al16(y)) && al16(mean) && al16(rstd);
-  if (v4)
-    hipLaunchKernelGGL((chan_partial_kernel<2, 4>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       workspace);
-  else
-    hipLaunchKernelGGL((chan_partial_kernel<2, 1>), G, 256, 0, stream, x, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       workspace);
-  ChanFin f{out, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
-  hipLaunchKernelGGL(chan_final_kernel<0>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_bwd_sums_impl<float>(x, y, dy, rows, C, relu, mean, rstd, out, workspace, stream);
+}
+int es_bn2d_bwd_sums_ex(const void* x, const void* y, const void* dy, int rows, int C, int relu, const float* mean,
+                        const float* rstd, float* out, float* workspace, int flags, hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_bwd_sums_impl<bf16>((const bf16*)x, (const bf16*)y, (const bf16*)dy, rows, C, relu, mean, rstd, out,
+                                    workspace, stream);
+  return bn2d_bwd_sums_impl<float>((const float*)x, (const float*)y, (const float*)dy, rows, C, relu, mean, rstd, out,
+                                   workspace, stream);
 }
 
 // Backward, global half: dx = rstd gamma (g - sum_g g / rows_g - xhat sum_g (g xhat) / rows_g) with the
@@ -1436,94 +1660,197 @@ int es_bn2d_bwd_sums(const float* x, const float* y, const float* dy, int rows, 
 int es_bn2d_bwd_global(const float* x, const float* y, const float* dy, int rows, int C, int relu, const float* gamma,
                        const float* mean, const float* rstd, const float* sums_local, const float* sums_g, int rows_g,
                        float* dx, float* gout, float* dgamma, float* dbeta, int accumulate, hipStream_t stream) {
-  if (!x || !dy || !gamma || !mean || !rstd || !sums_local || !sums_g || !dx || !dgamma || !dbeta || (relu && !y))
-    return ES_BAD_ARG;
-  if (rows <= 0 || C <= 0 || rows_g < rows) return ES_BAD_SHAPE;
-  const long n = (long)rows * C;
-  if (n >= (1L << 31)) return ES_BAD_SHAPE;
-  hipLaunchKernelGGL(bn_param_grads_kernel, (C + 255) / 256, 256, 0, stream, sums_local, C, dgamma, dbeta, accumulate);
-  const bool v4 = C % 4 == 0 && al16(x) && al16(dy) && (!y || al16(y)) && al16(dx) && (!gout || al16(gout)) &&
-                  al16(mean) && al16(rstd) && al16(gamma) && al16(sums_g);
-  if (v4)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
-                       rows_g, mean, rstd, gamma, sums_g, dx, gout);
-  else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<1>, grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows_g, mean,
-                       rstd, gamma, sums_g, dx, gout);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return bn2d_bwd_global_impl<float>(x, y, dy, rows, C, relu, gamma, mean, rstd, sums_local, sums_g, rows_g, dx, gout,
+                                     dgamma, dbeta, accumulate, stream);
+}
+int es_bn2d_bwd_global_ex(const void* x, const void* y, const void* dy, int rows, int C, int relu, const float* gamma,
+                          const float* mean, const float* rstd, const float* sums_local, const float* sums_g, int rows_g,
+                          void* dx, void* gout, float* dgamma, float* dbeta, int accumulate, int flags,
+                          hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_bwd_global_impl<bf16>((const bf16*)x, (const bf16*)y, (const bf16*)dy, rows, C, relu, gamma, mean, rstd,
+                                      sums_local, sums_g, rows_g, (bf16*)dx, (bf16*)gout, dgamma, dbeta, accumulate,
+                                      stream);
+  return bn2d_bwd_global_impl<float>((const float*)x, (const float*)y, (const float*)dy, rows, C, relu, gamma, mean,
+                                     rstd, sums_local, sums_g, rows_g, (float*)dx, (float*)gout, dgamma, dbeta,
+                                     accumulate, stream);
 }
 
-// MaxPool2d(k, s, p) over NHWC; arg = int8 window index of the (first) maximum
-int es_maxpool2d_fwd(const float* x, int N, int H, int W, int C, int k, int s, int p, float* y, void* arg,
-                     hipStream_t stream) {
-  if (!x || !y || !arg) return ES_BAD_ARG;
+// MaxPool2d(k, s, p) over NHWC; arg = int8 window index of the (first) maximum.  _ex flags: 2 = y is a
+// bf16 map (x stays fp32: the stem's BatchNorm output)
+int es_maxpool2d_fwd_ex(const float* x, int N, int H, int W, int C, int k, int s, int p, void* y, void* arg, int flags,
+                        hipStream_t stream) {
+  if (!x || !y || !arg || (flags & ~OUT_BF16)) return ES_BAD_ARG;
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 11 || s <= 0 || p < 0 || 2 * p > k) return ES_BAD_SHAPE;
   if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
-  if (C % 4 == 0)
-    hipLaunchKernelGGL(maxpool_fwd4_kernel, grid1d((long)N * Ho * Wo * C / 4), 256, 0, stream, x, N, H, W, C / 4, k, s,
-                       p, Ho, Wo, y, (int8_t*)arg);
-  else
-    hipLaunchKernelGGL(maxpool_fwd_kernel, grid1d((long)N * Ho * Wo * C), 256, 0, stream, x, N, H, W, C, k, s, p, Ho,
-                       Wo, y, (int8_t*)arg);
+  const bool b16 = flags & OUT_BF16;
+  if (C % 4 == 0) {
+    const int g = grid1d((long)N * Ho * Wo * C / 4);
+    if (b16)
+      hipLaunchKernelGGL(maxpool_fwd4_kernel<bf16>, g, 256, 0, stream, x, N, H, W, C / 4, k, s, p, Ho, Wo, (bf16*)y,
+                         (int8_t*)arg);
+    else
+      hipLaunchKernelGGL(maxpool_fwd4_kernel<float>, g, 256, 0, stream, x, N, H, W, C / 4, k, s, p, Ho, Wo, (float*)y,
+                         (int8_t*)arg);
+  } else {
+    const int g = grid1d((long)N * Ho * Wo * C);
+    if (b16)
+      hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, g, 256, 0, stream, x, N, H, W, C, k, s, p, Ho, Wo, (bf16*)y,
+                         (int8_t*)arg);
+    else
+      hipLaunchKernelGGL(maxpool_fwd_kernel<float>, g, 256, 0, stream, x, N, H, W, C, k, s, p, Ho, Wo, (float*)y,
+                         (int8_t*)arg);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
-
-int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,
+int es_maxpool2d_fwd(const float* x, int N, int H, int W, int C, int k, int s, int p, float* y, void* arg,
                      hipStream_t stream) {
-  if (!dy || !dx || !arg) return ES_BAD_ARG;
+  return es_maxpool2d_fwd_ex(x, N, H, W, C, k, s, p, y, arg, 0, stream);
+}
+
+// _ex flags: 1 = dy is a bf16 map (dx stays fp32)
+int es_maxpool2d_bwd_ex(const void* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,
+                        int flags, hipStream_t stream) {
+  if (!dy || !dx || !arg || (flags & ~MAPS_BF16)) return ES_BAD_ARG;
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || k <= 0 || k > 11 || s <= 0 || p < 0) return ES_BAD_SHAPE;
   if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
   const int Ho = (H + 2 * p - k) / s + 1, Wo = (W + 2 * p - k) / s + 1;
-  if (C % 4 == 0)
-    hipLaunchKernelGGL(maxpool_bwd4_kernel, grid1d((long)N * H * W * C / 4), 256, 0, stream, dy, (const int8_t*)arg, N,
-                       H, W, C / 4, k, s, p, Ho, Wo, dx);
-  else
-    hipLaunchKernelGGL(maxpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, dy, (const int8_t*)arg, N, H,
-                       W, C, k, s, p, Ho, Wo, dx);
+  const int8_t* a = (const int8_t*)arg;
+  if (C % 4 == 0) {
+    const int g = grid1d((long)N * H * W * C / 4);
+    if (flags)
+      hipLaunchKernelGGL(maxpool_bwd4_kernel<bf16>, g, 256, 0, stream, (const bf16*)dy, a, N, H, W, C / 4, k, s, p, Ho,
+                         Wo, dx);
+    else
+      hipLaunchKernelGGL(maxpool_bwd4_kernel<float>, g, 256, 0, stream, (const float*)dy, a, N, H, W, C / 4, k, s, p,
+                         Ho, Wo, dx);
+  } else {
+    const int g = grid1d((long)N * H * W * C);
+    if (flags)
+      hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, g, 256, 0, stream, (const bf16*)dy, a, N, H, W, C, k, s, p, Ho, Wo,
+                         dx);
+    else
+      hipLaunchKernelGGL(maxpool_bwd_kernel<float>, g, 256, 0, stream, (const float*)dy, a, N, H, W, C, k, s, p, Ho,
+                         Wo, dx);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
+int es_maxpool2d_bwd(const float* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,
+                     hipStream_t stream) {
+  return es_maxpool2d_bwd_ex(dy, arg, N, H, W, C, k, s, p, dx, 0, stream);
+}
 
-// AvgPool2d(kernel k, stride k, no padding) over NHWC (H, W multiples of k)
-int es_avgpool2d_fwd(const float* x, int N, int H, int W, int C, int k, float* y, hipStream_t stream) {
-  if (!x || !y) return ES_BAD_ARG;
-  if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k) return ES_BAD_SHAPE;
+// AvgPool2d(kernel k, stride k, no padding) over NHWC (H, W multiples of k).  _ex flags: 1 = x is a bf16
+// map, 2 = y is a bf16 map (C % 4 == 0 for any bf16 map)
+int es_avgpool2d_fwd_ex(const void* x, int N, int H, int W, int C, int k, void* y, int flags, hipStream_t stream) {
+  if (!x || !y || (flags & ~3)) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k || (flags && C % 4)) return ES_BAD_SHAPE;
   if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
-  hipLaunchKernelGGL(avgpool_fwd_kernel, grid1d((long)N * (H / k) * (W / k) * C), 256, 0, stream, x, N, H, W, C, k,
-                     H / k, W / k, y);
+  const int Ho = H / k, Wo = W / k;
+  if (C % 4 == 0 && al16(x) && al16(y)) {
+    const int g = grid1d((long)N * Ho * Wo * C / 4);
+#define AVG_F(TI, TO) \
+  hipLaunchKernelGGL((avgpool_fwd4_kernel<TI, TO>), g, 256, 0, stream, (const TI*)x, N, H, W, C / 4, k, Ho, Wo, (TO*)y)
+    switch (flags) {
+      case 0: AVG_F(float, float); break;
+      case 1: AVG_F(bf16, float); break;
+      case 2: AVG_F(float, bf16); break;
+      default: AVG_F(bf16, bf16); break;
+    }
+#undef AVG_F
+  } else {
+    if (flags) return ES_BAD_SHAPE;
+    hipLaunchKernelGGL(avgpool_fwd_kernel, grid1d((long)N * Ho * Wo * C), 256, 0, stream, (const float*)x, N, H, W, C,
+                       k, Ho, Wo, (float*)y);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
+int es_avgpool2d_fwd(const float* x, int N, int H, int W, int C, int k, float* y, hipStream_t stream) {
+  return es_avgpool2d_fwd_ex(x, N, H, W, C, k, y, 0, stream);
+}
 
+// _ex flags: 1 = dy is a bf16 map, 2 = dx is a bf16 map (accumulate: dx (+)=, added in fp32, rounded once)
+int es_avgpool2d_bwd_ex(const void* dy, int N, int H, int W, int C, int k, void* dx, int accumulate, int flags,
+                        hipStream_t stream) {
+  if (!dy || !dx || (flags & ~3)) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k || (flags && C % 4)) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
+  if (C % 4 == 0 && al16(dy) && al16(dx)) {
+    const int g = grid1d((long)N * H * W * C / 4);
+#define AVG_B(TI, TO)                                                                                            \
+  hipLaunchKernelGGL((avgpool_bwd4_kernel<TI, TO>), g, 256, 0, stream, (const TI*)dy, N, H, W, C / 4, k, H / k, W / k, \
+                     (TO*)dx, accumulate)
+    switch (flags) {
+      case 0: AVG_B(float, float); break;
+      case 1: AVG_B(bf16, float); break;
+      case 2: AVG_B(float, bf16); break;
+      default: AVG_B(bf16, bf16); break;
+    }
+#undef AVG_B
+  } else {
+    if (flags) return ES_BAD_SHAPE;
+    hipLaunchKernelGGL(avgpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, (const float*)dy, N, H, W, C, k,
+                       H / k, W / k, (float*)dx, accumulate);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
 int es_avgpool2d_bwd(const float* dy, int N, int H, int W, int C, int k, float* dx, int accumulate,
                      hipStream_t stream) {
-  if (!dy || !dx) return ES_BAD_ARG;
-  if (N <= 0 || C <= 0 || k <= 0 || H % k || W % k) return ES_BAD_SHAPE;
-  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
-  hipLaunchKernelGGL(avgpool_bwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, dy, N, H, W, C, k, H / k, W / k,
-                     dx, accumulate);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return es_avgpool2d_bwd_ex(dy, N, H, W, C, k, dx, accumulate, 0, stream);
 }
 
-// out[N, H, W, C] = base + nearest-upsample(src [N, H/s, W/s, C], x s)
+// out[N, H, W, C] = base + nearest-upsample(src [N, H/s, W/s, C], x s).  _ex flags: 1 = every map bf16
+int es_upsample_add_fwd_ex(const void* base, const void* src, int N, int H, int W, int C, int s, void* out, int flags,
+                           hipStream_t stream) {
+  if (!base || !src || !out || (flags & ~MAPS_BF16)) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s || (flags && C % 4)) return ES_BAD_SHAPE;
+  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
+  if (C % 4 == 0 && al16(base) && al16(src) && al16(out)) {
+    const int g = grid1d((long)N * H * W * C / 4);
+    if (flags)
+      hipLaunchKernelGGL(upsample_add_fwd4_kernel<bf16>, g, 256, 0, stream, (const bf16*)base, (const bf16*)src, N, H, W,
+                         C / 4, s, (bf16*)out);
+    else
+      hipLaunchKernelGGL(upsample_add_fwd4_kernel<float>, g, 256, 0, stream, (const float*)base, (const float*)src, N, H,
+                         W, C / 4, s, (float*)out);
+  } else {
+    if (flags) return ES_BAD_SHAPE;
+    hipLaunchKernelGGL(upsample_add_fwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, (const float*)base,
+                       (const float*)src, N, H, W, C, s, (float*)out);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
 int es_upsample_add_fwd(const float* base, const float* src, int N, int H, int W, int C, int s, float* out,
                         hipStream_t stream) {
-  if (!base || !src || !out) return ES_BAD_ARG;
-  if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s) return ES_BAD_SHAPE;
-  if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
-  hipLaunchKernelGGL(upsample_add_fwd_kernel, grid1d((long)N * H * W * C), 256, 0, stream, base, src, N, H, W, C, s,
-                     out);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  return es_upsample_add_fwd_ex(base, src, N, H, W, C, s, out, 0, stream);
 }
 
-// dsrc = block sums of dout (the base's gradient is dout itself)
-int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float* dsrc, hipStream_t stream) {
-  if (!dout || !dsrc) return ES_BAD_ARG;
-  if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s) return ES_BAD_SHAPE;
+// dsrc = block sums of dout (the base's gradient is dout itself).  _ex flags: 1 = both maps bf16
+int es_upsample_bwd_ex(const void* dout, int N, int H, int W, int C, int s, void* dsrc, int flags, hipStream_t stream) {
+  if (!dout || !dsrc || (flags & ~MAPS_BF16)) return ES_BAD_ARG;
+  if (N <= 0 || C <= 0 || s <= 0 || H % s || W % s || (flags && C % 4)) return ES_BAD_SHAPE;
   if ((long)N * H * W * C >= (1L << 31)) return ES_BAD_SHAPE;  // 32-bit index arithmetic in the kernels
-  hipLaunchKernelGGL(upsample_bwd_kernel, grid1d((long)N * (H / s) * (W / s) * C), 256, 0, stream, dout, N, H, W, C,
-                     s, dsrc);
+  if (C % 4 == 0 && al16(dout) && al16(dsrc)) {
+    const int g = grid1d((long)N * (H / s) * (W / s) * C / 4);
+    if (flags)
+      hipLaunchKernelGGL(upsample_bwd4_kernel<bf16>, g, 256, 0, stream, (const bf16*)dout, N, H, W, C / 4, s,
+                         (bf16*)dsrc);
+    else
+      hipLaunchKernelGGL(upsample_bwd4_kernel<float>, g, 256, 0, stream, (const float*)dout, N, H, W, C / 4, s,
+                         (float*)dsrc);
+  } else {
+    if (flags) return ES_BAD_SHAPE;
+    hipLaunchKernelGGL(upsample_bwd_kernel, grid1d((long)N * (H / s) * (W / s) * C), 256, 0, stream,
+                       (const float*)dout, N, H, W, C, s, (float*)dsrc);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
+int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float* dsrc, hipStream_t stream) {
+  return es_upsample_bwd_ex(dout, N, H, W, C, s, dsrc, 0, stream);
+}
+
 
 // FCUDown + ConvTransBlock's sum: out [N, np+1, D] (token rows) from pooled [N, np, D] and x_t.
 int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln_w, const float* ln_b, float* out,

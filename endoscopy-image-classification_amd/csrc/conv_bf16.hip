@@ -7,10 +7,14 @@
 //  es_conv2d_bwd_data_bf16          dx (+)= conv^T(dy)          implicit GEMM per stride phase
 //  es_conv2d_bwd_weight_bf16        dw (+)= sum_pixels dy x im2col(x)   split over pixels + reduce
 //
-// Numerical contract (the transformer GEMMs' one): the maps stay fp32 in HBM (BatchNorm statistics,
-// residual sums and ReLU masks are fp32); the conv OPERANDS -- the gathered activation / gradient
-// tile and the weights -- are rounded to bf16 as they are staged into LDS, products accumulate in
-// fp32 on v_mfma_f32_16x16x32_bf16 (8x the fp32 MFMA rate conv.hip's kernels run at).  The fp32
+// Numerical contract (the transformer GEMMs' one): the conv OPERANDS -- the gathered activation /
+// gradient tile and the weights -- are bf16 (rounded as they are staged into LDS when the map is fp32),
+// products accumulate in fp32 on v_mfma_f32_16x16x32_bf16 (8x the fp32 MFMA rate conv.hip's kernels run
+// at).  The maps themselves are fp32 or bf16 per operand (the _ex entry points' flags): the Conformer's
+// CNN branch keeps its activation and gradient maps in bf16 when every conv of the branch runs here
+// (conformer.NativeConformer.map_bf16), halving the map traffic of the HBM-bound 1x1 convs and
+// BatchNorms; outputs are rounded once from the fp32 accumulators (an accumulating store adds in fp32
+// and rounds once).  BatchNorm statistics in the epilogue come from the fp32 accumulators.  The fp32
 // kernels of conv.hip remain the parity mode and the path for convs these do not take (channel
 // counts not multiples of 32: the 3-channel stem, Conformer-Ti's 16-channel bottlenecks).
 //
@@ -40,10 +44,10 @@ __device__ __forceinline__ u32x4 f8_to_bf16x8(f32x4 a, f32x4 b) {
 }
 
 struct NTConv {
-  const float* src;   // gathered operand: x (forward) or dy (data grad), channel stride 1
+  const void* src;    // gathered operand (fp32 or bf16 map): x (forward) or dy (data grad), channel stride 1
   const bf16* wp;     // packed weights [Ncol][kh kw][C]
   const float* bias;  // [Ncol] or null
-  float* out;
+  void* out;          // fp32 or bf16 map
   int N, C, Ncol, Hs, Ws;  // C = gathered channels (Cin | Cout), Ncol = output channels (Cout | Cin)
   long ssn, ssh, ssw;
   int kh, kw, s, p;
@@ -60,7 +64,8 @@ constexpr int NT_BM = 128, NT_BK = 32;
 // DX = true:  blockIdx.z = stride phase (py, px); pixels (n, hq, wq) -> x pixel (hq s + py, wq s + px);
 //             taps ky = ky0 + s kyq (the only ones that reach this phase); source dy pixel
 //             (hq + qh - kyq, wq + qw - kxq) (conv.hip conv_dx_kernel's decomposition).
-template <int BN, bool DX, bool STATS = false>
+// TS / TO: element types of the gathered map and of the output map (float or bf16).
+template <int BN, bool DX, bool STATS, typename TS, typename TO>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void convb_nt_kernel(NTConv a) {
   constexpr int NF = BN / 32;       // 16-col fragments per wave (wave covers BN / 2 cols)
   constexpr int BJ = BN / 64;       // 16-byte weight loads per thread per step
@@ -89,8 +94,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int g = lane >> 4, r = lane & 15;
 
-  // gather slots: 8 lanes per pixel (one 16-byte channel quad each: a wave instruction reads 8
-  // whole 128-byte channel runs), pixel rows arow0 + 32 j
+  // gather slots: 8 lanes per pixel (one channel quad each -- 16 bytes of fp32, 8 of bf16: a wave
+  // instruction reads 8 whole channel runs), pixel rows arow0 + 32 j
   const int ac = tid & 7, arow0 = tid >> 3;
   long abase[4];
   int ahb[4], awb[4];
@@ -109,7 +114,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   }
   const int bchunk = tid & 3, brow0 = tid >> 2;
 
-  f32x4 ra4[4];
+  const TS* src = (const TS*)a.src;
+  typename Q4<TS>::t ra4[4];
   u32x4 rb[BJ];
   auto load = [&](int kt) {
     const int k0 = kt * NT_BK;
@@ -118,9 +124,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
-      ra4[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ra4[j] = q4_zero<TS>();
       if ((unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws)
-        ra4[j] = *(const f32x4*)(a.src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
+        ra4[j] = q4_load(src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
     }
     const int btap = (by0 + tyq * bs) * a.kw + bx0 + txq * bs;
 #pragma unroll
@@ -136,8 +142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = arow0 + 32 * j;
-      const bf16x4 o = {(bf16)ra4[j][0], (bf16)ra4[j][1], (bf16)ra4[j][2], (bf16)ra4[j][3]};
-      *(bf16x4*)(As + row * 64 + cswz64(row, ac >> 1) * 16 + (ac & 1) * 8) = o;
+      *(bf16x4*)(As + row * 64 + cswz64(row, ac >> 1) * 16 + (ac & 1) * 8) = q4_b16(ra4[j]);
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
@@ -258,10 +263,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       const int m = m0 + wm * 64 + i * 16 + row;
       if (m < M && ecol_ok) {
         const int bb = m % Wm, t = m / Wm, aa = t % Hm, n = t / Hm;
-        float* o = a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw + ecol;
+        TO* o = (TO*)a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw + ecol;
         f32x4 v = v0 + bv;
-        if (a.accumulate) v += *(const f32x4*)o;
-        *(f32x4*)o = v;
+        if (a.accumulate) v += q4_f32(q4_load(o));
+        q4_store(o, v);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -270,8 +275,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 
 // ---- weight gradient -------------------------------------------------------------------------
 struct DWConv {
-  const float* x;   // [N, H, W, Cin] at (sxn, sxh, sxw), channel stride 1
-  const float* dy;  // [N, Ho, Wo, Cout] at (syn, syh, syw), channel stride 1
+  const void* x;    // [N, H, W, Cin] at (sxn, sxh, sxw), channel stride 1 (fp32 or bf16 map)
+  const void* dy;   // [N, Ho, Wo, Cout] at (syn, syh, syw), channel stride 1 (fp32 or bf16 map)
   float* P;         // [splits][Cout][kh kw Cin] partials, column k' = tap Cin + ci
   int N, H, W, Cin, Ho, Wo, Cout, kh, kw, s, p;
   long sxn, sxh, sxw, syn, syh, syw;
@@ -300,7 +305,7 @@ struct PixWalk {
 };
 
 // P[split][co][k'] = sum_{pixels m of the split} dy[m][co] . im2col(x)[m][k'], tile B1 (co) x B2 (k')
-template <int B1, int B2>
+template <int B1, int B2, typename TX, typename TD>
 __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
   constexpr int WA = (B1 == 128 && B2 == 64) ? 4 : (B1 == 64 && B2 == 128) ? 1 : 2, WB = 4 / WA;
   constexpr int F1 = B1 / WA / 16, F2 = B2 / WB / 16;  // fragments per wave along co / k'
@@ -335,24 +340,27 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
 #pragma unroll
   for (int j = 0; j < J2; ++j) pw2[j].init(mbeg + r2 + RP2 * j, a.Ho, a.Wo);
 
-  f32x4 v1[J1], v2[J2];
+  const TX* xs = (const TX*)a.x;
+  const TD* dys = (const TD*)a.dy;
+  typename Q4<TD>::t v1[J1];
+  typename Q4<TX>::t v2[J2];
   auto load = [&](int mm) {
 #pragma unroll
     for (int j = 0; j < J1; ++j) {
       const int m = mm + r1 + RP1 * j;
-      v1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      v1[j] = q4_zero<TD>();
       if (m < mend && co_ok)
-        v1[j] = *(const f32x4*)(a.dy + (long)pw1[j].n * a.syn + (long)pw1[j].ho * a.syh + (long)pw1[j].wo * a.syw + co);
+        v1[j] = q4_load(dys + (long)pw1[j].n * a.syn + (long)pw1[j].ho * a.syh + (long)pw1[j].wo * a.syw + co);
       pw1[j].advance(32, a.Ho, a.Wo);
     }
 #pragma unroll
     for (int j = 0; j < J2; ++j) {
       const int m = mm + r2 + RP2 * j;
-      v2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      v2[j] = q4_zero<TX>();
       if (m < mend && kc_ok) {
         const int h = pw2[j].ho * a.s - a.p + ky, ww = pw2[j].wo * a.s - a.p + kx;
         if ((unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
-          v2[j] = *(const f32x4*)(a.x + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
+          v2[j] = q4_load(xs + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
       }
       pw2[j].advance(32, a.Ho, a.Wo);
     }
@@ -363,14 +371,12 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
 #pragma unroll
     for (int j = 0; j < J1; ++j) {
       const int row = r1 + RP1 * j;
-      bf16x4 o = {(bf16)v1[j][0], (bf16)v1[j][1], (bf16)v1[j][2], (bf16)v1[j][3]};
-      *(bf16x4*)(T1 + row * 256 + cswz256(row, q1 >> 1) * 16 + (q1 & 1) * 8) = o;
+      *(bf16x4*)(T1 + row * 256 + cswz256(row, q1 >> 1) * 16 + (q1 & 1) * 8) = q4_b16(v1[j]);
     }
 #pragma unroll
     for (int j = 0; j < J2; ++j) {
       const int row = r2 + RP2 * j;
-      bf16x4 o = {(bf16)v2[j][0], (bf16)v2[j][1], (bf16)v2[j][2], (bf16)v2[j][3]};
-      *(bf16x4*)(T2 + row * 256 + cswz256(row, q2 >> 1) * 16 + (q2 & 1) * 8) = o;
+      *(bf16x4*)(T2 + row * 256 + cswz256(row, q2 >> 1) * 16 + (q2 & 1) * 8) = q4_b16(v2[j]);
     }
   };
 
@@ -497,6 +503,29 @@ inline int dw_splits(int M, int Cout, int K, int splits) {
   return splits < 1 ? 1 : splits;
 }
 
+// the _ex entry points' map element-type flags: bit 0 = the gathered / input map is bf16, bit 1 = the
+// output map (bwd_weight: dy) is bf16
+
+template <int BN, bool DX, bool STATS>
+void launch_nt(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
+  switch (flags & 3) {
+    case 0: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, float>), grid, 256, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, float>), grid, 256, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, bf16>), grid, 256, 0, stream, a); break;
+    default: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, bf16>), grid, 256, 0, stream, a); break;
+  }
+}
+
+template <int B1, int B2>
+void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
+  switch (flags & 3) {
+    case 0: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, float>), grid, 256, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, float>), grid, 256, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, bf16>), grid, 256, 0, stream, a); break;
+    default: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, bf16>), grid, 256, 0, stream, a); break;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -516,15 +545,18 @@ int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void*
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-// y[n, ho, wo, co] (+)= bias[co] + conv(x) with wp = es_conv2d_pack_bf16's forward image.  Same
-// geometry arguments as es_conv2d_fwd; requires es_conv2d_bf16_eligible, sxc == 1, 16-byte aligned
-// pixel rows (strides % 4 == 0) and pointers.
-static int conv_fwd_bf16_impl(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
-                              const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
-                              float* y, long syn, long syh, long syw, int accumulate, float* bn_partials,
-                              hipStream_t stream) {
+// y[n, ho, wo, co] (+)= bias[co] + conv(x) with wp = es_conv2d_pack_bf16's forward image.  Same geometry
+// arguments as es_conv2d_fwd; requires es_conv2d_bf16_eligible, sxc == 1, 16-byte aligned pointers and
+// element strides % 4 == 0.  flags: 1 = x is a bf16 map, 2 = y is a bf16 map (else fp32).  bn_partials
+// (nullable, accumulate 0 only): y's BatchNorm statistics per 128-pixel block (es_conv2d_bnstats_size
+// floats; from the fp32 accumulators).
+int es_conv2d_fwd_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                          const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, void* y,
+                          long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
+                          hipStream_t stream) {
   if (!x || !wp || !y) return ES_BAD_ARG;
-  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
+  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0 ||
+      (flags & ~3))
     return ES_BAD_SHAPE;
   const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(x) || !al16(y) || !al16(wp) ||
@@ -536,15 +568,11 @@ static int conv_fwd_bf16_impl(const float* x, int N, int H, int W, int Cin, long
   const int M = N * Ho * Wo;
   const dim3 g128((M + 127) / 128, Cout / 128), g64((M + 127) / 128, (Cout + 63) / 64);
   if (Cout % 128 == 0) {
-    if (bn_partials)
-      hipLaunchKernelGGL((convb_nt_kernel<128, false, true>), g128, 256, 0, stream, a);
-    else
-      hipLaunchKernelGGL((convb_nt_kernel<128, false>), g128, 256, 0, stream, a);
+    if (bn_partials) launch_nt<128, false, true>(g128, flags, a, stream);
+    else launch_nt<128, false, false>(g128, flags, a, stream);
   } else {
-    if (bn_partials)
-      hipLaunchKernelGGL((convb_nt_kernel<64, false, true>), g64, 256, 0, stream, a);
-    else
-      hipLaunchKernelGGL((convb_nt_kernel<64, false>), g64, 256, 0, stream, a);
+    if (bn_partials) launch_nt<64, false, true>(g64, flags, a, stream);
+    else launch_nt<64, false, false>(g64, flags, a, stream);
   }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
@@ -552,8 +580,8 @@ static int conv_fwd_bf16_impl(const float* x, int N, int H, int W, int Cin, long
 int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
                        const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
                        long syn, long syh, long syw, int accumulate, hipStream_t stream) {
-  return conv_fwd_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh, syw,
-                            accumulate, nullptr, stream);
+  return es_conv2d_fwd_bf16_ex(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh,
+                               syw, accumulate, nullptr, 0, stream);
 }
 
 // floats of es_conv2d_fwd_bf16_bnstats' partials for M = N Ho Wo output pixels
@@ -568,17 +596,18 @@ int es_conv2d_fwd_bf16_bnstats(const float* x, int N, int H, int W, int Cin, lon
                                const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
                                float* y, long syn, long syh, long syw, float* partials, hipStream_t stream) {
   if (!partials) return ES_BAD_ARG;
-  return conv_fwd_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh, syw,
-                            0, partials, stream);
+  return es_conv2d_fwd_bf16_ex(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh,
+                               syw, 0, partials, 0, stream);
 }
 
 // dx[n, h, w, ci] (+)= conv^T(dy) with wt = es_conv2d_pack_bf16's transposed image.  Same geometry
-// arguments as es_conv2d_bwd_data.
-int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
-                            int Cin, int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh,
-                            long sxw, long sxc, int accumulate, hipStream_t stream) {
+// arguments as es_conv2d_bwd_data.  flags: 1 = dy is a bf16 map, 2 = dx is a bf16 map.
+int es_conv2d_bwd_data_bf16_ex(const void* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
+                               int Cin, int Cout, int kh, int kw, int stride, int pad, void* dx, long sxn, long sxh,
+                               long sxw, long sxc, int accumulate, int flags, hipStream_t stream) {
   if (!dy || !wt || !dx) return ES_BAD_ARG;
-  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
+  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0 ||
+      (flags & ~3))
     return ES_BAD_SHAPE;
   const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(dy) || !al16(dx) ||
@@ -589,10 +618,17 @@ int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const
   const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
   const unsigned ph = (unsigned)(stride * stride);
   if (Cin % 128 == 0)
-    hipLaunchKernelGGL((convb_nt_kernel<128, true>), dim3((Mq + 127) / 128, Cin / 128, ph), 256, 0, stream, a);
+    launch_nt<128, true, false>(dim3((Mq + 127) / 128, Cin / 128, ph), flags, a, stream);
   else
-    hipLaunchKernelGGL((convb_nt_kernel<64, true>), dim3((Mq + 127) / 128, (Cin + 63) / 64, ph), 256, 0, stream, a);
+    launch_nt<64, true, false>(dim3((Mq + 127) / 128, (Cin + 63) / 64, ph), flags, a, stream);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_conv2d_bwd_data_bf16(const float* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
+                            int Cin, int Cout, int kh, int kw, int stride, int pad, float* dx, long sxn, long sxh,
+                            long sxw, long sxc, int accumulate, hipStream_t stream) {
+  return es_conv2d_bwd_data_bf16_ex(dy, syn, syh, syw, wt, N, H, W, Cin, Cout, kh, kw, stride, pad, dx, sxn, sxh, sxw,
+                                    sxc, accumulate, 0, stream);
 }
 
 // fp32 workspace floats of es_conv2d_bwd_weight_bf16 for M = N Ho Wo output pixels (splits <= 0: auto)
@@ -604,11 +640,14 @@ size_t es_conv2d_bwd_weight_bf16_workspace(int M, int Cout, int Cin, int kh, int
 
 // dw[co, ci, ky, kx] (+)= sum over output pixels of dy x im2col(x) (bf16 operands, fp32 sums); same
 // geometry arguments as es_conv2d_bwd_weight; splits <= 0 sizes the pixel split for the chip.
-int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
-                              const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
-                              int pad, int splits, float* workspace, float* dw, int accumulate, hipStream_t stream) {
+// flags: 1 = x is a bf16 map, 2 = dy is a bf16 map.
+int es_conv2d_bwd_weight_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                                 const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
+                                 int pad, int splits, float* workspace, float* dw, int accumulate, int flags,
+                                 hipStream_t stream) {
   if (!x || !dy || !dw || !workspace) return ES_BAD_ARG;
-  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0)
+  if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0 ||
+      (flags & ~3))
     return ES_BAD_SHAPE;
   const int Ho = (H + 2 * pad - kh) / stride + 1, Wo = (W + 2 * pad - kw) / stride + 1;
   if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(x) || !al16(dy) ||
@@ -623,14 +662,21 @@ int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long
   int b1, b2;
   dw_tile(Cout, K, b1, b2);
   const dim3 grid((Cout + b1 - 1) / b1, (K + b2 - 1) / b2, S);
-  if (b1 == 128 && b2 == 128) hipLaunchKernelGGL((convb_dw_kernel<128, 128>), grid, 256, 0, stream, a);
-  else if (b1 == 64 && b2 == 128) hipLaunchKernelGGL((convb_dw_kernel<64, 128>), grid, 256, 0, stream, a);
-  else if (b1 == 128) hipLaunchKernelGGL((convb_dw_kernel<128, 64>), grid, 256, 0, stream, a);
-  else hipLaunchKernelGGL((convb_dw_kernel<64, 64>), grid, 256, 0, stream, a);
+  if (b1 == 128 && b2 == 128) launch_dw<128, 128>(grid, flags, a, stream);
+  else if (b1 == 64 && b2 == 128) launch_dw<64, 128>(grid, flags, a, stream);
+  else if (b1 == 128) launch_dw<128, 64>(grid, flags, a, stream);
+  else launch_dw<64, 64>(grid, flags, a, stream);
   const long n = (long)Cout * K;
   hipLaunchKernelGGL(convb_dw_reduce_kernel, (unsigned)((n / 4 + 63) / 64), 256, 0, stream, workspace, S, Cout, Cin,
                      kh * kw, dw, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                              const float* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
+                              int pad, int splits, float* workspace, float* dw, int accumulate, hipStream_t stream) {
+  return es_conv2d_bwd_weight_bf16_ex(x, N, H, W, Cin, sxn, sxh, sxw, sxc, dy, syn, syh, syw, Cout, kh, kw, stride, pad,
+                                      splits, workspace, dw, accumulate, 0, stream);
 }
 
 }  // extern "C"

@@ -105,6 +105,24 @@ SIGNATURES = {
     "es_avgpool2d_bwd": (I, [V, I, I, I, I, I, V, I, V]),
     "es_upsample_add_fwd": (I, [V, V, I, I, I, I, I, V, V]),
     "es_upsample_bwd": (I, [V, I, I, I, I, I, V, V]),
+    # bf16 activation / gradient maps (flags: bit 0 the input maps bf16, bit 1 the output map bf16)
+    "es_conv2d_fwd_bf16_ex": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, I, V, I, V]),
+    "es_conv2d_bwd_data_bf16_ex": (I, [V, L, L, L, V, I, I, I, I, I, I, I, I, I, V, L, L, L, L, I, I, V]),
+    "es_conv2d_bwd_weight_bf16_ex": (I, [V, I, I, I, I, L, L, L, L, V, L, L, L, I, I, I, I, I, I, V, V, I, I, V]),
+    "es_chan_sum_ex": (I, [V, I, I, L, L, I, V, V, I, I, V]),
+    "es_bn2d_fwd_ex": (I, [V, I, I, V, V, V, V, V, F, F, I, V, I, V, V, V, V, I, V]),
+    "es_bn2d_bwd_ex": (I, [V, V, V, I, I, I, V, V, V, I, V, F, V, V, V, V, I, V, I, V]),
+    "es_bn2d_fwd_partials_ex": (I, [V, I, I, V, V, V, V, V, V, F, F, V, I, V, V, V, I, V]),
+    "es_bn2d_sums_ex": (I, [V, I, I, I, V, I, V, V, I, V]),
+    "es_bn2d_fwd_global_ex": (I, [V, I, I, V, V, V, V, V, F, F, V, V, I, V, I, V, V, V, I, V]),
+    "es_bn2d_bwd_sums_ex": (I, [V, V, V, I, I, I, V, V, V, V, I, V]),
+    "es_bn2d_bwd_global_ex": (I, [V, V, V, I, I, I, V, V, V, V, V, I, V, V, V, V, I, I, V]),
+    "es_maxpool2d_fwd_ex": (I, [V, I, I, I, I, I, I, I, V, V, I, V]),
+    "es_maxpool2d_bwd_ex": (I, [V, V, I, I, I, I, I, I, I, V, I, V]),
+    "es_avgpool2d_fwd_ex": (I, [V, I, I, I, I, I, V, I, V]),
+    "es_avgpool2d_bwd_ex": (I, [V, I, I, I, I, I, V, I, I, V]),
+    "es_upsample_add_fwd_ex": (I, [V, V, I, I, I, I, I, V, I, V]),
+    "es_upsample_bwd_ex": (I, [V, I, I, I, I, I, V, I, V]),
     "es_fcu_down_tokens_fwd": (I, [V, V, V, V, V, V, V, I, I, I, F, V]),
     "es_fcu_down_workspace": (Z, [I, I, I]),
     "es_fcu_down_tokens_bwd": (I, [V, V, V, V, V, V, V, V, V, V, I, I, I, I, V, V]),

@@ -9,10 +9,13 @@ MI355X-first layout:
   * parameters live in ONE fp32 flat buffer in the reference's state_dict order (checkpoints
     interchange; the fused Adam + EMA sweep of optim.hip updates all of them in one pass); the
     BatchNorm running statistics are ordinary buffers of the BN submodules;
-  * the CNN branch keeps NHWC fp32 maps and runs on conv.hip (BatchNorm2d with fused residual +
+  * the CNN branch keeps NHWC maps and runs on conv.hip (BatchNorm2d with fused residual +
     ReLU, pools, nearest upsampling, fp32 implicit-GEMM convolutions) and conv_bf16.hip (the convs
     whose channel counts are multiples of 32, on bf16 operands: every conv of Conformer-B but the
-    3-channel stem; set_conv_precision("fp32") is the parity mode); the transformer branch is a
+    3-channel stem; set_conv_precision("fp32") is the parity mode).  When every conv after the stem
+    takes the bf16 kernels (Conformer-B: map_bf16) the activation AND gradient maps after the stem's
+    max-pool are bf16 (torch autocast's dtypes for the reference's conv / BatchNorm chain), BatchNorm
+    statistics and every reduction in fp32; otherwise fp32 maps; the transformer branch is a
     [tokens, D] fp32 residual stream padded to 256 rows (zero pad) and runs on the same bf16 MFMA
     kernels as the ViT (gemm / attention / layernorm); the FCU bridges read and write token rows
     in place through element strides (no transposes);
@@ -243,7 +246,7 @@ class _Map:
         self.sc, self.off = sc, off
 
     def p(self):
-        return ptr(self.t) + 4 * self.off
+        return ptr(self.t) + self.t.element_size() * self.off
 
     @staticmethod
     def nhwc(t):
@@ -270,6 +273,18 @@ CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
 BN_STATS_FUSED = os.environ.get("ENDOSSL_BN_STATS_FUSED", "1") != "0"
 # a ConvBlock input's two gradient contributions (conv1, residual) summed in place (_GradSink)
 GRAD_SINKS = os.environ.get("ENDOSSL_GRAD_SINKS", "1") != "0"
+# bf16 activation / gradient maps in the CNN branch when every conv after the stem runs on conv_bf16.hip
+# (NativeConformer.map_bf16); ENDOSSL_MAP_BF16=0 keeps fp32 maps with bf16 conv operands
+MAP_BF16 = os.environ.get("ENDOSSL_MAP_BF16", "1") != "0"
+
+
+def _fl(t):
+    """1 for a bf16 map, 0 for fp32 (the _ex entry points' flag bit)."""
+    return 1 if t.dtype == torch.bfloat16 else 0
+
+
+def _map_dtype(m):
+    return torch.bfloat16 if getattr(m, "map_bf16", False) else torch.float32
 
 
 def _conv_bf16(m, xmap, Cout, k):
@@ -329,13 +344,15 @@ class _ConvFn(torch.autograd.Function):
     ConvBlock / FCU convs, Conformer.conv1)."""
 
     @staticmethod
-    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None, stats=False, sink=None):
+    def forward(ctx, x, m, xmap, wname, bname, Cout, k, s, p, anchor=None, stats=False, sink=None, out_dtype=None):
         Ho, Wo = (xmap.H + 2 * p - k) // s + 1, (xmap.W + 2 * p - k) // s + 1
-        y = torch.empty(xmap.N, Ho, Wo, Cout, dtype=torch.float32, device=x.device)
+        y = torch.empty(xmap.N, Ho, Wo, Cout, dtype=out_dtype or torch.float32, device=x.device)
         b16 = _conv_bf16(m, xmap, Cout, k)
+        if not b16 and (x.dtype != torch.float32 or y.dtype != torch.float32):
+            raise _lib.EndosslCallError(f"{wname}: bf16 maps need the bf16 conv kernels (channel counts % 32)")
+        flags = _fl(x) | (_fl(y) << 1)
         args = (xmap.p(), xmap.N, xmap.H, xmap.W, xmap.C, xmap.sn, xmap.sh, xmap.sw, xmap.sc)
-        tail = (ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout, Wo * Cout, Cout, 0,
-                _s())
+        tail = (ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout, Wo * Cout, Cout, 0)
         if b16 and stats and m.training and BN_STATS_FUSED and not (getattr(m, "sync_bn", True)
                                                                     and dist.world_size() > 1):
             # the BatchNorm that follows takes its batch statistics from these per-block partials (one
@@ -343,13 +360,13 @@ class _ConvFn(torch.autograd.Function):
             # partials are requested only when they will be consumed)
             lib = _lib.load()
             part = torch.empty(lib.es_conv2d_bnstats_size(xmap.N * Ho * Wo, Cout), device=x.device)
-            call("es_conv2d_fwd_bf16_bnstats", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail[:-2],
-                 ptr(part), _s())
+            call("es_conv2d_fwd_bf16_ex", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail, ptr(part), flags,
+                 _s())
             m._bn_partials[y.data_ptr()] = (part, y.shape)
         elif b16:
-            call("es_conv2d_fwd_bf16", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail)
+            call("es_conv2d_fwd_bf16_ex", *args, ptr(m.conv_pack(wname, Cout, xmap.C, k)[0]), *tail, None, flags, _s())
         else:
-            call("es_conv2d_fwd", *args, ptr(m.pview(wname)), *tail)
+            call("es_conv2d_fwd", *args, ptr(m.pview(wname)), *tail, _s())
         ctx.save_for_backward(x)
         ctx.m, ctx.xmap, ctx.spec, ctx.b16 = m, xmap, (wname, bname, Cout, k, s, p, Ho, Wo), b16
         ctx.sink = sink
@@ -364,12 +381,12 @@ class _ConvFn(torch.autograd.Function):
         m, xm = ctx.m, ctx.xmap
         wname, bname, Cout, k, s, p, Ho, Wo = ctx.spec
         dy = dy.contiguous()
-        xp = ptr(x) + 4 * xm.off
+        xp = ptr(x) + x.element_size() * xm.off
         M = xm.N * Ho * Wo
         lib = _lib.load()
         b16 = ctx.b16
         if b16:  # the bf16 weight gradient sizes its own pixel split (splits = 0)
-            splits, dwfn = 0, "es_conv2d_bwd_weight_bf16"
+            splits, dwfn = 0, "es_conv2d_bwd_weight_bf16_ex"
             wsn = lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, xm.C, k, k, 0)
         else:  # pixel splits sized for ~2048 workgroups (8 per CU) over es_conv2d_bwd_weight's tiles
             tiles = lib.es_conv2d_dw_tiles(Cout, xm.C, k, k)
@@ -385,10 +402,12 @@ class _ConvFn(torch.autograd.Function):
         with torch.cuda.stream(side) if side is not None else _nullctx():
             ws = torch.empty(wsn, device=dy.device)
             call(dwfn, xp, xm.N, xm.H, xm.W, xm.C, xm.sn, xm.sh, xm.sw, xm.sc, ptr(dy),
-                 Ho * Wo * Cout, Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0, _s())
+                 Ho * Wo * Cout, Wo * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(m.gview(wname)), 0,
+                 *((_fl(x) | (_fl(dy) << 1),) if b16 else ()), _s())
             if bname:
                 wsb = torch.empty(lib.es_chan_workspace(M, Cout), device=dy.device)
-                call("es_chan_sum", ptr(dy), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(m.gview(bname)), 0, _s())
+                call("es_chan_sum_ex", ptr(dy), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(m.gview(bname)), 0, _fl(dy),
+                     _s())
         dx = None
         if ctx.needs_input_grad[0]:
             full = xm.off == 0 and xm.sc == 1 and xm.sn * xm.N == x.numel()
@@ -397,16 +416,16 @@ class _ConvFn(torch.autograd.Function):
             dx, acc = sink.take(alloc) if sink is not None else (alloc(), 0)
             wimg = m.conv_pack(wname, Cout, xm.C, k)[1] if b16 else m.pview(wname)
             before = _map_view(dx, xm).clone() if CAPTURE is not None and acc else None
-            call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
-                 ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + 4 * xm.off, xm.sn, xm.sh, xm.sw, xm.sc, acc,
-                 _s())
+            call("es_conv2d_bwd_data_bf16_ex" if b16 else "es_conv2d_bwd_data", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout,
+                 ptr(wimg), xm.N, xm.H, xm.W, xm.C, Cout, k, k, s, p, ptr(dx) + dx.element_size() * xm.off, xm.sn, xm.sh,
+                 xm.sw, xm.sc, acc, *((_fl(dy) | (_fl(dx) << 1),) if b16 else ()), _s())
             if CAPTURE is not None:
                 CAPTURE("bwd", wname, dy, before, _map_view(dx, xm))
             if sink is not None:  # first consumer: hand the buffer over; second: return the sum
                 dx = sink.give(dx, acc)
         elif CAPTURE is not None:  # no input gradient (the stem reads the images): dy for the weight gradient
             CAPTURE("bwd", wname, dy, None, None)
-        return dx, None, None, None, None, None, None, None, None, None, None, None
+        return dx, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 class _nullctx:
@@ -417,10 +436,11 @@ class _nullctx:
         return False
 
 
-def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None, stats=False, sink=None):
+def conv(m, x, xmap, wname, bname, Cout, k, s=1, p=0, anchor=None, stats=False, sink=None, out_dtype=None):
     """stats=True: the output feeds a train-mode BatchNorm, which then takes its batch statistics
-    from the conv's epilogue (BN_STATS_FUSED).  sink: a _GradSink shared with x's other consumer."""
-    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor, stats, sink)
+    from the conv's epilogue (BN_STATS_FUSED).  sink: a _GradSink shared with x's other consumer.
+    out_dtype: the output map's dtype (default: the model's map dtype, _map_dtype)."""
+    return _ConvFn.apply(x, m, xmap, wname, bname, Cout, k, s, p, anchor, stats, sink, out_dtype or _map_dtype(m))
 
 
 class _BNFn(torch.autograd.Function):
@@ -441,25 +461,28 @@ class _BNFn(torch.autograd.Function):
         res_c = res.contiguous() if res is not None else None  # keep temporaries alive across the launch
         world = dist.world_size() if train and getattr(m, "sync_bn", True) else 1
         part = m._bn_partials.pop(x.data_ptr(), None) if train and world == 1 else None
+        fl = _fl(x)
+        if res_c is not None and res_c.dtype != x.dtype:
+            raise _lib.EndosslCallError(f"{pre}: residual map {res_c.dtype} vs input map {x.dtype}")
         if part is not None and part[1] == x.shape:
-            call("es_bn2d_fwd_partials", ptr(x), rows, C, ptr(part[0]), ptr(m.pview(pre + "weight")),
+            call("es_bn2d_fwd_partials_ex", ptr(x), rows, C, ptr(part[0]), ptr(m.pview(pre + "weight")),
                  ptr(m.pview(pre + "bias")), ptr(rm), ptr(rv), ptr(nbt), BN_MOMENTUM, eps, ptr(res_c),
-                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), _s())
+                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), fl, _s())
         elif world > 1:
             # SyncBatchNorm over every rank's rows (the single-process statistics)
             rows_g = rows * world
             sums = torch.empty(2, C, device=x.device)
-            call("es_bn2d_sums", ptr(x), rows, C, 0, None, 0, ptr(sums[0]), ptr(ws), _s())
+            call("es_bn2d_sums_ex", ptr(x), rows, C, 0, None, 0, ptr(sums[0]), ptr(ws), fl, _s())
             dist.allreduce_inplace_(sums[0])
-            call("es_bn2d_sums", ptr(x), rows, C, 1, ptr(sums[0]), rows_g, ptr(sums[1]), ptr(ws), _s())
+            call("es_bn2d_sums_ex", ptr(x), rows, C, 1, ptr(sums[0]), rows_g, ptr(sums[1]), ptr(ws), fl, _s())
             dist.allreduce_inplace_(sums[1])
-            call("es_bn2d_fwd_global", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")),
+            call("es_bn2d_fwd_global_ex", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")),
                  ptr(rm), ptr(rv), ptr(nbt), BN_MOMENTUM, eps, ptr(sums[0]), ptr(sums[1]), rows_g, ptr(res_c),
-                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), _s())
+                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), fl, _s())
         else:
-            call("es_bn2d_fwd", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")), ptr(rm),
+            call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")), ptr(rm),
                  ptr(rv), ptr(nbt) if train else None, BN_MOMENTUM, eps, 1 if train else 0, ptr(res_c),
-                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), _s())
+                 1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), fl, _s())
         ctx.save_for_backward(x, y, mean, rstd)
         ctx.m, ctx.pre, ctx.eps, ctx.relu, ctx.train, ctx.has_res = m, pre, eps, relu, train, res is not None
         ctx.world = world
@@ -478,18 +501,21 @@ class _BNFn(torch.autograd.Function):
         gout = torch.empty_like(x) if ctx.has_res else None
         ws = torch.empty(_lib.load().es_chan_workspace(rows, C), device=x.device)
         _, rv, _ = m.bn_buffers(pre)
+        fl = _fl(x)
+        if dy.dtype != x.dtype:
+            dy = dy.to(x.dtype)
         if ctx.world > 1:
             loc = torch.empty(2 * C, device=x.device)
-            call("es_bn2d_bwd_sums", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(mean), ptr(rstd),
-                 ptr(loc), ptr(ws), _s())
+            call("es_bn2d_bwd_sums_ex", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(mean), ptr(rstd),
+                 ptr(loc), ptr(ws), fl, _s())
             glob = dist.allreduce_inplace_(loc.clone())
-            call("es_bn2d_bwd_global", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0,
+            call("es_bn2d_bwd_global_ex", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0,
                  ptr(m.pview(pre + "weight")), ptr(mean), ptr(rstd), ptr(loc), ptr(glob), rows * ctx.world, ptr(dx),
-                 ptr(gout), ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, _s())
+                 ptr(gout), ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, fl, _s())
             return dx, _BNFn._res_grad(ctx, gout), None, None, None, None, None
-        call("es_bn2d_bwd", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(m.pview(pre + "weight")),
+        call("es_bn2d_bwd_ex", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(m.pview(pre + "weight")),
              ptr(mean), ptr(rstd), 1 if ctx.train else 0, ptr(rv), ctx.eps, ptr(dx), ptr(gout),
-             ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(ws), _s())
+             ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(ws), fl, _s())
         return dx, _BNFn._res_grad(ctx, gout), None, None, None, None, None
 
     @staticmethod
@@ -510,13 +536,15 @@ def bn(m, x, pre, eps=BN_EPS_BLOCK, relu=False, res=None, res_sink=None):
 
 
 class _MaxPoolFn(torch.autograd.Function):
+    """MaxPool2d on the stem's fp32 map; out_dtype bf16: the pooled map starts the bf16 maps."""
+
     @staticmethod
-    def forward(ctx, x, k, s, p):
+    def forward(ctx, x, k, s, p, out_dtype=None):
         N, H, W, C = x.shape
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
-        y = torch.empty(N, Ho, Wo, C, device=x.device)
+        y = torch.empty(N, Ho, Wo, C, dtype=out_dtype or torch.float32, device=x.device)
         arg = torch.empty(N, Ho, Wo, C, dtype=torch.int8, device=x.device)
-        call("es_maxpool2d_fwd", ptr(x), N, H, W, C, k, s, p, ptr(y), ptr(arg), _s())
+        call("es_maxpool2d_fwd_ex", ptr(x), N, H, W, C, k, s, p, ptr(y), ptr(arg), _fl(y) << 1, _s())
         ctx.save_for_backward(arg)
         ctx.geom = (N, H, W, C, k, s, p)
         return y
@@ -527,25 +555,29 @@ class _MaxPoolFn(torch.autograd.Function):
         (arg,) = ctx.saved_tensors
         N, H, W, C, k, s, p = ctx.geom
         dx = torch.empty(N, H, W, C, device=dy.device)
-        call("es_maxpool2d_bwd", ptr(dy.contiguous()), ptr(arg), N, H, W, C, k, s, p, ptr(dx), _s())
-        return dx, None, None, None
+        dy = dy.contiguous()
+        call("es_maxpool2d_bwd_ex", ptr(dy), ptr(arg), N, H, W, C, k, s, p, ptr(dx), _fl(dy), _s())
+        return dx, None, None, None, None
 
 
 class _AvgPoolFn(torch.autograd.Function):
+    """AvgPool2d(k, k) map -> map of the same dtype."""
+
     @staticmethod
     def forward(ctx, x, k):
         N, H, W, C = x.shape
-        y = torch.empty(N, H // k, W // k, C, device=x.device)
-        call("es_avgpool2d_fwd", ptr(x.contiguous()), N, H, W, C, k, ptr(y), _s())
-        ctx.geom = (N, H, W, C, k)
+        y = torch.empty(N, H // k, W // k, C, dtype=x.dtype, device=x.device)
+        call("es_avgpool2d_fwd_ex", ptr(x.contiguous()), N, H, W, C, k, ptr(y), _fl(x) | (_fl(y) << 1), _s())
+        ctx.geom, ctx.dt = (N, H, W, C, k), x.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
         _own(dy)
         N, H, W, C, k = ctx.geom
-        dx = torch.empty(N, H, W, C, device=dy.device)
-        call("es_avgpool2d_bwd", ptr(dy.contiguous()), N, H, W, C, k, ptr(dx), 0, _s())
+        dx = torch.empty(N, H, W, C, dtype=ctx.dt, device=dy.device)
+        dy = dy.contiguous()
+        call("es_avgpool2d_bwd_ex", ptr(dy), N, H, W, C, k, ptr(dx), 0, _fl(dy) | (_fl(dx) << 1), _s())
         return dx, None
 
 
@@ -557,7 +589,9 @@ class _UpsampleAddFn(torch.autograd.Function):
         N, H, W, C = base.shape
         out = torch.empty_like(base)
         base_c, src_c = base.contiguous(), src.contiguous()
-        call("es_upsample_add_fwd", ptr(base_c), ptr(src_c), N, H, W, C, s, ptr(out), _s())
+        if src_c.dtype != base_c.dtype:
+            raise _lib.EndosslCallError(f"upsample-add of a {src_c.dtype} map onto a {base_c.dtype} map")
+        call("es_upsample_add_fwd_ex", ptr(base_c), ptr(src_c), N, H, W, C, s, ptr(out), _fl(base_c), _s())
         ctx.geom = (N, H, W, C, s)
         return out
 
@@ -566,8 +600,8 @@ class _UpsampleAddFn(torch.autograd.Function):
         _own(dout)
         N, H, W, C, s = ctx.geom
         dout = dout.contiguous()
-        dsrc = torch.empty(N, H // s, W // s, C, device=dout.device)
-        call("es_upsample_bwd", ptr(dout), N, H, W, C, s, ptr(dsrc), _s())
+        dsrc = torch.empty(N, H // s, W // s, C, dtype=dout.dtype, device=dout.device)
+        call("es_upsample_bwd_ex", ptr(dout), N, H, W, C, s, ptr(dsrc), _fl(dout), _s())
         return dout, dsrc, None
 
 
@@ -616,8 +650,11 @@ class _PatchTokensFn(torch.autograd.Function):
         xt = torch.zeros(_rup(N * T, 256), D, device=xb.device)
         b16 = _conv_bf16(m, _Map.nhwc(xb), D, dw)
         wimg = m.conv_pack("trans_patch_conv.weight", D, C, dw)[0] if b16 else m.pview("trans_patch_conv.weight")
-        call("es_conv2d_fwd_bf16" if b16 else "es_conv2d_fwd", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, ptr(wimg),
-             ptr(m.pview("trans_patch_conv.bias")), D, dw, dw, dw, 0, ptr(xt) + 4 * D, T * D, g * D, D, 0, _s())
+        if not b16 and xb.dtype != torch.float32:
+            raise _lib.EndosslCallError("trans_patch_conv: a bf16 map needs the bf16 conv kernels")
+        call("es_conv2d_fwd_bf16_ex" if b16 else "es_conv2d_fwd", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, ptr(wimg),
+             ptr(m.pview("trans_patch_conv.bias")), D, dw, dw, dw, 0, ptr(xt) + 4 * D, T * D, g * D, D, 0,
+             *((None, _fl(xb)) if b16 else ()), _s())
         call("es_tokens_cls_set", ptr(xt), N, T, D, ptr(m.pview("cls_token")), _s())
         ctx.save_for_backward(xb)
         ctx.m, ctx.b16 = m, b16
@@ -642,15 +679,16 @@ class _PatchTokensFn(torch.autograd.Function):
             splits = max(1, min(-(-M // 64), -(-2048 // lib.es_conv2d_dw_tiles(D, C, dw, dw))))
             ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(D, C, dw, dw, splits), device=dxt.device)
         dyp = ptr(dxt) + 4 * D
-        call("es_conv2d_bwd_weight_bf16" if b16 else "es_conv2d_bwd_weight", ptr(xb), N, H, W, C, H * W * C, W * C, C, 1, dyp, T * D, g * D, D, D, dw, dw, dw,
-             0, splits, ptr(ws), ptr(m.gview("trans_patch_conv.weight")), 0, _s())
+        call("es_conv2d_bwd_weight_bf16_ex" if b16 else "es_conv2d_bwd_weight", ptr(xb), N, H, W, C, H * W * C, W * C, C,
+             1, dyp, T * D, g * D, D, D, dw, dw, dw, 0, splits, ptr(ws), ptr(m.gview("trans_patch_conv.weight")), 0,
+             *((_fl(xb),) if b16 else ()), _s())
         wsb = torch.empty(lib.es_chan_workspace(M, D), device=dxt.device)
         call("es_chan_sum", dyp, M, D, T * D, D, cfg.np, ptr(wsb), ptr(m.gview("trans_patch_conv.bias")), 0, _s())
         call("es_chan_sum", ptr(dxt), N, D, T * D, 0, 1, ptr(wsb), ptr(m.gview("cls_token")), 0, _s())
         dxb = torch.empty_like(xb)
         wimg = m.conv_pack("trans_patch_conv.weight", D, C, dw)[1] if b16 else m.pview("trans_patch_conv.weight")
-        call("es_conv2d_bwd_data_bf16" if b16 else "es_conv2d_bwd_data", dyp, T * D, g * D, D, ptr(wimg), N, H, W, C,
-             D, dw, dw, dw, 0, ptr(dxb), H * W * C, W * C, C, 1, 0, _s())
+        call("es_conv2d_bwd_data_bf16_ex" if b16 else "es_conv2d_bwd_data", dyp, T * D, g * D, D, ptr(wimg), N, H, W, C,
+             D, dw, dw, dw, 0, ptr(dxb), H * W * C, W * C, C, 1, 0, *((_fl(dxb) << 1,) if b16 else ()), _s())
         return dxb, None
 
 
@@ -787,12 +825,12 @@ class _ConvHeadFn(torch.autograd.Function):
             raise ValueError(f"the global-pool head expects square maps, got {H}x{W}")
         ncls = m.cfg.num_classes
         pooled = torch.empty(N, C, device=x.device)
-        call("es_avgpool2d_fwd", ptr(x.contiguous()), N, H, W, C, H, ptr(pooled), _s())
+        call("es_avgpool2d_fwd_ex", ptr(x.contiguous()), N, H, W, C, H, ptr(pooled), _fl(x), _s())
         logits = torch.empty(N, ncls, device=x.device)
         call("es_dense_fwd", ptr(pooled), C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")),
              ptr(logits), ncls, N, C, ncls, 0, 0.0, None, 1.0, _s())
         ctx.save_for_backward(pooled)
-        ctx.m, ctx.geom, ctx.pre = m, (N, H, W, C), pre
+        ctx.m, ctx.geom, ctx.pre, ctx.dt = m, (N, H, W, C), pre, x.dtype
         return logits
 
     @staticmethod
@@ -811,8 +849,8 @@ class _ConvHeadFn(torch.autograd.Function):
              ptr(m.gview(pre + "bias")), N, C, ncls, ptr(ws), _s())
         if getattr(m, "frozen_trunk", False):  # IS_FREEZE: the head's parameters only
             return None, None, None, None
-        dx = torch.empty(N, H, W, C, device=dl.device)
-        call("es_avgpool2d_bwd", ptr(dpooled), N, H, W, C, H, ptr(dx), 0, _s())
+        dx = torch.empty(N, H, W, C, dtype=ctx.dt, device=dl.device)
+        call("es_avgpool2d_bwd_ex", ptr(dpooled), N, H, W, C, H, ptr(dx), 0, _fl(dx) << 1, _s())
         return dx, None, None, None
 
 
@@ -874,6 +912,12 @@ class NativeConformer(nn.Module):
         self.version = 0
         self.cur_n = 0
         self.conv_bf16 = CONV_BF16
+
+    @property
+    def map_bf16(self):
+        """bf16 activation / gradient maps after the stem: the bf16 convs on and every conv of the CNN
+        branch eligible for them (stage-1 bottleneck s1 / 4 a multiple of 32: Conformer-B's 64)."""
+        return bool(self.conv_bf16 and MAP_BF16 and (self.cfg.s1 // 4) % 32 == 0 and self.cfg.s1 % 32 == 0)
 
     def set_conv_precision(self, precision):
         """"bf16": convs with channel counts % 32 == 0 on bf16 operands (default); "fp32": all on
@@ -1076,8 +1120,8 @@ class NativeConformer(nn.Module):
         on_tape = torch.is_grad_enabled() and self.training
         frozen = getattr(self, "frozen_trunk", False)
         anchor = self._anchor if (on_tape and not frozen) else None
-        h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor)
-        x_base = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1)
+        h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor, out_dtype=torch.float32)
+        x_base = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1, _map_dtype(self))
         main = torch.cuda.current_stream(x.device)
         tb = _branch_stream(x.device) if BRANCH_STREAMS else main
 
@@ -1127,7 +1171,7 @@ class NativeConformer(nn.Module):
         # arithmetic; fp32 rounding order only)
         x2p = _AvgPoolFn.apply(x2, dw) if dw > 1 else x2
         pooled = conv(self, x2p, _Map.nhwc(x2p), pre + "squeeze_block.conv_project.weight",
-                      pre + "squeeze_block.conv_project.bias", D, 1)
+                      pre + "squeeze_block.conv_project.bias", D, 1, out_dtype=torch.float32)
         xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.")
         xt = _BlockFn.apply(xt, self, pre + "trans_block.")
         # FCUUp (:187-194): token rows 1.. as a [n, g, g, D] map -> 1x1 conv (bias) -> BN -> ReLU;

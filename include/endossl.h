@@ -347,6 +347,60 @@ int es_avgpool2d_bwd(const float* dy, int N, int H, int W, int C, int k, float* 
 int es_upsample_add_fwd(const float* base, const float* src, int N, int H, int W, int C, int s, float* out,
                         hipStream_t stream);
 int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float* dsrc, hipStream_t stream);
+
+/* ---- bf16 activation / gradient maps (the Conformer CNN branch when every conv of the branch takes the
+ * bf16 kernels: conformer.NativeConformer.map_bf16).  Same arguments as the fp32 entry points above plus
+ * `flags`: conv fwd / data grad, pools: bit 0 = the input map is bf16, bit 1 = the output map is bf16;
+ * conv weight grad: bit 0 = x bf16, bit 1 = dy bf16; BatchNorm / chan_sum / upsampling: bit 0 = every map
+ * argument bf16.  Arithmetic in fp32, each output rounded once (an accumulating store adds in fp32).
+ * These replace the same reference ops as their fp32 forms (code/models/conformer.py:75-200 ConvBlock /
+ * FCUDown / FCUUp, torch autocast's bf16 conv outputs). */
+int es_conv2d_fwd_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                          const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, void* y,
+                          long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
+                          hipStream_t stream);
+int es_conv2d_bwd_data_bf16_ex(const void* dy, long syn, long syh, long syw, const void* wt, int N, int H, int W,
+                               int Cin, int Cout, int kh, int kw, int stride, int pad, void* dx, long sxn, long sxh,
+                               long sxw, long sxc, int accumulate, int flags, hipStream_t stream);
+int es_conv2d_bwd_weight_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                                 const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
+                                 int pad, int splits, float* workspace, float* dw, int accumulate, int flags,
+                                 hipStream_t stream);
+int es_chan_sum_ex(const void* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
+                   int accumulate, int flags, hipStream_t stream);
+int es_bn2d_fwd_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                   float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const void* res,
+                   int relu, void* y, float* mean, float* rstd, float* workspace, int flags, hipStream_t stream);
+int es_bn2d_bwd_ex(const void* x, const void* y, const void* dy, int rows, int C, int relu, const float* gamma,
+                   const float* mean, const float* rstd, int train, const float* running_var, float eps, void* dx,
+                   void* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, int flags,
+                   hipStream_t stream);
+int es_bn2d_fwd_partials_ex(const void* x, int rows, int C, float* partials, const float* gamma, const float* beta,
+                            float* running_mean, float* running_var, void* num_batches_tracked, float momentum,
+                            float eps, const void* res, int relu, void* y, float* mean, float* rstd, int flags,
+                            hipStream_t stream);
+int es_bn2d_sums_ex(const void* x, int rows, int C, int mode, const float* sum_g, int rows_g, float* out,
+                    float* workspace, int flags, hipStream_t stream);
+int es_bn2d_fwd_global_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
+                          float* running_var, void* num_batches_tracked, float momentum, float eps, const float* sum_g,
+                          const float* sq_g, int rows_g, const void* res, int relu, void* y, float* mean, float* rstd,
+                          int flags, hipStream_t stream);
+int es_bn2d_bwd_sums_ex(const void* x, const void* y, const void* dy, int rows, int C, int relu, const float* mean,
+                        const float* rstd, float* out, float* workspace, int flags, hipStream_t stream);
+int es_bn2d_bwd_global_ex(const void* x, const void* y, const void* dy, int rows, int C, int relu, const float* gamma,
+                          const float* mean, const float* rstd, const float* sums_local, const float* sums_g, int rows_g,
+                          void* dx, void* gout, float* dgamma, float* dbeta, int accumulate, int flags,
+                          hipStream_t stream);
+int es_maxpool2d_fwd_ex(const float* x, int N, int H, int W, int C, int k, int s, int p, void* y, void* arg, int flags,
+                        hipStream_t stream);
+int es_maxpool2d_bwd_ex(const void* dy, const void* arg, int N, int H, int W, int C, int k, int s, int p, float* dx,
+                        int flags, hipStream_t stream);
+int es_avgpool2d_fwd_ex(const void* x, int N, int H, int W, int C, int k, void* y, int flags, hipStream_t stream);
+int es_avgpool2d_bwd_ex(const void* dy, int N, int H, int W, int C, int k, void* dx, int accumulate, int flags,
+                        hipStream_t stream);
+int es_upsample_add_fwd_ex(const void* base, const void* src, int N, int H, int W, int C, int s, void* out, int flags,
+                           hipStream_t stream);
+int es_upsample_bwd_ex(const void* dout, int N, int H, int W, int C, int s, void* dsrc, int flags, hipStream_t stream);
 /* FCUDown LayerNorm + GELU + cat(cls) fused with ConvTransBlock's x_st + x_t */
 int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln_w, const float* ln_b, float* out,
                            float* mean, float* rstd, int N, int np, int D, float eps, hipStream_t stream);

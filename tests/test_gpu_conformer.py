@@ -331,6 +331,170 @@ def test_bn2d_fwd_bwd(rows_shape, C, relu, with_res):
     _close(y2.cpu(), ref, atol=2e-5)
 
 
+# ------------------------------------------------------------------------------------ bf16 maps
+B16 = torch.bfloat16
+
+
+def _rep(*shape, scale=1.0, shift=0.0):
+    """fp32 values exactly representable in bf16 (so an fp32-map kernel and a bf16-map kernel read the
+    same numbers)."""
+    return (torch.randn(*shape, device=DEV) * scale + shift).to(B16).float()
+
+
+@pytest.mark.parametrize("N,Cin,H,Cout,k,s,p", [(2, 64, 16, 64, 1, 1, 0), (3, 64, 15, 128, 3, 2, 1),
+                                                (2, 32, 13, 96, 3, 1, 1)])
+def test_conv_bf16_maps_match_fp32_maps_rounded(N, Cin, H, Cout, k, s, p):
+    """es_conv2d_*_bf16_ex with bf16 maps: the same gathers, MFMAs and fp32 accumulation order as the fp32-map
+    kernels, one rounding at the store -- so on bf16-representable inputs every bf16-map output is EXACTLY
+    the fp32-map output rounded to bf16 (accumulating stores: the fp32 sum of the two, rounded), the weight
+    gradient and the BatchNorm partials bit-identical, for every input / output dtype combination."""
+    torch.manual_seed(N * 7 + Cin + Cout + k)
+    lib = _lib.load()
+    Ho = (H + 2 * p - k) // s + 1
+    x32 = _rep(N, H, H, Cin)
+    w = torch.randn(Cout, Cin, k, k, device=DEV) * 0.2
+    b = torch.randn(Cout, device=DEV)
+    n = Cout * Cin * k * k
+    wp, wt = torch.empty(n, dtype=B16, device=DEV), torch.empty(n, dtype=B16, device=DEV)
+    call("es_conv2d_pack_bf16", ptr(w), Cout, Cin, k, k, ptr(wp), ptr(wt), S())
+    geo_x = (H * H * Cin, H * Cin, Cin)
+    geo_y = (Ho * Ho * Cout, Ho * Cout, Cout)
+    M = N * Ho * Ho
+    prior = _rep(N, Ho, Ho, Cout)
+    outs = {}
+    for fx in (0, 1):
+        for fy in (0, 1):
+            xin = x32.to(B16) if fx else x32
+            y = torch.empty(N, Ho, Ho, Cout, dtype=B16 if fy else torch.float32, device=DEV)
+            part = torch.empty(lib.es_conv2d_bnstats_size(M, Cout), device=DEV)
+            call("es_conv2d_fwd_bf16_ex", ptr(xin), N, H, H, Cin, *geo_x, 1, ptr(wp), ptr(b), Cout, k, k, s, p, ptr(y),
+                 *geo_y, 0, ptr(part), fx | (fy << 1), S())
+            ya = (prior.to(B16) if fy else prior.clone())
+            call("es_conv2d_fwd_bf16_ex", ptr(xin), N, H, H, Cin, *geo_x, 1, ptr(wp), ptr(b), Cout, k, k, s, p, ptr(ya),
+                 *geo_y, 1, None, fx | (fy << 1), S())
+            outs[(fx, fy)] = (y, part, ya)
+    y0, part0, ya0 = outs[(0, 0)]
+    for (fx, fy), (y, part, ya) in outs.items():
+        assert torch.equal(part, part0), (fx, fy)
+        assert torch.equal(y.float(), y0.to(y.dtype).float()), (fx, fy)
+        assert torch.equal(ya.float(), ya0.to(ya.dtype).float()), (fx, fy)
+    # data gradient (dy -> dx) and weight gradient (x, dy)
+    dy32 = _rep(N, Ho, Ho, Cout)
+    dxp = _rep(N, H, H, Cin)
+    dxs, dws = {}, {}
+    for fa in (0, 1):
+        for fb in (0, 1):
+            dyin = dy32.to(B16) if fa else dy32
+            dx = dxp.to(B16) if fb else dxp.clone()
+            call("es_conv2d_bwd_data_bf16_ex", ptr(dyin), *geo_y, ptr(wt), N, H, H, Cin, Cout, k, k, s, p, ptr(dx),
+                 *geo_x, 1, 1, fa | (fb << 1), S())
+            dxs[(fa, fb)] = dx
+            xin = x32.to(B16) if fa else x32
+            dyw = dy32.to(B16) if fb else dy32
+            ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, Cin, k, k, 0), device=DEV)
+            dw = torch.empty(Cout, Cin, k, k, device=DEV)
+            call("es_conv2d_bwd_weight_bf16_ex", ptr(xin), N, H, H, Cin, *geo_x, 1, ptr(dyw), *geo_y, Cout, k, k, s, p,
+                 0, ptr(ws), ptr(dw), 0, fa | (fb << 1), S())
+            dws[(fa, fb)] = dw
+    for key in dxs:
+        assert torch.equal(dxs[key].float(), dxs[(0, 0)].to(dxs[key].dtype).float()), key
+        assert torch.equal(dws[key], dws[(0, 0)]), key
+
+
+@pytest.mark.parametrize("relu,with_res,C", [(True, True, 64), (True, False, 256), (False, False, 128), (True, True, 6)])
+def test_bn_pool_bf16_maps_match_fp32_maps_rounded(relu, with_res, C):
+    """BatchNorm (statistics pass, conv partials, eval, backward, SyncBatchNorm halves), channel sums, max /
+    average pooling and the nearest upsample-add over bf16 maps: fp32 arithmetic on the widened values, each
+    output rounded once -- on bf16-representable inputs exactly the fp32-map kernels' outputs rounded."""
+    torch.manual_seed(C + relu)
+    N, H, W = 2, 12, 10
+    rows = N * H * W
+    lib = _lib.load()
+    x32 = _rep(N, H, W, C, scale=1.5, shift=0.3)
+    res32 = _rep(N, H, W, C) if with_res else None
+    dy32 = _rep(N, H, W, C)
+    g, b = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    ws = torch.empty(lib.es_chan_workspace(rows, C), device=DEV)
+    res_ = {}
+    for fl in (0, 1):
+        cv = (lambda t: None if t is None else t.to(B16)) if fl else (lambda t: t)
+        x, res, dy = cv(x32), cv(res32), cv(dy32)
+        rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        nbt = torch.zeros((), dtype=torch.int64, device=DEV)
+        y, mean, rstd = torch.empty_like(x), torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm), ptr(rv), ptr(nbt), 0.1, 1e-6, 1, ptr(res),
+             int(relu), ptr(y), ptr(mean), ptr(rstd), ptr(ws), fl, S())
+        ye = torch.empty_like(x)
+        call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm), ptr(rv), None, 0.1, 1e-6, 0, ptr(res),
+             int(relu), ptr(ye), None, None, None, fl, S())
+        dx, gout = torch.empty_like(x), torch.empty_like(x)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        call("es_bn2d_bwd_ex", ptr(x), ptr(y), ptr(dy), rows, C, int(relu), ptr(g), ptr(mean), ptr(rstd), 1, ptr(rv),
+             1e-6, ptr(dx), ptr(gout), ptr(dg), ptr(db), 0, ptr(ws), fl, S())
+        sums = torch.empty(2, C, device=DEV)
+        call("es_bn2d_sums_ex", ptr(x), rows, C, 0, None, 0, ptr(sums[0]), ptr(ws), fl, S())
+        call("es_bn2d_sums_ex", ptr(x), rows, C, 1, ptr(sums[0]), rows, ptr(sums[1]), ptr(ws), fl, S())
+        yg, mg, rg = torch.empty_like(x), torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+        rm2, rv2 = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+        call("es_bn2d_fwd_global_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm2), ptr(rv2), None, 0.1, 1e-6,
+             ptr(sums[0]), ptr(sums[1]), rows, ptr(res), int(relu), ptr(yg), ptr(mg), ptr(rg), fl, S())
+        loc = torch.empty(2 * C, device=DEV)
+        call("es_bn2d_bwd_sums_ex", ptr(x), ptr(yg), ptr(dy), rows, C, int(relu), ptr(mg), ptr(rg), ptr(loc), ptr(ws),
+             fl, S())
+        dxg, dg2, db2 = torch.empty_like(x), torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        call("es_bn2d_bwd_global_ex", ptr(x), ptr(yg), ptr(dy), rows, C, int(relu), ptr(g), ptr(mg), ptr(rg), ptr(loc),
+             ptr(loc), rows, ptr(dxg), None, ptr(dg2), ptr(db2), 0, fl, S())
+        cs = torch.empty(C, device=DEV)
+        call("es_chan_sum_ex", ptr(dy), rows, C, rows * C, C, rows, ptr(ws), ptr(cs), 0, fl, S())
+        out = {"y": y, "ye": ye, "dx": dx, "gout": gout, "yg": yg, "dxg": dxg, "mean": mean, "rstd": rstd, "rm": rm,
+               "rv": rv, "dg": dg, "db": db, "loc": loc, "dg2": dg2, "db2": db2, "cs": cs}
+        res_[fl] = out
+    for k, v1 in res_[1].items():
+        v0 = res_[0][k]
+        assert torch.equal(v1.float(), v0.to(B16).float() if v1.dtype == B16 else v0), k
+    if C % 4:
+        return
+    # pools / upsampling (bf16 maps always have C % 4 == 0), stage by stage: each bf16-map kernel against the
+    # fp32-map kernel fed the same (widened) inputs, rounded
+    H2, W2 = H // 2, W // 2
+    x16 = x32.to(B16)
+
+    def both(name, mk_out, args16, args32, flags):
+        o16, o32 = mk_out(B16), mk_out(torch.float32)
+        call(name + "_ex", *args16(o16), flags, S())
+        call(name, *args32(o32), S())
+        return o16, o32
+
+    yp16, yp32 = both("es_avgpool2d_fwd", lambda dt: torch.empty(N, H2, W2, C, dtype=dt, device=DEV),
+                      lambda o: (ptr(x16), N, H, W, C, 2, ptr(o)), lambda o: (ptr(x32), N, H, W, C, 2, ptr(o)), 3)
+    assert torch.equal(yp16.float(), yp32.to(B16).float())
+    ypw = yp16.float()
+    dxp32 = _rep(N, H, W, C)
+    d16, d32 = dxp32.to(B16), dxp32.clone()
+    call("es_avgpool2d_bwd_ex", ptr(yp16), N, H, W, C, 2, ptr(d16), 1, 3, S())
+    call("es_avgpool2d_bwd", ptr(ypw), N, H, W, C, 2, ptr(d32), 1, S())
+    assert torch.equal(d16.float(), d32.to(B16).float())
+    up16, up32 = both("es_upsample_add_fwd", lambda dt: torch.empty(N, H, W, C, dtype=dt, device=DEV),
+                      lambda o: (ptr(x16), ptr(yp16), N, H, W, C, 2, ptr(o)),
+                      lambda o: (ptr(x32), ptr(ypw), N, H, W, C, 2, ptr(o)), 1)
+    assert torch.equal(up16.float(), up32.to(B16).float())
+    upw = up16.float()
+    ds16, ds32 = both("es_upsample_bwd", lambda dt: torch.empty(N, H2, W2, C, dtype=dt, device=DEV),
+                      lambda o: (ptr(up16), N, H, W, C, 2, ptr(o)), lambda o: (ptr(upw), N, H, W, C, 2, ptr(o)), 1)
+    assert torch.equal(ds16.float(), ds32.to(B16).float())
+    Hm, Wm = (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1
+    a16, a32 = (torch.empty(N, Hm, Wm, C, dtype=torch.int8, device=DEV) for _ in range(2))
+    mp16, mp32 = both("es_maxpool2d_fwd", lambda dt: torch.empty(N, Hm, Wm, C, dtype=dt, device=DEV),
+                      lambda o: (ptr(x32), N, H, W, C, 3, 2, 1, ptr(o), ptr(a16)),
+                      lambda o: (ptr(x32), N, H, W, C, 3, 2, 1, ptr(o), ptr(a32)), 2)
+    assert torch.equal(mp16.float(), mp32.to(B16).float()) and torch.equal(a16, a32)
+    mpw = mp16.float()
+    dm16, dm32 = torch.empty(N, H, W, C, device=DEV), torch.empty(N, H, W, C, device=DEV)
+    call("es_maxpool2d_bwd_ex", ptr(mp16), ptr(a16), N, H, W, C, 3, 2, 1, ptr(dm16), 1, S())
+    call("es_maxpool2d_bwd", ptr(mpw), ptr(a32), N, H, W, C, 3, 2, 1, ptr(dm32), S())
+    assert torch.equal(dm16, dm32)
+
+
 # ------------------------------------------------------------------------------------ pools
 @pytest.mark.parametrize("C", [24, 6])  # the 4-channel vector kernels, and the scalar ones
 def test_maxpool_avgpool_upsample(C):
@@ -507,7 +671,8 @@ def _check_model_vs_oracle(m, state, ocfg, x, bn_keys):
     for bf in (True, False):
         p = {k: v.clone().float().requires_grad_(True) for k, v in state.items() if not cr.is_buffer(k)}
         bufs = {k: v.clone() for k, v in state.items() if cr.is_buffer(k)}
-        oc, ot = cr.conformer_forward(p, bufs, x, ocfg, train=True, bf16=bf, bf16_conv=bf and conv16)
+        oc, ot = cr.conformer_forward(p, bufs, x, ocfg, train=True, bf16=bf, bf16_conv=bf and conv16,
+                                      bf16_maps=bf and m.map_bf16)
         res[bf] = (oc, ot, p, bufs)
     m.train()
     m.flat_grad.zero_()
@@ -604,14 +769,15 @@ def test_semiformer_trainer_vs_reference_train_one(golden, conv):
                        WARMUP_LR=5e-4, LR_DECAY=0.8, SCH_NAME="const", FREQ_EVAL=1)))
     np.testing.assert_allclose(tr.class_weights.cpu().numpy(), d["class_weights"], rtol=1e-6)
     cw = torch.tensor(d["class_weights"]).float()
-    emu = cr.SemiFormerRef(state, ocfg, class_weights=cw, thres=thres, bf16=True, bf16_conv=c16)
+    emu = cr.SemiFormerRef(state, ocfg, class_weights=cw, thres=thres, bf16=True, bf16_conv=c16, bf16_maps=m.map_bf16)
     rec = {}
     for i in range(steps):
         # the oracle at the HIP path's own pre-step state (parameters + BN buffers): every step is checked
         # tightly against the bf16-contract emulation of that state, not against a diverging trajectory
         # (Adam turns bf16 noise on near-zero gradients into +-lr moves, which BatchNorm then amplifies)
         snap = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
-        ref16 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=True, bf16_conv=c16)
+        ref16 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=True, bf16_conv=c16,
+                                 bf16_maps=m.map_bf16)
         ref32 = cr.SemiFormerRef(snap, ocfg, class_weights=cw, thres=thres, bf16=False)
         o = tr.step((lab[i], unl[i]))
         r16, r32 = ref16.step(*lab[i], *unl[i][0]), ref32.step(*lab[i], *unl[i][0])
