@@ -1272,6 +1272,8 @@ int g_attn_fwd_occ = 2;
 // (attn_bwd_dq2_kernel) and dkv2, 0 = the plain loops (all bit-identical).  Default 3: 0.257 ms vs 0.269 (1) and
 // 0.289 (0) for the F1 head batch in isolation, F1 32.51-32.56 vs 32.69-32.72 ms (scripts/attn_bench.py, same box)
 int g_attn_bwd_pipe = 3;
+// the same variants for T = 577 (the 37-tile kernels: one 151-KiB head per CU, four waves)
+int g_attn_bwd_long = 1;
 
 }  // namespace
 
@@ -1289,6 +1291,13 @@ int es_set_attn_variant(int occ) {
 int es_set_attn_bwd_variant(int v) {
   const int old = g_attn_bwd_pipe;
   g_attn_bwd_pipe = v;
+  return old;
+}
+
+// tuning knob: 1 = es_set_attn_bwd_variant's variant also at T > 256 (37 tiles), 0 = the plain loops there
+int es_set_attn_bwd_long(int v) {
+  const int old = g_attn_bwd_long;
+  g_attn_bwd_long = v;
   return old;
 }
 
@@ -1335,23 +1344,27 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
-  if (g_attn_bwd_pipe && nt16 == 13) {  // ViT/16 at 224^2 (T = 197): the pipelined loops
-    if (g_attn_bwd_pipe == 3) {
-      allow_lds(attn_bwd_dq2_kernel<13>, lds_dq);
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<13>), nimg * H, 256, lds_dq, stream, a);
-    } else {
-      allow_lds(attn_bwd_dq_pipe_kernel<13>, lds_dq);
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<13>), nimg * H, 256, lds_dq, stream, a);
-    }
-    if (g_attn_bwd_pipe >= 2) {
-      allow_lds(attn_bwd_dkv2_kernel<13>, lds_dkv);
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<13>), nimg * H, 256, lds_dkv, stream, a);
-    } else {
-      allow_lds(attn_bwd_dkv_pipe_kernel<13>, lds_dkv);
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<13>), nimg * H, 256, lds_dkv, stream, a);
-    }
-    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-  }
+  // ViT/16 at 224^2 (T = 197, 13 tiles) and at 384^2 (T = 577, the 37-tile instantiation): the pipelined /
+  // two-tile loops (bit-identical to the plain ones)
+#define BWD_VARIANTS(N_)                                                                                    \
+  if (g_attn_bwd_pipe == 3) {                                                                               \
+    allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq);                                                             \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq, stream, a);         \
+  } else {                                                                                                  \
+    allow_lds(attn_bwd_dq_pipe_kernel<N_>, lds_dq);                                                         \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<N_>), nimg * H, 256, lds_dq, stream, a);     \
+  }                                                                                                         \
+  if (g_attn_bwd_pipe >= 2) {                                                                               \
+    allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv);                                                           \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);       \
+  } else {                                                                                                  \
+    allow_lds(attn_bwd_dkv_pipe_kernel<N_>, lds_dkv);                                                       \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);   \
+  }                                                                                                         \
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  if (g_attn_bwd_pipe && nt16 == 13) { BWD_VARIANTS(13) }
+  if (g_attn_bwd_pipe && nt16 == 37 && g_attn_bwd_long) { BWD_VARIANTS(37) }
+#undef BWD_VARIANTS
   ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
   ATTN_DISPATCH(attn_bwd_dkv_kernel, nt16, nimg * H, lds_dkv, stream, a);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;

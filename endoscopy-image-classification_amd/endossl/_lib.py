@@ -26,6 +26,7 @@ SIGNATURES = {
     "es_set_tn_variant": (I, [I]),
     "es_set_attn_variant": (I, [I]),
     "es_set_attn_bwd_variant": (I, [I]),
+    "es_set_attn_bwd_long": (I, [I]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),
     "es_tn_problem_size": (Z, []),
     "es_gemm_tn_grouped_prepare": (I, [V, I]),
@@ -190,7 +191,7 @@ def load(path=None):
     # ENDOSSL_ATTN_VARIANT
     for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"),
                     ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant"),
-                    ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant")):
+                    ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant"), ("ENDOSSL_ATTN_BWD_LONG", "es_set_attn_bwd_long")):
         if os.environ.get(env):
             getattr(lib, fn)(int(os.environ[env]))
     if path is None:

@@ -88,6 +88,8 @@ int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate,
 int es_set_attn_variant(int occ);
 /* attention backward loops: 1 = software-pipelined (default), 0 = plain; returns the previous value */
 int es_set_attn_bwd_variant(int v);
+/* 1 (default): the backward variant above also for T > 256 (the 37-tile kernels); 0: plain loops there. */
+int es_set_attn_bwd_long(int v);
 /* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 592 (384^2 / 16) ------ */
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream);

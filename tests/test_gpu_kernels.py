@@ -283,12 +283,12 @@ def test_attention_bwd(n, T, H):
     torch.testing.assert_close(delta2, delta, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("n", [3, 64])
-def test_attention_bwd_pipelined_matches_plain(n):
-    """The software-pipelined dQ / dK-dV loops (es_set_attn_bwd_variant 1) and the two-key-tiles-per-wave
-    dK / dV (2) issue the same MFMAs on the same operands in the same order per key tile as the plain loops
-    (0): dqkv and delta bit-identical."""
-    T, H = 197, 6
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (64, 197, 6), (3, 577, 12), (2, 300, 2)])
+def test_attention_bwd_pipelined_matches_plain(n, T, H):
+    """The software-pipelined dQ / dK-dV loops (es_set_attn_bwd_variant 1), the two-key-tiles-per-wave
+    dK / dV (2) and two-query-tiles dQ (3) issue the same MFMAs on the same operands in the same order per
+    tile as the plain loops (0): dqkv and delta bit-identical, at T = 197 (13 tiles) and in the 37-tile
+    kernels (T = 577, and T = 300 with masked rows)."""
     D = H * 64
     torch.manual_seed(7 + n)
     qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
