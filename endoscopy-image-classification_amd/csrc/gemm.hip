@@ -468,46 +468,52 @@ __global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
 // registers and drop to 3 (measured slower).  The other epilogues fit without the bound.
 template <int EPI>
 constexpr int nt_min_waves() { return (EPI == EPI_GELU || EPI == EPI_GELU_ACT || EPI == EPI_GELU_D) ? 4 : 1; }
-template <int EPI, int BKT, int NST>
+// TBM: output rows per workgroup -- 128 (waves 64 x 64) or 64 (waves 32 x 64: twice the workgroups for a
+// rank's small token shard, where 128-row tiles leave most CUs with one tile and a few with two).
+template <int EPI, int BKT, int NST, int TBM = 128>
 __global__ __launch_bounds__(256, nt_min_waves<EPI>()) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int ROWB = BKT * 2;              // bytes per LDS row
   constexpr int RPI = 1024 / ROWB;           // rows per 1-KiB glds instruction
   constexpr int CPR = ROWB / 16;             // 16-B chunks per row
-  constexpr int IPW = (BM / RPI) / 4;        // glds instructions per wave per operand per stage
-  constexpr int PER = 2 * IPW;               // per stage per wave
-  constexpr int TILE = BM * ROWB;            // bytes per operand tile
-  constexpr int STAGE = 2 * TILE;
+  constexpr int MF = TBM / 32;               // A fragments per wave (wave tile TBM/2 x 64)
+  constexpr int IPA = (TBM / RPI) / 4;       // glds instructions per wave per stage: A operand
+  constexpr int IPB = (BN / RPI) / 4;        //                                     B operand
+  constexpr int PER = IPA + IPB;             // per stage per wave
+  constexpr int TILEA = TBM * ROWB;          // bytes of the A tile
+  constexpr int STAGE = TILEA + BN * ROWB;
+  static_assert(IPA >= 1 && IPB >= 1, "tile");
   const int ntn = p.N / BN;
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+  const int m0 = (wg / ntn) * TBM, n0 = (wg % ntn) * BN;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w >> 1, wn = w & 1;
   const int g = lane >> 4, r = lane & 15;
 
-  const EpiPre<EPI, 4> epre = epi_prefetch<EPI, 4>(p, m0 + wm * 64, n0 + wn * 64, lane);
+  const EpiPre<EPI, 4> epre = epi_prefetch<EPI, 4>(p, m0 + wm * (TBM / 2), n0 + wn * 64, lane);
 
-  const bf16* ga[IPW];
-  const bf16* gb[IPW];
+  const bf16* ga[IPA];
+  const bf16* gb[IPB];
 #pragma unroll
-  for (int j = 0; j < IPW; ++j) {
-    const int row = (w * IPW + j) * RPI + lane / CPR;
-    const int lc = swzk<BKT>(row, lane % CPR);
-    ga[j] = p.A + (size_t)(m0 + row) * p.lda + lc * 8;
-    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + lc * 8;
+  for (int j = 0; j < IPA; ++j) {
+    const int row = (w * IPA + j) * RPI + lane / CPR;
+    ga[j] = p.A + (size_t)(m0 + row) * p.lda + swzk<BKT>(row, lane % CPR) * 8;
+  }
+#pragma unroll
+  for (int j = 0; j < IPB; ++j) {
+    const int row = (w * IPB + j) * RPI + lane / CPR;
+    gb[j] = p.B + (size_t)(n0 + row) * p.ldb + swzk<BKT>(row, lane % CPR) * 8;
   }
 #define NT_ISSUE(BUF, K0)                                                                           \
   {                                                                                                 \
     char* As_ = smem + (BUF) * STAGE;                                                               \
-    _Pragma("unroll") for (int j = 0; j < IPW; ++j) {                                               \
-      glds16(ga[j] + (K0), As_ + (w * IPW + j) * 1024);                                                 \
-      glds16(gb[j] + (K0), As_ + TILE + (w * IPW + j) * 1024);                                          \
-    }                                                                                               \
+    _Pragma("unroll") for (int j = 0; j < IPA; ++j) glds16(ga[j] + (K0), As_ + (w * IPA + j) * 1024); \
+    _Pragma("unroll") for (int j = 0; j < IPB; ++j) glds16(gb[j] + (K0), As_ + TILEA + (w * IPB + j) * 1024); \
   }
 
-  f32x4 acc[4][4];
+  f32x4 acc[MF][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MF; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -526,19 +532,21 @@ __global__ __launch_bounds__(256, nt_min_waves<EPI>()) void gemm_nt_kernel(NTArg
       NT_ISSUE(nb, (kt + NST - 1) * BKT)
     }
     const char* As = smem + buf * STAGE;
-    const char* Bs = As + TILE;
+    const char* Bs = As + TILEA;
 #pragma unroll
     for (int kk = 0; kk < BKT / 32; ++kk) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[MF], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int ra = wm * 64 + i * 16 + r;
-        af[i] = *(const bf16x8*)(As + ra * ROWB + swzk<BKT>(ra, kk * 4 + g) * 16);
+        if (i < MF) {
+          const int ra = wm * (TBM / 2) + i * 16 + r;
+          af[i] = *(const bf16x8*)(As + ra * ROWB + swzk<BKT>(ra, kk * 4 + g) * 16);
+        }
         const int rb = wn * 64 + i * 16 + r;
         bfr[i] = *(const bf16x8*)(Bs + rb * ROWB + swzk<BKT>(rb, kk * 4 + g) * 16);
       }
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < MF; ++mi)
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = mfma16(bfr[ni], af[mi], acc[mi][ni]);
     }
@@ -547,7 +555,7 @@ __global__ __launch_bounds__(256, nt_min_waves<EPI>()) void gemm_nt_kernel(NTArg
 
   // ---- epilogue through LDS (stage buffers are free once every wave passed the last MFMA) ----
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane, epre);
+  staged_epilogue_g<EPI, MF, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * (TBM / 2), n0 + wn * 64, lane, epre);
 }
 #undef NT_ISSUE
 
@@ -946,33 +954,35 @@ inline void launch_reduce_partials(const float* P, float* out, int G, int N, int
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
 // template commas out of the launch macro; a kernel referenced only through a function pointer
 // gets no host stub).
-#define NT_LAUNCH(E, BKT_, NST_)                                                           \
+#define NT_LAUNCH(E, BKT_, NST_, TBM_)                                                     \
   {                                                                                        \
-    const size_t lds = std::max((size_t)NST_ * 2 * BM * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES);   \
-    allow_lds(gemm_nt_kernel<E, BKT_, NST_>, lds);                                         \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_kernel<E, BKT_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
+    const size_t lds = std::max((size_t)NST_ * (TBM_ + BN) * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES); \
+    allow_lds(gemm_nt_kernel<E, BKT_, NST_, TBM_>, lds);                                   \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_kernel<E, BKT_, NST_, TBM_>), dim3(grid), dim3(256), lds, stream, a); \
     return ES_OK;                                                                          \
   }
-#define NT_EPIS(BKT_, NST_)                              \
-  switch (epi) {                                         \
-    case EPI_BF16: NT_LAUNCH(EPI_BF16, BKT_, NST_)       \
-    case EPI_GELU: NT_LAUNCH(EPI_GELU, BKT_, NST_)       \
-    case EPI_F32_RESID: NT_LAUNCH(EPI_F32_RESID, BKT_, NST_) \
-    case EPI_DGELU: NT_LAUNCH(EPI_DGELU, BKT_, NST_)     \
-    case EPI_F32: NT_LAUNCH(EPI_F32, BKT_, NST_)         \
-    case EPI_PATCH: NT_LAUNCH(EPI_PATCH, BKT_, NST_)     \
-    case EPI_GELU_ACT: NT_LAUNCH(EPI_GELU_ACT, BKT_, NST_) \
-    case EPI_GELU_D: NT_LAUNCH(EPI_GELU_D, BKT_, NST_)   \
-    case EPI_MULAUX: NT_LAUNCH(EPI_MULAUX, BKT_, NST_)   \
-    default: return ES_BAD_ARG;                          \
+#define NT_EPIS(BKT_, NST_, TBM_)                                  \
+  switch (epi) {                                                   \
+    case EPI_BF16: NT_LAUNCH(EPI_BF16, BKT_, NST_, TBM_)           \
+    case EPI_GELU: NT_LAUNCH(EPI_GELU, BKT_, NST_, TBM_)           \
+    case EPI_F32_RESID: NT_LAUNCH(EPI_F32_RESID, BKT_, NST_, TBM_) \
+    case EPI_DGELU: NT_LAUNCH(EPI_DGELU, BKT_, NST_, TBM_)         \
+    case EPI_F32: NT_LAUNCH(EPI_F32, BKT_, NST_, TBM_)             \
+    case EPI_PATCH: NT_LAUNCH(EPI_PATCH, BKT_, NST_, TBM_)         \
+    case EPI_GELU_ACT: NT_LAUNCH(EPI_GELU_ACT, BKT_, NST_, TBM_)   \
+    case EPI_GELU_D: NT_LAUNCH(EPI_GELU_D, BKT_, NST_, TBM_)       \
+    case EPI_MULAUX: NT_LAUNCH(EPI_MULAUX, BKT_, NST_, TBM_)       \
+    default: return ES_BAD_ARG;                                    \
   }
 int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   switch (cfg) {
-    case 0: NT_EPIS(64, 2)
-    case 3: NT_EPIS(32, 4)
-    case 4: NT_EPIS(64, 3)
-    case 5: NT_EPIS(32, 2)
-    default: NT_EPIS(32, 3)
+    case 0: NT_EPIS(64, 2, 128)
+    case 3: NT_EPIS(32, 4, 128)
+    case 4: NT_EPIS(64, 3, 128)
+    case 5: NT_EPIS(32, 2, 128)
+    case 11: NT_EPIS(64, 2, 64)
+    case 12: NT_EPIS(32, 3, 64)
+    default: NT_EPIS(32, 3, 128)
   }
 }
 #undef NT_EPIS
@@ -1019,6 +1029,7 @@ using namespace es_gemm;
 // ----------------------------------------------------------------- C-ABI entry points
 static int g_gemm_variant = -1;
 static int g_tn_variant = -1;
+static int g_small_tile = 0;  // the 64 x 128 tile rule for small token shards (es_set_gemm_small_tile; off: r03 A/B)
 
 
 extern "C" {
@@ -1050,6 +1061,10 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //  * ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
   //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
   //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
+  //  * (opt-in, es_set_gemm_small_tile(1)) a rank's small token shard (M < 32768): the 64 x 128 tile (variant
+  //    11) for the residual and weak-GELU epilogues and the N = 384 outputs -- twice the workgroups of the
+  //    128 x 128 tile, 0.88-0.96x its time in isolation (scripts/gemm_bench.py --shard, r03), but no gain in
+  //    the N = 8 shard step (5.578 / 5.579 vs 5.583 / 5.570 ms) and a loss at N = 4 (9.72 vs 9.45 ms);
   //  * (variant -1 only; -2 keeps the rules above) the 256 x 128 two-workgroups-per-CU kernel
   //    (variant 10) for the plain / residual / MULAUX epilogues at F1's long token axis: the qkv and
   //    proj forwards (K = 384), the fc2 data gradient and the N = 384 data gradients of fc1 / qkv:
@@ -1066,6 +1081,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
       variant = M < 32768 ? 0 : 6;
     else if (K >= 768 && N % 256 == 0 && epi != EPI_DGELU)
       variant = 6;
+    else if (g_small_tile && M < 32768 && (epi == EPI_F32_RESID || epi == EPI_GELU_ACT || (N <= 384 && (epi == EPI_BF16 || epi == EPI_F32))))
+      variant = 11;
     else if (gelu)
       variant = K <= 384 ? 5 : 1;
     else if (K <= 384)
@@ -1097,7 +1114,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     if (N % tbn) return ES_BAD_SHAPE;
     return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
   }
-  const int grid = ((M + BM - 1) / BM) * (N / BN);
+  const int tbm = (variant == 11 || variant == 12) ? 64 : BM;
+  const int grid = ((M + tbm - 1) / tbm) * (N / BN);
   const int rc = launch_nt(variant, epi, grid, stream, a);
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -1108,11 +1126,20 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 // 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage; 8 waves, one workgroup per CU, 128x64 or
 // 128x48 per wave: 6 = 256x256 BK64 2-stage, 7 = 256x192 BK64 2-stage, 8 = 256x256 BK32
 // 4-stage, 9 = 256x192 BK32 4-stage; 6/8 need N % 256 == 0, 7/9 N % 192 == 0; 10 = 256x128 BK32
-// 3-stage, 64x64 per wave, two workgroups per CU).
+// 3-stage, 64x64 per wave, two workgroups per CU; 11 / 12 = 64x128 (waves of 32x64) BK64 2-stage / BK32
+// 3-stage).
 // Returns the previous value.
 int es_set_gemm_variant(int v) {
   const int old = g_gemm_variant;
   g_gemm_variant = v;
+  return old;
+}
+
+// Tuning knob: 1 = the 64 x 128 tile for small token shards in the per-shape rules, 0 (default) = without it.
+// Returns the previous value.
+int es_set_gemm_small_tile(int v) {
+  const int old = g_small_tile;
+  g_small_tile = v;
   return old;
 }
 

@@ -20,6 +20,7 @@ SIGNATURES = {
     "es_abi_version": (I, []),
     "es_gemm_nt": (I, [I, V, I, V, I, V, V, I, V, V, I, I, I, I, I, V]),
     "es_set_gemm_variant": (I, [I]),
+    "es_set_gemm_small_tile": (I, [I]),
     "es_gemm_tn_workspace": (Z, [I, I, I]),
     "es_gemm_tn": (I, [V, I, V, I, I, I, I, I, V, V, I, V, V]),
     "es_gemm_tn_ex": (I, [V, I, V, I, I, I, I, I, V, V, I, V, I, V]),
@@ -189,7 +190,7 @@ def load(path=None):
         raise EndosslLibraryError(f"ABI mismatch: library {lib.es_abi_version()} != python {ABI_VERSION}")
     # kernel-family knobs for A/B runs (scripts/, bench.py): ENDOSSL_TN_VARIANT / ENDOSSL_GEMM_VARIANT /
     # ENDOSSL_ATTN_VARIANT
-    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"),
+    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"), ("ENDOSSL_SMALL_TILE", "es_set_gemm_small_tile"),
                     ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant"),
                     ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant"), ("ENDOSSL_ATTN_BWD_LONG", "es_set_attn_bwd_long")):
         if os.environ.get(env):

@@ -45,7 +45,8 @@ def main():
         m, d, hd = 120 * 577, 768, 3072
         NT = [("qkv_fwd", 0, m, 3 * d, d), ("proj_fwd", 2, m, d, d), ("fc1_fwd", 7, m, hd, d), ("fc2_fwd", 2, m, d, hd),
               ("fc2_dgrad", 8, m, hd, d), ("fc1_dgrad", 0, m, d, hd), ("proj_dgrad", 0, m, d, d),
-              ("qkv_dgrad", 0, m, d, 3 * d)]
+              ("qkv_dgrad", 0, m, d, 3 * d), ("fc2_dgrad_dgelu", 3, m, hd, d), ("fc1_fwd_gelu", 1, m, hd, d),
+              ("fc2_dgrad_plain", 0, m, hd, d)]
         TN = [("fc2_wgrad", m, d, hd), ("fc1_wgrad", m, hd, d), ("proj_wgrad", m, d, d), ("qkv_wgrad", m, 3 * d, d)]
     if args.shard > 1 and not args.s1:
         NT = [(n, e, M // args.shard, N, K) for n, e, M, N, K in NT]

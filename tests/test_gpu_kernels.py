@@ -40,7 +40,7 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]
+GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]
 _TILE_N = {6: 256, 7: 192, 8: 256, 9: 192, 10: 128}  # big-tile variants: N must be a multiple of the tile width
 
 
