@@ -238,6 +238,7 @@ def run_secondary(args):
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    map_dtype = None  # the Conformer's CNN map dtype (S1)
     if args.workload == "c1":
         from endossl.comatch import CoMatch
         from endossl.comatch_model import NativeViTEmb
@@ -323,7 +324,9 @@ def run_secondary(args):
         exe = tfl
         desc = (f"S1: SemiFormer step on {name}, {S}^2 ({ccfg.T} tokens), B={B} + 2 x mu*B={B * MU} per GPU, C=23, "
                 f"tau=0.95, lambda_u=1, EMA 0.999; transformer GEMMs and convs with channels % 32 == 0 on bf16 "
-                f"MFMA ({'on' if model.conv_bf16 else 'off: ENDOSSL_CONV_BF16=0'}), BatchNorm / maps fp32")
+                f"MFMA ({'on' if model.conv_bf16 else 'off: ENDOSSL_CONV_BF16=0'}), CNN activation / gradient maps "
+                f"{'bf16' if getattr(model, 'map_bf16', False) else 'fp32'}, BatchNorm statistics fp32")
+        map_dtype = "bf16" if getattr(model, "map_bf16", False) else "fp32"
     steplog = os.environ.get("ENDOSSL_BENCH_STEPLOG") == "1"  # diagnostics: synchronises every step
     for _ in range(args.warmup):
         tr.step(batch)
@@ -387,7 +390,8 @@ def run_secondary(args):
             "value": round(world * unl * args.steps / T, 2),
             "unit": "labeled images/s" if args.workload == "p0" else "unlabeled images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "bf16 operands (GEMMs, convs) / fp32 accumulate, maps, BatchNorm",
+            "dtype": (f"bf16 operands (GEMMs, convs) / fp32 accumulate, BatchNorm statistics; CNN maps {map_dtype}"
+                      if map_dtype else "bf16 operands (GEMMs, convs) / fp32 accumulate, maps, BatchNorm"),
             "data": "synthetic (HBM-resident, seed 0)", "config": {"workload": desc, "parallelism": f"dp{world}"},
             "step_tflop": round(tfl, 3), "executed_step_tflop": round(exe, 3),
             "step_tflops": round(tfl / (ms / 1e3), 1),
