@@ -103,9 +103,12 @@ __device__ __forceinline__ u32x4 pack_bf16x8(const float* v) {
 }
 
 // 8 consecutive outputs C[m][n .. n+7]: v0, v1 = accumulator + bias.
-template <int EPI>
+template <int EPI, int STAUX = 0>
 __device__ __forceinline__ void epi_store8(const NTArgs& p, const EpiCtx<EPI>& x, int m, int n, f32x4 v0, f32x4 v1,
                                            const EpiAuxRegs& a) {
+  auto buf_store16 = [](u32x4 v, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, STAUX);
+  };
   const bool ok = m < p.M;
   int crow = m;
   if constexpr (EPI == EPI_PATCH) {
@@ -193,7 +196,7 @@ template <int NF>
 __host__ __device__ constexpr int epi_wave_bytes() { return 16 * (NF * 64 + 16); }
 constexpr int EPI_WAVE_BYTES = epi_wave_bytes<4>();  // 4352
 
-template <int EPI, int MF, int NF>
+template <int EPI, int MF, int NF, int STAUX = 0>
 __device__ __forceinline__ void staged_epilogue_g(const NTArgs& p, char* wlds, const f32x4 (&acc)[MF][NF], int mw0,
                                                   int nw0, int lane, const EpiPre<EPI, NF>& e) {
   using E = EpiPre<EPI, NF>;
@@ -229,8 +232,8 @@ __device__ __forceinline__ void staged_epilogue_g(const NTArgs& p, char* wlds, c
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it)
-      epi_store8<EPI>(p, x, mw0 + mi * 16 + e.srow[it], nw0 + e.scol[it], v[it][0] + e.b0[it], v[it][1] + e.b1[it],
-                      aux[mi & 1][it]);
+      epi_store8<EPI, STAUX>(p, x, mw0 + mi * 16 + e.srow[it], nw0 + e.scol[it], v[it][0] + e.b0[it],
+                             v[it][1] + e.b1[it], aux[mi & 1][it]);
   }
 }
 
@@ -333,7 +336,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
   }
 
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, 4, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane, epre);
+  staged_epilogue_g<EPI, 4, 4, 2>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * 64, n0 + wn * 64, lane, epre);
 }
 
 
@@ -347,7 +350,14 @@ __global__ __launch_bounds__(512, 1) void gemm_nt256_kernel(NTArgs p) {
 // vmcnt arithmetic holds for every wave.
 // OCC: waves per SIMD the register budget is sized for (launch_bounds' second argument; 4: <= 128
 // VGPRs, so two 8-wave workgroups share a CU and one's epilogue runs beside the other's main loop).
-template <int EPI, int WM, int MF, int NF, int NST, int BKT, int OCC = 1>
+// PROBE (measurement variants 13..15 only): 1 = operand stream alone, 2 = MFMAs alone (no DMA),
+// 3 = no epilogue (main loop only), 4 = operand stream alone without the epilogue, 5 = epilogue alone;
+// 0 = the kernel.
+// STAUX: cache-policy bits of the epilogue's C stores (0 plain, 2 nt, 16 sc1).  nt by default in every NT
+// family: isolated at the F1 shapes (r03, scripts/gemm_bench.py) the qkv forward 138 -> 122.5 us, proj
+// forward 92.6 -> 78.7, fc1 forward 254 -> 195 (256x128 tile), qkv data gradient 131 -> 107 (128x128 BK64);
+// sc1 (write-through, dropped from L2) was slower than plain.
+template <int EPI, int WM, int MF, int NF, int NST, int BKT, int OCC = 1, int PROBE = 0, int STAUX = 2>
 __global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int WN = 8 / WM;
@@ -396,10 +406,12 @@ __global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
 #define BIG_ISSUE(BUF, K0)                                                        \
   {                                                                               \
     char* S_ = smem + (BUF) * STAGE;                                              \
+    if constexpr (PROBE != 2 && PROBE != 5) {                                     \
     _Pragma("unroll") for (int j = 0; j < IA; ++j) glds16(ga[j] + (K0), S_ + da[j]); \
     _Pragma("unroll") for (int j = 0; j < IBF; ++j) glds16(gb[j] + (K0), S_ + db[j]); \
     if constexpr (IBH) {                                                          \
       if (lane < 32) glds16(gb[IBF] + (K0), S_ + db[IBF]);                        \
+    }                                                                             \
     }                                                                             \
   }
 
@@ -425,7 +437,7 @@ __global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
     const char* As = smem + buf * STAGE;
     const char* Bs = As + TA;
 #pragma unroll
-    for (int kk = 0; kk < BKT / 32; ++kk) {
+    for (int kk = 0; kk < ((PROBE == 1 || PROBE >= 4) ? 0 : BKT / 32); ++kk) {
       bf16x8 af[MF], bfr[NF];
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
@@ -447,10 +459,189 @@ __global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
     buf = buf + 1 == NST ? 0 : buf + 1;
   }
 #undef BIG_ISSUE
+  if constexpr (PROBE == 3 || PROBE == 4) {
+    if (acc[0][0][0] == 1.2345f) ((float*)p.C)[tid] = acc[MF - 1][NF - 1][3];  // keeps the MFMAs live
+    return;
+  }
   if constexpr (OCC >= 4) epre = epi_prefetch<EPI, NF>(p, m0 + wm * MF * 16, n0 + wn * NF * 16, lane);
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, MF, NF>(p, smem + w * epi_wave_bytes<NF>(), acc, m0 + wm * MF * 16, n0 + wn * NF * 16,
-                                 lane, epre);
+  staged_epilogue_g<EPI, MF, NF, STAUX>(p, smem + w * epi_wave_bytes<NF>(), acc, m0 + wm * MF * 16,
+                                        n0 + wn * NF * 16, lane, epre);
+}
+
+// ---- persistent ring NT kernel ------------------------------------------------------------------
+// One 512-thread workgroup per CU walks its tiles (256 x 128 output, 8 waves of 64 x 64, 32-deep K
+// steps); the LDS ring of RING slots runs ACROSS tiles: the step sequence is (tile, k) flattened, and
+// step s + RING - 1 is issued right after the barrier that publishes step s, whichever tile it
+// belongs to -- so the next tile's first stages are in flight during this tile's epilogue, and no
+// workgroup launch, prologue bubble or teardown sits between tiles.  Measured on the isolated
+// variant-10 kernel (two workgroups per CU, one tile each) at the qkv forward shape: main loop alone
+// 77 us, epilogue alone 35 us, operand stream alone 74 us, operand stream + epilogue 142 us (the full
+// kernel 139 us) -- the tile-serial structure, not the arithmetic, set its time.
+// Each slot holds the A (256 x 32) and B (128 x 32) stages plus the tile's 128 bias values (every step
+// carries them: 512 B per 24 KiB, a uniform DMA count per step); the epilogue stages its fp32 rows in
+// the slot the tile's last step just freed (8-row chunks, 2,176 B per wave), so the ring keeps
+// RING - 1 = 5 steps (120 KiB) in flight.  The DMA is inline asm (glds16_asm: the compiler would
+// drain pending LDS-DMA in front of the epilogue's LDS writes); every wait is a counted vmcnt over
+// the wave's own DMA and epilogue operations.  Tiles: t = j * G + xcd * (G / 8) + slot, so the
+// workgroups of one XCD work on 32 consecutive tiles (shared A rows in that XCD's L2).
+template <int EPI>
+constexpr int ring_epi_ops() {  // vm operations per lane per 8-row chunk: C stores + aux loads
+  return ((EPI == EPI_GELU || EPI == EPI_GELU_D || EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PATCH) ? 2 : 1) +
+         ((EPI == EPI_F32_RESID || EPI == EPI_PATCH) ? 2 : ((EPI == EPI_DGELU || EPI == EPI_MULAUX) ? 1 : 0));
+}
+
+// vmcnt immediates 0..63 (counted waits computed at run time)
+__device__ __forceinline__ void wait_vmcnt_any(int n) {
+  switch (n) {
+#define ES_VM1(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define ES_VM8(B) ES_VM1(B) ES_VM1(B + 1) ES_VM1(B + 2) ES_VM1(B + 3) ES_VM1(B + 4) ES_VM1(B + 5) ES_VM1(B + 6) ES_VM1(B + 7)
+    ES_VM8(1) ES_VM8(9) ES_VM8(17) ES_VM8(25) ES_VM8(33) ES_VM8(41) ES_VM8(49) ES_VM1(57) ES_VM1(58) ES_VM1(59)
+    ES_VM1(60) ES_VM1(61) ES_VM1(62) ES_VM1(63)
+#undef ES_VM8
+#undef ES_VM1
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+template <int EPI, int RING, int STAUX, int OCC = 1>
+__global__ __launch_bounds__(512, OCC) void gemm_nt_ring_kernel(NTArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TBM = 256, TBN = 128, BKT = 32, ROWB = 64, RPI = 16, CPR = 4;
+  constexpr int IA = TBM / (8 * RPI), IB = TBN / (8 * RPI);  // 2 + 1 full pieces per wave per step
+  constexpr int PER = IA + IB + 1;                          // + the bias piece
+  constexpr int TA = TBM * ROWB, TB = TBN * ROWB, SLOT = TA + TB + TBN * 4;
+  constexpr int D = RING - 1;
+  constexpr int EOPS = 8 * ring_epi_ops<EPI>();
+  constexpr int EROWB = 4 * 64 + 16;  // epilogue staging row: 64 fp32 + 16 B pad
+  const int ntn = p.N / TBN, T = ((p.M + TBM - 1) / TBM) * ntn;
+  const int G = gridDim.x, per_x = G >> 3;
+  const int t0 = (blockIdx.x & 7) * per_x + (blockIdx.x >> 3);
+  const int ntiles = t0 < T ? (T - 1 - t0) / G + 1 : 0;
+  const int KS = p.K / BKT;
+  const int S = ntiles * KS;
+  if (S == 0) return;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int g = lane >> 4, r = lane & 15;
+
+  // per-lane DMA source offsets (elements) relative to the tile's (m0, n0, k0)
+  size_t oa[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = (j * 8 + w) * RPI + lane / CPR;
+    oa[j] = (size_t)row * p.lda + swz64(row, lane % CPR) * 8;
+  }
+  const int rowb = w * RPI + lane / CPR;
+  const size_t ob = (size_t)rowb * p.ldb + swz64(rowb, lane % CPR) * 8;
+  const float* biasp = p.bias ? p.bias : (const float*)p.A;  // null bias: harmless bytes, never read back
+  // issue-side cursor: step si = (tile ji, step ki)
+  int ji = 0, ki = 0;
+  const bf16* ta = p.A;
+  const bf16* tb = p.B;
+  const float* tbias = biasp;
+  auto set_tile = [&](int j) {
+    const int t = j * G + t0, mb = t / ntn, nb = t - mb * ntn;
+    ta = p.A + (size_t)mb * TBM * p.lda;
+    tb = p.B + (size_t)nb * TBN * p.ldb;
+    tbias = biasp + (p.bias ? nb * TBN : 0);
+  };
+  set_tile(0);
+  auto issue_next = [&](int slot) {
+    char* S_ = smem + slot * SLOT;
+    const int k0 = ki * BKT;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) glds16_asm(ta + oa[j] + k0, S_ + (j * 8 + w) * 1024);
+    glds16_asm(tb + ob + k0, S_ + TA + w * 1024);
+    if (lane < 4) glds16_asm(tbias + lane * 4 + w * 16, S_ + TA + TB + w * 64);  // 64 B per wave (lane-linear)
+    if (++ki == KS) {
+      ki = 0;
+      if (++ji < ntiles) set_tile(ji);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int npro = S < D ? S : D;
+  for (int st = 0; st < npro; ++st) issue_next(st);
+  int slot = 0;      // slot of step s
+  int jt = 0;        // tile of step s
+  for (int s = 0; s < S; ++s) {
+    // ops issued after DMA(s): the DMAs of steps s+1 .. min(s+D-1, S-1) and the epilogues of tile-final
+    // steps e in [max(0, s-D), s-1] (DMA(s) was issued during step s-D, before its compute)
+    {
+      const int nd = min(s + D - 1, S - 1) - s;
+      const int lo = s - D > 0 ? s - D : 0;
+      const int ne = s / KS - lo / KS;  // tile-final steps e with lo <= e <= s-1: (e + 1) % KS == 0
+      wait_vmcnt_any(nd * PER + ne * EOPS);
+    }
+    __builtin_amdgcn_s_barrier();
+    if (s + D < S) {
+      int ns = slot + D;
+      ns = ns >= RING ? ns - RING : ns;
+      issue_next(ns);
+    }
+    const char* As = smem + slot * SLOT;
+    const char* Bs = As + TA;
+    {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int rb = wn * 64 + j * 16 + r;
+        bfr[j] = *(const bf16x8*)(Bs + rb * ROWB + swz64(rb, g) * 16);
+        const int ra = wm * 64 + j * 16 + r;
+        af[j] = *(const bf16x8*)(As + ra * ROWB + swz64(ra, g) * 16);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if ((s + 1) % KS == 0) {
+      // tile epilogue in the slot this step just freed (refilled only by DMA(s + RING), issued after the
+      // next step's barrier)
+      __builtin_amdgcn_s_barrier();
+      const int t = jt * G + t0, mb = t / ntn, nb = t - mb * ntn;
+      const int mw0 = mb * TBM + wm * 64, nw0 = nb * TBN + wn * 64;
+      char* stg = (char*)As + w * (8 * EROWB);
+      const int srow = lane >> 3, scol = (lane & 7) * 8;
+      f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
+      if (p.bias) {
+        const float* bl = (const float*)(As + TA + TB) + wn * 64 + scol;
+        b0 = *(const f32x4*)bl;
+        b1 = *(const f32x4*)(bl + 4);
+      }
+      const EpiCtx<EPI> x = epi_ctx<EPI>(p);
+      EpiAuxRegs aux[2];
+      aux[0] = epi_load_aux<EPI>(p, x, mw0 + srow, nw0 + scol);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const int mi = c >> 1, h = c & 1;
+        if ((r >> 3) == h) {
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) *(f32x4*)(stg + (r & 7) * EROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
+        }
+        __builtin_amdgcn_wave_barrier();
+        const f32x4 v0 = *(const f32x4*)(stg + srow * EROWB + scol * 4);
+        const f32x4 v1 = *(const f32x4*)(stg + srow * EROWB + scol * 4 + 16);
+        __builtin_amdgcn_wave_barrier();
+        if (c + 1 < 8) aux[(c + 1) & 1] = epi_load_aux<EPI>(p, x, mw0 + (c + 1) * 8 + srow, nw0 + scol);
+        epi_store8<EPI, STAUX>(p, x, mw0 + c * 8 + srow, nw0 + scol, v0 + b0, v1 + b1, aux[c & 1]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      ++jt;
+    }
+    slot = slot + 1 == RING ? 0 : slot + 1;
+  }
 }
 
 // v0 family: 128x128 output tile, 4 waves (2x2, 64x64 each), K step BKT in {32, 64}, NST-stage
@@ -470,7 +661,7 @@ template <int EPI>
 constexpr int nt_min_waves() { return (EPI == EPI_GELU || EPI == EPI_GELU_ACT || EPI == EPI_GELU_D) ? 4 : 1; }
 // TBM: output rows per workgroup -- 128 (waves 64 x 64) or 64 (waves 32 x 64: twice the workgroups for a
 // rank's small token shard, where 128-row tiles leave most CUs with one tile and a few with two).
-template <int EPI, int BKT, int NST, int TBM = 128>
+template <int EPI, int BKT, int NST, int TBM = 128, int STAUX = 2>
 __global__ __launch_bounds__(256, nt_min_waves<EPI>()) void gemm_nt_kernel(NTArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int ROWB = BKT * 2;              // bytes per LDS row
@@ -555,7 +746,8 @@ __global__ __launch_bounds__(256, nt_min_waves<EPI>()) void gemm_nt_kernel(NTArg
 
   // ---- epilogue through LDS (stage buffers are free once every wave passed the last MFMA) ----
   __builtin_amdgcn_s_barrier();
-  staged_epilogue_g<EPI, MF, 4>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * (TBM / 2), n0 + wn * 64, lane, epre);
+  staged_epilogue_g<EPI, MF, 4, STAUX>(p, smem + w * EPI_WAVE_BYTES, acc, m0 + wm * (TBM / 2), n0 + wn * 64, lane,
+                                       epre);
 }
 #undef NT_ISSUE
 
@@ -722,7 +914,9 @@ __global__ __launch_bounds__(256) void gemm_tn_grouped_kernel(const TNGroupEntry
 constexpr int TB1 = 384, TB2 = 192;
 __device__ __forceinline__ int swz384(int r, int c) { return c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2)); }
 
-template <int BKM, int NST, bool ASM = true>
+// PROBE (measurement variants only, es_gemm_tn_ex 10..13): 1 = the operand stream alone (no transposed
+// reads, no MFMAs), 2 = the MFMAs alone on whatever the ring holds (no DMA); 0 = the kernel.
+template <int BKM, int NST, bool ASM = true, int PROBE = 0>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int R1B = TB1 * 2, R2B = TB2 * 2;          // LDS row bytes: 768, 384
@@ -740,7 +934,11 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
   const int n1_0 = (tile / nt2) * TB1, n2_0 = (tile % nt2) * TB2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int w1 = w >> 1, w2 = w & 1;
-  const bool do_bias = p.PB != nullptr && (tile % nt2) == 0 && w2 == 0;
+  // the bias gradient's 6 extra MFMAs per A1 fragment row are split between the two w2 waves (3 each), so
+  // every SIMD of a bias workgroup carries the same MFMA count (waves 0, 2, 4, 6 sit on SIMDs 0 / 1 and
+  // 1, 3, 5, 7 on SIMDs 2 / 3: with the bias on the w2 = 0 waves alone two SIMDs ran 84 MFMAs per 32
+  // tokens against 72)
+  const bool do_bias = p.PB != nullptr && (tile % nt2) == 0;
   const int mbeg = split * p.mchunk;
   const int mend = min(mbeg + p.mchunk, (p.M + BKM - 1) / BKM * BKM);
   const int g = lane >> 4, t = lane & 15, q = t >> 2, p4 = t & 3;
@@ -765,10 +963,12 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
     char* S_ = smem + (BUF) * STAGE;                                                             \
     const char* x1 = b1 + (size_t)(KT) * s1;                                                     \
     const char* x2 = b2 + (size_t)(KT) * s2;                                                     \
+    if constexpr (PROBE != 2) {                                                                  \
     _Pragma("unroll") for (int j = 0; j < F1; ++j) GLDS(x1 + o1[j], S_ + (j * 8 + w) * 1024);  \
     _Pragma("unroll") for (int j = 0; j < F2; ++j) GLDS(x2 + o2[j], S_ + T1B + (j * 8 + w) * 1024); \
     if constexpr (H2) {                                                                          \
       if (lane < 32) GLDS(x2 + o2[F2], S_ + T1B + F2 * 8192 + w * 512);                          \
+    }                                                                                            \
     }                                                                                            \
   }
 
@@ -778,10 +978,11 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
     if constexpr (ASM) glds16_asm(src, dst);
     else glds16(src, dst);
   };
-  f32x4 acc[6][6], bacc[6];
+  f32x4 acc[6][6], bacc[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    bacc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -805,7 +1006,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
     const char* T1 = smem + buf * STAGE;
     const char* T2 = T1 + T1B;
 #pragma unroll
-    for (int hh = 0; hh < BKM / 32; ++hh) {
+    for (int hh = 0; hh < (PROBE == 1 ? 0 : BKM / 32); ++hh) {
       const int r1 = hh * 32 + 8 * g + q, r2 = r1 + 4;
       const int off = (p4 & 1) * 8;
       bf16x8 bfr[6];
@@ -816,8 +1017,13 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
                       lds_tr4(T1 + r2 * R1B + swz256(r2, cb) * 16 + off));
       }
       if (do_bias) {
+        if (w2 == 0) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) bacc[i] = mfma16(ones, bfr[i], bacc[i]);
+          for (int i = 0; i < 3; ++i) bacc[i] = mfma16(ones, bfr[i], bacc[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 3; ++i) bacc[i] = mfma16(ones, bfr[3 + i], bacc[i]);
+        }
       }
 #pragma unroll
       for (int a = 0; a < 6; ++a) {
@@ -844,7 +1050,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
   }
   if (do_bias && g == 0) {
 #pragma unroll
-    for (int i = 0; i < 6; ++i) p.PB[(size_t)split * p.N1 + n1_0 + w1 * 96 + i * 16 + t] = bacc[i][0];
+    for (int i = 0; i < 3; ++i) p.PB[(size_t)split * p.N1 + n1_0 + w1 * 96 + (w2 * 3 + i) * 16 + t] = bacc[i][0];
   }
 }
 
@@ -954,25 +1160,25 @@ inline void launch_reduce_partials(const float* P, float* out, int G, int N, int
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
 // template commas out of the launch macro; a kernel referenced only through a function pointer
 // gets no host stub).
-#define NT_LAUNCH(E, BKT_, NST_, TBM_)                                                     \
+#define NT_LAUNCH(E, BKT_, NST_, TBM_, ...)                                                \
   {                                                                                        \
     const size_t lds = std::max((size_t)NST_ * (TBM_ + BN) * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES); \
-    allow_lds(gemm_nt_kernel<E, BKT_, NST_, TBM_>, lds);                                   \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_kernel<E, BKT_, NST_, TBM_>), dim3(grid), dim3(256), lds, stream, a); \
+    allow_lds(gemm_nt_kernel<E, BKT_, NST_, TBM_, ##__VA_ARGS__>, lds);                   \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_kernel<E, BKT_, NST_, TBM_, ##__VA_ARGS__>), dim3(grid), dim3(256), lds, stream, a); \
     return ES_OK;                                                                          \
   }
-#define NT_EPIS(BKT_, NST_, TBM_)                                  \
-  switch (epi) {                                                   \
-    case EPI_BF16: NT_LAUNCH(EPI_BF16, BKT_, NST_, TBM_)           \
-    case EPI_GELU: NT_LAUNCH(EPI_GELU, BKT_, NST_, TBM_)           \
-    case EPI_F32_RESID: NT_LAUNCH(EPI_F32_RESID, BKT_, NST_, TBM_) \
-    case EPI_DGELU: NT_LAUNCH(EPI_DGELU, BKT_, NST_, TBM_)         \
-    case EPI_F32: NT_LAUNCH(EPI_F32, BKT_, NST_, TBM_)             \
-    case EPI_PATCH: NT_LAUNCH(EPI_PATCH, BKT_, NST_, TBM_)         \
-    case EPI_GELU_ACT: NT_LAUNCH(EPI_GELU_ACT, BKT_, NST_, TBM_)   \
-    case EPI_GELU_D: NT_LAUNCH(EPI_GELU_D, BKT_, NST_, TBM_)       \
-    case EPI_MULAUX: NT_LAUNCH(EPI_MULAUX, BKT_, NST_, TBM_)       \
-    default: return ES_BAD_ARG;                                    \
+#define NT_EPIS(BKT_, NST_, TBM_, ...)                                            \
+  switch (epi) {                                                                  \
+    case EPI_BF16: NT_LAUNCH(EPI_BF16, BKT_, NST_, TBM_, ##__VA_ARGS__)           \
+    case EPI_GELU: NT_LAUNCH(EPI_GELU, BKT_, NST_, TBM_, ##__VA_ARGS__)           \
+    case EPI_F32_RESID: NT_LAUNCH(EPI_F32_RESID, BKT_, NST_, TBM_, ##__VA_ARGS__) \
+    case EPI_DGELU: NT_LAUNCH(EPI_DGELU, BKT_, NST_, TBM_, ##__VA_ARGS__)         \
+    case EPI_F32: NT_LAUNCH(EPI_F32, BKT_, NST_, TBM_, ##__VA_ARGS__)             \
+    case EPI_PATCH: NT_LAUNCH(EPI_PATCH, BKT_, NST_, TBM_, ##__VA_ARGS__)         \
+    case EPI_GELU_ACT: NT_LAUNCH(EPI_GELU_ACT, BKT_, NST_, TBM_, ##__VA_ARGS__)   \
+    case EPI_GELU_D: NT_LAUNCH(EPI_GELU_D, BKT_, NST_, TBM_, ##__VA_ARGS__)       \
+    case EPI_MULAUX: NT_LAUNCH(EPI_MULAUX, BKT_, NST_, TBM_, ##__VA_ARGS__)       \
+    default: return ES_BAD_ARG;                                                   \
   }
 int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   switch (cfg) {
@@ -988,11 +1194,11 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
 #undef NT_EPIS
 #undef NT_LAUNCH
 
-#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_, BKT_, OCC_)                                             \
+#define BIG_LAUNCH(E, WM_, MF_, NF_, NST_, BKT_, OCC_, ...)                                        \
   {                                                                                                 \
     const size_t lds = (size_t)NST_ * (WM_ * MF_ * 16 + (8 / WM_) * NF_ * 16) * BKT_ * 2;            \
-    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_, OCC_>, lds);                         \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_, OCC_>), dim3(grid), \
+    allow_lds(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_, OCC_, ##__VA_ARGS__>, lds);          \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_big_kernel<E, WM_, MF_, NF_, NST_, BKT_, OCC_, ##__VA_ARGS__>), dim3(grid), \
                        dim3(512), lds, stream, a);                                                  \
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;                                  \
   }
@@ -1011,6 +1217,13 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   }
 #define BIG_EPIS(WM_, MF_, NF_, NST_, BKT_) BIG_EPIS2(WM_, MF_, NF_, NST_, BKT_, 1)
 int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
+  if (cfg >= 13 && cfg <= 17 && epi == EPI_BF16) {  // probes of variant 10 (plain epilogue only)
+    if (cfg == 13) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 1)
+    if (cfg == 14) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 2)
+    if (cfg == 16) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 4)
+    if (cfg == 17) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 5)
+    BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 3)
+  }
   switch (cfg) {
     case 10: BIG_EPIS2(4, 4, 4, 3, 32, 4)  // 256x128, BK32, 3 stages (72 KiB), two workgroups per CU
     case 6: BIG_EPIS(2, 8, 4, 2, 64)   // 256x256, BK64, 2 stages (128 KiB)
@@ -1029,7 +1242,7 @@ using namespace es_gemm;
 // ----------------------------------------------------------------- C-ABI entry points
 static int g_gemm_variant = -1;
 static int g_tn_variant = -1;
-static int g_small_tile = 0;  // the 64 x 128 tile rule for small token shards (es_set_gemm_small_tile; off: r03 A/B)
+static int g_small_tile = 1;  // the 64 x 128 tile rules (es_set_gemm_small_tile; 0 = without them)
 
 
 extern "C" {
@@ -1048,45 +1261,45 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     return ES_BAD_ARG;
   if (epi == EPI_PATCH && np <= 0) return ES_BAD_ARG;
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, K, lda, ldb, ldc, ldaux, np};
-  // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py, isolated launches
-  // at the F1 shapes and at 1/2, 1/4, 1/8 of the batch -- a rank's share at N GPUs, --shard):
-  //  * the GELU epilogues (fc1 forward): 128x128 BK32 two-stage at 4-5 workgroups/CU for K <= 384;
-  //  * the other K <= 384 GEMMs: 128x128 BK64 two-stage (variant 0) for the N = 384 outputs (proj
-  //    forward / dgrad: 0.91-0.96x the BK32 kernels' time at every batch share) and for M < 32768
-  //    (qkv forward 0.90x at 1/4, 0.85x at 1/8), else BK32 (three-stage for DGELU);
-  //  * fc2 dgrad (EPI_MULAUX: 310 MB of GELU' read at F1) on the 256x256 tile (200 vs 228 us), on
-  //    variant 0 below M = 32768 (0.90x at 1/4, 0.78x at 1/8);
-  //  * long K (fc2 forward, fc1 / qkv dgrad): the 256x128 three-stage ring, variant 0 below
-  //    M = 65536 (0.81x for the two dgrads at 1/2);
+  // variant -1 (default): per-shape choice measured on MI355X (scripts/gemm_bench.py, isolated launches at
+  // the F1 shapes and at 1/2, 1/4, 1/8 of the batch -- a rank's share at N GPUs, --shard; r03 sweep with the
+  // nt C stores, profiles/r03_nt_sweep.txt):
+  //  * N = 384 outputs on the 64 x 128 tile (variant 11: twice the workgroups of the 128 x 128 tile): the
+  //    residual proj forward (K = 384) at every size (F1 78.7 -> 69.9 us, weak 77.7 -> 63.4) and every
+  //    N = 384 output of a rank's small shard (M < 32,768: fc2 forward, the fc1 / qkv / proj data
+  //    gradients, 0.85-0.93x), and the weak fc1 (GELU) there;
+  //  * the long-K N = 384 data gradients (fc1 / qkv dgrad) at F1: 128x128 BK64 (qkv dgrad 116.5 -> 101 us);
+  //  * the plain / residual / MULAUX / GELU_D epilogues at F1's long token axis (the qkv forward, the fc1
+  //    forward with its GELU' output, the fc2 forward and data gradient): the 256 x 128 two-workgroups-per-CU
+  //    kernel (variant 10; fc1 forward 204 -> 196 us vs the 128 x 128 kernel);
+  //  * the GELU epilogues otherwise (weak fc1): 128x128 BK32 two-stage at 4-5 workgroups/CU for K <= 384;
+  //  * the other K <= 384 GEMMs: 128x128 BK64 two-stage (variant 0) below M = 65,536 (qkv forward at a
+  //    rank's half share 73 -> 61 us) and for N <= 384, else BK32;
   //  * ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
   //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
   //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
-  //  * (opt-in, es_set_gemm_small_tile(1)) a rank's small token shard (M < 32768): the 64 x 128 tile (variant
-  //    11) for the residual and weak-GELU epilogues and the N = 384 outputs -- twice the workgroups of the
-  //    128 x 128 tile, 0.88-0.96x its time in isolation (scripts/gemm_bench.py --shard, r03), but no gain in
-  //    the N = 8 shard step (5.578 / 5.579 vs 5.583 / 5.570 ms) and a loss at N = 4 (9.72 vs 9.45 ms);
-  //  * (variant -1 only; -2 keeps the rules above) the 256 x 128 two-workgroups-per-CU kernel
-  //    (variant 10) for the plain / residual / MULAUX epilogues at F1's long token axis: the qkv and
-  //    proj forwards (K = 384), the fc2 data gradient and the N = 384 data gradients of fc1 / qkv:
-  //    0.96-0.97x the time of the kernels above at those shapes (scripts/gemm_bench.py, r02d); F1
-  //    35.41 -> 35.21 ms, and 34.58 -> 34.48 ms with the fc2 data gradient too (same-box A/Bs).
+  //  es_set_gemm_small_tile(0) drops the 64 x 128 rules; variant -2 drops the two-workgroup rules.
   int variant = g_gemm_variant;
   const bool two_wg = variant == -1;
   if (variant < 0) {
     const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
     const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || epi == EPI_MULAUX;
-    if (two_wg && plain && M >= 65536 && ((K <= 384 && N >= 384) || (K >= 768 && N == 384)))
+    if (g_small_tile && N <= 384 && ((K <= 384 && epi == EPI_F32_RESID) || (M < 32768 && (plain || epi == EPI_GELU_ACT))))
+      variant = 11;
+    else if (g_small_tile && M < 32768 && epi == EPI_GELU_ACT)
+      variant = 11;
+    else if (two_wg && M >= 65536 && K >= 768 && N == 384 && epi == EPI_BF16)
+      variant = 0;
+    else if (two_wg && (plain || epi == EPI_GELU_D) && M >= 65536 && ((K <= 384 && N >= 384) || (K >= 768 && N == 384)))
       variant = 10;
     else if (K <= 384 && N % 256 == 0 && epi == EPI_MULAUX)
-      variant = M < 32768 ? 0 : 6;
+      variant = M < 65536 ? 0 : 6;
     else if (K >= 768 && N % 256 == 0 && epi != EPI_DGELU)
       variant = 6;
-    else if (g_small_tile && M < 32768 && (epi == EPI_F32_RESID || epi == EPI_GELU_ACT || (N <= 384 && (epi == EPI_BF16 || epi == EPI_F32))))
-      variant = 11;
     else if (gelu)
       variant = K <= 384 ? 5 : 1;
     else if (K <= 384)
-      variant = (epi == EPI_F32_RESID || N <= 384 || M < 32768) ? 0 : (epi == EPI_DGELU ? 2 : 5);
+      variant = (epi == EPI_F32_RESID || N <= 384 || M < 65536) ? 0 : (epi == EPI_DGELU ? 2 : 5);
     else
       variant = M < 65536 ? 0 : 1;
   }
@@ -1109,8 +1322,41 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
-  if (variant >= 6 && variant <= 10) {
-    const int tbn = (variant == 6 || variant == 8) ? 256 : (variant == 10 ? 128 : 192);
+  if (variant >= 21 && variant <= 24) {
+    // 21 / 22: six-slot ring, one workgroup per CU (plain / nt C stores); 23 / 24: three-slot rings, two
+    // workgroups per CU
+    if (N % 128 || K % 32) return ES_BAD_SHAPE;
+    const int tiles = ((M + 255) / 256) * (N / 128);
+    const int per_cu = variant >= 23 ? 2 : 1;
+    const int grid = std::min(256 * per_cu, (tiles + 7) / 8 * 8);
+#define RL(E, R, X, O)                                                                                    \
+    {                                                                                                   \
+      const size_t lds = (size_t)R * (256 * 64 + 128 * 64 + 128 * 4);                                     \
+      allow_lds(gemm_nt_ring_kernel<E, R, X, O>, lds);                                                    \
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_ring_kernel<E, R, X, O>), grid, 512, lds, stream, a);    \
+    }                                                                                                   \
+    break;
+#define RLE(R, X, O)                                 \
+    switch (epi) {                                   \
+      case EPI_BF16: RL(EPI_BF16, R, X, O)           \
+      case EPI_GELU: RL(EPI_GELU, R, X, O)           \
+      case EPI_F32_RESID: RL(EPI_F32_RESID, R, X, O) \
+      case EPI_DGELU: RL(EPI_DGELU, R, X, O)         \
+      case EPI_F32: RL(EPI_F32, R, X, O)             \
+      case EPI_PATCH: RL(EPI_PATCH, R, X, O)         \
+      case EPI_GELU_ACT: RL(EPI_GELU_ACT, R, X, O)   \
+      case EPI_GELU_D: RL(EPI_GELU_D, R, X, O)       \
+      case EPI_MULAUX: RL(EPI_MULAUX, R, X, O)       \
+      default: return ES_BAD_ARG;                    \
+    }
+    if (variant == 21) { RLE(6, 0, 1) } else if (variant == 22) { RLE(6, 2, 1) }
+    else if (variant == 23) { RLE(3, 0, 2) } else { RLE(3, 2, 2) }
+#undef RLE
+#undef RL
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
+  if ((variant >= 6 && variant <= 10) || (variant >= 13 && variant <= 17)) {
+    const int tbn = (variant == 6 || variant == 8) ? 256 : ((variant == 10 || variant >= 13) ? 128 : 192);
     if (N % tbn) return ES_BAD_SHAPE;
     return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
   }
@@ -1167,7 +1413,7 @@ static bool tn_big_ok(int N1, int N2, int ld1, int ld2) {
 }
 static int tn_pick(int M, int N1, int N2, int ld1, int ld2, int v) {
   if (!(N1 % BM == 0 && N2 % BN == 0)) return 7;  // only the big tile covers N2 = 192 (caller checked)
-  if (v >= 5 && v <= 9) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
+  if (v >= 5 && v <= 13) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
   if (v >= 0) return v;
   return (tn_big_ok(N1, N2, ld1, ld2) && M >= 65536) ? 7 : 0;
 }
@@ -1202,11 +1448,11 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
   if (M <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!tn_big_ok(N1, N2, ld1, ld2) && ((N1 % BM) || (N2 % BN))) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
-  if (variant > 9) return ES_BAD_ARG;
+  if (variant > 13) return ES_BAD_ARG;
   // variant: 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3;
   // 5..7 = 384x192 tile with 32x2 (72 KiB: two workgroups per CU), 32x3, 64x2
   const int v = tn_pick(M, N1, N2, ld1, ld2, variant >= 0 ? variant : g_tn_variant);
-  const int BKM = (v == 3 || v == 4 || v == 7 || v == 9) ? 64 : 32;  // (8: 384x192, 32x4)
+  const int BKM = (v == 3 || v == 4 || v == 7 || v == 9 || v == 10 || v == 11) ? 64 : 32;  // (8: 384x192, 32x4)
   const int msteps = (M + BKM - 1) / BKM;
   if (splits <= 0) splits = tn_auto_splits(v, M, N1, N2);
   splits = std::min(splits, msteps);
@@ -1223,11 +1469,11 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
     allow_lds(gemm_tn_kernel<BKM_, NST_>, lds);                                                       \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_kernel<BKM_, NST_>), dim3(grid), dim3(256), lds, stream, a); \
   }
-#define TNB_LAUNCH(BKM_, NST_, ASM_)                                                                    \
+#define TNB_LAUNCH(BKM_, NST_, ASM_, ...)                                                               \
   {                                                                                                   \
     const size_t lds = (size_t)NST_ * BKM_ * (TB1 + TB2) * 2;                                         \
-    allow_lds(gemm_tn_big_kernel<BKM_, NST_, ASM_>, lds);                                             \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_kernel<BKM_, NST_, ASM_>), dim3(grid), dim3(512), lds, stream, a); \
+    allow_lds(gemm_tn_big_kernel<BKM_, NST_, ASM_, ##__VA_ARGS__>, lds);                              \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_kernel<BKM_, NST_, ASM_, ##__VA_ARGS__>), dim3(grid), dim3(512), lds, stream, a); \
   }
   switch (v) {
     case 0: TN_LAUNCH(32, 2) break;
@@ -1240,6 +1486,10 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
     case 7: TNB_LAUNCH(64, 2, true) break;
     case 8: TNB_LAUNCH(32, 4, true) break;
     case 9: TNB_LAUNCH(64, 2, false) break;  // A/B: the builtin transposed reads (compiler-drained prefetch)
+    case 10: TNB_LAUNCH(64, 2, true, 1) break;  // probes: operand stream alone / MFMAs alone
+    case 11: TNB_LAUNCH(64, 2, true, 2) break;
+    case 12: TNB_LAUNCH(32, 4, true, 1) break;
+    case 13: TNB_LAUNCH(32, 4, true, 2) break;
     default: TN_LAUNCH(32, 2) break;
   }
 #undef TN_LAUNCH

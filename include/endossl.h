@@ -43,7 +43,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
 /* tuning knob: NT kernel family (-1 = per-shape default, 0..5 = fixed tilings, see gemm.hip); returns the old one */
 int es_set_gemm_variant(int variant);
-/* 1: the 64 x 128 NT tile for small token shards (M < 32768) in the per-shape rules; 0 (default): without. */
+/* 1 (default): the 64 x 128 NT tile rules (N <= 384 outputs of small token shards, M < 32768, and the residual
+ * proj forward); 0: without them.  Returns the old value. */
 int es_set_gemm_small_tile(int v);
 /* weight gradient: out[N1,N2] (+)= sum_m A1[m,N1]^T A2[m,N2], token axis split `splits` ways into
  * fp32 slabs (workspace = es_gemm_tn_workspace floats) and reduced; bias_out (nullable) (+)=

@@ -20,7 +20,8 @@ D, HD = 384, 1536
 # (name, epi, M, N, K)  -- NT: C[M,N] = A[M,K] B[N,K]^T
 NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 7, M_T, HD, D),
       ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 8, M_T, HD, D),
-      ("fc1_dgrad", 4, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 4, M_T, D, 3 * D)]
+      ("fc1_dgrad", 4, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 4, M_T, D, 3 * D),
+      ("qkv_fwd_weak", 0, M_W, 3 * D, D), ("proj_fwd_weak", 2, M_W, D, D), ("fc2_fwd_weak", 2, M_W, D, HD)]
 # (name, M, N1, N2)  -- TN: out[N1,N2] = sum_m A1[m,N1] A2[m,N2]
 TN = [("fc2_wgrad", M_T, D, HD), ("fc1_wgrad", M_T, HD, D), ("proj_wgrad", M_T, D, D), ("qkv_wgrad", M_T, 3 * D, D)]
 
@@ -80,7 +81,7 @@ def main():
         times = {v: [] for v in variants}
         for _ in range(args.rounds):
             for v in variants:
-                if N % {6: 256, 7: 192, 8: 256, 9: 192, 10: 128}.get(v, 128):
+                if N % {6: 256, 7: 192, 8: 256, 9: 192, 10: 128, 28: 256}.get(v, 128):
                     continue
                 lib.es_set_gemm_variant(v)
                 auxp = aux if epi in (2,) else (aux.bfloat16() if epi in (3, 8) else None)

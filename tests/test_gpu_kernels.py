@@ -40,8 +40,8 @@ def _lib_loaded():
 
 
 # ------------------------------------------------------------------------------------- GEMM NT
-GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12]
-_TILE_N = {6: 256, 7: 192, 8: 256, 9: 192, 10: 128}  # big-tile variants: N must be a multiple of the tile width
+GEMM_VARIANTS = [-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 21, 22, 23, 24, 25, 26, 27, 28]
+_TILE_N = {6: 256, 7: 192, 8: 256, 9: 192, 10: 128, 28: 256}  # big-tile variants: N must be a multiple of the tile width
 
 
 @pytest.fixture(params=GEMM_VARIANTS, ids=["auto"] + [f"v{v}" for v in GEMM_VARIANTS[1:]])
@@ -57,9 +57,11 @@ def _skip_untileable(variant, N):
 
 
 @pytest.mark.parametrize("M,N,K", [(300, 256, 192), (1000, 384, 384), (128, 128, 64), (5000, 1152, 1536),
-                                   (600, 768, 320)])
+                                   (600, 768, 320), (40000, 1152, 384), (33000, 384, 1536)])
 def test_gemm_nt_exact_integers(M, N, K, gemm_variant):
     _skip_untileable(gemm_variant, N)
+    if M > 10000 and gemm_variant not in (-1, 10, 21, 22, 23, 24, 25):
+        pytest.skip("multi-tile-per-workgroup shapes: the persistent kernels and the defaults")
     g = torch.Generator().manual_seed(M + N + K)
     A = _pad_rows(_int_bf16(M, K, gen=g))
     B = _int_bf16(N, K, gen=g)
@@ -74,11 +76,13 @@ def test_gemm_nt_exact_integers(M, N, K, gemm_variant):
     torch.testing.assert_close(Cb.float(), ref.bfloat16().float(), rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("N", [512, 384])
-def test_gemm_nt_epilogues_vs_fp32(N, gemm_variant):
+@pytest.mark.parametrize("N,M", [(512, 777), (384, 777), (384, 70000), (1536, 30000)])
+def test_gemm_nt_epilogues_vs_fp32(N, M, gemm_variant):
     _skip_untileable(gemm_variant, N)
+    if M > 10000 and gemm_variant not in (-1, 10, 21, 22, 23, 24, 25):
+        pytest.skip("multi-tile-per-workgroup shapes: the persistent kernels and the defaults")
     torch.manual_seed(0)
-    M, K = 777, 384
+    K = 384
     A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
     B = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
     bias = torch.randn(N, device=DEV) * 0.1
