@@ -186,15 +186,15 @@ def pmc_traffic(kernel_substr):
     (profiles/pmc_traffic.json: FETCH_SIZE x2 (gfx950 half-count correction) + WRITE_SIZE, KiB->B)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
-        return None
+        return None, None
     try:
         d = json.load(open(p))
         for k, v in d.get("kernels", {}).items():
             if kernel_substr in k:
-                return v.get("hbm_bytes_per_launch")
+                return v.get("hbm_bytes_per_launch"), f"committed profiles/pmc_traffic.json entry '{k}'"
     except (OSError, ValueError):
-        return None
-    return None
+        return None, None
+    return None, None
 
 
 def conformer_step_tflop(cfg, n_images):
@@ -606,7 +606,7 @@ def main():
     tflops = sum(f for _, _, f in probe["events"]) / (sum(ev_ms) / 1e3) / 1e12
     M_tok = B * (1 + MU) * 197
     share = (Engine.TN_SHARE if (ov[0] and not grouped and Engine.TN_SHARE < 1.0 and M_tok >= 16384) else 1.0)
-    traffic = None if grouped else pmc_traffic("gemm_tn")
+    traffic, traffic_src = (None, None) if grouped else pmc_traffic("gemm_tn")
     lib = __import__("endossl._lib", fromlist=["load"]).load()
     tn_ws = lib.es_gemm_tn_workspace(1536, 384, 0)
 
@@ -645,6 +645,8 @@ def main():
                                     "gemm_tn_grouped_kernel"),
                          "bound": "mfma", "achieved": round(tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1),
                          "unit": "TFLOP/s", "frac": round(tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                         "traffic_source": (traffic_src + " (a separate rocprofv3 --pmc pass over this bench, "
+                                            "not measured in this run)") if traffic_src else None,
                          "algorithmic_flop": flop, "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms),
                          "timed": "live in the timed steps" if live else "2 untimed eager steps after the timed "
                                                                          "(graph-replayed) steps",
