@@ -600,13 +600,17 @@ def main():
     iso_tflops = (sum(f for _, _, f in iso["events"]) / (sum(e0.elapsed_time(e1) for e0, e1, _ in iso["events"]) / 1e3)
                   / 1e12)
     grouped = probe.get("kernel")  # the small-shard backward: the weight gradients as grouped launches
+    layer = probe.get("layer_kernel")  # a block's weight gradients as one split-K launch (Engine.LAYER_WGRAD)
     ev_ms = [e0.elapsed_time(e1) for e0, e1, _ in probe["events"]]
     mean_ms = sum(ev_ms) / len(ev_ms)
     flop = sum(f for _, _, f in probe["events"]) / len(ev_ms)  # per launch (uniform at the fc1 site)
     tflops = sum(f for _, _, f in probe["events"]) / (sum(ev_ms) / 1e3) / 1e12
     M_tok = B * (1 + MU) * 197
-    share = (Engine.TN_SHARE if (ov[0] and not grouped and Engine.TN_SHARE < 1.0 and M_tok >= 16384) else 1.0)
-    traffic, traffic_src = (None, None) if grouped else pmc_traffic("gemm_tn")
+    if layer:
+        share = Engine.LAYER_TN_SHARE if ov[0] else 1.0
+    else:
+        share = (Engine.TN_SHARE if (ov[0] and not grouped and Engine.TN_SHARE < 1.0 and M_tok >= 16384) else 1.0)
+    traffic, traffic_src = (None, None) if grouped else pmc_traffic("es_gemm_tn_big_grouped" if layer else "gemm_tn")
     lib = __import__("endossl._lib", fromlist=["load"]).load()
     tn_ws = lib.es_gemm_tn_workspace(1536, 384, 0)
 
@@ -635,7 +639,9 @@ def main():
                                                            if Engine.PRUNE_LAST and Engine.LANES != 2 else 0.0))
                                          * glob_unl / 448.0, 3),
             "final_loss": round(loss, 6),
-            "roofline": {"kernel": (f"es_gemm_tn (weight gradient, fc1 site: out[1536, 384] = dY^T X over M={M_tok} "
+            "roofline": {"kernel": (layer + " (bf16 operands, fp32 split-K slabs; rocprofv3: "
+                                    "gemm_tn_big_grouped_kernel + splitk_reduce_grouped_kernel)" if layer else
+                                    f"es_gemm_tn (weight gradient, fc1 site: out[1536, 384] = dY^T X over M={M_tok} "
                                     "train tokens, bf16 operands, fp32 split-K slabs + reduction, fused bias "
                                     "gradient); rocprofv3: gemm_tn_big_kernel + splitk_reduce_kernel"
                                     if not grouped else
@@ -648,6 +654,7 @@ def main():
                          "traffic_source": (traffic_src + " (a separate rocprofv3 --pmc pass over this bench, "
                                             "not measured in this run)") if traffic_src else None,
                          "algorithmic_flop": flop, "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms),
+                         "algorithmic_bytes": probe.get("layer_bytes"),
                          "timed": "live in the timed steps" if live else "2 untimed eager steps after the timed "
                                                                          "(graph-replayed) steps",
                          "streams": 2 if ov[0] else 1, "tn_workspace_floats": int(tn_ws),

@@ -917,8 +917,7 @@ __device__ __forceinline__ int swz384(int r, int c) { return c ^ ((((r >> 1) & 1
 // PROBE (measurement variants only, es_gemm_tn_ex 10..13): 1 = the operand stream alone (no transposed
 // reads, no MFMAs), 2 = the MFMAs alone on whatever the ring holds (no DMA); 0 = the kernel.
 template <int BKM, int NST, bool ASM = true, int PROBE = 0>
-__global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+__device__ __forceinline__ void tn_big_body(const TNArgs& p, int split, int tile, char* smem) {
   constexpr int R1B = TB1 * 2, R2B = TB2 * 2;          // LDS row bytes: 768, 384
   constexpr int C1 = R1B / 16, C2 = R2B / 16;           // 16-B chunks per row: 48, 24
   constexpr int T1B = BKM * R1B, T2B = BKM * R2B;
@@ -928,9 +927,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
   constexpr int H2 = ((T2B / 1024) % 8) ? 1 : 0;        // plus one half piece (lanes 0..31)
   static_assert((T1B / 1024) % 8 == 0 && ((T2B / 1024) % 8 == 0 || (T2B / 1024) % 8 == 4), "pieces");
   constexpr int PER = F1 + F2 + H2;
-  const int nt2 = p.N2 / TB2, ntiles = (p.N1 / TB1) * nt2;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = wg / ntiles, tile = wg - split * ntiles;
+  const int nt2 = p.N2 / TB2;
   const int n1_0 = (tile / nt2) * TB1, n2_0 = (tile % nt2) * TB2;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int w1 = w >> 1, w2 = w & 1;
@@ -1052,6 +1049,65 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) p.PB[(size_t)split * p.N1 + n1_0 + w1 * 96 + (w2 * 3 + i) * 16 + t] = bacc[i][0];
   }
+}
+
+template <int BKM, int NST, bool ASM = true, int PROBE = 0>
+__global__ __launch_bounds__(512, 1) void gemm_tn_big_kernel(TNArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int ntiles = (p.N1 / TB1) * (p.N2 / TB2);
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = wg / ntiles;
+  tn_big_body<BKM, NST, ASM, PROBE>(p, split, wg - split * ntiles, smem);
+}
+
+// ---- a Linear layer's weight gradients as ONE split-K launch on the 384 x 192 tile ----------------
+// Entry e owns the workgroups [wg0_e, wg0_e + splits_e * ntiles_e), split-major (the tiles of one token
+// range are consecutive, so xcd_remap puts them on one XCD and they share that range's dY / X rows in its
+// L2).  Every tile of every entry is the same 384 x 192 output over the same number of tokens per split,
+// so the workgroups carry equal work; the few splits per problem that a whole layer's tiles (fc1 8 + fc2 8
+// + qkv 6 + proj 2 = 24 at ViT-S) need to fill the granted CUs keep the fp32 slabs small (S x the layer's
+// outputs, vs ~16-32 slabs per GEMM when each GEMM alone fills them).
+struct TNBigEntry {
+  TNArgs a;
+  int wg0, ntiles, pad0, pad1;
+};
+__global__ __launch_bounds__(512, 1) void gemm_tn_big_grouped_kernel(const TNBigEntry* __restrict__ grp, int ng) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  int e = 0;
+  while (e + 1 < ng && grp[e + 1].wg0 <= wg) ++e;
+  const TNArgs a = grp[e].a;
+  const int local = wg - grp[e].wg0, nt = grp[e].ntiles;
+  const int split = local / nt;
+  tn_big_body<64, 2, true, 0>(a, split, local - split * nt, smem);
+}
+
+// out[i] = sum_s P[s][i] for every entry of a table (the grouped launch's weight slabs and bias
+// partials): block b belongs to the entry with the largest blk0 <= b and sums 1,024 of its floats with
+// splitk_reduce_kernel's chains and order (4 interleaved chains over s, (s0 + s1) + (s2 + s3)).
+struct TNRedEntry {
+  const float* P;
+  float* out;
+  int S, n, blk0, pad;
+};
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const TNRedEntry* __restrict__ red, int nr) {
+  int e = 0;
+  while (e + 1 < nr && red[e + 1].blk0 <= (int)blockIdx.x) ++e;
+  const float* P = red[e].P;
+  const int S = red[e].S, n = red[e].n;
+  const int i = ((int)blockIdx.x - red[e].blk0) * 256 + (int)threadIdx.x;
+  if (i >= (n >> 2)) return;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0, s2 = s0, s3 = s0;
+  int k = 0;
+#pragma unroll 4
+  for (; k + 4 <= S; k += 4) {
+    s0 += ((const f32x4*)(P + (size_t)k * n))[i];
+    s1 += ((const f32x4*)(P + (size_t)(k + 1) * n))[i];
+    s2 += ((const f32x4*)(P + (size_t)(k + 2) * n))[i];
+    s3 += ((const f32x4*)(P + (size_t)(k + 3) * n))[i];
+  }
+  for (; k < S; ++k) s0 += ((const f32x4*)(P + (size_t)k * n))[i];
+  ((f32x4*)red[e].out)[i] = (s0 + s1) + (s2 + s3);
 }
 
 // out[i] = (accumulate ? out[i] : 0) + sum_s P[s][i]   (n % 4 == 0); 4 independent partial sums
@@ -1535,6 +1591,98 @@ int es_gemm_tn_grouped(const void* device_table, int count, int total_tiles, hip
   allow_lds(gemm_tn_grouped_kernel<32, 2>, lds);
   hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_grouped_kernel<32, 2>), dim3(total_tiles), dim3(256), lds, stream,
                      (const TNGroupEntry*)device_table, count);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// ---- a layer's weight gradients as one split-K launch on the 384 x 192 tile (include/endossl.h) ----
+static_assert(sizeof(TNBigEntry) == 72 && sizeof(TNRedEntry) == 32, "grouped big-tile table layout");
+// 64-token steps per split when a problem of M tokens gets (at most) S0 splits
+static int tn_group_per(int M, int S0) {
+  const int msteps = (M + 63) / 64, s = std::min(S0, msteps);
+  return (msteps + s - 1) / s;
+}
+size_t es_gemm_tn_big_grouped_table_bytes(int count) {
+  return count <= 0 ? 0 : (size_t)count * (sizeof(TNBigEntry) + 2 * sizeof(TNRedEntry));
+}
+size_t es_gemm_tn_big_grouped_workspace(const void* problems, int count, int target_wgs) {
+  if (!problems || count <= 0) return 0;
+  const TNGroupEntry* q = (const TNGroupEntry*)problems;
+  int tiles = 0;
+  for (int i = 0; i < count; ++i) tiles += (q[i].a.N1 / TB1) * (q[i].a.N2 / TB2);
+  const int S0 = std::max(1, target_wgs / std::max(1, tiles));
+  size_t f = 0;
+  for (int i = 0; i < count; ++i) {
+    const int per = tn_group_per(q[i].a.M, S0), S = ((q[i].a.M + 63) / 64 + per - 1) / per;
+    f += (size_t)S * ((size_t)q[i].a.N1 * q[i].a.N2 + (q[i].a.PB ? q[i].a.N1 : 0));
+  }
+  return f;
+}
+
+// Build the device table of es_gemm_tn_big_grouped from `count` es_tn_problem entries (dy, x, out,
+// bias_out, M, N1, N2, ld1, ld2; the other fields ignored): splits = target_wgs / (the problems' 384 x 192
+// tiles) for every problem (at most one per 64 tokens), slabs and bias partials carved from `workspace`
+// in problem order.  Writes TNBigEntry[count] then TNRedEntry[nred] to `table` (es_gemm_tn_big_grouped_
+// table_bytes(count) bytes) and {workgroups, reduce blocks, reduce entries} to dims[0..2].
+int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_wgs, float* workspace,
+                                   size_t workspace_floats, void* table, int* dims) {
+  if (!problems || count <= 0 || !workspace || !table || !dims || target_wgs <= 0) return ES_BAD_ARG;
+  const TNGroupEntry* q = (const TNGroupEntry*)problems;
+  int tiles = 0;
+  for (int i = 0; i < count; ++i) {
+    const TNArgs& a = q[i].a;
+    if (!a.A1 || !a.A2 || !a.P) return ES_BAD_ARG;
+    if (a.M <= 0 || !tn_big_ok(a.N1, a.N2, a.ld1, a.ld2)) return ES_BAD_SHAPE;
+    tiles += (a.N1 / TB1) * (a.N2 / TB2);
+  }
+  const int S0 = std::max(1, target_wgs / tiles);
+  TNBigEntry* g = (TNBigEntry*)table;
+  TNRedEntry* r = (TNRedEntry*)(g + count);
+  size_t off = 0;
+  int wg = 0, blk = 0, nr = 0;
+  for (int i = 0; i < count; ++i) {
+    const TNArgs& a = q[i].a;
+    const int msteps = (a.M + 63) / 64;
+    const int per = tn_group_per(a.M, S0);
+    const int S = (msteps + per - 1) / per;
+    const size_t nslab = (size_t)a.N1 * a.N2;
+    const size_t need = (size_t)S * nslab + (q[i].a.PB ? (size_t)S * a.N1 : 0);
+    if (off + need > workspace_floats) return ES_BAD_SHAPE;
+    float* P = workspace + off;
+    float* PB = q[i].a.PB ? P + (size_t)S * nslab : nullptr;
+    off += need;
+    const int nt = (a.N1 / TB1) * (a.N2 / TB2);
+    g[i].a = TNArgs{a.A1, a.A2, P, PB, a.M, a.N1, a.N2, a.ld1, a.ld2, per * 64};
+    g[i].wg0 = wg;
+    g[i].ntiles = nt;
+    g[i].pad0 = S;
+    g[i].pad1 = 0;
+    wg += S * nt;
+    r[nr] = TNRedEntry{P, (float*)a.P, S, (int)nslab, blk, 0};
+    blk += (int)((nslab / 4 + 255) / 256);
+    ++nr;
+    if (PB) {
+      r[nr] = TNRedEntry{PB, q[i].a.PB, S, a.N1, blk, 0};
+      blk += (a.N1 / 4 + 255) / 256;
+      ++nr;
+    }
+  }
+  dims[0] = wg;
+  dims[1] = blk;
+  dims[2] = nr;
+  return ES_OK;
+}
+
+// out_g = dY_g^T X_g and bias_g = column sums of dY_g (both overwritten) for every problem of a device
+// copy of the table es_gemm_tn_big_grouped_prepare wrote: the split-K GEMM launch, then one reduce
+// launch over every problem's slabs and bias partials.
+int es_gemm_tn_big_grouped(const void* device_table, int count, const int* dims, hipStream_t stream) {
+  if (!device_table || count <= 0 || !dims || dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0) return ES_BAD_ARG;
+  const size_t lds = (size_t)2 * 64 * (TB1 + TB2) * 2;
+  allow_lds(gemm_tn_big_grouped_kernel, lds);
+  const TNBigEntry* g = (const TNBigEntry*)device_table;
+  hipLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), lds, stream, g, count);
+  hipLaunchKernelGGL(splitk_reduce_grouped_kernel, dim3(dims[1]), dim3(256), 0, stream,
+                     (const TNRedEntry*)(g + count), dims[2]);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -32,6 +32,10 @@ SIGNATURES = {
     "es_tn_problem_size": (Z, []),
     "es_gemm_tn_grouped_prepare": (I, [V, I]),
     "es_gemm_tn_grouped": (I, [V, I, I, V]),
+    "es_gemm_tn_big_grouped_table_bytes": (Z, [I]),
+    "es_gemm_tn_big_grouped_workspace": (Z, [V, I, I]),
+    "es_gemm_tn_big_grouped_prepare": (I, [V, I, I, V, Z, V, V]),
+    "es_gemm_tn_big_grouped": (I, [V, I, V, V]),
     "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
     "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
     "es_attn_bwd": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),

@@ -253,6 +253,15 @@ class Engine:
     GROUP_WGRAD = os.environ.get("ENDOSSL_GROUP_WGRAD", "auto")
     GROUP_WGRAD_MAX_M = 16384
     GROUP_LAYERS = int(os.environ.get("ENDOSSL_GROUP_LAYERS", "6"))  # layers per grouped launch
+    # A block's long-axis weight gradients (fc2, fc1, proj, qkv: 8 + 8 + 2 + 6 = 24 tiles of 384 x 192 at
+    # ViT-S) as ONE split-K launch on the side stream once the block's data-gradient chain has produced
+    # its last dY (es_gemm_tn_big_grouped), plus one reduce launch over the block's slabs and bias
+    # partials -- instead of four GEMM launches (16-32 splits each at the F1 batch), four slab
+    # reductions and four bias reductions.  A grid sized to the granted CUs needs only a few splits per
+    # GEMM when the block's 24 tiles share it: the fc1 site's fp32 slab traffic drops from 75.5 MB
+    # (16 splits) to 23.6 MB (5 splits) per step layer.  ENDOSSL_LAYER_WGRAD=0: the per-GEMM launches.
+    LAYER_WGRAD = os.environ.get("ENDOSSL_LAYER_WGRAD", "1") == "1"
+    LAYER_TN_SHARE = float(os.environ.get("ENDOSSL_LAYER_TN_SHARE", os.environ.get("ENDOSSL_TN_SHARE", "0.5")))
     _OV = os.environ.get("ENDOSSL_OVERLAP", "1")
     OVERLAP_FWD = _OV in ("1", "fwd")
     OVERLAP = _OV in ("1", "bwd")
@@ -662,12 +671,18 @@ class Engine:
             GS = self._grads[key]
         ovw = ov and not grouped
         problems = []
+        layer_wg = self.LAYER_WGRAD and not grouped and self.precision == "bf16" and M >= self.TN_SHARE_MIN_M
+        lp = []  # this block's long-axis weight gradients (layer_wg): one grouped launch at the block's end
 
         def wgrad_side(dy, N1, x, N2, Mw, out, bias_out=None, ld1=None, ld2=None, label=None):
             """Weight-gradient GEMM on the side stream once the main stream has produced dY (or, grouped,
-            recorded for the one launch after the chain)."""
+            recorded for the one launch after the chain / at the end of the block)."""
             if grouped:
                 problems.append((dy, N1, x, N2, Mw, out, bias_out, ld1 or N1, ld2 or N2))
+                return
+            if (layer_wg and Mw >= self.TN_SHARE_MIN_M and N1 % 384 == 0 and N2 % 192 == 0
+                    and (ld1 or N1) % 8 == 0 and (ld2 or N2) % 8 == 0):
+                lp.append((dy, N1, x, N2, Mw, out, bias_out, ld1 or N1, ld2 or N2, label))
                 return
             if not ov:
                 self._wgrad(dy, N1, x, N2, Mw, out, bias_out, ld1=ld1, ld2=ld2, label=label)
@@ -677,6 +692,19 @@ class Engine:
                 self._wgrad(dy, N1, x, N2, Mw, out, bias_out, ld1=ld1, ld2=ld2, label=label)
 
         done = {}
+
+        def flush_layer(i):
+            """Block i's recorded weight gradients as one grouped split-K launch on the side stream."""
+            if not lp:
+                return
+            probs = list(lp)
+            lp.clear()
+            if ov:
+                side.wait_stream(main)
+                with torch.cuda.stream(side):
+                    self._wgrad_layer(probs, i)
+            else:
+                self._wgrad_layer(probs, i)
 
         def block_done(i):
             if self.capture is not None:
@@ -759,6 +787,7 @@ class Engine:
                     wgrad_side(Gi.dqkv, D, A.h1[i], D, n, gw[:D * D], gb[:D], ld1=T * 3 * D, ld2=T * D)
                 else:
                     wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gw, gb)
+                flush_layer(i)
                 if ovw:
                     done[i] = side.record_event()
                 self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), Gi.dxm_cls, G.dx, Gn.dxb,
@@ -805,6 +834,7 @@ class Engine:
             if cap is not None:
                 cap("b_dqkv", True, i, Gi.dqkv[:M])
                 cap("b_dh1", True, i, G.dh[:M])
+            flush_layer(i)
             if ovw:
                 done[i] = side.record_event()
                 if i + 1 in done:  # set (i-1) % 2 was layer i+1's: its weight gradients must be done
@@ -818,11 +848,65 @@ class Engine:
              s)
         npat = n * cfg.np
         wgrad_side(G.dpatch, D, A.patches, K0, npat, gv("patch_embed.proj.weight"), gv("patch_embed.proj.bias"))
+        flush_layer(-1)  # the patch-embedding weight gradient (layer_wg): the backward's last launch
         if grouped:
             self._launch_grouped(problems, 0)
         if ov:
             main.wait_stream(side)
         return grad
+
+    def _wgrad_layer(self, problems, layer):
+        """One es_gemm_tn_big_grouped launch (+ its reduce) over a block's weight gradients, on the
+        current stream.  Sized to LAYER_TN_SHARE of the CUs while the data-gradient chain still runs
+        beside it; the first block's (the last launch of the backward: nothing left beside it) and the
+        serial engine's to the whole chip.  The device table (pointers into cached buffers) is re-made
+        only when its bytes change, so steady-state steps launch with no host->device copy."""
+        lib = _lib.load()
+        if self._ncu is None:
+            self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        share = self.LAYER_TN_SHARE if (self.overlap and layer > 0) else 1.0  # block 0 / the embedding: chip
+        target = max(1, int(self._ncu * share))
+        n = len(problems)
+        tab = (_TNProblem * n)()
+        for e, (dy, N1, x, N2, Mw, out, bias, ld1, ld2, _) in zip(tab, problems):
+            e.dy, e.x, e.out, e.bias_out = ptr(dy), ptr(x), ptr(out), ptr(bias) if bias is not None else None
+            e.M, e.N1, e.N2, e.ld1, e.ld2 = Mw, N1, N2, ld1, ld2
+        ws = self.workspace(0)
+        need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), n, target)
+        if need > ws.numel():
+            raise RuntimeError(f"grouped weight-gradient workspace too small: {need} > {ws.numel()} floats")
+        raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(n))
+        dims = (ctypes.c_int * 3)()
+        rc = lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), n, target, ptr(ws), ws.numel(), raw, dims)
+        if rc != 0:
+            raise _lib.EndosslLibraryError(f"es_gemm_tn_big_grouped_prepare: status {rc}")
+        raw = raw.raw
+        if not hasattr(self, "_ltab"):
+            self._ltab = {}
+        cache = self._ltab.get(layer)
+        if cache is None or cache[0] != raw:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("layer weight-gradient table changed during hipGraph capture; run one eager "
+                                   "step of this shape first")
+            dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device, non_blocking=False)
+            self._ltab[layer] = cache = (raw, dev, dims)
+        pr = self.probe
+        # probed at the launches sized like the timed ones: the CU-share-sized blocks (or every block of the
+        # serial engine), not the first block's whole-chip launch at the end of an overlapped backward
+        if pr is not None and any(q[9] == pr["label"] for q in problems) and (layer > 0 or not self.overlap):
+            flop = sum(2.0 * q[4] * q[1] * q[3] for q in problems)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            call("es_gemm_tn_big_grouped", ptr(cache[1]), n, cache[2], _lib.stream())
+            e1.record()
+            pr["events"].append((e0, e1, flop))
+            pr["layer_kernel"] = (f"es_gemm_tn_big_grouped: one block's {n} weight-gradient GEMMs "
+                                  f"({'+'.join(str(q[1]) + 'x' + str(q[3]) for q in problems)}) over M={problems[0][4]} "
+                                  f"tokens, {cache[2][0]} workgroups of 384x192, then one reduce launch")
+            pr["layer_bytes"] = sum(2.0 * q[4] * (q[1] + q[3]) + 4.0 * q[1] * q[3] + (4.0 * q[1] if q[6] is not None else 0)
+                                    for q in problems)
+        else:
+            call("es_gemm_tn_big_grouped", ptr(cache[1]), n, cache[2], _lib.stream())
 
     def _grouped_wgrad(self, M, grad_ready):
         if self.precision != "bf16" or grad_ready is not None:  # per-block hand-over needs per-layer launches

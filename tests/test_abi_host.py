@@ -211,3 +211,38 @@ def test_build_model_routes_conformer():
     assert type(m).__name__ == "NativeConformer"
     assert m.cfg.dim == 384 and m.cfg.depth == 12 and m.cfg.heads == 6 and m.cfg.T == 197
     assert m.get_parameter("conv_cls_head.weight").shape == (23, 256)
+
+
+def test_tn_big_grouped_prepare_layout():
+    """es_gemm_tn_big_grouped_prepare is host code (no GPU): a ViT-S block's four weight gradients at the
+    F1 token count get the same split count (target / 24 tiles), split-major workgroup ranges, slabs and
+    bias partials carved from the workspace in problem order, and one reduce entry per slab set and per
+    bias; a workspace one float short is refused."""
+    import ctypes
+    import struct
+
+    from endossl import _lib
+    from endossl.vit import _TNProblem
+    lib = _lib.load()
+    D, Hd, M = 384, 1536, 100864
+    shapes = [(D, Hd), (Hd, D), (D, D), (3 * D, D)]
+    tab = (_TNProblem * 4)()
+    for k, (e, (N1, N2)) in enumerate(zip(tab, shapes)):
+        e.dy, e.x, e.out, e.bias_out = 0x1000 * (k + 1), 0x100000 * (k + 1), 0x2000000 * (k + 1), 0x30000000 * (k + 1)
+        e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, N1, N2
+    need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), 4, 128)
+    assert need == 5 * sum(N1 * N2 + N1 for N1, N2 in shapes)
+    raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(4))
+    dims = (ctypes.c_int * 3)()
+    base = 0x7000000000
+    assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), 4, 128, ctypes.c_void_p(base), need, raw, dims) == 0
+    assert list(dims)[0] == 5 * 24 and list(dims)[2] == 8
+    off, wg = 0, 0
+    for i, (N1, N2) in enumerate(shapes):
+        a1, a2, P, PB, m, n1, n2, l1, l2, mchunk, wg0, nt, S, _ = struct.unpack_from("4Q6i4i", raw.raw, i * 72)
+        assert (a1, a2, m, n1, n2) == (tab[i].dy, tab[i].x, M, N1, N2) and S == 5 and mchunk == 316 * 64
+        assert P == base + 4 * off and PB == P + 4 * S * N1 * N2 and wg0 == wg and nt == (N1 // 384) * (N2 // 192)
+        off += S * (N1 * N2 + N1)
+        wg += S * nt
+    assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), 4, 128, ctypes.c_void_p(base), need - 1, raw,
+                                              dims) != 0

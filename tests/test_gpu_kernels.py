@@ -201,6 +201,86 @@ def test_gemm_tn_grouped_exact_integers():
     assert lib.es_gemm_tn_grouped_prepare(ctypes.byref(bad), 1) == -1  # N1 % 128
 
 
+def _big_grouped(problems, target):
+    """es_gemm_tn_big_grouped over [(A1, A2, out, bias, M, N1, N2, ld1, ld2)] -> dims."""
+    import ctypes
+    from endossl.vit import _TNProblem
+    lib = _lib.load()
+    tab = (_TNProblem * len(problems))()
+    for e, (A1, A2, out, bias, M, N1, N2, ld1, ld2) in zip(tab, problems):
+        e.dy, e.x, e.out, e.bias_out = ptr(A1), ptr(A2), ptr(out), ptr(bias) if bias is not None else None
+        e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, ld1, ld2
+    need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), len(problems), target)
+    ws = torch.empty(need, device=DEV)
+    raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(len(problems)))
+    dims = (ctypes.c_int * 3)()
+    assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need, raw, dims) == 0
+    assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need - 1, raw,
+                                              dims) != 0  # workspace bound enforced
+    assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need, raw, dims) == 0
+    dtab = torch.frombuffer(bytearray(raw.raw), dtype=torch.uint8).to(DEV)
+    call("es_gemm_tn_big_grouped", ptr(dtab), len(problems), dims, S())
+    torch.cuda.synchronize()
+    return list(dims), ws, dtab
+
+
+def test_gemm_tn_big_grouped_exact_integers():
+    """es_gemm_tn_big_grouped: a ViT-S block's four weight gradients (fc2 384x1536, fc1 1536x384, proj
+    384x384, qkv 1152x384 -- the last with a row stride wider than N1, as the engine's K/V slice of dqkv)
+    plus a problem with a ragged token count, in one split-K launch on the 384x192 tile and one reduce
+    launch: exact on integer data (every partial sum is an integer below 2^24), outputs and biases
+    overwritten, at a few split counts (target workgroups)."""
+    g = torch.Generator().manual_seed(12)
+    shapes = [(6016, 384, 1536, None), (6016, 1536, 384, None), (6016, 384, 384, None), (6016, 768, 384, 1152),
+              (1000, 384, 192, None)]
+    for target in (24, 120, 256):
+        probs, refs = [], []
+        for M, N1, N2, ld1 in shapes:
+            ld1 = ld1 or N1
+            A1 = _pad_rows(_int_bf16(M, ld1, lo=-2, hi=3, gen=g))
+            A2 = _pad_rows(_int_bf16(M, N2, lo=-2, hi=3, gen=g))
+            out = torch.full((N1, N2), 3.0, device=DEV)
+            bias = torch.full((N1,), 5.0, device=DEV) if N2 != 192 else None
+            probs.append((A1, A2, out, bias, M, N1, N2, ld1, N2))
+            refs.append((out, bias, A1[:M, :N1].float().t() @ A2[:M].float(), A1[:M, :N1].float().sum(0)))
+        dims, _, _ = _big_grouped(probs, target)
+        assert dims[0] >= 23 and dims[2] == 2 * len(shapes) - 1
+        for out, bias, ref, bref in refs:
+            torch.testing.assert_close(out, ref, rtol=0, atol=0)
+            if bias is not None:
+                torch.testing.assert_close(bias, bref, rtol=0, atol=0)
+
+
+def test_gemm_tn_big_grouped_matches_per_gemm_launch():
+    """Random bf16 data at an F1-like token count: the grouped launch's weight gradients are
+    bit-identical to es_gemm_tn_ex on the same 384x192 tile (variant 7) with the same split count
+    (same per-split token ranges, same kernel body, same slab-reduction order); the bias gradients
+    (reduced in another order by the per-GEMM path) within fp32 rounding, and both within 1e-5 of an
+    fp32 torch reference."""
+    torch.manual_seed(13)
+    M = 25216
+    shapes = [(384, 1536), (1536, 384), (384, 384), (1152, 384)]
+    probs, singles = [], []
+    for N1, N2 in shapes:
+        A1 = _pad_rows(torch.randn(M, N1, device=DEV).bfloat16())
+        A2 = _pad_rows(torch.randn(M, N2, device=DEV).bfloat16())
+        probs.append((A1, A2, torch.empty(N1, N2, device=DEV), torch.empty(N1, device=DEV), M, N1, N2, N1, N2))
+    tiles = sum((N1 // 384) * (N2 // 192) for N1, N2 in shapes)
+    target = 5 * tiles
+    _big_grouped(probs, target)
+    lib = _lib.load()
+    ws = torch.empty(lib.es_gemm_tn_workspace(1536, 1536, 8), device=DEV)
+    for A1, A2, out, bias, M_, N1, N2, ld1, ld2 in probs:
+        o1, b1 = torch.empty(N1, N2, device=DEV), torch.empty(N1, device=DEV)
+        call("es_gemm_tn_ex", ptr(A1), N1, ptr(A2), N2, M_, N1, N2, 5, ptr(ws), ptr(o1), 0, ptr(b1), 7, S())
+        torch.cuda.synchronize()
+        assert torch.equal(out, o1)
+        torch.testing.assert_close(bias, b1, rtol=1e-6, atol=1e-4)
+        ref = A1[:M_].float().t() @ A2[:M_].float()
+        assert ((out - ref).norm() / ref.norm()).item() < 1e-5
+        torch.testing.assert_close(bias, A1[:M_].float().sum(0), rtol=1e-5, atol=1e-2)
+
+
 def test_colsum():
     torch.manual_seed(2)
     M, N = 5000, 1152
