@@ -1071,13 +1071,20 @@ struct TNBigEntry {
   TNArgs a;
   int wg0, ntiles, pad0, pad1;
 };
-__global__ __launch_bounds__(512, 1) void gemm_tn_big_grouped_kernel(const TNBigEntry* __restrict__ grp, int ng) {
+// The table travels in the kernel arguments (no device copy to make or keep in sync: the tensors'
+// pointers may change every step, and a hipGraph capture records the arguments by value).
+constexpr int TNG_MAX = 8;
+struct TNBigTable {
+  TNBigEntry e[TNG_MAX];
+  int ng, pad;
+};
+__global__ __launch_bounds__(512, 1) void gemm_tn_big_grouped_kernel(const TNBigTable t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
   int e = 0;
-  while (e + 1 < ng && grp[e + 1].wg0 <= wg) ++e;
-  const TNArgs a = grp[e].a;
-  const int local = wg - grp[e].wg0, nt = grp[e].ntiles;
+  while (e + 1 < t.ng && t.e[e + 1].wg0 <= wg) ++e;
+  const TNArgs a = t.e[e].a;
+  const int local = wg - t.e[e].wg0, nt = t.e[e].ntiles;
   const int split = local / nt;
   tn_big_body<64, 2, true, 0>(a, split, local - split * nt, smem);
 }
@@ -1090,7 +1097,13 @@ struct TNRedEntry {
   float* out;
   int S, n, blk0, pad;
 };
-__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const TNRedEntry* __restrict__ red, int nr) {
+struct TNRedTable {
+  TNRedEntry r[2 * TNG_MAX];
+  int nr, pad;
+};
+__global__ __launch_bounds__(256) void splitk_reduce_grouped_kernel(const TNRedTable t) {
+  const TNRedEntry* red = t.r;
+  const int nr = t.nr;
   int e = 0;
   while (e + 1 < nr && red[e + 1].blk0 <= (int)blockIdx.x) ++e;
   const float* P = red[e].P;
@@ -1613,7 +1626,7 @@ size_t es_gemm_tn_big_grouped_workspace(const void* problems, int count, int tar
   size_t f = 0;
   for (int i = 0; i < count; ++i) {
     const int per = tn_group_per(q[i].a.M, S0), S = ((q[i].a.M + 63) / 64 + per - 1) / per;
-    f += (size_t)S * ((size_t)q[i].a.N1 * q[i].a.N2 + (q[i].a.PB ? q[i].a.N1 : 0));
+    if (S > 1) f += (size_t)S * ((size_t)q[i].a.N1 * q[i].a.N2 + (q[i].a.PB ? q[i].a.N1 : 0));
   }
   return f;
 }
@@ -1626,6 +1639,7 @@ size_t es_gemm_tn_big_grouped_workspace(const void* problems, int count, int tar
 int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_wgs, float* workspace,
                                    size_t workspace_floats, void* table, int* dims) {
   if (!problems || count <= 0 || !workspace || !table || !dims || target_wgs <= 0) return ES_BAD_ARG;
+  if (count > TNG_MAX) return ES_BAD_SHAPE;
   const TNGroupEntry* q = (const TNGroupEntry*)problems;
   int tiles = 0;
   for (int i = 0; i < count; ++i) {
@@ -1645,10 +1659,11 @@ int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_w
     const int per = tn_group_per(a.M, S0);
     const int S = (msteps + per - 1) / per;
     const size_t nslab = (size_t)a.N1 * a.N2;
-    const size_t need = (size_t)S * nslab + (q[i].a.PB ? (size_t)S * a.N1 : 0);
+    const size_t need = S == 1 ? 0 : (size_t)S * nslab + (q[i].a.PB ? (size_t)S * a.N1 : 0);
     if (off + need > workspace_floats) return ES_BAD_SHAPE;
-    float* P = workspace + off;
-    float* PB = q[i].a.PB ? P + (size_t)S * nslab : nullptr;
+    // one split: the tile writes the weight and bias gradients in place (no slab, no reduce entry)
+    float* P = S == 1 ? (float*)a.P : workspace + off;
+    float* PB = q[i].a.PB ? (S == 1 ? q[i].a.PB : P + (size_t)S * nslab) : nullptr;
     off += need;
     const int nt = (a.N1 / TB1) * (a.N2 / TB2);
     g[i].a = TNArgs{a.A1, a.A2, P, PB, a.M, a.N1, a.N2, a.ld1, a.ld2, per * 64};
@@ -1657,6 +1672,7 @@ int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_w
     g[i].pad0 = S;
     g[i].pad1 = 0;
     wg += S * nt;
+    if (S == 1) continue;
     r[nr] = TNRedEntry{P, (float*)a.P, S, (int)nslab, blk, 0};
     blk += (int)((nslab / 4 + 255) / 256);
     ++nr;
@@ -1672,17 +1688,26 @@ int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_w
   return ES_OK;
 }
 
-// out_g = dY_g^T X_g and bias_g = column sums of dY_g (both overwritten) for every problem of a device
-// copy of the table es_gemm_tn_big_grouped_prepare wrote: the split-K GEMM launch, then one reduce
-// launch over every problem's slabs and bias partials.
-int es_gemm_tn_big_grouped(const void* device_table, int count, const int* dims, hipStream_t stream) {
-  if (!device_table || count <= 0 || !dims || dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0) return ES_BAD_ARG;
+// out_g = dY_g^T X_g and bias_g = column sums of dY_g (both overwritten) for every problem of the
+// (host) table es_gemm_tn_big_grouped_prepare wrote: the split-K GEMM launch, then one reduce launch
+// over every problem's slabs and bias partials.  The table is passed by value in the kernel arguments.
+int es_gemm_tn_big_grouped(const void* table, int count, const int* dims, hipStream_t stream) {
+  if (!table || count <= 0 || !dims || dims[0] <= 0 || dims[1] < 0 || dims[2] < 0) return ES_BAD_ARG;
+  if (count > TNG_MAX || dims[2] > 2 * TNG_MAX) return ES_BAD_SHAPE;
   const size_t lds = (size_t)2 * 64 * (TB1 + TB2) * 2;
   allow_lds(gemm_tn_big_grouped_kernel, lds);
-  const TNBigEntry* g = (const TNBigEntry*)device_table;
-  hipLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), lds, stream, g, count);
-  hipLaunchKernelGGL(splitk_reduce_grouped_kernel, dim3(dims[1]), dim3(256), 0, stream,
-                     (const TNRedEntry*)(g + count), dims[2]);
+  const TNBigEntry* g = (const TNBigEntry*)table;
+  TNBigTable bt{};
+  for (int i = 0; i < count; ++i) bt.e[i] = g[i];
+  bt.ng = count;
+  hipLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), lds, stream, bt);
+  if (dims[2] > 0) {
+    TNRedTable rt{};
+    const TNRedEntry* r = (const TNRedEntry*)(g + count);
+    for (int i = 0; i < dims[2]; ++i) rt.r[i] = r[i];
+    rt.nr = dims[2];
+    hipLaunchKernelGGL(splitk_reduce_grouped_kernel, dim3(dims[1]), dim3(256), 0, stream, rt);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -259,6 +259,37 @@ class _Map:
 CONF_TN_SHARE = float(os.environ.get("ENDOSSL_CONF_TN_SHARE", "0.5"))
 
 
+# A transformer block's four weight gradients (fc2, fc1, proj, qkv: 96 tiles of 384 x 192 at
+# Conformer-B) as ONE launch on the weight-gradient stream at the end of the block's backward
+# (es_gemm_tn_big_grouped, as the ViT engine's Engine.LAYER_WGRAD) instead of four split-K launches with
+# their slab and bias reductions; at the CU share's 128 workgroups every GEMM gets one split, written in
+# place.  Measured at S1 (same box): 152.8 ms (CU share 0.5) / 152.5 (0.75) vs 151.9 ms with the per-GEMM
+# launches -- S1's weight gradients are off its critical path beside the two branch streams, so this stays
+# opt-in (ENDOSSL_CONF_LAYER_WGRAD=1).
+LAYER_WGRAD = os.environ.get("ENDOSSL_CONF_LAYER_WGRAD", "0") == "1"
+
+
+def _tn_block(lib, problems, M, gv, dev):
+    """One es_gemm_tn_big_grouped launch (+ reduce, when a GEMM gets more than one split) on the current
+    stream over [(dy, N1, x, N2, weight name, bias name)], sized to CONF_TN_SHARE of the CUs."""
+    from .vit import _TNProblem
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    target = max(1, int(ncu * CONF_TN_SHARE))
+    n = len(problems)
+    tab = (_TNProblem * n)()
+    for e, (dy, N1, x, N2, wname, bname) in zip(tab, problems):
+        e.dy, e.x, e.out, e.bias_out = ptr(dy), ptr(x), ptr(gv(wname)), ptr(gv(bname))
+        e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, N1, N2
+    need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), n, target)
+    ws = torch.empty(max(1, need), device=dev)
+    raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(n))
+    dims = (ctypes.c_int * 3)()
+    rc = lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), n, target, ptr(ws), ws.numel(), raw, dims)
+    if rc != 0:
+        raise _lib.EndosslLibraryError(f"es_gemm_tn_big_grouped_prepare: status {rc}")
+    call("es_gemm_tn_big_grouped", raw, n, dims, _s())
+
+
 def _tn_splits(M, N1, N2):
     """0: es_gemm_tn sizes the split-K for the kernel it picks (as the ViT engine, Engine._tn_splits)."""
     return 0
@@ -765,7 +796,12 @@ class _BlockFn(torch.autograd.Function):
         wt, pv, gv = m.wt, m.pview, m.gview
         ws_ln = torch.empty(2 * 1024 * D, device=dev)
 
+        lp = []  # LAYER_WGRAD: this block's weight gradients, one grouped launch at the end
+
         def wgrad(dy, N1, x, N2, wname, bname):
+            if LAYER_WGRAD and side is not None and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
+                lp.append((dy, N1, x, N2, wname, bname))
+                return
             sp = _tn_splits(M, N1, N2)
             if side is not None and CONF_TN_SHARE < 1.0 and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
                 # beside the branch streams: the 384 x 192 tile on a share of the CUs (as Engine.TN_SHARE)
@@ -806,6 +842,10 @@ class _BlockFn(torch.autograd.Function):
         call("es_layernorm_bwd_b16", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
+        if lp:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                _tn_block(lib, lp, M, gv, dev)
         if side is not None:
             for t in (act, h2, o, h1):  # saved activations the side stream still reads
                 t.record_stream(side)

@@ -260,8 +260,11 @@ class Engine:
     # reductions and four bias reductions.  A grid sized to the granted CUs needs only a few splits per
     # GEMM when the block's 24 tiles share it: the fc1 site's fp32 slab traffic drops from 75.5 MB
     # (16 splits) to 23.6 MB (5 splits) per step layer.  ENDOSSL_LAYER_WGRAD=0: the per-GEMM launches.
+    # Sized to 3/8 of the CUs (96 workgroups = 4 splits of the 24 tiles): same-box F1 sweep, two rounds each,
+    # ms/step at share 0.25 / 0.3125 / 0.375 / 0.4375 / 0.5 = 36.8 / 31.5 / 31.0 / 31.0 / 31.5 (2 / 3 / 4 /
+    # 4 / 5 splits) vs 31.53 with the per-GEMM launches; C1 66.8 vs 67.2, the N = 2 shard 16.53 vs 16.99.
     LAYER_WGRAD = os.environ.get("ENDOSSL_LAYER_WGRAD", "1") == "1"
-    LAYER_TN_SHARE = float(os.environ.get("ENDOSSL_LAYER_TN_SHARE", os.environ.get("ENDOSSL_TN_SHARE", "0.5")))
+    LAYER_TN_SHARE = float(os.environ.get("ENDOSSL_LAYER_TN_SHARE", "0.375"))
     _OV = os.environ.get("ENDOSSL_OVERLAP", "1")
     OVERLAP_FWD = _OV in ("1", "fwd")
     OVERLAP = _OV in ("1", "bwd")
@@ -859,8 +862,8 @@ class Engine:
         """One es_gemm_tn_big_grouped launch (+ its reduce) over a block's weight gradients, on the
         current stream.  Sized to LAYER_TN_SHARE of the CUs while the data-gradient chain still runs
         beside it; the first block's (the last launch of the backward: nothing left beside it) and the
-        serial engine's to the whole chip.  The device table (pointers into cached buffers) is re-made
-        only when its bytes change, so steady-state steps launch with no host->device copy."""
+        serial engine's to the whole chip.  The problem table travels in the kernel arguments (no
+        host->device copy; capturable)."""
         lib = _lib.load()
         if self._ncu is None:
             self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
@@ -880,16 +883,6 @@ class Engine:
         rc = lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), n, target, ptr(ws), ws.numel(), raw, dims)
         if rc != 0:
             raise _lib.EndosslLibraryError(f"es_gemm_tn_big_grouped_prepare: status {rc}")
-        raw = raw.raw
-        if not hasattr(self, "_ltab"):
-            self._ltab = {}
-        cache = self._ltab.get(layer)
-        if cache is None or cache[0] != raw:
-            if torch.cuda.is_current_stream_capturing():
-                raise RuntimeError("layer weight-gradient table changed during hipGraph capture; run one eager "
-                                   "step of this shape first")
-            dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device, non_blocking=False)
-            self._ltab[layer] = cache = (raw, dev, dims)
         pr = self.probe
         # probed at the launches sized like the timed ones: the CU-share-sized blocks (or every block of the
         # serial engine), not the first block's whole-chip launch at the end of an overlapped backward
@@ -897,16 +890,16 @@ class Engine:
             flop = sum(2.0 * q[4] * q[1] * q[3] for q in problems)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            call("es_gemm_tn_big_grouped", ptr(cache[1]), n, cache[2], _lib.stream())
+            call("es_gemm_tn_big_grouped", raw, n, dims, _lib.stream())
             e1.record()
             pr["events"].append((e0, e1, flop))
             pr["layer_kernel"] = (f"es_gemm_tn_big_grouped: one block's {n} weight-gradient GEMMs "
                                   f"({'+'.join(str(q[1]) + 'x' + str(q[3]) for q in problems)}) over M={problems[0][4]} "
-                                  f"tokens, {cache[2][0]} workgroups of 384x192, then one reduce launch")
+                                  f"tokens, {dims[0]} workgroups of 384x192, then one reduce launch")
             pr["layer_bytes"] = sum(2.0 * q[4] * (q[1] + q[3]) + 4.0 * q[1] * q[3] + (4.0 * q[1] if q[6] is not None else 0)
                                     for q in problems)
         else:
-            call("es_gemm_tn_big_grouped", ptr(cache[1]), n, cache[2], _lib.stream())
+            call("es_gemm_tn_big_grouped", raw, n, dims, _lib.stream())
 
     def _grouped_wgrad(self, M, grad_ready):
         if self.precision != "bf16" or grad_ready is not None:  # per-block hand-over needs per-layer launches

@@ -87,16 +87,16 @@ int es_gemm_tn_grouped(const void* device_table, int count, int total_tiles, hip
  * M, N1, N2, ld1, ld2; mchunk / tile0 / pad ignored), N1 % 384 == 0, N2 % 192 == 0, rows
  * [M, round_up(M, 64)) of dy zero; out / bias_out overwritten.  Every problem gets
  * max(1, target_wgs / its-and-the-others' 384x192 tiles) splits (at most one per 64 tokens), so the
- * slabs are S x the layer's outputs with S a few, not 16-32 per GEMM.  _prepare writes the device table
- * (es_gemm_tn_big_grouped_table_bytes(count) bytes, host memory: the caller copies it to the device) and
- * dims[3] = {workgroups, reduce blocks, reduce entries}; workspace >= es_gemm_tn_big_grouped_workspace
- * floats.  Replaces the per-Linear es_gemm_tn launches of code/models/conformer.py:13-23,35-50's
+ * slabs are S x the layer's outputs with S a few, not 16-32 per GEMM (one split: written in place).
+ * count <= 8.  _prepare writes the table (es_gemm_tn_big_grouped_table_bytes(count) bytes of HOST memory;
+ * es_gemm_tn_big_grouped passes it by value in the kernel arguments) and dims[3] = {workgroups, reduce
+ * blocks, reduce entries}; workspace >= es_gemm_tn_big_grouped_workspace floats.  Replaces the per-Linear es_gemm_tn launches of code/models/conformer.py:13-23,35-50's
  * backward (autograd's addmm weight gradients). */
 size_t es_gemm_tn_big_grouped_table_bytes(int count);
 size_t es_gemm_tn_big_grouped_workspace(const void* problems, int count, int target_wgs);
 int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_wgs, float* workspace,
                                    size_t workspace_floats, void* table, int* dims);
-int es_gemm_tn_big_grouped(const void* device_table, int count, const int* dims, hipStream_t stream);
+int es_gemm_tn_big_grouped(const void* table, int count, const int* dims, hipStream_t stream);
 /* bias gradient: out[n] (+)= sum_m Y[m][n]  (workspace >= blocks*N floats) */
 int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
               hipStream_t stream);

@@ -211,17 +211,17 @@ def _big_grouped(problems, target):
         e.dy, e.x, e.out, e.bias_out = ptr(A1), ptr(A2), ptr(out), ptr(bias) if bias is not None else None
         e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, ld1, ld2
     need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), len(problems), target)
-    ws = torch.empty(need, device=DEV)
+    ws = torch.empty(max(need, 1), device=DEV)
     raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(len(problems)))
     dims = (ctypes.c_int * 3)()
     assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need, raw, dims) == 0
-    assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need - 1, raw,
-                                              dims) != 0  # workspace bound enforced
+    if need > 0:  # workspace bound enforced (one split per problem: written in place, no workspace)
+        assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need - 1, raw,
+                                                  dims) != 0
     assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need, raw, dims) == 0
-    dtab = torch.frombuffer(bytearray(raw.raw), dtype=torch.uint8).to(DEV)
-    call("es_gemm_tn_big_grouped", ptr(dtab), len(problems), dims, S())
+    call("es_gemm_tn_big_grouped", raw, len(problems), dims, S())
     torch.cuda.synchronize()
-    return list(dims), ws, dtab
+    return list(dims), ws, raw
 
 
 def test_gemm_tn_big_grouped_exact_integers():
@@ -244,7 +244,7 @@ def test_gemm_tn_big_grouped_exact_integers():
             probs.append((A1, A2, out, bias, M, N1, N2, ld1, N2))
             refs.append((out, bias, A1[:M, :N1].float().t() @ A2[:M].float(), A1[:M, :N1].float().sum(0)))
         dims, _, _ = _big_grouped(probs, target)
-        assert dims[0] >= 23 and dims[2] == 2 * len(shapes) - 1
+        assert dims[0] >= 23 and dims[2] == (0 if target == 24 else 2 * len(shapes) - 1)
         for out, bias, ref, bref in refs:
             torch.testing.assert_close(out, ref, rtol=0, atol=0)
             if bias is not None:
