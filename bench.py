@@ -174,11 +174,20 @@ def cpu_baseline(B=8, MU=7, steps=2):
                 break
     except OSError:
         pass
+    mem = "unknown"
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemTotal"):
+                mem = f"{int(line.split()[1]) / 2**20:.0f} GiB"
+                break
+    except (OSError, ValueError, IndexError):
+        pass
     return {"value": round(B * MU / dt, 3), "unit": "unlabeled images/s", "cores": used,
             "kind": "port",
-            "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step), "
+            "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step; the "
+                      f"F1 batch B=64 would hold ~100 GB of fp32 autograd activations and ~10x the CPU time), "
                       f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', host CPUs {cpu_info}, "
-                      f"torch.get_num_threads()={used}"}
+                      f"host RAM {mem} (the job may use at most ~270 GiB of it), torch.get_num_threads()={used}"}
 
 
 def pmc_traffic(kernel_substr):
@@ -459,6 +468,10 @@ def main():
                          "the reference's transforms on the granted host threads from decoded 500x375 RGB "
                          "frames, pinned uint8 batches copied on a side stream); reported as 'host_input', "
                          "never as value")
+    ap.add_argument("--allreduce", choices=("auto", "single", "overlap"), default="auto",
+                    help="N > 1: the gradient all-reduce as one launch after the backward (single), per-block "
+                         "buckets overlapped with it (overlap), or auto = whichever ran faster in 3 untimed "
+                         "steps each before the timed region (max over ranks)")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="hipGraph replay of the step's forward/backward (on); auto = off = eager launches "
                          "(measured faster than the replay at N = 1 and at the N = 8 shard, DESIGN.md §5)")
@@ -511,6 +524,29 @@ def main():
 
     for _ in range(args.warmup):
         tr.step(batch)
+    ar_probe = None
+    if world > 1 and args.allreduce == "auto":
+        # untimed: the gradient all-reduce as one launch after the backward vs per-block buckets overlapped
+        # with it (FixMatch.overlap_allreduce), 3 steps each after 2 settling steps, max over ranks (so every
+        # rank picks the same form); the timed steps run the faster one, the other is reported beside it
+        ar_probe = {}
+        for form in (False, True):
+            tr.overlap_allreduce = form
+            for _ in range(2):
+                tr.step(batch)
+            torch.cuda.synchronize()
+            dist.barrier()
+            p0 = time.perf_counter()
+            for _ in range(3):
+                tr.step(batch)
+            torch.cuda.synchronize()
+            dist.barrier()
+            pe = torch.tensor([(time.perf_counter() - p0) / 3], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(pe, op=torch.distributed.ReduceOp.MAX)
+            ar_probe["overlapped" if form else "single"] = round(pe.item() * 1e3, 3)
+        tr.overlap_allreduce = ar_probe["overlapped"] < ar_probe["single"]
+    elif world > 1:
+        tr.overlap_allreduce = args.allreduce == "overlap"
     if graph and tr.static_batch() is not None:
         batch = tr.static_batch()  # the graph's own input buffers already hold this batch: no copy per step
     eng = model.engine()
@@ -674,6 +710,10 @@ def main():
         if ar_overlap is not None:
             res["allreduce_form"] = "overlapped per-block buckets" if tr.overlap_allreduce else "one after the backward"
             res["allreduce_other_form"] = ar_overlap
+            if ar_probe is not None:
+                res["allreduce_choice"] = {"probe_ms_per_step": ar_probe,
+                                           "note": "--allreduce auto: both forms timed for 3 untimed steps before the "
+                                                   "timed region (max over ranks); the faster one is the headline"}
         if host_input is not None:
             res["host_input"] = host_input
         if world == 1 and not args.no_cpu_baseline:
