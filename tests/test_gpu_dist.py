@@ -27,7 +27,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, layer=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     sys.path.insert(0, os.path.join(ROOT, "endoscopy-image-classification_amd"))
@@ -35,10 +35,15 @@ def _worker(rank, world, port, q):
     from endossl.vit import NativeViT, ViTConfig
     dist.init_from_env(backend="gloo")
     try:
-        cfg = ViTConfig(img_size=64, dim=128, depth=3, heads=2, num_classes=23)
+        if layer:  # ViT-S widths: every block's weight gradients as one grouped split-K launch (LAYER_WGRAD)
+            cfg = ViTConfig(img_size=64, dim=384, depth=3, heads=6, num_classes=23)
+        else:
+            cfg = ViTConfig(img_size=64, dim=128, depth=3, heads=2, num_classes=23)
         m = NativeViT(cfg, seed=3).to("cuda")
         eng = m.engine()
         eng.GROUP_WGRAD = "0"  # the same split-K weight-gradient launches in both reverse passes
+        if layer:
+            eng.LAYER_WGRAD, eng.TN_SHARE_MIN_M = True, 512  # 64 images x 17 tokens = 1,088 rows
         eng.pack(m.flat, m.version)
         g = torch.Generator(device="cuda").manual_seed(10 + rank)
         x = torch.randn(64, 3, 64, 64, device="cuda", generator=g)
@@ -72,11 +77,12 @@ def _worker(rank, world, port, q):
         torch.distributed.destroy_process_group()
 
 
-def test_two_rank_overlapped_allreduce_bit_identical():
+@pytest.mark.parametrize("layer", [False, True], ids=["per_gemm", "block_grouped"])
+def test_two_rank_overlapped_allreduce_bit_identical(layer):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, layer)) for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=100) for _ in procs]
