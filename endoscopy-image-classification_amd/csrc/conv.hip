@@ -1081,6 +1081,234 @@ __global__ void tokens_cls_set_kernel(float* __restrict__ xt, int N, int T, int 
 
 // row groups of the per-channel reductions: ~64 rows each, at most 1024 (4 workgroups per CU)
 inline int chan_groups(int rows) { return rows < 64 * 1024 ? (rows + 63) / 64 : 1024; }
+// ---- the 3-channel 7x7 / stride-2 / pad-3 stem (Conformer.conv1 code/models/conformer.py:313-315,
+// timm resnet18's conv1) on NHWC fp32 images, 64 output channels: specialised forward and weight
+// gradient.  The generic kernels above gather one 4-byte tap per thread per 16-deep K step for this
+// conv (Cin = 3 is not 4-aligned) and re-load the 37.6 KB weight per 64-pixel tile; here a tile is a
+// 64-pixel segment of one output row, its 7 input rows (133 pixels x 3 channels each, zero-padded) are
+// staged into LDS with coalesced row loads, and persistent workgroups keep W^T in LDS across tiles.
+// K' = (ky, kx, ci) with ci fastest = ky*21 + kx*3 + ci -- conv_fwd_kernel's K order -- padded to 148;
+// v_mfma_f32_16x16x4_f32 is a k-ordered fmaf chain, so the forward is bit-identical to
+// conv_fwd_kernel's.  A tap (ky, kx, ci) of output pixel p sits at float 6p + kx*3 + ci of staged row ky.
+constexpr int STEM_PX = 64;     // output pixels per tile
+constexpr int STEM_K = 148;     // 147 taps x channels + one zero row (the MFMA's K step is 4)
+constexpr int STEM_RF = 399;    // floats per staged input row: (2 * STEM_PX + 5) pixels x 3 channels
+constexpr int STEM_ROWF = 400;  // LDS row stride
+constexpr int STEM_LD = 80;     // LDS row stride of the [k'][co] / [pixel][co] images: 80 = 16 mod 32
+                                // puts lanes 16-31 (the next k / pixel) on the other half of the banks
+
+// the 7 input rows of output row `ho`, pixels [wo0, wo0 + 64): As[ky][3 * j + ci] =
+// x[n][2 ho - 3 + ky][2 wo0 - 3 + j][ci] (0 outside the image).  Loaded into registers (STEM_PRE per
+// thread) one tile ahead and stored into LDS after the previous tile's MFMAs, so the global latency
+// hides behind the matrix work.
+constexpr int STEM_PRE = (7 * STEM_RF + 255) / 256;  // 11
+__device__ __forceinline__ void stem_load_rows(float (&r)[STEM_PRE], const float* __restrict__ x, int n, int ho, int wo0,
+                                               int H, int W) {
+  const int wlo = 2 * wo0 - 3;
+#pragma unroll
+  for (int j = 0; j < STEM_PRE; ++j) {
+    const int i = threadIdx.x + 256 * j;
+    const int ky = i / STEM_RF, f = i - ky * STEM_RF;
+    const int hi = 2 * ho - 3 + ky, wi = wlo + f / 3;
+    r[j] = (i < 7 * STEM_RF && (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
+               ? x[(((long)n * H + hi) * W) * 3 + (long)wlo * 3 + f]
+               : 0.f;
+  }
+}
+__device__ __forceinline__ void stem_store_rows(float* As, const float (&r)[STEM_PRE]) {
+#pragma unroll
+  for (int j = 0; j < STEM_PRE; ++j) {
+    const int i = threadIdx.x + 256 * j;
+    if (i < 7 * STEM_RF) {
+      const int ky = i / STEM_RF;
+      As[ky * STEM_ROWF + (i - ky * STEM_RF)] = r[j];
+    }
+  }
+}
+struct StemTile {
+  int n, ho, wo0;
+  __device__ StemTile(int t, int Ho, int tpr) {
+    const int seg = t % tpr, row = t / tpr;
+    ho = row % Ho;
+    n = row / Ho;
+    wo0 = seg * STEM_PX;
+  }
+};
+
+__global__ __launch_bounds__(256, 2) void stem_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, float* __restrict__ y, int N,
+                                                          int H, int W, int Ho, int Wo, long syn, long syh, long syw,
+                                                          int accumulate) {
+  __shared__ float Bs[STEM_K * STEM_LD];  // W^T [k'][co]
+  __shared__ float As[7 * STEM_ROWF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int i = tid; i < STEM_K * 64; i += 256) {
+    const int kp = i >> 6, co = i & 63;
+    float v = 0.f;
+    if (kp < 147) {
+      const int ky = kp / 21, r = kp - ky * 21, kx = r / 3, ci = r - kx * 3;
+      v = w[co * 147 + ci * 49 + ky * 7 + kx];
+    }
+    Bs[kp * STEM_LD + co] = v;
+  }
+  const int tpr = (Wo + STEM_PX - 1) / STEM_PX, ntiles = N * Ho * tpr;
+  const int pr = lane & 15, kl = lane >> 4;
+  const int p = wv * 16 + pr;  // this lane's A row (output pixel in the tile)
+  float bv[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) bv[c] = bias ? bias[c * 16 + pr] : 0.f;
+  float pre[STEM_PRE];
+  if (blockIdx.x < ntiles) {
+    const StemTile t0(blockIdx.x, Ho, tpr);
+    stem_load_rows(pre, x, t0.n, t0.ho, t0.wo0, H, W);
+  }
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const StemTile tt(t, Ho, tpr);
+    const int ho = tt.ho, n = tt.n, wo0 = tt.wo0;
+    __syncthreads();  // the previous tile's reads of As (and, first time round, the W^T writes)
+    stem_store_rows(As, pre);
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) {  // the next tile's rows in flight during this tile's MFMAs
+      const StemTile tn(t + gridDim.x, Ho, tpr);
+      stem_load_rows(pre, x, tn.n, tn.ho, tn.wo0, H, W);
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int ks = 0; ks < STEM_K / 4; ++ks) {
+      const int kp = ks * 4 + kl;
+      const int ky = kp / 21, r = kp - ky * 21;
+      const float a = kp < 147 ? As[ky * STEM_ROWF + 6 * p + r] : 0.f;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, Bs[kp * STEM_LD + c * 16 + pr], acc[c], 0, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int wo = wo0 + wv * 16 + 4 * kl + q;
+      if (wo >= Wo) continue;
+      float* yr = y + n * syn + ho * syh + wo * syw;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float v = acc[c][q] + bv[c];
+        yr[c * 16 + pr] = accumulate ? yr[c * 16 + pr] + v : v;
+      }
+    }
+  }
+}
+
+// weight gradient partials P[block][co][k'] = sum over the block's tiles' pixels of dy[pix][co] x
+// im2col[pix][k']: A = dy^T (rows co, k = pixel) from an LDS image of the tile's 64 dy rows, B = the
+// staged input rows (cols k', k = pixel); wave w owns co rows [16w, 16w + 16) x all 148 k' (10 tiles).
+__global__ __launch_bounds__(256, 2) void stem_dw_kernel(const float* __restrict__ x, const float* __restrict__ dy,
+                                                         float* __restrict__ P, int N, int H, int W, int Ho, int Wo,
+                                                         long syn, long syh, long syw) {
+  __shared__ float Ds[STEM_PX * STEM_LD];  // dy [pixel][co]
+  __shared__ float As[7 * STEM_ROWF];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int pr = lane & 15, kl = lane >> 4;
+  int off[10];
+  bool ok[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const int kp = j * 16 + pr, ky = kp / 21, r = kp - ky * 21;
+    ok[j] = kp < 147;
+    off[j] = ok[j] ? ky * STEM_ROWF + r : 0;
+  }
+  f32x4 acc[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int tpr = (Wo + STEM_PX - 1) / STEM_PX, ntiles = N * Ho * tpr;
+  float pre[STEM_PRE];
+  f32x4 dpre[4];  // 64 pixels x 64 channels of dy = 1,024 float4s, 4 per thread
+  auto load_dy = [&](const StemTile& tt) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + 256 * j, px = i >> 4, c4 = (i & 15) * 4;
+      dpre[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (tt.wo0 + px < Wo) dpre[j] = *(const f32x4*)(dy + tt.n * syn + tt.ho * syh + (long)(tt.wo0 + px) * syw + c4);
+    }
+  };
+  if (blockIdx.x < ntiles) {
+    const StemTile t0(blockIdx.x, Ho, tpr);
+    stem_load_rows(pre, x, t0.n, t0.ho, t0.wo0, H, W);
+    load_dy(t0);
+  }
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    __syncthreads();
+    stem_store_rows(As, pre);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = tid + 256 * j;
+      *(f32x4*)(Ds + (i >> 4) * STEM_LD + (i & 15) * 4) = dpre[j];
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) {  // the next tile's operands in flight during this tile's MFMAs
+      const StemTile tn(t + gridDim.x, Ho, tpr);
+      stem_load_rows(pre, x, tn.n, tn.ho, tn.wo0, H, W);
+      load_dy(tn);
+    }
+#pragma unroll 2
+    for (int s = 0; s < STEM_PX / 4; ++s) {
+      const int px = 4 * s + kl;
+      const float a = Ds[px * STEM_LD + wv * 16 + pr];
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const float b = ok[j] ? As[off[j] + 6 * px] : 0.f;
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+      }
+    }
+  }
+  // acc[j][q]: co = 16 wv + 4 kl + q, k' = 16 j + pr
+  float* out = P + (long)blockIdx.x * 64 * 147;
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    if (!ok[j]) continue;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) out[(wv * 16 + 4 * kl + q) * 147 + j * 16 + pr] = acc[j][q];
+  }
+}
+
+// dw[co][ci][ky][kx] (+)= sum_b P[b][co][k'], k' = ky*21 + kx*3 + ci.  A block owns 64 outputs; its 4 waves
+// each sum a quarter of the slabs (4 chains), combined in a fixed order through LDS (deterministic).
+__global__ __launch_bounds__(256) void stem_dw_reduce_kernel(const float* __restrict__ P, float* __restrict__ dw, int S,
+                                                             int accumulate) {
+  __shared__ float part[4][64];
+  const int o = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + o;
+  const int b0 = (S * q) / 4, b1 = (S * (q + 1)) / 4;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (i < 64 * 147) {
+    int b = b0;
+    for (; b + 4 <= b1; b += 4) {
+      s0 += P[(long)b * 9408 + i];
+      s1 += P[(long)(b + 1) * 9408 + i];
+      s2 += P[(long)(b + 2) * 9408 + i];
+      s3 += P[(long)(b + 3) * 9408 + i];
+    }
+    for (; b < b1; ++b) s0 += P[(long)b * 9408 + i];
+  }
+  part[q][o] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q != 0 || i >= 64 * 147) return;
+  const float v = (part[0][o] + part[1][o]) + (part[2][o] + part[3][o]);
+  const int co = i / 147, kp = i - co * 147, ky = kp / 21, r = kp - ky * 21, kx = r / 3, ci = r - kx * 3;
+  float* d = dw + co * 147 + ci * 49 + ky * 7 + kx;
+  *d = accumulate ? *d + v : v;
+}
+
+// the stem kernels' preconditions: 3 -> 64 channels, 7x7 / 2 / 3, NHWC-contiguous fp32 images, channel-
+// contiguous output rows
+inline bool stem_ok(const ConvGeom& g) {
+  return g.Cin == 3 && g.Cout == 64 && g.kh == 7 && g.kw == 7 && g.stride == 2 && g.pad == 3 && g.sxc == 1 &&
+         g.sxw == 3 && g.sxh == 3L * g.W && g.sxn == 3L * g.W * g.H && g.syw >= 64 && g.syw % 4 == 0 &&
+         g.syh % 4 == 0 && g.syn % 4 == 0;
+}
+constexpr int STEM_GRID = 512;  // two 256-thread workgroups per CU (launch_bounds(256, 2))
+int g_stem_kernels = 1;  // es_set_stem_kernels: 0 = the generic kernels for the stem too (A/B, tests)
+inline bool stem_generic() { return g_stem_kernels == 0; }
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 inline int grid1d(long n) {
@@ -1436,6 +1664,14 @@ constexpr int MAPS_BF16 = 1, OUT_BF16 = 2;
 
 extern "C" {
 
+// 1 (default): the specialised stem kernels for 3 -> 64 channel 7x7 / 2 / 3 convs on NHWC images;
+// 0: the generic implicit-GEMM kernels (bit-identical forward).  Returns the previous value.
+int es_set_stem_kernels(int v) {
+  const int old = g_stem_kernels;
+  g_stem_kernels = v;
+  return old;
+}
+
 // y[n, ho, wo, co] (+)= conv(x)  (Conv2d, groups = 1).  x at element strides (sxn, sxh, sxw, sxc),
 // y at (syn, syh, syw) with channel stride 1.  Ho = (H + 2p - kh) / s + 1.
 int es_conv2d_fwd(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
@@ -1444,6 +1680,12 @@ int es_conv2d_fwd(const float* x, int N, int H, int W, int Cin, long sxn, long s
   if (!x || !w || !y) return ES_BAD_ARG;
   const ConvGeom g = make_geom(N, H, W, Cin, sxn, sxh, sxw, sxc, Cout, kh, kw, stride, pad, syn, syh, syw);
   if (!geom_ok(g)) return ES_BAD_SHAPE;
+  if (stem_ok(g) && al16(y) && !stem_generic()) {
+    const int tiles = N * g.Ho * ((g.Wo + STEM_PX - 1) / STEM_PX);
+    hipLaunchKernelGGL(stem_fwd_kernel, std::min(tiles, STEM_GRID), 256, 0, stream, x, w, bias, y, N, H, W, g.Ho, g.Wo,
+                       syn, syh, syw, accumulate);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   const bool v4 = Cin % 4 == 0 && sxc == 1 && sxw % 4 == 0 && sxh % 4 == 0 && sxn % 4 == 0 && al16(x);
   return v4 ? launch_conv_fwd<4>(x, w, bias, y, g, accumulate, stream)
             : launch_conv_fwd<1>(x, w, bias, y, g, accumulate, stream);
@@ -1481,6 +1723,13 @@ int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn,
   const ConvGeom g = make_geom(N, H, W, Cin, sxn, sxh, sxw, sxc, Cout, kh, kw, stride, pad, syn, syh, syw);
   if (!geom_ok(g) || splits <= 0) return ES_BAD_SHAPE;
   const int M = N * g.Ho * g.Wo, K = Cin * kh * kw;
+  if (stem_ok(g) && al16(dy) && !stem_generic()) {  // partial slabs: one per workgroup
+    const int tiles = N * g.Ho * ((g.Wo + STEM_PX - 1) / STEM_PX);
+    const int grid = std::min(std::min(tiles, STEM_GRID), splits);  // the caller sized `splits` slabs
+    hipLaunchKernelGGL(stem_dw_kernel, grid, 256, 0, stream, x, dy, workspace, N, H, W, g.Ho, g.Wo, syn, syh, syw);
+    hipLaunchKernelGGL(stem_dw_reduce_kernel, (64 * 147 + 63) / 64, 256, 0, stream, workspace, dw, grid, accumulate);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   int chunk = (M + splits - 1) / splits;
   chunk = (chunk + CBK - 1) / CBK * CBK;
   const int S = (M + chunk - 1) / chunk;

@@ -32,6 +32,7 @@ SIGNATURES = {
     "es_tn_problem_size": (Z, []),
     "es_gemm_tn_grouped_prepare": (I, [V, I]),
     "es_gemm_tn_grouped": (I, [V, I, I, V]),
+    "es_set_stem_kernels": (I, [I]),
     "es_gemm_tn_big_grouped_table_bytes": (Z, [I]),
     "es_gemm_tn_big_grouped_workspace": (Z, [V, I, I]),
     "es_gemm_tn_big_grouped_prepare": (I, [V, I, I, V, Z, V, V]),
@@ -196,7 +197,8 @@ def load(path=None):
     # ENDOSSL_ATTN_VARIANT
     for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"), ("ENDOSSL_SMALL_TILE", "es_set_gemm_small_tile"),
                     ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant"),
-                    ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant"), ("ENDOSSL_ATTN_BWD_LONG", "es_set_attn_bwd_long")):
+                    ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant"), ("ENDOSSL_ATTN_BWD_LONG", "es_set_attn_bwd_long"),
+                    ("ENDOSSL_STEM_KERNELS", "es_set_stem_kernels")):
         if os.environ.get(env):
             getattr(lib, fn)(int(os.environ[env]))
     if path is None:

@@ -282,6 +282,10 @@ int es_poly_ce_fwd_bwd(const float* logits, int ldl, const int64_t* targets, con
  * fp32 NHWC maps with element strides; Conv2d groups = 1, weights in the reference layout
  * [Cout][Cin][kh][kw].  Replaces the reference's aten conv2d / batch_norm / max_pool2d /
  * avg_pool2d / upsample_nearest2d calls in ConvBlock, FCUDown, FCUUp and the stem. */
+/* 1 (default): the 3 -> 64 channel 7x7 / stride-2 / pad-3 stem (Conformer.conv1, resnet18.conv1) on NHWC fp32
+ * images runs on its own forward (bit-identical to the generic kernel) and weight-gradient kernels inside
+ * es_conv2d_fwd / es_conv2d_bwd_weight; 0: the generic kernels.  Returns the previous value. */
+int es_set_stem_kernels(int v);
 int es_conv2d_fwd(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
                   const float* w, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y, long syn,
                   long syh, long syw, int accumulate, hipStream_t stream);

@@ -108,6 +108,47 @@ def test_conv2d_fwd_bwd(N, Cin, H, Cout, k, s, p):
     _close(dbd.cpu() - 3.0, br.grad)
 
 
+@pytest.mark.parametrize("N,H", [(2, 40), (1, 150), (2, 224)])
+def test_stem_conv_kernels(N, H):
+    """The specialised 3 -> 64 channel 7x7 / 2 / 3 stem kernels (es_set_stem_kernels(1), the default)
+    on NHWC fp32 images: forward bit-identical to the generic implicit-GEMM kernel (same (ky, kx, ci)
+    fmaf order), both passes within fp32 tolerance of fp64 torch, the weight gradient also at a
+    caller-sized slab count below the kernel's grid, with accumulate; partial 64-pixel row segments
+    (Wo = 20, 75, 112)."""
+    lib = _lib.load()
+    torch.manual_seed(N + H)
+    Cin, Cout, k, s, p = 3, 64, 7, 2, 3
+    x = torch.randn(N, Cin, H, H, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, k, k, dtype=torch.float64) * 0.2
+    b = torch.randn(Cout, dtype=torch.float64)
+    xr, wr = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    y = F.conv2d(xr, wr, b, stride=s, padding=p)
+    Ho = y.shape[2]
+    xd, wd, bd = _nhwc(x).float().to(DEV), w.float().to(DEV), b.float().to(DEV)
+    args = (ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(wd), ptr(bd), Cout, k, k, s, p)
+    outs = {}
+    for stem in (1, 0):
+        old = lib.es_set_stem_kernels(stem)
+        try:
+            yd = torch.empty(N, Ho, Ho, Cout, device=DEV)
+            call("es_conv2d_fwd", *args, ptr(yd), Ho * Ho * Cout, Ho * Cout, Cout, 0, S())
+            torch.cuda.synchronize()
+            outs[stem] = yd
+        finally:
+            lib.es_set_stem_kernels(old)
+    assert torch.equal(outs[1], outs[0])
+    _close(_nchw(outs[1].cpu()), y)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    dyd = _nhwc(dy).float().to(DEV)
+    for splits in (683, 7):
+        ws = torch.empty(lib.es_conv2d_bwd_weight_workspace(Cout, Cin, k, k, splits), device=DEV)
+        dwd = torch.full_like(wd, 0.5)
+        call("es_conv2d_bwd_weight", ptr(xd), N, H, H, Cin, H * H * Cin, H * Cin, Cin, 1, ptr(dyd), Ho * Ho * Cout,
+             Ho * Cout, Cout, Cout, k, k, s, p, splits, ptr(ws), ptr(dwd), 1, S())
+        _close(dwd.cpu() - 0.5, wr.grad)
+
+
 def _bf(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
