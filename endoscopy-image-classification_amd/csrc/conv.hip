@@ -952,6 +952,7 @@ __global__ void upsample_bwd_kernel(const float* __restrict__ dout, int N, int H
 // ---- FCUDown tokens: out[n][0] = 2 x_t[n][0]; out[n][1+p] = gelu(LN(pooled[n][p])) + x_t[n][1+p]
 // (the `x_st + x_t` of ConvTransBlock: x_st's cls row is x_t[:, 0] itself, code/models/conformer.py
 // :176-177,345).  One wave per row, D <= 1024; saves mean / rstd per row.
+template <int NJ>  // 64-column slots per lane: D <= 64 NJ; the row stays in registers (one read of pooled / x_t)
 __global__ __launch_bounds__(256) void fcu_down_fwd_kernel(const float* __restrict__ pooled, const float* __restrict__ xt,
                                                            const float* __restrict__ gam, const float* __restrict__ bet,
                                                            float* __restrict__ out, float* __restrict__ mean,
@@ -962,27 +963,49 @@ __global__ __launch_bounds__(256) void fcu_down_fwd_kernel(const float* __restri
   const int n = wv / T, tk = wv % T;
   const float* xr = xt + (long)wv * D;
   float* orow = out + (long)wv * D;
+  float xv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    xv[j] = c < D ? xr[c] : 0.f;
+  }
   if (tk == 0) {
-    for (int c = lane; c < D; c += 64) orow[c] = 2.f * xr[c];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (j * 64 + lane < D) orow[j * 64 + lane] = 2.f * xv[j];
     return;
   }
   const float* pr = pooled + ((long)n * np + tk - 1) * D;
+  float pv[NJ];
   float s = 0.f;
-  for (int c = lane; c < D; c += 64) s += pr[c];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    pv[j] = c < D ? pr[c] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    if (j * 64 + lane < D) s += pv[j];
   const float mu = warp_sum(s) / (float)D;
   float q = 0.f;
-  for (int c = lane; c < D; c += 64) {
-    const float d = pr[c] - mu;
-    q = fmaf(d, d, q);
-  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+    if (j * 64 + lane < D) {
+      const float d = pv[j] - mu;
+      q = fmaf(d, d, q);
+    }
   const float rs = 1.0f / sqrtf(warp_sum(q) / (float)D + eps);
   if (lane == 0) {
     mean[(long)n * np + tk - 1] = mu;
     rstd[(long)n * np + tk - 1] = rs;
   }
-  for (int c = lane; c < D; c += 64) {
-    const float z = (pr[c] - mu) * rs * gam[c] + bet[c];
-    orow[c] = 0.5f * z * (1.0f + erff(z * 0.70710678118654752f)) + xr[c];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = j * 64 + lane;
+    if (c < D) {
+      const float z = (pv[j] - mu) * rs * gam[c] + bet[c];
+      orow[c] = 0.5f * z * (1.0f + erff(z * 0.70710678118654752f)) + xv[j];
+    }
   }
 }
 
@@ -1011,16 +1034,31 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
     pgw[j] = pbw[j] = 0.f;
   }
   const int r0 = blockIdx.x * rows_per_block, r1 = min(r0 + rows_per_block, N * T);
-  for (int row = r0 + wv; row < r1; row += 4) {
+  // the next row's dout / pooled values are loaded while this row computes (registers nd / np_), so a
+  // wave's rows do not each wait a full memory latency
+  float nd[NJ], npv[NJ];
+  auto load_row = [&](int row) {
     const int n = row / T, tk = row - n * T;
     const float* dr = dout + (long)row * D;
-    float* xr = dxt + (long)row * D;
-    float d[NJ];
+    const float* pr = pooled + ((long)n * np + (tk > 0 ? tk - 1 : 0)) * D;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c = j * 64 + lane;
-      d[j] = c < D ? dr[c] : 0.f;
+      nd[j] = c < D ? dr[c] : 0.f;
+      npv[j] = (c < D && tk > 0) ? pr[c] : 0.f;
     }
+  };
+  if (r0 + wv < r1) load_row(r0 + wv);
+  for (int row = r0 + wv; row < r1; row += 4) {
+    const int n = row / T, tk = row - n * T;
+    float* xr = dxt + (long)row * D;
+    float d[NJ], pvv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      d[j] = nd[j];
+      pvv[j] = npv[j];
+    }
+    if (row + 4 < r1) load_row(row + 4);
     if (tk == 0) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
@@ -1028,7 +1066,6 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
       continue;
     }
     const long pi = (long)n * np + tk - 1;
-    const float* pr = pooled + pi * D;
     const float mu = mean[pi], rs = rstd[pi];
     float xh[NJ], gz[NJ];
     float s1 = 0.f, s2 = 0.f;
@@ -1037,7 +1074,7 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
       const int c = j * 64 + lane;
       if (c < D) {
         xr[c] = d[j];
-        xh[j] = (pr[c] - mu) * rs;
+        xh[j] = (pvv[j] - mu) * rs;
         const float z = xh[j] * ga[j] + be[j];
         const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
         gz[j] = d[j] * fmaf(z, 0.39894228040143268f * __expf(-0.5f * z * z), cdf);
@@ -2105,10 +2142,19 @@ int es_upsample_bwd(const float* dout, int N, int H, int W, int C, int s, float*
 int es_fcu_down_tokens_fwd(const float* pooled, const float* xt, const float* ln_w, const float* ln_b, float* out,
                            float* mean, float* rstd, int N, int np, int D, float eps, hipStream_t stream) {
   if (!pooled || !xt || !ln_w || !ln_b || !out || !mean || !rstd) return ES_BAD_ARG;
-  if (N <= 0 || np <= 0 || D <= 0 || D > 4096) return ES_BAD_SHAPE;
+  if (N <= 0 || np <= 0 || D <= 0 || D > 64 * FCU_NJ) return ES_BAD_SHAPE;
   const long waves = (long)N * (np + 1);
-  hipLaunchKernelGGL(fcu_down_fwd_kernel, (unsigned)((waves + 3) / 4), 256, 0, stream, pooled, xt, ln_w, ln_b, out,
-                     mean, rstd, N, np, D, eps);
+  const unsigned blocks = (unsigned)((waves + 3) / 4);
+  const int nj = (D + 63) / 64;
+#define FCU_FWD(NJ_) \
+  hipLaunchKernelGGL(fcu_down_fwd_kernel<NJ_>, blocks, 256, 0, stream, pooled, xt, ln_w, ln_b, out, mean, rstd, N, np, D, eps)
+  if (nj <= 2) FCU_FWD(2);
+  else if (nj <= 4) FCU_FWD(4);
+  else if (nj <= 6) FCU_FWD(6);
+  else if (nj <= 8) FCU_FWD(8);
+  else if (nj <= 12) FCU_FWD(12);
+  else FCU_FWD(16);
+#undef FCU_FWD
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
