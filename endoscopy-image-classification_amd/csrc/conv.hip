@@ -1022,7 +1022,7 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
                                                            const float* __restrict__ mean, const float* __restrict__ rstd,
                                                            float* __restrict__ dxt, float* __restrict__ dpooled,
                                                            float* __restrict__ partial, int N, int np, int D,
-                                                           int rows_per_block) {
+                                                           int rows_per_block, int dxt_acc) {
   extern __shared__ float pg[];  // [4 waves][2 * D]
   const int T = np + 1, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   float ga[NJ], be[NJ], pgw[NJ], pbw[NJ];
@@ -1062,7 +1062,7 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
     if (tk == 0) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        if (j * 64 + lane < D) xr[j * 64 + lane] = 2.f * d[j];
+        if (j * 64 + lane < D) xr[j * 64 + lane] = dxt_acc ? xr[j * 64 + lane] + 2.f * d[j] : 2.f * d[j];
       continue;
     }
     const long pi = (long)n * np + tk - 1;
@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(256) void fcu_down_bwd_kernel(const float* __restri
     for (int j = 0; j < NJ; ++j) {
       const int c = j * 64 + lane;
       if (c < D) {
-        xr[c] = d[j];
+        xr[c] = dxt_acc ? xr[c] + d[j] : d[j];
         xh[j] = (pvv[j] - mu) * rs;
         const float z = xh[j] * ga[j] + be[j];
         const float cdf = 0.5f * (1.0f + erff(z * 0.70710678118654752f));
@@ -2163,9 +2163,23 @@ size_t es_fcu_down_workspace(int N, int np, int D) {
 }
 
 // backward: dxt [N, np+1, D] (overwritten), dpooled [N, np, D] (overwritten), ln_w / ln_b grads (+)=
+int es_fcu_down_tokens_bwd_ex(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
+                              const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
+                              float* dln_b, int accumulate, int N, int np, int D, float* workspace, int dxt_accumulate,
+                              hipStream_t stream);
 int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
                            const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
                            float* dln_b, int accumulate, int N, int np, int D, float* workspace, hipStream_t stream) {
+  return es_fcu_down_tokens_bwd_ex(dout, pooled, ln_w, ln_b, mean, rstd, dxt, dpooled, dln_w, dln_b, accumulate, N, np,
+                                   D, workspace, 0, stream);
+}
+
+// es_fcu_down_tokens_bwd with dxt (+)= (dxt_accumulate: the x_t gradient added to what dxt holds -- the
+// second consumer of a gradient sink, conformer._GradSink)
+int es_fcu_down_tokens_bwd_ex(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
+                              const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
+                              float* dln_b, int accumulate, int N, int np, int D, float* workspace, int dxt_accumulate,
+                              hipStream_t stream) {
   if (!dout || !pooled || !ln_w || !ln_b || !mean || !rstd || !dxt || !dpooled || !dln_w || !dln_b || !workspace)
     return ES_BAD_ARG;
   if (N <= 0 || np <= 0 || D <= 0 || D > 64 * FCU_NJ) return ES_BAD_SHAPE;
@@ -2176,7 +2190,7 @@ int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* 
   const int nj = (D + 63) / 64;
 #define FCU_BWD(NJ_)                                                                                           \
   hipLaunchKernelGGL(fcu_down_bwd_kernel<NJ_>, blocks, 256, lds, stream, dout, pooled, ln_w, ln_b, mean, rstd, dxt, \
-                     dpooled, workspace, N, np, D, per)
+                     dpooled, workspace, N, np, D, per, dxt_accumulate)
   if (nj <= 2) FCU_BWD(2);
   else if (nj <= 4) FCU_BWD(4);
   else if (nj <= 6) FCU_BWD(6);

@@ -133,6 +133,7 @@ SIGNATURES = {
     "es_fcu_down_tokens_fwd": (I, [V, V, V, V, V, V, V, I, I, I, F, V]),
     "es_fcu_down_workspace": (Z, [I, I, I]),
     "es_fcu_down_tokens_bwd": (I, [V, V, V, V, V, V, V, V, V, V, I, I, I, I, V, V]),
+    "es_fcu_down_tokens_bwd_ex": (I, [V, V, V, V, V, V, V, V, V, V, I, I, I, I, V, I, V]),
     "es_tokens_cls_set": (I, [V, I, I, I, V, V]),
     "es_ce_weighted_fwd_bwd": (I, [V, I, V, V, I, I, F, V, I, V, V]),
     "es_ce_weight_sum": (I, [V, V, I, I, V, V]),

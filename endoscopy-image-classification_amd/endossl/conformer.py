@@ -304,6 +304,8 @@ CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
 BN_STATS_FUSED = os.environ.get("ENDOSSL_BN_STATS_FUSED", "1") != "0"
 # a ConvBlock input's two gradient contributions (conv1, residual) summed in place (_GradSink)
 GRAD_SINKS = os.environ.get("ENDOSSL_GRAD_SINKS", "1") != "0"
+# ... and the token buffer's two consumers (a block's FCUUp conv, the next block's FCUDown), _trans_branch
+TOKEN_SINK = os.environ.get("ENDOSSL_TOKEN_SINK", "1") != "0"
 # bf16 activation / gradient maps in the CNN branch when every conv after the stem runs on conv_bf16.hip
 # (NativeConformer.map_bf16); ENDOSSL_MAP_BF16=0 keeps fp32 maps with bf16 conv operands
 MAP_BF16 = os.environ.get("ENDOSSL_MAP_BF16", "1") != "0"
@@ -640,7 +642,7 @@ class _FcuTokensFn(torch.autograd.Function):
     """FCUDown's LayerNorm + GELU + cat(cls) fused with ConvTransBlock's `x_st + x_t`."""
 
     @staticmethod
-    def forward(ctx, pooled, xt, m, pre):
+    def forward(ctx, pooled, xt, m, pre, sink=None):
         N, h, w, D = pooled.shape
         np_ = h * w
         out = _zero_pad(torch.empty_like(xt), N * (np_ + 1))  # the kernel writes every token row
@@ -649,7 +651,7 @@ class _FcuTokensFn(torch.autograd.Function):
         call("es_fcu_down_tokens_fwd", ptr(pooled.contiguous()), ptr(xt), ptr(m.pview(pre + "ln.weight")),
              ptr(m.pview(pre + "ln.bias")), ptr(out), ptr(mean), ptr(rstd), N, np_, D, LN_EPS, _s())
         ctx.save_for_backward(pooled, mean, rstd)
-        ctx.m, ctx.pre = m, pre
+        ctx.m, ctx.pre, ctx.sink = m, pre, sink
         return out
 
     @staticmethod
@@ -660,13 +662,17 @@ class _FcuTokensFn(torch.autograd.Function):
         N, h, w, D = pooled.shape
         np_ = h * w
         dout = dout.contiguous()
-        dxt = _zero_pad(torch.empty_like(dout), N * (np_ + 1))
+        alloc = lambda: _zero_pad(torch.empty_like(dout), N * (np_ + 1))  # noqa: E731
+        sink = ctx.sink
+        dxt, acc = sink.take(alloc) if sink is not None else (alloc(), 0)
         dpooled = torch.empty_like(pooled)
         ws = torch.empty(_lib.load().es_fcu_down_workspace(N, np_, D), device=dout.device)
-        call("es_fcu_down_tokens_bwd", ptr(dout), ptr(pooled), ptr(m.pview(pre + "ln.weight")),
+        call("es_fcu_down_tokens_bwd_ex", ptr(dout), ptr(pooled), ptr(m.pview(pre + "ln.weight")),
              ptr(m.pview(pre + "ln.bias")), ptr(mean), ptr(rstd), ptr(dxt), ptr(dpooled),
-             ptr(m.gview(pre + "ln.weight")), ptr(m.gview(pre + "ln.bias")), 0, N, np_, D, ptr(ws), _s())
-        return dpooled, dxt, None, None
+             ptr(m.gview(pre + "ln.weight")), ptr(m.gview(pre + "ln.bias")), 0, N, np_, D, ptr(ws), acc, _s())
+        if sink is not None:
+            dxt = sink.give(dxt, acc)
+        return dpooled, dxt, None, None, None
 
 
 class _PatchTokensFn(torch.autograd.Function):
@@ -1181,7 +1187,9 @@ class NativeConformer(nn.Module):
             xt = _BlockFn.apply(xt, self, "trans_1.")
         xc = self._conv_block("conv_1.", x_base, 1, True, return_x2=False)
         T, g = cfg.T, cfg.grid
-        for name, _, outp, res_conv, stride, dw, last in cfg.stages():
+        stages = list(cfg.stages())
+        tsink = None  # the token buffer's gradient sink between a block's FCUUp and the next block's FCUDown
+        for si, (name, _, outp, res_conv, stride, dw, last) in enumerate(stages):
             pre = name + "."
             med = outp // 4
             xin = xc
@@ -1189,7 +1197,7 @@ class NativeConformer(nn.Module):
             x2 = self._conv_block_head(pre + "cnn_block.", xin, stride, sink=sink)
             to_branch(x2)
             with torch.cuda.stream(tb):
-                xt, up = self._trans_branch(pre, x2, xt, dw, med)
+                xt, up, tsink = self._trans_branch(pre, x2, xt, dw, med, tsink, si == len(stages) - 1)
             xc = self._conv_block_tail(pre + "cnn_block.", xin, x2, stride, res_conv, sink=sink)
             to_main(up)
             xc = self._conv_block(pre + "fusion_block.", xc, 2 if last else 1, last, x_t=up, return_x2=False)
@@ -1199,9 +1207,13 @@ class NativeConformer(nn.Module):
         trans_cls = _TransHeadFn.apply(xt, self, head_anchor)
         return conv_cls, trans_cls
 
-    def _trans_branch(self, pre, x2, xt, dw, med):
+    def _trans_branch(self, pre, x2, xt, dw, med, sink_in=None, final=False):
         """FCUDown -> transformer block -> FCUUp of one ConvTransBlock (:334-352); returns the new token
-        buffer and the FCUUp map the fusion block adds."""
+        buffer, the FCUUp map the fusion block adds and the gradient sink of the new token buffer.  That
+        buffer feeds this block's FCUUp conv and the next block's FCUDown (`x_st + x_t`): with GRAD_SINKS
+        the two backward contributions are summed in place (_GradSink; in either order -- the FCUDown
+        backward has an accumulate form) instead of by autograd's add over [n*T, D] fp32 (S1: 12 adds of
+        ~100-146 us); the final block's buffer also feeds the transformer head, so it keeps autograd's add."""
         cfg, n = self.cfg, self.cur_n
         D, T, g = cfg.dim, cfg.T, cfg.grid
         # FCUDown (:161-170): 1x1 conv (bias) -> avg-pool dw -> LN -> GELU -> cat(cls), + x_t.
@@ -1212,12 +1224,13 @@ class NativeConformer(nn.Module):
         x2p = _AvgPoolFn.apply(x2, dw) if dw > 1 else x2
         pooled = conv(self, x2p, _Map.nhwc(x2p), pre + "squeeze_block.conv_project.weight",
                       pre + "squeeze_block.conv_project.bias", D, 1, out_dtype=torch.float32)
-        xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.")
+        xt = _FcuTokensFn.apply(pooled, xt, self, pre + "squeeze_block.", sink_in)
         xt = _BlockFn.apply(xt, self, pre + "trans_block.")
         # FCUUp (:187-194): token rows 1.. as a [n, g, g, D] map -> 1x1 conv (bias) -> BN -> ReLU;
         # the nearest upsampling is fused into the fusion block's conv2 input
         tok = _Map(xt, n, g, g, D, sn=T * D, sh=g * D, sw=D, sc=1, off=D)
+        sink_out = _GradSink() if (GRAD_SINKS and TOKEN_SINK and not final) else None
         up = conv(self, xt, tok, pre + "expand_block.conv_project.weight", pre + "expand_block.conv_project.bias",
-                  med, 1, stats=True)
+                  med, 1, stats=True, sink=sink_out)
         up = bn(self, up, pre + "expand_block.bn.", relu=True)
-        return xt, up
+        return xt, up, sink_out

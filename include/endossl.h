@@ -433,6 +433,11 @@ size_t es_fcu_down_workspace(int N, int np, int D);
 int es_fcu_down_tokens_bwd(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
                            const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
                            float* dln_b, int accumulate, int N, int np, int D, float* workspace, hipStream_t stream);
+/* es_fcu_down_tokens_bwd with dxt (+)= when dxt_accumulate (the second consumer of a gradient sink) */
+int es_fcu_down_tokens_bwd_ex(const float* dout, const float* pooled, const float* ln_w, const float* ln_b,
+                              const float* mean, const float* rstd, float* dxt, float* dpooled, float* dln_w,
+                              float* dln_b, int accumulate, int N, int np, int D, float* workspace, int dxt_accumulate,
+                              hipStream_t stream);
 int es_tokens_cls_set(float* xt, int N, int T, int D, const float* cls, hipStream_t stream);
 /* F.cross_entropy(weight=w, reduction='mean') (code/loss.py:118): out[0] = sum w_y l / sum w_y;
  * dlogits = grad_scale * d(out[0]) / d logits */
