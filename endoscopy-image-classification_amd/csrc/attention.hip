@@ -161,15 +161,26 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16k16(lds_trT4(Vs, (NT16 - 1) * 16, dt * 16, g, r), pf, o[dt]);
     }
-    if (qv) {
+    // O through this query tile's own Q rows in LDS (read only by this wave, whose Q fragments are in
+    // registers): each lane holds 4 dims of one query per dt, so direct stores would write 16 rows x 32 B
+    // per instruction (partial lines: WRITE_SIZE 137 MB per F1 launch vs 80 MB of o + lse); re-read as
+    // 16-B chunks, two store instructions write the tile's 16 rows x 128 B as whole segments
+    {
       const float inv = 1.0f / l;
-      bf16* orow = a.o + (size_t)(img * T + q) * a.ldo + h * 64;
+      char* st = Qs + (qb * 16) * 128;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         bf16x4 v = {(bf16)(o[dt][0] * inv), (bf16)(o[dt][1] * inv), (bf16)(o[dt][2] * inv), (bf16)(o[dt][3] * inv)};
-        *(bf16x4*)(orow + dt * 16 + 4 * g) = v;
+        *(bf16x4*)(st + r * 128 + (dt * 16 + 4 * g) * 2) = v;
       }
-      if (g == 0) a.lse[(size_t)bh * T + q] = (mx + __log2f(l)) * 0.69314718055994531f;  // natural log
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int rr = hf * 8 + (lane >> 3), ch = lane & 7;
+        const bf16x8 v = *(const bf16x8*)(st + rr * 128 + ch * 16);
+        if (qb * 16 + rr < T) *(bf16x8*)(a.o + (size_t)(img * T + qb * 16 + rr) * a.ldo + h * 64 + ch * 8) = v;
+      }
+      if (qv && g == 0) a.lse[(size_t)bh * T + q] = (mx + __log2f(l)) * 0.69314718055994531f;  // natural log
     }
   }
 }

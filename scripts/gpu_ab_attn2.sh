@@ -1,0 +1,17 @@
+#!/bin/bash
+# attention forward output staged through LDS: tests, microbench and F1, HEAD library (build/ab/HEAD) vs tree
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; OUT="$GRAFT_REPO_ROOT/gpurun_out"
+run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.log" | head -1) $(grep -o '"fwd_occ2": {[^}]*}' "$OUT/$name.log")"; return $rc; }
+PT="python -u -m pytest -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread"
+OLD="$GRAFT_REPO_ROOT/build/ab/HEAD/libendossl_hip.so"
+run ta 400 $PT -m gpu tests/test_gpu_kernels.py -k "attention or attn" -x || exit 1
+run ts 300 $PT -m gpu tests/test_gpu_step.py -x || exit 1
+for r in 1 2; do
+  ENDOSSL_LIB=$OLD run abo_$r 120 python scripts/attn_bench.py --rounds 3 --iters 10 || exit 1
+  run abn_$r 120 python scripts/attn_bench.py --rounds 3 --iters 10 || exit 1
+done
+for r in 1 2; do
+  ENDOSSL_LIB=$OLD run f1o_$r 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit 1
+  run f1n_$r 200 python bench.py --steps 10 --warmup 3 --no-cpu-baseline || exit 1
+done
+exit 0
