@@ -84,6 +84,29 @@ __device__ __forceinline__ bf16x8 ld_row8(const bf16* p, bool valid) {
   return *(const bf16x8*)p;
 }
 
+// A 16 x 64 output tile in the MFMA C layout (lane (g, r) holds row r, columns dt*16 + 4g .. +3 of acc[dt]),
+// bf16(acc * s) out to rows dst + i * ld, i < nrows.  Direct stores would write 16 rows x 32 B per
+// instruction (partial lines: the forward's WRITE_SIZE was 137 MB per F1 launch against 80 MB of o + lse),
+// so the tile goes through `slot` (2 KiB of LDS read and written only by this wave; 16-B chunk c of row i
+// at c ^ (i & 7)) and out as 16-B lanes, two instructions writing whole 128-B row segments.
+__device__ __forceinline__ void tile_rows_out(char* slot, const f32x4* acc, float s, bf16* dst, size_t ld,
+                                              int nrows) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    const bf16x4 v = {(bf16)(acc[dt][0] * s), (bf16)(acc[dt][1] * s), (bf16)(acc[dt][2] * s), (bf16)(acc[dt][3] * s)};
+    *(bf16x4*)(slot + r * 128 + ((2 * dt + (g >> 1)) ^ (r & 7)) * 16 + (g & 1) * 8) = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    const int rr = hf * 8 + (lane >> 3), ch = lane & 7;
+    const bf16x8 v = *(const bf16x8*)(slot + rr * 128 + (ch ^ (rr & 7)) * 16);
+    if (rr < nrows) *(bf16x8*)(dst + rr * ld + ch * 8) = v;
+  }
+  __builtin_amdgcn_wave_barrier();  // the slot is rewritten by the wave's next tile
+}
+
 template <int NT16, int OCC>  // 16-key tiles: T <= 16*NT16; OCC workgroups per CU (register budget)
 __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -162,26 +185,10 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
       for (int dt = 0; dt < 4; ++dt) o[dt] = mfma16k16(lds_trT4(Vs, (NT16 - 1) * 16, dt * 16, g, r), pf, o[dt]);
     }
     // O through this query tile's own Q rows in LDS (read only by this wave, whose Q fragments are in
-    // registers): each lane holds 4 dims of one query per dt, so direct stores would write 16 rows x 32 B
-    // per instruction (partial lines: WRITE_SIZE 137 MB per F1 launch vs 80 MB of o + lse); re-read as
-    // 16-B chunks, two store instructions write the tile's 16 rows x 128 B as whole segments
-    {
-      const float inv = 1.0f / l;
-      char* st = Qs + (qb * 16) * 128;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 v = {(bf16)(o[dt][0] * inv), (bf16)(o[dt][1] * inv), (bf16)(o[dt][2] * inv), (bf16)(o[dt][3] * inv)};
-        *(bf16x4*)(st + r * 128 + (dt * 16 + 4 * g) * 2) = v;
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf) {
-        const int rr = hf * 8 + (lane >> 3), ch = lane & 7;
-        const bf16x8 v = *(const bf16x8*)(st + rr * 128 + ch * 16);
-        if (qb * 16 + rr < T) *(bf16x8*)(a.o + (size_t)(img * T + qb * 16 + rr) * a.ldo + h * 64 + ch * 8) = v;
-      }
-      if (qv && g == 0) a.lse[(size_t)bh * T + q] = (mx + __log2f(l)) * 0.69314718055994531f;  // natural log
-    }
+    // registers), whole-row stores
+    tile_rows_out(Qs + (qb * 16) * 128, o, 1.0f / l, a.o + (size_t)(img * T + qb * 16) * a.ldo + h * 64, a.ldo,
+                  T - qb * 16);
+    if (qv && g == 0) a.lse[(size_t)bh * T + q] = (mx + __log2f(l)) * 0.69314718055994531f;  // natural log
   }
 }
 
@@ -780,6 +787,7 @@ template <int NT16, bool SELF_DELTA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
+  constexpr bool TILE_OUT = NT16 <= 16;  // + 8 KiB of LDS: four 2-KiB output slots (not at 37 tiles: 160 KiB)
   constexpr int NP = NT16 / 2;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
@@ -931,20 +939,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
         dkB[dt] = mfma16k16(tq4[dt], dsf, dkB[dt]);
       }
     }
-    auto store = [&](int key, bool kv, const f32x4* dk, const f32x4* dv) {
-      if (!kv) return;
-      bf16* drow = a.dqkv + ((size_t)img * T + key) * a.lddqkv + D + h * 64;
+    if constexpr (TILE_OUT) {  // whole-row stores through the wave's LDS slot (dV: bf16(x * 1) = bf16(x))
+      char* slot = smem + 2 * TP * 128 + 2 * TP * 4 + w * 2048;
+      bf16* d0 = a.dqkv + ((size_t)img * T + kp * 32) * a.lddqkv + D + h * 64;
+      tile_rows_out(slot, dkA, a.scale, d0, a.lddqkv, T - kp * 32);
+      tile_rows_out(slot, dvA, 1.0f, d0 + D, a.lddqkv, T - kp * 32);
+      tile_rows_out(slot, dkB, a.scale, d0 + 16 * (size_t)a.lddqkv, a.lddqkv, T - kp * 32 - 16);
+      tile_rows_out(slot, dvB, 1.0f, d0 + 16 * (size_t)a.lddqkv + D, a.lddqkv, T - kp * 32 - 16);
+    } else {
+      auto store = [&](int key, bool kv, const f32x4* dk, const f32x4* dv) {
+        if (!kv) return;
+        bf16* drow = a.dqkv + ((size_t)img * T + key) * a.lddqkv + D + h * 64;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 vk = {(bf16)(dk[dt][0] * a.scale), (bf16)(dk[dt][1] * a.scale), (bf16)(dk[dt][2] * a.scale),
-                     (bf16)(dk[dt][3] * a.scale)};
-        bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
-        *(bf16x4*)(drow + dt * 16 + 4 * g) = vk;
-        *(bf16x4*)(drow + D + dt * 16 + 4 * g) = vv;
-      }
-    };
-    store(keyA, kvA, dkA, dvA);
-    store(keyB, kvB, dkB, dvB);
+        for (int dt = 0; dt < 4; ++dt) {
+          bf16x4 vk = {(bf16)(dk[dt][0] * a.scale), (bf16)(dk[dt][1] * a.scale), (bf16)(dk[dt][2] * a.scale),
+                       (bf16)(dk[dt][3] * a.scale)};
+          bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
+          *(bf16x4*)(drow + dt * 16 + 4 * g) = vk;
+          *(bf16x4*)(drow + D + dt * 16 + 4 * g) = vv;
+        }
+      };
+      store(keyA, kvA, dkA, dvA);
+      store(keyB, kvB, dkB, dvB);
+    }
   }
 }
 
@@ -956,6 +973,7 @@ template <int NT16>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
+  constexpr bool TILE_OUT = NT16 <= 16;  // + 8 KiB of LDS: four 2-KiB output slots (not at 37 tiles: 160 KiB)
   constexpr int NP = NT16 / 2;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
@@ -1021,6 +1039,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
     return ds;
   };
   auto store = [&](const QOps& Q, const f32x4* dq) {
+    if constexpr (TILE_OUT) {  // whole-row stores through the wave's LDS slot
+      const int q0 = Q.q - r;
+      tile_rows_out(smem + 2 * TP * 128 + w * 2048, dq, a.scale, a.dqkv + ((size_t)img * T + q0) * a.lddqkv + h * 64,
+                    a.lddqkv, T - q0);
+      return;
+    }
     if (!Q.qv) return;
     bf16* drow = a.dqkv + ((size_t)img * T + Q.q) * a.lddqkv + h * 64;
 #pragma unroll
@@ -1355,19 +1379,20 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
+  const size_t tile_out = nt16 <= 16 ? 4 * 2048 : 0;  // dq2 / dkv2's per-wave output slots (TILE_OUT)
   // ViT/16 at 224^2 (T = 197, 13 tiles) and at 384^2 (T = 577, the 37-tile instantiation): the pipelined /
   // two-tile loops (bit-identical to the plain ones)
 #define BWD_VARIANTS(N_)                                                                                    \
   if (g_attn_bwd_pipe == 3) {                                                                               \
-    allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq);                                                             \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq, stream, a);         \
+    allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq + tile_out);                                                             \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq + tile_out, stream, a);         \
   } else {                                                                                                  \
     allow_lds(attn_bwd_dq_pipe_kernel<N_>, lds_dq);                                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<N_>), nimg * H, 256, lds_dq, stream, a);     \
   }                                                                                                         \
   if (g_attn_bwd_pipe >= 2) {                                                                               \
-    allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv);                                                           \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);       \
+    allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv + tile_out);                                                           \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv + tile_out, stream, a);       \
   } else {                                                                                                  \
     allow_lds(attn_bwd_dkv_pipe_kernel<N_>, lds_dkv);                                                       \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);   \

@@ -1,7 +1,7 @@
 #!/bin/bash
 # attention forward output staged through LDS: tests, microbench and F1, HEAD library (build/ab/HEAD) vs tree
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; OUT="$GRAFT_REPO_ROOT/gpurun_out"
-run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.log" | head -1) $(grep -o '"fwd_occ2": {[^}]*}' "$OUT/$name.log")"; return $rc; }
+run() { local name=$1 lim=$2; shift 2; timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1; local rc=$?; echo "$name rc=$rc $(grep -o '"ms_per_step": [0-9.]*' "$OUT/$name.log" | head -1) $(grep -o "\"fwd_occ2\": {[^}]*}\|\"bwd_dq2_dkv2\": {[^}]*}\|dq2 + dkv2 == plain: [A-Za-z]*" "$OUT/$name.log" | tr "\n" " ")"; return $rc; }
 PT="python -u -m pytest -q -rf -p no:cacheprovider --timeout 120 --timeout-method thread"
 OLD="$GRAFT_REPO_ROOT/build/ab/HEAD/libendossl_hip.so"
 run ta 400 $PT -m gpu tests/test_gpu_kernels.py -k "attention or attn" -x || exit 1
