@@ -87,24 +87,34 @@ __device__ __forceinline__ bf16x8 ld_row8(const bf16* p, bool valid) {
 // A 16 x 64 output tile in the MFMA C layout (lane (g, r) holds row r, columns dt*16 + 4g .. +3 of acc[dt]),
 // bf16(acc * s) out to rows dst + i * ld, i < nrows.  Direct stores would write 16 rows x 32 B per
 // instruction (partial lines: the forward's WRITE_SIZE was 137 MB per F1 launch against 80 MB of o + lse),
-// so the tile goes through `slot` (2 KiB of LDS read and written only by this wave; 16-B chunk c of row i
-// at c ^ (i & 7)) and out as 16-B lanes, two instructions writing whole 128-B row segments.
+// so the tile goes through `slot` (SLOT_ROWS x 128 B of LDS read and written only by this wave; 16-B chunk
+// c of slot row i at c ^ (i & 7)) and out as 16-B lanes, each instruction writing whole 128-B row segments.
+// SLOT_ROWS = 8 (1 KiB, where the LDS is full) moves the tile in two halves.
+template <int SLOT_ROWS = 16>
 __device__ __forceinline__ void tile_rows_out(char* slot, const f32x4* acc, float s, bf16* dst, size_t ld,
                                               int nrows) {
   const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+  bf16x4 v[4];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    const bf16x4 v = {(bf16)(acc[dt][0] * s), (bf16)(acc[dt][1] * s), (bf16)(acc[dt][2] * s), (bf16)(acc[dt][3] * s)};
-    *(bf16x4*)(slot + r * 128 + ((2 * dt + (g >> 1)) ^ (r & 7)) * 16 + (g & 1) * 8) = v;
-  }
-  __builtin_amdgcn_wave_barrier();
+  for (int dt = 0; dt < 4; ++dt)
+    v[dt] = bf16x4{(bf16)(acc[dt][0] * s), (bf16)(acc[dt][1] * s), (bf16)(acc[dt][2] * s), (bf16)(acc[dt][3] * s)};
 #pragma unroll
-  for (int hf = 0; hf < 2; ++hf) {
-    const int rr = hf * 8 + (lane >> 3), ch = lane & 7;
-    const bf16x8 v = *(const bf16x8*)(slot + rr * 128 + (ch ^ (rr & 7)) * 16);
-    if (rr < nrows) *(bf16x8*)(dst + rr * ld + ch * 8) = v;
+  for (int p = 0; p < 16 / SLOT_ROWS; ++p) {
+    const int sr = r - p * SLOT_ROWS;  // this lane's row in the slot
+    if (SLOT_ROWS == 16 || (unsigned)sr < (unsigned)SLOT_ROWS) {
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        *(bf16x4*)(slot + sr * 128 + ((2 * dt + (g >> 1)) ^ (sr & 7)) * 16 + (g & 1) * 8) = v[dt];
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int hf = 0; hf < SLOT_ROWS / 8; ++hf) {
+      const int rr = hf * 8 + (lane >> 3), ch = lane & 7, row = p * SLOT_ROWS + rr;
+      const bf16x8 x = *(const bf16x8*)(slot + rr * 128 + (ch ^ (rr & 7)) * 16);
+      if (row < nrows) *(bf16x8*)(dst + row * ld + ch * 8) = x;
+    }
+    __builtin_amdgcn_wave_barrier();  // the slot is rewritten by the next half / the wave's next tile
   }
-  __builtin_amdgcn_wave_barrier();  // the slot is rewritten by the wave's next tile
 }
 
 template <int NT16, int OCC>  // 16-key tiles: T <= 16*NT16; OCC workgroups per CU (register budget)
@@ -292,16 +302,10 @@ __global__ __launch_bounds__(512) void attn_fwd_long_kernel(AttnArgs a) {
     if constexpr (NT16 % FCH) fwd_long_chunk<NT16 % FCH>(Ks, Vs, NT16 - NT16 % FCH, T, sl, g, r, qf0, qf1, m, l, o);
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
-    if (qv) {
-      const float inv = 1.0f / l;
-      bf16* orow = a.o + (size_t)(img * T + q) * a.ldo + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 v = {(bf16)(o[dt][0] * inv), (bf16)(o[dt][1] * inv), (bf16)(o[dt][2] * inv), (bf16)(o[dt][3] * inv)};
-        *(bf16x4*)(orow + dt * 16 + 4 * g) = v;
-      }
-      if (g == 0) a.lse[(size_t)bh * T + q] = (m + __log2f(l)) * 0.69314718055994531f;  // natural log
-    }
+    // whole-row stores through the wave's 1-KiB slot past K and V (two halves: the LDS is full)
+    tile_rows_out<8>(smem + 2 * TP * 128 + w * 1024, o, 1.0f / l, a.o + (size_t)(img * T + qb * 16) * a.ldo + h * 64,
+                     a.ldo, T - qb * 16);
+    if (qv && g == 0) a.lse[(size_t)bh * T + q] = (m + __log2f(l)) * 0.69314718055994531f;  // natural log
   }
 }
 
@@ -787,7 +791,7 @@ template <int NT16, bool SELF_DELTA = false>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
-  constexpr bool TILE_OUT = NT16 <= 16;  // + 8 KiB of LDS: four 2-KiB output slots (not at 37 tiles: 160 KiB)
+  constexpr int SLOT_ROWS = NT16 <= 16 ? 16 : 8;  // + 4 x 2 KiB of LDS (1 KiB per wave at 37 tiles: 160 KiB)
   constexpr int NP = NT16 / 2;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
@@ -939,28 +943,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
         dkB[dt] = mfma16k16(tq4[dt], dsf, dkB[dt]);
       }
     }
-    if constexpr (TILE_OUT) {  // whole-row stores through the wave's LDS slot (dV: bf16(x * 1) = bf16(x))
-      char* slot = smem + 2 * TP * 128 + 2 * TP * 4 + w * 2048;
+    {  // whole-row stores through the wave's LDS slot (dV: bf16(x * 1) = bf16(x))
+      char* slot = smem + 2 * TP * 128 + 2 * TP * 4 + w * (SLOT_ROWS * 128);
       bf16* d0 = a.dqkv + ((size_t)img * T + kp * 32) * a.lddqkv + D + h * 64;
-      tile_rows_out(slot, dkA, a.scale, d0, a.lddqkv, T - kp * 32);
-      tile_rows_out(slot, dvA, 1.0f, d0 + D, a.lddqkv, T - kp * 32);
-      tile_rows_out(slot, dkB, a.scale, d0 + 16 * (size_t)a.lddqkv, a.lddqkv, T - kp * 32 - 16);
-      tile_rows_out(slot, dvB, 1.0f, d0 + 16 * (size_t)a.lddqkv + D, a.lddqkv, T - kp * 32 - 16);
-    } else {
-      auto store = [&](int key, bool kv, const f32x4* dk, const f32x4* dv) {
-        if (!kv) return;
-        bf16* drow = a.dqkv + ((size_t)img * T + key) * a.lddqkv + D + h * 64;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          bf16x4 vk = {(bf16)(dk[dt][0] * a.scale), (bf16)(dk[dt][1] * a.scale), (bf16)(dk[dt][2] * a.scale),
-                       (bf16)(dk[dt][3] * a.scale)};
-          bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
-          *(bf16x4*)(drow + dt * 16 + 4 * g) = vk;
-          *(bf16x4*)(drow + D + dt * 16 + 4 * g) = vv;
-        }
-      };
-      store(keyA, kvA, dkA, dvA);
-      store(keyB, kvB, dkB, dvB);
+      tile_rows_out<SLOT_ROWS>(slot, dkA, a.scale, d0, a.lddqkv, T - kp * 32);
+      tile_rows_out<SLOT_ROWS>(slot, dvA, 1.0f, d0 + D, a.lddqkv, T - kp * 32);
+      tile_rows_out<SLOT_ROWS>(slot, dkB, a.scale, d0 + 16 * (size_t)a.lddqkv, a.lddqkv, T - kp * 32 - 16);
+      tile_rows_out<SLOT_ROWS>(slot, dvB, 1.0f, d0 + 16 * (size_t)a.lddqkv + D, a.lddqkv, T - kp * 32 - 16);
     }
   }
 }
@@ -973,7 +962,6 @@ template <int NT16>
 __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
-  constexpr bool TILE_OUT = NT16 <= 16;  // + 8 KiB of LDS: four 2-KiB output slots (not at 37 tiles: 160 KiB)
   constexpr int NP = NT16 / 2;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
@@ -1038,21 +1026,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
     for (int i = 0; i < 4; ++i) ds[i] = pv[i] * (dp[i] - Q.delta);
     return ds;
   };
-  auto store = [&](const QOps& Q, const f32x4* dq) {
-    if constexpr (TILE_OUT) {  // whole-row stores through the wave's LDS slot
-      const int q0 = Q.q - r;
-      tile_rows_out(smem + 2 * TP * 128 + w * 2048, dq, a.scale, a.dqkv + ((size_t)img * T + q0) * a.lddqkv + h * 64,
-                    a.lddqkv, T - q0);
-      return;
-    }
-    if (!Q.qv) return;
-    bf16* drow = a.dqkv + ((size_t)img * T + Q.q) * a.lddqkv + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16x4 v = {(bf16)(dq[dt][0] * a.scale), (bf16)(dq[dt][1] * a.scale), (bf16)(dq[dt][2] * a.scale),
-                  (bf16)(dq[dt][3] * a.scale)};
-      *(bf16x4*)(drow + dt * 16 + 4 * g) = v;
-    }
+  auto store = [&](const QOps& Q, const f32x4* dq) {  // whole-row stores through the wave's 2-KiB LDS slot
+    const int q0 = Q.q - r;
+    tile_rows_out(smem + 2 * TP * 128 + w * 2048, dq, a.scale, a.dqkv + ((size_t)img * T + q0) * a.lddqkv + h * 64,
+                  a.lddqkv, T - q0);
   };
 
   for (int it = w; it < nitems; it += 4) {
@@ -1351,7 +1328,7 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
   if (!qkv || !o || !lse) return ES_BAD_ARG;
   AttnArgs a{(const bf16*)qkv, (bf16*)o, lse, nullptr, nullptr, nullptr, ldqkv, ldo, 0, 0, T, H, scale};
   if (T > 256) {  // online softmax over key chunks, K / V staged, eight waves
-    const size_t lds = 2 * (size_t)37 * 16 * 128;
+    const size_t lds = 2 * (size_t)37 * 16 * 128 + 8 * 1024;  // K, V + eight 1-KiB output slots
     allow_lds(attn_fwd_long_kernel<37>, lds);
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_fwd_long_kernel<37>), nimg * H, 512, lds, stream, a);
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
@@ -1379,20 +1356,20 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
-  const size_t tile_out = nt16 <= 16 ? 4 * 2048 : 0;  // dq2 / dkv2's per-wave output slots (TILE_OUT)
+  const size_t slots_dq = 4 * 2048, slots_dkv = nt16 <= 16 ? 4 * 2048 : 4 * 1024;  // dq2 / dkv2 output slots
   // ViT/16 at 224^2 (T = 197, 13 tiles) and at 384^2 (T = 577, the 37-tile instantiation): the pipelined /
   // two-tile loops (bit-identical to the plain ones)
 #define BWD_VARIANTS(N_)                                                                                    \
   if (g_attn_bwd_pipe == 3) {                                                                               \
-    allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq + tile_out);                                                             \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq + tile_out, stream, a);         \
+    allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq + slots_dq);                                                             \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq + slots_dq, stream, a);         \
   } else {                                                                                                  \
     allow_lds(attn_bwd_dq_pipe_kernel<N_>, lds_dq);                                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<N_>), nimg * H, 256, lds_dq, stream, a);     \
   }                                                                                                         \
   if (g_attn_bwd_pipe >= 2) {                                                                               \
-    allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv + tile_out);                                                           \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv + tile_out, stream, a);       \
+    allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv + slots_dkv);                                                           \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv + slots_dkv, stream, a);       \
   } else {                                                                                                  \
     allow_lds(attn_bwd_dkv_pipe_kernel<N_>, lds_dkv);                                                       \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);   \

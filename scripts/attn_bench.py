@@ -1,4 +1,4 @@
-"""Attention microbenchmark at the F1 train shape (512 images x 6 heads x 197 tokens), forward
+"""Attention microbenchmark at the F1 train shape (512 images x 6 heads x 197 tokens; --s1: 120 x 12 x 577), forward
 occupancy variants A/B'd in one process (interleaved rounds, median); backward (dQ + dK/dV).
 
   python scripts/attn_bench.py [--rounds 5] [--iters 10]
@@ -31,9 +31,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--s1", action="store_true", help="the S1 shape instead: 120 images x 12 heads x 577 tokens "
+                    "(Conformer-B at 384^2, the long-sequence kernels)")
     args = ap.parse_args()
     lib = _lib.load()
-    n, T, H = 512, 197, 6
+    n, T, H = (120, 577, 12) if args.s1 else (512, 197, 6)
     D = 64 * H
     M = n * T
     torch.manual_seed(0)
