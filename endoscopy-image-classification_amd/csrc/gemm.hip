@@ -1187,12 +1187,12 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const bf16* __restr
 // thread), then a fixed-order LDS combine (deterministic).  Narrow blocks (CW = 4) for short rows so
 // a 384-column reduction still spreads over ~100 workgroups.
 template <int CW>
-__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ P, float* __restrict__ out,
-                                                              int G, int N, int accumulate) {
+__device__ __forceinline__ void reduce_partials_body(const float* __restrict__ P, float* __restrict__ out, int G,
+                                                     int N, int accumulate, int blk) {
   constexpr int RG = 256 / CW;
   __shared__ float red[RG][CW + 1];
   const int cl = threadIdx.x % CW, rg = threadIdx.x / CW;
-  const int col = blockIdx.x * CW + cl;
+  const int col = blk * CW + cl;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (col < N) {
     int g = rg;
@@ -1218,12 +1218,43 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __res
   }
 }
 
+template <int CW>
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float* __restrict__ P, float* __restrict__ out,
+                                                              int G, int N, int accumulate) {
+  reduce_partials_body<CW>(P, out, G, N, accumulate, blockIdx.x);
+}
+
+// two independent reductions of the same shape in one launch (a LayerNorm backward's dgamma and dbeta):
+// blocks [0, nb) reduce P0 -> out0, blocks [nb, 2 nb) P1 -> out1, each column as reduce_partials_kernel
+template <int CW>
+__global__ __launch_bounds__(256) void reduce_partials_pair_kernel(const float* __restrict__ P0, float* __restrict__ out0,
+                                                                   const float* __restrict__ P1, float* __restrict__ out1,
+                                                                   int G, int N, int accumulate, int nb) {
+  const bool second = (int)blockIdx.x >= nb;
+  reduce_partials_body<CW>(second ? P1 : P0, second ? out1 : out0, G, N, accumulate, blockIdx.x - (second ? nb : 0));
+}
+
 // launch: 4-column blocks when that still leaves <= 512 blocks, else 16-column blocks
 inline void launch_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream) {
   if (N <= 2048 && G >= 64)
     hipLaunchKernelGGL(reduce_partials_kernel<4>, (N + 3) / 4, 256, 0, stream, P, out, G, N, accumulate);
   else
     hipLaunchKernelGGL(reduce_partials_kernel<16>, (N + 15) / 16, 256, 0, stream, P, out, G, N, accumulate);
+}
+
+// out0 (+)= sum_g P0[g], out1 (+)= sum_g P1[g] in one launch; bit-identical to two es_reduce_partials calls
+int reduce_partials_pair(const float* P0, float* out0, const float* P1, float* out1, int G, int N, int accumulate,
+                         hipStream_t stream) {
+  if (G <= 0 || N <= 0) return ES_BAD_SHAPE;
+  if (N <= 2048 && G >= 64) {
+    const int nb = (N + 3) / 4;
+    hipLaunchKernelGGL(reduce_partials_pair_kernel<4>, 2 * nb, 256, 0, stream, P0, out0, P1, out1, G, N, accumulate, nb);
+  } else {
+    const int nb = (N + 15) / 16;
+    hipLaunchKernelGGL(reduce_partials_pair_kernel<16>, 2 * nb, 256, 0, stream, P0, out0, P1, out1, G, N, accumulate,
+                       nb);
+  }
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the

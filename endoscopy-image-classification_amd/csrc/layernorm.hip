@@ -159,7 +159,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
 
 }  // namespace
 
-extern "C" int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream);
+namespace es_gemm {  // gemm.hip: dgamma and dbeta reductions in one launch (the LayerNorm backward's two tails)
+int reduce_partials_pair(const float* P0, float* out0, const float* P1, float* out1, int G, int N, int accumulate,
+                         hipStream_t stream);
+}
 
 #define LN_DISPATCH(KER, V_, GRID, STREAM, ...)                                \
   switch (V_) {                                                                \
@@ -193,9 +196,7 @@ static int ln_bwd_launch(const DY* dy, int lddy, const float* x, int ldx, const 
   LN_BWD_DISPATCH(DY, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx, (bf16*)dxb,
                   lddxb, pg, pb, M);
   if (hipGetLastError() != hipSuccess) return ES_HIP_ERROR;
-  int rc = es_reduce_partials(pg, dgamma, grid, D, accumulate, stream);
-  if (rc) return rc;
-  return es_reduce_partials(pb, dbeta, grid, D, accumulate, stream);
+  return es_gemm::reduce_partials_pair(pg, dgamma, pb, dbeta, grid, D, accumulate, stream);
 }
 
 extern "C" {
