@@ -42,9 +42,10 @@ __device__ __forceinline__ int aswz(int r, int c) { return c ^ (((r >> 1) & 3) <
 // [TP][64] bf16 image of rows [0, TP) of `src` (row stride ld) by LDS-DMA: wave-instruction i moves
 // rows 8i..8i+7 (lane -> row 8i + lane/8, physical chunk lane%8 holding logical chunk
 // aswz(row, lane%8)); rows >= T re-read row T-1.  Caller waits (vmcnt) and barriers.
+template <int NW = 4>  // waves of the workgroup
 __device__ __forceinline__ void stage_head(char* lds, const bf16* src, int ld, int T, int TP) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int i = w; i < TP / 8; i += 4) {
+  for (int i = w; i < TP / 8; i += NW) {
     const int row = i * 8 + (lane >> 3);
     const int sr = row < T ? row : T - 1;
     glds16(src + (size_t)sr * ld + aswz(row, lane & 7) * 8, lds + i * 1024);
@@ -117,8 +118,10 @@ __device__ __forceinline__ void tile_rows_out(char* slot, const f32x4* acc, floa
   }
 }
 
-template <int NT16, int OCC>  // 16-key tiles: T <= 16*NT16; OCC workgroups per CU (register budget)
-__global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
+// NW waves per workgroup: 4, or 7 (13 query tiles of T = 197 over 7 waves: at most 2 each, where 4 waves
+// take 4 / 3 / 3 / 3; two 7-wave workgroups per CU = 14 waves at <= 128 VGPRs)
+template <int NT16, int OCC, int NW = 4>  // 16-key tiles: T <= 16*NT16; OCC workgroups per CU (register budget)
+__global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
@@ -127,16 +130,16 @@ __global__ __launch_bounds__(256, OCC) void attn_fwd_kernel(AttnArgs a) {
   char* Ks = smem;
   char* Vs = smem + TP * 128;
   char* Qs = smem + 2 * TP * 128;  // Q staged with K and V: one wait, no per-tile global latency
-  stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
-  stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
-  stage_head(Qs, base + h * 64, a.ldqkv, T, TP);
+  stage_head<NW>(Ks, base + D + h * 64, a.ldqkv, T, TP);
+  stage_head<NW>(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  stage_head<NW>(Qs, base + h * 64, a.ldqkv, T, TP);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   const int nqt = (T + 15) >> 4;
   const float sl = a.scale * 1.44269504088896341f;
-  for (int qb = w; qb < nqt; qb += 4) {
+  for (int qb = w; qb < nqt; qb += NW) {
     const int q = qb * 16 + r;
     const bool qv = q < T;
     const bf16x8 qf0 = lds_row8(Qs, q, g), qf1 = lds_row8(Qs, q, 4 + g);
@@ -1277,8 +1280,10 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
 
 // forward occupancy target (workgroups per CU the register budget is sized for): 2 = no cap
 // (measured faster: 108 vs 150 us at the F1 shape, scripts/attn_bench.py),
-// 3 = 168 VGPRs (three 52-KiB heads per CU, small spill)
-int g_attn_fwd_occ = 2;
+// 3 = 168 VGPRs (three 52-KiB heads per CU, small spill), 7 (default) = variant 2 with seven waves per
+// workgroup at 13 tiles (T = 197): 0.0851 / 0.0836 -> 0.0731 / 0.0728 ms at the F1 head batch,
+// bit-identical (scripts/attn_bench.py; 14 waves per CU instead of 8, no 4-tile wave)
+int g_attn_fwd_occ = 7;
 // backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 2 = the pipelined dQ
 // and the two-key-tiles-per-wave dK / dV (attn_bwd_dkv2_kernel), 3 = two query tiles per wave for dQ
 // (attn_bwd_dq2_kernel) and dkv2, 0 = the plain loops (all bit-identical).  Default 3: 0.257 ms vs 0.269 (1) and
@@ -1335,7 +1340,10 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
   }
   const int nt16 = (T + 15) / 16;
   const size_t lds = 3 * (size_t)nt16 * 16 * 128;  // K, V, Q head tiles (two heads per CU at T = 197)
-  if (g_attn_fwd_occ == 2) {
+  if (g_attn_fwd_occ == 7 && nt16 == 13) {
+    allow_lds(attn_fwd_kernel<13, 2, 7>, lds);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_fwd_kernel<13, 2, 7>), nimg * H, 448, lds, stream, a);
+  } else if (g_attn_fwd_occ == 2 || g_attn_fwd_occ == 7) {
     FWD_DISPATCH(nt16, 2, nimg * H, lds, stream, a);
   } else {
     FWD_DISPATCH(nt16, 3, nimg * H, lds, stream, a);

@@ -49,12 +49,14 @@ def main():
     fwd = lambda: call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 0.125, s)  # noqa: E731
     bwd = lambda: call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(do), D, ptr(dqkv),  # noqa
                        3 * D, n, T, H, 0.125, s)
-    res = {"fwd_occ2": [], "fwd_occ3": [], "bwd_plain": [], "bwd_pipe": [], "bwd_dkv2": [], "bwd_dq2_dkv2": []}
+    res = {"fwd_occ2": [], "fwd_occ3": [], "fwd_occ7": [], "bwd_plain": [], "bwd_pipe": [], "bwd_dkv2": [],
+           "bwd_dq2_dkv2": []}
     outs = {}
     for _ in range(args.rounds):
-        for occ in (2, 3):
+        for occ in (2, 3, 7):  # 7: seven waves per workgroup (T = 197)
             lib.es_set_attn_variant(occ)
             res[f"fwd_occ{occ}"].append(timed(fwd, args.iters))
+            outs[f"fwd_occ{occ}"] = (o.clone(), lse.clone())
         lib.es_set_attn_variant(2)
         fwd()
         for v, name in ((0, "bwd_plain"), (1, "bwd_pipe"), (2, "bwd_dkv2"), (3, "bwd_dq2_dkv2")):
@@ -62,6 +64,8 @@ def main():
             res[name].append(timed(bwd, args.iters))
             outs[name] = dqkv.clone()
     lib.es_set_attn_bwd_variant(1)
+    print("fwd occ7 == occ2 (bit-exact):", all(torch.equal(x, y) for x, y in zip(outs["fwd_occ7"], outs["fwd_occ2"])),
+          flush=True)
     print("bwd pipe == plain (bit-exact):", torch.equal(outs["bwd_pipe"], outs["bwd_plain"]),
           "dkv2 == plain:", torch.equal(outs["bwd_dkv2"], outs["bwd_plain"]),
           "dq2 + dkv2 == plain:", torch.equal(outs["bwd_dq2_dkv2"], outs["bwd_plain"]), flush=True)
