@@ -40,10 +40,10 @@ if os.path.exists(tr):
               "|---:|---:|---:|---|---:|"]
     for (n, g), (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
         lines.append(f"| {t / steps / 1e3:.3f} | {c / steps:.1f} | {t / c:.1f} | `{n}` | {g} |")
-    lines += ["", "The bench's roofline site (fc1 weight gradient, N1 x N2 = 1536 x 384 over M = 100,864 tokens) is "
-              "the `gemm_tn_big_kernel` launch of 256 workgroups (8 tiles x 32 splits; the fc2 site has the same "
-              "grid) plus its `splitk_reduce_kernel` of 576 workgroups (1536 x 384 / 4 / 256). Durations under "
-              "the profiler run longer than the bench's live HIP-event figure (lower clocks while profiling, "
-              "MI355X_MICROARCH.md 'DVFS give-back' item 2)."]
+    lines += ["", "The bench's roofline site (a block's four weight-gradient GEMMs, fc2 / fc1 / proj / qkv over "
+              "M = 100,864 tokens) is the `gemm_tn_big_grouped_kernel` launch of 96 workgroups (24 tiles of 384 x 192 "
+              "x 4 splits, 3/8 of the CUs, 12 per step + the patch-embedding one) plus its "
+              "`splitk_reduce_grouped_kernel`. Durations under the profiler run longer than the bench's live "
+              "HIP-event figure (lower clocks while profiling, MI355X_MICROARCH.md 'DVFS give-back' item 2)."]
 open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines[:20]))
