@@ -1280,7 +1280,12 @@ int reduce_partials_pair(const float* P0, float* out0, const float* P1, float* o
     case EPI_MULAUX: NT_LAUNCH(EPI_MULAUX, BKT_, NST_, TBM_, ##__VA_ARGS__)       \
     default: return ES_BAD_ARG;                                                   \
   }
+// The residual-stream outputs (EPI_F32_RESID: the proj / fc2 forward's x + f(x), read right away by the
+// next LayerNorm) keep plain, cacheable C stores instead of nt: F1 30.82 / 30.84 -> 30.59 / 30.66 ms on one
+// box (scripts/gpu_storeplain.sh); plain stores for the qkv (EPI_BF16) or fc1 (EPI_GELU_D) outputs were
+// slower (30.90 / 31.03 ms).
 int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
+  if (cfg == 11 && epi == EPI_F32_RESID) NT_LAUNCH(EPI_F32_RESID, 64, 2, 64, 0)
   switch (cfg) {
     case 0: NT_EPIS(64, 2, 128)
     case 3: NT_EPIS(32, 4, 128)
@@ -1324,6 +1329,7 @@ int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) 
     if (cfg == 17) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 5)
     BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 3)
   }
+  if (cfg == 10 && epi == EPI_F32_RESID) BIG_LAUNCH(EPI_F32_RESID, 4, 4, 4, 3, 32, 4, 0, 0)  // plain stores
   switch (cfg) {
     case 10: BIG_EPIS2(4, 4, 4, 3, 32, 4)  // 256x128, BK32, 3 stages (72 KiB), two workgroups per CU
     case 6: BIG_EPIS(2, 8, 4, 2, 64)   // 256x256, BK64, 2 stages (128 KiB)
