@@ -103,9 +103,12 @@ int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks,
 /* out[n] (+)= sum_g P[g][n]  (per-workgroup partials -> parameter gradient) */
 int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream);
 
-/* tuning knob: forward attention occupancy target (2 or 3 workgroups per CU); returns previous */
+/* tuning knob: forward attention kernel -- 7 (default) = seven waves per workgroup at T <= 208 (13 tiles),
+   else as 2; 2 = four waves, register budget of two workgroups per CU; 3 = four waves, three per CU;
+   returns previous */
 int es_set_attn_variant(int occ);
-/* attention backward loops: 1 = software-pipelined (default), 0 = plain; returns the previous value */
+/* attention backward loops: 3 (default) = two query / key tiles per wave item (dq2 / dkv2), 2 = pipelined
+   dQ + dkv2, 1 = software-pipelined, 0 = plain (all bit-identical); returns the previous value */
 int es_set_attn_bwd_variant(int v);
 /* 1 (default): the backward variant above also for T > 256 (the 37-tile kernels); 0: plain loops there. */
 int es_set_attn_bwd_long(int v);
