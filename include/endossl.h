@@ -103,7 +103,7 @@ int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks,
 /* out[n] (+)= sum_g P[g][n]  (per-workgroup partials -> parameter gradient) */
 int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate, hipStream_t stream);
 
-/* tuning knob: forward attention kernel -- 7 (default) = seven waves per workgroup at T <= 208 (13 tiles),
+/* tuning knob: forward attention kernel -- 7 (default) = seven waves per workgroup at 13 key tiles (193 <= T <= 208: ViT/16 at 224^2),
    else as 2; 2 = four waves, register budget of two workgroups per CU; 3 = four waves, three per CU;
    returns previous */
 int es_set_attn_variant(int occ);
