@@ -306,7 +306,7 @@ def _attn_ref(qkv, n, T, H):
     return o, lse
 
 
-@pytest.fixture(params=[2, 3], ids=["occ2", "occ3"])
+@pytest.fixture(params=[2, 3, 7], ids=["occ2", "occ3", "w7"])
 def attn_occ(request):
     old = _lib.load().es_set_attn_variant(request.param)
     yield request.param
@@ -326,6 +326,29 @@ def test_attention_fwd(n, T, H, attn_occ):
     torch.testing.assert_close(o[:n * T].float(), o_ref, rtol=2e-2, atol=2e-2)
     torch.testing.assert_close(lse.view(n, H, T), lse_ref, rtol=1e-3, atol=2e-3)
     assert torch.all(o[n * T:] == 0)
+
+
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 200, 2), (64, 197, 6)])
+def test_attention_fwd_seven_waves_bit_identical(n, T, H):
+    """The seven-wave forward (es_set_attn_variant 7, the default at 13 key tiles) runs each query tile's
+    MFMAs, softmax and output staging exactly as the four-wave kernel (2): o and lse bit-identical, rows
+    past n*T untouched."""
+    D = H * 64
+    torch.manual_seed(11 + T)
+    qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
+    lib = _lib.load()
+    res = {}
+    for v in (2, 7):
+        old = lib.es_set_attn_variant(v)
+        o = torch.full((qkv.shape[0], D), 5.0, dtype=torch.bfloat16, device=DEV)
+        lse = torch.zeros(n * H * T, device=DEV)
+        call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
+        torch.cuda.synchronize()
+        lib.es_set_attn_variant(old)
+        res[v] = (o, lse)
+    assert torch.equal(res[2][0], res[7][0])
+    assert torch.equal(res[2][1], res[7][1])
+    assert torch.all(res[7][0][n * T:] == 5.0)
 
 
 @pytest.mark.parametrize("n,T,H", [(3, 197, 6), (4, 17, 2), (3, 40, 2), (2, 250, 1), (2, 1, 1), (2, 577, 3),
@@ -542,6 +565,19 @@ def test_layernorm_fwd_bwd(D, M):
     torch.testing.assert_close(dx3, dx4, rtol=0, atol=0)
     torch.testing.assert_close(dg3, dg4, rtol=0, atol=0)
     torch.testing.assert_close(db3, db4, rtol=0, atol=0)
+    # dgamma / dbeta leave through one paired reduction launch: bit-identical to es_reduce_partials over
+    # the partials the kernel left in the workspace (pg = ws[:G*D], pb = ws[G*D:2*G*D]); accumulate adds
+    G = min(1024, (M + 7) // 8)
+    rg, rb = torch.zeros_like(dg), torch.zeros_like(db)
+    call("es_reduce_partials", ptr(ws), ptr(rg), G, D, 0, S())
+    call("es_reduce_partials", ptr(ws[G * D:]), ptr(rb), G, D, 0, S())
+    torch.testing.assert_close(dg4, rg, rtol=0, atol=0)
+    torch.testing.assert_close(db4, rb, rtol=0, atol=0)
+    dg5, db5 = dg4.clone(), db4.clone()
+    call("es_layernorm_bwd", ptr(dyr), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx4), D,
+         None, D, ptr(dg5), ptr(db5), ptr(ws), 1024, M, D, 1, S())
+    torch.testing.assert_close(dg5, dg4 + rg, rtol=0, atol=0)
+    torch.testing.assert_close(db5, db4 + rb, rtol=0, atol=0)
 
 
 # ------------------------------------------------------------------------------------- ViT ends
