@@ -986,8 +986,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
     int q;
     bool qv;
   };
-  auto load_q = [&](int qb) {
-    QOps o;
+  // a query tile's rows from HBM (issued one wave item ahead of their use: their latency hides behind the
+  // current item's MFMAs), then finished -- delta = rowsum(dO * O) -- when the item starts
+  struct QRaw {
+    bf16x8 qf0, qf1, df0, df1, of0, of1;
+    float lse;
+    int q;
+    bool qv;
+  };
+  auto load_raw = [&](int qb) {
+    QRaw o;
     o.q = qb * 16 + r;
     o.qv = o.q < T;
     const size_t tok = (size_t)img * T + o.q;
@@ -998,15 +1006,27 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
     o.qf1 = ld_row8(qrow + 32 + 8 * g, o.qv);
     o.df0 = ld_row8(dorow + 8 * g, o.qv);
     o.df1 = ld_row8(dorow + 32 + 8 * g, o.qv);
-    const bf16x8 of0 = ld_row8(orow + 8 * g, o.qv), of1 = ld_row8(orow + 32 + 8 * g, o.qv);
+    o.of0 = ld_row8(orow + 8 * g, o.qv);
+    o.of1 = ld_row8(orow + 32 + 8 * g, o.qv);
+    o.lse = o.qv ? a.lse[(size_t)bh * T + o.q] : 0.f;
+    return o;
+  };
+  auto finish_q = [&](const QRaw& x) {
+    QOps o;
+    o.q = x.q;
+    o.qv = x.qv;
+    o.qf0 = x.qf0;
+    o.qf1 = x.qf1;
+    o.df0 = x.df0;
+    o.df1 = x.df1;
     float delta = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) delta += (float)o.df0[j] * (float)of0[j] + (float)o.df1[j] * (float)of1[j];
+    for (int j = 0; j < 8; ++j) delta += (float)x.df0[j] * (float)x.of0[j] + (float)x.df1[j] * (float)x.of1[j];
     delta += __shfl_xor(delta, 16, 64);
     delta += __shfl_xor(delta, 32, 64);
     o.delta = delta;
     if (o.qv && g == 0) a.delta[(size_t)bh * T + o.q] = delta;  // consumed by the dK/dV pass
-    o.lq = o.qv ? a.lse[(size_t)bh * T + o.q] * 1.44269504088896341f : 0.f;  // log2 units
+    o.lq = o.qv ? x.lse * 1.44269504088896341f : 0.f;            // log2 units
     return o;
   };
   // dS^T tile t (keys 16t + 4g + i on this lane's query) from the key tile's K / V rows
@@ -1035,8 +1055,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
                   a.lddqkv, T - q0);
   };
 
+  QRaw rA = load_raw(2 * w), rB = load_raw(2 * w + 1);
   for (int it = w; it < nitems; it += 4) {
-    const QOps QA = load_q(2 * it), QB = load_q(2 * it + 1);
+    const QOps QA = finish_q(rA), QB = finish_q(rB);
+    if (it + 4 < nitems) {
+      rA = load_raw(2 * (it + 4));
+      rB = load_raw(2 * (it + 4) + 1);
+    }
     f32x4 dqA[4], dqB[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dqA[dt] = dqB[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
