@@ -291,11 +291,21 @@ __global__ __launch_bounds__(512) void attn_fwd_long_kernel(AttnArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   const int nqt = (T + 15) >> 4;
   const float sl = a.scale * 1.44269504088896341f;
+  // the query block's Q fragments come from HBM one block ahead of their use (their latency hides behind the
+  // current block's chunks)
+  auto load_qf = [&](int qb, bf16x8& f0, bf16x8& f1) {
+    const int q = qb * 16 + r;
+    const bf16* qrow = base + (size_t)(q < T ? q : T - 1) * a.ldqkv + h * 64;
+    f0 = *(const bf16x8*)(qrow + 8 * g);
+    f1 = *(const bf16x8*)(qrow + 32 + 8 * g);
+  };
+  bf16x8 nq0, nq1;
+  if (w < nqt) load_qf(w, nq0, nq1);
   for (int qb = w; qb < nqt; qb += 8) {
     const int q = qb * 16 + r;
     const bool qv = q < T;
-    const bf16* qrow = base + (size_t)(qv ? q : T - 1) * a.ldqkv + h * 64;
-    const bf16x8 qf0 = *(const bf16x8*)(qrow + 8 * g), qf1 = *(const bf16x8*)(qrow + 32 + 8 * g);
+    const bf16x8 qf0 = nq0, qf1 = nq1;
+    if (qb + 8 < nqt) load_qf(qb + 8, nq0, nq1);
     float m = -INFINITY, l = 0.f;
     f32x4 o[4];
 #pragma unroll
