@@ -591,6 +591,25 @@ def test_im2col_matches_unfold():
     torch.testing.assert_close(pt.float(), ref.bfloat16().float(), rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("n,Sz", [(5, 224), (3, 64), (2, 384), (448, 224)])
+def test_im2col_u8_matches_normalised_fp32(n, Sz):
+    """es_patch_im2col_u8 (uint8 pixels, ToTensor + Normalize fused; one (image, patch row) per workgroup
+    staged through LDS) == es_patch_im2col over the same pixels normalised in fp32, bit for bit, incl. the
+    F1 weak batch (448 images) and the ViT-B/16 384^2 size."""
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    g = torch.Generator().manual_seed(n + Sz)
+    u8 = torch.randint(0, 256, (n, 3, Sz, Sz), generator=g, dtype=torch.uint8)
+    f32 = ((u8.float() / 255.0 - torch.tensor(mean).view(1, 3, 1, 1)) / torch.tensor(std).view(1, 3, 1, 1)).to(DEV)
+    rows = n * (Sz // 16) ** 2
+    pa = torch.full((rows + 7, 768), 9.0, dtype=torch.bfloat16, device=DEV)
+    pb = torch.zeros(rows, 768, dtype=torch.bfloat16, device=DEV)
+    call("es_patch_im2col_u8", ptr(u8.to(DEV)), *mean, *std, ptr(pa), n, Sz, 16, S())
+    call("es_patch_im2col", ptr(f32), ptr(pb), n, Sz, 16, S())
+    torch.cuda.synchronize()
+    assert torch.equal(pa[:rows], pb)
+    assert torch.all(pa[rows:] == 9.0)
+
+
 def test_cls_head_fwd_bwd():
     torch.manual_seed(4)
     n, T, D, C = 37, 5, 384, 23
