@@ -271,7 +271,7 @@ def run_secondary(args):
         batch = (batch[0], (batch[1], None))
         unl, tfl = B * MU, 3 * 9.197e9 * (B + 3 * B * MU) / 1e12 + 2 * (B * MU) * Q * (L + 23) / 1e12
         from endossl.vit import Engine
-        exe = tfl - (vit_s_pruned_tflop(B + 3 * B * MU, B + 3 * B * MU) if Engine.PRUNE_LAST and Engine.LANES != 2
+        exe = tfl - (vit_s_pruned_tflop(B + 3 * B * MU, B + 3 * B * MU) if Engine.PRUNE_LAST
                      else 0.0)
         desc = (f"C1: CoMatch ViT-S/16 step, B={B} + 3 x mu*B={B * MU} (weak, strong0, strong1), 224^2, L={L}, "
                 f"bank Q={Q} (memory smoothing over all Q rows), EMA 0.999, lambda_u=lambda_c=2")
@@ -336,7 +336,7 @@ def run_secondary(args):
                 f"MFMA ({'on' if model.conv_bf16 else 'off: ENDOSSL_CONV_BF16=0'}), CNN activation / gradient maps "
                 f"{'bf16' if getattr(model, 'map_bf16', False) else 'fp32'}, BatchNorm statistics fp32")
         map_dtype = "bf16" if getattr(model, "map_bf16", False) else "fp32"
-    steplog = os.environ.get("ENDOSSL_BENCH_STEPLOG") == "1"  # diagnostics: synchronises every step
+    steplog = args.steplog  # diagnostics: synchronises every step
     for _ in range(args.warmup):
         tr.step(batch)
     torch.cuda.synchronize()
@@ -472,6 +472,7 @@ def main():
                     help="N > 1: the gradient all-reduce as one launch after the backward (single), per-block "
                          "buckets overlapped with it (overlap), or auto = whichever ran faster in 3 untimed "
                          "steps each before the timed region (max over ranks)")
+    ap.add_argument("--steplog", action="store_true", help="diagnostics: synchronise and log every timed step")
     ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
                     help="hipGraph replay of the step's forward/backward (on); auto = off = eager launches "
                          "(measured faster than the replay at N = 1 and at the N = 8 shard, DESIGN.md §5)")
@@ -672,7 +673,7 @@ def main():
             "step_tflops": round(work / (ms / 1e3), 1),
             "step_mfma_frac": round(work / (ms / 1e3) / PEAK_BF16_TFLOPS / world, 4),
             "executed_step_tflop": round((STEP_TFLOP_F1 - (vit_s_pruned_tflop(448 + 512, 512)
-                                                           if Engine.PRUNE_LAST and Engine.LANES != 2 else 0.0))
+                                                           if Engine.PRUNE_LAST else 0.0))
                                          * glob_unl / 448.0, 3),
             "final_loss": round(loss, 6),
             "roofline": {"kernel": (layer + " (bf16 operands, fp32 split-K slabs; rocprofv3: "

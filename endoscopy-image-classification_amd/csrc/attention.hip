@@ -1427,49 +1427,6 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
 }
 
 
-// es_attn_bwd split in two independent launches (run them on two streams): the dQ pass, and the
-// dK/dV pass computing its own delta = rowsum(dO * O).  delta: workspace [nimg*H*T] of the dQ pass.
-int es_attn_bwd_dq(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta,
-                   const void* dout, int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale,
-                   hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > ATTN_TMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
-      (lddqkv % 8) || (ldo % 8) || (lddo % 8))
-    return ES_BAD_SHAPE;
-  if (!qkv || !o || !lse || !delta || !dout || !dqkv) return ES_BAD_ARG;
-  AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, delta, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
-             lddqkv, T, H, scale};
-  const int nt16 = attn_tiles(T);
-  const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
-  ATTN_DISPATCH(attn_bwd_dq_kernel, nt16, nimg * H, lds_dq, stream, a);
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-}
-
-#define DKV_SELF(N_) attn_bwd_dkv_kernel<N_, true>
-int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
-                    void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream) {
-  if (nimg <= 0 || T <= 0 || T > ATTN_TMAX || H <= 0 || ldqkv < 3 * H * 64 || lddqkv < 3 * H * 64 || (ldqkv % 8) ||
-      (lddqkv % 8) || (ldo % 8) || (lddo % 8))
-    return ES_BAD_SHAPE;
-  if (!qkv || !o || !lse || !dout || !dqkv) return ES_BAD_ARG;
-  AttnArgs a{(const bf16*)qkv, (bf16*)o, (float*)lse, nullptr, (const bf16*)dout, (bf16*)dqkv, ldqkv, ldo, lddo,
-             lddqkv, T, H, scale};
-  const int nt16 = attn_tiles(T);
-  const size_t lds_dkv = 2 * (size_t)nt16 * 16 * 128 + 2 * (size_t)nt16 * 16 * 4;
-  switch (nt16) {
-#define DKV_CASE(N_)                                                                                   \
-  case N_:                                                                                            \
-    allow_lds(DKV_SELF(N_), lds_dkv);                                                                 \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(DKV_SELF(N_)), nimg * H, 256, lds_dkv, stream, a);             \
-    break;
-    DKV_CASE(1) DKV_CASE(2) DKV_CASE(3) DKV_CASE(4) DKV_CASE(5) DKV_CASE(6) DKV_CASE(7) DKV_CASE(8)
-    DKV_CASE(9) DKV_CASE(10) DKV_CASE(11) DKV_CASE(12) DKV_CASE(13) DKV_CASE(14) DKV_CASE(15) DKV_CASE(16) DKV_CASE(37)
-#undef DKV_CASE
-    default: return ES_BAD_SHAPE;
-  }
-  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-}
-#undef DKV_SELF
-
 // CLS-query attention of a block whose non-CLS outputs are unused (the ViT's last block): qkv
 // [nimg*T, ldqkv] -> o [nimg, ldo] (the CLS rows only, compact), lse [nimg*H].
 int es_attn_cls_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,

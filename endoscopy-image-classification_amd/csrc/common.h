@@ -43,6 +43,25 @@ __device__ __forceinline__ void glds16_asm(const void* src, char* lds) {
                : "memory");
 }
 
+// Buffer-addressed 16-byte LDS-DMA (buffer_load_dwordx4 ... offen lds), inline asm like glds16_asm: the
+// source is resource + voff (per lane, 32 bit) + soff (wave-uniform), so a loop that walks a tensor keeps one
+// VGPR per piece instead of a 64-bit address.  Out-of-range pieces read as zero.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 rsrc_i4(const void* base, unsigned bytes) {
+  const uint64_t b = (uint64_t)(uintptr_t)base;
+  return i32x4{__builtin_amdgcn_readfirstlane((int)(uint32_t)b), __builtin_amdgcn_readfirstlane((int)(b >> 32)),
+               __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000};
+}
+__device__ __forceinline__ void bl16_asm(i32x4 rsrc, unsigned voff, unsigned soff, char* lds) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(dst), "s"(__builtin_amdgcn_readfirstlane(soff))
+               : "memory");
+}
+
 // Raw buffer access (range-checked by the resource: out-of-range loads return 0, out-of-range
 // stores are dropped).  Epilogues map rows past M to an out-of-range offset with a select instead
 // of branching, which keeps the code straight-line so the waitcnt pass can count (a divergent
@@ -220,6 +239,19 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   const int xcd = orig & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+// vmcnt immediates 0..63 (counted waits computed at run time)
+__device__ __forceinline__ void wait_vmcnt_any(int n) {
+  switch (n) {
+#define ES_VM1(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+#define ES_VM8(B) ES_VM1(B) ES_VM1(B + 1) ES_VM1(B + 2) ES_VM1(B + 3) ES_VM1(B + 4) ES_VM1(B + 5) ES_VM1(B + 6) ES_VM1(B + 7)
+    ES_VM8(1) ES_VM8(9) ES_VM8(17) ES_VM8(25) ES_VM8(33) ES_VM8(41) ES_VM8(49) ES_VM1(57) ES_VM1(58) ES_VM1(59)
+    ES_VM1(60) ES_VM1(61) ES_VM1(62) ES_VM1(63)
+#undef ES_VM8
+#undef ES_VM1
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
 }
 
 // Opt a kernel into more than 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU).  Set once per kernel

@@ -469,181 +469,6 @@ __global__ __launch_bounds__(512, OCC) void gemm_nt_big_kernel(NTArgs p) {
                                         n0 + wn * NF * 16, lane, epre);
 }
 
-// ---- persistent ring NT kernel ------------------------------------------------------------------
-// One 512-thread workgroup per CU walks its tiles (256 x 128 output, 8 waves of 64 x 64, 32-deep K
-// steps); the LDS ring of RING slots runs ACROSS tiles: the step sequence is (tile, k) flattened, and
-// step s + RING - 1 is issued right after the barrier that publishes step s, whichever tile it
-// belongs to -- so the next tile's first stages are in flight during this tile's epilogue, and no
-// workgroup launch, prologue bubble or teardown sits between tiles.  Measured on the isolated
-// variant-10 kernel (two workgroups per CU, one tile each) at the qkv forward shape: main loop alone
-// 77 us, epilogue alone 35 us, operand stream alone 74 us, operand stream + epilogue 142 us (the full
-// kernel 139 us) -- the tile-serial structure, not the arithmetic, set its time.
-// Each slot holds the A (256 x 32) and B (128 x 32) stages plus the tile's 128 bias values (every step
-// carries them: 512 B per 24 KiB, a uniform DMA count per step); the epilogue stages its fp32 rows in
-// the slot the tile's last step just freed (8-row chunks, 2,176 B per wave), so the ring keeps
-// RING - 1 = 5 steps (120 KiB) in flight.  The DMA is inline asm (glds16_asm: the compiler would
-// drain pending LDS-DMA in front of the epilogue's LDS writes); every wait is a counted vmcnt over
-// the wave's own DMA and epilogue operations.  Tiles: t = j * G + xcd * (G / 8) + slot, so the
-// workgroups of one XCD work on 32 consecutive tiles (shared A rows in that XCD's L2).
-template <int EPI>
-constexpr int ring_epi_ops() {  // vm operations per lane per 8-row chunk: C stores + aux loads
-  return ((EPI == EPI_GELU || EPI == EPI_GELU_D || EPI == EPI_F32 || EPI == EPI_F32_RESID || EPI == EPI_PATCH) ? 2 : 1) +
-         ((EPI == EPI_F32_RESID || EPI == EPI_PATCH) ? 2 : ((EPI == EPI_DGELU || EPI == EPI_MULAUX) ? 1 : 0));
-}
-
-// vmcnt immediates 0..63 (counted waits computed at run time)
-__device__ __forceinline__ void wait_vmcnt_any(int n) {
-  switch (n) {
-#define ES_VM1(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
-#define ES_VM8(B) ES_VM1(B) ES_VM1(B + 1) ES_VM1(B + 2) ES_VM1(B + 3) ES_VM1(B + 4) ES_VM1(B + 5) ES_VM1(B + 6) ES_VM1(B + 7)
-    ES_VM8(1) ES_VM8(9) ES_VM8(17) ES_VM8(25) ES_VM8(33) ES_VM8(41) ES_VM8(49) ES_VM1(57) ES_VM1(58) ES_VM1(59)
-    ES_VM1(60) ES_VM1(61) ES_VM1(62) ES_VM1(63)
-#undef ES_VM8
-#undef ES_VM1
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <int EPI, int RING, int STAUX, int OCC = 1>
-__global__ __launch_bounds__(512, OCC) void gemm_nt_ring_kernel(NTArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int TBM = 256, TBN = 128, BKT = 32, ROWB = 64, RPI = 16, CPR = 4;
-  constexpr int IA = TBM / (8 * RPI), IB = TBN / (8 * RPI);  // 2 + 1 full pieces per wave per step
-  constexpr int PER = IA + IB + 1;                          // + the bias piece
-  constexpr int TA = TBM * ROWB, TB = TBN * ROWB, SLOT = TA + TB + TBN * 4;
-  constexpr int D = RING - 1;
-  constexpr int EOPS = 8 * ring_epi_ops<EPI>();
-  constexpr int EROWB = 4 * 64 + 16;  // epilogue staging row: 64 fp32 + 16 B pad
-  const int ntn = p.N / TBN, T = ((p.M + TBM - 1) / TBM) * ntn;
-  const int G = gridDim.x, per_x = G >> 3;
-  const int t0 = (blockIdx.x & 7) * per_x + (blockIdx.x >> 3);
-  const int ntiles = t0 < T ? (T - 1 - t0) / G + 1 : 0;
-  const int KS = p.K / BKT;
-  const int S = ntiles * KS;
-  if (S == 0) return;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
-  const int g = lane >> 4, r = lane & 15;
-
-  // per-lane DMA source offsets (elements) relative to the tile's (m0, n0, k0)
-  size_t oa[IA];
-#pragma unroll
-  for (int j = 0; j < IA; ++j) {
-    const int row = (j * 8 + w) * RPI + lane / CPR;
-    oa[j] = (size_t)row * p.lda + swz64(row, lane % CPR) * 8;
-  }
-  const int rowb = w * RPI + lane / CPR;
-  const size_t ob = (size_t)rowb * p.ldb + swz64(rowb, lane % CPR) * 8;
-  const float* biasp = p.bias ? p.bias : (const float*)p.A;  // null bias: harmless bytes, never read back
-  // issue-side cursor: step si = (tile ji, step ki)
-  int ji = 0, ki = 0;
-  const bf16* ta = p.A;
-  const bf16* tb = p.B;
-  const float* tbias = biasp;
-  auto set_tile = [&](int j) {
-    const int t = j * G + t0, mb = t / ntn, nb = t - mb * ntn;
-    ta = p.A + (size_t)mb * TBM * p.lda;
-    tb = p.B + (size_t)nb * TBN * p.ldb;
-    tbias = biasp + (p.bias ? nb * TBN : 0);
-  };
-  set_tile(0);
-  auto issue_next = [&](int slot) {
-    char* S_ = smem + slot * SLOT;
-    const int k0 = ki * BKT;
-#pragma unroll
-    for (int j = 0; j < IA; ++j) glds16_asm(ta + oa[j] + k0, S_ + (j * 8 + w) * 1024);
-    glds16_asm(tb + ob + k0, S_ + TA + w * 1024);
-    if (lane < 4) glds16_asm(tbias + lane * 4 + w * 16, S_ + TA + TB + w * 64);  // 64 B per wave (lane-linear)
-    if (++ki == KS) {
-      ki = 0;
-      if (++ji < ntiles) set_tile(ji);
-    }
-  };
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const int npro = S < D ? S : D;
-  for (int st = 0; st < npro; ++st) issue_next(st);
-  int slot = 0;      // slot of step s
-  int jt = 0;        // tile of step s
-  for (int s = 0; s < S; ++s) {
-    // ops issued after DMA(s): the DMAs of steps s+1 .. min(s+D-1, S-1) and the epilogues of tile-final
-    // steps e in [max(0, s-D), s-1] (DMA(s) was issued during step s-D, before its compute)
-    {
-      const int nd = min(s + D - 1, S - 1) - s;
-      const int lo = s - D > 0 ? s - D : 0;
-      const int ne = s / KS - lo / KS;  // tile-final steps e with lo <= e <= s-1: (e + 1) % KS == 0
-      wait_vmcnt_any(nd * PER + ne * EOPS);
-    }
-    __builtin_amdgcn_s_barrier();
-    if (s + D < S) {
-      int ns = slot + D;
-      ns = ns >= RING ? ns - RING : ns;
-      issue_next(ns);
-    }
-    const char* As = smem + slot * SLOT;
-    const char* Bs = As + TA;
-    {
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int rb = wn * 64 + j * 16 + r;
-        bfr[j] = *(const bf16x8*)(Bs + rb * ROWB + swz64(rb, g) * 16);
-        const int ra = wm * 64 + j * 16 + r;
-        af[j] = *(const bf16x8*)(As + ra * ROWB + swz64(ra, g) * 16);
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    if ((s + 1) % KS == 0) {
-      // tile epilogue in the slot this step just freed (refilled only by DMA(s + RING), issued after the
-      // next step's barrier)
-      __builtin_amdgcn_s_barrier();
-      const int t = jt * G + t0, mb = t / ntn, nb = t - mb * ntn;
-      const int mw0 = mb * TBM + wm * 64, nw0 = nb * TBN + wn * 64;
-      char* stg = (char*)As + w * (8 * EROWB);
-      const int srow = lane >> 3, scol = (lane & 7) * 8;
-      f32x4 b0 = f32x4{0.f, 0.f, 0.f, 0.f}, b1 = b0;
-      if (p.bias) {
-        const float* bl = (const float*)(As + TA + TB) + wn * 64 + scol;
-        b0 = *(const f32x4*)bl;
-        b1 = *(const f32x4*)(bl + 4);
-      }
-      const EpiCtx<EPI> x = epi_ctx<EPI>(p);
-      EpiAuxRegs aux[2];
-      aux[0] = epi_load_aux<EPI>(p, x, mw0 + srow, nw0 + scol);
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const int mi = c >> 1, h = c & 1;
-        if ((r >> 3) == h) {
-#pragma unroll
-          for (int ni = 0; ni < 4; ++ni) *(f32x4*)(stg + (r & 7) * EROWB + (ni * 16 + 4 * g) * 4) = acc[mi][ni];
-        }
-        __builtin_amdgcn_wave_barrier();
-        const f32x4 v0 = *(const f32x4*)(stg + srow * EROWB + scol * 4);
-        const f32x4 v1 = *(const f32x4*)(stg + srow * EROWB + scol * 4 + 16);
-        __builtin_amdgcn_wave_barrier();
-        if (c + 1 < 8) aux[(c + 1) & 1] = epi_load_aux<EPI>(p, x, mw0 + (c + 1) * 8 + srow, nw0 + scol);
-        epi_store8<EPI, STAUX>(p, x, mw0 + c * 8 + srow, nw0 + scol, v0 + b0, v1 + b1, aux[c & 1]);
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      ++jt;
-    }
-    slot = slot + 1 == RING ? 0 : slot + 1;
-  }
-}
-
 // v0 family: 128x128 output tile, 4 waves (2x2, 64x64 each), K step BKT in {32, 64}, NST-stage
 // LDS ring.  Stage k+NST-1 is issued right after the barrier that publishes stage k; the wait
 // for stage k is a counted vmcnt (the younger stages' glds stay in flight), the barrier a raw
@@ -1288,12 +1113,9 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   if (cfg == 11 && epi == EPI_F32_RESID) NT_LAUNCH(EPI_F32_RESID, 64, 2, 64, 0)
   switch (cfg) {
     case 0: NT_EPIS(64, 2, 128)
-    case 3: NT_EPIS(32, 4, 128)
-    case 4: NT_EPIS(64, 3, 128)
     case 5: NT_EPIS(32, 2, 128)
     case 11: NT_EPIS(64, 2, 64)
-    case 12: NT_EPIS(32, 3, 64)
-    default: NT_EPIS(32, 3, 128)
+    default: NT_EPIS(32, 3, 128)  // 2
   }
 }
 #undef NT_EPIS
@@ -1322,20 +1144,10 @@ int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   }
 #define BIG_EPIS(WM_, MF_, NF_, NST_, BKT_) BIG_EPIS2(WM_, MF_, NF_, NST_, BKT_, 1)
 int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
-  if (cfg >= 13 && cfg <= 17 && epi == EPI_BF16) {  // probes of variant 10 (plain epilogue only)
-    if (cfg == 13) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 1)
-    if (cfg == 14) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 2)
-    if (cfg == 16) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 4)
-    if (cfg == 17) BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 5)
-    BIG_LAUNCH(EPI_BF16, 4, 4, 4, 3, 32, 4, 3)
-  }
   if (cfg == 10 && epi == EPI_F32_RESID) BIG_LAUNCH(EPI_F32_RESID, 4, 4, 4, 3, 32, 4, 0, 0)  // plain stores
   switch (cfg) {
     case 10: BIG_EPIS2(4, 4, 4, 3, 32, 4)  // 256x128, BK32, 3 stages (72 KiB), two workgroups per CU
-    case 6: BIG_EPIS(2, 8, 4, 2, 64)   // 256x256, BK64, 2 stages (128 KiB)
-    case 7: BIG_EPIS(2, 8, 3, 2, 64)   // 256x192, BK64, 2 stages (112 KiB)
-    case 9: BIG_EPIS(2, 8, 3, 4, 32)   // 256x192, BK32, 4 stages
-    default: BIG_EPIS(2, 8, 4, 4, 32)  // 8: 256x256, BK32, 4 stages
+    default: BIG_EPIS(2, 8, 4, 2, 64)      // 6: 256x256, BK64, 2 stages (128 KiB)
   }
 }
 #undef BIG_EPIS
@@ -1355,6 +1167,10 @@ extern "C" {
 
 int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                   float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream);
+
+// gemm_panel.hip: the activation-stationary K = 384 kernel (variant 30)
+int es_panel_gemm(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
+                  void* C2, const void* aux, int ldaux, int M, int N, int K, int stores_nt, hipStream_t stream);
 
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C,
                int ldc, void* C2, const void* aux, int ldaux, int M, int N, int K, int np,
@@ -1428,45 +1244,18 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
-  if (variant >= 21 && variant <= 24) {
-    // 21 / 22: six-slot ring, one workgroup per CU (plain / nt C stores); 23 / 24: three-slot rings, two
-    // workgroups per CU
-    if (N % 128 || K % 32) return ES_BAD_SHAPE;
-    const int tiles = ((M + 255) / 256) * (N / 128);
-    const int per_cu = variant >= 23 ? 2 : 1;
-    const int grid = std::min(256 * per_cu, (tiles + 7) / 8 * 8);
-#define RL(E, R, X, O)                                                                                    \
-    {                                                                                                   \
-      const size_t lds = (size_t)R * (256 * 64 + 128 * 64 + 128 * 4);                                     \
-      allow_lds(gemm_nt_ring_kernel<E, R, X, O>, lds);                                                    \
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_ring_kernel<E, R, X, O>), grid, 512, lds, stream, a);    \
-    }                                                                                                   \
-    break;
-#define RLE(R, X, O)                                 \
-    switch (epi) {                                   \
-      case EPI_BF16: RL(EPI_BF16, R, X, O)           \
-      case EPI_GELU: RL(EPI_GELU, R, X, O)           \
-      case EPI_F32_RESID: RL(EPI_F32_RESID, R, X, O) \
-      case EPI_DGELU: RL(EPI_DGELU, R, X, O)         \
-      case EPI_F32: RL(EPI_F32, R, X, O)             \
-      case EPI_PATCH: RL(EPI_PATCH, R, X, O)         \
-      case EPI_GELU_ACT: RL(EPI_GELU_ACT, R, X, O)   \
-      case EPI_GELU_D: RL(EPI_GELU_D, R, X, O)       \
-      case EPI_MULAUX: RL(EPI_MULAUX, R, X, O)       \
-      default: return ES_BAD_ARG;                    \
-    }
-    if (variant == 21) { RLE(6, 0, 1) } else if (variant == 22) { RLE(6, 2, 1) }
-    else if (variant == 23) { RLE(3, 0, 2) } else { RLE(3, 2, 2) }
-#undef RLE
-#undef RL
-    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  if (variant == 30 || variant == 31) {  // 31: plain C stores
+    const int rc = es_panel_gemm(epi, A, lda, B, ldb, bias, C, ldc, C2, aux, ldaux, M, N, K, variant == 30, stream);
+    if (rc != ES_BAD_SHAPE) return rc;
+    variant = 0;
   }
-  if ((variant >= 6 && variant <= 10) || (variant >= 13 && variant <= 17)) {
-    const int tbn = (variant == 6 || variant == 8) ? 256 : ((variant == 10 || variant >= 13) ? 128 : 192);
+  if (variant == 6 || variant == 10) {
+    const int tbn = variant == 6 ? 256 : 128;
     if (N % tbn) return ES_BAD_SHAPE;
     return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
   }
-  const int tbm = (variant == 11 || variant == 12) ? 64 : BM;
+  if (variant != 0 && variant != 2 && variant != 5 && variant != 11) variant = 0;  // unknown pins
+  const int tbm = variant == 11 ? 64 : BM;
   const int grid = ((M + tbm - 1) / tbm) * (N / BN);
   const int rc = launch_nt(variant, epi, grid, stream, a);
   if (rc) return rc;
@@ -1495,17 +1284,18 @@ int es_set_gemm_small_tile(int v) {
   return old;
 }
 
-// Tuning knob for es_gemm_tn: -1 = default, 0..4 = 128x128 tile with (token step, ring depth) in
-// {32x2, 32x3, 32x4, 64x2, 64x3}, 5..7 = 384x192 tile with 32x2, 32x3, 64x2 (shapes that do not
-// tile fall back to 0).  Returns the previous value.
+// Tuning knob for es_gemm_tn: -1 = default, 0 = the 128x128 tile (32-token steps, two stages), 7 = the
+// 384x192 tile (64-token steps, two stages; shapes that do not tile fall back to 0).  A pin (>= 0) also
+// overrides the variant es_gemm_tn_ex callers name.  Returns the previous value.  (The other ring depths
+// and step sizes were measured slower and removed in round 4.)
 int es_set_tn_variant(int v) {
   const int old = g_tn_variant;
   g_tn_variant = v;
   return old;
 }
 
-// es_gemm_tn kernel choice and split-K sizing (splits <= 0: auto).  Kernels: 0..4 the 128 x 128
-// four-wave tile, 5..8 the 384 x 192 eight-wave tile (where the shape tiles).  Auto: the big tile
+// es_gemm_tn kernel choice and split-K sizing (splits <= 0: auto).  Kernels: 0 the 128 x 128
+// four-wave tile, 7 the 384 x 192 eight-wave tile (where the shape tiles).  Auto: the big tile
 // for long token axes (M >= 65536: 15-25 % faster alone at the F1 shapes, scripts/gemm_bench.py),
 // the 128 x 128 tile below that (more tiles to spread a short axis over).  Splits: enough
 // workgroups to fill the chip (target), but at least TN_MIN_SPLIT_TOKENS tokens per split -- each
@@ -1519,12 +1309,12 @@ static bool tn_big_ok(int N1, int N2, int ld1, int ld2) {
 }
 static int tn_pick(int M, int N1, int N2, int ld1, int ld2, int v) {
   if (!(N1 % BM == 0 && N2 % BN == 0)) return 7;  // only the big tile covers N2 = 192 (caller checked)
-  if (v >= 5 && v <= 13) return tn_big_ok(N1, N2, ld1, ld2) ? v : 0;
-  if (v >= 0) return v;
+  if (v == 7) return tn_big_ok(N1, N2, ld1, ld2) ? 7 : 0;
+  if (v >= 0) return 0;
   return (tn_big_ok(N1, N2, ld1, ld2) && M >= 65536) ? 7 : 0;
 }
-static int tn_target(int v) { return v == 5 ? 512 : (v >= 6 ? 256 : 768); }
-static int tn_tiles(int v, int N1, int N2) { return v >= 5 ? (N1 / TB1) * (N2 / TB2) : (N1 / BM) * (N2 / BN); }
+static int tn_target(int v) { return v == 7 ? 256 : 768; }
+static int tn_tiles(int v, int N1, int N2) { return v == 7 ? (N1 / TB1) * (N2 / TB2) : (N1 / BM) * (N2 / BN); }
 static int tn_auto_splits(int v, int M, int N1, int N2) {
   const int by_fill = std::max(1, tn_target(v) / tn_tiles(v, N1, N2));
   const int by_len = std::max(1, M / TN_MIN_SPLIT_TOKENS);
@@ -1547,18 +1337,16 @@ int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, 
 }
 
 // es_gemm_tn with the kernel chosen by the caller (variant >= 0, as es_set_tn_variant; shapes the
-// chosen tile does not cover fall back as there) instead of the process-wide knob (variant -1):
-// no global state changes, so concurrent launchers never see each other's choice.
+// chosen tile does not cover fall back as there) instead of the default (variant -1); a process-wide pin
+// (es_set_tn_variant >= 0, an A/B run) wins over the caller's choice.
 int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                   float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream) {
   if (M <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!tn_big_ok(N1, N2, ld1, ld2) && ((N1 % BM) || (N2 % BN))) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
   if (variant > 13) return ES_BAD_ARG;
-  // variant: 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3;
-  // 5..7 = 384x192 tile with 32x2 (72 KiB: two workgroups per CU), 32x3, 64x2
-  const int v = tn_pick(M, N1, N2, ld1, ld2, variant >= 0 ? variant : g_tn_variant);
-  const int BKM = (v == 3 || v == 4 || v == 7 || v == 9 || v == 10 || v == 11) ? 64 : 32;  // (8: 384x192, 32x4)
+  const int v = tn_pick(M, N1, N2, ld1, ld2, g_tn_variant >= 0 ? g_tn_variant : variant);
+  const int BKM = v == 7 ? 64 : 32;
   const int msteps = (M + BKM - 1) / BKM;
   if (splits <= 0) splits = tn_auto_splits(v, M, N1, N2);
   splits = std::min(splits, msteps);
@@ -1582,21 +1370,8 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
     hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_kernel<BKM_, NST_, ASM_, ##__VA_ARGS__>), dim3(grid), dim3(512), lds, stream, a); \
   }
   switch (v) {
-    case 0: TN_LAUNCH(32, 2) break;
-    case 1: TN_LAUNCH(32, 3) break;
-    case 3: TN_LAUNCH(64, 2) break;
-    case 4: TN_LAUNCH(64, 3) break;
-    case 2: TN_LAUNCH(32, 4) break;
-    case 5: TNB_LAUNCH(32, 2, true) break;
-    case 6: TNB_LAUNCH(32, 3, true) break;
     case 7: TNB_LAUNCH(64, 2, true) break;
-    case 8: TNB_LAUNCH(32, 4, true) break;
-    case 9: TNB_LAUNCH(64, 2, false) break;  // A/B: the builtin transposed reads (compiler-drained prefetch)
-    case 10: TNB_LAUNCH(64, 2, true, 1) break;  // probes: operand stream alone / MFMAs alone
-    case 11: TNB_LAUNCH(64, 2, true, 2) break;
-    case 12: TNB_LAUNCH(32, 4, true, 1) break;
-    case 13: TNB_LAUNCH(32, 4, true, 2) break;
-    default: TN_LAUNCH(32, 2) break;
+    default: TN_LAUNCH(32, 2) break;  // 0
   }
 #undef TN_LAUNCH
 #undef TNB_LAUNCH

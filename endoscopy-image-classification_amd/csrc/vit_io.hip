@@ -62,42 +62,6 @@ __global__ void im2col_u8_kernel(const uint8_t* __restrict__ img, bf16* __restri
   }
 }
 
-// The same gather one (image, patch row) per workgroup: the 3 x P image rows of the patch row come into LDS
-// as whole-row 8-byte loads (coalesced; the per-element kernel above reads 8 bytes of 32 different image rows
-// per wave instruction), then the patch row's G x K outputs -- one contiguous stretch of `out` -- leave as
-// 16-byte stores.  Same per-element arithmetic: bit-identical.  S % 8 == 0, 3 * P * S bytes of LDS.
-template <int P>
-__global__ __launch_bounds__(256) void im2col_u8_rows_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out,
-                                                             int n, int S, ChanNorm nm) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t rows[];  // [3][P][S]
-  const int G = S / P, K = 3 * P * P, W8 = S / 8;
-  for (int b = blockIdx.x; b < n * G; b += gridDim.x) {
-    const int im = b / G, py = b - im * G;
-    __syncthreads();  // the previous patch row's reads of `rows` are done
-    for (int i = threadIdx.x; i < 3 * P * W8; i += blockDim.x) {
-      const int r = i / W8, w = i - r * W8, c = r / P, ky = r - c * P;
-      const uint2 v = *(const uint2*)(img + (((size_t)im * 3 + c) * S + py * P + ky) * S + w * 8);
-      *(uint2*)(rows + r * S + w * 8) = v;
-    }
-    __syncthreads();
-    bf16* orow = out + (size_t)b * G * K;  // patches (im, py, 0 .. G-1) are consecutive rows of `out`
-    for (int i = threadIdx.x; i < G * (K / 8); i += blockDim.x) {
-      const int px = i / (K / 8), k = (i - px * (K / 8)) * 8;
-      const int c = k / (P * P), ky = (k / P) % P, kx = k % P;
-      const uint2 raw = *(const uint2*)(rows + (c * P + ky) * S + px * P + kx);
-      const float mu = c == 0 ? nm.mean[0] : (c == 1 ? nm.mean[1] : nm.mean[2]);
-      const float sd = c == 0 ? nm.std[0] : (c == 1 ? nm.std[1] : nm.std[2]);
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const unsigned v = ((j < 4 ? raw.x : raw.y) >> (8 * (j & 3))) & 255u;
-        o[j] = (bf16)(((float)v / 255.0f - mu) / sd);
-      }
-      *(bf16x8*)(orow + (size_t)px * K + k) = o;
-    }
-  }
-}
-
 // x[img*T + 0][d] = cls[d] + pos[0][d]
 __global__ void cls_init_kernel(float* __restrict__ x, int ldx, const float* __restrict__ cls,
                                 const float* __restrict__ pos, int n, int T, int D) {
@@ -331,13 +295,6 @@ __global__ __launch_bounds__(256) void cls_ln_bwd_kernel(const float* __restrict
 
 extern "C" {
 
-// es_patch_im2col_u8's kernel: 1 = one (image, patch row) per workgroup through LDS, 0 = per element (the
-// default; ENDOSSL_IM2COL_ROWS=1 selects the row kernel)
-static int g_im2col_rows = [] {
-  const char* e = getenv("ENDOSSL_IM2COL_ROWS");
-  return e ? atoi(e) : 0;
-}();
-
 int es_patch_im2col(const float* img, void* patches, int n, int S, int P, hipStream_t stream) {
   if (n <= 0 || P != 16 || S % P) return ES_BAD_SHAPE;
   if (!img || !patches) return ES_BAD_ARG;
@@ -356,12 +313,6 @@ int es_patch_im2col_u8(const void* img, float mean0, float mean1, float mean2, f
   long grid = (total + 255) / 256;
   if (grid > 65536) grid = 65536;
   const ChanNorm nm{{mean0, mean1, mean2}, {std0, std1, std2}};
-  if (g_im2col_rows && S % 8 == 0 && 3 * P * S <= 48 * 1024) {
-    const long blocks = (long)n * (S / P);
-    hipLaunchKernelGGL(im2col_u8_rows_kernel<16>, (int)(blocks < 65536 ? blocks : 65536), 256, 3 * P * S, stream,
-                       (const uint8_t*)img, (bf16*)patches, n, S, nm);
-    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-  }
   hipLaunchKernelGGL(im2col_u8_kernel<16>, (int)grid, 256, 0, stream, (const uint8_t*)img, (bf16*)patches, n, S, nm);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }

@@ -40,11 +40,7 @@ SIGNATURES = {
     "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
     "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
     "es_attn_bwd": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),
-    "es_attn_bwd_dq": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),
-    "es_attn_bwd_dkv": (I, [V, I, V, I, V, V, I, V, I, I, I, I, F, V]),
     "es_attn_cls_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
-    "es_mlp_fwd_infer": (I, [V, I, V, V, V, V, V, I, V, I, I, I, I, V]),
-    "es_pack_chunk32": (I, [V, V, I, I, V]),
     "es_attn_cls_bwd": (I, [V, I, V, I, V, V, I, V, I, I, I, I, F, V]),
     "es_reduce_partials": (I, [V, V, I, I, I, V]),
     "es_layernorm_fwd": (I, [V, I, V, V, V, I, V, V, I, I, F, V]),
@@ -194,12 +190,9 @@ def load(path=None):
         fn.argtypes = args
     if lib.es_abi_version() != ABI_VERSION:
         raise EndosslLibraryError(f"ABI mismatch: library {lib.es_abi_version()} != python {ABI_VERSION}")
-    # kernel-family knobs for A/B runs (scripts/, bench.py): ENDOSSL_TN_VARIANT / ENDOSSL_GEMM_VARIANT /
-    # ENDOSSL_ATTN_VARIANT
-    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"), ("ENDOSSL_SMALL_TILE", "es_set_gemm_small_tile"),
-                    ("ENDOSSL_ATTN_VARIANT", "es_set_attn_variant"),
-                    ("ENDOSSL_ATTN_BWD_VARIANT", "es_set_attn_bwd_variant"), ("ENDOSSL_ATTN_BWD_LONG", "es_set_attn_bwd_long"),
-                    ("ENDOSSL_STEM_KERNELS", "es_set_stem_kernels")):
+    # kernel-family pins for A/B runs (scripts/): ENDOSSL_GEMM_VARIANT / ENDOSSL_TN_VARIANT (the other
+    # es_set_* knobs are reached through the library handle)
+    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant")):
         if os.environ.get(env):
             getattr(lib, fn)(int(os.environ[env]))
     if path is None:

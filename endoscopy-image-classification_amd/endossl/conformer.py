@@ -14,8 +14,10 @@ MI355X-first layout:
     whose channel counts are multiples of 32, on bf16 operands: every conv of Conformer-B but the
     3-channel stem; set_conv_precision("fp32") is the parity mode).  When every conv after the stem
     takes the bf16 kernels (Conformer-B: map_bf16) the activation AND gradient maps after the stem's
-    max-pool are bf16 (torch autocast's dtypes for the reference's conv / BatchNorm chain), BatchNorm
-    statistics and every reduction in fp32; otherwise fp32 maps; the transformer branch is a
+    max-pool are bf16 -- this repo's own bf16-storage contract: the reference runs its conv / BatchNorm
+    chain in fp32 (no autocast); parity for it is per conv against the bf16-rounded-operand contract
+    (tests/test_gpu_convs.py) and ENDOSSL_MAP_BF16=0 keeps fp32 maps --, BatchNorm statistics and every
+    reduction in fp32; otherwise fp32 maps; the transformer branch is a
     [tokens, D] fp32 residual stream padded to 256 rows (zero pad) and runs on the same bf16 MFMA
     kernels as the ViT (gemm / attention / layernorm); the FCU bridges read and write token rows
     in place through element strides (no transposes);
@@ -171,7 +173,7 @@ def _s():
 # such launch of a backward pass queues an autograd final callback that makes the backward's stream
 # wait for the side stream, so whatever runs after `backward()` returns (the all-reduce, the
 # optimizer, a test reading .grad) sees complete gradients.
-CONV_DW_SIDE = os.environ.get("ENDOSSL_CONV_DW_SIDE", "1") != "0"
+CONV_DW_SIDE = True
 _wgrad_streams = {}
 _join_queued = set()
 
@@ -193,7 +195,7 @@ def _queue_join(main, side):
 # after the cnn_block's conv2 / bn2 produce x2, FCUDown -> transformer block -> FCUUp run on the
 # branch stream while the cnn_block's conv3 / residual / bn3 tail runs on the caller's stream; the
 # fusion block joins them (code/models/conformer.py:334-357 data flow, unchanged arithmetic).
-BRANCH_STREAMS = os.environ.get("ENDOSSL_BRANCH_STREAMS", "1") != "0"
+BRANCH_STREAMS = True
 _branch_streams = {}
 
 
@@ -256,38 +258,7 @@ class _Map:
 
 # share of the CUs the transformer blocks' overlapped weight gradients are sized to (Engine.TN_SHARE's
 # counterpart; 1 = the library's whole-chip sizing): S1 195.46 / 195.46 -> 193.26 / 193.38 ms same-box A/B)
-CONF_TN_SHARE = float(os.environ.get("ENDOSSL_CONF_TN_SHARE", "0.5"))
-
-
-# A transformer block's four weight gradients (fc2, fc1, proj, qkv: 96 tiles of 384 x 192 at
-# Conformer-B) as ONE launch on the weight-gradient stream at the end of the block's backward
-# (es_gemm_tn_big_grouped, as the ViT engine's Engine.LAYER_WGRAD) instead of four split-K launches with
-# their slab and bias reductions; at the CU share's 128 workgroups every GEMM gets one split, written in
-# place.  Measured at S1 (same box): 152.8 ms (CU share 0.5) / 152.5 (0.75) vs 151.9 ms with the per-GEMM
-# launches -- S1's weight gradients are off its critical path beside the two branch streams, so this stays
-# opt-in (ENDOSSL_CONF_LAYER_WGRAD=1).
-LAYER_WGRAD = os.environ.get("ENDOSSL_CONF_LAYER_WGRAD", "0") == "1"
-
-
-def _tn_block(lib, problems, M, gv, dev):
-    """One es_gemm_tn_big_grouped launch (+ reduce, when a GEMM gets more than one split) on the current
-    stream over [(dy, N1, x, N2, weight name, bias name)], sized to CONF_TN_SHARE of the CUs."""
-    from .vit import _TNProblem
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    target = max(1, int(ncu * CONF_TN_SHARE))
-    n = len(problems)
-    tab = (_TNProblem * n)()
-    for e, (dy, N1, x, N2, wname, bname) in zip(tab, problems):
-        e.dy, e.x, e.out, e.bias_out = ptr(dy), ptr(x), ptr(gv(wname)), ptr(gv(bname))
-        e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, N1, N2
-    need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), n, target)
-    ws = torch.empty(max(1, need), device=dev)
-    raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(n))
-    dims = (ctypes.c_int * 3)()
-    rc = lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), n, target, ptr(ws), ws.numel(), raw, dims)
-    if rc != 0:
-        raise _lib.EndosslLibraryError(f"es_gemm_tn_big_grouped_prepare: status {rc}")
-    call("es_gemm_tn_big_grouped", raw, n, dims, _s())
+CONF_TN_SHARE = 0.5
 
 
 def _tn_splits(M, N1, N2):
@@ -301,11 +272,11 @@ def _tn_splits(M, N1, N2):
 CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
 # train-mode BatchNorm statistics of a bf16 conv's output computed in the conv's epilogue
 # (es_conv2d_fwd_bf16_bnstats -> es_bn2d_fwd_partials): no two statistics passes over the map
-BN_STATS_FUSED = os.environ.get("ENDOSSL_BN_STATS_FUSED", "1") != "0"
+BN_STATS_FUSED = True
 # a ConvBlock input's two gradient contributions (conv1, residual) summed in place (_GradSink)
-GRAD_SINKS = os.environ.get("ENDOSSL_GRAD_SINKS", "1") != "0"
+GRAD_SINKS = True
 # ... and the token buffer's two consumers (a block's FCUUp conv, the next block's FCUDown), _trans_branch
-TOKEN_SINK = os.environ.get("ENDOSSL_TOKEN_SINK", "1") != "0"
+TOKEN_SINK = True
 # bf16 activation / gradient maps in the CNN branch when every conv after the stem runs on conv_bf16.hip
 # (NativeConformer.map_bf16); ENDOSSL_MAP_BF16=0 keeps fp32 maps with bf16 conv operands
 MAP_BF16 = os.environ.get("ENDOSSL_MAP_BF16", "1") != "0"
@@ -802,12 +773,7 @@ class _BlockFn(torch.autograd.Function):
         wt, pv, gv = m.wt, m.pview, m.gview
         ws_ln = torch.empty(2 * 1024 * D, device=dev)
 
-        lp = []  # LAYER_WGRAD: this block's weight gradients, one grouped launch at the end
-
         def wgrad(dy, N1, x, N2, wname, bname):
-            if LAYER_WGRAD and side is not None and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
-                lp.append((dy, N1, x, N2, wname, bname))
-                return
             sp = _tn_splits(M, N1, N2)
             if side is not None and CONF_TN_SHARE < 1.0 and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
                 # beside the branch streams: the 384 x 192 tile on a share of the CUs (as Engine.TN_SHARE)
@@ -848,10 +814,6 @@ class _BlockFn(torch.autograd.Function):
         call("es_layernorm_bwd_b16", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
-        if lp:
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                _tn_block(lib, lp, M, gv, dev)
         if side is not None:
             for t in (act, h2, o, h1):  # saved activations the side stream still reads
                 t.record_stream(side)

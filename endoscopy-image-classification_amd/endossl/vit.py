@@ -221,90 +221,54 @@ class _TNProblem(ctypes.Structure):
 class Engine:
     """Explicit forward / backward of the ViT over C-ABI kernels.  One per (model, device)."""
 
+    # Kernel-choice and overlap settings.  Class attributes (tests override them per instance); the
+    # measured A/Bs behind each value are in DESIGN.md §5.  Paths measured slower were removed in round 4
+    # (two-lane backward, fused inference MLP, split attention backward): their record stays in DESIGN.md.
+    #
     # split-K sizing of the weight-gradient GEMMs: floor(TN_TARGET_BLOCKS / tiles) splits, so the grid
-    # never exceeds the target (a ceil left 792 workgroups for 768, and 24 CUs holding one more).
-    # Alone, the whole-chip fill (1024 = 4 workgroups per CU, the kernel's register-limited residency)
-    # is fastest (scripts/gemm_bench.py: fc2 / fc1 / qkv 175 / 169 / 132 us vs 212 / 182 / 138 at
-    # floor 768); inside the F1 step, where the weight gradients share the CUs with the data-gradient
-    # chain on the other stream, 768 leaves the chain room: 35.10-35.13 ms/step vs 35.41-35.43 (1024),
-    # 35.39 (640), 35.99 (512); C1 prefers 1024 (73.9 vs 74.2 ms).  The split count is capped so the
-    # slabs stay small for the 384x384 projection.
-    TN_TARGET_SET = "ENDOSSL_TN_TARGET" in os.environ
-    TN_TARGET_BLOCKS = int(os.environ.get("ENDOSSL_TN_TARGET", "768"))
-    # share of the CUs the overlapped long-axis weight-gradient launches are sized to (1 = the whole
-    # chip, the library's sizing).  Half: the 384 x 192 tile's 147-KiB workgroups otherwise hold every
-    # CU's LDS and the data-gradient chain's launches wait for CUs; F1 34.43 / 34.36 -> 33.66 / 33.84
-    # ms (same-box A/B, 0.375 of the CUs: 35.03 / 35.11)
-    TN_SHARE = float(os.environ.get("ENDOSSL_TN_SHARE", "0.5"))
-    TN_SHARE_MIN_M = int(os.environ.get("ENDOSSL_TN_SHARE_MIN_M", "16384"))  # shortest token axis it applies to
-    TN_CEIL = os.environ.get("ENDOSSL_TN_CEIL", "0") == "1"  # A/B knob: the earlier ceil sizing
+    # never exceeds the target (768 leaves the data-gradient chain on the other stream room: 35.10-35.13
+    # ms/step vs 35.41-35.43 at 1024, 35.99 at 512, r01).
+    TN_TARGET_BLOCKS = 768
+    # share of the CUs the overlapped long-axis weight-gradient launches are sized to (half: the 384 x 192
+    # tile's 147-KiB workgroups otherwise hold every CU's LDS; F1 34.43 / 34.36 -> 33.66 / 33.84 ms, r02)
+    TN_SHARE = 0.5
+    TN_SHARE_MIN_M = 16384  # shortest token axis it applies to
     TN_MAX_SPLITS = 128
+    # Weight gradients of a small shard (strong scaling: M = 12,608 train tokens per rank at N = 8) as ONE
+    # grouped launch per GROUP_LAYERS layers after the data-gradient chain (es_gemm_tn_grouped: every
+    # 128x128 tile over its GEMM's whole token axis -- no split-K slabs): B=8 6.11-6.15 vs 6.35 ms/step.
+    # "auto": when the train tokens M < GROUP_WGRAD_MAX_M; "1" always; "0" never.  bf16 engines only.
+    GROUP_WGRAD = "auto"
+    GROUP_WGRAD_MAX_M = 16384
+    GROUP_LAYERS = 6
+    # A block's long-axis weight gradients (fc2, fc1, proj, qkv: 24 tiles of 384 x 192 at ViT-S) as ONE
+    # split-K launch on the side stream once the block's data-gradient chain has produced its last dY
+    # (es_gemm_tn_big_grouped) plus one reduce launch, sized to LAYER_TN_SHARE of the CUs (4 splits):
+    # F1 31.53 -> 31.0 ms, C1 67.2 -> 66.8 (r03).
+    LAYER_WGRAD = True
+    LAYER_TN_SHARE = 0.375
     # second HIP stream: the weak forward beside the train forward ("fwd") and the weight-gradient
     # GEMMs beside the data-gradient chain ("bwd"); ENDOSSL_OVERLAP=0 serialises everything on the
-    # caller's stream
-    # Weight gradients of a small shard (strong scaling: M = 12,608 train tokens per rank at N = 8) as ONE
-    # grouped launch after the data-gradient chain (es_gemm_tn_grouped: every 128x128 tile over its
-    # GEMM's whole token axis -- no split-K slabs, no per-GEMM reductions) instead of split-K launches
-    # on the side stream; the first half of the layers' launch overlaps the rest of the chain.
-    # Measured (bench.py --batch B, one MI355X, ms/step grouped vs split-K): B=8 6.11-6.15 vs 6.35;
-    # B=16 10.44 vs 10.34; B=32 19.41 vs 18.79; launches every 2 / 4 / 6 / 12 layers at B=8: 6.88 /
-    # 6.36 / 6.14 / 6.22.  "auto": when the train tokens M < GROUP_WGRAD_MAX_M (the N=8 shard of F1,
-    # M = 12,608); "1" always; "0" never.  bf16 engines only (no fp32 twin).
-    GROUP_WGRAD = os.environ.get("ENDOSSL_GROUP_WGRAD", "auto")
-    GROUP_WGRAD_MAX_M = 16384
-    GROUP_LAYERS = int(os.environ.get("ENDOSSL_GROUP_LAYERS", "6"))  # layers per grouped launch
-    # A block's long-axis weight gradients (fc2, fc1, proj, qkv: 8 + 8 + 2 + 6 = 24 tiles of 384 x 192 at
-    # ViT-S) as ONE split-K launch on the side stream once the block's data-gradient chain has produced
-    # its last dY (es_gemm_tn_big_grouped), plus one reduce launch over the block's slabs and bias
-    # partials -- instead of four GEMM launches (16-32 splits each at the F1 batch), four slab
-    # reductions and four bias reductions.  A grid sized to the granted CUs needs only a few splits per
-    # GEMM when the block's 24 tiles share it: the fc1 site's fp32 slab traffic drops from 75.5 MB
-    # (16 splits) to 23.6 MB (5 splits) per step layer.  ENDOSSL_LAYER_WGRAD=0: the per-GEMM launches.
-    # Sized to 3/8 of the CUs (96 workgroups = 4 splits of the 24 tiles): same-box F1 sweep, two rounds each,
-    # ms/step at share 0.25 / 0.3125 / 0.375 / 0.4375 / 0.5 = 36.8 / 31.5 / 31.0 / 31.0 / 31.5 (2 / 3 / 4 /
-    # 4 / 5 splits) vs 31.53 with the per-GEMM launches; C1 66.8 vs 67.2, the N = 2 shard 16.53 vs 16.99.
-    LAYER_WGRAD = os.environ.get("ENDOSSL_LAYER_WGRAD", "1") == "1"
-    LAYER_TN_SHARE = float(os.environ.get("ENDOSSL_LAYER_TN_SHARE", "0.375"))
+    # caller's stream (a diagnostic: step_timeline / single-stream kernel tables)
     _OV = os.environ.get("ENDOSSL_OVERLAP", "1")
     OVERLAP_FWD = _OV in ("1", "fwd")
     OVERLAP = _OV in ("1", "bwd")
-    # two-lane backward (with OVERLAP): the train batch's images are split in halves and each half's
-    # reverse pass -- its data-gradient chain AND its own weight gradients -- runs on its own HIP
-    # stream, so the two streams carry equal work (the single-lane split, chain vs weight gradients,
-    # leaves the chain stream ~2x busier).  Lane 1 writes a second flat gradient, summed into the
-    # first at the end.  Used when each half's token and patch rows are multiples of 256 (every
-    # half-batch buffer is then an exact GEMM-tile view).  Off by default (ENDOSSL_LANES=2 turns it
-    # on): at F1 it balances the streams (35.4 / 33.9 ms of kernels) but the step gets slower, 40.2
-    # vs 39.1 ms -- the chip is throughput-bound, co-running kernels each take ~2x as long, and the
-    # single-lane split keeps the weight-gradient GEMMs (the most MFMA-dense work) off the chain.
-    LANES = int(os.environ.get("ENDOSSL_LANES", "1"))
-    # d(LN output) from the fc1 / qkv dgrad GEMMs in bf16 (ENDOSSL_DH_BF16=0: fp32) -- every GEMM
-    # operand of the backward is bf16 already; halves those epilogues' writes and the LN-backward reads
-    DH_BF16 = os.environ.get("ENDOSSL_DH_BF16", "1") == "1"
+    # d(LN output) from the fc1 / qkv dgrad GEMMs in bf16 -- every GEMM operand of the backward is bf16
+    # already; halves those epilogues' writes and the LN-backward reads
+    DH_BF16 = True
     # the train fc1 forward stores GELU'(pre) instead of the pre-activation (EPI_GELU_D: shares the
     # erf's exp), so the fc2 dgrad epilogue is one multiply instead of an erf + two exps per element
-    # (EPI_MULAUX); ENDOSSL_GELU_D=0 keeps pre + EPI_DGELU
-    GELU_D = os.environ.get("ENDOSSL_GELU_D", "1") == "1"
+    # (EPI_MULAUX)
+    GELU_D = True
     # the last block on its CLS rows only: timm's head reads x[:, 0] after the last block
     # (VisionTransformer.forward_features / forward_head), so the last block's attention is needed for
     # the CLS queries only (over all keys) and its projection, LayerNorm 2 and MLP for the CLS rows
     # only; in the backward d(loss)/d(non-CLS rows) of the last block's output is exactly zero, so the
-    # skipped rows contribute exactly nothing to any gradient.  ENDOSSL_PRUNE_LAST=0 runs every row.
-    PRUNE_LAST = os.environ.get("ENDOSSL_PRUNE_LAST", "1") == "1"
-    # ... and its Q projection (forward) and Q weight gradient on the CLS rows only (ENDOSSL_PRUNE_Q=0:
-    # all rows, with a dQ that is zero off the CLS rows)
-    PRUNE_Q = os.environ.get("ENDOSSL_PRUNE_Q", "1") == "1"
-    # inference rows (the weak forward): fc1 -> GELU -> fc2 + residual in one kernel
-    # (es_mlp_fwd_infer), the [tokens, 4D] activation never written to HBM.  Off by default
-    # (ENDOSSL_FUSED_MLP=1 turns it on): at the F1 weak shape it takes 0.43 ms vs 0.375 ms for the
-    # two GEMMs -- one wave per SIMD (the fc2 accumulators and the register-resident h rows use
-    # ~420 registers) leaves the LDS-fragment latency exposed (scripts/mlp_bench.py)
-    FUSED_MLP = os.environ.get("ENDOSSL_FUSED_MLP", "0") == "1"
-    # attention backward as two independent launches, dQ on the caller's stream and dK/dV (with its
-    # own delta) on a third stream, joined before the qkv data gradient.  Off by default
-    # (ENDOSSL_ATTN_SPLIT=1): F1 35.00-35.10 vs 34.88-34.95 ms/step in one box -- the chip is already
-    # full with the weight gradients on the side stream
-    ATTN_SPLIT = os.environ.get("ENDOSSL_ATTN_SPLIT", "0") == "1"
+    # skipped rows contribute exactly nothing to any gradient.  False runs every row (tests compare).
+    PRUNE_LAST = True
+    # ... and its Q projection (forward) and Q weight gradient on the CLS rows only (False: all rows,
+    # with a dQ that is zero off the CLS rows)
+    PRUNE_Q = True
 
     # fp32 parity mode (csrc/parity.hip): the same launch sequence over fp32 operand storage; the
     # entry points with an fp32 form, by their bf16 names
@@ -320,8 +284,6 @@ class Engine:
         self.cfg, self.device = cfg, device
         self.precision = precision
         self.op_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
-        if precision == "fp32":  # one lane, the plain launch forms (the opt-in variants have no fp32 form)
-            self.LANES, self.FUSED_MLP, self.ATTN_SPLIT = 1, False, False
         self.layout, self.offs, self.numel = param_layout(cfg)
         self.shapes = dict(self.layout)
         self._acts = {}
@@ -370,8 +332,6 @@ class Engine:
         """C-ABI call; in parity mode the fp32 form of the entry point."""
         if self.precision == "fp32":
             name = self.PARITY_NAMES.get(name, name)
-            if name in ("es_mlp_fwd_infer", "es_attn_bwd_dq", "es_attn_bwd_dkv", "es_pack_chunk32"):
-                raise RuntimeError(f"{name} has no fp32 parity form")
         return call(name, *args)
 
     def _gemm(self, label, *args):
@@ -397,14 +357,6 @@ class Engine:
         if version is not None and version == self._packed_version:
             return
         self._call("es_pack_weights", ptr(flat), ptr(self._pack_tab), self._nmat, _lib.stream())
-        if self.FUSED_MLP:  # chunk-major fc2 images for es_mlp_fwd_infer
-            cfg = self.cfg
-            if not hasattr(self, "_w2c"):
-                self._w2c = {i: torch.zeros(cfg.hidden // 32, cfg.dim, 32, dtype=torch.bfloat16, device=self.device)
-                             for i in range(cfg.depth)}
-            for i in range(cfg.depth):
-                self._call("es_pack_chunk32", ptr(self.wb[f"blocks.{i}.mlp.fc2.weight"]), ptr(self._w2c[i]), cfg.dim,
-                     cfg.hidden, _lib.stream())
         self._packed_version = version if version is not None else -1
 
     def acts(self, n, train):
@@ -433,12 +385,6 @@ class Engine:
         if lane not in self._ws_ln:
             self._ws_ln[lane] = torch.empty(2 * 1024 * self.cfg.dim, dtype=torch.float32, device=self.device)
         return self._ws_ln[lane]
-
-    def attn_stream(self):
-        """Third HIP stream: the dK/dV attention-backward pass beside the dQ pass (ATTN_SPLIT)."""
-        if getattr(self, "_attn_s", None) is None:
-            self._attn_s = torch.cuda.Stream(device=self.device)
-        return self._attn_s
 
     def side_stream(self):
         """The second HIP stream (weak forward beside the train forward; weight gradients beside
@@ -511,13 +457,6 @@ class Engine:
             self._call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
                  ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
                  cfg.eps, s)
-            if not train and self.FUSED_MLP and D in (128, 384) and hasattr(self, "_w2c"):
-                self._call("es_mlp_fwd_infer", ptr(h2), D, ptr(self.wb[b + "mlp.fc1.weight"]),
-                     ptr(self.view(flat, b + "mlp.fc1.bias")), ptr(self._w2c[i]),
-                     ptr(self.view(flat, b + "mlp.fc2.bias")), ptr(xmid), D, ptr(xout), D, M, D, Hd, s)
-                if self.capture is not None:
-                    self.capture("fwd", train, i, xin[:M], xout[:M])
-                continue
             if train:
                 self._gemm("fc1_fwd", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(h2), D,
                            ptr(self.wb[b + "mlp.fc1.weight"]), D,
@@ -547,7 +486,7 @@ class Engine:
     def _prune(self):
         """PRUNE_LAST in effect (read at each forward / backward: tests override it per instance);
         the two-lane backward runs every row."""
-        return self.PRUNE_LAST and self.LANES != 2
+        return self.PRUNE_LAST
 
     def _last_block_cls_fwd(self, flat, A, b, li, xin, n, train, s):
         """The last block after its qkv GEMM, on the CLS rows only (PRUNE_LAST): CLS-query attention
@@ -573,21 +512,15 @@ class Engine:
 
     # -------------------------------------------------------------- backward
     def _tn_splits(self, M, N1, N2):
-        """0 = the library's automatic split-K sizing for the kernel it picks (es_gemm_tn); with
-        ENDOSSL_TN_TARGET set, floor(target / 128x128 tiles) splits (the round-1 sizing).  With the
+        """0 = the library's automatic split-K sizing for the kernel it picks (es_gemm_tn).  With the
         weight gradients overlapped on the side stream and TN_SHARE < 1, the 384 x 192 tile's launches
         are sized to that share of the CUs (the rest stay free for the data-gradient chain)."""
-        if not self.TN_TARGET_SET:
-            if self._tn_shared(M, N1, N2):
-                if self._ncu is None:
-                    self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-                tiles = (N1 // 384) * (N2 // 192)
-                return max(1, int(self._ncu * self.TN_SHARE) // tiles)
-            return 0
-        tiles = (N1 // 128) * (N2 // 128)
-        msteps = (M + 31) // 32
-        sp = -(-self.TN_TARGET_BLOCKS // tiles) if self.TN_CEIL else self.TN_TARGET_BLOCKS // tiles
-        return max(1, min(msteps, self.TN_MAX_SPLITS, sp))
+        if self._tn_shared(M, N1, N2):
+            if self._ncu is None:
+                self._ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+            tiles = (N1 // 384) * (N2 // 192)
+            return max(1, int(self._ncu * self.TN_SHARE) // tiles)
+        return 0
 
     def _tn_shared(self, M, N1, N2):
         """The overlapped weight gradient on the 384 x 192 tile sized to TN_SHARE of the CUs: from the
@@ -605,12 +538,9 @@ class Engine:
         need = getattr(_lib.load(), "es_gemm_tn_f32_workspace" if self.precision == "fp32" else "es_gemm_tn_workspace")
         if need(N1, N2, splits) > ws.numel():
             raise RuntimeError(f"wgrad workspace too small for {N1}x{N2} x {splits} splits")
-        # the CU-share-sized launches name the 384 x 192 tile explicitly (es_gemm_tn_ex); an A/B pin of
-        # the process-wide knob (ENDOSSL_TN_VARIANT) still wins, as before
-        variant = -1
-        if (splits and not self.TN_TARGET_SET and self._tn_shared(M, N1, N2)
-                and not os.environ.get("ENDOSSL_TN_VARIANT")):
-            variant = 7
+        # the CU-share-sized launches name the 384 x 192 tile explicitly (es_gemm_tn_ex); a process-wide
+        # pin (es_set_tn_variant, ENDOSSL_TN_VARIANT) still wins inside the library
+        variant = 7 if splits and self._tn_shared(M, N1, N2) else -1
         args = (ptr(dy), ld1 or N1, ptr(x), ld2 or N2, M, N1, N2, splits, ptr(ws), ptr(out), 0, ptr(bias_out))
         self._wgrad_launch(args, variant, M, N1, N2, label)
 
@@ -749,10 +679,6 @@ class Engine:
                  cfg.num_classes, s)
         if self.capture is not None:
             self.capture("dtop", True, cfg.depth - 1, dtop[:n] if prune else G.dx[:M])
-        nh = n // 2
-        if (not grouped and not prune and ov and self.LANES == 2 and n % 2 == 0 and (nh * T) % 256 == 0
-                and (nh * cfg.np) % 256 == 0 and grad.numel() % 4 == 0):
-            return self._backward_lanes(flat, grad, A, G.dx, nh)
         if prune:
             self._call("es_cast_f32_bf16", ptr(GL.c_dx), ptr(GL.c_dxb), n * D, s)
         else:
@@ -819,18 +745,8 @@ class Engine:
             if cap is not None:
                 cap("b_dxm", True, i, G.dxm[:M], Gi.dxmb[:M])
                 cap("b_do", True, i, G.do[:M])
-            if ov and self.ATTN_SPLIT:
-                s3 = self.attn_stream()
-                s3.wait_stream(main)
-                with torch.cuda.stream(s3):
-                    self._call("es_attn_bwd_dkv", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.do), D,
-                         ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, _lib.stream())
-                self._call("es_attn_bwd_dq", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do),
-                     D, ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
-                main.wait_stream(s3)
-            else:
-                self._call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
-                     ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
+            self._call("es_attn_bwd", ptr(A.qkv[i]), 3 * D, ptr(A.o[i]), D, ptr(A.lse[i]), ptr(G.delta), ptr(G.do), D,
+                 ptr(Gi.dqkv), 3 * D, n, T, H, 64 ** -0.5, s)
             self._call("es_gemm_nt", EPI_DH, ptr(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
                  ptr(G.dh), D, None, None, 0, M, D, 3 * D, 0, s)
             wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
@@ -967,85 +883,6 @@ class Engine:
                    ptr(self.view(grad, "head.bias")), ptr(gnw), ptr(gnb), n, D, C, _lib.stream())
         return grad
 
-    def _backward_lanes(self, flat, grad, A, dx_full, nh):
-        """Two-lane reverse pass (see LANES): lane 0 = images [0, nh) on the caller's stream into
-        `grad`, lane 1 = images [nh, 2 nh) on the side stream into a second flat gradient.  dx_full
-        holds d(loss)/d(final tokens) for all images (head backward already done); each lane's
-        residual-gradient buffer is its disjoint row range of it.  Issue is interleaved per layer so
-        both streams fill from the start."""
-        cfg = self.cfg
-        EPI_DH = EPI_BF16 if self.DH_BF16 else EPI_F32  # noqa: N806
-        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
-        Ml, Pl = nh * T, nh * cfg.np
-        main = torch.cuda.current_stream(self.device)
-        side = self.side_stream()
-        if self._grad_b is None or self._grad_b.numel() != grad.numel():
-            # entries outside the trunk (head, final norm) are never written by a lane: they stay 0
-            self._grad_b = torch.zeros_like(grad)
-        key = nh
-        if key not in self._lane_state:
-            self._lane_state[key] = [_Grads(cfg, nh, self.device, self.op_dtype),
-                                     _Grads(cfg, nh, self.device, self.op_dtype)]
-        lanes = []
-        for ln, (st, g) in enumerate(((main, grad), (side, self._grad_b))):
-            r0 = ln * Ml
-            lanes.append(dict(id=ln, stream=st, grad=g, G=self._lane_state[key][ln], r0=r0, r1=r0 + Ml,
-                              dx=dx_full[r0:r0 + Ml], lse0=ln * nh * H * T, p0=ln * Pl))
-        side.wait_stream(main)  # head backward (dx_full) and the zeroed grad
-        for L in lanes:
-            with torch.cuda.stream(L["stream"]):
-                self._call("es_cast_f32_bf16", ptr(L["dx"]), ptr(L["G"].dxb), Ml * D, _lib.stream())
-        fv = lambda name: self.view(flat, name)  # noqa: E731
-        for i in reversed(range(cfg.depth)):
-            b = f"blocks.{i}."
-            for L in lanes:
-                with torch.cuda.stream(L["stream"]):
-                    s = _lib.stream()
-                    G, ln, r0, r1 = L["G"], L["id"], L["r0"], L["r1"]
-                    gv = lambda name, _g=L["grad"]: self.view(_g, name)  # noqa: E731
-                    pre, act, h2, h1 = A.pre[i][r0:r1], A.act[i][r0:r1], A.h2[i][r0:r1], A.h1[i][r0:r1]
-                    xmid, x, o, qkv = A.xmid[i][r0:r1], A.x[i][r0:r1], A.o[i][r0:r1], A.qkv[i][r0:r1]
-                    m1, s1 = A.mean1[i][r0:r1], A.rstd1[i][r0:r1]
-                    m2, s2 = A.mean2[i][r0:r1], A.rstd2[i][r0:r1]
-                    lse = A.lse[i][L["lse0"]:]
-                    # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
-                    self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, ptr(G.dxb), D,
-                         ptr(self.wt[b + "mlp.fc2.weight"]), D, None,
-                         ptr(G.dpre), Hd, None, ptr(pre), Hd, Ml, Hd, D, 0, s)
-                    self._wgrad(G.dxb, D, act, Hd, Ml, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"), lane=ln)
-                    self._call("es_gemm_nt", EPI_DH, ptr(G.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
-                         ptr(G.dh), D, None, None, 0, Ml, D, Hd, 0, s)
-                    self._wgrad(G.dpre, Hd, h2, D, Ml, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"), lane=ln)
-                    self._ln_bwd(G.dh, xmid, m2, s2, fv(b + "norm2.weight"), L["dx"], G.dxm, G.dxmb,
-                                 gv(b + "norm2.weight"), gv(b + "norm2.bias"), Ml, lane=ln)
-                    # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
-                    self._call("es_gemm_nt", EPI_BF16, ptr(G.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
-                         ptr(G.do), D, None, None, 0, Ml, D, D, 0, s)
-                    self._wgrad(G.dxmb, D, o, D, Ml, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"), lane=ln)
-                    self._call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(G.delta), ptr(G.do), D,
-                         ptr(G.dqkv), 3 * D, nh, T, H, 64 ** -0.5, s)
-                    self._call("es_gemm_nt", EPI_DH, ptr(G.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D,
-                         None, ptr(G.dh), D, None, None, 0, Ml, D, 3 * D, 0, s)
-                    self._wgrad(G.dqkv, 3 * D, h1, D, Ml, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"),
-                                lane=ln)
-                    self._ln_bwd(G.dh, x, m1, s1, fv(b + "norm1.weight"), G.dxm, L["dx"], G.dxb,
-                                 gv(b + "norm1.weight"), gv(b + "norm1.bias"), Ml, lane=ln)
-        K0 = 3 * cfg.patch * cfg.patch
-        for L in lanes:
-            with torch.cuda.stream(L["stream"]):
-                G = L["G"]
-                gv = lambda name, _g=L["grad"]: self.view(_g, name)  # noqa: E731
-                self._call("es_embed_bwd", ptr(L["dx"]), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")),
-                     nh, T, D, 0, _lib.stream())
-                self._wgrad(G.dpatch, D, A.patches[L["p0"]:L["p0"] + Pl], K0, Pl, gv("patch_embed.proj.weight"),
-                            gv("patch_embed.proj.bias"), lane=L["id"])
-        main.wait_stream(side)
-        self._call("es_add_f32", ptr(grad), ptr(self._grad_b), grad.numel(), _lib.stream())
-        return grad
-
-
-class _ViTFunction(torch.autograd.Function):
-    @staticmethod
     def forward(ctx, x, module, *params):
         ctx.module = module
         ctx.n = int(x.shape[0])

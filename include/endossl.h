@@ -118,13 +118,6 @@ int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int ni
 /* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass) */
 int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
                 int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
-/* es_attn_bwd as two independent launches (two streams): the dQ pass (writes delta) and the dK/dV
- * pass computing its own delta = rowsum(dO * O); they write disjoint column ranges of dqkv */
-int es_attn_bwd_dq(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta,
-                   const void* dout, int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale,
-                   hipStream_t stream);
-int es_attn_bwd_dkv(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
-                    void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
 /* CLS-query attention for a block whose non-CLS outputs are unused (the last block: only the CLS
  * token reaches timm's head, VisionTransformer.forward_features x[:, 0]).  o / dout are compact
  * [nimg, ld] CLS rows, lse [nimg*H]; the backward writes dqkv for every token (q part zero off the
@@ -133,16 +126,6 @@ int es_attn_cls_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, in
                     hipStream_t stream);
 int es_attn_cls_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, const void* dout, int lddo,
                     void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
-
-/* ---- fused MLP for inference rows (timm Mlp, code/models/conformer.py:13-23, + the residual add) --
- * out [M, D] fp32 = resid + fc2(gelu(fc1(h))), the [M, Hd] activation never written: the FixMatch
- * weak forward (detached logits, code/loss.py:144) and evaluation.  h bf16 with ceil(M/128)*128
- * readable rows; w1 [Hd, D] bf16, w2c [Hd/32, D, 32] bf16 (fc2.weight [D, Hd] by es_pack_chunk32);
- * D in {128, 384}; Hd % 32 == 0; out != resid. */
-int es_mlp_fwd_infer(const void* h, int ldh, const void* w1, const float* b1, const void* w2c, const float* b2,
-                     const float* resid, int ldr, float* out, int ldo, int M, int D, int Hd, hipStream_t stream);
-/* dst [K/32, N, 32] = src [N, K] bf16 in 32-column chunks; K % 32 == 0 */
-int es_pack_chunk32(const void* src, void* dst, int N, int K, hipStream_t stream);
 
 /* ---- LayerNorm(eps) (code/models/conformer.py:58,60,65) -------------------------------------- */
 int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,
