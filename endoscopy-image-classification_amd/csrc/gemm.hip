@@ -1244,8 +1244,9 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
-  if (variant == 30 || variant == 31) {  // 31: plain C stores
-    const int rc = es_panel_gemm(epi, A, lda, B, ldb, bias, C, ldc, C2, aux, ldaux, M, N, K, variant == 30, stream);
+  if (variant == 30 || variant == 31 || (variant >= 41 && variant <= 44)) {  // 31: plain C stores; 41-44 probes
+    const int rc = es_panel_gemm(epi, A, lda, B, ldb, bias, C, ldc, C2, aux, ldaux, M, N, K,
+                                 variant >= 41 ? variant : variant == 30, stream);
     if (rc != ES_BAD_SHAPE) return rc;
     variant = 0;
   }

@@ -94,7 +94,9 @@ __device__ __forceinline__ u32x4 pack8(const float* v) {
 // k-step and tile offsets are instruction immediates.
 __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * ((q >> 2) & 3))) & 3; }
 
-template <int EPI, int STAUX>
+// PROBE (measurement only, variants 41..44): 1 no epilogue stores, 2 no weight DMA in the loop, 3 no barrier,
+// 4 no fragment reads / MFMAs
+template <int EPI, int STAUX, int PROBE = 0>
 __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int R = ring_of<EPI>();
@@ -119,8 +121,6 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
                                               (unsigned)p.M * p.ldc * ESZ);
 
   // weight-chunk DMA: piece j of wave w covers the slot's 16-B units L = (j * 4 + w) * 64 + lane; unit L is
-  // LDS row q = L / 48 (weight row perm(q)), chunk (L % 48) ^ (q & 15)
-  // weight-chunk DMA: piece j of wave w covers the slot's 16-B units L = (j * 4 + w) * 64 + lane; unit L is
   // k-block kk = L / 128, LDS row q = (L % 128) / 4 (weight row perm(q)), position u = L % 4, which holds the
   // k-chunk 4 kk + (u ^ hsw(q))
   unsigned ob[PD];  // byte offsets within a chunk's weight rows
@@ -131,41 +131,57 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
     ob[j] = (unsigned)(row * p.ldb + (4 * kk + (u ^ hsw(q))) * 8) * 2u;
   }
   const i32x4 rB = rsrc_i4(p.B, (unsigned)p.N * p.ldb * 2u);
+  // a null bias: a zero-size resource, every piece reads zeros
   const i32x4 rBias = rsrc_i4(p.bias ? (const void*)p.bias : (const void*)p.B, p.bias ? (unsigned)p.N * 4u : 0u);
   constexpr int AESZ = PA == 4 ? 4 : 2;  // aux element bytes
   const i32x4 rX = rsrc_i4(PA ? p.aux : (const void*)p.B, PA ? (unsigned)p.M * p.ldaux * AESZ : 0u);
-  const float bscale = p.bias ? 1.f : 0.f;
-  auto step_of = [&](int k) { return rev ? s1 - 1 - k : s0 + k; };
-  int issued = 0;  // vector-memory operations this wave has issued (loads, DMA, stores)
-  auto issue_w = [&](int k) {  // the weight chunk + bias of step k into slot k % R
-    const int s = step_of(k), ch = s % p.CH;
-    const unsigned so = (unsigned)(ch * NC * p.ldb) * 2u;
-    char* dst = smem + (k % R) * SLOT;
-#pragma unroll
-    for (int j = 0; j < PD; ++j) bl16_asm(rB, ob[j], so, dst + (j * WAVES + w) * 1024);
-    // 128 B of bias from lanes 0..7 (the same bytes from every wave; a null bias reads zeros)
-    if (lane < 8) bl16_asm(rBias, lane * 16u, (unsigned)(ch * NC) * 4u, dst + WB);
+
+  // Step descriptors, advanced incrementally (no divisions in the loop): chunk and panel of a step.
+  struct Pos { int ch, panel; };
+  auto adv = [&](Pos q) {
+    if (!rev) return q.ch + 1 == p.CH ? Pos{0, q.panel + 1} : Pos{q.ch + 1, q.panel};
+    return q.ch == 0 ? Pos{p.CH - 1, q.panel - 1} : Pos{q.ch - 1, q.panel};
+  };
+  const int sf = rev ? s1 - 1 : s0;
+  const Pos first{sf % p.CH, sf / p.CH};
+
+  int issued = 0;  // vector-memory operations this wave has issued (loads, DMA, stores): the slow-path waits
+  // the weight chunk + bias of a step into slot `slot`: one asm block, M0 stepped by 4 KiB between the pieces
+  auto issue_w = [&](Pos q, int slot) {
+    const unsigned so = (unsigned)(q.ch * NC * p.ldb) * 2u;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(
+        (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(smem + slot * SLOT + w * 1024));
+    static_assert(PD == 6, "issue_w pieces");
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %8\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %3, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %4, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %5, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %6, %7, %9 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(ob[0]), "v"(ob[1]), "v"(ob[2]), "v"(ob[3]), "v"(ob[4]), "v"(ob[5]), "s"(rB), "s"(dst), "s"(so)
+        : "memory", "scc");
+    // 128 B of bias from lanes 0..7 (the same bytes from every wave)
+    if (lane < 8) bl16_asm(rBias, lane * 16u, (unsigned)(q.ch * NC) * 4u, smem + slot * SLOT + WB);
     issued += PD + 1;
   };
-  // the aux rows of step k's epilogue: lane (g, r) fetches row (16 mt + r), columns 8 g .. + 8 (bf16) or
-  // 8 g + 4 h .. + 4 (fp32, h = 0, 1) into its own 16 B of the wave's stage; xrow[mt] = the lane's row offsets
-  // in the current panel (rows past M are out of the resource's range: zeros, outputs dropped)
-  unsigned xrow[2] = {0u, 0u};
-  auto set_rows = [&](int panel) {
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const int m = panel * PANEL + w * RW + 16 * mt + r;
-      xrow[mt] = m < p.M ? (unsigned)(m * p.ldaux + 8 * g) * (unsigned)AESZ : ES_OOB;
-    }
+  // the aux rows of a step's epilogue: lane (g, r) fetches row (16 mt + r), columns 8 g .. + 8 (bf16) or
+  // 8 g + 4 h .. + 4 (fp32, h = 0, 1) into its own 16 B of the wave's stage (rows past M are out of the
+  // resource's range: zeros, their outputs dropped)
+  auto lane_row = [&](int panel, int mt, int ld, int esz) {
+    const int m = panel * PANEL + w * RW + 16 * mt + r;
+    return m < p.M ? (unsigned)(m * ld + 8 * g) * (unsigned)esz : ES_OOB;
   };
-  auto issue_aux = [&](int k) {
+  auto issue_aux = [&](Pos q, int stage) {
     if constexpr (PA > 0) {
-      const int ch = step_of(k) % p.CH;
-      char* dst = auxs + ((k & 1) * WAVES + w) * PA * 1024;
+      char* dst = auxs + (stage * WAVES + w) * PA * 1024;
 #pragma unroll
       for (int j = 0; j < PA; ++j) {
         const int mt = PA == 2 ? j : (j >> 1), h = PA == 2 ? 0 : (j & 1);
-        bl16_asm(rX, xrow[mt] + 16u * h, (unsigned)(ch * NC) * AESZ, dst + j * 1024);
+        bl16_asm(rX, lane_row(q.panel, mt, p.ldaux, AESZ) + 16u * h, (unsigned)(q.ch * NC) * AESZ, dst + j * 1024);
       }
       issued += PA;
     }
@@ -174,7 +190,6 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
   // A fragments: a[mt][kk] = A[row0 + 16 mt + r][32 kk + 8 g .. + 8]
   bf16x8 a[2][KT];
   auto load_a = [&](int panel) {
-    if constexpr (PA > 0) set_rows(panel);
     const int m0 = panel * PANEL + w * RW;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -186,27 +201,22 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
     issued += 2 * KT;
   };
 
-  // bias of step k's columns (the lane's eight), read from slot k % R in step k: DMA(k + R) reuses the slot at
-  // the top of step k + 1, before step k's epilogue
-  f32x4 bias_c[2], bias_p[2];
-  auto read_bias = [&](int k) {
-    const char* bs = smem + (k % R) * SLOT + WB + 32 * g;
-    bias_c[0] = *(const f32x4*)bs * bscale;
-    bias_c[1] = *(const f32x4*)(bs + 16) * bscale;
-  };
-  auto epilogue = [&](int k, const f32x4 (&acc)[2][2]) {
-    const int s = step_of(k), panel = s / p.CH, ch = s - panel * p.CH;
-    const int n0 = ch * NC + 8 * g, m0 = panel * PANEL + w * RW + r;
-    const f32x4 b0 = bias_p[0], b1 = bias_p[1];
-    const char* as = auxs + ((k & 1) * WAVES + w) * PA * 1024 + lane * 16;
+  // the epilogue of a step (q) from its accumulators, the bias values the lane read from its slot, and the
+  // wave's aux stage (a segment's last epilogue runs in the next segment's first step: its rows come from q)
+  auto epilogue = [&](Pos q, const f32x4 (&acc)[2][2], const f32x4 (&bias)[2], int stage) {
+    const unsigned cofs = (unsigned)(q.ch * NC) * (unsigned)ESZ;
+    const char* as = auxs + (stage * WAVES + w) * PA * 1024 + lane * 16;
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-      const int m = m0 + mt * 16;
-      const unsigned off = m < p.M ? (unsigned)(m * p.ldc + n0) * (unsigned)ESZ : ES_OOB;
-      const f32x4 v0 = acc[mt][0] + b0, v1 = acc[mt][1] + b1;
+      const unsigned off = lane_row(q.panel, mt, p.ldc, ESZ) + cofs;
+      const f32x4 v0 = acc[mt][0] + bias[0], v1 = acc[mt][1] + bias[1];
       float v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
       auto st = [&](__amdgpu_buffer_rsrc_t rr, unsigned o, u32x4 d) {
-        __builtin_amdgcn_raw_buffer_store_b128(d, rr, o, 0, STAUX);
+        if constexpr (PROBE == 1) {
+          if (d[0] == 0x12345u && d[1] == 0x777u) __builtin_amdgcn_raw_buffer_store_b128(d, rr, o, 0, STAUX);
+        } else {
+          __builtin_amdgcn_raw_buffer_store_b128(d, rr, o, 0, STAUX);
+        }
       };
       if constexpr (EPI == EPI_BF16) {
         st(rc, off, pack8(v));
@@ -218,10 +228,10 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
         st(rc, off, __builtin_bit_cast(u32x4, v0 + x0));
         st(rc, off + 16, __builtin_bit_cast(u32x4, v1 + x1));
       } else if constexpr (EPI == EPI_MULAUX || EPI == EPI_DGELU) {
-        const bf16x8 q = *(const bf16x8*)(as + mt * 1024);
+        const bf16x8 qq = *(const bf16x8*)(as + mt * 1024);
         float o[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = EPI == EPI_MULAUX ? v[i] * (float)q[i] : v[i] * gelu_grad_f((float)q[i]);
+        for (int i = 0; i < 8; ++i) o[i] = EPI == EPI_MULAUX ? v[i] * (float)qq[i] : v[i] * gelu_grad_f((float)qq[i]);
         st(rc, off, pack8(o));
       } else {  // GELU family: the same packed routine as gemm.hip's epilogues (bit-identical outputs)
         float gv[8], dv[8];
@@ -240,17 +250,28 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
     issued += EST;
   };
 
-  f32x4 acc[2][2], pacc[2][2];
-  // `issued` right after DMA(k) and (R = 3) DMA(k + 1) at the top of step k, rotated each step (scalars: an
-  // array under a dynamic index would live in scratch, whose accesses count in vmcnt), and after aux(k - 1)
-  int mw0 = 0, mw1 = 0, mx = 0;
-  // one step.  FIRST (compile-time): step 0, no epilogue before it -- so that no compiler-visible load and
-  // its wait sit on different conditional paths (the compiler's wait bookkeeping is path-insensitive).
-  auto step = [&](auto first_tag, int k) {
+  // Steady-state wait counts (every step of the window issued all its operations), per step k in issue
+  // order [DMA(k + R - 1): PD + 1][aux(k): PA][MFMAs][epilogue(k - 1): EST]:
+  //   DMA(k), issued in step k - R + 1: R = 3: aux(k - 2) + epi(k - 3) + DMA(k + 1) + aux(k - 1) + epi(k - 2);
+  //                                     R = 2: aux(k - 1) + epi(k - 2)
+  //   aux(k - 1), issued in step k - 1: epi(k - 2) + DMA(k + R - 1) + aux(k)
+  constexpr int NW = R == 3 ? 2 * PA + 2 * EST + PD + 1 : PA + EST;
+  constexpr int NX = EST + PD + 1 + PA;
+  static_assert(NW <= 63 && NX <= 63, "vmcnt");
+  int mw0 = 0, mw1 = 0, mx = 0;  // slow path: `issued` after DMA(k), DMA(k + 1) (R = 3), aux(k - 1)
+
+  // one step k at position qk (qe: position of step k - 1, qd: of step k + R - 1).  FIRST (compile-time): step
+  // 0, no epilogue before it -- no compiler-visible load and its wait sit on different conditional paths
+  // (the compiler's wait bookkeeping is path-insensitive).  accC / biasC: this step's; accP / biasP: the
+  // previous step's (two register sets, alternated by the caller: no copies).
+  auto step = [&](auto first_tag, int k, Pos qk, Pos qe, Pos qd, f32x4 (&accC)[2][2], f32x4 (&accP)[2][2],
+                  f32x4 (&biasC)[2], f32x4 (&biasP)[2]) {
     constexpr bool FIRST = decltype(first_tag)::value;
-    wait_vmcnt_any(min(issued - mw0, 63));  // this wave's pieces of DMA(k); the barrier: every wave's
-    __builtin_amdgcn_s_barrier();
-    if (k + R - 1 < n) issue_w(k + R - 1);  // into slot (k - 1) % R, read in step k - 1, which every wave left
+    const bool steady = k >= R + 1 && k + R - 2 < n;
+    if (steady) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
+    else wait_vmcnt_any(min(issued - mw0, 63));  // this wave's pieces of DMA(k); the barrier: every wave's
+    if constexpr (PROBE != 3) __builtin_amdgcn_s_barrier();
+    if (PROBE != 2 && k + R - 1 < n) issue_w(qd, (k + R - 1) % R);  // slot (k - 1) % R: read in step k - 1, which all left
     if constexpr (R == 3) {
       mw0 = mw1;
       mw1 = issued;
@@ -258,71 +279,82 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
       mw0 = issued;
     }
     const int mx_prev = mx;
-    issue_aux(k);
+    issue_aux(qk, k & 1);
     mx = issued;
     const char* Bs = smem + (k % R) * SLOT + fo;
-    read_bias(k);
+    {  // the bias of this step's columns (the lane's eight): DMA(k + R) reuses the slot before the epilogue
+      const char* bs = smem + (k % R) * SLOT + WB + 32 * g;
+      biasC[0] = *(const f32x4*)bs;
+      biasC[1] = *(const f32x4*)(bs + 16);
+    }
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // fragments one k-step ahead (two register sets); the group barriers pin the order [2 fragment reads of
-    // step kk + 1][4 MFMAs of step kk], so the scheduler neither hoists all 24 reads (96 VGPRs) nor bunches them
-    bf16x8 b[2][2];
+      for (int nt = 0; nt < 2; ++nt) accC[mt][nt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fragments two k-steps ahead (three register sets); the group barriers pin the order [2 fragment reads
+    // of step kk + 2][4 MFMAs of step kk]
+    bf16x8 b[3][2];
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt) b[0][nt] = *(const bf16x8*)(Bs + nt * 1024);
+    for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int kk = 0; kk < KT; ++kk) {
-      if (kk + 1 < KT) {
+      for (int nt = 0; nt < 2; ++nt) b[kk][nt] = *(const bf16x8*)(Bs + kk * 2048 + nt * 1024);
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) b[(kk + 1) & 1][nt] = *(const bf16x8*)(Bs + (kk + 1) * 2048 + nt * 1024);
+    for (int kk = 0; kk < (PROBE == 4 ? 0 : KT); ++kk) {
+      if (kk + 2 < KT) {
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) b[(kk + 2) % 3][nt] = *(const bf16x8*)(Bs + (kk + 2) * 2048 + nt * 1024);
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
       }
 #pragma unroll
       for (int mt = 0; mt < 2; ++mt)
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) acc[mt][nt] = mfma16(b[kk & 1][nt], a[mt][kk], acc[mt][nt]);
+        for (int nt = 0; nt < 2; ++nt) accC[mt][nt] = mfma16(b[kk % 3][nt], a[mt][kk], accC[mt][nt]);
       __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
     if constexpr (!FIRST) {
-      if constexpr (PA > 0) wait_vmcnt_any(min(issued - mx_prev, 63));  // this wave's aux(k - 1)
-      epilogue(k - 1, pacc);
+      if constexpr (PA > 0) {  // this wave's aux(k - 1)
+        if (k >= 2 && k + R - 1 < n) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NX) : "memory");
+        else wait_vmcnt_any(min(issued - mx_prev, 63));
+      }
+      epilogue(qe, accP, biasP, (k - 1) & 1);
     }
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt)
-#pragma unroll
-      for (int nt = 0; nt < 2; ++nt) pacc[mt][nt] = acc[mt][nt];
-    bias_p[0] = bias_c[0];
-    bias_p[1] = bias_c[1];
   };
-  // panel segments: a segment's rows are loaded into registers at its start and drained with a wait the
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  f32x4 acc0[2][2], acc1[2][2], bias0[2], bias1[2];
+  // panel segments: a segment's rows are loaded into registers at its first step and drained with a wait the
   // compiler sees (vmcnt(0)), so no A load is pending inside the steps.  (Loading the next panel's rows
   // during the previous segment's last step needs 96 more registers than two waves per SIMD leave.)
-  int panel = step_of(0) / p.CH;
+  // Positions: qe (step k - 1), qk (k), q1 (k + 1), q2 (k + 2); the DMA of step k targets k + R - 1.
+  Pos qe = first, qk = first, q1 = adv(first), q2 = adv(q1);
+  int panel = qk.panel;
   load_a(panel);
-  issue_w(0);  // the prologue: DMA(0 .. R - 2)
+  issue_w(qk, 0);
   mw0 = issued;
   if constexpr (R == 3) {
-    if (n > 1) issue_w(1);
+    if (n > 1) issue_w(q1, 1);
     mw1 = issued;
   }
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-  step(std::true_type{}, 0);
-  int k = 1;
-  while (k < n) {
-    const int pk = step_of(k) / p.CH;
-    if (pk != panel) {
-      panel = pk;
+  step(T_{}, 0, qk, qe, R == 3 ? q2 : q1, acc0, acc1, bias0, bias1);
+  for (int k = 1; k < n; ++k) {
+    qe = qk;
+    qk = q1;
+    q1 = q2;
+    q2 = adv(q2);
+    if (qk.panel != panel) {
+      panel = qk.panel;
       load_a(panel);
-      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     }
-    int kend = k + 1;
-    while (kend < n && step_of(kend) / p.CH == panel) ++kend;
-    for (; k < kend; ++k) step(std::false_type{}, k);
+    const Pos qd = R == 3 ? q2 : q1;
+    if (k & 1) step(F_{}, k, qk, qe, qd, acc1, acc0, bias1, bias0);
+    else step(F_{}, k, qk, qe, qd, acc0, acc1, bias0, bias1);
   }
   if constexpr (PA > 0) wait_vmcnt_any(min(issued - mx, 63));
-  epilogue(n - 1, pacc);
+  if ((n - 1) & 1) epilogue(qk, acc1, bias1, (n - 1) & 1);
+  else epilogue(qk, acc0, bias0, (n - 1) & 1);
 }
 
 }  // namespace es_panel
@@ -332,6 +364,7 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
 extern "C" int es_panel_gemm(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C,
                              int ldc, void* C2, const void* aux, int ldaux, int M, int N, int K, int stores_nt,
                              hipStream_t stream) {
+  const int probe = stores_nt >= 41 ? stores_nt - 40 : 0;
   using namespace es_panel;
   if (K != KT * 32 || N % NC || M <= 0 || (lda % 8) || (ldb % 8) || (ldc % 8) || (ldaux % 8)) return ES_BAD_SHAPE;
   static int cus = 0;
@@ -351,6 +384,18 @@ extern "C" int es_panel_gemm(int epi, const void* A, int lda, const void* B, int
   }
 #define PLE(E) \
   if (stores_nt) PL(E, 2) else PL(E, 0)
+  if (probe) {  // measurement variants 41..44 (EPI_BF16 only)
+    constexpr int E = EPI_BF16;
+    auto go = [&](auto kern) {
+      allow_lds(kern, lds_bytes<E>());
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds_bytes<E>(), stream, a);
+    };
+    if (probe == 1) go(gemm_panel_kernel<E, 2, 1>);
+    else if (probe == 2) go(gemm_panel_kernel<E, 2, 2>);
+    else if (probe == 3) go(gemm_panel_kernel<E, 2, 3>);
+    else go(gemm_panel_kernel<E, 2, 4>);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   switch (epi) {
     case EPI_BF16: PLE(EPI_BF16)
     case EPI_F32: PLE(EPI_F32)

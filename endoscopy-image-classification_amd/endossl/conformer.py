@@ -331,6 +331,13 @@ class _GradSink:
         return None
 
 
+# test hook (tests/test_gpu_s1_blocks.py, teacher-forced per-op parity of the transformer branch at S1's
+# shape): called as BLOCK_CAPTURE("fwd", prefix, n, xt, h1, qkv, o, lse, xmid, h2, pre, act, out) after a
+# transformer block's forward and BLOCK_CAPTURE("bwd", prefix, n, dout, dxb, dpre, dh, dxm, dxmb, do, dqkv,
+# dh2, dx) after its reverse pass (before the side-stream weight gradients are joined), on the launch stream
+# with the block's own buffers; the callee clones what it keeps.
+BLOCK_CAPTURE = None
+
 # test hook (tests/test_gpu_convs.py, teacher-forced per-conv parity): called as CAPTURE("fwd", wname, x, y,
 # spec) after each convolution's forward and CAPTURE("bwd", wname, dy, dx_before, dx) after its input
 # gradient, on the launch stream, with the conv's own NHWC views (x: the input map as the kernel reads it;
@@ -740,6 +747,8 @@ class _BlockFn(torch.autograd.Function):
              ptr(pv(pre + "mlp.fc2.bias")), ptr(out), D, None, ptr(xmid), D, M, D, Hd, 0, s)
         ctx.save_for_backward(xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, pre_, act)
         ctx.m, ctx.pre, ctx.n = m, pre, n
+        if BLOCK_CAPTURE is not None:
+            BLOCK_CAPTURE("fwd", pre, n, xt, h1, qkv, o, lse, xmid, h2, pre_, act, out)
         return out
 
     @staticmethod
@@ -814,6 +823,8 @@ class _BlockFn(torch.autograd.Function):
         call("es_layernorm_bwd_b16", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),
              ptr(ws_ln), 1024, M, D, 0, s)
+        if BLOCK_CAPTURE is not None:
+            BLOCK_CAPTURE("bwd", pre, n, dout, dxb, dpre, dh, dxm, dxmb, do, dqkv, dh2, dx)
         if side is not None:
             for t in (act, h2, o, h1):  # saved activations the side stream still reads
                 t.record_stream(side)

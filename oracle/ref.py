@@ -342,6 +342,29 @@ def attn_fwd_bf16(qkv, n, T, H):
     return o, mx + torch.log(l)
 
 
+def attn_fwd_bf16_online(qkv, n, T, H, chunk=128):
+    """attn_fwd_bf16 at the rounding points of the long-sequence forward (T > 256, csrc/attention.hip
+    fwd_long_chunk): the same softmax(q k^T hd^-0.5) v (code/models/conformer.py:41-50), taken over key
+    chunks of `chunk` keys with a running max m -- per chunk P = exp(s - m_running) enters P.V as bf16(P),
+    o and the unrounded sum l are rescaled by exp(m_old - m_new) when the max grows; o = bf16(o / l),
+    lse = m + log(l).  Equal to attn_fwd_bf16 in exact arithmetic; the bf16(P) rounding is taken relative
+    to the running max instead of the row max."""
+    q, k, v = qkv.view(n, T, 3, H, 64).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-2, -1)) * 64 ** -0.5
+    m = torch.full(s.shape[:-1] + (1,), -float("inf"), dtype=s.dtype, device=s.device)
+    l = torch.zeros_like(m)
+    o = torch.zeros(q.shape, dtype=s.dtype, device=s.device)
+    for c0 in range(0, T, chunk):
+        sc = s[..., c0:c0 + chunk]
+        mn = torch.maximum(m, sc.amax(-1, keepdim=True))
+        alpha = torch.exp(m - mn)
+        e = torch.exp(sc - mn)
+        o = o * alpha + _rb(e) @ v[..., c0:c0 + chunk, :]
+        l = l * alpha + e.sum(-1, keepdim=True)
+        m = mn
+    return _rb((o / l).transpose(1, 2).reshape(n * T, H * 64)), m + torch.log(l)
+
+
 def attn_bwd_bf16(qkv, o, lse, do, n, T, H):
     """Reverse pass of attn_fwd_bf16 (flash-style recomputation): P = exp(s - lse), delta =
     rowsum(dO * O), dS = P (dO v^T - delta); dV = bf16(bf16(P)^T dO), dK = bf16(bf16(dS)^T q * scale),
