@@ -190,6 +190,18 @@ def cpu_baseline(B=8, MU=7, steps=2):
                       f"host RAM {mem} (the job may use at most ~270 GiB of it), torch.get_num_threads()={used}"}
 
 
+def step_counters():
+    """The committed step-level counter summary (scripts/gpu_step_counters.sh -> profiles/<tag>_step_counters.json,
+    the newest tag): MFMA-busy SIMD-cycles and HBM bytes of one F1 step, measured by rocprofv3 --pmc passes over
+    this bench."""
+    pdir = os.path.join(ROOT, "profiles")
+    cands = sorted(f for f in os.listdir(pdir) if f.endswith("_step_counters.json"))
+    if not cands:
+        return None, None
+    with open(os.path.join(pdir, cands[-1])) as f:
+        return json.load(f), "profiles/" + cands[-1]
+
+
 def pmc_traffic(kernel_substr):
     """Per-launch HBM bytes of the dominant kernel from the committed rocprofv3 --pmc summary
     (profiles/pmc_traffic.json: FETCH_SIZE x2 (gfx950 half-count correction) + WRITE_SIZE, KiB->B)."""
@@ -612,9 +624,9 @@ def main():
         del xw, yw, bw
     ar_overlap = None
     if world > 1:
-        # the same step with the gradient all-reduce bucketed per block and overlapped with the reverse pass
-        # (FixMatch.overlap_allreduce / dist.GradBuckets, opt-in) -- reported beside the headline, which runs
-        # the default single post-backward all-reduce, so one multi-GPU run measures both forms
+        # the same step with the OTHER all-reduce form (the headline runs the form --allreduce chose: with
+        # `auto` the faster of the per-block buckets overlapped with the reverse pass -- FixMatch.
+        # overlap_allreduce / dist.GradBuckets -- and one all-reduce after it), so one multi-GPU run measures both
         prev_ov, tr.overlap_allreduce = tr.overlap_allreduce, not tr.overlap_allreduce
         for _ in range(2):
             tr.step(batch)
@@ -706,6 +718,20 @@ def main():
                                       "note": "same launch with the engine's second HIP stream off (2 untimed "
                                               "steps): the live figure shares the CUs with the data-gradient chain"}},
         }
+        sc, sc_src = step_counters()
+        if sc is not None and world == 1:
+            busy = sc["step"]["mfma_busy_simd_cycles"]
+            res["mfma_util"] = {
+                "value": round(busy / (1024 * (ms / 1e3) * 2.4e9), 4),
+                "mfma_busy_simd_cycles_per_step": busy,
+                "profiled": {k: round(v, 4) for k, v in sc["step"].items() if k.startswith(("mfma_util", "effective"))},
+                "hbm_bytes_per_step": sc["step"]["hbm_bytes"],
+                "hbm_tbs_at_this_step_time": round(sc["step"]["hbm_bytes"] / (ms / 1e3) / 1e12, 3),
+                "source": (sc_src + " (rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES / FETCH_SIZE / WRITE_SIZE passes over "
+                           "this bench; committed, not measured in this run)"),
+                "note": "value = the step's MFMA-busy SIMD-cycles / (1024 SIMDs x this run's ms_per_step x 2.4 GHz "
+                        "nominal): a lower bound (the chip holds a lower clock under load); per-family figures in "
+                        "the .md"}
         if weak is not None:
             res["weak_scaling"] = weak
         if ar_overlap is not None:

@@ -15,10 +15,10 @@
 // step late, after the next chunk's MFMAs, so a wave's stores and VALU work sit beside the other
 // workgroup's matrix work on the same SIMDs.
 //
-// Layout: 256 threads = 4 waves (one per SIMD), two workgroups per CU, so one workgroup's panel switch (a
-// 24-KiB-per-wave burst of A loads) hides behind the other's MFMAs.  Persistent grid: the (panel, chunk)
-// steps are cut into equal contiguous ranges, one per workgroup; adjacent ranges share their boundary panel
-// and run in opposite directions (they reach it at the same time, on one XCD).
+// Layout: 512 threads = 8 waves (two per SIMD), one workgroup per CU: a 256-row panel, so every weight chunk
+// brought into LDS feeds 256 rows (qkv forward: 0.35 GB of LDS-DMA per launch).  Persistent grid: the
+// (panel, chunk) steps are cut into equal contiguous ranges, one per workgroup; adjacent ranges share their
+// boundary panel and run in opposite directions (they reach it at the same time, on one XCD).
 //
 // MFMA v_mfma_f32_16x16x32_bf16 with the weight fragment as the A operand: lane (g, r) accumulates
 // C[row0 + r][col0 + perm(16 nt + 4 g + i)].  The chunk's weight rows are stored in LDS permuted so that
@@ -49,13 +49,13 @@ enum {
 
 constexpr int KT = 12;             // K / 32
 constexpr int ROWB = KT * 64;      // LDS bytes of one weight row (768)
-constexpr int WAVES = 4;
+constexpr int WAVES = 8;
 constexpr int RW = 32;             // activation rows per wave
-constexpr int PANEL = WAVES * RW;  // 128
+constexpr int PANEL = WAVES * RW;  // 256
 constexpr int NC = 32;             // output columns per step
 constexpr int WB = NC * ROWB;      // weight bytes of a step (24 KiB)
 constexpr int SLOT = WB + NC * 4;  // + the step's bias
-constexpr int PD = WB / 1024 / WAVES;  // weight LDS-DMA pieces per wave per step (6)
+constexpr int PD = WB / 1024 / WAVES;  // weight LDS-DMA pieces per wave per step (3)
 
 struct PArgs {
   const bf16* A; const bf16* B; const float* bias;
@@ -75,9 +75,9 @@ template <int EPI>
 constexpr int stores_per_row() {  // 16-B C stores per lane per 16-row tile
   return (EPI == EPI_GELU || EPI == EPI_GELU_D || f32_out<EPI>()) ? 2 : 1;
 }
-// ring depth: three weight slots when the epilogue has no aux rows, two (plus two per-wave aux stages) else
+// ring depth: three weight slots (plus two per-wave aux stages when the epilogue reads aux rows)
 template <int EPI>
-constexpr int ring_of() { return aux_pieces<EPI>() ? 2 : 3; }
+constexpr int ring_of() { return 3; }
 template <int EPI>
 constexpr int lds_bytes() { return ring_of<EPI>() * SLOT + 2 * WAVES * aux_pieces<EPI>() * 1024; }
 
@@ -97,7 +97,7 @@ __device__ __forceinline__ int hsw(int q) { return (0x78 >> (2 * ((q >> 2) & 3))
 // PROBE (measurement only, variants 41..44): 1 no epilogue stores, 2 no weight DMA in the loop, 3 no barrier,
 // 4 no fragment reads / MFMAs
 template <int EPI, int STAUX, int PROBE = 0>
-__global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
+__global__ __launch_bounds__(512, 2) void gemm_panel_kernel(PArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int R = ring_of<EPI>();
   constexpr int PA = aux_pieces<EPI>();
@@ -151,18 +151,15 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(PArgs p) {
     const unsigned so = (unsigned)(q.ch * NC * p.ldb) * 2u;
     const unsigned dst = __builtin_amdgcn_readfirstlane(
         (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(smem + slot * SLOT + w * 1024));
-    static_assert(PD == 6, "issue_w pieces");
+    static_assert(PD == 3 && WAVES == 8, "issue_w pieces");
     unsigned keep;
     asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %8\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %1, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %2, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %3, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %4, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %5, %7, %9 offen lds\n\ts_add_u32 m0, m0, 4096\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %6, %7, %9 offen lds\n\ts_mov_b32 m0, %0"
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %5\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %4, %6 offen lds\n\ts_add_u32 m0, m0, 8192\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %4, %6 offen lds\n\ts_add_u32 m0, m0, 8192\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %3, %4, %6 offen lds\n\ts_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(ob[0]), "v"(ob[1]), "v"(ob[2]), "v"(ob[3]), "v"(ob[4]), "v"(ob[5]), "s"(rB), "s"(dst), "s"(so)
+        : "v"(ob[0]), "v"(ob[1]), "v"(ob[2]), "s"(rB), "s"(dst), "s"(so)
         : "memory", "scc");
     // 128 B of bias from lanes 0..7 (the same bytes from every wave)
     if (lane < 8) bl16_asm(rBias, lane * 16u, (unsigned)(q.ch * NC) * 4u, smem + slot * SLOT + WB);
@@ -375,11 +372,11 @@ extern "C" int es_panel_gemm(int epi, const void* A, int lda, const void* B, int
   }
   PArgs a{(const bf16*)A, (const bf16*)B, bias, C, C2, aux, M, N, lda, ldb, ldc, ldaux, N / NC, 0};
   a.S = ((M + PANEL - 1) / PANEL) * a.CH;
-  const int grid = std::min(2 * cus, a.S);
+  const int grid = std::min(cus, a.S);
 #define PL(E, X)                                                                                       \
   {                                                                                                    \
     allow_lds(gemm_panel_kernel<E, X>, lds_bytes<E>());                                                \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_panel_kernel<E, X>), dim3(grid), dim3(256), lds_bytes<E>(), stream, a); \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_panel_kernel<E, X>), dim3(grid), dim3(512), lds_bytes<E>(), stream, a); \
     break;                                                                                             \
   }
 #define PLE(E) \
@@ -388,7 +385,7 @@ extern "C" int es_panel_gemm(int epi, const void* A, int lda, const void* B, int
     constexpr int E = EPI_BF16;
     auto go = [&](auto kern) {
       allow_lds(kern, lds_bytes<E>());
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds_bytes<E>(), stream, a);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds_bytes<E>(), stream, a);
     };
     if (probe == 1) go(gemm_panel_kernel<E, 2, 1>);
     else if (probe == 2) go(gemm_panel_kernel<E, 2, 2>);
@@ -404,7 +401,8 @@ extern "C" int es_panel_gemm(int epi, const void* A, int lda, const void* B, int
     case EPI_GELU_D: PLE(EPI_GELU_D)
     case EPI_MULAUX: PLE(EPI_MULAUX)
     case EPI_DGELU: PLE(EPI_DGELU)
-    default: return ES_BAD_SHAPE;  // EPI_F32_RESID (its fp32 aux stages would not fit two workgroups per CU)
+    case EPI_F32_RESID: PLE(EPI_F32_RESID)
+    default: return ES_BAD_SHAPE;
   }
 #undef PLE
 #undef PL
