@@ -1129,6 +1129,373 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
   }
 }
 
+// ---- single-pass backward (T in (192, 208]: 13 tiles) ------------------------------------------------
+// One persistent workgroup per CU (eight waves, 148 KiB of LDS), heads bh = blockIdx.x, + gridDim.x, ...
+// HBM is touched once per operand: Q, dO and K of a head by LDS-DMA, O and lse into registers (delta, the
+// log2 lse), the K / V rows of phase 1 into registers, and dQ, dK, dV written once -- where the two-pass
+// form (attn_bwd_dq2_kernel + attn_bwd_dkv2_kernel) read Q, K, V, dO twice and wrote / re-read delta.
+// A head runs in two rounds over its queries (tiles 0..7, then 8..12):
+//   phase 1, key on the lane (wave w < 7 owns key tiles 2w, 2w + 1 and their K / V rows): S, P, dP and dS of
+//     the round's query pairs exactly as attn_bwd_dkv2_kernel, dV / dK accumulated in registers, and
+//     bf16(dS) written to LDS as [key][query] images (64 queries per 128-B row; within a 32-query segment
+//     column 8g + i holds query 4g + i of the first tile (i < 4) and 16 + 4g + i - 4 of the second, so the
+//     lane's packed dK operand goes out as one 16-B store; 8-B pieces swizzled by sws);
+//   phase 2, query on the lane (one query tile per wave): dQ^T = K^T . dS^T from the K image and the dS
+//     images (both transposed reads), attn_bwd_dq2_kernel's MFMAs without recomputing S and dP.
+// dK / dV are stored after the second round's phase 1.  The next head's Q / dO rows are DMA'd into the rows
+// a round's phase 1 has finished with, its K after the last phase 2, and its O / lse / K / V fragments are
+// loaded into registers during the last phase 2: only the first head's loads are exposed.  The DMAs are
+// inline asm (hipcc would otherwise drain them in front of every transposed read) retired by counted waits;
+// the barriers wait for LDS only, so a prefetch stays in flight across them.
+// Rounding points and fp32 accumulation orders are attn_bwd_dq2_kernel's (delta, dQ) and
+// attn_bwd_dkv2_kernel's (dK, dV): phase 1's S and dP are the transposed MFMA products of dq2's, the same
+// fp32 dot products.
+
+// dS image row k: logical 8-B piece p (= 2 x chunk + half) at piece p ^ sws(k).  Conflict-free both for the
+// transposed reads (a 32-lane group: rows k0..k0+7, four chunks, one half) and for the 16-B row stores (8 lanes:
+// rows k0..k0+7, one chunk): bits 1-3 of sws are a bijection of k & 7, and bits 0 and 3 differ over the four
+// rows of one parity.
+__device__ __forceinline__ int sws(int k) { return ((k & 4) << 1) | ((k & 1) << 2) | (((k >> 1) & 1) * 3); }
+
+// dS^T fragment (B operand of dQ^T = K^T . dS^T) of query tile `half` of a 32-query segment of a dS image:
+// elements 0..3 = keys base + 4g .. + 3, elements 4..7 = keys base + 16 + 4g .. + 3 (lds_trT's k order)
+__device__ __forceinline__ bf16x8 lds_trS(const char* img, int base, int seg, int half, int g, int t) {
+  const int p = 2 * (seg * 4 + (t & 3)) + half;
+  const int r1 = base + 4 * g + (t >> 2), r2 = r1 + 16;
+  return cat8(lds_tr4(img + r1 * 128 + (p ^ sws(r1)) * 8), lds_tr4(img + r2 * 128 + (p ^ sws(r2)) * 8));
+}
+__device__ __forceinline__ bf16x4 lds_trS4(const char* img, int base, int seg, int half, int g, int t) {
+  const int p = 2 * (seg * 4 + (t & 3)) + half;
+  const int r1 = base + 4 * g + (t >> 2);
+  return lds_tr4(img + r1 * 128 + (p ^ sws(r1)) * 8);
+}
+
+// LDS byte address of a pointer into LDS (a non-template function: see glds16)
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// bl16_asm with the LDS destination already a wave-uniform 32-bit LDS address (no generic pointer formed)
+__device__ __forceinline__ void bl16_m0(i32x4 rsrc, unsigned voff, unsigned soff, unsigned lds_byte) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rsrc), "s"(lds_byte), "s"(soff)
+               : "memory");
+}
+
+// LDS writes visible to the workgroup; VMEM (DMA, stores) left in flight
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ unsigned long long g_attn_stamps[2][8][16][12];  // (measurement) workgroups 0 / 101
+
+template <int NT16, int STAMP = 0>
+__global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh) {
+  static_assert(NT16 == 13, "rounds of 8 + 5 query tiles, 7 key-tile pairs over 8 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TP = NT16 * 16, IMG = TP * 128, NP = NT16 / 2, PA = 4, NG = TP / 8;
+  char* Qs = smem;
+  char* Ds = smem + IMG;
+  char* Ks = smem + 2 * IMG;
+  char* Ss = smem + 3 * IMG;  // two dS images
+  float* lse_s = (float*)(smem + 5 * IMG);
+  float* del_s = lse_s + TP;
+  // the wave index in a scalar register: wave-uniform branches and loop trips stay scalar
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  char* slot = (char*)(del_s + TP) + w * 2048;
+  const unsigned lds0 = lds_addr(smem);  // LDS byte address of the dynamic allocation
+  const int D = a.H * 64, T = a.T;
+  const float sl = a.scale * 1.44269504088896341f;
+  // the lane index as an opaque value: each phase derives its LDS addresses from a fresh copy, so hipcc
+  // cannot hoist them all out of the head loop (two dozen loop-invariant addresses live across every phase
+  // were spilled to scratch, and every reload's vmcnt wait drained the prefetch DMAs)
+  auto fresh_lane = [&]() {
+    int l = threadIdx.x & 63;
+    asm volatile("" : "+v"(l));
+    return l;
+  };
+
+  // whole-tensor buffer resources (the launcher keeps every tensor under 2 GiB): per-head offsets are 32-bit
+  // scalars, so no 64-bit head pointer is ever formed in (and spilled from) vector registers
+  const int nrows = nbh / a.H * T;
+  const i32x4 sQKV = rsrc_i4(a.qkv, (unsigned)nrows * a.ldqkv * 2u);
+  const i32x4 sDO = rsrc_i4(a.dout, (unsigned)nrows * a.lddo * 2u);
+  const auto bQKV = buf_rsrc(a.qkv, (unsigned)nrows * a.ldqkv * 2u);
+  const auto bO = buf_rsrc(a.o, (unsigned)nrows * a.ldo * 2u);
+  const auto bLSE = buf_rsrc(a.lse, (unsigned)nbh * T * 4u);
+
+  // 8-row groups [i0, i1) of a head image (rows >= T re-read row T - 1; colb: the head's byte column, ldb: the
+  // row pitch in bytes, base: the image's first byte), by waves w0..7: this wave's share groups i0 + w - w0,
+  // + 8 - w0, ..
+  auto stage = [&](const char* lds, i32x4 rs, unsigned base, unsigned colb, unsigned ldb, int i0, int i1, int w0) {
+    const int l = fresh_lane();
+    const unsigned dst = lds0 + (unsigned)(lds - smem);
+    for (int i = i0 + w - w0; w >= w0 && i < i1; i += 8 - w0) {
+      const int row = i * 8 + (l >> 3);
+      const int sr = row < T ? row : T - 1;
+      bl16_m0(rs, (unsigned)sr * ldb + colb + aswz(row, l & 7) * 16, base, dst + i * 1024);
+    }
+  };
+  auto stage_qdo = [&](int bh, int i0, int i1, int w0) {
+    const int img = bh / a.H, h = bh - img * a.H;
+    stage(Qs, sQKV, (unsigned)img * T * a.ldqkv * 2u, h * 128, a.ldqkv * 2, i0, i1, w0);
+    stage(Ds, sDO, (unsigned)img * T * a.lddo * 2u, h * 128, a.lddo * 2, i0, i1, w0);
+  };
+  auto stage_k = [&](int bh) {
+    const int img = bh / a.H, h = bh - img * a.H;
+    stage(Ks, sQKV, (unsigned)img * T * a.ldqkv * 2u, (D + h * 64) * 2, a.ldqkv * 2, 0, NG, 0);
+  };
+
+  // register operands of a head: O rows of the wave's delta tiles (w, w + 8), K / V rows of its key tiles
+  // (2w, 2w + 1), the lse of query threadIdx.x -- buffer loads, rows past T read as zero
+  struct Pre {
+    bf16x8 o[2][2];
+    bf16x8 kv[8];
+    float lse;
+  };
+  auto prefetch = [&](int bh) {
+    Pre p;
+    const int l = fresh_lane(), g = l >> 4, r = l & 15;
+    const int img = bh / a.H, h = bh - img * a.H;
+    // in order of use (lse and O by the deltas, K / V by phase 1): hipcc's counted waits for the early ones
+    // then leave the younger K-image DMA in flight
+    const int tq = l + 64 * w;
+    p.lse = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                          bLSE, tq < T ? (unsigned)(bh * T + tq) * 4u : ES_OOB, 0, 0));
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int q = (w + 8 * j) * 16 + r;
+      const unsigned off = q < T ? (unsigned)((img * T + q) * a.ldo + h * 64 + 8 * g) * 2u : ES_OOB;
+      p.o[j][0] = __builtin_bit_cast(bf16x8, buf_load16(bO, off));
+      p.o[j][1] = __builtin_bit_cast(bf16x8, buf_load16(bO, off + 64));
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = w * 32 + 16 * t + r;
+      const unsigned off = key < T ? (unsigned)((img * T + key) * a.ldqkv + D + h * 64 + 8 * g) * 2u : ES_OOB;
+      p.kv[4 * t + 0] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off));
+      p.kv[4 * t + 1] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 64));
+      p.kv[4 * t + 2] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 2 * D));
+      p.kv[4 * t + 3] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 2 * D + 64));
+    }
+    return p;
+  };
+  // delta = rowsum(dO * O) with attn_bwd_dq2_kernel's lane split and order; lse in log2 units
+  auto deltas = [&](const Pre& p) {
+    const int l = fresh_lane(), g = l >> 4, r = l & 15;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int tile = w + 8 * j;
+      if (tile < NT16) {
+        const int q = tile * 16 + r;
+        const bf16x8 d0 = lds_row8(Ds, q, g), d1 = lds_row8(Ds, q, 4 + g);
+        float delta = 0.f;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj)
+          delta += (float)d0[jj] * (float)p.o[j][0][jj] + (float)d1[jj] * (float)p.o[j][1][jj];
+        delta += __shfl_xor(delta, 16, 64);
+        delta += __shfl_xor(delta, 32, 64);
+        if (g == 0) del_s[q] = q < T ? delta : 0.f;
+      }
+    }
+    if ((int)threadIdx.x < TP) lse_s[threadIdx.x] = (int)threadIdx.x < T ? p.lse * 1.44269504088896341f : INFINITY;
+  };
+
+  // P and dS of one query tile against one key tile (attn_bwd_dkv2_kernel's p_ds)
+  auto p_ds = [&](bf16x8 q0, bf16x8 q1, bf16x8 d0, bf16x8 d1, f32x4 l4, f32x4 d4, bf16x8 kf0, bf16x8 kf1,
+                  bf16x8 vf0, bf16x8 vf1, f32x4& p, f32x4& ds) {
+    f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+    sv = mfma16(q0, kf0, sv);
+    sv = mfma16(q1, kf1, sv);
+    dp = mfma16(d0, vf0, dp);
+    dp = mfma16(d1, vf1, dp);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      p[i] = __builtin_amdgcn_exp2f(sv[i] * sl - l4[i]);
+      ds[i] = p[i] * (dp[i] - d4[i]);
+    }
+  };
+  const bf16x8 zero8 = {};
+  const bf16x4 zero4 = {};
+  // phase 1 over query pairs [s0, s1) (+ the odd tile NT16 - 1), dS written for queries qbase..
+  auto phase1 = [&](const bf16x8 (&kv)[8], f32x4 (&dk)[2][4], f32x4 (&dv)[2][4], int s0, int s1, bool odd,
+                    int qbase) {
+    const int l = fresh_lane(), g = l >> 4, r = l & 15;
+    const int keyA = w * 32 + r, keyB = keyA + 16;
+    const bool wrB = w * 32 + 16 < TP;  // the phantom tile past the head (keys 208..223) is not written
+#pragma unroll 1
+    for (int sc = s0; sc < s1; ++sc) {
+      const int ua = 2 * sc * 16 + r, ub = ua + 16;
+      const bf16x8 qa0 = lds_row8(Qs, ua, g), qa1 = lds_row8(Qs, ua, 4 + g);
+      const bf16x8 da0 = lds_row8(Ds, ua, g), da1 = lds_row8(Ds, ua, 4 + g);
+      const bf16x8 qb0 = lds_row8(Qs, ub, g), qb1 = lds_row8(Qs, ub, 4 + g);
+      const bf16x8 db0 = lds_row8(Ds, ub, g), db1 = lds_row8(Ds, ub, 4 + g);
+      const f32x4 la = *(const f32x4*)(lse_s + 2 * sc * 16 + 4 * g);
+      const f32x4 dla = *(const f32x4*)(del_s + 2 * sc * 16 + 4 * g);
+      const f32x4 lb = *(const f32x4*)(lse_s + 2 * sc * 16 + 16 + 4 * g);
+      const f32x4 dlb = *(const f32x4*)(del_s + 2 * sc * 16 + 16 + 4 * g);
+      bf16x8 tdo[4], tq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        tdo[dt] = lds_trT(Ds, sc * 32, dt * 16, g, r);
+        tq[dt] = lds_trT(Qs, sc * 32, dt * 16, g, r);
+      }
+      const int ql = sc * 32 - qbase;
+      char* img = Ss + (ql >> 6) * IMG;
+      const int c = ((ql >> 5) & 1) * 4 + g;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x4 p0, p1, s0_, s1_;
+        p_ds(qa0, qa1, da0, da1, la, dla, kv[4 * kt], kv[4 * kt + 1], kv[4 * kt + 2], kv[4 * kt + 3], p0, s0_);
+        p_ds(qb0, qb1, db0, db1, lb, dlb, kv[4 * kt], kv[4 * kt + 1], kv[4 * kt + 2], kv[4 * kt + 3], p1, s1_);
+        bf16x8 pf, dsf;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          pf[i] = (bf16)p0[i];
+          pf[4 + i] = (bf16)p1[i];
+          dsf[i] = (bf16)s0_[i];
+          dsf[4 + i] = (bf16)s1_[i];
+        }
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[kt][dt] = mfma16(tdo[dt], pf, dv[kt][dt]);
+          dk[kt][dt] = mfma16(tq[dt], dsf, dk[kt][dt]);
+        }
+        const int key = kt ? keyB : keyA, f = sws(key);
+        const bf16x8 sw = (f & 1) ? __builtin_shufflevector(dsf, dsf, 4, 5, 6, 7, 0, 1, 2, 3) : dsf;
+        if (kt == 0 || wrB) *(bf16x8*)(img + key * 128 + (c ^ (f >> 1)) * 16) = key < T ? sw : zero8;
+      }
+    }
+    if (odd) {
+      const int u = NT16 - 1;
+      const bf16x8 q0 = lds_row8(Qs, u * 16 + r, g), q1 = lds_row8(Qs, u * 16 + r, 4 + g);
+      const bf16x8 d0 = lds_row8(Ds, u * 16 + r, g), d1 = lds_row8(Ds, u * 16 + r, 4 + g);
+      const f32x4 l4 = *(const f32x4*)(lse_s + u * 16 + 4 * g), d4 = *(const f32x4*)(del_s + u * 16 + 4 * g);
+      bf16x4 tdo4[4], tq4[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        tdo4[dt] = lds_trT4(Ds, u * 16, dt * 16, g, r);
+        tq4[dt] = lds_trT4(Qs, u * 16, dt * 16, g, r);
+      }
+      const int ql = u * 16 - qbase;
+      char* img = Ss + (ql >> 6) * IMG;
+      const int c = ((ql >> 5) & 1) * 4 + g;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        f32x4 p0, s0_;
+        p_ds(q0, q1, d0, d1, l4, d4, kv[4 * kt], kv[4 * kt + 1], kv[4 * kt + 2], kv[4 * kt + 3], p0, s0_);
+        const bf16x4 pf = {(bf16)p0[0], (bf16)p0[1], (bf16)p0[2], (bf16)p0[3]};
+        const bf16x4 dsf = {(bf16)s0_[0], (bf16)s0_[1], (bf16)s0_[2], (bf16)s0_[3]};
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[kt][dt] = mfma16k16(tdo4[dt], pf, dv[kt][dt]);
+          dk[kt][dt] = mfma16k16(tq4[dt], dsf, dk[kt][dt]);
+        }
+        const int key = kt ? keyB : keyA;
+        if (kt == 0 || wrB) *(bf16x4*)(img + key * 128 + ((2 * c) ^ sws(key)) * 8) = key < T ? dsf : zero4;
+      }
+    }
+  };
+  // phase 2: dQ of query tile `tile` (queries qbase.. in the dS images), out through the wave's slot
+  auto phase2 = [&](int bh, int tile, int qbase) {
+    const int l = fresh_lane(), g = l >> 4, r = l & 15;
+    const int ql = tile * 16 - qbase;
+    const char* img = Ss + (ql >> 6) * IMG;
+    const int seg = (ql >> 5) & 1, half = (ql >> 4) & 1;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 3
+    for (int sc = 0; sc < NP; ++sc) {
+      bf16x8 tk[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) tk[dt] = lds_trT(Ks, sc * 32, dt * 16, g, r);
+      const bf16x8 dsf = lds_trS(img, sc * 32, seg, half, g, r);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tk[dt], dsf, dq[dt]);
+    }
+    {
+      const int t = NT16 - 1;
+      bf16x4 tk4[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) tk4[dt] = lds_trT4(Ks, t * 16, dt * 16, g, r);
+      const bf16x4 dsf = lds_trS4(img, t * 16, seg, half, g, r);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16k16(tk4[dt], dsf, dq[dt]);
+    }
+    const int img_i = bh / a.H, h = bh - img_i * a.H, q0 = tile * 16;
+    tile_rows_out(slot, dq, a.scale, a.dqkv + ((size_t)img_i * T + q0) * a.lddqkv + h * 64, a.lddqkv, T - q0);
+  };
+
+  int hi = 0;
+  auto stamp = [&](int k) {
+    if constexpr (STAMP != 0) {
+      if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == 101) && hi < 16)
+        g_attn_stamps[blockIdx.x ? 1 : 0][w][hi][k] = __builtin_amdgcn_s_memtime();
+    }
+  };
+  int bh = blockIdx.x;
+  stamp(11);
+  stage_qdo(bh, 0, NG, 0);
+  stage_k(bh);
+  Pre pre = prefetch(bh);
+  const int nk = (NG - w + 7) / 8;  // this wave's K pieces: the youngest VMEM ops at the top of a head
+  for (;;) {
+    const int img = bh / a.H, h = bh - img * a.H;
+    const int nx = bh + gridDim.x;
+    const bool more = nx < nbh;
+    if (nk == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // Q / dO landed (K may be in flight)
+    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    lds_barrier();
+    stamp(0);
+    deltas(pre);
+    lds_barrier();
+    stamp(1);
+    f32x4 dk[2][4], dv[2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dk[t][dt] = dv[t][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 kv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) kv[j] = pre.kv[j];
+    if (w < (NT16 + 1) / 2) phase1(kv, dk, dv, 0, PA, false, 0);
+    stamp(2);
+    // this head's K; the builtin (vmcnt(0) hipcc sees) also retires the register prefetch on every path,
+    // so no later counted wait of hipcc's drains the DMAs issued below
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    lds_barrier();
+    stamp(3);
+    if (more) stage_qdo(nx, 0, PA * 32 / 8, 0);  // rows 0..127: phase 1 is done with them
+    phase2(bh, w, 0);
+    stamp(4);
+    lds_barrier();
+    stamp(5);
+    if (w < (NT16 + 1) / 2) {
+      phase1(kv, dk, dv, PA, NP, true, 2 * PA * 16);
+      bf16* d0 = a.dqkv + ((size_t)img * T + w * 32) * a.lddqkv + D + h * 64;
+      tile_rows_out(slot, dk[0], a.scale, d0, a.lddqkv, T - w * 32);
+      tile_rows_out(slot, dv[0], 1.0f, d0 + D, a.lddqkv, T - w * 32);
+      tile_rows_out(slot, dk[1], a.scale, d0 + 16 * (size_t)a.lddqkv, a.lddqkv, T - w * 32 - 16);
+      tile_rows_out(slot, dv[1], 1.0f, d0 + 16 * (size_t)a.lddqkv + D, a.lddqkv, T - w * 32 - 16);
+    }
+    stamp(6);
+    lds_barrier();
+    stamp(7);
+    if (more) stage_qdo(nx, PA * 32 / 8, NG, NT16 - 2 * PA);  // by the waves without a phase-2 tile
+    // unconditional (the last head re-reads its own rows): a conditional assignment would keep the old
+    // operands live through the phases for the join
+    pre = prefetch(more ? nx : bh);
+    if (w < NT16 - 2 * PA) phase2(bh, 2 * PA + w, 2 * PA * 16);
+    stamp(8);
+    lds_barrier();
+    stamp(9);
+    ++hi;
+    if (!more) break;
+    stage_k(nx);
+    bh = nx;
+  }
+}
+
 // ---- CLS-query attention (the last block: only the CLS rows reach the head) ---------------------
 // One wave per (image, head).  Lane (c = lane & 7, jg = lane >> 3) holds dims 8c..8c+7 and walks keys
 // j = jg, jg + 8, ...: each 8-lane group reads whole 128-B K / V rows (coalesced) and completes a
@@ -1418,6 +1785,26 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);   \
   }                                                                                                         \
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  if ((g_attn_bwd_pipe == 4 || g_attn_bwd_pipe == 5) && nt16 == 13 &&
+      (size_t)nimg * T * std::max(std::max(ldqkv, ldo), lddo) * 2 < ((size_t)1 << 31)) {
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    const size_t lds = 5 * (size_t)13 * 16 * 128 + 2 * 13 * 16 * 4 + 8 * 2048;
+    if (g_attn_bwd_pipe == 5) {
+      allow_lds(attn_bwd_fused_kernel<13, 1>, lds);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13, 1>), std::min(cus, nimg * H), 512, lds, stream, a,
+                         nimg * H);
+    } else {
+      allow_lds(attn_bwd_fused_kernel<13>, lds);
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), std::min(cus, nimg * H), 512, lds, stream, a,
+                         nimg * H);
+    }
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   if (g_attn_bwd_pipe && nt16 == 13) { BWD_VARIANTS(13) }
   if (g_attn_bwd_pipe && nt16 == 37 && g_attn_bwd_long) { BWD_VARIANTS(37) }
 #undef BWD_VARIANTS
@@ -1426,6 +1813,12 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+
+// (measurement) the single-pass kernel's phase stamps of workgroups 0 and 101 (variant 5): 2 x 8 x 16 x 12 u64
+int es_attn_bwd_stamps(void* host_out) {
+  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? ES_OK
+                                                                                                       : ES_HIP_ERROR;
+}
 
 // CLS-query attention of a block whose non-CLS outputs are unused (the ViT's last block): qkv
 // [nimg*T, ldqkv] -> o [nimg, ldo] (the CLS rows only, compact), lse [nimg*H].

@@ -33,7 +33,10 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--s1", action="store_true", help="the S1 shape instead: 120 images x 12 heads x 577 tokens "
                     "(Conformer-B at 384^2, the long-sequence kernels)")
+    ap.add_argument("--bwd", default="0,1,2,3,4", help="backward variants to time (es_set_attn_bwd_variant)")
+    ap.add_argument("--no-fwd", action="store_true", help="skip the forward occupancy variants")
     args = ap.parse_args()
+    bwd_vs = [int(v) for v in args.bwd.split(",")]
     lib = _lib.load()
     n, T, H = (120, 577, 12) if args.s1 else (512, 197, 6)
     D = 64 * H
@@ -50,28 +53,33 @@ def main():
     bwd = lambda: call("es_attn_bwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), ptr(delta), ptr(do), D, ptr(dqkv),  # noqa
                        3 * D, n, T, H, 0.125, s)
     res = {"fwd_occ2": [], "fwd_occ3": [], "fwd_occ7": [], "bwd_plain": [], "bwd_pipe": [], "bwd_dkv2": [],
-           "bwd_dq2_dkv2": []}
+           "bwd_dq2_dkv2": [], "bwd_fused": []}
     outs = {}
     for _ in range(args.rounds):
-        for occ in (2, 3, 7):  # 7: seven waves per workgroup (T = 197)
+        for occ in (() if args.no_fwd else (2, 3, 7)):  # 7: seven waves per workgroup (T = 197)
             lib.es_set_attn_variant(occ)
             res[f"fwd_occ{occ}"].append(timed(fwd, args.iters))
             outs[f"fwd_occ{occ}"] = (o.clone(), lse.clone())
         lib.es_set_attn_variant(2)
         fwd()
-        for v, name in ((0, "bwd_plain"), (1, "bwd_pipe"), (2, "bwd_dkv2"), (3, "bwd_dq2_dkv2")):
+        for v, name in ((0, "bwd_plain"), (1, "bwd_pipe"), (2, "bwd_dkv2"), (3, "bwd_dq2_dkv2"), (4, "bwd_fused")):
+            if v not in bwd_vs:
+                continue
             lib.es_set_attn_bwd_variant(v)
             res[name].append(timed(bwd, args.iters))
             outs[name] = dqkv.clone()
     lib.es_set_attn_bwd_variant(1)
-    print("fwd occ7 == occ2 (bit-exact):", all(torch.equal(x, y) for x, y in zip(outs["fwd_occ7"], outs["fwd_occ2"])),
-          flush=True)
-    print("bwd pipe == plain (bit-exact):", torch.equal(outs["bwd_pipe"], outs["bwd_plain"]),
-          "dkv2 == plain:", torch.equal(outs["bwd_dkv2"], outs["bwd_plain"]),
-          "dq2 + dkv2 == plain:", torch.equal(outs["bwd_dq2_dkv2"], outs["bwd_plain"]), flush=True)
+    if not args.no_fwd:
+        print("fwd occ7 == occ2 (bit-exact):",
+              all(torch.equal(x, y) for x, y in zip(outs["fwd_occ7"], outs["fwd_occ2"])), flush=True)
+    if "bwd_plain" in outs:
+        print("bwd == plain (bit-exact):", {k: torch.equal(v, outs["bwd_plain"]) for k, v in outs.items()
+                                            if k.startswith("bwd_")}, flush=True)
     flops_f = 4.0 * n * H * T * T * 64
     out = {}
     for k, v in res.items():
+        if not v:
+            continue
         t = sorted(v)[len(v) // 2]
         fl = flops_f if k.startswith("fwd") else 2.5 * flops_f
         out[k] = {"ms": round(t, 4), "tflops": round(fl / t / 1e9, 1)}

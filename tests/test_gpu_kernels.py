@@ -450,12 +450,14 @@ def test_attention_bwd(n, T, H):
     assert torch.all(dqkv[n * T:] == 0)
 
 
-@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (64, 197, 6), (3, 577, 12), (2, 300, 2)])
+@pytest.mark.parametrize("n,T,H", [(3, 197, 6), (64, 197, 6), (160, 197, 6), (3, 208, 2), (5, 193, 1), (3, 577, 12),
+                                   (2, 300, 2)])
 def test_attention_bwd_pipelined_matches_plain(n, T, H):
     """The software-pipelined dQ / dK-dV loops (es_set_attn_bwd_variant 1), the two-key-tiles-per-wave
-    dK / dV (2) and two-query-tiles dQ (3) issue the same MFMAs on the same operands in the same order per
-    tile as the plain loops (0): dqkv and delta bit-identical, at T = 197 (13 tiles) and in the 37-tile
-    kernels (T = 577, and T = 300 with masked rows)."""
+    dK / dV (2), two-query-tiles dQ (3) and the single-pass kernel (4, 13 tiles: 192 < T <= 208; persistent,
+    so 960 heads run several per workgroup) issue the same MFMAs on the same operands in the same order per
+    tile as the plain loops (0): dqkv bit-identical (and delta, which the single pass keeps on chip), at
+    T = 197 and in the 37-tile kernels (T = 577, and T = 300 with masked rows)."""
     D = H * 64
     torch.manual_seed(7 + n)
     qkv = _pad_rows(torch.randn(n * T, 3 * D, device=DEV).bfloat16())
@@ -465,7 +467,7 @@ def test_attention_bwd_pipelined_matches_plain(n, T, H):
     call("es_attn_fwd", ptr(qkv), 3 * D, ptr(o), D, ptr(lse), n, T, H, 64 ** -0.5, S())
     res = {}
     lib = _lib.load()
-    for v in (0, 1, 2, 3):
+    for v in (0, 1, 2, 3, 4):
         old = lib.es_set_attn_bwd_variant(v)
         dqkv = torch.full_like(qkv, 3.0)
         delta = torch.zeros(n * H * T, device=DEV)
@@ -474,9 +476,10 @@ def test_attention_bwd_pipelined_matches_plain(n, T, H):
         torch.cuda.synchronize()
         lib.es_set_attn_bwd_variant(old)
         res[v] = (dqkv[:n * T].clone(), delta)
-    for v in (1, 2, 3):
+    for v in (1, 2, 3, 4):
         assert torch.equal(res[0][0], res[v][0]), v
-        assert torch.equal(res[0][1], res[v][1]), v
+        if v != 4 or (T + 15) // 16 != 13:
+            assert torch.equal(res[0][1], res[v][1]), v
 
 
 @pytest.mark.parametrize("n,T,H", [(3, 197, 6), (5, 17, 2), (2, 250, 2), (3, 40, 1), (2, 1, 1), (4, 256, 1),
