@@ -1186,9 +1186,7 @@ __device__ __forceinline__ void bl16_m0(i32x4 rsrc, unsigned voff, unsigned soff
 // LDS writes visible to the workgroup; VMEM (DMA, stores) left in flight
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-__device__ unsigned long long g_attn_stamps[2][8][16][12];  // (measurement) workgroups 0 / 101
-
-template <int NT16, int STAMP = 0>
+template <int NT16>
 __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh) {
   static_assert(NT16 == 13, "rounds of 8 + 5 query tiles, 7 key-tile pairs over 8 waves");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1200,7 +1198,7 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
   float* lse_s = (float*)(smem + 5 * IMG);
   float* del_s = lse_s + TP;
   // the wave index in a scalar register: wave-uniform branches and loop trips stay scalar
-  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   char* slot = (char*)(del_s + TP) + w * 2048;
   const unsigned lds0 = lds_addr(smem);  // LDS byte address of the dynamic allocation
   const int D = a.H * 64, T = a.T;
@@ -1224,40 +1222,41 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
   const auto bLSE = buf_rsrc(a.lse, (unsigned)nbh * T * 4u);
 
   // 8-row groups [i0, i1) of a head image (rows >= T re-read row T - 1; colb: the head's byte column, ldb: the
-  // row pitch in bytes, base: the image's first byte), by waves w0..7: this wave's share groups i0 + w - w0,
-  // + 8 - w0, ..
-  auto stage = [&](const char* lds, i32x4 rs, unsigned base, unsigned colb, unsigned ldb, int i0, int i1, int w0) {
+  // row pitch in bytes, base: the image's first byte), by waves w0 .. w0 + nw - 1: this wave's share groups
+  // i0 + w - w0, + nw, ..
+  auto stage = [&](const char* lds, i32x4 rs, unsigned base, unsigned colb, unsigned ldb, int i0, int i1, int w0,
+                   int nw) {
     const int l = fresh_lane();
     const unsigned dst = lds0 + (unsigned)(lds - smem);
-    for (int i = i0 + w - w0; w >= w0 && i < i1; i += 8 - w0) {
+    for (int i = i0 + w - w0; w >= w0 && w < w0 + nw && i < i1; i += nw) {
       const int row = i * 8 + (l >> 3);
       const int sr = row < T ? row : T - 1;
       bl16_m0(rs, (unsigned)sr * ldb + colb + aswz(row, l & 7) * 16, base, dst + i * 1024);
     }
   };
-  auto stage_qdo = [&](int bh, int i0, int i1, int w0) {
+  auto stage_qdo = [&](int bh, int i0, int i1, int w0, int nw) {
     const int img = bh / a.H, h = bh - img * a.H;
-    stage(Qs, sQKV, (unsigned)img * T * a.ldqkv * 2u, h * 128, a.ldqkv * 2, i0, i1, w0);
-    stage(Ds, sDO, (unsigned)img * T * a.lddo * 2u, h * 128, a.lddo * 2, i0, i1, w0);
+    stage(Qs, sQKV, (unsigned)img * T * a.ldqkv * 2u, h * 128, a.ldqkv * 2, i0, i1, w0, nw);
+    stage(Ds, sDO, (unsigned)img * T * a.lddo * 2u, h * 128, a.lddo * 2, i0, i1, w0, nw);
   };
   auto stage_k = [&](int bh) {
     const int img = bh / a.H, h = bh - img * a.H;
-    stage(Ks, sQKV, (unsigned)img * T * a.ldqkv * 2u, (D + h * 64) * 2, a.ldqkv * 2, 0, NG, 0);
+    stage(Ks, sQKV, (unsigned)img * T * a.ldqkv * 2u, (D + h * 64) * 2, a.ldqkv * 2, 0, NG, 0, 8);
   };
 
-  // register operands of a head: O rows of the wave's delta tiles (w, w + 8), K / V rows of its key tiles
-  // (2w, 2w + 1), the lse of query threadIdx.x -- buffer loads, rows past T read as zero
+  // register operands of a head: O rows of the wave's delta tiles (w, w + 8), V rows of its key tiles
+  // (2w, 2w + 1; the K rows come from the K image), the lse of query threadIdx.x -- buffer loads, rows past
+  // T read as zero
   struct Pre {
     bf16x8 o[2][2];
-    bf16x8 kv[8];
+    bf16x8 v[4];
     float lse;
   };
   auto prefetch = [&](int bh) {
     Pre p;
     const int l = fresh_lane(), g = l >> 4, r = l & 15;
     const int img = bh / a.H, h = bh - img * a.H;
-    // in order of use (lse and O by the deltas, K / V by phase 1): hipcc's counted waits for the early ones
-    // then leave the younger K-image DMA in flight
+    // in order of use (lse and O by the deltas, V by phase 1)
     const int tq = l + 64 * w;
     p.lse = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                                           bLSE, tq < T ? (unsigned)(bh * T + tq) * 4u : ES_OOB, 0, 0));
@@ -1271,11 +1270,9 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int key = w * 32 + 16 * t + r;
-      const unsigned off = key < T ? (unsigned)((img * T + key) * a.ldqkv + D + h * 64 + 8 * g) * 2u : ES_OOB;
-      p.kv[4 * t + 0] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off));
-      p.kv[4 * t + 1] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 64));
-      p.kv[4 * t + 2] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 2 * D));
-      p.kv[4 * t + 3] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 2 * D + 64));
+      const unsigned off = key < T ? (unsigned)((img * T + key) * a.ldqkv + 2 * D + h * 64 + 8 * g) * 2u : ES_OOB;
+      p.v[2 * t + 0] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off));
+      p.v[2 * t + 1] = __builtin_bit_cast(bf16x8, buf_load16(bQKV, off + 64));
     }
     return p;
   };
@@ -1426,16 +1423,8 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
     tile_rows_out(slot, dq, a.scale, a.dqkv + ((size_t)img_i * T + q0) * a.lddqkv + h * 64, a.lddqkv, T - q0);
   };
 
-  int hi = 0;
-  auto stamp = [&](int k) {
-    if constexpr (STAMP != 0) {
-      if (lane == 0 && (blockIdx.x == 0 || blockIdx.x == 101) && hi < 16)
-        g_attn_stamps[blockIdx.x ? 1 : 0][w][hi][k] = __builtin_amdgcn_s_memtime();
-    }
-  };
   int bh = blockIdx.x;
-  stamp(11);
-  stage_qdo(bh, 0, NG, 0);
+  stage_qdo(bh, 0, NG, 0, 8);
   stage_k(bh);
   Pre pre = prefetch(bh);
   const int nk = (NG - w + 7) / 8;  // this wave's K pieces: the youngest VMEM ops at the top of a head
@@ -1446,50 +1435,53 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
     if (nk == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // Q / dO landed (K may be in flight)
     else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
     lds_barrier();
-    stamp(0);
     deltas(pre);
+    // this head's K image (DMA'd behind the previous head's last phase) and the register prefetch; the builtin
+    // (a vmcnt(0) hipcc sees) retires the prefetch on every path, so no later counted wait of hipcc's drains
+    // the DMAs issued below
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     lds_barrier();
-    stamp(1);
     f32x4 dk[2][4], dv[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dk[t][dt] = dv[t][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    bf16x8 kv[8];
+    bf16x8 kv[8];  // per key tile t: K dims 8g.. / 32 + 8g.., V the same (zero past T)
+    {
+      const int l = fresh_lane(), g = l >> 4, r = l & 15;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) kv[j] = pre.kv[j];
+      for (int t = 0; t < 2; ++t) {
+        const int key = w * 32 + 16 * t + r;
+        const bf16x8 k0 = lds_row8(Ks, key < TP ? key : 0, g), k1 = lds_row8(Ks, key < TP ? key : 0, 4 + g);
+        kv[4 * t + 0] = key < T ? k0 : zero8;
+        kv[4 * t + 1] = key < T ? k1 : zero8;
+        kv[4 * t + 2] = pre.v[2 * t];
+        kv[4 * t + 3] = pre.v[2 * t + 1];
+      }
+    }
     if (w < (NT16 + 1) / 2) phase1(kv, dk, dv, 0, PA, false, 0);
-    stamp(2);
-    // this head's K; the builtin (vmcnt(0) hipcc sees) also retires the register prefetch on every path,
-    // so no later counted wait of hipcc's drains the DMAs issued below
-    __builtin_amdgcn_s_waitcnt(0x0F70);
     lds_barrier();
-    stamp(3);
-    if (more) stage_qdo(nx, 0, PA * 32 / 8, 0);  // rows 0..127: phase 1 is done with them
+    if (more) stage_qdo(nx, 0, PA * 32 / 8, 0, 8);  // rows 0..127: phase 1 is done with them
     phase2(bh, w, 0);
-    stamp(4);
     lds_barrier();
-    stamp(5);
+    if (w < (NT16 + 1) / 2) phase1(kv, dk, dv, PA, NP, true, 2 * PA * 16);
+    lds_barrier();
+    // the round-2 tiles go to waves 3..7, the next head's DMAs to waves 0..2; every wave's loads issue before
+    // its dK / dV stores (stores issue at ~14 B/clk per CU: VMEM ops behind them would wait)
+    constexpr int W2 = 8 - (NT16 - 2 * PA);
+    if (more) stage_qdo(nx, PA * 32 / 8, NG, 0, W2);
+    // unconditional (the last head re-reads its own rows): a conditional assignment would keep the old
+    // operands live through the phases for the join
+    pre = prefetch(more ? nx : bh);
+    if (w >= W2) phase2(bh, 2 * PA + w - W2, 2 * PA * 16);
     if (w < (NT16 + 1) / 2) {
-      phase1(kv, dk, dv, PA, NP, true, 2 * PA * 16);
       bf16* d0 = a.dqkv + ((size_t)img * T + w * 32) * a.lddqkv + D + h * 64;
       tile_rows_out(slot, dk[0], a.scale, d0, a.lddqkv, T - w * 32);
       tile_rows_out(slot, dv[0], 1.0f, d0 + D, a.lddqkv, T - w * 32);
       tile_rows_out(slot, dk[1], a.scale, d0 + 16 * (size_t)a.lddqkv, a.lddqkv, T - w * 32 - 16);
       tile_rows_out(slot, dv[1], 1.0f, d0 + 16 * (size_t)a.lddqkv + D, a.lddqkv, T - w * 32 - 16);
     }
-    stamp(6);
     lds_barrier();
-    stamp(7);
-    if (more) stage_qdo(nx, PA * 32 / 8, NG, NT16 - 2 * PA);  // by the waves without a phase-2 tile
-    // unconditional (the last head re-reads its own rows): a conditional assignment would keep the old
-    // operands live through the phases for the join
-    pre = prefetch(more ? nx : bh);
-    if (w < NT16 - 2 * PA) phase2(bh, 2 * PA + w, 2 * PA * 16);
-    stamp(8);
-    lds_barrier();
-    stamp(9);
-    ++hi;
     if (!more) break;
     stage_k(nx);
     bh = nx;
@@ -1688,9 +1680,10 @@ __global__ __launch_bounds__(64) void attn_cls_bwd_kernel(const bf16* __restrict
 int g_attn_fwd_occ = 7;
 // backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 2 = the pipelined dQ
 // and the two-key-tiles-per-wave dK / dV (attn_bwd_dkv2_kernel), 3 = two query tiles per wave for dQ
-// (attn_bwd_dq2_kernel) and dkv2, 0 = the plain loops (all bit-identical).  Default 3: 0.257 ms vs 0.269 (1) and
-// 0.289 (0) for the F1 head batch in isolation, F1 32.51-32.56 vs 32.69-32.72 ms (scripts/attn_bench.py, same box)
-int g_attn_bwd_pipe = 3;
+// (attn_bwd_dq2_kernel) and dkv2, 4 = the single pass (attn_bwd_fused_kernel; 13-tile heads, others as 3),
+// 0 = the plain loops (all bit-identical).  Default 4: 0.210 ms vs 0.258 (3) for the F1 head batch in isolation
+// (scripts/attn_bench.py, same box; round 3: 3 at 0.257 vs 0.269 (1) and 0.289 (0))
+int g_attn_bwd_pipe = 4;
 // the same variants for T = 577 (the 37-tile kernels: one 151-KiB head per CU, four waves)
 int g_attn_bwd_long = 1;
 
@@ -1785,7 +1778,7 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);   \
   }                                                                                                         \
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-  if ((g_attn_bwd_pipe == 4 || g_attn_bwd_pipe == 5) && nt16 == 13 &&
+  if (g_attn_bwd_pipe == 4 && nt16 == 13 &&
       (size_t)nimg * T * std::max(std::max(ldqkv, ldo), lddo) * 2 < ((size_t)1 << 31)) {
     static int cus = 0;
     if (!cus) {
@@ -1794,15 +1787,9 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
       if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     }
     const size_t lds = 5 * (size_t)13 * 16 * 128 + 2 * 13 * 16 * 4 + 8 * 2048;
-    if (g_attn_bwd_pipe == 5) {
-      allow_lds(attn_bwd_fused_kernel<13, 1>, lds);
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13, 1>), std::min(cus, nimg * H), 512, lds, stream, a,
-                         nimg * H);
-    } else {
-      allow_lds(attn_bwd_fused_kernel<13>, lds);
-      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), std::min(cus, nimg * H), 512, lds, stream, a,
-                         nimg * H);
-    }
+    allow_lds(attn_bwd_fused_kernel<13>, lds);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), std::min(cus, nimg * H), 512, lds, stream, a,
+                       nimg * H);
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   if (g_attn_bwd_pipe && nt16 == 13) { BWD_VARIANTS(13) }
@@ -1813,12 +1800,6 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-
-// (measurement) the single-pass kernel's phase stamps of workgroups 0 and 101 (variant 5): 2 x 8 x 16 x 12 u64
-int es_attn_bwd_stamps(void* host_out) {
-  return hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_attn_stamps), sizeof(g_attn_stamps)) == hipSuccess ? ES_OK
-                                                                                                       : ES_HIP_ERROR;
-}
 
 // CLS-query attention of a block whose non-CLS outputs are unused (the ViT's last block): qkv
 // [nimg*T, ldqkv] -> o [nimg, ldo] (the CLS rows only, compact), lse [nimg*H].

@@ -115,7 +115,8 @@ int es_set_attn_bwd_long(int v);
 /* ---- attention (code/models/conformer.py:40-50), head dim 64, tokens T <= 592 (384^2 / 16) ------ */
 int es_attn_fwd(const void* qkv, int ldqkv, void* o, int ldo, float* lse, int nimg, int T, int H, float scale,
                 hipStream_t stream);
-/* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass) */
+/* delta: fp32 workspace [nimg*H*T] (rowsum(dO*O), produced by the dQ pass for the dK/dV pass; the single-pass
+   kernel that 13-tile heads (192 < T <= 208) use by default keeps it on chip and leaves the workspace untouched) */
 int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float* lse, float* delta, const void* dout,
                 int lddo, void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
 /* CLS-query attention for a block whose non-CLS outputs are unused (the last block: only the CLS

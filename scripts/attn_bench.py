@@ -68,7 +68,7 @@ def main():
             lib.es_set_attn_bwd_variant(v)
             res[name].append(timed(bwd, args.iters))
             outs[name] = dqkv.clone()
-    lib.es_set_attn_bwd_variant(1)
+    lib.es_set_attn_bwd_variant(4)
     if not args.no_fwd:
         print("fwd occ7 == occ2 (bit-exact):",
               all(torch.equal(x, y) for x, y in zip(outs["fwd_occ7"], outs["fwd_occ2"])), flush=True)
