@@ -141,10 +141,13 @@ def host_input_run(tr, B, MU, steps, dev):
             "source": "synthetic decoded RGB 500x375 frames (64), IS_CROP, S=224; decode not timed"}
 
 
-def cpu_baseline(B=8, MU=7, steps=2):
+def cpu_baseline(B=64, MU=7, steps=1, warmup=0):
     """Oracle (pinned CPU restatement) FixMatch step on every host core this process may use -- a
     reported baseline (torch.set_num_threads(os.cpu_count()), capped by the CPU share the
-    box grants: more threads than cores only oversubscribes)."""
+    box grants: more threads than cores only oversubscribes).  Default: the full F1 batch (B=64, mu=7:
+    ~100 GB of fp32 autograd activations, within the ~270 GiB a GPU-box job may hold) for one step without a
+    separate warm-up (the timed step includes first-touch allocation; ~70 s); --cpu-batch 8 --cpu-steps 2
+    --cpu-warmup 1 is the round-3 sample."""
     from oracle import ref
     threads, cpu_info = host_cpus()
     prev = torch.get_num_threads()
@@ -157,8 +160,9 @@ def cpu_baseline(B=8, MU=7, steps=2):
     y = torch.randint(0, 23, (B,), generator=g)
     uw = synth_images(B * MU, 224, g, "cpu")
     us = synth_images(B * MU, 224, g, "cpu")
-    fm.step(x, y, uw, us)  # warm-up
-    print(f"cpu_baseline: warm-up step done on {threads} threads", file=sys.stderr, flush=True)
+    for _ in range(warmup):
+        fm.step(x, y, uw, us)
+        print(f"cpu_baseline: warm-up step done on {threads} threads", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     for i in range(steps):
         fm.step(x, y, uw, us)
@@ -184,9 +188,9 @@ def cpu_baseline(B=8, MU=7, steps=2):
         pass
     return {"value": round(B * MU / dt, 3), "unit": "unlabeled images/s", "cores": used,
             "kind": "port",
-            "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step; the "
-                      f"F1 batch B=64 would hold ~100 GB of fp32 autograd activations and ~10x the CPU time), "
-                      f"1 warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', host CPUs {cpu_info}, "
+            "sample": f"oracle FixMatch step, ViT-S/16 224^2 fp32, B={B} mu={MU} ({B * MU} unlabeled imgs/step"
+                      f"{'; the full F1 batch' if B == 64 else '; a reduced batch, not the F1 B=64'}), "
+                      f"{warmup} warm-up + {steps} timed steps, {dt:.2f} s/step, cpu='{cpu}', host CPUs {cpu_info}, "
                       f"host RAM {mem} (the job may use at most ~270 GiB of it), torch.get_num_threads()={used}"}
 
 
@@ -469,6 +473,9 @@ def main():
     ap.add_argument("--mu", type=int, default=7)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=64, help="cpu_baseline labeled batch B (64 = the F1 batch)")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-warmup", type=int, default=0)
     ap.add_argument("--inputs", choices=("u8", "f32"), default="u8",
                     help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")
     ap.add_argument("--workload", choices=("f1", "c1", "s1", "p0"), default="f1",
@@ -744,7 +751,7 @@ def main():
         if host_input is not None:
             res["host_input"] = host_input
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline()
+            res["cpu_baseline"] = cpu_baseline(B=args.cpu_batch, steps=args.cpu_steps, warmup=args.cpu_warmup)
         print(json.dumps(res), flush=True)
     dist.barrier()
 

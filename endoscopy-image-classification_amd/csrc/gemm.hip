@@ -1168,10 +1168,6 @@ extern "C" {
 int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                   float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream);
 
-// gemm_panel.hip: the activation-stationary K = 384 kernel (variant 30)
-int es_panel_gemm(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
-                  void* C2, const void* aux, int ldaux, int M, int N, int K, int stores_nt, hipStream_t stream);
-
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C,
                int ldc, void* C2, const void* aux, int ldaux, int M, int N, int K, int np,
                hipStream_t stream) {
@@ -1243,12 +1239,6 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     }
 #undef L2
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
-  }
-  if (variant == 30 || variant == 31 || (variant >= 41 && variant <= 44)) {  // 31: plain C stores; 41-44 probes
-    const int rc = es_panel_gemm(epi, A, lda, B, ldb, bias, C, ldc, C2, aux, ldaux, M, N, K,
-                                 variant >= 41 ? variant : variant == 30, stream);
-    if (rc != ES_BAD_SHAPE) return rc;
-    variant = 0;
   }
   if (variant == 6 || variant == 10) {
     const int tbn = variant == 6 ? 256 : 128;
