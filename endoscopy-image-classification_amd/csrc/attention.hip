@@ -85,6 +85,22 @@ __device__ __forceinline__ bf16x8 ld_row8(const bf16* p, bool valid) {
   return *(const bf16x8*)p;
 }
 
+// The left or right half of tile_rows_out's tile (acc[0..1]: columns dt*16 + 4g .. + 3 of 32): through 1 KiB
+// of the wave's slot (64-B rows, 16-B chunk c of row i at c ^ ((i >> 1) & 3)) and out as one 16-B store per
+// lane (64-B row segments).  Same values as tile_rows_out's.
+__device__ __forceinline__ void half_rows_out(char* slot, const f32x4* acc, float s, bf16* dst, size_t ld, int nrows) {
+  const int lane = threadIdx.x & 63, g = lane >> 4, r = lane & 15;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt)
+    *(bf16x4*)(slot + r * 64 + (((2 * dt + (g >> 1)) ^ ((r >> 1) & 3)) * 16) + (g & 1) * 8) =
+        bf16x4{(bf16)(acc[dt][0] * s), (bf16)(acc[dt][1] * s), (bf16)(acc[dt][2] * s), (bf16)(acc[dt][3] * s)};
+  __builtin_amdgcn_wave_barrier();
+  const int rr = lane >> 2, ch = lane & 3;
+  const bf16x8 x = *(const bf16x8*)(slot + rr * 64 + ((ch ^ ((rr >> 1) & 3)) * 16));
+  if (rr < nrows) *(bf16x8*)(dst + rr * ld + ch * 8) = x;
+  __builtin_amdgcn_wave_barrier();
+}
+
 // A 16 x 64 output tile in the MFMA C layout (lane (g, r) holds row r, columns dt*16 + 4g .. +3 of acc[dt]),
 // bf16(acc * s) out to rows dst + i * ld, i < nrows.  Direct stores would write 16 rows x 32 B per
 // instruction (partial lines: the forward's WRITE_SIZE was 137 MB per F1 launch against 80 MB of o + lse),
@@ -1393,35 +1409,42 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
     }
   };
   // phase 2: dQ of query tile `tile` (queries qbase.. in the dS images), out through the wave's slot
-  auto phase2 = [&](int bh, int tile, int qbase) {
+  // NDT = 4: the whole tile; NDT = 2: its dims 32 hd .. + 31 (the second round, where five tiles meet eight
+  // waves, runs ten halves).  Per 16-dim block the same MFMAs in the same order either way.
+  auto phase2 = [&](auto ndt_tag, int bh, int tile, int hd, int qbase) {
+    constexpr int NDT = decltype(ndt_tag)::value;
     const int l = fresh_lane(), g = l >> 4, r = l & 15;
     const int ql = tile * 16 - qbase;
     const char* img = Ss + (ql >> 6) * IMG;
-    const int seg = (ql >> 5) & 1, half = (ql >> 4) & 1;
-    f32x4 dq[4];
+    const int seg = (ql >> 5) & 1, half = (ql >> 4) & 1, d0 = NDT == 4 ? 0 : 2 * hd;
+    f32x4 dq[NDT];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int dt = 0; dt < NDT; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 3
     for (int sc = 0; sc < NP; ++sc) {
-      bf16x8 tk[4];
+      bf16x8 tk[NDT];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) tk[dt] = lds_trT(Ks, sc * 32, dt * 16, g, r);
+      for (int dt = 0; dt < NDT; ++dt) tk[dt] = lds_trT(Ks, sc * 32, (d0 + dt) * 16, g, r);
       const bf16x8 dsf = lds_trS(img, sc * 32, seg, half, g, r);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(tk[dt], dsf, dq[dt]);
+      for (int dt = 0; dt < NDT; ++dt) dq[dt] = mfma16(tk[dt], dsf, dq[dt]);
     }
     {
       const int t = NT16 - 1;
-      bf16x4 tk4[4];
+      bf16x4 tk4[NDT];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) tk4[dt] = lds_trT4(Ks, t * 16, dt * 16, g, r);
+      for (int dt = 0; dt < NDT; ++dt) tk4[dt] = lds_trT4(Ks, t * 16, (d0 + dt) * 16, g, r);
       const bf16x4 dsf = lds_trS4(img, t * 16, seg, half, g, r);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16k16(tk4[dt], dsf, dq[dt]);
+      for (int dt = 0; dt < NDT; ++dt) dq[dt] = mfma16k16(tk4[dt], dsf, dq[dt]);
     }
     const int img_i = bh / a.H, h = bh - img_i * a.H, q0 = tile * 16;
-    tile_rows_out(slot, dq, a.scale, a.dqkv + ((size_t)img_i * T + q0) * a.lddqkv + h * 64, a.lddqkv, T - q0);
+    bf16* dst = a.dqkv + ((size_t)img_i * T + q0) * a.lddqkv + h * 64 + d0 * 16;
+    if constexpr (NDT == 4) tile_rows_out(slot, dq, a.scale, dst, a.lddqkv, T - q0);
+    else half_rows_out(slot, dq, a.scale, dst, a.lddqkv, T - q0);
   };
+  using Whole = std::integral_constant<int, 4>;
+  using Half = std::integral_constant<int, 2>;
 
   int bh = blockIdx.x;
   stage_qdo(bh, 0, NG, 0, 8);
@@ -1462,18 +1485,25 @@ __global__ __launch_bounds__(512) void attn_bwd_fused_kernel(AttnArgs a, int nbh
     if (w < (NT16 + 1) / 2) phase1(kv, dk, dv, 0, PA, false, 0);
     lds_barrier();
     if (more) stage_qdo(nx, 0, PA * 32 / 8, 0, 8);  // rows 0..127: phase 1 is done with them
-    phase2(bh, w, 0);
+    phase2(Whole{}, bh, w, 0, 0);
     lds_barrier();
     if (w < (NT16 + 1) / 2) phase1(kv, dk, dv, PA, NP, true, 2 * PA * 16);
     lds_barrier();
-    // the round-2 tiles go to waves 3..7, the next head's DMAs to waves 0..2; every wave's loads issue before
-    // its dK / dV stores (stores issue at ~14 B/clk per CU: VMEM ops behind them would wait)
-    constexpr int W2 = 8 - (NT16 - 2 * PA);
-    if (more) stage_qdo(nx, PA * 32 / 8, NG, 0, W2);
+    // every wave's loads issue before its dK / dV stores (stores issue at ~14 B/clk per CU: VMEM ops behind
+    // them would wait); the round-2 dQ as ten half tiles: waves 0..6 one each beside their dK / dV stores,
+    // wave 7 (no key tiles) three
+    if (more) stage_qdo(nx, PA * 32 / 8, NG, 0, 8);
     // unconditional (the last head re-reads its own rows): a conditional assignment would keep the old
     // operands live through the phases for the join
     pre = prefetch(more ? nx : bh);
-    if (w >= W2) phase2(bh, 2 * PA + w - W2, 2 * PA * 16);
+    static_assert(2 * (NT16 - 2 * PA) == 10, "ten half tiles");
+    if (w < 7) {
+      phase2(Half{}, bh, 2 * PA + (w >> 1), w & 1, 2 * PA * 16);
+    } else {
+      phase2(Half{}, bh, 2 * PA + 3, 1, 2 * PA * 16);
+      phase2(Half{}, bh, 2 * PA + 4, 0, 2 * PA * 16);
+      phase2(Half{}, bh, 2 * PA + 4, 1, 2 * PA * 16);
+    }
     if (w < (NT16 + 1) / 2) {
       bf16* d0 = a.dqkv + ((size_t)img * T + w * 32) * a.lddqkv + D + h * 64;
       tile_rows_out(slot, dk[0], a.scale, d0, a.lddqkv, T - w * 32);
