@@ -816,11 +816,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_pipe_kernel(AttnArgs a) {
 // second tile past the head (odd tile count) computes on zero K / V rows and stores nothing.  Per key
 // tile the operands, MFMAs, rounding points and fp32 accumulation order are those of
 // attn_bwd_dkv_kernel: bit-identical dK / dV.
-template <int NT16, bool SELF_DELTA = false>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
+template <int NT16, bool SELF_DELTA = false, int NW = 4>  // NW waves: 4, or 6 for the 37-tile heads
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dkv2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
-  constexpr int SLOT_ROWS = NT16 <= 16 ? 16 : 8;  // + 4 x 2 KiB of LDS (1 KiB per wave at 37 tiles: 160 KiB)
+  constexpr int SLOT_ROWS = NT16 <= 16 ? 16 : 8;  // + NW x 2 KiB of LDS (1 KiB per wave at 37 tiles)
   constexpr int NP = NT16 / 2;
   const int bh = blockIdx.x, img = bh / a.H, h = bh - img * a.H;
   const int D = a.H * 64, T = a.T;
@@ -829,8 +829,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
   char* Ds = smem + TP * 128;
   float* lse_s = (float*)(smem + 2 * TP * 128);
   float* del_s = lse_s + TP;
-  stage_head(Qs, base + h * 64, a.ldqkv, T, TP);
-  stage_head(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
+  stage_head<NW>(Qs, base + h * 64, a.ldqkv, T, TP);
+  stage_head<NW>(Ds, a.dout + (size_t)img * T * a.lddo + h * 64, a.lddo, T, TP);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   for (int t = threadIdx.x; t < TP; t += blockDim.x)
     lse_s[t] = t < T ? a.lse[(size_t)bh * T + t] * 1.44269504088896341f : INFINITY;
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int t0 = 0; t0 < TP; t0 += 64) {
+    for (int t0 = 0; t0 < TP; t0 += NW * 16) {
       const int tq = t0 + (threadIdx.x >> 2), part = threadIdx.x & 3;
       float dsum = 0.f;
       if (tq < T) {
@@ -877,7 +877,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
 
   const int nkt = (T + 15) >> 4;
   const int nitems = (nkt + 1) >> 1;
-  for (int kp = w; kp < nitems; kp += 4) {
+  for (int kp = w; kp < nitems; kp += NW) {
     const int keyA = kp * 32 + r, keyB = keyA + 16;
     const bool kvA = keyA < T, kvB = keyB < T;
     const bf16* krA = base + (size_t)keyA * a.ldqkv + D + h * 64;
@@ -987,8 +987,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv2_kernel(AttnArgs a) {
 // read from LDS for a key pair feed both query tiles' MFMAs (half the LDS bytes per MFMA of
 // attn_bwd_dq_kernel).  A second tile past the head (odd tile count) runs on zero rows and stores nothing.
 // Per query tile: the operands, MFMAs, rounding points and fp32 order of attn_bwd_dq_kernel (bit-identical).
-template <int NT16>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
+template <int NT16, int NW = 4>  // NW waves: 4, or 8 for the 37-tile heads (1-KiB output slots there)
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TP = NT16 * 16;
   constexpr int NP = NT16 / 2;
@@ -997,8 +997,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
   const bf16* base = a.qkv + (size_t)img * T * a.ldqkv;
   char* Ks = smem;
   char* Vs = smem + TP * 128;
-  stage_head(Ks, base + D + h * 64, a.ldqkv, T, TP);
-  stage_head(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
+  stage_head<NW>(Ks, base + D + h * 64, a.ldqkv, T, TP);
+  stage_head<NW>(Vs, base + 2 * D + h * 64, a.ldqkv, T, TP);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -1077,16 +1077,17 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq2_kernel(AttnArgs a) {
   };
   auto store = [&](const QOps& Q, const f32x4* dq) {  // whole-row stores through the wave's 2-KiB LDS slot
     const int q0 = Q.q - r;
-    tile_rows_out(smem + 2 * TP * 128 + w * 2048, dq, a.scale, a.dqkv + ((size_t)img * T + q0) * a.lddqkv + h * 64,
-                  a.lddqkv, T - q0);
+    constexpr int SR = NW == 4 ? 16 : 8;  // slot rows: 2 KiB per wave, 1 KiB with eight waves
+    tile_rows_out<SR>(smem + 2 * TP * 128 + w * SR * 128, dq, a.scale,
+                      a.dqkv + ((size_t)img * T + q0) * a.lddqkv + h * 64, a.lddqkv, T - q0);
   };
 
   QRaw rA = load_raw(2 * w), rB = load_raw(2 * w + 1);
-  for (int it = w; it < nitems; it += 4) {
+  for (int it = w; it < nitems; it += NW) {
     const QOps QA = finish_q(rA), QB = finish_q(rB);
-    if (it + 4 < nitems) {
-      rA = load_raw(2 * (it + 4));
-      rB = load_raw(2 * (it + 4) + 1);
+    if (it + NW < nitems) {
+      rA = load_raw(2 * (it + NW));
+      rB = load_raw(2 * (it + NW) + 1);
     }
     f32x4 dqA[4], dqB[4];
 #pragma unroll
@@ -1789,20 +1790,34 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
   const int nt16 = attn_tiles(T);
   const size_t lds_dq = 2 * (size_t)nt16 * 16 * 128;
   const size_t lds_dkv = lds_dq + 2 * (size_t)nt16 * 16 * 4;
-  const size_t slots_dq = 4 * 2048, slots_dkv = nt16 <= 16 ? 4 * 2048 : 4 * 1024;  // dq2 / dkv2 output slots
+  // dq2 / dkv2 output slots; the 37-tile heads (one 148-KiB head per CU) run 8 / 6 waves, so each SIMD holds
+  // two of them (four waves left one per SIMD with nothing to hide the LDS latency behind)
+  const int nw_dq = nt16 == 37 ? 8 : 4, nw_dkv = nt16 == 37 ? 6 : 4;
+  const size_t slots_dq = nw_dq * (nw_dq == 4 ? 2048 : 1024), slots_dkv = nw_dkv * (nt16 <= 16 ? 2048 : 1024);
   // ViT/16 at 224^2 (T = 197, 13 tiles) and at 384^2 (T = 577, the 37-tile instantiation): the pipelined /
   // two-tile loops (bit-identical to the plain ones)
 #define BWD_VARIANTS(N_)                                                                                    \
-  if (g_attn_bwd_pipe == 3) {                                                                               \
-    allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq + slots_dq);                                                             \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq + slots_dq, stream, a);         \
+  if (g_attn_bwd_pipe >= 3) {                                                                               \
+    if (nw_dq == 8) {                                                                                       \
+      allow_lds(attn_bwd_dq2_kernel<N_, 8>, lds_dq + slots_dq);                                             \
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_, 8>), nimg * H, 512, lds_dq + slots_dq, stream, a); \
+    } else {                                                                                                \
+      allow_lds(attn_bwd_dq2_kernel<N_>, lds_dq + slots_dq);                                                \
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq2_kernel<N_>), nimg * H, 256, lds_dq + slots_dq, stream, a); \
+    }                                                                                                       \
   } else {                                                                                                  \
     allow_lds(attn_bwd_dq_pipe_kernel<N_>, lds_dq);                                                         \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dq_pipe_kernel<N_>), nimg * H, 256, lds_dq, stream, a);     \
   }                                                                                                         \
   if (g_attn_bwd_pipe >= 2) {                                                                               \
-    allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv + slots_dkv);                                                           \
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv + slots_dkv, stream, a);       \
+    if (nw_dkv == 6) {                                                                                      \
+      allow_lds(attn_bwd_dkv2_kernel<N_, false, 6>, lds_dkv + slots_dkv);                                   \
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_, false, 6>), nimg * H, 384, lds_dkv + slots_dkv, \
+                         stream, a);                                                                        \
+    } else {                                                                                                \
+      allow_lds(attn_bwd_dkv2_kernel<N_>, lds_dkv + slots_dkv);                                             \
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv2_kernel<N_>), nimg * H, 256, lds_dkv + slots_dkv, stream, a); \
+    }                                                                                                       \
   } else {                                                                                                  \
     allow_lds(attn_bwd_dkv_pipe_kernel<N_>, lds_dkv);                                                       \
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_dkv_pipe_kernel<N_>), nimg * H, 256, lds_dkv, stream, a);   \
