@@ -480,8 +480,11 @@ __global__ void convb_pack_kernel(const float* __restrict__ w, int Cout, int Cin
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool st4(long a, long b, long c) { return a % 4 == 0 && b % 4 == 0 && c % 4 == 0; }
 
-constexpr int DW_TARGET_WG = 2048;  // ~8 workgroups per CU over the pixel splits (the small-tile
-constexpr int DW_MAX_SPLITS = 1024;  // shapes are load-latency bound: occupancy hides it)
+// ~8 workgroups per CU over the pixel splits (the small-tile shapes are load-latency bound: occupancy hides
+// it); every split writes an fp32 slab of the whole weight gradient that convb_dw_reduce_kernel sums, so
+// fewer, longer splits trade occupancy for slab traffic (es_set_conv_dw_target, an A/B knob)
+int g_dw_target_wg = 2048;
+constexpr int DW_MAX_SPLITS = 1024;
 
 inline void dw_tile(int Cout, int K, int& b1, int& b2) {
   b1 = Cout <= 64 ? 64 : 128;
@@ -495,7 +498,7 @@ inline int dw_tiles(int Cout, int K) {
 inline int dw_splits(int M, int Cout, int K, int splits) {
   if (splits <= 0) {
     const int tiles = dw_tiles(Cout, K);
-    splits = (DW_TARGET_WG + tiles - 1) / tiles;
+    splits = (g_dw_target_wg + tiles - 1) / tiles;
     const int maxs = (M + 127) / 128;  // at least 4 pixel steps per split
     splits = splits < maxs ? splits : maxs;
   }
@@ -531,6 +534,14 @@ void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
 extern "C" {
 
 // 1 if the bf16 kernels take a conv of these channel counts (both multiples of 32)
+// tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 2048);
+// returns the previous value (v <= 0: unchanged)
+int es_set_conv_dw_target(int v) {
+  const int old = g_dw_target_wg;
+  if (v > 0) g_dw_target_wg = v;
+  return old;
+}
+
 int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw) {
   return Cin > 0 && Cout > 0 && Cin % 32 == 0 && Cout % 32 == 0 && kh > 0 && kw > 0 && kh * kw <= 64;
 }

@@ -86,6 +86,7 @@ SIGNATURES = {
     "es_conv2d_bwd_weight_workspace": (Z, [I, I, I, I, I]),
     "es_conv2d_bwd_weight": (I, [V, I, I, I, I, L, L, L, L, V, L, L, L, I, I, I, I, I, I, V, V, I, V]),
     "es_conv2d_bf16_eligible": (I, [I, I, I, I]),
+    "es_set_conv_dw_target": (I, [I]),
     "es_conv2d_pack_bf16": (I, [V, I, I, I, I, V, V, V]),
     "es_conv2d_fwd_bf16": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, I, V]),
     "es_conv2d_bwd_data_bf16": (I, [V, L, L, L, V, I, I, I, I, I, I, I, I, I, V, L, L, L, L, I, V]),

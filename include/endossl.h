@@ -293,6 +293,9 @@ int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn,
  * es_conv2d_pack_bf16 first: wp [Cout][kh kw][Cin] (forward), wt [Cin][kh kw][Cout] (data grad),
  * Cout Cin kh kw bf16 each, either pointer may be null. */
 int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw);
+/* tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 2048;
+   each split writes an fp32 slab of the gradient that a reduce kernel sums); returns the previous value */
+int es_set_conv_dw_target(int v);
 int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);
 int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
                        const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
