@@ -883,6 +883,9 @@ class Engine:
                    ptr(self.view(grad, "head.bias")), ptr(gnw), ptr(gnb), n, D, C, _lib.stream())
         return grad
 
+
+class _ViTFunction(torch.autograd.Function):
+    @staticmethod
     def forward(ctx, x, module, *params):
         ctx.module = module
         ctx.n = int(x.shape[0])
