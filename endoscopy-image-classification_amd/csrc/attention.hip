@@ -1712,11 +1712,16 @@ int g_attn_fwd_occ = 7;
 // backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 2 = the pipelined dQ
 // and the two-key-tiles-per-wave dK / dV (attn_bwd_dkv2_kernel), 3 = two query tiles per wave for dQ
 // (attn_bwd_dq2_kernel) and dkv2, 4 = the single pass (attn_bwd_fused_kernel; 13-tile heads, others as 3),
-// 0 = the plain loops (all bit-identical).  Default 4: 0.210 ms vs 0.258 (3) for the F1 head batch in isolation
-// (scripts/attn_bench.py, same box; round 3: 3 at 0.257 vs 0.269 (1) and 0.289 (0))
-int g_attn_bwd_pipe = 4;
+// 0 = the plain loops (all bit-identical).  Default 3: the single pass wins in isolation (F1 head batch 0.2015
+// vs 0.2419 ms, 633 vs 941 MB) but loses inside the two-stream F1 step, where its persistent workgroups hold
+// CUs the overlapped weight gradients would take (31.61-31.63 ms/step vs 31.13-31.19 on one box; on 160 CUs
+// 31.30; scripts/gpu_ab_attnv.sh).  Round 3: 3 at 0.257 vs 0.269 (1) and 0.289 (0)
+int g_attn_bwd_pipe = 3;
 // the same variants for T = 577 (the 37-tile kernels: one 151-KiB head per CU, four waves)
 int g_attn_bwd_long = 1;
+// the single pass's persistent grid: 0 = one workgroup per CU, else this many (a caller that runs other
+// kernels beside it -- the overlapped weight gradients -- leaves their CUs free)
+int g_attn_bwd_grid = 0;
 
 }  // namespace
 
@@ -1734,6 +1739,13 @@ int es_set_attn_variant(int occ) {
 int es_set_attn_bwd_variant(int v) {
   const int old = g_attn_bwd_pipe;
   g_attn_bwd_pipe = v;
+  return old;
+}
+
+// tuning knob: the single-pass backward's workgroups (0 = one per CU); returns the previous value
+int es_set_attn_bwd_grid(int workgroups) {
+  const int old = g_attn_bwd_grid;
+  g_attn_bwd_grid = workgroups < 0 ? 0 : workgroups;
   return old;
 }
 
@@ -1833,8 +1845,8 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
     }
     const size_t lds = 5 * (size_t)13 * 16 * 128 + 2 * 13 * 16 * 4 + 8 * 2048;
     allow_lds(attn_bwd_fused_kernel<13>, lds);
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), std::min(cus, nimg * H), 512, lds, stream, a,
-                       nimg * H);
+    const int grid = std::min(g_attn_bwd_grid > 0 ? std::min(g_attn_bwd_grid, cus) : cus, nimg * H);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), grid, 512, lds, stream, a, nimg * H);
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
   if (g_attn_bwd_pipe && nt16 == 13) { BWD_VARIANTS(13) }
