@@ -1719,8 +1719,8 @@ int g_attn_fwd_occ = 7;
 int g_attn_bwd_pipe = 3;
 // the same variants for T = 577 (the 37-tile kernels: one 151-KiB head per CU, four waves)
 int g_attn_bwd_long = 1;
-// the single pass's persistent grid: 0 = one workgroup per CU, else this many (a caller that runs other
-// kernels beside it -- the overlapped weight gradients -- leaves their CUs free)
+// the single pass's grid: 0 = one persistent workgroup per CU, else this many (fewer: a caller that runs
+// other kernels beside it leaves their CUs free; one per head: short workgroups, no cross-head prefetch)
 int g_attn_bwd_grid = 0;
 
 }  // namespace
@@ -1845,7 +1845,7 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
     }
     const size_t lds = 5 * (size_t)13 * 16 * 128 + 2 * 13 * 16 * 4 + 8 * 2048;
     allow_lds(attn_bwd_fused_kernel<13>, lds);
-    const int grid = std::min(g_attn_bwd_grid > 0 ? std::min(g_attn_bwd_grid, cus) : cus, nimg * H);
+    const int grid = std::min(g_attn_bwd_grid > 0 ? g_attn_bwd_grid : cus, nimg * H);
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), grid, 512, lds, stream, a, nimg * H);
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }
