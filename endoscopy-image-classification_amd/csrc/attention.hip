@@ -1712,16 +1712,18 @@ int g_attn_fwd_occ = 7;
 // backward kernels: 1 = the software-pipelined dQ / dK-dV loops (attn_bwd_*_pipe_kernel), 2 = the pipelined dQ
 // and the two-key-tiles-per-wave dK / dV (attn_bwd_dkv2_kernel), 3 = two query tiles per wave for dQ
 // (attn_bwd_dq2_kernel) and dkv2, 4 = the single pass (attn_bwd_fused_kernel; 13-tile heads, others as 3),
-// 0 = the plain loops (all bit-identical).  Default 3: the single pass wins in isolation (F1 head batch 0.2015
-// vs 0.2419 ms, 633 vs 941 MB) but loses inside the two-stream F1 step, where its persistent workgroups hold
-// CUs the overlapped weight gradients would take (31.61-31.63 ms/step vs 31.13-31.19 on one box; on 160 CUs
-// 31.30; scripts/gpu_ab_attnv.sh).  Round 3: 3 at 0.257 vs 0.269 (1) and 0.289 (0)
-int g_attn_bwd_pipe = 3;
+// 0 = the plain loops (all bit-identical).  Default 4: F1 head batch 0.2015 vs 0.2419 ms (3) isolated, 633 vs
+// 941 MB; inside the two-stream step on g_attn_bwd_grid's default grid (one workgroup per CU: worse than 3).
+// Round 3: 3 at 0.257 vs 0.269 (1) and 0.289 (0)
+int g_attn_bwd_pipe = 4;
 // the same variants for T = 577 (the 37-tile kernels: one 151-KiB head per CU, four waves)
 int g_attn_bwd_long = 1;
-// the single pass's grid: 0 = one persistent workgroup per CU, else this many (fewer: a caller that runs
-// other kernels beside it leaves their CUs free; one per head: short workgroups, no cross-head prefetch)
-int g_attn_bwd_grid = 0;
+// the single pass's grid: -1 (default) = max(CUs, heads / 4), 0 = one persistent workgroup per CU, else this
+// many.  Inside the two-stream F1 step (scripts/gpu_ab_attnv.sh, profiles/r04_attn_bwd_live_ab.txt) a head
+// or two per workgroup lets the side stream's weight-gradient launches take CUs between them, twelve per
+// workgroup (one per CU) holds the CUs: 3072 heads on 768 workgroups 30.78-30.80 ms/step, 1024: 30.86-30.90,
+// 1536: 30.80-30.87, 3072: 31.05-31.09, 256: +0.5 ms, the two-pass kernels 30.95-31.03 (one box)
+int g_attn_bwd_grid = -1;
 
 }  // namespace
 
@@ -1742,10 +1744,11 @@ int es_set_attn_bwd_variant(int v) {
   return old;
 }
 
-// tuning knob: the single-pass backward's workgroups (0 = one per CU); returns the previous value
+// tuning knob: the single-pass backward's workgroups (-1 = max(CUs, heads / 4), 0 = one per CU); returns the
+// previous value
 int es_set_attn_bwd_grid(int workgroups) {
   const int old = g_attn_bwd_grid;
-  g_attn_bwd_grid = workgroups < 0 ? 0 : workgroups;
+  g_attn_bwd_grid = workgroups < -1 ? -1 : workgroups;
   return old;
 }
 
@@ -1845,7 +1848,10 @@ int es_attn_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const float*
     }
     const size_t lds = 5 * (size_t)13 * 16 * 128 + 2 * 13 * 16 * 4 + 8 * 2048;
     allow_lds(attn_bwd_fused_kernel<13>, lds);
-    const int grid = std::min(g_attn_bwd_grid > 0 ? g_attn_bwd_grid : cus, nimg * H);
+    const int heads = nimg * H;
+    const int grid = std::min(g_attn_bwd_grid > 0 ? g_attn_bwd_grid
+                                                  : (g_attn_bwd_grid == 0 ? cus : std::max(cus, (heads + 3) / 4)),
+                              heads);
     hipLaunchKernelGGL(HIP_KERNEL_NAME(attn_bwd_fused_kernel<13>), grid, 512, lds, stream, a, nimg * H);
     return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
   }

@@ -110,8 +110,8 @@ int es_set_attn_variant(int occ);
 /* attention backward loops: 3 (default) = two query / key tiles per wave item (dq2 / dkv2), 2 = pipelined
    dQ + dkv2, 1 = software-pipelined, 0 = plain (all bit-identical); returns the previous value */
 int es_set_attn_bwd_variant(int v);
-/* tuning knob: the single-pass attention backward's persistent workgroups (0 = one per CU); returns the
-   previous value */
+/* tuning knob: the single-pass attention backward's workgroups (-1, the default: max(CUs, heads / 4);
+   0: one persistent workgroup per CU); returns the previous value */
 int es_set_attn_bwd_grid(int workgroups);
 /* 1 (default): the backward variant above also for T > 256 (the 37-tile kernels); 0: plain loops there. */
 int es_set_attn_bwd_long(int v);
