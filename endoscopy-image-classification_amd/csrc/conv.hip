@@ -453,17 +453,30 @@ __device__ __forceinline__ void stv(bf16* __restrict__ p, const float (&v)[VEC])
   }
 }
 
+// The BatchNorm affine map of the forward, (x - mean) * rstd * gamma + beta: one function for bn_apply_kernel
+// and for the backward kernels that rebuild the ReLU mask from x (same expression, same rounding).
+__device__ __forceinline__ float bn_affine(float x, float mu, float rs, float ga, float be) {
+  return (x - mu) * rs * ga + be;
+}
+// the forward's y > 0 for a ReLU BatchNorm without residual: relu(affine) rounded to the map type T
+template <typename T>
+__device__ __forceinline__ bool bn_relu_live(float x, float mu, float rs, float ga, float be) {
+  return (float)(T)fmaxf(bn_affine(x, mu, rs, ga, be), 0.f) > 0.f;
+}
 // MODE 0: sum v;  MODE 1: sum (v - mean[c])^2;  MODE 2: sum g, sum g * xhat  (g = dy * [y > 0 if relu],
 // xhat = (x - mean) * rstd), written as partial[block][c] and partial[block][C + c].
 // A thread owns VEC channels and walks every rp-th row of the block's chunk; contiguous views
 // (sn = HW * sp, every BatchNorm) take 4 rows per iteration so 4 (MODE 2: 12) loads are in flight.
 // T: element type of the maps v, dy, y (fp32 or bf16); sums in fp32.
+// MODE 2 with relu and y == null (gamma / beta given): the mask rebuilt from x (bn_relu_live), no y read
 template <int MODE, int VEC, typename T = float>
 __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__ v, RowMap rm, int rows, int C,
                                                            int rows_per, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, const T* __restrict__ dy,
                                                            const T* __restrict__ y, int relu,
-                                                           float* __restrict__ partial) {
+                                                           float* __restrict__ partial,
+                                                           const float* __restrict__ gamma = nullptr,
+                                                           const float* __restrict__ beta = nullptr) {
   __shared__ float red[256 * VEC];
   __shared__ float red2[MODE == 2 ? 256 * VEC : 1];
   const int CV = C / VEC;
@@ -478,11 +491,14 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__
 #pragma unroll
     for (int j = 0; j < VEC; ++j) s[j] = s2[j] = 0.f;
     if (rl < rp && cv < CV) {
-      float mu[VEC], rs[VEC];
+      float mu[VEC], rs[VEC], ga[VEC], be[VEC];
+      const bool rebuild = MODE == 2 && relu && !y;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         mu[j] = MODE >= 1 ? mean[c + j] : 0.f;
         rs[j] = MODE == 2 ? rstd[c + j] : 0.f;
+        ga[j] = rebuild ? gamma[c + j] : 0.f;
+        be[j] = rebuild ? beta[c + j] : 0.f;
       }
       auto acc = [&](long o) {
         float a[VEC];
@@ -499,10 +515,11 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__
         } else {
           float gd[VEC], yy[VEC];
           ldv<VEC>(dy + o, gd);
-          if (relu) ldv<VEC>(y + o, yy);
+          if (relu && !rebuild) ldv<VEC>(y + o, yy);
 #pragma unroll
           for (int j = 0; j < VEC; ++j) {
-            const float gg = (relu && !(yy[j] > 0.f)) ? 0.f : gd[j];
+            const bool live = !relu || (rebuild ? bn_relu_live<T>(a[j], mu[j], rs[j], ga[j], be[j]) : yy[j] > 0.f);
+            const float gg = live ? gd[j] : 0.f;
             s[j] += gg;
             s2[j] = fmaf(gg, (a[j] - mu[j]) * rs[j], s2[j]);
           }
@@ -623,7 +640,7 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, int nv, int CV, const f
       ldv<VEC>(rstd + c, rs);
     }
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) o[j] = (xv[j] - mu[j]) * rs[j] * ga[j] + be[j];
+    for (int j = 0; j < VEC; ++j) o[j] = bn_affine(xv[j], mu[j], rs[j], ga[j], be[j]);
     if (res) {
       float rr[VEC];
       ldv<VEC>(res + (long)i * VEC, rr);
@@ -640,12 +657,13 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, int nv, int CV, const f
 
 // dx = rstd * gamma * (g - sum(g)/P - xhat * sum(g xhat)/P); g = dy [* (y > 0)] (written to gout
 // when given: the residual branch's gradient)
+// relu with y == null (beta given): the mask rebuilt from x (bn_relu_live)
 template <int VEC, typename T = float>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                     const T* __restrict__ y, int relu, int nv, int CV, int rows,
                                     const float* __restrict__ mean, const float* __restrict__ rstd,
                                     const float* __restrict__ gamma, const float* __restrict__ sums,
-                                    T* __restrict__ dx, T* __restrict__ gout) {
+                                    T* __restrict__ dx, T* __restrict__ gout, const float* __restrict__ beta = nullptr) {
   const float inv = 1.0f / (float)rows;
   const int C = CV * VEC;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nv; i += gridDim.x * blockDim.x) {
@@ -653,16 +671,22 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict
     float xv[VEC], gg[VEC], yy[VEC], mu[VEC], rs[VEC], ga[VEC], s0[VEC], s1[VEC], o[VEC];
     ldv<VEC>(x + (long)i * VEC, xv);
     ldv<VEC>(dy + (long)i * VEC, gg);
-    if (relu) {
+    ldv<VEC>(mean + c, mu);
+    ldv<VEC>(rstd + c, rs);
+    ldv<VEC>(gamma + c, ga);
+    if (relu && y) {
       ldv<VEC>(y + (long)i * VEC, yy);
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
         if (!(yy[j] > 0.f)) gg[j] = 0.f;
+    } else if (relu) {
+      float be[VEC];
+      ldv<VEC>(beta + c, be);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (!bn_relu_live<T>(xv[j], mu[j], rs[j], ga[j], be[j])) gg[j] = 0.f;
     }
     if (gout) stv<VEC>(gout + (long)i * VEC, gg);
-    ldv<VEC>(mean + c, mu);
-    ldv<VEC>(rstd + c, rs);
-    ldv<VEC>(gamma + c, ga);
     ldv<VEC>(sums + c, s0);
     ldv<VEC>(sums + C + c, s1);
 #pragma unroll
@@ -1506,13 +1530,14 @@ void bn_apply_launch(bool v4, const T* x, long n, int C, const float* mu, const 
 
 template <int MODE, typename T>
 void chan_partial_launch(bool v4, int G, const T* v, RowMap rm, int rows, int C, int per, const float* mean,
-                         const float* rstd, const T* dy, const T* y, int relu, float* ws, hipStream_t stream) {
+                         const float* rstd, const T* dy, const T* y, int relu, float* ws, hipStream_t stream,
+                         const float* gamma = nullptr, const float* beta = nullptr) {
   if (v4)
     hipLaunchKernelGGL((chan_partial_kernel<MODE, 4, T>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       ws);
+                       ws, gamma, beta);
   else
     hipLaunchKernelGGL((chan_partial_kernel<MODE, 1, T>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       ws);
+                       ws, gamma, beta);
 }
 
 template <typename T>
@@ -1560,11 +1585,12 @@ int bn2d_fwd_impl(const T* x, int rows, int C, const float* gamma, const float* 
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+// y == null with relu: the mask rebuilt from x (train mode, no residual; beta required)
 template <typename T>
 int bn2d_bwd_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu, const float* gamma, const float* mean,
                   const float* rstd, int train, const float* running_var, float eps, T* dx, T* gout, float* dgamma,
-                  float* dbeta, int accumulate, float* workspace, hipStream_t stream) {
-  if (!x || !dy || !dx || !gamma || (relu && !y)) return ES_BAD_ARG;
+                  float* dbeta, int accumulate, float* workspace, hipStream_t stream, const float* beta = nullptr) {
+  if (!x || !dy || !dx || !gamma || (relu && !y && (!beta || !train))) return ES_BAD_ARG;
   if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
   const long n = (long)rows * C;
   if (n >= (1L << 31)) return ES_BAD_SHAPE;
@@ -1579,17 +1605,18 @@ int bn2d_bwd_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu
   const int per = (rows + G - 1) / G;
   const RowMap rm{(long)rows * C, (long)C, rows};
   float* sums = workspace + (size_t)G * 2 * C;  // [2C]: sum g, sum g xhat
-  const bool v4 = map_v4<T>(C, x, dy, y, dx, gout) && al16(mean) && al16(rstd) && al16(gamma) && al16(sums);
-  chan_partial_launch<2, T>(v4, G, x, rm, rows, C, per, mean, rstd, dy, y, relu, workspace, stream);
+  const bool v4 = map_v4<T>(C, x, dy, y, dx, gout) && al16(mean) && al16(rstd) && al16(gamma) && al16(sums) &&
+                  (!beta || al16(beta));
+  chan_partial_launch<2, T>(v4, G, x, rm, rows, C, per, mean, rstd, dy, y, relu, workspace, stream, gamma, beta);
   // sums[0..C) = sum g -> dbeta, sums[C..2C) = sum g xhat -> dgamma
   ChanFin f{dbeta, dgamma, sums, nullptr, nullptr, nullptr, 0.f, 0.f, rows, C, accumulate};
   hipLaunchKernelGGL(chan_final_kernel<3>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
   if (v4)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
-                       rows, mean, rstd, gamma, sums, dx, gout);
+                       rows, mean, rstd, gamma, sums, dx, gout, beta);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows, mean,
-                       rstd, gamma, sums, dx, gout);
+                       rstd, gamma, sums, dx, gout, beta);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -1909,6 +1936,19 @@ int es_bn2d_fwd_partials(const float* x, int rows, int C, float* partials, const
                          hipStream_t stream) {
   return bn2d_fwd_partials_impl<float>(x, rows, C, partials, gamma, beta, running_mean, running_var,
                                        num_batches_tracked, momentum, eps, res, relu, y, mean, rstd, stream);
+}
+// es_bn2d_bwd_ex for a train-mode ReLU BatchNorm without residual whose output y was not kept: the ReLU mask is
+// rebuilt from x with the forward's affine map and rounding (bn_relu_live), so the backward reads x and dy only
+int es_bn2d_bwd_recompute_ex(const void* x, const void* dy, int rows, int C, const float* gamma, const float* beta,
+                             const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta, int accumulate,
+                             float* workspace, int flags, hipStream_t stream) {
+  if (flags & ~MAPS_BF16) return ES_BAD_ARG;
+  if (!beta) return ES_BAD_ARG;
+  if (flags)
+    return bn2d_bwd_impl<bf16>((const bf16*)x, nullptr, (const bf16*)dy, rows, C, 1, gamma, mean, rstd, 1, nullptr, 0.f,
+                               (bf16*)dx, nullptr, dgamma, dbeta, accumulate, workspace, stream, beta);
+  return bn2d_bwd_impl<float>((const float*)x, nullptr, (const float*)dy, rows, C, 1, gamma, mean, rstd, 1, nullptr,
+                              0.f, (float*)dx, nullptr, dgamma, dbeta, accumulate, workspace, stream, beta);
 }
 int es_bn2d_fwd_partials_ex(const void* x, int rows, int C, float* partials, const float* gamma, const float* beta,
                             float* running_mean, float* running_var, void* num_batches_tracked, float momentum,

@@ -117,6 +117,7 @@ SIGNATURES = {
     "es_chan_sum_ex": (I, [V, I, I, L, L, I, V, V, I, I, V]),
     "es_bn2d_fwd_ex": (I, [V, I, I, V, V, V, V, V, F, F, I, V, I, V, V, V, V, I, V]),
     "es_bn2d_bwd_ex": (I, [V, V, V, I, I, I, V, V, V, I, V, F, V, V, V, V, I, V, I, V]),
+    "es_bn2d_bwd_recompute_ex": (I, [V, V, I, I, V, V, V, V, V, V, V, I, V, I, V]),
     "es_bn2d_fwd_partials_ex": (I, [V, I, I, V, V, V, V, V, V, F, F, V, I, V, V, V, I, V]),
     "es_bn2d_sums_ex": (I, [V, I, I, I, V, I, V, V, I, V]),
     "es_bn2d_fwd_global_ex": (I, [V, I, I, V, V, V, V, V, F, F, V, V, I, V, I, V, V, V, I, V]),

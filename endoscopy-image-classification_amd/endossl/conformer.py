@@ -494,7 +494,10 @@ class _BNFn(torch.autograd.Function):
             call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(m.pview(pre + "weight")), ptr(m.pview(pre + "bias")), ptr(rm),
                  ptr(rv), ptr(nbt) if train else None, BN_MOMENTUM, eps, 1 if train else 0, ptr(res_c),
                  1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), fl, _s())
-        ctx.save_for_backward(x, y, mean, rstd)
+        # the ReLU mask of a train-mode BatchNorm without residual is rebuilt from x in the backward
+        # (es_bn2d_bwd_recompute_ex): y is not read there (one map read less in both backward kernels)
+        keep_y = relu and (res is not None or world > 1 or not train)
+        ctx.save_for_backward(x, y if keep_y else None, mean, rstd)
         ctx.m, ctx.pre, ctx.eps, ctx.relu, ctx.train, ctx.has_res = m, pre, eps, relu, train, res is not None
         ctx.world = world
         ctx.res_sink = res_sink if res is not None else None
@@ -524,6 +527,11 @@ class _BNFn(torch.autograd.Function):
                  ptr(m.pview(pre + "weight")), ptr(mean), ptr(rstd), ptr(loc), ptr(glob), rows * ctx.world, ptr(dx),
                  ptr(gout), ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, fl, _s())
             return dx, _BNFn._res_grad(ctx, gout), None, None, None, None, None
+        if ctx.relu and y is None:
+            call("es_bn2d_bwd_recompute_ex", ptr(x), ptr(dy), rows, C, ptr(m.pview(pre + "weight")),
+                 ptr(m.pview(pre + "bias")), ptr(mean), ptr(rstd), ptr(dx), ptr(m.gview(pre + "weight")),
+                 ptr(m.gview(pre + "bias")), 0, ptr(ws), fl, _s())
+            return dx, None, None, None, None, None, None
         call("es_bn2d_bwd_ex", ptr(x), ptr(y), ptr(dy), rows, C, 1 if ctx.relu else 0, ptr(m.pview(pre + "weight")),
              ptr(mean), ptr(rstd), 1 if ctx.train else 0, ptr(rv), ctx.eps, ptr(dx), ptr(gout),
              ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(ws), fl, _s())

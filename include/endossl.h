@@ -393,6 +393,11 @@ int es_bn2d_bwd_ex(const void* x, const void* y, const void* dy, int rows, int C
                    const float* mean, const float* rstd, int train, const float* running_var, float eps, void* dx,
                    void* gout, float* dgamma, float* dbeta, int accumulate, float* workspace, int flags,
                    hipStream_t stream);
+/* es_bn2d_bwd_ex for a train-mode ReLU BatchNorm without residual whose output y was not kept: the ReLU mask
+   is rebuilt from x with the forward's affine map and rounding, so the backward reads x and dy only */
+int es_bn2d_bwd_recompute_ex(const void* x, const void* dy, int rows, int C, const float* gamma, const float* beta,
+                             const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta, int accumulate,
+                             float* workspace, int flags, hipStream_t stream);
 int es_bn2d_fwd_partials_ex(const void* x, int rows, int C, float* partials, const float* gamma, const float* beta,
                             float* running_mean, float* running_var, void* num_batches_tracked, float momentum,
                             float eps, const void* res, int relu, void* y, float* mean, float* rstd, int flags,

@@ -442,6 +442,47 @@ def test_conv_bf16_maps_match_fp32_maps_rounded(N, Cin, H, Cout, k, s, p):
         assert torch.equal(dws[key], dws[(0, 0)]), key
 
 
+@pytest.mark.parametrize("C,fl", [(64, 0), (64, 1), (256, 1), (6, 0), (6, 1)])
+def test_bn_bwd_recompute_matches_bwd_with_y(C, fl):
+    """es_bn2d_bwd_recompute_ex (the ReLU mask rebuilt from x with the forward's affine map and rounding, y not
+    read) against es_bn2d_bwd_ex given the forward's y: dx, dgamma, dbeta bit-identical, fp32 and bf16 maps,
+    vector (C % 4 == 0) and scalar kernels; x includes values on which the affine map lands at 0 and just
+    beside it, where a mask that differed from the forward's would show."""
+    torch.manual_seed(C + 17 * fl)
+    N, H, W = 3, 9, 7
+    rows = N * H * W
+    lib = _lib.load()
+    x = _rep(N, H, W, C, scale=1.5, shift=0.1)
+    dy = _rep(N, H, W, C)
+    g, b = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    if fl:
+        x, dy = x.to(B16), dy.to(B16)
+    ws = torch.empty(lib.es_chan_workspace(rows, C), device=DEV)
+    rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+    y, mean, rstd = torch.empty_like(x), torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+    call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm), ptr(rv), None, 0.1, 1e-6, 1, None, 1, ptr(y),
+         ptr(mean), ptr(rstd), ptr(ws), fl, S())
+    # put every 5th row where the first pass's affine map is 0 (x = mean - beta / (rstd gamma), rounded), then
+    # take the statistics and y of the edited map: those rows sit at the ReLU's edge
+    x.view(rows, C)[::5] = (mean - b / (rstd * g)).to(x.dtype)
+    call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm), ptr(rv), None, 0.1, 1e-6, 1, None, 1, ptr(y),
+         ptr(mean), ptr(rstd), ptr(ws), fl, S())
+    out = {}
+    for mode in ("y", "recompute"):
+        dx = torch.empty_like(x)
+        dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+        if mode == "y":
+            call("es_bn2d_bwd_ex", ptr(x), ptr(y), ptr(dy), rows, C, 1, ptr(g), ptr(mean), ptr(rstd), 1, ptr(rv),
+                 1e-6, ptr(dx), None, ptr(dg), ptr(db), 0, ptr(ws), fl, S())
+        else:
+            call("es_bn2d_bwd_recompute_ex", ptr(x), ptr(dy), rows, C, ptr(g), ptr(b), ptr(mean), ptr(rstd), ptr(dx),
+                 ptr(dg), ptr(db), 0, ptr(ws), fl, S())
+        out[mode] = (dx, dg, db)
+    for a, c in zip(out["y"], out["recompute"]):
+        assert torch.equal(a, c)
+    assert (y.float() == 0).any() and (y.float() > 0).any()
+
+
 @pytest.mark.parametrize("relu,with_res,C", [(True, True, 64), (True, False, 256), (False, False, 128), (True, True, 6)])
 def test_bn_pool_bf16_maps_match_fp32_maps_rounded(relu, with_res, C):
     """BatchNorm (statistics pass, conv partials, eval, backward, SyncBatchNorm halves), channel sums, max /
