@@ -273,6 +273,8 @@ CONV_BF16 = os.environ.get("ENDOSSL_CONV_BF16", "1") != "0"
 # train-mode BatchNorm statistics of a bf16 conv's output computed in the conv's epilogue
 # (es_conv2d_fwd_bf16_bnstats -> es_bn2d_fwd_partials): no two statistics passes over the map
 BN_STATS_FUSED = True
+# the backward of a train-mode ReLU BatchNorm without residual rebuilds its mask from x instead of reading y
+BN_Y_FREE = True
 # a ConvBlock input's two gradient contributions (conv1, residual) summed in place (_GradSink)
 GRAD_SINKS = True
 # ... and the token buffer's two consumers (a block's FCUUp conv, the next block's FCUDown), _trans_branch
@@ -496,7 +498,7 @@ class _BNFn(torch.autograd.Function):
                  1 if relu else 0, ptr(y), ptr(mean), ptr(rstd), ptr(ws), fl, _s())
         # the ReLU mask of a train-mode BatchNorm without residual is rebuilt from x in the backward
         # (es_bn2d_bwd_recompute_ex): y is not read there (one map read less in both backward kernels)
-        keep_y = relu and (res is not None or world > 1 or not train)
+        keep_y = relu and (res is not None or world > 1 or not train or not BN_Y_FREE)
         ctx.save_for_backward(x, y if keep_y else None, mean, rstd)
         ctx.m, ctx.pre, ctx.eps, ctx.relu, ctx.train, ctx.has_res = m, pre, eps, relu, train, res is not None
         ctx.world = world
