@@ -468,8 +468,8 @@ __device__ __forceinline__ bool bn_relu_live(float x, float mu, float rs, float 
 // A thread owns VEC channels and walks every rp-th row of the block's chunk; contiguous views
 // (sn = HW * sp, every BatchNorm) take 4 rows per iteration so 4 (MODE 2: 12) loads are in flight.
 // T: element type of the maps v, dy, y (fp32 or bf16); sums in fp32.
-// MODE 2 with relu and y == null (gamma / beta given): the mask rebuilt from x (bn_relu_live), no y read
-template <int MODE, int VEC, typename T = float>
+// REBUILD (MODE 2, relu): the mask rebuilt from x with gamma / beta (bn_relu_live), y not read
+template <int MODE, int VEC, typename T = float, bool REBUILD = false>
 __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__ v, RowMap rm, int rows, int C,
                                                            int rows_per, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, const T* __restrict__ dy,
@@ -492,13 +492,14 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__
     for (int j = 0; j < VEC; ++j) s[j] = s2[j] = 0.f;
     if (rl < rp && cv < CV) {
       float mu[VEC], rs[VEC], ga[VEC], be[VEC];
-      const bool rebuild = MODE == 2 && relu && !y;
 #pragma unroll
       for (int j = 0; j < VEC; ++j) {
         mu[j] = MODE >= 1 ? mean[c + j] : 0.f;
         rs[j] = MODE == 2 ? rstd[c + j] : 0.f;
-        ga[j] = rebuild ? gamma[c + j] : 0.f;
-        be[j] = rebuild ? beta[c + j] : 0.f;
+        if constexpr (REBUILD) {
+          ga[j] = gamma[c + j];
+          be[j] = beta[c + j];
+        }
       }
       auto acc = [&](long o) {
         float a[VEC];
@@ -515,11 +516,12 @@ __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__
         } else {
           float gd[VEC], yy[VEC];
           ldv<VEC>(dy + o, gd);
-          if (relu && !rebuild) ldv<VEC>(y + o, yy);
+          if (!REBUILD && relu) ldv<VEC>(y + o, yy);
 #pragma unroll
           for (int j = 0; j < VEC; ++j) {
-            const bool live = !relu || (rebuild ? bn_relu_live<T>(a[j], mu[j], rs[j], ga[j], be[j]) : yy[j] > 0.f);
-            const float gg = live ? gd[j] : 0.f;
+            float gg;
+            if constexpr (REBUILD) gg = bn_relu_live<T>(a[j], mu[j], rs[j], ga[j], be[j]) ? gd[j] : 0.f;
+            else gg = (relu && !(yy[j] > 0.f)) ? 0.f : gd[j];
             s[j] += gg;
             s2[j] = fmaf(gg, (a[j] - mu[j]) * rs[j], s2[j]);
           }
@@ -657,8 +659,8 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, int nv, int CV, const f
 
 // dx = rstd * gamma * (g - sum(g)/P - xhat * sum(g xhat)/P); g = dy [* (y > 0)] (written to gout
 // when given: the residual branch's gradient)
-// relu with y == null (beta given): the mask rebuilt from x (bn_relu_live)
-template <int VEC, typename T = float>
+// REBUILD (relu): the mask rebuilt from x with beta (bn_relu_live), y not read
+template <int VEC, typename T = float, bool REBUILD = false>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                     const T* __restrict__ y, int relu, int nv, int CV, int rows,
                                     const float* __restrict__ mean, const float* __restrict__ rstd,
@@ -671,22 +673,25 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict
     float xv[VEC], gg[VEC], yy[VEC], mu[VEC], rs[VEC], ga[VEC], s0[VEC], s1[VEC], o[VEC];
     ldv<VEC>(x + (long)i * VEC, xv);
     ldv<VEC>(dy + (long)i * VEC, gg);
-    ldv<VEC>(mean + c, mu);
-    ldv<VEC>(rstd + c, rs);
-    ldv<VEC>(gamma + c, ga);
-    if (relu && y) {
+    if constexpr (REBUILD) {
+      float mu0[VEC], rs0[VEC], ga0[VEC], be[VEC];
+      ldv<VEC>(mean + c, mu0);
+      ldv<VEC>(rstd + c, rs0);
+      ldv<VEC>(gamma + c, ga0);
+      ldv<VEC>(beta + c, be);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (!bn_relu_live<T>(xv[j], mu0[j], rs0[j], ga0[j], be[j])) gg[j] = 0.f;
+    } else if (relu) {
       ldv<VEC>(y + (long)i * VEC, yy);
 #pragma unroll
       for (int j = 0; j < VEC; ++j)
         if (!(yy[j] > 0.f)) gg[j] = 0.f;
-    } else if (relu) {
-      float be[VEC];
-      ldv<VEC>(beta + c, be);
-#pragma unroll
-      for (int j = 0; j < VEC; ++j)
-        if (!bn_relu_live<T>(xv[j], mu[j], rs[j], ga[j], be[j])) gg[j] = 0.f;
     }
     if (gout) stv<VEC>(gout + (long)i * VEC, gg);
+    ldv<VEC>(mean + c, mu);
+    ldv<VEC>(rstd + c, rs);
+    ldv<VEC>(gamma + c, ga);
     ldv<VEC>(sums + c, s0);
     ldv<VEC>(sums + C + c, s1);
 #pragma unroll
@@ -1532,12 +1537,21 @@ template <int MODE, typename T>
 void chan_partial_launch(bool v4, int G, const T* v, RowMap rm, int rows, int C, int per, const float* mean,
                          const float* rstd, const T* dy, const T* y, int relu, float* ws, hipStream_t stream,
                          const float* gamma = nullptr, const float* beta = nullptr) {
+  if (MODE == 2 && relu && !y) {  // the mask rebuilt from x (gamma / beta)
+    if (v4)
+      hipLaunchKernelGGL((chan_partial_kernel<MODE, 4, T, true>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd,
+                         dy, y, relu, ws, gamma, beta);
+    else
+      hipLaunchKernelGGL((chan_partial_kernel<MODE, 1, T, true>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd,
+                         dy, y, relu, ws, gamma, beta);
+    return;
+  }
   if (v4)
     hipLaunchKernelGGL((chan_partial_kernel<MODE, 4, T>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       ws, gamma, beta);
+                       ws, nullptr, nullptr);
   else
     hipLaunchKernelGGL((chan_partial_kernel<MODE, 1, T>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd, dy, y, relu,
-                       ws, gamma, beta);
+                       ws, nullptr, nullptr);
 }
 
 template <typename T>
@@ -1611,12 +1625,19 @@ int bn2d_bwd_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu
   // sums[0..C) = sum g -> dbeta, sums[C..2C) = sum g xhat -> dgamma
   ChanFin f{dbeta, dgamma, sums, nullptr, nullptr, nullptr, 0.f, 0.f, rows, C, accumulate};
   hipLaunchKernelGGL(chan_final_kernel<3>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
-  if (v4)
+  const bool rebuild = relu && !y;
+  if (v4 && rebuild)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T, true>), grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4),
+                       C / 4, rows, mean, rstd, gamma, sums, dx, gout, beta);
+  else if (rebuild)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T, true>), grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows,
+                       mean, rstd, gamma, sums, dx, gout, beta);
+  else if (v4)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T>), grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4), C / 4,
-                       rows, mean, rstd, gamma, sums, dx, gout, beta);
+                       rows, mean, rstd, gamma, sums, dx, gout, nullptr);
   else
     hipLaunchKernelGGL((bn_bwd_apply_kernel<1, T>), grid1d(n), 256, 0, stream, x, dy, y, relu, (int)n, C, rows, mean,
-                       rstd, gamma, sums, dx, gout, beta);
+                       rstd, gamma, sums, dx, gout, nullptr);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
