@@ -39,6 +39,7 @@ from ._lib import call, ptr
 from .vit import IMAGENET_MEAN, IMAGENET_STD
 
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32 = 0, 1, 2, 3, 4
+EPI_GELU_ACT, EPI_GELU_D, EPI_MULAUX = 6, 7, 8
 BN_EPS_BLOCK, BN_EPS_STEM, LN_EPS, LN_EPS_TRANS_NORM = 1e-6, 1e-5, 1e-6, 1e-5
 BN_MOMENTUM = 0.1
 
@@ -334,10 +335,11 @@ class _GradSink:
 
 
 # test hook (tests/test_gpu_s1_blocks.py, teacher-forced per-op parity of the transformer branch at S1's
-# shape): called as BLOCK_CAPTURE("fwd", prefix, n, xt, h1, qkv, o, lse, xmid, h2, pre, act, out) after a
-# transformer block's forward and BLOCK_CAPTURE("bwd", prefix, n, dout, dxb, dpre, dh, dxm, dxmb, do, dqkv,
-# dh2, dx) after its reverse pass (before the side-stream weight gradients are joined), on the launch stream
-# with the block's own buffers; the callee clones what it keeps.
+# shape): called as BLOCK_CAPTURE("fwd", prefix, n, xt, h1, qkv, o, lse, xmid, h2, gd, act, out) after a
+# transformer block's forward with gradients (gd = GELU'(fc1 pre-activation)) and BLOCK_CAPTURE("bwd",
+# prefix, n, dout, dxb, dpre, dh, dxm, dxmb, do, dqkv, dh2, dx) after its reverse pass (before the side-stream
+# weight gradients are joined), on the launch stream with the block's own buffers; the callee clones what it
+# keeps.
 BLOCK_CAPTURE = None
 
 # test hook (tests/test_gpu_convs.py, teacher-forced per-conv parity): called as CAPTURE("fwd", wname, x, y,
@@ -740,7 +742,12 @@ class _BlockFn(torch.autograd.Function):
         qkv, o = e(Mp, 3 * D, dt=b16), zp(Mp, D, dt=b16)
         lse = e(n * H * T)
         xmid, out = e(Mp, D), zp(Mp, D)
-        pre_, act = e(Mp, Hd, dt=b16), zp(Mp, Hd, dt=b16)
+        # fc1 + GELU: with gradients the epilogue writes GELU'(pre) beside the activation (the ViT engine's
+        # GELU_D form), so the backward's fc2 data gradient multiplies by it (EPI_MULAUX) instead of
+        # re-evaluating the erf per element behind its K loop (EPI_DGELU: 1.6 ms per S1 launch); without
+        # gradients (the weak pass) the activation alone
+        grad = ctx.needs_input_grad[0]
+        gd, act = (e(Mp, Hd, dt=b16) if grad else None), zp(Mp, Hd, dt=b16)
         pv, wb = m.pview, m.wb
         call("es_layernorm_fwd", ptr(xt), D, ptr(pv(pre + "norm1.weight")), ptr(pv(pre + "norm1.bias")), ptr(h1), D,
              ptr(mean1), ptr(rstd1), M, D, LN_EPS, s)
@@ -751,20 +758,24 @@ class _BlockFn(torch.autograd.Function):
              ptr(pv(pre + "attn.proj.bias")), ptr(xmid), D, None, ptr(xt), D, M, D, D, 0, s)
         call("es_layernorm_fwd", ptr(xmid), D, ptr(pv(pre + "norm2.weight")), ptr(pv(pre + "norm2.bias")), ptr(h2), D,
              ptr(mean2), ptr(rstd2), M, D, LN_EPS, s)
-        call("es_gemm_nt", EPI_GELU, ptr(h2), D, ptr(wb[pre + "mlp.fc1.weight"]), D, ptr(pv(pre + "mlp.fc1.bias")),
-             ptr(pre_), Hd, ptr(act), None, 0, M, Hd, D, 0, s)
+        if grad:
+            call("es_gemm_nt", EPI_GELU_D, ptr(h2), D, ptr(wb[pre + "mlp.fc1.weight"]), D,
+                 ptr(pv(pre + "mlp.fc1.bias")), ptr(gd), Hd, ptr(act), None, 0, M, Hd, D, 0, s)
+        else:
+            call("es_gemm_nt", EPI_GELU_ACT, ptr(h2), D, ptr(wb[pre + "mlp.fc1.weight"]), D,
+                 ptr(pv(pre + "mlp.fc1.bias")), ptr(act), Hd, None, None, 0, M, Hd, D, 0, s)
         call("es_gemm_nt", EPI_F32_RESID, ptr(act), Hd, ptr(wb[pre + "mlp.fc2.weight"]), Hd,
              ptr(pv(pre + "mlp.fc2.bias")), ptr(out), D, None, ptr(xmid), D, M, D, Hd, 0, s)
-        ctx.save_for_backward(xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, pre_, act)
+        ctx.save_for_backward(xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, gd, act)
         ctx.m, ctx.pre, ctx.n = m, pre, n
-        if BLOCK_CAPTURE is not None:
-            BLOCK_CAPTURE("fwd", pre, n, xt, h1, qkv, o, lse, xmid, h2, pre_, act, out)
+        if BLOCK_CAPTURE is not None and grad:
+            BLOCK_CAPTURE("fwd", pre, n, xt, h1, qkv, o, lse, xmid, h2, gd, act, out)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         _own(dout)
-        xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, pre_, act = ctx.saved_tensors
+        xt, h1, mean1, rstd1, qkv, o, lse, xmid, h2, mean2, rstd2, gd, act = ctx.saved_tensors
         m, pre, n = ctx.m, ctx.pre, ctx.n
         cfg = m.cfg
         D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
@@ -806,8 +817,8 @@ class _BlockFn(torch.autograd.Function):
                      ptr(gv(bname)), _s())
 
         dpre = z("dpre", Mp, Hd, dt=b16)
-        call("es_gemm_nt", EPI_DGELU, ptr(dxb), D, ptr(wt[pre + "mlp.fc2.weight"]), D, None, ptr(dpre), Hd, None,
-             ptr(pre_), Hd, M, Hd, D, 0, s)
+        call("es_gemm_nt", EPI_MULAUX, ptr(dxb), D, ptr(wt[pre + "mlp.fc2.weight"]), D, None, ptr(dpre), Hd, None,
+             ptr(gd), Hd, M, Hd, D, 0, s)
         wgrad(dxb, D, act, Hd, pre + "mlp.fc2.weight", pre + "mlp.fc2.bias")
         dh = z("dh", Mp, D, dt=b16)  # d(LN output) in bf16, as the ViT engine (Engine.DH_BF16)
         call("es_gemm_nt", EPI_BF16, ptr(dpre), Hd, ptr(wt[pre + "mlp.fc1.weight"]), Hd, None, ptr(dh), D, None,

@@ -101,9 +101,9 @@ def test_s1_transformer_ops_teacher_forced():
         return xh, rstd, xh * w0[pre + which + ".weight"] + w0[pre + which + ".bias"]
 
     for pre in cap["fwd"]:
-        n, xt, h1, qkv, o, lse, xmid, h2, pre_, act, out = cap["fwd"][pre]
+        n, xt, h1, qkv, o, lse, xmid, h2, gd, act, out = cap["fwd"][pre]
         f = lambda t: t.double()  # noqa: E731
-        x, h1, qkv, o, xmid, h2, pre_, act, out = map(f, (xt, h1, qkv, o, xmid, h2, pre_, act, out))
+        x, h1, qkv, o, xmid, h2, gd, act, out = map(f, (xt, h1, qkv, o, xmid, h2, gd, act, out))
         lse = lse[:n * H * T].double().view(n, H, T, 1)
         W = lambda nm: rb(w0[pre + nm + ".weight"])  # noqa: E731
         bias = lambda nm: w0[pre + nm + ".bias"]  # noqa: E731
@@ -118,15 +118,15 @@ def test_s1_transformer_ops_teacher_forced():
         xh2, r2, y2 = ln(xmid, pre, "norm2")
         chk(f"{k}.op.ln2", h2, rb(y2), B16)
         z = h2 @ W("mlp.fc1").T + bias("mlp.fc1")
-        chk(f"{k}.op.fc1_pre", pre_, rb(z), B16)
         chk(f"{k}.op.fc1_gelu", act, rb(ref._gelu_exact(z)), B16)
+        chk(f"{k}.op.fc1_gelu_grad", gd, rb(ref._gelu_grad(z)), B16)
         chk(f"{k}.op.fc2_resid", out, xmid + (act @ W("mlp.fc2").T + bias("mlp.fc2")), F32)
         # reverse pass, each op from the device's own inputs
         _, dout, dxb, dpre, dh, dxm, dxmb, do, dqkv, dh2, dx = cap["bwd"][pre]
         dout, dxb, dpre, dh, dxm, dxmb, do, dqkv, dh2, dx = map(f, (dout, dxb, dpre, dh, dxm, dxmb, do, dqkv, dh2, dx))
         assert torch.equal(dxb, rb(dout)), pre
         assert torch.equal(dxmb, rb(dxm)), pre
-        chk(f"{k}.op.fc2_dgrad_x_gelu_grad", dpre, rb((dxb @ W("mlp.fc2")) * ref._gelu_grad(pre_)), B16)
+        chk(f"{k}.op.fc2_dgrad_x_gelu_grad", dpre, rb((dxb @ W("mlp.fc2")) * gd), B16)
         chk(f"{k}.op.fc1_dgrad", dh, rb(dpre @ W("mlp.fc1")), B16)
         dln2, dg2, db2 = ref._ln_bwd(dh, xh2, r2, w0[pre + "norm2.weight"])
         chk(f"{k}.op.ln2_bwd_resid", dxm, dln2 + dout, F32)
