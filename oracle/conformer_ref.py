@@ -27,7 +27,7 @@ output (the conv epilogue's statistics, es_conv2d_fwd_bf16_ex) and normalise the
 import torch
 import torch.nn.functional as F
 
-from .ref import _bf, consistency, ema_update
+from .ref import _bf, _gelu_grad, consistency, ema_update
 
 BN_EPS_BLOCK = 1e-6   # ConvBlock / FCUUp norm_layer = partial(nn.BatchNorm2d, eps=1e-6)
 BN_EPS_STEM = 1e-5    # Conformer.bn1 = nn.BatchNorm2d(64)
@@ -86,6 +86,22 @@ class _RoundMap(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         return _bf(g)
+
+
+class _GeluB16(torch.autograd.Function):
+    """GELU of the fp32 fc1 output under the bf16 contract: the device's fc1 epilogue writes GELU'(pre) rounded
+    to bf16 beside the activation (endossl/conformer.py, EPI_GELU_D) and the backward multiplies by that stored
+    value (EPI_MULAUX), so the reverse pass here uses the same rounded derivative."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return F.gelu(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return g * _bf(_gelu_grad(x))
 
 
 def _bn_map(y32, p, bufs, pre, eps, train):
@@ -151,7 +167,8 @@ def block(p, pre, t, heads, bf16=False):
     o = r(o.transpose(1, 2).reshape(B, N, D))
     t = t + F.linear(o, r(p[pre + "attn.proj.weight"]), p[pre + "attn.proj.bias"])
     h = r(F.layer_norm(t, (D,), p[pre + "norm2.weight"], p[pre + "norm2.bias"], LN_EPS_BLOCK))
-    h = r(F.gelu(F.linear(h, r(p[pre + "mlp.fc1.weight"]), p[pre + "mlp.fc1.bias"])))
+    gelu = _GeluB16.apply if bf16 else F.gelu
+    h = r(gelu(F.linear(h, r(p[pre + "mlp.fc1.weight"]), p[pre + "mlp.fc1.bias"])))
     return t + F.linear(h, r(p[pre + "mlp.fc2.weight"]), p[pre + "mlp.fc2.bias"])
 
 
