@@ -81,7 +81,7 @@ def main():
         times = {v: [] for v in variants}
         for _ in range(args.rounds):
             for v in variants:
-                if N % {6: 256, 7: 192, 8: 256, 9: 192, 10: 128, 28: 256}.get(v, 128):
+                if N % {6: 256, 10: 128}.get(v, 128):
                     continue
                 lib.es_set_gemm_variant(v)
                 auxp = aux if epi in (2,) else (aux.bfloat16() if epi in (3, 8) else None)
