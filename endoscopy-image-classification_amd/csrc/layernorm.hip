@@ -67,6 +67,79 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ x
   }
 }
 
+// The same rows, numerics and stores as ln_fwd_kernel, but each wave walks row pairs grid-stride and issues
+// the next pair's loads before it normalises the current one (two pairs in flight per wave).
+template <int V>
+__global__ __launch_bounds__(256) void ln_fwd_loop_kernel(const float* __restrict__ x, int ldx,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, bf16* __restrict__ y,
+                                                          int ldy, float* __restrict__ mean_out,
+                                                          float* __restrict__ rstd_out, int M, float eps) {
+  constexpr int D = V * 128, R = 2;
+  const int lane = threadIdx.x & 63;
+  const int stride = gridDim.x * 4 * R;
+  int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R;
+  if (row0 >= M) return;
+  auto load = [&](float2 (&v)[R][V], int r0) {
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const float* xr = x + (size_t)min(r0 + q, M - 1) * ldx;
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[q][j] = *(const float2*)(xr + (j * 64 + lane) * 2);
+    }
+  };
+  float2 v[R][V];
+  load(v, row0);
+  float2 gm[V], bt[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    const int c = (j * 64 + lane) * 2;
+    gm[j] = *(const float2*)(gamma + c);
+    bt[j] = *(const float2*)(beta + c);
+  }
+  for (;;) {
+    const int nx = row0 + stride;
+    float2 nv[R][V];
+    if (nx < M) load(nv, nx);
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      const int row = row0 + q;
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) s += v[q][j].x + v[q][j].y;
+      const float mean = warp_sum(s) * (1.0f / D);
+      float ss = 0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float a = v[q][j].x - mean, b = v[q][j].y - mean;
+        ss += a * a + b * b;
+      }
+      const float rstd = 1.0f / sqrtf(warp_sum(ss) * (1.0f / D) + eps);
+      if (row < M) {
+        bf16* yr = y + (size_t)row * ldy;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+          const int c = (j * 64 + lane) * 2;
+          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+          bf16x2 o = {(bf16)((v[q][j].x - mean) * rstd * gm[j].x + bt[j].x),
+                      (bf16)((v[q][j].y - mean) * rstd * gm[j].y + bt[j].y)};
+          *(bf16x2*)(yr + c) = o;
+        }
+        if (lane == 0) {
+          mean_out[row] = mean;
+          rstd_out[row] = rstd;
+        }
+      }
+    }
+    if (nx >= M) break;
+#pragma unroll
+    for (int q = 0; q < R; ++q)
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[q][j] = nv[q][j];
+    row0 = nx;
+  }
+}
+
 // two consecutive dy values as float2 (fp32 or bf16 storage)
 __device__ __forceinline__ float2 ld_dy2(const float* p) { return *(const float2*)p; }
 __device__ __forceinline__ float2 ld_dy2(const bf16* p) {
@@ -199,14 +272,34 @@ static int ln_bwd_launch(const DY* dy, int lddy, const float* x, int ldx, const 
   return es_gemm::reduce_partials_pair(pg, dgamma, pb, dbeta, grid, D, accumulate, stream);
 }
 
+// > 0 (default 2048): the grid-stride forward on this many workgroups when the one-shot grid would be larger;
+// 0: the one-shot kernel.  F1 same box, interleaved three times (scripts/gpu_ab_knobs3.sh): 0 30.51 ms/step
+// mean, 1024 30.42, 2048 30.28, 4096 30.30; isolated at F1's LN2 (scripts/ln_bench.py, x L3-resident) the
+// one-shot kernel is faster (35.1 vs 37.9 us): the gain is in the two-stream step, where 12,608 short-lived
+// workgroups per launch interleave worse with the other stream's kernels
+static int g_ln_fwd_grid = 2048;
+
 extern "C" {
+
+// tuning knob: LayerNorm forward grid (0 = one workgroup per 8 rows, the one-shot kernel; > 0 = the grid-stride
+// kernel with the next row pair's loads in flight, on this many workgroups); returns the previous value
+int es_set_ln_fwd_grid(int g) {
+  const int old = g_ln_fwd_grid;
+  g_ln_fwd_grid = g;
+  return old;
+}
 
 int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,
                      float* rstd, int M, int D, float eps, hipStream_t stream) {
   if (M <= 0 || D % 128 || ldx % 2 || ldy % 2) return ES_BAD_SHAPE;
   if (!x || !gamma || !beta || !y || !mean || !rstd) return ES_BAD_ARG;
   const int grid = (M + 7) / 8;  // 4 waves x 2 rows
-  LN_DISPATCH(ln_fwd_kernel, D / 128, grid, stream, x, ldx, gamma, beta, (bf16*)y, ldy, mean, rstd, M, eps);
+  if (g_ln_fwd_grid > 0 && grid > g_ln_fwd_grid) {
+    LN_DISPATCH(ln_fwd_loop_kernel, D / 128, g_ln_fwd_grid, stream, x, ldx, gamma, beta, (bf16*)y, ldy, mean, rstd, M,
+                eps);
+  } else {
+    LN_DISPATCH(ln_fwd_kernel, D / 128, grid, stream, x, ldx, gamma, beta, (bf16*)y, ldy, mean, rstd, M, eps);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

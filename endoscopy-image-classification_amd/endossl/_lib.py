@@ -28,6 +28,7 @@ SIGNATURES = {
     "es_set_attn_variant": (I, [I]),
     "es_set_attn_bwd_variant": (I, [I]),
     "es_set_attn_bwd_grid": (I, [I]),
+    "es_set_ln_fwd_grid": (I, [I]),
     "es_set_attn_bwd_long": (I, [I]),
     "es_splitk_reduce": (I, [V, V, I, I, I, V]),
     "es_tn_problem_size": (Z, []),

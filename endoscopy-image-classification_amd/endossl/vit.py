@@ -28,6 +28,8 @@ from . import _lib
 from ._lib import call, ptr
 
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT, EPI_GELU_D, EPI_MULAUX = range(9)
+# LayerNorm backward workgroups (grid-stride over row pairs; per-workgroup dgamma / dbeta partials)
+LN_BWD_BLOCKS = 1024
 
 
 # code/dataset.py:21-22 (transforms.Normalize on every ViT input); uint8 batches are normalised on the GPU
@@ -383,7 +385,7 @@ class Engine:
         if self._ws_ln is None:
             self._ws_ln = {}
         if lane not in self._ws_ln:
-            self._ws_ln[lane] = torch.empty(2 * 1024 * self.cfg.dim, dtype=torch.float32, device=self.device)
+            self._ws_ln[lane] = torch.empty(2 * LN_BWD_BLOCKS * self.cfg.dim, dtype=torch.float32, device=self.device)
         return self._ws_ln[lane]
 
     def side_stream(self):
@@ -564,7 +566,7 @@ class Engine:
         ws = self.ln_workspace(lane)
         fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"  # (_f32 in parity mode)
         self._call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
-             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), 1024, M, D, 0, _lib.stream())
+             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), LN_BWD_BLOCKS, M, D, 0, _lib.stream())
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True, grad_ready=None):
         """dlogits fp32 [n, C] (head "cls") or dfts fp32 [n, D] (head "emb") for the last train

@@ -132,6 +132,9 @@ int es_attn_cls_bwd(const void* qkv, int ldqkv, const void* o, int ldo, const fl
                     void* dqkv, int lddqkv, int nimg, int T, int H, float scale, hipStream_t stream);
 
 /* ---- LayerNorm(eps) (code/models/conformer.py:58,60,65) -------------------------------------- */
+/* tuning knob: 0 = the one-shot forward (a workgroup per 8 rows), > 0 = the grid-stride forward on this many
+   workgroups (bit-identical); returns the previous value */
+int es_set_ln_fwd_grid(int workgroups);
 int es_layernorm_fwd(const float* x, int ldx, const float* gamma, const float* beta, void* y, int ldy, float* mean,
                      float* rstd, int M, int D, float eps, hipStream_t stream);
 int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,

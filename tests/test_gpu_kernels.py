@@ -512,6 +512,17 @@ def test_layernorm_fwd_bwd(D, M):
     yr = F.layer_norm(xr, (D,), gr, br, 1e-6)
     torch.testing.assert_close(y.float(), yr.detach(), rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(mean, x.mean(1), rtol=1e-5, atol=1e-5)
+    # the one-shot forward (a workgroup per 8 rows) and the grid-stride one (few workgroups: each wave walks
+    # many row pairs with the next pair's loads in flight) are bit-identical
+    lib = _lib.load()
+    for grid in (0, 3):
+        old = lib.es_set_ln_fwd_grid(grid)
+        y2 = torch.full_like(y, 7.0)
+        m2, r2 = torch.zeros_like(mean), torch.zeros_like(rstd)
+        call("es_layernorm_fwd", ptr(x), D, ptr(gamma), ptr(beta), ptr(y2), D, ptr(m2), ptr(r2), M, D, 1e-6, S())
+        torch.cuda.synchronize()
+        lib.es_set_ln_fwd_grid(old)
+        assert torch.equal(y2, y) and torch.equal(m2, mean) and torch.equal(r2, rstd), grid
     dy = torch.randn(M, D, device=DEV)
     dres = torch.randn(M, D, device=DEV)
     yr.backward(dy)
