@@ -198,12 +198,17 @@ def _queue_join(main, side):
 # fusion block joins them (code/models/conformer.py:334-357 data flow, unchanged arithmetic).
 BRANCH_STREAMS = True
 _branch_streams = {}
+# HIP priorities of the branch stream and the weight-gradient stream (0 = the default stream's, -1 = higher).
+# S1 same box (scripts/gpu_prio.sh, profiles/r04_stream_priority.txt): both 0 139.81 / 140.01 ms, branch -1
+# 139.53 / 139.00, weight gradients -1 140.26 / 139.92, both -1 139.21 / 139.20
+BRANCH_PRIORITY = -1
+WGRAD_PRIORITY = 0
 
 
 def _branch_stream(device):
     st = _branch_streams.get(device)
     if st is None:
-        st = _branch_streams[device] = torch.cuda.Stream(device=device)
+        st = _branch_streams[device] = torch.cuda.Stream(device=device, priority=BRANCH_PRIORITY)
     return st
 
 
@@ -217,7 +222,7 @@ def _own(t):
 def _wgrad_stream(device):
     st = _wgrad_streams.get(device)
     if st is None:
-        st = _wgrad_streams[device] = torch.cuda.Stream(device=device)
+        st = _wgrad_streams[device] = torch.cuda.Stream(device=device, priority=WGRAD_PRIORITY)
     return st
 
 

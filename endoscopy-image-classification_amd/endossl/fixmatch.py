@@ -121,7 +121,7 @@ class FixMatch:
         stats = torch.empty(4, dtype=torch.float32, device=dev)  # lx, lu, mask_mean, total
         frozen = getattr(self, "frozen", False)
         if eng.overlap_fwd:  # weak forward on the side stream, beside the train forward
-            main, side = torch.cuda.current_stream(dev), eng.side_stream()
+            main, side = torch.cuda.current_stream(dev), eng.side_stream((B + nu) * m.cfg.T)
             side.wait_stream(main)
             with torch.cuda.stream(side):
                 logits_w = eng.forward(m.flat, [inputs_u_w], train=False)

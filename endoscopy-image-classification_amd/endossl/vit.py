@@ -30,6 +30,12 @@ from ._lib import call, ptr
 EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT, EPI_GELU_D, EPI_MULAUX = range(9)
 # LayerNorm backward workgroups (grid-stride over row pairs; per-workgroup dgamma / dbeta partials)
 LN_BWD_BLOCKS = 1024
+# HIP priority of the second stream (weak forward, overlapped weight gradients) for steps of at least
+# SIDE_PRIORITY_MIN_M train tokens (below it: 0, the default stream's).  Same-box A/Bs (scripts/gpu_ab_knobs3.sh,
+# scripts/gpu_prio.sh, profiles/r04_stream_priority.txt): F1 (100,864 tokens) -1 vs 0 30.34 / 30.33 / 30.22 vs
+# 30.59 / 30.51 / 30.39 ms; the N = 8 shard (12,608) 5.35 / 5.36 vs 5.32 / 5.31
+SIDE_PRIORITY = -1
+SIDE_PRIORITY_MIN_M = 65536
 
 
 # code/dataset.py:21-22 (transforms.Normalize on every ViT input); uint8 batches are normalised on the GPU
@@ -388,12 +394,16 @@ class Engine:
             self._ws_ln[lane] = torch.empty(2 * LN_BWD_BLOCKS * self.cfg.dim, dtype=torch.float32, device=self.device)
         return self._ws_ln[lane]
 
-    def side_stream(self):
+    def side_stream(self, tokens=0):
         """The second HIP stream (weak forward beside the train forward; weight gradients beside
-        the data-gradient chain)."""
+        the data-gradient chain): at SIDE_PRIORITY for a step of at least SIDE_PRIORITY_MIN_M train tokens,
+        else at the default stream's priority."""
+        prio = SIDE_PRIORITY if tokens >= SIDE_PRIORITY_MIN_M else 0
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        return self._side
+            self._side = {}
+        if prio not in self._side:
+            self._side[prio] = torch.cuda.Stream(device=self.device, priority=prio)
+        return self._side[prio]
 
     # -------------------------------------------------------------- forward
     def forward(self, flat, images_list, train):
@@ -595,7 +605,7 @@ class Engine:
         fv = lambda name: self.view(flat, name)  # noqa: E731
         ov = self.overlap
         main = torch.cuda.current_stream(self.device)
-        side = self.side_stream() if ov else None
+        side = self.side_stream(M) if ov else None
         grouped = self._grouped_wgrad(M, grad_ready)
         if grouped:
             # one dY set per layer (+ a spare for layer 0's unused dY of the embedding): the grouped launch
