@@ -17,10 +17,11 @@ from endossl._lib import call, ptr  # noqa: E402
 
 M_T, M_W = 512 * 197, 448 * 197
 D, HD = 384, 1536
-# (name, epi, M, N, K)  -- NT: C[M,N] = A[M,K] B[N,K]^T
+# (name, epi, M, N, K)  -- NT: C[M,N] = A[M,K] B[N,K]^T; the engine's epilogues (data gradients of the LN
+# inputs in bf16: Engine.DH_BF16)
 NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 7, M_T, HD, D),
       ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 8, M_T, HD, D),
-      ("fc1_dgrad", 4, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 4, M_T, D, 3 * D),
+      ("fc1_dgrad", 0, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 0, M_T, D, 3 * D),
       ("qkv_fwd_weak", 0, M_W, 3 * D, D), ("proj_fwd_weak", 2, M_W, D, D), ("fc2_fwd_weak", 2, M_W, D, HD)]
 # (name, M, N1, N2)  -- TN: out[N1,N2] = sum_m A1[m,N1] A2[m,N2]
 TN = [("fc2_wgrad", M_T, D, HD), ("fc1_wgrad", M_T, HD, D), ("proj_wgrad", M_T, D, D), ("qkv_wgrad", M_T, 3 * D, D)]

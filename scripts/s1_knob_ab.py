@@ -17,9 +17,13 @@ while args and "=" in args[0] and (args[0].startswith("es_") or args[0].startswi
     else:  # a module constant of the package, e.g. endossl.conformer.BN_Y_FREE=0
         import importlib
         mod, attr = knob.rsplit(".", 1)
-        m = importlib.import_module(mod)
+        try:
+            m = importlib.import_module(mod)
+        except ModuleNotFoundError:  # a class attribute, e.g. endossl.vit.Engine.TN_SHARE=0.5
+            pm, cls = mod.rsplit(".", 1)
+            m = getattr(importlib.import_module(pm), cls)
         old = getattr(m, attr)
-        setattr(m, attr, type(old)(int(val)))
+        setattr(m, attr, type(old)(float(val)) if isinstance(old, float) else type(old)(int(val)))
     print(f"{knob}={val} (was {old})", file=sys.stderr, flush=True)
 sys.argv = ["bench.py"] + (args or ["--workload", "s1", "--steps", "3", "--warmup", "2", "--no-cpu-baseline"])
 import bench  # noqa: E402
