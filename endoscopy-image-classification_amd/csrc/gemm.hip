@@ -1193,6 +1193,7 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //  * the GELU epilogues otherwise (weak fc1): 128x128 BK32 two-stage at 4-5 workgroups/CU for K <= 384;
   //  * the other K <= 384 GEMMs: 128x128 BK64 two-stage (variant 0) below M = 65,536 (qkv forward at a
   //    rank's half share 73 -> 61 us) and for N <= 384, else BK32;
+  //  * the patch embedding (EPI_PATCH): 128x128 BK64 at every size (r04: 0.74 / 0.68x the 256x128 BK64 kernel);
   //  * ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
   //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
   //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
@@ -1214,6 +1215,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
       variant = M < 65536 ? 0 : 6;
     else if (K >= 768 && N % 256 == 0 && epi != EPI_DGELU)
       variant = 6;
+    else if (epi == EPI_PATCH)  // the patch embedding (K = 768): F1 88.9 vs 120.0 us on nt256, weak 76.5 vs 111.7
+      variant = 0;
     else if (gelu)
       variant = K <= 384 ? 5 : 1;
     else if (K <= 384)

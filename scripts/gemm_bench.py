@@ -22,7 +22,8 @@ D, HD = 384, 1536
 NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 7, M_T, HD, D),
       ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 8, M_T, HD, D),
       ("fc1_dgrad", 0, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 0, M_T, D, 3 * D),
-      ("qkv_fwd_weak", 0, M_W, 3 * D, D), ("proj_fwd_weak", 2, M_W, D, D), ("fc2_fwd_weak", 2, M_W, D, HD)]
+      ("qkv_fwd_weak", 0, M_W, 3 * D, D), ("proj_fwd_weak", 2, M_W, D, D), ("fc2_fwd_weak", 2, M_W, D, HD),
+      ("patch_fwd", 5, 512 * 196, D, 768), ("patch_fwd_weak", 5, 448 * 196, D, 768)]
 # (name, M, N1, N2)  -- TN: out[N1,N2] = sum_m A1[m,N1] A2[m,N2]
 TN = [("fc2_wgrad", M_T, D, HD), ("fc1_wgrad", M_T, HD, D), ("proj_wgrad", M_T, D, D), ("qkv_wgrad", M_T, 3 * D, D)]
 
@@ -85,9 +86,9 @@ def main():
                 if N % {6: 256, 10: 128}.get(v, 128):
                     continue
                 lib.es_set_gemm_variant(v)
-                auxp = aux if epi in (2,) else (aux.bfloat16() if epi in (3, 8) else None)
+                auxp = aux if epi in (2, 5) else (aux.bfloat16() if epi in (3, 8) else None)
                 st = [ptr(A), K, ptr(Bw), K, ptr(bias) if epi not in (3, 4, 8) else None, ptr(C), N,
-                      ptr(C2) if epi in (1, 7) else None, ptr(auxp) if auxp is not None else None, N, M, N, K, 0, s]
+                      ptr(C2) if epi in (1, 7) else None, ptr(auxp) if auxp is not None else None, N, M, N, K, 196 if epi == 5 else 0, s]
                 call("es_gemm_nt", epi, *st)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
