@@ -23,7 +23,8 @@ NT = [("qkv_fwd", 0, M_T, 3 * D, D), ("proj_fwd", 2, M_T, D, D), ("fc1_fwd", 7, 
       ("fc2_fwd", 2, M_T, D, HD), ("fc1_fwd_weak", 6, M_W, HD, D), ("fc2_dgrad", 8, M_T, HD, D),
       ("fc1_dgrad", 0, M_T, D, HD), ("proj_dgrad", 0, M_T, D, D), ("qkv_dgrad", 0, M_T, D, 3 * D),
       ("qkv_fwd_weak", 0, M_W, 3 * D, D), ("proj_fwd_weak", 2, M_W, D, D), ("fc2_fwd_weak", 2, M_W, D, HD),
-      ("patch_fwd", 5, 512 * 196, D, 768), ("patch_fwd_weak", 5, 448 * 196, D, 768)]
+      ("patch_fwd", 5, 512 * 196, D, 768), ("patch_fwd_weak", 5, 448 * 196, D, 768),
+      ("kv_fwd_last", 0, M_T, 2 * D, D), ("kv_fwd_last_weak", 0, M_W, 2 * D, D)]  # last block: K / V only
 # (name, M, N1, N2)  -- TN: out[N1,N2] = sum_m A1[m,N1] A2[m,N2]
 TN = [("fc2_wgrad", M_T, D, HD), ("fc1_wgrad", M_T, HD, D), ("proj_wgrad", M_T, D, D), ("qkv_wgrad", M_T, 3 * D, D)]
 
