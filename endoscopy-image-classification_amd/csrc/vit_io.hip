@@ -195,33 +195,42 @@ __global__ __launch_bounds__(256) void cls_head_bwd_kernel(const float* __restri
   for (int j = 0; j < V; ++j) dx[(size_t)im * T * lddx + j * 64 + lane] = rstd * (gd[j] - s1 - xh[j] * s2);
 }
 
-// Parameter grads of the head + final norm, summed over images (fp32 atomics, small):
-//  dW[c][d] += sum dl[i][c] * y[i][d], db[c] += sum dl[i][c], dgamma[d] += sum dyn*xhat, dbeta += sum dyn
-__global__ void cls_head_wgrad_kernel(const float* __restrict__ dl, int lddl, const float* __restrict__ xhat,
-                                      const float* __restrict__ dyn, const float* __restrict__ gamma,
-                                      const float* __restrict__ beta, float* __restrict__ dW, float* __restrict__ db,
-                                      float* __restrict__ dgamma, float* __restrict__ dbeta, int n, int C, int D,
-                                      int chunk) {
-  const int d = blockIdx.x * blockDim.x + threadIdx.x;
-  const int i0 = blockIdx.y * chunk, i1 = min(i0 + chunk, n);
-  if (d < D) {
-    float sg = 0.f, sb = 0.f;
-    for (int i = i0; i < i1; ++i) {
-      sg += dyn[(size_t)i * D + d] * xhat[(size_t)i * D + d];
-      sb += dyn[(size_t)i * D + d];
-    }
-    atomicAdd(dgamma + d, sg);
-    atomicAdd(dbeta + d, sb);
-    for (int c = 0; c < C; ++c) {
-      float s = 0.f;
-      for (int i = i0; i < i1; ++i) s += dl[(size_t)i * lddl + c] * (xhat[(size_t)i * D + d] * gamma[d] + beta[d]);
-      atomicAdd(dW + (size_t)c * D + d, s);
-    }
+// Parameter grads of the head + final norm, summed over images in a fixed order (run-to-run reproducible):
+//  dW[c][d] += sum_i dl[i][c] * y[i][d], db[c] += sum_i dl[i][c], dgamma[d] += sum_i dyn*xhat, dbeta += sum_i dyn
+// Workgroup (x, r): columns d = 64x .. 64x + 63 of row r (r < C: dW row c = r; C: dgamma; C + 1: dbeta); wave w
+// sums images w, w + 4, .. per lane, the four wave sums are added in wave order; db[c] by wave 0 of workgroup
+// (0, c) over lanes, then a fixed shuffle tree.
+__global__ __launch_bounds__(256) void cls_head_wgrad_kernel(const float* __restrict__ dl, int lddl,
+                                                             const float* __restrict__ xhat,
+                                                             const float* __restrict__ dyn,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float* __restrict__ dW,
+                                                             float* __restrict__ db, float* __restrict__ dgamma,
+                                                             float* __restrict__ dbeta, int n, int C, int D) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int d = blockIdx.x * 64 + lane, r = blockIdx.y;
+  float s = 0.f;
+  if (r < C) {
+    const float g = gamma[d], b = beta[d];
+    for (int i = w; i < n; i += 4) s += dl[(size_t)i * lddl + r] * (xhat[(size_t)i * D + d] * g + b);
+  } else if (r == C) {
+    for (int i = w; i < n; i += 4) s += dyn[(size_t)i * D + d] * xhat[(size_t)i * D + d];
+  } else {
+    for (int i = w; i < n; i += 4) s += dyn[(size_t)i * D + d];
   }
-  if (blockIdx.x == 0 && threadIdx.x < C) {
-    float s = 0.f;
-    for (int i = i0; i < i1; ++i) s += dl[(size_t)i * lddl + threadIdx.x];
-    atomicAdd(db + threadIdx.x, s);
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0) {
+    const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    float* dst = r < C ? dW + (size_t)r * D : (r == C ? dgamma : dbeta);
+    dst[d] += t;
+    if (blockIdx.x == 0 && r < C) {
+      float sb = 0.f;
+      for (int i = lane; i < n; i += 64) sb += dl[(size_t)i * lddl + r];
+      sb = warp_sum(sb);
+      if (lane == 0) db[r] += sb;
+    }
   }
 }
 
@@ -361,12 +370,9 @@ int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamm
   if (n <= 0 || D % 64 || C <= 0 || C > 256) return ES_BAD_SHAPE;
   const int grid = (n + 3) / 4;
   HEAD_DISPATCH(cls_head_bwd_kernel, D / 64, grid, stream, dl, lddl, W, gamma, xhat, rstd, dyn, dx, lddx, T, n, C);
-  // ~64 image chunks (was 64 images per chunk: 16 workgroups, each thread 64 x C serial sums, 184 us
-  // at n = 512 on the critical path of the backward)
-  const int chunk = n >= 256 ? (n + 63) / 64 : 4;
-  dim3 g2((D + 255) / 256, (n + chunk - 1) / chunk);
+  dim3 g2(D / 64, C + 2);
   hipLaunchKernelGGL(cls_head_wgrad_kernel, g2, 256, 0, stream, dl, lddl, xhat, dyn, gamma, beta, dW, db, dgamma,
-                     dbeta, n, C, D, chunk);
+                     dbeta, n, C, D);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

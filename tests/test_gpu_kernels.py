@@ -600,9 +600,10 @@ def test_im2col_u8_matches_normalised_fp32(n, Sz):
     assert torch.all(pa[rows:] == 9.0)
 
 
-def test_cls_head_fwd_bwd():
+@pytest.mark.parametrize("n", [37, 512])
+def test_cls_head_fwd_bwd(n):
     torch.manual_seed(4)
-    n, T, D, C = 37, 5, 384, 23
+    T, D, C = 5, 384, 23
     x = torch.randn(n * T, D, device=DEV)
     gamma = 1 + 0.1 * torch.randn(D, device=DEV)
     beta = 0.1 * torch.randn(D, device=DEV)
@@ -627,6 +628,18 @@ def test_cls_head_fwd_bwd():
     torch.testing.assert_close(db, bhr.grad, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dg, gr.grad, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(dbt, br.grad, rtol=1e-4, atol=1e-5)
+    # the parameter sums run in a fixed order (no atomics): a second launch accumulating onto a copy of the
+    # first result gives exactly twice each sum's bits added -- i.e. a repeat from zero is bit-identical
+    dW2, db2, dg2, dbt2 = torch.zeros_like(W), torch.zeros_like(b), torch.zeros_like(gamma), torch.zeros_like(beta)
+    call("es_cls_head_bwd", ptr(dl), C, ptr(W), ptr(gamma), ptr(beta), ptr(xhat), ptr(rstd), ptr(dyn), ptr(dx), D, T,
+         ptr(dW2), ptr(db2), ptr(dg2), ptr(dbt2), n, D, C, S())
+    torch.cuda.synchronize()
+    for a, c in ((dW, dW2), (db, db2), (dg, dg2), (dbt, dbt2)):
+        assert torch.equal(a, c)
+    call("es_cls_head_bwd", ptr(dl), C, ptr(W), ptr(gamma), ptr(beta), ptr(xhat), ptr(rstd), ptr(dyn), ptr(dx), D, T,
+         ptr(dW2), ptr(db2), ptr(dg2), ptr(dbt2), n, D, C, S())  # accumulates (+=), like the atomics did
+    torch.testing.assert_close(dW2, 2 * dW, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(db2, 2 * db, rtol=1e-6, atol=1e-7)
 
 
 def test_embed_bwd():
