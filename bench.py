@@ -711,8 +711,12 @@ def main():
                                             "not measured in this run)") if traffic_src else None,
                          "algorithmic_flop": flop, "mean_launch_ms": round(mean_ms, 4), "launches": len(ev_ms),
                          "algorithmic_bytes": probe.get("layer_bytes"),
-                         "timed": "live in the timed steps" if live else "2 untimed eager steps after the timed "
-                                                                         "(graph-replayed) steps",
+                         "timed": ("live in the timed steps" if live else "2 untimed eager steps after the timed "
+                                                                          "(graph-replayed) steps")
+                                  + ("; by events the kernel dispatches stamp themselves (hipExtLaunchKernelGGL: "
+                                     "from the grouped kernel's start to the reduce launch's end, the span a "
+                                     "rocprofv3 kernel trace shows, not the stream position of an event record)"
+                                     if layer else ""),
                          "streams": 2 if ov[0] else 1, "tn_workspace_floats": int(tn_ws),
                          "cu_share": share,
                          "frac_of_share": round(tflops / (PEAK_BF16_TFLOPS * share), 4),

@@ -16,6 +16,8 @@
 // step k+1 is issued before the MFMAs of step k.
 #include <algorithm>
 
+#include <hip/hip_ext.h>
+
 #include "common.h"
 
 namespace es_gemm {
@@ -1497,7 +1499,8 @@ int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_w
 // out_g = dY_g^T X_g and bias_g = column sums of dY_g (both overwritten) for every problem of the
 // (host) table es_gemm_tn_big_grouped_prepare wrote: the split-K GEMM launch, then one reduce launch
 // over every problem's slabs and bias partials.  The table is passed by value in the kernel arguments.
-int es_gemm_tn_big_grouped(const void* table, int count, const int* dims, hipStream_t stream) {
+static int tn_big_grouped_launch(const void* table, int count, const int* dims, hipStream_t stream, hipEvent_t e0,
+                                 hipEvent_t e1) {
   if (!table || count <= 0 || !dims || dims[0] <= 0 || dims[1] < 0 || dims[2] < 0) return ES_BAD_ARG;
   if (count > TNG_MAX || dims[2] > 2 * TNG_MAX) return ES_BAD_SHAPE;
   const size_t lds = (size_t)2 * 64 * (TB1 + TB2) * 2;
@@ -1506,15 +1509,57 @@ int es_gemm_tn_big_grouped(const void* table, int count, const int* dims, hipStr
   TNBigTable bt{};
   for (int i = 0; i < count; ++i) bt.e[i] = g[i];
   bt.ng = count;
-  hipLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), lds, stream, bt);
+  // with events: hipExtLaunchKernelGGL stamps them at the kernels' own start / end (what rocprofv3's kernel
+  // trace reports), not where the stream reaches a hipEventRecord
+  if (e0 || e1)
+    hipExtLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), (uint32_t)lds, stream, e0,
+                          dims[2] > 0 ? nullptr : e1, 0, bt);
+  else
+    hipLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), lds, stream, bt);
   if (dims[2] > 0) {
     TNRedTable rt{};
     const TNRedEntry* r = (const TNRedEntry*)(g + count);
     for (int i = 0; i < dims[2]; ++i) rt.r[i] = r[i];
     rt.nr = dims[2];
-    hipLaunchKernelGGL(splitk_reduce_grouped_kernel, dim3(dims[1]), dim3(256), 0, stream, rt);
+    if (e1)
+      hipExtLaunchKernelGGL(splitk_reduce_grouped_kernel, dim3(dims[1]), dim3(256), 0, stream, nullptr, e1, 0, rt);
+    else
+      hipLaunchKernelGGL(splitk_reduce_grouped_kernel, dim3(dims[1]), dim3(256), 0, stream, rt);
   }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_gemm_tn_big_grouped(const void* table, int count, const int* dims, hipStream_t stream) {
+  return tn_big_grouped_launch(table, count, dims, stream, nullptr, nullptr);
+}
+
+// es_gemm_tn_big_grouped with timing: `start` takes the grouped kernel's start, `stop` the end of the reduce
+// launch (or of the kernel when there is none).  Events from es_event_create.
+int es_gemm_tn_big_grouped_timed(const void* table, int count, const int* dims, void* start, void* stop,
+                                 hipStream_t stream) {
+  if (!start || !stop) return ES_BAD_ARG;
+  return tn_big_grouped_launch(table, count, dims, stream, (hipEvent_t)start, (hipEvent_t)stop);
+}
+
+// timing events for the *_timed launches: created with timing enabled; elapsed = stop - start in ms after the
+// stop event completed (it waits for it)
+int es_event_create(void** ev) {
+  if (!ev) return ES_BAD_ARG;
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return ES_HIP_ERROR;
+  *ev = (void*)e;
+  return ES_OK;
+}
+
+int es_event_elapsed(void* start, void* stop, float* ms) {
+  if (!start || !stop || !ms) return ES_BAD_ARG;
+  if (hipEventSynchronize((hipEvent_t)stop) != hipSuccess) return ES_HIP_ERROR;
+  return hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop) == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_event_destroy(void* ev) {
+  if (!ev) return ES_BAD_ARG;
+  return hipEventDestroy((hipEvent_t)ev) == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
 int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream) {

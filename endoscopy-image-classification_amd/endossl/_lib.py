@@ -39,6 +39,10 @@ SIGNATURES = {
     "es_gemm_tn_big_grouped_workspace": (Z, [V, I, I]),
     "es_gemm_tn_big_grouped_prepare": (I, [V, I, I, V, Z, V, V]),
     "es_gemm_tn_big_grouped": (I, [V, I, V, V]),
+    "es_gemm_tn_big_grouped_timed": (I, [V, I, V, V, V, V]),
+    "es_event_create": (I, [V]),
+    "es_event_elapsed": (I, [V, V, V]),
+    "es_event_destroy": (I, [V]),
     "es_colsum": (I, [V, I, I, I, V, I, V, I, V]),
     "es_attn_fwd": (I, [V, I, V, I, V, I, I, I, F, V]),
     "es_attn_bwd": (I, [V, I, V, I, V, V, V, I, V, I, I, I, I, F, V]),
@@ -223,3 +227,29 @@ def ptr(t):
 
 def stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+class KernelEvent:
+    """A timing event for the library's *_timed launches (es_event_create): stamped by the kernel dispatch
+    itself, so start.elapsed_time(stop) is the launches' execution time as a rocprofv3 kernel trace reports
+    it.  Same interface as torch.cuda.Event.elapsed_time (ms; waits for `stop`)."""
+
+    def __init__(self):
+        self.handle = ctypes.c_void_p()
+        rc = load().es_event_create(ctypes.byref(self.handle))
+        if rc != 0:
+            raise EndosslLibraryError(f"es_event_create: status {rc}")
+
+    def elapsed_time(self, stop):
+        ms = ctypes.c_float()
+        rc = load().es_event_elapsed(self.handle, stop.handle, ctypes.byref(ms))
+        if rc != 0:
+            raise EndosslLibraryError(f"es_event_elapsed: status {rc}")
+        return ms.value
+
+    def __del__(self):
+        try:
+            if self.handle:
+                load().es_event_destroy(self.handle)
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass

@@ -816,10 +816,9 @@ class Engine:
         # serial engine), not the first block's whole-chip launch at the end of an overlapped backward
         if pr is not None and any(q[9] == pr["label"] for q in problems) and (layer > 0 or not self.overlap):
             flop = sum(2.0 * q[4] * q[1] * q[3] for q in problems)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            call("es_gemm_tn_big_grouped", raw, n, dims, _lib.stream())
-            e1.record()
+            # timed by the kernels' own start / end (hipExtLaunchKernelGGL events), as a kernel trace sees them
+            e0, e1 = _lib.KernelEvent(), _lib.KernelEvent()
+            call("es_gemm_tn_big_grouped_timed", raw, n, dims, e0.handle, e1.handle, _lib.stream())
             pr["events"].append((e0, e1, flop))
             pr["layer_kernel"] = (f"es_gemm_tn_big_grouped: one block's {n} weight-gradient GEMMs "
                                   f"({'+'.join(str(q[1]) + 'x' + str(q[3]) for q in problems)}) over M={problems[0][4]} "

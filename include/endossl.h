@@ -97,6 +97,15 @@ size_t es_gemm_tn_big_grouped_workspace(const void* problems, int count, int tar
 int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_wgs, float* workspace,
                                    size_t workspace_floats, void* table, int* dims);
 int es_gemm_tn_big_grouped(const void* table, int count, const int* dims, hipStream_t stream);
+/* the same launch with timing: `start` is stamped at the grouped kernel's own start, `stop` at the end of its
+   reduce launch (hipExtLaunchKernelGGL events: the kernels' execution, as a rocprofv3 kernel trace sees it, not
+   the stream position of a hipEventRecord).  Events from es_event_create. */
+int es_gemm_tn_big_grouped_timed(const void* table, int count, const int* dims, void* start, void* stop,
+                                 hipStream_t stream);
+/* timing events for the *_timed launches (hipEvent_t handles): create, elapsed ms (waits for `stop`), destroy */
+int es_event_create(void** ev);
+int es_event_elapsed(void* start, void* stop, float* ms);
+int es_event_destroy(void* ev);
 /* bias gradient: out[n] (+)= sum_m Y[m][n]  (workspace >= blocks*N floats) */
 int es_colsum(const void* Y, int ld, int M, int N, float* workspace, int blocks, float* out, int accumulate,
               hipStream_t stream);

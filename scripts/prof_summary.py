@@ -29,7 +29,8 @@ tr = os.path.join(src, "run_kernel_trace.csv")
 if os.path.exists(tr):
     agg = collections.defaultdict(lambda: [0, 0.0])
     for r in csv.DictReader(open(tr)):
-        m = re.search(r"(gemm_nt\w*<[^>]*>|gemm_tn_kernel|gemm_tn_big_kernel|splitk_reduce_kernel|attn_\w+<\d+>)",
+        m = re.search(r"(gemm_nt\w*<[^>]*>|gemm_tn_kernel|gemm_tn_big_grouped_kernel|gemm_tn_big_kernel|"
+                      r"splitk_reduce_grouped_kernel|splitk_reduce_kernel|attn_\w+<\d+>)",
                       r["Kernel_Name"])
         if not m:
             continue
@@ -40,10 +41,27 @@ if os.path.exists(tr):
               "|---:|---:|---:|---|---:|"]
     for (n, g), (c, t) in sorted(agg.items(), key=lambda x: -x[1][1]):
         lines.append(f"| {t / steps / 1e3:.3f} | {c / steps:.1f} | {t / c:.1f} | `{n}` | {g} |")
+    # the roofline site as the bench times it: a 96-workgroup grouped launch's start to the end of the reduce
+    # launch that follows it on the same queue
+    rows = sorted(csv.DictReader(open(tr)), key=lambda r: int(r["Start_Timestamp"]))
+    byq = collections.defaultdict(list)
+    for r in rows:
+        byq[r["Queue_Id"]].append(r)
+    spans, kern = [], []
+    for q in byq.values():
+        for i, r in enumerate(q[:-1]):
+            if ("tn_big_grouped" in r["Kernel_Name"] and int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]) == 96
+                    and "splitk_reduce_grouped" in q[i + 1]["Kernel_Name"]):
+                spans.append((int(q[i + 1]["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+                kern.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    site = (f" In this trace: {len(spans)} such launches, kernel {sum(kern) / len(kern):.1f} us on average, "
+            f"kernel start to reduce end {sum(spans) / len(spans):.1f} us (the span the bench's `mean_launch_ms` "
+            "times with kernel-stamped events).") if spans else ""
     lines += ["", "The bench's roofline site (a block's four weight-gradient GEMMs, fc2 / fc1 / proj / qkv over "
               "M = 100,864 tokens) is the `gemm_tn_big_grouped_kernel` launch of 96 workgroups (24 tiles of 384 x 192 "
-              "x 4 splits, 3/8 of the CUs, 12 per step + the patch-embedding one) plus its "
-              "`splitk_reduce_grouped_kernel`. Durations under the profiler run longer than the bench's live "
-              "HIP-event figure (lower clocks while profiling, MI355X_MICROARCH.md 'DVFS give-back' item 2)."]
+              "x 4 splits, 3/8 of the CUs, 12 per step) plus its `splitk_reduce_grouped_kernel`; the first block's "
+              "launch (whole chip, the end of the backward) and the patch embedding's are other grid sizes above."
+              + site + " Durations under the profiler run at lower clocks (MI355X_MICROARCH.md 'DVFS give-back' "
+              "item 2)."]
 open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines[:20]))

@@ -229,8 +229,9 @@ def test_gemm_tn_grouped_exact_integers():
     assert lib.es_gemm_tn_grouped_prepare(ctypes.byref(bad), 1) == -1  # N1 % 128
 
 
-def _big_grouped(problems, target):
-    """es_gemm_tn_big_grouped over [(A1, A2, out, bias, M, N1, N2, ld1, ld2)] -> dims."""
+def _big_grouped(problems, target, timed=False):
+    """es_gemm_tn_big_grouped over [(A1, A2, out, bias, M, N1, N2, ld1, ld2)] -> dims; `timed`: the
+    es_gemm_tn_big_grouped_timed form (kernel-stamped events; the span must be positive)."""
     import ctypes
     from endossl.vit import _TNProblem
     lib = _lib.load()
@@ -247,7 +248,12 @@ def _big_grouped(problems, target):
         assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need - 1, raw,
                                                   dims) != 0
     assert lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), len(problems), target, ptr(ws), need, raw, dims) == 0
-    call("es_gemm_tn_big_grouped", raw, len(problems), dims, S())
+    if timed:
+        e0, e1 = _lib.KernelEvent(), _lib.KernelEvent()
+        call("es_gemm_tn_big_grouped_timed", raw, len(problems), dims, e0.handle, e1.handle, S())
+        assert e0.elapsed_time(e1) > 0.0
+    else:
+        call("es_gemm_tn_big_grouped", raw, len(problems), dims, S())
     torch.cuda.synchronize()
     return list(dims), ws, raw
 
@@ -271,7 +277,7 @@ def test_gemm_tn_big_grouped_exact_integers():
             bias = torch.full((N1,), 5.0, device=DEV) if N2 != 192 else None
             probs.append((A1, A2, out, bias, M, N1, N2, ld1, N2))
             refs.append((out, bias, A1[:M, :N1].float().t() @ A2[:M].float(), A1[:M, :N1].float().sum(0)))
-        dims, _, _ = _big_grouped(probs, target)
+        dims, _, _ = _big_grouped(probs, target, timed=target in (24, 256))  # the timed form: same results
         assert dims[0] >= 23 and dims[2] == (0 if target == 24 else 2 * len(shapes) - 1)
         for out, bias, ref, bref in refs:
             torch.testing.assert_close(out, ref, rtol=0, atol=0)
