@@ -78,27 +78,54 @@ struct PackEntry {
   int N, K;
 };
 
-// grid.y = matrix, grid.x strides over 64x64 tiles of that matrix
+// grid.y = matrix, grid.x strides over 64x64 tiles of that matrix.  N, K multiples of 4 (every ViT / Conformer
+// Linear): 16-B loads of the fp32 master rows, 8-B bf16 stores of W rows and, through the LDS tile, of W^T rows;
+// otherwise element-wise.
 __global__ void pack_kernel(const float* __restrict__ flat, const PackEntry* __restrict__ tab) {
   __shared__ float tile[64][65];
   const PackEntry en = tab[blockIdx.y];
   const int tn = (en.N + 63) / 64, tk = (en.K + 63) / 64;
   const float* src = flat + en.src;
+  const bool vec = (en.N % 4 == 0) && (en.K % 4 == 0);
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
   for (int t = blockIdx.x; t < tn * tk; t += gridDim.x) {
     const int n0 = (t / tk) * 64, k0 = (t % tk) * 64;
-    for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
-      const int rr = i / 64, cc = i % 64;
-      const int n = n0 + rr, k = k0 + cc;
-      const float x = (n < en.N && k < en.K) ? src[(size_t)n * en.K + k] : 0.f;
-      tile[rr][cc] = x;
-      if (en.dst && n < en.N && k < en.K) en.dst[(size_t)n * en.K + k] = (bf16)x;
-    }
-    __syncthreads();
-    if (en.dstT) {
+    if (vec) {
+      for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) {
+        const int rr = i / 16, c4 = (i % 16) * 4;
+        const int n = n0 + rr, k = k0 + c4;
+        const bool ok = n < en.N && k < en.K;
+        const f32x4 x = ok ? *(const f32x4*)(src + (size_t)n * en.K + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tile[rr][c4 + j] = x[j];
+        if (en.dst && ok)
+          *(bf16x4_t*)(en.dst + (size_t)n * en.K + k) = bf16x4_t{(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+      }
+      __syncthreads();
+      if (en.dstT) {
+        for (int i = threadIdx.x; i < 64 * 16; i += blockDim.x) {
+          const int kk = i / 16, n4 = (i % 16) * 4;
+          const int n = n0 + n4, k = k0 + kk;
+          if (n < en.N && k < en.K)
+            *(bf16x4_t*)(en.dstT + (size_t)k * en.N + n) =
+                bf16x4_t{(bf16)tile[n4][kk], (bf16)tile[n4 + 1][kk], (bf16)tile[n4 + 2][kk], (bf16)tile[n4 + 3][kk]};
+        }
+      }
+    } else {
       for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
-        const int kk = i / 64, nn = i % 64;
-        const int n = n0 + nn, k = k0 + kk;
-        if (n < en.N && k < en.K) en.dstT[(size_t)k * en.N + n] = (bf16)tile[nn][kk];
+        const int rr = i / 64, cc = i % 64;
+        const int n = n0 + rr, k = k0 + cc;
+        const float x = (n < en.N && k < en.K) ? src[(size_t)n * en.K + k] : 0.f;
+        tile[rr][cc] = x;
+        if (en.dst && n < en.N && k < en.K) en.dst[(size_t)n * en.K + k] = (bf16)x;
+      }
+      __syncthreads();
+      if (en.dstT) {
+        for (int i = threadIdx.x; i < 64 * 64; i += blockDim.x) {
+          const int kk = i / 64, nn = i % 64;
+          const int n = n0 + nn, k = k0 + kk;
+          if (n < en.N && k < en.K) en.dstT[(size_t)k * en.N + n] = (bf16)tile[nn][kk];
+        }
       }
     }
     __syncthreads();
