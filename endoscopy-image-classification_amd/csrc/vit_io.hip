@@ -62,6 +62,38 @@ __global__ void im2col_u8_kernel(const uint8_t* __restrict__ img, bf16* __restri
   }
 }
 
+// The same values, one workgroup per (image, patch row): the band's 3 x 16 image rows arrive with 16-B loads
+// (whole rows, coalesced) into LDS, and the band's G consecutive output rows leave as 16-B stores in order
+// (every wave-instruction one contiguous KiB).  S % 16 == 0 (16-B source rows), dynamic LDS 48 x S bytes.
+__global__ __launch_bounds__(256) void im2col_u8_band_kernel(const uint8_t* __restrict__ img, bf16* __restrict__ out,
+                                                             int S, ChanNorm nm) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t band[];  // [3][16][S]
+  constexpr int P = 16, K = 3 * P * P;
+  const int G = S / P, im = blockIdx.x / G, py = blockIdx.x - im * G;
+  const int cpr = S / 16;  // 16-B chunks per image row
+  for (int i = threadIdx.x; i < 48 * cpr; i += blockDim.x) {
+    const int rr = i / cpr, ch = i - rr * cpr, c = rr >> 4, ky = rr & 15;
+    *(uint4*)(band + rr * S + ch * 16) =
+        *(const uint4*)(img + (((size_t)im * 3 + c) * S + py * P + ky) * S + ch * 16);
+  }
+  __syncthreads();
+  bf16* dst = out + (size_t)blockIdx.x * G * K;  // rows (im * G + py) * G .. + G - 1
+  for (int i = threadIdx.x; i < G * (K / 8); i += blockDim.x) {
+    const int px = i / (K / 8), k = (i - px * (K / 8)) * 8;
+    const int c = k / (P * P), ky = (k / P) % P, kx = k % P;
+    const uint2 raw = *(const uint2*)(band + (c * 16 + ky) * S + px * P + kx);
+    const float mu = c == 0 ? nm.mean[0] : (c == 1 ? nm.mean[1] : nm.mean[2]);
+    const float sd = c == 0 ? nm.std[0] : (c == 1 ? nm.std[1] : nm.std[2]);
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned b = ((j < 4 ? raw.x : raw.y) >> (8 * (j & 3))) & 255u;
+      o[j] = (bf16)(((float)b / 255.0f - mu) / sd);
+    }
+    *(bf16x8*)(dst + (size_t)i * 8) = o;
+  }
+}
+
 // x[img*T + 0][d] = cls[d] + pos[0][d]
 __global__ void cls_init_kernel(float* __restrict__ x, int ldx, const float* __restrict__ cls,
                                 const float* __restrict__ pos, int n, int T, int D) {
@@ -322,6 +354,11 @@ int es_patch_im2col_u8(const void* img, float mean0, float mean1, float mean2, f
   long grid = (total + 255) / 256;
   if (grid > 65536) grid = 65536;
   const ChanNorm nm{{mean0, mean1, mean2}, {std0, std1, std2}};
+  if (S % 16 == 0 && !((uintptr_t)img & 15) && 48 * S <= 65536) {
+    hipLaunchKernelGGL(im2col_u8_band_kernel, n * (S / 16), 256, 48 * S, stream, (const uint8_t*)img, (bf16*)patches,
+                       S, nm);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   hipLaunchKernelGGL(im2col_u8_kernel<16>, (int)grid, 256, 0, stream, (const uint8_t*)img, (bf16*)patches, n, S, nm);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }

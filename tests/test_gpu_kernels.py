@@ -604,6 +604,13 @@ def test_im2col_u8_matches_normalised_fp32(n, Sz):
     torch.cuda.synchronize()
     assert torch.equal(pa[:rows], pb)
     assert torch.all(pa[rows:] == 9.0)
+    if n == 5:  # pixels 8-B but not 16-B aligned: the element-wise gather instead of the LDS band kernel
+        buf = torch.zeros(u8.numel() + 16, dtype=torch.uint8, device=DEV)
+        buf[8:8 + u8.numel()] = u8.reshape(-1).to(DEV)
+        pc = torch.full((rows, 768), 9.0, dtype=torch.bfloat16, device=DEV)
+        call("es_patch_im2col_u8", ptr(buf) + 8, *mean, *std, ptr(pc), n, Sz, 16, S())
+        torch.cuda.synchronize()
+        assert torch.equal(pc, pb)
 
 
 @pytest.mark.parametrize("n", [37, 512])
