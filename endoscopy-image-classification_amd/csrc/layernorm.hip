@@ -166,12 +166,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
     ag[j] = ab[j] = make_float2(0.f, 0.f);
     gm[j] = *(const float2*)(gamma + (j * 64 + lane) * 2);
   }
-  for (int row0 = (blockIdx.x * 4 + w) * R; row0 < M; row0 += gridDim.x * 4 * R) {
-    float2 d[R][V], xv[R][V], rv[R][V];
-    float mean[R], rstd[R];
+  // the next row pair's dy / x / dres / mean / rstd loads are issued before this pair's math (two pairs in
+  // flight per wave); the arithmetic and its order are unchanged
+  float2 d[R][V], xv[R][V], rv[R][V];
+  float mean[R], rstd[R];
+  auto load = [&](int r0) {
 #pragma unroll
     for (int q = 0; q < R; ++q) {
-      const int row = min(row0 + q, M - 1);
+      const int row = min(r0 + q, M - 1);
       mean[q] = mean_in[row];
       rstd[q] = rstd_in[row];
 #pragma unroll
@@ -182,6 +184,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
         rv[q][j] = dres ? *(const float2*)(dres + (size_t)row * ldres + c) : make_float2(0.f, 0.f);
       }
     }
+  };
+  const int stride = gridDim.x * 4 * R;
+  int row0 = (blockIdx.x * 4 + w) * R;
+  if (row0 < M) load(row0);
+  for (; row0 < M; row0 += stride) {
+    float2 cd[R][V], cx[R][V], cr[R][V];
+    float cm[R], cs[R];
+#pragma unroll
+    for (int q = 0; q < R; ++q) {
+      cm[q] = mean[q];
+      cs[q] = rstd[q];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        cd[q][j] = d[q][j];
+        cx[q][j] = xv[q][j];
+        cr[q][j] = rv[q][j];
+      }
+    }
+    if (row0 + stride < M) load(row0 + stride);
 #pragma unroll
     for (int q = 0; q < R; ++q) {
       const int row = row0 + q;
@@ -190,22 +211,22 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
       for (int j = 0; j < V; ++j) {
-        xh[j] = make_float2((xv[q][j].x - mean[q]) * rstd[q], (xv[q][j].y - mean[q]) * rstd[q]);
-        gd[j] = make_float2(d[q][j].x * gm[j].x, d[q][j].y * gm[j].y);
+        xh[j] = make_float2((cx[q][j].x - cm[q]) * cs[q], (cx[q][j].y - cm[q]) * cs[q]);
+        gd[j] = make_float2(cd[q][j].x * gm[j].x, cd[q][j].y * gm[j].y);
         s1 += gd[j].x + gd[j].y;
         s2 += gd[j].x * xh[j].x + gd[j].y * xh[j].y;
-        ag[j].x += d[q][j].x * xh[j].x;
-        ag[j].y += d[q][j].y * xh[j].y;
-        ab[j].x += d[q][j].x;
-        ab[j].y += d[q][j].y;
+        ag[j].x += cd[q][j].x * xh[j].x;
+        ag[j].y += cd[q][j].y * xh[j].y;
+        ab[j].x += cd[q][j].x;
+        ab[j].y += cd[q][j].y;
       }
       s1 = warp_sum(s1) * (1.0f / D);
       s2 = warp_sum(s2) * (1.0f / D);
 #pragma unroll
       for (int j = 0; j < V; ++j) {
         const int c = (j * 64 + lane) * 2;
-        const float2 o = make_float2(rstd[q] * (gd[j].x - s1 - xh[j].x * s2) + rv[q][j].x,
-                                     rstd[q] * (gd[j].y - s1 - xh[j].y * s2) + rv[q][j].y);
+        const float2 o = make_float2(cs[q] * (gd[j].x - s1 - xh[j].x * s2) + cr[q][j].x,
+                                     cs[q] * (gd[j].y - s1 - xh[j].y * s2) + cr[q][j].y);
         *(float2*)(dx + (size_t)row * lddx + c) = o;
         if (dxb) {
           typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
