@@ -467,8 +467,10 @@ def _check_world(args, world):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 200 timed steps by default (~6 s of GPU work at F1): long enough for an external utilisation sampler to
+    # see the timed region, not only the CPU baseline
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="global labeled batch B (strong) / per-GPU B (weak)")
     ap.add_argument("--mu", type=int, default=7)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
