@@ -146,6 +146,56 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const float* __restrict_
   }
 }
 
+// embed_bwd_kernel with four consecutive features per lane (D, lddx, ldp multiples of 4): 16-B loads of dx,
+// 8-B bf16 stores of dpatch; every feature's image sums run in the same order, so the results are bit-identical.
+__global__ __launch_bounds__(256) void embed_bwd_vec_kernel(const float* __restrict__ dx, int lddx,
+                                                            bf16* __restrict__ dpatch, int ldp, float* __restrict__ dpos,
+                                                            float* __restrict__ dcls, int n, int T, int D,
+                                                            int accumulate) {
+  __shared__ f32x4 red[4][64];
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  const int id = (blockIdx.x * 64 + (threadIdx.x & 63)) * 4, ig = threadIdx.x >> 6;
+  const int total = T * D;
+  f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = s0;
+  int t = 0, d = 0;
+  if (id < total) {
+    t = id / D;
+    d = id % D;
+    int im = ig;
+#pragma unroll 4
+    for (; im + 4 < n; im += 8) {
+      const f32x4 v0 = *(const f32x4*)(dx + ((size_t)im * T + t) * lddx + d);
+      const f32x4 v1 = *(const f32x4*)(dx + ((size_t)(im + 4) * T + t) * lddx + d);
+      s0 += v0;
+      s1 += v1;
+      if (t > 0) {
+        *(bf16x4_t*)(dpatch + ((size_t)im * (T - 1) + t - 1) * ldp + d) =
+            bf16x4_t{(bf16)v0[0], (bf16)v0[1], (bf16)v0[2], (bf16)v0[3]};
+        *(bf16x4_t*)(dpatch + ((size_t)(im + 4) * (T - 1) + t - 1) * ldp + d) =
+            bf16x4_t{(bf16)v1[0], (bf16)v1[1], (bf16)v1[2], (bf16)v1[3]};
+      }
+    }
+    for (; im < n; im += 4) {
+      const f32x4 v = *(const f32x4*)(dx + ((size_t)im * T + t) * lddx + d);
+      s0 += v;
+      if (t > 0)
+        *(bf16x4_t*)(dpatch + ((size_t)im * (T - 1) + t - 1) * ldp + d) =
+            bf16x4_t{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    }
+  }
+  red[ig][threadIdx.x & 63] = s0 + s1;
+  __syncthreads();
+  if (ig == 0 && id < total) {
+    const int l = threadIdx.x & 63;
+    const f32x4 sv = (red[0][l] + red[1][l]) + (red[2][l] + red[3][l]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dpos[id + j] = accumulate ? dpos[id + j] + sv[j] : sv[j];
+      if (t == 0) dcls[d + j] = accumulate ? dcls[d + j] + sv[j] : sv[j];
+    }
+  }
+}
+
 // One wave per image: y = LN(x_cls) (eps), logits = y W^T + b.  Saves xhat (pre-affine) + rstd.
 template <int V>
 __global__ __launch_bounds__(256) void cls_head_fwd_kernel(const float* __restrict__ x, int ldx, int T,
@@ -373,6 +423,11 @@ int es_cls_init(float* x, int ldx, const float* cls, const float* pos, int n, in
 int es_embed_bwd(const float* dx, int lddx, void* dpatch, int ldp, float* dpos, float* dcls, int n, int T, int D,
                  int accumulate, hipStream_t stream) {
   if (n <= 0 || T <= 1 || D <= 0) return ES_BAD_SHAPE;
+  if (D % 4 == 0 && lddx % 4 == 0 && ldp % 4 == 0 && !((uintptr_t)dx & 15) && !((uintptr_t)dpatch & 7)) {
+    hipLaunchKernelGGL(embed_bwd_vec_kernel, (T * D / 4 + 63) / 64, 256, 0, stream, dx, lddx, (bf16*)dpatch, ldp, dpos,
+                       dcls, n, T, D, accumulate);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   const int grid = (T * D + 63) / 64;
   hipLaunchKernelGGL(embed_bwd_kernel, grid, 256, 0, stream, dx, lddx, (bf16*)dpatch, ldp, dpos, dcls, n, T, D,
                      accumulate);

@@ -15,14 +15,16 @@ from endossl._lib import call, ptr  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--pad", type=int, default=0, help="row stride D + pad (1: the per-feature kernel)")
     args = ap.parse_args()
     n, T, D = 512, 197, 384
-    dx = torch.randn(n * T, D, device="cuda")
+    ld = D + args.pad
+    dx = torch.randn(n * T, ld, device="cuda")
     dpatch = torch.empty(n * (T - 1), D, device="cuda", dtype=torch.bfloat16)
     dpos = torch.empty(T * D, device="cuda")
     dcls = torch.empty(D, device="cuda")
     s = _lib.stream()
-    f = lambda: call("es_embed_bwd", ptr(dx), D, ptr(dpatch), D, ptr(dpos), ptr(dcls), n, T, D, 0, s)  # noqa: E731
+    f = lambda: call("es_embed_bwd", ptr(dx), ld, ptr(dpatch), D, ptr(dpos), ptr(dcls), n, T, D, 0, s)  # noqa: E731
     ts = []
     for _ in range(5):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -33,7 +35,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1) / args.iters * 1e3)
-    print(f"embed_bwd {sorted(ts)[2]:.1f} us ({os.environ.get('ENDOSSL_LIB', 'in-tree')})")
+    print(f"embed_bwd {sorted(ts)[2]:.1f} us (row stride {ld}; {os.environ.get('ENDOSSL_LIB', 'in-tree')})")
 
 
 if __name__ == "__main__":

@@ -666,6 +666,18 @@ def test_embed_bwd():
     torch.testing.assert_close(dpos, v.sum(0), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dcls, v[:, 0].sum(0), rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(dp.float(), v[:, 1:].reshape(-1, D).bfloat16().float(), rtol=0, atol=0)
+    # the four-features-per-lane kernel (above: D, strides multiples of 4) vs the per-feature one (a row stride of
+    # D + 1 selects it): the same sums in the same order, bit for bit; accumulate adds onto the outputs
+    dxp = torch.zeros(n * T, D + 1, device=DEV)
+    dxp[:, :D] = dx
+    dp2 = torch.zeros_like(dp)
+    dpos2, dcls2 = torch.zeros_like(dpos), torch.zeros_like(dcls)
+    call("es_embed_bwd", ptr(dxp), D + 1, ptr(dp2), D, ptr(dpos2), ptr(dcls2), n, T, D, 0, S())
+    torch.cuda.synchronize()
+    assert torch.equal(dp2, dp) and torch.equal(dpos2, dpos) and torch.equal(dcls2, dcls)
+    call("es_embed_bwd", ptr(dx), D, ptr(dp), D, ptr(dpos), ptr(dcls), n, T, D, 1, S())
+    torch.testing.assert_close(dpos, 2 * dpos2, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(dcls, 2 * dcls2, rtol=1e-6, atol=1e-6)
 
 
 # ------------------------------------------------------------------------------------- losses (golden)
