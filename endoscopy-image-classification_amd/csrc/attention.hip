@@ -1736,9 +1736,11 @@ int es_set_attn_variant(int occ) {
   return old;
 }
 
-// tuning knob: attention backward loops (0 plain, 1 pipelined, 2 pipelined dQ + dkv2, 3 dq2 + dkv2 = default);
-// returns the previous value
+// tuning knob: attention backward loops (0 plain, 1 pipelined, 2 pipelined dQ + dkv2, 3 dq2 + dkv2,
+// 4 = default: the single-pass kernel for 13-tile heads, else as 3); returns the previous value, or
+// ES_BAD_ARG (state unchanged) for any other value
 int es_set_attn_bwd_variant(int v) {
+  if (v < 0 || v > 4) return ES_BAD_ARG;
   const int old = g_attn_bwd_pipe;
   g_attn_bwd_pipe = v;
   return old;

@@ -535,7 +535,7 @@ void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
 extern "C" {
 
 // 1 if the bf16 kernels take a conv of these channel counts (both multiples of 32)
-// tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 2048);
+// tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 512);
 // returns the previous value (v <= 0: unchanged)
 int es_set_conv_dw_target(int v) {
   const int old = g_dw_target_wg;

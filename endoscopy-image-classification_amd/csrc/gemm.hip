@@ -1199,9 +1199,9 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //  * ViT-B / Conformer-B widths (K >= 768, N % 256 == 0: every S1 transformer GEMM): the 256x256
   //    tile, 710-930 vs 620-900 TF/s (--s1) -- except the erf-per-element EPI_DGELU epilogue, serial
   //    behind the 8 waves' K loop at one workgroup per CU (S1 fc2 dgrad 1.97 vs 1.65 ms on the ring).
-  //  es_set_gemm_small_tile(0) drops the 64 x 128 rules; variant -2 drops the two-workgroup rules.
+  //  es_set_gemm_small_tile(0) drops the 64 x 128 rules.
   int variant = g_gemm_variant;
-  const bool two_wg = variant == -1;
+  const bool two_wg = true;
   if (variant < 0) {
     const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
     const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || epi == EPI_MULAUX;
@@ -1250,7 +1250,7 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
     if (N % tbn) return ES_BAD_SHAPE;
     return launch_big(variant, epi, ((M + 255) / 256) * (N / tbn), stream, a);
   }
-  if (variant != 0 && variant != 2 && variant != 5 && variant != 11) variant = 0;  // unknown pins
+  if (variant != 0 && variant != 2 && variant != 5 && variant != 11) return ES_BAD_ARG;  // es_set_gemm_variant checks
   const int tbm = variant == 11 ? 64 : BM;
   const int grid = ((M + tbm - 1) / tbm) * (N / BN);
   const int rc = launch_nt(variant, epi, grid, stream, a);
@@ -1259,20 +1259,22 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 }
 
 // Tuning knob: which NT kernel family es_gemm_nt launches (-1 = per-shape default, 0 = 128x128
-// BK64 2-stage, 1 = 256x128 BK64 3-stage, 2 = 128x128 BK32 3-stage, 3 = 128x128 BK32 4-stage,
-// 4 = 128x128 BK64 3-stage, 5 = 128x128 BK32 2-stage; 8 waves, one workgroup per CU, 128x64 or
-// 128x48 per wave: 6 = 256x256 BK64 2-stage, 7 = 256x192 BK64 2-stage, 8 = 256x256 BK32
-// 4-stage, 9 = 256x192 BK32 4-stage; 6/8 need N % 256 == 0, 7/9 N % 192 == 0; 10 = 256x128 BK32
-// 3-stage, 64x64 per wave, two workgroups per CU; 11 / 12 = 64x128 (waves of 32x64) BK64 2-stage / BK32
-// 3-stage).
-// Returns the previous value.
+// BK64 2-stage, 1 = 256x128 BK64 3-stage, 2 = 128x128 BK32 3-stage, 5 = 128x128 BK32 2-stage;
+// 6 = 256x256 BK64 2-stage (8 waves of 128x64, one workgroup per CU, N % 256 == 0); 10 = 256x128 BK32
+// 3-stage, 64x64 per wave, two workgroups per CU (N % 128 == 0); 11 = 64x128 (waves of 32x64) BK64
+// 2-stage).  Returns the previous value, or ES_BAD_ARG (state unchanged) for a family that does not
+// exist (the others were measured slower and removed in round 4).
+static bool gemm_variant_ok(int v) {
+  return v == -1 || v == 0 || v == 1 || v == 2 || v == 5 || v == 6 || v == 10 || v == 11;
+}
 int es_set_gemm_variant(int v) {
+  if (!gemm_variant_ok(v)) return ES_BAD_ARG;
   const int old = g_gemm_variant;
   g_gemm_variant = v;
   return old;
 }
 
-// Tuning knob: 1 = the 64 x 128 tile for small token shards in the per-shape rules, 0 (default) = without it.
+// Tuning knob: 1 (default) = the 64 x 128 tile for small token shards in the per-shape rules, 0 = without it.
 // Returns the previous value.
 int es_set_gemm_small_tile(int v) {
   const int old = g_small_tile;
@@ -1282,9 +1284,11 @@ int es_set_gemm_small_tile(int v) {
 
 // Tuning knob for es_gemm_tn: -1 = default, 0 = the 128x128 tile (32-token steps, two stages), 7 = the
 // 384x192 tile (64-token steps, two stages; shapes that do not tile fall back to 0).  A pin (>= 0) also
-// overrides the variant es_gemm_tn_ex callers name.  Returns the previous value.  (The other ring depths
-// and step sizes were measured slower and removed in round 4.)
+// overrides the variant es_gemm_tn_ex callers name (an A/B run pins every weight gradient).  Returns the
+// previous value, or ES_BAD_ARG (state unchanged) for any other value (the other ring depths and step
+// sizes were measured slower and removed in round 4).
 int es_set_tn_variant(int v) {
+  if (v != -1 && v != 0 && v != 7) return ES_BAD_ARG;
   const int old = g_tn_variant;
   g_tn_variant = v;
   return old;
@@ -1340,7 +1344,7 @@ int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N
   if (M <= 0 || (ld1 % 8) || (ld2 % 8)) return ES_BAD_SHAPE;
   if (!tn_big_ok(N1, N2, ld1, ld2) && ((N1 % BM) || (N2 % BN))) return ES_BAD_SHAPE;
   if (!A1 || !A2 || !out || !workspace) return ES_BAD_ARG;
-  if (variant > 13) return ES_BAD_ARG;
+  if (variant != -1 && variant != 0 && variant != 7) return ES_BAD_ARG;
   const int v = tn_pick(M, N1, N2, ld1, ld2, g_tn_variant >= 0 ? g_tn_variant : variant);
   const int BKM = v == 7 ? 64 : 32;
   const int msteps = (M + BKM - 1) / BKM;

@@ -201,8 +201,8 @@ def load(path=None):
     # kernel-family pins for A/B runs (scripts/): ENDOSSL_GEMM_VARIANT / ENDOSSL_TN_VARIANT (the other
     # es_set_* knobs are reached through the library handle)
     for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant")):
-        if os.environ.get(env):
-            getattr(lib, fn)(int(os.environ[env]))
+        if os.environ.get(env) and getattr(lib, fn)(int(os.environ[env])) == -2:
+            raise EndosslLibraryError(f"{env}={os.environ[env]}: no such kernel family ({fn} returned ES_BAD_ARG)")
     if path is None:
         _lib = lib
     return lib

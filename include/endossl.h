@@ -41,7 +41,8 @@ int es_abi_version(void);
  * N % 128 == 0, K % 64 == 0; A readable for round_up(M,256) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
-/* tuning knob: NT kernel family (-1 = per-shape default, 0..5 = fixed tilings, see gemm.hip); returns the old one */
+/* tuning knob: NT kernel family (-1 = per-shape default; 0, 1, 2, 5, 6, 10, 11 = fixed tilings, see gemm.hip);
+ * returns the old one, or -2 (state unchanged) for a family that does not exist */
 int es_set_gemm_variant(int variant);
 /* 1 (default): the 64 x 128 NT tile rules (N <= 384 outputs of small token shards, M < 32768, and the residual
  * proj forward); 0: without them.  Returns the old value. */
@@ -52,15 +53,16 @@ int es_set_gemm_small_tile(int v);
  * picks (es_gemm_tn_workspace(N1, N2, 0) bounds the workspace).  N1,N2 % 128 == 0, or N1 % 384 == 0
  * and N2 % 192 == 0; rows in [M, round_up(M,64)) of A1 must be zero. */
 /* tuning knob for es_gemm_tn: -1 = default (384x192 tile for M >= 65536 where it tiles, else
- * 128x128), 0..4 = 128x128 tile with (token step, ring depth) 32x2, 32x3, 32x4, 64x2, 64x3, 5..8 =
- * 384x192 tile with 32x2, 32x3, 64x2, 32x4; returns the previous value */
+ * 128x128), 0 = the 128x128 tile (32-token steps, two stages), 7 = the 384x192 tile (64-token steps,
+ * two stages); a pin >= 0 also overrides the variant es_gemm_tn_ex callers pass.  Returns the previous
+ * value, or -2 (state unchanged) for any other value */
 int es_set_tn_variant(int variant);
 size_t es_gemm_tn_workspace(int N1, int N2, int splits);
 int es_gemm_tn(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                float* workspace, float* out, int accumulate, float* bias_out, hipStream_t stream);
-/* es_gemm_tn with an explicit kernel choice (variant >= 0, the es_set_tn_variant numbering; -1 = the
- * process-wide setting): the engine passes the 384x192 tile for its CU-share-sized launches this way
- * instead of toggling the global knob around each call */
+/* es_gemm_tn with an explicit kernel choice (0 or 7, the es_set_tn_variant numbering; -1 = the
+ * library's per-shape choice; anything else -2): the engine passes the 384x192 tile for its
+ * CU-share-sized launches this way instead of toggling the global knob around each call */
 int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                   float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream);
 int es_splitk_reduce(const float* P, float* out, int S, int n, int accumulate, hipStream_t stream);
@@ -116,8 +118,9 @@ int es_reduce_partials(const float* P, float* out, int G, int N, int accumulate,
    else as 2; 2 = four waves, register budget of two workgroups per CU; 3 = four waves, three per CU;
    returns previous */
 int es_set_attn_variant(int occ);
-/* attention backward loops: 3 (default) = two query / key tiles per wave item (dq2 / dkv2), 2 = pipelined
-   dQ + dkv2, 1 = software-pipelined, 0 = plain (all bit-identical); returns the previous value */
+/* attention backward loops: 4 (default) = the single-pass kernel for 13-tile heads (192 < T <= 208), else
+   as 3; 3 = two query / key tiles per wave item (dq2 / dkv2), 2 = pipelined dQ + dkv2, 1 = software-pipelined,
+   0 = plain (all bit-identical); returns the previous value, or -2 (state unchanged) for any other value */
 int es_set_attn_bwd_variant(int v);
 /* tuning knob: the single-pass attention backward's workgroups (-1, the default: max(CUs, heads / 4);
    0: one persistent workgroup per CU); returns the previous value */
@@ -308,7 +311,7 @@ int es_conv2d_bwd_weight(const float* x, int N, int H, int W, int Cin, long sxn,
  * es_conv2d_pack_bf16 first: wp [Cout][kh kw][Cin] (forward), wt [Cin][kh kw][Cout] (data grad),
  * Cout Cin kh kw bf16 each, either pointer may be null. */
 int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw);
-/* tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 2048;
+/* tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 512;
    each split writes an fp32 slab of the gradient that a reduce kernel sums); returns the previous value */
 int es_set_conv_dw_target(int v);
 int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);

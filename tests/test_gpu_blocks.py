@@ -70,11 +70,18 @@ def _trainer(m, B, MU, thres):
     return tr
 
 
-@pytest.fixture(scope="module")
-def f1_step():
-    """One production FixMatch step at configs[1]'s size with the engine's capture hook on."""
+# configs[1]'s full batch, and the per-rank shard of configs[2] at N = 8 (B = 8, mu = 7: M = 12,608 train
+# tokens, where the engine runs every weight gradient of the step as the small shard's grouped launches,
+# Engine.GROUP_WGRAD, after the data-gradient chain)
+SIZES = {"f1": (64, 7), "shard8": (8, 7)}
+
+
+@pytest.fixture(scope="module", params=sorted(SIZES), ids=sorted(SIZES))
+def f1_step(request):
+    """One production FixMatch step at configs[1]'s size (and at the N = 8 shard) with the engine's
+    capture hook on."""
     from endossl.vit import NativeViT, ViTConfig
-    B, MU = 64, 7
+    B, MU = SIZES[request.param]
     rcfg = ref.Cfg()
     params = ref.random_params(rcfg, seed=31, head_std=0.5)
     g = torch.Generator(device=DEV).manual_seed(12)
@@ -103,7 +110,9 @@ def f1_step():
     eng.capture = None
     assert 0.0 < out["mask_mean"].item() < 1.0
     n_tr, n_w = B + B * MU, B * MU
-    return dict(rcfg=rcfg, params=params, p64={k: v.to(DEV, torch.float64) for k, v in params.items()},
+    # the weight-gradient path under test: split-K 384 x 192 launches at F1, the grouped launch at the shard
+    assert eng._grouped_wgrad(n_tr * rcfg.T, None) == (request.param == "shard8")
+    return dict(tag=request.param, rcfg=rcfg, params=params, p64={k: v.to(DEV, torch.float64) for k, v in params.items()},
                 x=x, us=us, uw=uw, m=m, eng=eng, cap=cap, tau=tau, mask_mean=out["mask_mean"].item(),
                 n_tr=n_tr, n_w=n_w, logits_tr=eng.acts(n_tr, True).logits.clone(),
                 logits_w=eng.acts(n_w, False).logits.clone())
@@ -188,7 +197,7 @@ def test_f1_ops_teacher_forced(f1_step):
             chk(f"block{i}.op.grad.{k}", eng.view(m.flat_grad, b + k).view(v.shape), v, F32)
         torch.cuda.empty_cache()
     rec["worst"] = _worst(rec)
-    _dump("op_parity_metrics.json", rec)
+    _dump(f"op_parity_metrics_{S['tag']}.json", rec)
     print("worst per op:", json.dumps({k: f"{v:.2e}" for k, v in sorted(rec["worst"].items())}))
     bad = {k: (v, bars[k]) for k, v in rec.items() if k in bars and v > bars[k]}
     assert not bad, f"above the bar: {bad}"
@@ -279,7 +288,7 @@ def test_f1_blockwise_teacher_forced_parity(f1_step):
     rec["floor_f32_vs_f64"] = floor
     rec["worst"] = _worst(rec)
     rec["worst_floor"] = _worst(floor)
-    _dump("block_parity_metrics.json", rec)
+    _dump(f"block_parity_metrics_{S['tag']}.json", rec)
     print("worst per category:", json.dumps({k: f"{v:.2e}" for k, v in sorted(rec["worst"].items())}))
     print("contract floor (oracle f32 vs f64):", json.dumps({k: f"{v:.2e}" for k, v in sorted(rec["worst_floor"].items())}))
     # the CPU and device float32 evaluations of the oracle: same contract, different summation order

@@ -283,6 +283,81 @@ def test_full_size_step_properties():
             mask_mean=out["mask_mean"].item())
 
 
+@pytest.mark.parametrize("nimg", [40, 64])
+def test_grouped_weight_gradients_match_split_k(nimg):
+    """Engine.GROUP_WGRAD (the small-shard backward): every weight gradient from ONE grouped launch
+    after the data-gradient chain, one dY set per layer, gives the split-K side-stream gradients up to
+    fp32 summation order (split-K slabs vs whole-axis tiles); the rest of the step is the same launch
+    sequence.  nimg 64: the last block's CLS-row Q weight gradient (strided rows) is in the group."""
+    from endossl.vit import NativeViT
+    vcfg, _ = _tiny_cfgs()
+    m = NativeViT(vcfg, seed=6).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn(nimg, 3, 64, 64, device=DEV, generator=g)
+    dl = torch.randn(nimg, 23, device=DEV, generator=g) * 1e-2
+    grads = {}
+    for mode in ("0", "1"):
+        eng.GROUP_WGRAD = mode
+        for _ in range(2):  # the second pass reuses the cached device table
+            eng.forward(m.flat, [x], train=True)
+            gr = torch.full_like(m.flat, 9.0)
+            eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        grads[mode] = gr.clone()
+    del eng.GROUP_WGRAD
+    worst = 0.0
+    for name, _ in eng.layout:
+        a, b = eng.view(grads["1"], name), eng.view(grads["0"], name)
+        assert torch.isfinite(a).all()
+        if b.abs().max() > 0:
+            worst = max(worst, _rel(a, b))
+    _record(f"grouped_wgrad_{nimg}", worst_rel_l2=worst)
+    assert worst <= 1e-5, worst
+
+
+@pytest.mark.parametrize("head,nimg", [("cls", 40), ("emb", 40), ("cls", 64), ("emb", 64)])
+def test_last_block_cls_rows_match_full_rows(head, nimg):
+    """Engine.PRUNE_LAST (the last block's attention for the CLS queries only, its projection / LN2 /
+    MLP on the CLS rows only) gives the logits / CLS features and every parameter gradient of the
+    full-row last block: the skipped rows feed nothing downstream, their gradient is exactly zero.
+    Differences come only from the CLS attention's fp32 summation order (bf16 rounding of o / dqkv)."""
+    from endossl.vit import NativeViT
+    vcfg, _ = _tiny_cfgs()
+    if head == "emb":
+        vcfg = type(vcfg)(**{**vcfg.as_dict(), "head": "emb"})
+    m = NativeViT(vcfg, seed=7).to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = torch.randn(nimg, 3, 64, 64, device=DEV, generator=g)  # 64: the CLS-row Q weight gradient (n % 32 == 0)
+    outs, grads = {}, {}
+    for prune in (False, True):
+        eng.PRUNE_LAST = prune
+        y = eng.forward(m.flat, [x], train=True).clone()
+        dy = torch.randn(y.shape, device=DEV, generator=torch.Generator(device=DEV).manual_seed(9)) * 1e-2
+        gr = torch.zeros_like(m.flat)
+        if head == "emb":
+            eng.backward(m.flat, gr, dfts=dy)
+        else:
+            eng.backward(m.flat, gr, dlogits=dy)
+        yw = eng.forward(m.flat, [x], train=False).clone()
+        torch.cuda.synchronize()
+        outs[prune], grads[prune] = (y, yw), gr.clone()
+    del eng.PRUNE_LAST
+    for a, b in zip(outs[True], outs[False]):
+        assert _rel(a, b) <= 2e-3, _rel(a, b)
+    worst = 0.0
+    for name, _ in eng.layout:
+        a, b = eng.view(grads[True], name), eng.view(grads[False], name)
+        assert torch.isfinite(a).all()
+        if b.abs().max() > 0:
+            worst = max(worst, _rel(a, b))
+    _record(f"last_block_cls_rows_{head}_{nimg}", worst_rel_l2=worst, out_rel=_rel(outs[True][0], outs[False][0]))
+    assert worst <= 1e-2, worst
+
+
 def test_uint8_input_path_matches_normalised_fp32():
     """es_patch_im2col_u8 (ToTensor + Normalize fused into the patch gather, code/dataset.py:21-22,
     49-51) gives the same logits, bit for bit, as the fp32 images normalised the torchvision way."""
