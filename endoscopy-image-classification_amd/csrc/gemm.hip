@@ -905,6 +905,8 @@ struct TNBigTable {
   TNBigEntry e[TNG_MAX];
   int ng, pad;
 };
+// BKM x NST: the token step and ring depth (64 x 2 by default; es_set_tn_grouped_ring picks 32 x 4 / 32 x 3)
+template <int BKM = 64, int NST = 2>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_grouped_kernel(const TNBigTable t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wg = xcd_remap(blockIdx.x, gridDim.x);
@@ -913,7 +915,7 @@ __global__ __launch_bounds__(512, 1) void gemm_tn_big_grouped_kernel(const TNBig
   const TNArgs a = t.e[e].a;
   const int local = wg - t.e[e].wg0, nt = t.e[e].ntiles;
   const int split = local / nt;
-  tn_big_body<64, 2, true, 0>(a, split, local - split * nt, smem);
+  tn_big_body<BKM, NST, true, 0>(a, split, local - split * nt, smem);
 }
 
 // out[i] = sum_s P[s][i] for every entry of a table (the grouped launch's weight slabs and bias
@@ -1163,6 +1165,7 @@ using namespace es_gemm;
 static int g_gemm_variant = -1;
 static int g_tn_variant = -1;
 static int g_small_tile = 1;  // the 64 x 128 tile rules (es_set_gemm_small_tile; 0 = without them)
+static int g_tn_grouped_ring = 0;  // es_gemm_tn_big_grouped's token step x ring depth (es_set_tn_grouped_ring)
 
 
 extern "C" {
@@ -1291,6 +1294,17 @@ int es_set_tn_variant(int v) {
   if (v != -1 && v != 0 && v != 7) return ES_BAD_ARG;
   const int old = g_tn_variant;
   g_tn_variant = v;
+  return old;
+}
+
+// Tuning knob for es_gemm_tn_big_grouped: 0 (default) = 64-token steps in a two-stage ring (147 KiB of LDS:
+// one 72-KiB stage in flight behind the MFMAs), 1 = 32-token steps in a four-stage ring (three 36-KiB stages in
+// flight, twice the barriers), 2 = 32-token steps, three stages.  Bit-identical results (the same per-token
+// MFMA order).  Returns the previous value, or ES_BAD_ARG (state unchanged) for any other value.
+int es_set_tn_grouped_ring(int v) {
+  if (v < 0 || v > 2) return ES_BAD_ARG;
+  const int old = g_tn_grouped_ring;
+  g_tn_grouped_ring = v;
   return old;
 }
 
@@ -1507,19 +1521,27 @@ static int tn_big_grouped_launch(const void* table, int count, const int* dims, 
                                  hipEvent_t e1) {
   if (!table || count <= 0 || !dims || dims[0] <= 0 || dims[1] < 0 || dims[2] < 0) return ES_BAD_ARG;
   if (count > TNG_MAX || dims[2] > 2 * TNG_MAX) return ES_BAD_SHAPE;
-  const size_t lds = (size_t)2 * 64 * (TB1 + TB2) * 2;
-  allow_lds(gemm_tn_big_grouped_kernel, lds);
   const TNBigEntry* g = (const TNBigEntry*)table;
   TNBigTable bt{};
   for (int i = 0; i < count; ++i) bt.e[i] = g[i];
   bt.ng = count;
   // with events: hipExtLaunchKernelGGL stamps them at the kernels' own start / end (what rocprofv3's kernel
   // trace reports), not where the stream reaches a hipEventRecord
-  if (e0 || e1)
-    hipExtLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), (uint32_t)lds, stream, e0,
-                          dims[2] > 0 ? nullptr : e1, 0, bt);
-  else
-    hipLaunchKernelGGL(gemm_tn_big_grouped_kernel, dim3(dims[0]), dim3(512), lds, stream, bt);
+#define TNG_LAUNCH(BKM_, NST_)                                                                              \
+  {                                                                                                       \
+    const size_t lds = (size_t)NST_ * BKM_ * (TB1 + TB2) * 2;                                             \
+    allow_lds(gemm_tn_big_grouped_kernel<BKM_, NST_>, lds);                                               \
+    if (e0 || e1)                                                                                         \
+      hipExtLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_grouped_kernel<BKM_, NST_>), dim3(dims[0]), dim3(512), \
+                            (uint32_t)lds, stream, e0, dims[2] > 0 ? nullptr : e1, 0, bt);                \
+    else                                                                                                  \
+      hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_grouped_kernel<BKM_, NST_>), dim3(dims[0]), dim3(512), lds, \
+                         stream, bt);                                                                     \
+  }
+  if (g_tn_grouped_ring == 1) TNG_LAUNCH(32, 4)
+  else if (g_tn_grouped_ring == 2) TNG_LAUNCH(32, 3)
+  else TNG_LAUNCH(64, 2)
+#undef TNG_LAUNCH
   if (dims[2] > 0) {
     TNRedTable rt{};
     const TNRedEntry* r = (const TNRedEntry*)(g + count);

@@ -33,6 +33,10 @@ Two granularities, relative L2 throughout:
       measured per quantity in the same run (the oracle evaluated in float32 on the device).
 The oracle runs through torch in float64 on the device at this size; the CPU fp32 oracle of one block
 (16 host threads) is checked against its float32 device evaluation in the same test.
+
+Both tests also run at configs[2]'s per-rank shard at N = 8 (B = 8, mu = 7: M = 12,608 train tokens), where
+the engine takes its small-shard paths -- the 64 x 128 NT tiles and every weight gradient of the step in the
+grouped whole-token-axis launches (Engine.GROUP_WGRAD) -- at the same bars (fp32 weight gradients 1e-5).
 """
 import json
 import os
