@@ -18,20 +18,24 @@ with strong scaling the line also carries `weak_scaling`: the same step timed wi
 rank (configs[2] as DDP would run it).
 
 Reported beside it:
-  roofline      the dominant kernel (the most GPU time per step: rocprofv3, profiles/r02*_summary.md)
-                = the weight-gradient GEMM gemm_tn (es_gemm_tn: TN kernel + split-K reduction), timed
-                live with HIP events on its launch stream (the side stream of the backward) at the
-                fc1 weight-gradient site: algorithmic 2*M*1536*384 FLOP per launch (M = train tokens)
-                vs the bf16 dense MFMA peak 2516.6 TFLOP/s.  traffic = HBM bytes of that same site
-                inside the F1 step (kernel + split-K and bias reductions), from rocprofv3 --pmc
-                FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes over this bench (scripts/gpu_pmc_step.sh,
-                scripts/pmc_site_bytes.py -> profiles/pmc_traffic.json).
+  roofline      the dominant kernel (the most GPU time per step: rocprofv3, profiles/r04e_summary.md) = a
+                transformer block's four weight-gradient GEMMs as ONE split-K launch (es_gemm_tn_big_grouped:
+                gemm_tn_big_grouped_kernel + its reduce), timed live by events the kernels stamp themselves
+                (hipExtLaunchKernelGGL) on the side stream they run on, at the CU-share-sized launches of blocks
+                10..1: algorithmic 2*M*(384*1536 + 1536*384 + 384*384 + 1152*384) FLOP per launch (M = train
+                tokens) vs the bf16 dense MFMA peak 2516.6 TFLOP/s; `isolated` = the same launch with the second
+                stream off.  traffic = HBM bytes of that launch inside the F1 step from rocprofv3 --pmc
+                FETCH_SIZE (x2, gfx950) / WRITE_SIZE passes over this bench (scripts/gpu_pmc_step.sh ->
+                profiles/pmc_traffic.json, labelled with the library build it was measured on).
   step_tflops   algorithmic 18.247 TFLOP per F1 step / step time.  The engine skips
                 the last block's non-CLS rows after its qkv GEMM (their outputs never reach the head;
                 Engine.PRUNE_LAST), so it executes fewer FLOPs than that: `executed_step_tflop`.
-  cpu_baseline  the oracle (CPU fp32 restatement pinned to the reference, kind "port") timed on a
-                bounded sample (B=8, mu=7: 56 unlabeled images/step) with torch.set_num_threads(
-                os.cpu_count()) on the host, rank 0, N=1.
+  mfma_util     the step's MFMA-busy SIMD-cycles from committed rocprofv3 --pmc passes
+                (profiles/<tag>_step_counters.json) over this run's step time; marked as measured on this
+                library build or as an estimate from another one (sha256 of libendossl_hip.so).
+  cpu_baseline  the oracle (CPU fp32 restatement pinned to the reference, kind "port") on every host core the
+                job may use, rank 0, N=1, on a bounded sample: B=16, mu=7 (112 unlabeled images per step),
+                one warm-up step then one timed step (~15 s each on the GPU box's 16 threads).
 """
 import argparse
 import json
@@ -141,13 +145,13 @@ def host_input_run(tr, B, MU, steps, dev):
             "source": "synthetic decoded RGB 500x375 frames (64), IS_CROP, S=224; decode not timed"}
 
 
-def cpu_baseline(B=64, MU=7, steps=1, warmup=0):
+def cpu_baseline(B=16, MU=7, steps=1, warmup=1):
     """Oracle (pinned CPU restatement) FixMatch step on every host core this process may use -- a
     reported baseline (torch.set_num_threads(os.cpu_count()), capped by the CPU share the
-    box grants: more threads than cores only oversubscribes).  Default: the full F1 batch (B=64, mu=7:
-    ~100 GB of fp32 autograd activations, within the ~270 GiB a GPU-box job may hold) for one step without a
-    separate warm-up (the timed step includes first-touch allocation; ~70 s); --cpu-batch 8 --cpu-steps 2
-    --cpu-warmup 1 is the round-3 sample."""
+    box grants: more threads than cores only oversubscribes).  Default: a bounded sample of the F1 step,
+    B=16, mu=7 (112 unlabeled images), one warm-up step (thread pools, first-touch of the allocator's pages)
+    then one timed step, ~30 s in all; --cpu-batch 64 runs the full F1 batch (~100 GB of fp32 autograd
+    activations, ~55 s per step)."""
     from oracle import ref
     threads, cpu_info = host_cpus()
     prev = torch.get_num_threads()
@@ -194,6 +198,17 @@ def cpu_baseline(B=64, MU=7, steps=1, warmup=0):
                       f"host RAM {mem} (the job may use at most ~270 GiB of it), torch.get_num_threads()={used}"}
 
 
+def lib_sha256():
+    """sha256 of the device library this process loads (ties committed counter files to a build)."""
+    import hashlib
+    from endossl import _lib
+    try:
+        with open(_lib.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def step_counters():
     """The committed step-level counter summary (scripts/gpu_step_counters.sh -> profiles/<tag>_step_counters.json,
     the newest tag): MFMA-busy SIMD-cycles and HBM bytes of one F1 step, measured by rocprofv3 --pmc passes over
@@ -216,7 +231,9 @@ def pmc_traffic(kernel_substr):
         d = json.load(open(p))
         for k, v in d.get("kernels", {}).items():
             if kernel_substr in k:
-                return v.get("hbm_bytes_per_launch"), f"committed profiles/pmc_traffic.json entry '{k}'"
+                build = ("measured on this library build" if v.get("lib_sha256") and v.get("lib_sha256") == lib_sha256()
+                         else "measured on another library build: an estimate for this one")
+                return v.get("hbm_bytes_per_launch"), f"committed profiles/pmc_traffic.json entry '{k}', {build}"
     except (OSError, ValueError):
         return None, None
     return None, None
@@ -475,9 +492,9 @@ def main():
     ap.add_argument("--mu", type=int, default=7)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=64, help="cpu_baseline labeled batch B (64 = the F1 batch)")
+    ap.add_argument("--cpu-batch", type=int, default=16, help="cpu_baseline labeled batch B (64 = the F1 batch)")
     ap.add_argument("--cpu-steps", type=int, default=1)
-    ap.add_argument("--cpu-warmup", type=int, default=0)
+    ap.add_argument("--cpu-warmup", type=int, default=1)
     ap.add_argument("--inputs", choices=("u8", "f32"), default="u8",
                     help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")
     ap.add_argument("--workload", choices=("f1", "c1", "s1", "p0"), default="f1",
@@ -734,8 +751,11 @@ def main():
         sc, sc_src = step_counters()
         if sc is not None and world == 1:
             busy = sc["step"]["mfma_busy_simd_cycles"]
+            same = sc.get("lib_sha256") is not None and sc.get("lib_sha256") == lib_sha256()
             res["mfma_util"] = {
                 "value": round(busy / (1024 * (ms / 1e3) * 2.4e9), 4),
+                "kind": ("counters measured on this library build" if same else
+                         "ESTIMATE: counters measured on another library build (" + str(sc.get("lib_sha256"))[:16] + ")"),
                 "mfma_busy_simd_cycles_per_step": busy,
                 "profiled": {k: round(v, 4) for k, v in sc["step"].items() if k.startswith(("mfma_util", "effective"))},
                 "hbm_bytes_per_step": sc["step"]["hbm_bytes"],

@@ -124,6 +124,28 @@ template <typename T> __device__ __forceinline__ typename Q4<T>::t q4_load(const
 }
 __device__ __forceinline__ void q4_store(float* p, f32x4 v) { *(f32x4*)p = v; }
 __device__ __forceinline__ void q4_store(bf16* p, f32x4 v) { *(bf16x4*)p = q4_b16(v); }
+// The BatchNorm affine map of the forward, (x - mean) * rstd * gamma + beta, with its one rounding point pinned
+// (an explicit fma): shared by conv.hip's bn_apply / mask-rebuilding backward kernels and by the bf16 convs'
+// gathers that apply a BatchNorm + ReLU to their input map on the fly (conv_bf16.hip, INBN), so the fused
+// gather reproduces the normalised map's bits exactly.
+__device__ __forceinline__ float bn_affine(float x, float mu, float rs, float ga, float be) {
+  return __builtin_fmaf((x - mu) * rs, ga, be);
+}
+// relu(bn_affine) of 4 consecutive channels, in the map's element type (bf16 maps: rounded once, as bn_apply
+// stores its output)
+__device__ __forceinline__ f32x4 bn_relu4(f32x4 x, f32x4 mu, f32x4 rs, f32x4 ga, f32x4 be) {
+  f32x4 o;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = fmaxf(bn_affine(x[j], mu[j], rs[j], ga[j], be[j]), 0.f);
+  return o;
+}
+__device__ __forceinline__ f32x4 q4_bn_relu(f32x4 x, f32x4 mu, f32x4 rs, f32x4 ga, f32x4 be) {
+  return bn_relu4(x, mu, rs, ga, be);
+}
+__device__ __forceinline__ bf16x4 q4_bn_relu(bf16x4 x, f32x4 mu, f32x4 rs, f32x4 ga, f32x4 be) {
+  return q4_b16(bn_relu4(q4_f32(x), mu, rs, ga, be));
+}
+
 // scalar forms
 __device__ __forceinline__ float m_f32(float v) { return v; }
 __device__ __forceinline__ float m_f32(bf16 v) { return (float)v; }

@@ -453,11 +453,8 @@ __device__ __forceinline__ void stv(bf16* __restrict__ p, const float (&v)[VEC])
   }
 }
 
-// The BatchNorm affine map of the forward, (x - mean) * rstd * gamma + beta: one function for bn_apply_kernel
-// and for the backward kernels that rebuild the ReLU mask from x (same expression, same rounding).
-__device__ __forceinline__ float bn_affine(float x, float mu, float rs, float ga, float be) {
-  return (x - mu) * rs * ga + be;
-}
+// The BatchNorm affine map of the forward (bn_affine, common.h): one function for bn_apply_kernel, for the
+// backward kernels that rebuild the ReLU mask from x and for the bf16 convs' BatchNorm-applying gathers.
 // the forward's y > 0 for a ReLU BatchNorm without residual: relu(affine) rounded to the map type T
 template <typename T>
 __device__ __forceinline__ bool bn_relu_live(float x, float mu, float rs, float ga, float be) {
@@ -1675,8 +1672,10 @@ int bn2d_fwd_global_impl(const T* x, int rows, int C, const float* gamma, const 
   hipLaunchKernelGGL(bn_finalize_global_kernel, (C + 255) / 256, 256, 0, stream, sum_g, sq_g, (float)rows_g, C, eps,
                      momentum, mean, rstd, running_mean, running_var);
   if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
-  const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
-  bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  if (y) {
+    const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
+    bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
@@ -1684,7 +1683,10 @@ template <typename T>
 int bn2d_fwd_partials_impl(const T* x, int rows, int C, float* partials, const float* gamma, const float* beta,
                            float* running_mean, float* running_var, void* num_batches_tracked, float momentum, float eps,
                            const T* res, int relu, T* y, float* mean, float* rstd, hipStream_t stream) {
-  if (!x || !partials || !gamma || !beta || !running_mean || !running_var || !y || !mean || !rstd) return ES_BAD_ARG;
+  // y == NULL (no residual): the statistics, running buffers and mean / rstd only -- a bf16 conv applies the
+  // normalisation as it gathers this map (es_conv2d_fwd_bf16_bnin_ex)
+  if (!x || !partials || !gamma || !beta || !running_mean || !running_var || (!y && res) || !mean || !rstd)
+    return ES_BAD_ARG;
   if (rows <= 0 || C <= 0) return ES_BAD_SHAPE;
   const long n = (long)rows * C;
   if (n >= (1L << 31)) return ES_BAD_SHAPE;
@@ -1701,8 +1703,10 @@ int bn2d_fwd_partials_impl(const T* x, int rows, int C, float* partials, const f
                        nblk, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
   }
   if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
-  const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
-  bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  if (y) {
+    const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
+    bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -55,6 +55,9 @@ struct NTConv {
   long osn, osh, osw;
   int accumulate;
   float* stats;  // forward only, nullable: per 128-pixel block [sum | M2] of every output channel
+  // forward only (INBN): the gathered map is a train-mode BatchNorm's INPUT; each in-range gathered channel
+  // quad becomes relu(bn_affine(x)) in the map's type -- the normalised map itself is never written
+  const float* bnm; const float* bnr; const float* bng; const float* bnb;
 };
 
 constexpr int NT_BM = 128, NT_BK = 32;
@@ -65,7 +68,8 @@ constexpr int NT_BM = 128, NT_BK = 32;
 //             taps ky = ky0 + s kyq (the only ones that reach this phase); source dy pixel
 //             (hq + qh - kyq, wq + qw - kxq) (conv.hip conv_dx_kernel's decomposition).
 // TS / TO: element types of the gathered map and of the output map (float or bf16).
-template <int BN, bool DX, bool STATS, typename TS, typename TO>
+// INBN (forward): BatchNorm + ReLU applied to every in-range gathered quad (padding stays zero).
+template <int BN, bool DX, bool STATS, typename TS, typename TO, bool INBN = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void convb_nt_kernel(NTConv a) {
   constexpr int NF = BN / 32;       // 16-col fragments per wave (wave covers BN / 2 cols)
   constexpr int BJ = BN / 64;       // 16-byte weight loads per thread per step
@@ -117,16 +121,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   const TS* src = (const TS*)a.src;
   typename Q4<TS>::t ra4[4];
   u32x4 rb[BJ];
+  // INBN: the step's BatchNorm channel quad and which gathered rows are in range (padding stays zero); the
+  // affine map + ReLU is applied in store(), after this step's MFMAs, so the loads stay in flight behind them
+  f32x4 bm, br, bg, bb;
+  bool aok[4];
   auto load = [&](int kt) {
     const int k0 = kt * NT_BK;
     const int tq = k0 / a.C, c0 = k0 - tq * a.C;
     const int tyq = tq / twx, txq = tq - tyq * twx;
+    if constexpr (INBN) {  // this step's channel quad of the BatchNorm (c0 + ac * 4: abase carries ac * 4)
+      const int cq = c0 + ac * 4;
+      bm = *(const f32x4*)(a.bnm + cq);
+      br = *(const f32x4*)(a.bnr + cq);
+      bg = *(const f32x4*)(a.bng + cq);
+      bb = *(const f32x4*)(a.bnb + cq);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
       ra4[j] = q4_zero<TS>();
-      if ((unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws)
-        ra4[j] = q4_load(src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
+      aok[j] = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
+      if (aok[j]) ra4[j] = q4_load(src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
     }
     const int btap = (by0 + tyq * bs) * a.kw + bx0 + txq * bs;
 #pragma unroll
@@ -142,7 +157,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int row = arow0 + 32 * j;
-      *(bf16x4*)(As + row * 64 + cswz64(row, ac >> 1) * 16 + (ac & 1) * 8) = q4_b16(ra4[j]);
+      typename Q4<TS>::t v = ra4[j];
+      if constexpr (INBN) v = aok[j] ? q4_bn_relu(v, bm, br, bg, bb) : q4_zero<TS>();
+      *(bf16x4*)(As + row * 64 + cswz64(row, ac >> 1) * 16 + (ac & 1) * 8) = q4_b16(v);
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
@@ -281,6 +298,7 @@ struct DWConv {
   int N, H, W, Cin, Ho, Wo, Cout, kh, kw, s, p;
   long sxn, sxh, sxw, syn, syh, syw;
   int M, mchunk;
+  const float* bnm; const float* bnr; const float* bng; const float* bnb;  // INBN: x is a BatchNorm's input
 };
 
 // pixel index -> (n, ho, wo), advanced without division
@@ -305,7 +323,8 @@ struct PixWalk {
 };
 
 // P[split][co][k'] = sum_{pixels m of the split} dy[m][co] . im2col(x)[m][k'], tile B1 (co) x B2 (k')
-template <int B1, int B2, typename TX, typename TD>
+// INBN: x is a train-mode BatchNorm's input; the gathered quads get its affine map + ReLU (as the forward's)
+template <int B1, int B2, typename TX, typename TD, bool INBN = false>
 __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
   constexpr int WA = (B1 == 128 && B2 == 64) ? 4 : (B1 == 64 && B2 == 128) ? 1 : 2, WB = 4 / WA;
   constexpr int F1 = B1 / WA / 16, F2 = B2 / WB / 16;  // fragments per wave along co / k'
@@ -334,6 +353,15 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
     ky = tap / a.kw;
     kx = tap - ky * a.kw;
   }
+  f32x4 bm = {0.f, 0.f, 0.f, 0.f}, br = bm, bg = bm, bb = bm;
+  if constexpr (INBN) {
+    if (kc_ok) {  // a thread's im2col columns keep one channel quad for the whole kernel
+      bm = *(const f32x4*)(a.bnm + ci);
+      br = *(const f32x4*)(a.bnr + ci);
+      bg = *(const f32x4*)(a.bng + ci);
+      bb = *(const f32x4*)(a.bnb + ci);
+    }
+  }
   PixWalk pw1[J1], pw2[J2];
 #pragma unroll
   for (int j = 0; j < J1; ++j) pw1[j].init(mbeg + r1 + RP1 * j, a.Ho, a.Wo);
@@ -344,6 +372,7 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
   const TD* dys = (const TD*)a.dy;
   typename Q4<TD>::t v1[J1];
   typename Q4<TX>::t v2[J2];
+  bool xok[J2];  // INBN: in-range im2col rows (the BatchNorm is applied in store(), padding stays zero)
   auto load = [&](int mm) {
 #pragma unroll
     for (int j = 0; j < J1; ++j) {
@@ -357,10 +386,11 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
     for (int j = 0; j < J2; ++j) {
       const int m = mm + r2 + RP2 * j;
       v2[j] = q4_zero<TX>();
+      xok[j] = false;
       if (m < mend && kc_ok) {
         const int h = pw2[j].ho * a.s - a.p + ky, ww = pw2[j].wo * a.s - a.p + kx;
-        if ((unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W)
-          v2[j] = q4_load(xs + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
+        xok[j] = (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+        if (xok[j]) v2[j] = q4_load(xs + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
       }
       pw2[j].advance(32, a.Ho, a.Wo);
     }
@@ -376,7 +406,9 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
 #pragma unroll
     for (int j = 0; j < J2; ++j) {
       const int row = r2 + RP2 * j;
-      *(bf16x4*)(T2 + row * 256 + cswz256(row, q2 >> 1) * 16 + (q2 & 1) * 8) = q4_b16(v2[j]);
+      typename Q4<TX>::t v = v2[j];
+      if constexpr (INBN) v = xok[j] ? q4_bn_relu(v, bm, br, bg, bb) : q4_zero<TX>();
+      *(bf16x4*)(T2 + row * 256 + cswz256(row, q2 >> 1) * 16 + (q2 & 1) * 8) = q4_b16(v);
     }
   };
 
@@ -510,24 +542,36 @@ inline int dw_splits(int M, int Cout, int K, int splits) {
 // the _ex entry points' map element-type flags: bit 0 = the gathered / input map is bf16, bit 1 = the
 // output map (bwd_weight: dy) is bf16
 
-template <int BN, bool DX, bool STATS>
+template <int BN, bool DX, bool STATS, bool INBN = false>
 void launch_nt(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
   switch (flags & 3) {
-    case 0: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, float>), grid, 256, 0, stream, a); break;
-    case 1: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, float>), grid, 256, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, bf16>), grid, 256, 0, stream, a); break;
-    default: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, bf16>), grid, 256, 0, stream, a); break;
+    case 0: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, float, INBN>), grid, 256, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, float, INBN>), grid, 256, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, bf16, INBN>), grid, 256, 0, stream, a); break;
+    default: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, bf16, INBN>), grid, 256, 0, stream, a); break;
   }
 }
 
-template <int B1, int B2>
+template <int B1, int B2, bool INBN = false>
 void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
   switch (flags & 3) {
-    case 0: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, float>), grid, 256, 0, stream, a); break;
-    case 1: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, float>), grid, 256, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, bf16>), grid, 256, 0, stream, a); break;
-    default: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, bf16>), grid, 256, 0, stream, a); break;
+    case 0: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, float, INBN>), grid, 256, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, float, INBN>), grid, 256, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, bf16, INBN>), grid, 256, 0, stream, a); break;
+    default: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, bf16, INBN>), grid, 256, 0, stream, a); break;
   }
+}
+
+// the forward / weight-gradient launches with or without the input BatchNorm
+template <int BN, bool STATS>
+void launch_fwd(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
+  if (a.bnm) launch_nt<BN, false, STATS, true>(grid, flags, a, stream);
+  else launch_nt<BN, false, STATS, false>(grid, flags, a, stream);
+}
+template <int B1, int B2>
+void launch_dw_bn(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
+  if (a.bnm) launch_dw<B1, B2, true>(grid, flags, a, stream);
+  else launch_dw<B1, B2, false>(grid, flags, a, stream);
 }
 
 }  // namespace
@@ -562,10 +606,11 @@ int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void*
 // element strides % 4 == 0.  flags: 1 = x is a bf16 map, 2 = y is a bf16 map (else fp32).  bn_partials
 // (nullable, accumulate 0 only): y's BatchNorm statistics per 128-pixel block (es_conv2d_bnstats_size
 // floats; from the fp32 accumulators).
-int es_conv2d_fwd_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
-                          const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, void* y,
-                          long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
-                          hipStream_t stream) {
+static int conv_fwd_bf16_impl(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                              const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, void* y,
+                              long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
+                              const float* bnm, const float* bnr, const float* bng, const float* bnb,
+                              hipStream_t stream) {
   if (!x || !wp || !y) return ES_BAD_ARG;
   if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0 ||
       (flags & ~3))
@@ -574,19 +619,42 @@ int es_conv2d_fwd_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn,
   if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(x) || !al16(y) || !al16(wp) ||
       (bias && !al16(bias)))
     return ES_BAD_SHAPE;
+  if (bnm && (!bnr || !bng || !bnb || !al16(bnm) || !al16(bnr) || !al16(bng) || !al16(bnb))) return ES_BAD_ARG;
   NTConv a{x, (const bf16*)wp, bias, y, N, Cin, Cout, H, W, sxn, sxh, sxw, kh, kw, stride, pad, Ho, Wo, syn, syh, syw,
-           accumulate, bn_partials};
+           accumulate, bn_partials, bnm, bnr, bng, bnb};
   if (bn_partials && accumulate) return ES_BAD_ARG;
   const int M = N * Ho * Wo;
   const dim3 g128((M + 127) / 128, Cout / 128), g64((M + 127) / 128, (Cout + 63) / 64);
   if (Cout % 128 == 0) {
-    if (bn_partials) launch_nt<128, false, true>(g128, flags, a, stream);
-    else launch_nt<128, false, false>(g128, flags, a, stream);
+    if (bn_partials) launch_fwd<128, true>(g128, flags, a, stream);
+    else launch_fwd<128, false>(g128, flags, a, stream);
   } else {
-    if (bn_partials) launch_nt<64, false, true>(g64, flags, a, stream);
-    else launch_nt<64, false, false>(g64, flags, a, stream);
+    if (bn_partials) launch_fwd<64, true>(g64, flags, a, stream);
+    else launch_fwd<64, false>(g64, flags, a, stream);
   }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_conv2d_fwd_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                          const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, void* y,
+                          long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
+                          hipStream_t stream) {
+  return conv_fwd_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh, syw,
+                            accumulate, bn_partials, flags, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+// es_conv2d_fwd_bf16_ex whose input map x is a train-mode BatchNorm + ReLU's INPUT: the conv reads
+// relu((x - mean) rstd gamma + beta) (rounded to x's map type, exactly as es_bn2d_fwd*_ex would have stored
+// it) as it gathers, so the normalised map is never written.  mean / rstd from es_bn2d_fwd_partials_ex with
+// y = NULL; all four per-channel arrays 16-byte aligned.
+int es_conv2d_fwd_bf16_bnin_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                               const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
+                               void* y, long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
+                               const float* in_mean, const float* in_rstd, const float* in_gamma,
+                               const float* in_beta, hipStream_t stream) {
+  if (!in_mean) return ES_BAD_ARG;
+  return conv_fwd_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, wp, bias, Cout, kh, kw, stride, pad, y, syn, syh, syw,
+                            accumulate, bn_partials, flags, in_mean, in_rstd, in_gamma, in_beta, stream);
 }
 
 int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
@@ -653,10 +721,10 @@ size_t es_conv2d_bwd_weight_bf16_workspace(int M, int Cout, int Cin, int kh, int
 // dw[co, ci, ky, kx] (+)= sum over output pixels of dy x im2col(x) (bf16 operands, fp32 sums); same
 // geometry arguments as es_conv2d_bwd_weight; splits <= 0 sizes the pixel split for the chip.
 // flags: 1 = x is a bf16 map, 2 = dy is a bf16 map.
-int es_conv2d_bwd_weight_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
-                                 const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
-                                 int pad, int splits, float* workspace, float* dw, int accumulate, int flags,
-                                 hipStream_t stream) {
+static int conv_dw_bf16_impl(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                             const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride, int pad,
+                             int splits, float* workspace, float* dw, int accumulate, int flags, const float* bnm,
+                             const float* bnr, const float* bng, const float* bnb, hipStream_t stream) {
   if (!x || !dy || !dw || !workspace) return ES_BAD_ARG;
   if (!es_conv2d_bf16_eligible(Cin, Cout, kh, kw) || N <= 0 || H <= 0 || W <= 0 || stride <= 0 || pad < 0 ||
       (flags & ~3))
@@ -665,23 +733,45 @@ int es_conv2d_bwd_weight_bf16_ex(const void* x, int N, int H, int W, int Cin, lo
   if (Ho <= 0 || Wo <= 0 || sxc != 1 || !st4(sxn, sxh, sxw) || !st4(syn, syh, syw) || !al16(x) || !al16(dy) ||
       !al16(workspace))
     return ES_BAD_SHAPE;
+  if (bnm && (!bnr || !bng || !bnb || !al16(bnm) || !al16(bnr) || !al16(bng) || !al16(bnb))) return ES_BAD_ARG;
   const int M = N * Ho * Wo, K = Cin * kh * kw;
   const int S0 = dw_splits(M, Cout, K, splits);
   int chunk = (M + S0 - 1) / S0;
   chunk = (chunk + 31) / 32 * 32;
   const int S = (M + chunk - 1) / chunk;
-  DWConv a{x, dy, workspace, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, sxn, sxh, sxw, syn, syh, syw, M, chunk};
+  DWConv a{x, dy, workspace, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, sxn, sxh, sxw, syn, syh, syw, M, chunk,
+           bnm, bnr, bng, bnb};
   int b1, b2;
   dw_tile(Cout, K, b1, b2);
   const dim3 grid((Cout + b1 - 1) / b1, (K + b2 - 1) / b2, S);
-  if (b1 == 128 && b2 == 128) launch_dw<128, 128>(grid, flags, a, stream);
-  else if (b1 == 64 && b2 == 128) launch_dw<64, 128>(grid, flags, a, stream);
-  else if (b1 == 128) launch_dw<128, 64>(grid, flags, a, stream);
-  else launch_dw<64, 64>(grid, flags, a, stream);
+  if (b1 == 128 && b2 == 128) launch_dw_bn<128, 128>(grid, flags, a, stream);
+  else if (b1 == 64 && b2 == 128) launch_dw_bn<64, 128>(grid, flags, a, stream);
+  else if (b1 == 128) launch_dw_bn<128, 64>(grid, flags, a, stream);
+  else launch_dw_bn<64, 64>(grid, flags, a, stream);
   const long n = (long)Cout * K;
   hipLaunchKernelGGL(convb_dw_reduce_kernel, (unsigned)((n / 4 + 63) / 64), 256, 0, stream, workspace, S, Cout, Cin,
                      kh * kw, dw, accumulate);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_conv2d_bwd_weight_bf16_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                                 const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
+                                 int pad, int splits, float* workspace, float* dw, int accumulate, int flags,
+                                 hipStream_t stream) {
+  return conv_dw_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, dy, syn, syh, syw, Cout, kh, kw, stride, pad, splits,
+                           workspace, dw, accumulate, flags, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+// es_conv2d_bwd_weight_bf16_ex for the conv of es_conv2d_fwd_bf16_bnin_ex: x is the BatchNorm's input and the
+// im2col gather applies the same affine map + ReLU
+int es_conv2d_bwd_weight_bf16_bnin_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw,
+                                      long sxc, const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw,
+                                      int stride, int pad, int splits, float* workspace, float* dw, int accumulate,
+                                      int flags, const float* in_mean, const float* in_rstd, const float* in_gamma,
+                                      const float* in_beta, hipStream_t stream) {
+  if (!in_mean) return ES_BAD_ARG;
+  return conv_dw_bf16_impl(x, N, H, W, Cin, sxn, sxh, sxw, sxc, dy, syn, syh, syw, Cout, kh, kw, stride, pad, splits,
+                           workspace, dw, accumulate, flags, in_mean, in_rstd, in_gamma, in_beta, stream);
 }
 
 int es_conv2d_bwd_weight_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,

@@ -285,6 +285,10 @@ BN_Y_FREE = True
 GRAD_SINKS = True
 # ... and the token buffer's two consumers (a block's FCUUp conv, the next block's FCUDown), _trans_branch
 TOKEN_SINK = True
+# a train-mode BatchNorm + ReLU whose output feeds ONE bf16 conv (a ConvBlock's bn1 -> conv2 without the FCUUp
+# add, and bn2 -> conv3 where x2 has no other consumer) is applied by that conv's gathers instead of being
+# written as a map (_BNConvFn); False materialises it (bn, then conv)
+BN_CONV_FUSED = True
 # bf16 activation / gradient maps in the CNN branch when every conv after the stem runs on conv_bf16.hip
 # (NativeConformer.map_bf16); ENDOSSL_MAP_BF16=0 keeps fp32 maps with bf16 conv operands
 MAP_BF16 = os.environ.get("ENDOSSL_MAP_BF16", "1") != "0"
@@ -561,6 +565,95 @@ class _BNFn(torch.autograd.Function):
 
 def bn(m, x, pre, eps=BN_EPS_BLOCK, relu=False, res=None, res_sink=None):
     return _BNFn.apply(x, res, m, pre, eps, relu, res_sink)
+
+
+class _BNConvFn(torch.autograd.Function):
+    """relu(BatchNorm2d(x)) -> Conv2d with the normalised map never written (code/models/conformer.py:118-134:
+    ConvBlock bn1 -> act1 -> conv2, bn2 -> act2 -> conv3).  Forward: the batch statistics from the producing
+    conv's epilogue partials (es_bn2d_fwd_partials_ex with y = NULL: running buffers, mean / rstd), then the
+    conv gathers relu((x - mean) rstd gamma + beta) rounded to the map's type (es_conv2d_fwd_bf16_bnin_ex) --
+    bit for bit the operand bn() would have written.  Backward: the conv's data gradient d(BN output), its
+    weight gradient with the same BatchNorm-applying gather (side stream), and the BatchNorm backward that
+    rebuilds the ReLU mask from x (es_bn2d_bwd_recompute_ex): every gradient bit-identical to bn() + conv()."""
+
+    @staticmethod
+    def forward(ctx, x, m, pre, eps, wname, bname, Cout, k, s, p, stats, out_dtype):
+        N, H, W, C = x.shape
+        rows = N * H * W
+        mean = torch.empty(C, device=x.device)
+        rstd = torch.empty(C, device=x.device)
+        rm, rv, nbt = m.bn_buffers(pre)
+        part = m._bn_partials.pop(x.data_ptr())
+        fl = _fl(x)
+        gam, bet = m.pview(pre + "weight"), m.pview(pre + "bias")
+        call("es_bn2d_fwd_partials_ex", ptr(x), rows, C, ptr(part[0]), ptr(gam), ptr(bet), ptr(rm), ptr(rv), ptr(nbt),
+             BN_MOMENTUM, eps, None, 1, None, ptr(mean), ptr(rstd), fl, _s())
+        xmap = _Map.nhwc(x)
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        y = torch.empty(N, Ho, Wo, Cout, dtype=out_dtype, device=x.device)
+        flags = fl | (_fl(y) << 1)
+        args = (xmap.p(), N, H, W, C, xmap.sn, xmap.sh, xmap.sw, xmap.sc)
+        tail = (ptr(m.pview(bname)) if bname else None, Cout, k, k, s, p, ptr(y), Ho * Wo * Cout, Wo * Cout, Cout, 0)
+        part_out = None
+        if stats and BN_STATS_FUSED:  # the next BatchNorm's statistics, as _ConvFn (train mode, world 1 here)
+            part_out = torch.empty(_lib.load().es_conv2d_bnstats_size(N * Ho * Wo, Cout), device=x.device)
+        call("es_conv2d_fwd_bf16_bnin_ex", *args, ptr(m.conv_pack(wname, Cout, C, k)[0]), *tail,
+             ptr(part_out) if part_out is not None else None, flags, ptr(mean), ptr(rstd), ptr(gam), ptr(bet), _s())
+        if part_out is not None:
+            m._bn_partials[y.data_ptr()] = (part_out, y.shape)
+        ctx.save_for_backward(x, mean, rstd)
+        ctx.m, ctx.pre, ctx.spec = m, pre, (wname, bname, Cout, k, s, p, Ho, Wo)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        _own(dy)
+        x, mean, rstd = ctx.saved_tensors
+        m, pre = ctx.m, ctx.pre
+        wname, bname, Cout, k, s, p, Ho, Wo = ctx.spec
+        N, H, W, C = x.shape
+        rows, M = N * H * W, N * Ho * Wo
+        dy = dy.contiguous()
+        lib = _lib.load()
+        gam, bet = m.pview(pre + "weight"), m.pview(pre + "bias")
+        side = _wgrad_stream(dy.device) if CONV_DW_SIDE and dy.is_cuda else None
+        if side is not None:
+            main = torch.cuda.current_stream(dy.device)
+            side.wait_stream(main)
+            _queue_join(main, side)
+            for t in (x, dy, mean, rstd):
+                t.record_stream(side)
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, C, k, k, 0), device=dy.device)
+            call("es_conv2d_bwd_weight_bf16_bnin_ex", ptr(x), N, H, W, C, H * W * C, W * C, C, 1, ptr(dy),
+                 Ho * Wo * Cout, Wo * Cout, Cout, Cout, k, k, s, p, 0, ptr(ws), ptr(m.gview(wname)), 0,
+                 _fl(x) | (_fl(dy) << 1), ptr(mean), ptr(rstd), ptr(gam), ptr(bet), _s())
+            if bname:
+                wsb = torch.empty(lib.es_chan_workspace(M, Cout), device=dy.device)
+                call("es_chan_sum_ex", ptr(dy), M, Cout, M * Cout, Cout, M, ptr(wsb), ptr(m.gview(bname)), 0, _fl(dy),
+                     _s())
+        dh = torch.empty_like(x)  # d(loss) / d(BN output): every pixel written (all stride phases)
+        call("es_conv2d_bwd_data_bf16_ex", ptr(dy), Ho * Wo * Cout, Wo * Cout, Cout, ptr(m.conv_pack(wname, Cout, C, k)[1]),
+             N, H, W, C, Cout, k, k, s, p, ptr(dh), H * W * C, W * C, C, 1, 0, _fl(dy) | (_fl(dh) << 1), _s())
+        dx = torch.empty_like(x)
+        wsn = torch.empty(lib.es_chan_workspace(rows, C), device=x.device)
+        call("es_bn2d_bwd_recompute_ex", ptr(x), ptr(dh), rows, C, ptr(gam), ptr(bet), ptr(mean), ptr(rstd), ptr(dx),
+             ptr(m.gview(pre + "weight")), ptr(m.gview(pre + "bias")), 0, ptr(wsn), _fl(x), _s())
+        return dx, None, None, None, None, None, None, None, None, None, None, None
+
+
+def bn_conv(m, x, pre, wname, bname, Cout, k, s=1, p=0, stats=False, out_dtype=None, eps=BN_EPS_BLOCK):
+    """conv(relu(bn(x))) for a train-mode BatchNorm whose output feeds this conv alone: fused (_BNConvFn) when the
+    conv runs on the bf16 kernels and the BatchNorm takes its statistics from x's producing conv (one rank's
+    rows); otherwise the two ops with the normalised map in between."""
+    out_dtype = out_dtype or _map_dtype(m)
+    world = dist.world_size() if getattr(m, "sync_bn", True) else 1
+    part = m._bn_partials.get(x.data_ptr())
+    if (BN_CONV_FUSED and BN_Y_FREE and m.training and world == 1 and CAPTURE is None and part is not None
+            and part[1] == x.shape and x.is_contiguous() and _conv_bf16(m, _Map.nhwc(x), Cout, k)):
+        return _BNConvFn.apply(x, m, pre, eps, wname, bname, Cout, k, s, p, stats, out_dtype)
+    h = bn(m, x, pre, eps=eps, relu=True)
+    return conv(m, h, _Map.nhwc(h), wname, bname, Cout, k, s, p, stats=stats, out_dtype=out_dtype)
 
 
 class _MaxPoolFn(torch.autograd.Function):
@@ -1102,27 +1195,34 @@ class NativeConformer(nn.Module):
 
     # ---- forward (code/models/conformer.py:418-445) ------------------------------------------
     def _conv_block(self, pre, x, stride, res_conv, x_t=None, return_x2=True):
-        """ConvBlock.forward (:107-144)."""
+        """ConvBlock.forward (:107-144).  Without return_x2, x2 feeds conv3 alone: bn2 + ReLU are applied by
+        conv3's gathers (bn_conv)."""
         sink = _GradSink() if GRAD_SINKS else None
-        x2 = self._conv_block_head(pre, x, stride, x_t, sink=sink)
-        out = self._conv_block_tail(pre, x, x2, stride, res_conv, sink=sink)
+        x2 = self._conv_block_head(pre, x, stride, x_t, sink=sink, raw_x2=not return_x2)
+        out = self._conv_block_tail(pre, x, x2, stride, res_conv, sink=sink, x2_raw=not return_x2)
         return (out, x2) if return_x2 else out
 
-    def _conv_block_head(self, pre, x, stride, x_t=None, sink=None):
+    def _conv_block_head(self, pre, x, stride, x_t=None, sink=None, raw_x2=False):
         """conv1 -> bn1 -> ReLU (-> + upsampled x_t) -> conv2 -> bn2 -> ReLU: x2 (:118-130).  sink: the
-        _GradSink x shares with the tail's residual."""
+        _GradSink x shares with the tail's residual.  Without the FCUUp add, bn1 + ReLU are applied by conv2's
+        gathers (bn_conv); raw_x2: return conv2's output before bn2 (the tail's conv3 applies it)."""
         med = self.shapes[pre + "conv1.weight"][0]
-        h = bn(self, conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1, stats=True, sink=sink),
-               pre + "bn1.", relu=True)
+        h = conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, med, 1, stats=True, sink=sink)
         if x_t is not None:
-            h = _UpsampleAddFn.apply(h, x_t, h.shape[1] // x_t.shape[1])
-        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1, stats=True)
-        return bn(self, h, pre + "bn2.", relu=True)
+            h = _UpsampleAddFn.apply(bn(self, h, pre + "bn1.", relu=True), x_t, h.shape[1] // x_t.shape[1])
+            h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, med, 3, stride, 1, stats=True)
+        else:
+            h = bn_conv(self, h, pre + "bn1.", pre + "conv2.weight", None, med, 3, stride, 1, stats=True)
+        return h if raw_x2 else bn(self, h, pre + "bn2.", relu=True)
 
-    def _conv_block_tail(self, pre, x, x2, stride, res_conv, sink=None):
-        """conv3 -> bn3 (+ residual, via residual_conv / residual_bn) -> ReLU (:132-144)."""
+    def _conv_block_tail(self, pre, x, x2, stride, res_conv, sink=None, x2_raw=False):
+        """conv3 -> bn3 (+ residual, via residual_conv / residual_bn) -> ReLU (:132-144).  x2_raw: x2 is conv2's
+        output before bn2 + ReLU, which conv3 applies (bn_conv)."""
         outp = self.shapes[pre + "conv3.weight"][0]
-        h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1, stats=True)
+        if x2_raw:
+            h = bn_conv(self, x2, pre + "bn2.", pre + "conv3.weight", None, outp, 1, stats=True)
+        else:
+            h = conv(self, x2, _Map.nhwc(x2), pre + "conv3.weight", None, outp, 1, stats=True)
         residual = x
         if res_conv:
             r = conv(self, x, _Map.nhwc(x), pre + "residual_conv.weight", None, outp, 1, stride, stats=True,

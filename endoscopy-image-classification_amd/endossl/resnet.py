@@ -19,7 +19,7 @@ import torch.nn as nn
 
 from . import _lib
 from .conformer import (BN_EPS_STEM, CONV_BF16, GRAD_SINKS, NativeConformer, _ConvHeadFn, _GradSink, _Map, _MaxPoolFn,
-                        _join_queued, _rup, bn, conv)
+                        _join_queued, _rup, bn, bn_conv, conv)
 
 BN_EPS = 1e-5  # timm BasicBlock norm_layer = nn.BatchNorm2d (default eps)
 
@@ -115,8 +115,8 @@ class NativeResNet(NativeConformer):
         """timm BasicBlock.forward: relu(bn2(conv2(relu(bn1(conv1(x))))) + shortcut)."""
         sink = _GradSink() if GRAD_SINKS else None  # x's two gradient contributions summed in place
         h = conv(self, x, _Map.nhwc(x), pre + "conv1.weight", None, planes, 3, stride, 1, stats=True, sink=sink)
-        h = bn(self, h, pre + "bn1.", eps=BN_EPS, relu=True)
-        h = conv(self, h, _Map.nhwc(h), pre + "conv2.weight", None, planes, 3, 1, 1, stats=True)
+        # bn1 + ReLU feed conv2 alone: applied by conv2's gathers where the bf16 kernels run it (bn_conv)
+        h = bn_conv(self, h, pre + "bn1.", pre + "conv2.weight", None, planes, 3, 1, 1, stats=True, eps=BN_EPS)
         if ds:
             sc = conv(self, x, _Map.nhwc(x), pre + "downsample.0.weight", None, planes, 1, stride, 0, stats=True,
                       sink=sink)

@@ -402,6 +402,21 @@ int es_conv2d_bwd_weight_bf16_ex(const void* x, int N, int H, int W, int Cin, lo
                                  const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw, int stride,
                                  int pad, int splits, float* workspace, float* dw, int accumulate, int flags,
                                  hipStream_t stream);
+/* The same forward / weight-gradient convs when x is the INPUT of a train-mode BatchNorm2d + ReLU whose output
+ * feeds this conv alone (ConvBlock bn1 -> conv2, bn2 -> conv3, code/models/conformer.py:118-134): the gathers
+ * apply relu((x - mean) rstd gamma + beta), rounded to x's map type exactly as es_bn2d_fwd*_ex stores it,
+ * so the normalised map is never written (es_bn2d_fwd_partials_ex with y = NULL gives mean / rstd; the
+ * backward is es_bn2d_bwd_recompute_ex).  Per-channel arrays 16-byte aligned. */
+int es_conv2d_fwd_bf16_bnin_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
+                               const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad,
+                               void* y, long syn, long syh, long syw, int accumulate, float* bn_partials, int flags,
+                               const float* in_mean, const float* in_rstd, const float* in_gamma,
+                               const float* in_beta, hipStream_t stream);
+int es_conv2d_bwd_weight_bf16_bnin_ex(const void* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw,
+                                      long sxc, const void* dy, long syn, long syh, long syw, int Cout, int kh, int kw,
+                                      int stride, int pad, int splits, float* workspace, float* dw, int accumulate,
+                                      int flags, const float* in_mean, const float* in_rstd, const float* in_gamma,
+                                      const float* in_beta, hipStream_t stream);
 int es_chan_sum_ex(const void* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
                    int accumulate, int flags, hipStream_t stream);
 int es_bn2d_fwd_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
@@ -416,6 +431,7 @@ int es_bn2d_bwd_ex(const void* x, const void* y, const void* dy, int rows, int C
 int es_bn2d_bwd_recompute_ex(const void* x, const void* dy, int rows, int C, const float* gamma, const float* beta,
                              const float* mean, const float* rstd, void* dx, float* dgamma, float* dbeta, int accumulate,
                              float* workspace, int flags, hipStream_t stream);
+/* es_bn2d_fwd_partials(_ex) with y = NULL (and no residual): statistics, running buffers, mean / rstd only */
 int es_bn2d_fwd_partials_ex(const void* x, int rows, int C, float* partials, const float* gamma, const float* beta,
                             float* running_mean, float* running_var, void* num_batches_tracked, float momentum,
                             float eps, const void* res, int relu, void* y, float* mean, float* rstd, int flags,

@@ -4,7 +4,7 @@ whole F1 step, from the FETCH_SIZE / WRITE_SIZE passes of scripts/gpu_pmc_step.s
 FETCH_SIZE x2 (the gfx950 correction of MI355X_MICROARCH.md), KiB -> bytes.  Blocks 10..1 (the CU-share
 sized launches; block 0's runs on the whole chip after the chain, the last block's is the K/V slice
 alone).  Writes the entry bench.py reports as roofline.traffic into profiles/pmc_traffic.json.
-  python scripts/pmc_layer_bytes.py gpurun_out [step]"""
+  python scripts/pmc_layer_bytes.py gpurun_out [step] [tag]"""
 import csv
 import json
 import os
@@ -13,6 +13,7 @@ import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
 want = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+tag = sys.argv[3] if len(sys.argv) > 3 else "r05"
 seqs = {}
 for i, cname in ((1, "FETCH_SIZE"), (2, "WRITE_SIZE")):
     rows = sorted((r for r in csv.DictReader(open(f"{root}/pstep{i}/run_counter_collection.csv"))
@@ -49,9 +50,14 @@ entry = {
     "note": "per block: dY and X of fc2 / fc1 / proj / qkv bf16 once + fp32 weight and bias outputs; the rest are "
             "the split-K slabs written by the GEMM kernel and re-read by the reduction",
 }
+import hashlib  # noqa: E402
+_root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+entry["lib_sha256"] = hashlib.sha256(open(os.path.join(_root, "endoscopy-image-classification_amd", "endossl", "lib",
+                                                       "libendossl_hip.so"), "rb").read()).hexdigest()
 print(json.dumps(entry, indent=1))
-p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_traffic.json")
+p = os.path.join(_root, "profiles", "pmc_traffic.json")
 d = json.load(open(p))
-d["kernels"] = {"es_gemm_tn_big_grouped block weight gradients in the F1 step (r03)": entry,
-                **{k: v for k, v in d["kernels"].items() if "es_gemm_tn_big_grouped" not in k}}
+# the newest measurement first (bench.py reports the first entry that names the kernel); older ones kept as history
+d["kernels"] = {f"es_gemm_tn_big_grouped block weight gradients in the F1 step ({tag})": entry,
+                **{k: v for k, v in d["kernels"].items() if not k.endswith(f"({tag})")}}
 json.dump(d, open(p, "w"), indent=1)

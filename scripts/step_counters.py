@@ -107,8 +107,11 @@ lines += ["", f"Step (profiled): wall {wall * 1e3:.2f} ms (two streams), kernel 
           f"**{step['mfma_util_effective_clock']:.3f}** at the effective clock {clk / 1e9:.2f} GHz "
           f"({step['mfma_util_nominal_clock']:.3f} at the nominal 2.4 GHz); HBM {tot['hbm'] / 1e9:.2f} GB = "
           f"{step['hbm_tbs']:.2f} TB/s over the step."]
-res = {"tag": tag, "families": out, "step": step,
-       "source": "scripts/gpu_step_counters.sh (rocprofv3 --kernel-trace --pmc, 3 passes over bench.py)"}
 pdir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
+import hashlib  # noqa: E402
+_lib_so = os.path.join(os.path.dirname(pdir), "endoscopy-image-classification_amd", "endossl", "lib", "libendossl_hip.so")
+res = {"tag": tag, "families": out, "step": step,
+       "lib_sha256": hashlib.sha256(open(_lib_so, "rb").read()).hexdigest(),
+       "source": "scripts/gpu_step_counters.sh (rocprofv3 --kernel-trace --pmc, 3 passes over bench.py)"}
 json.dump(res, open(os.path.join(pdir, f"{tag}_step_counters.json"), "w"), indent=1)
 open(os.path.join(pdir, f"{tag}_step_counters.md"), "w").write("\n".join(lines) + "\n")

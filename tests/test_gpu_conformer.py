@@ -738,6 +738,58 @@ def test_conformer_b_cnn_branch_bf16_vs_oracle():
                                               "conv_trans_3.cnn_block.bn1.running_mean"))
 
 
+def test_bn_relu_fused_into_conv_gather_bit_identical():
+    """conformer.BN_CONV_FUSED: a ConvBlock's bn1 -> conv2 and (x2 not returned) bn2 -> conv3 with the BatchNorm +
+    ReLU applied by the bf16 conv's gathers (es_conv2d_fwd_bf16_bnin_ex / es_conv2d_bwd_weight_bf16_bnin_ex, the
+    statistics-only es_bn2d_fwd_partials_ex, es_bn2d_bwd_recompute_ex) against the same ops with the normalised
+    map written in between: logits, every parameter gradient and every BatchNorm running buffer BIT-identical
+    over two train steps' forward + backward (Conformer-B's CNN branch, bf16 maps, strided 3x3 convs)."""
+    from endossl import conformer as cf
+    from endossl.conformer import ConformerConfig, NativeConformer
+    kw = dict(img_size=64, patch=16, base_channel=64, channel_ratio=4, embed_dim=128, depth=3, heads=2, num_classes=23)
+    saved = cf.BN_CONV_FUSED
+    res = {}
+    calls = {}
+    try:
+        for fused in (False, True):
+            cf.BN_CONV_FUSED = fused
+            m = NativeConformer(ConformerConfig(**kw), seed=11).to(DEV)
+            assert m.conv_bf16 and m.map_bf16
+            m.train()
+            g = torch.Generator().manual_seed(12)
+            n_fused = [0]
+            orig = cf._BNConvFn.apply
+
+            def counting(*a, _o=orig, _n=n_fused):
+                _n[0] += 1
+                return _o(*a)
+            cf._BNConvFn.apply = counting
+            outs = []
+            try:
+                for _ in range(2):
+                    x = torch.randn(6, 3, 64, 64, generator=g).to(DEV)
+                    m.flat_grad.zero_()
+                    oc, ot = m(x)
+                    w = torch.randn(oc.shape, generator=g).to(DEV), torch.randn(ot.shape, generator=g).to(DEV)
+                    (oc * w[0]).sum().add((ot * w[1]).sum()).backward()
+                    torch.cuda.synchronize()
+                    outs.append((oc.detach().clone(), ot.detach().clone(), m.flat_grad.clone(),
+                                 {k: v.clone() for k, v in m.state_dict().items() if cr.is_buffer(k)}))
+            finally:
+                cf._BNConvFn.apply = orig
+            res[fused], calls[fused] = outs, n_fused[0]
+    finally:
+        cf.BN_CONV_FUSED = saved
+    # conv_1's bn1 / bn2, each stage's cnn_block bn1 and fusion_block bn2 (fusion bn1 feeds the FCUUp add)
+    nst = len(list(ConformerConfig(**kw).stages()))
+    assert calls[False] == 0 and calls[True] == 2 * (2 + 2 * nst), calls
+    for (a_oc, a_ot, a_g, a_b), (b_oc, b_ot, b_g, b_b) in zip(res[False], res[True]):
+        assert torch.equal(a_oc, b_oc) and torch.equal(a_ot, b_ot)
+        assert torch.equal(a_g, b_g), (a_g - b_g).abs().max().item()
+        for k in a_b:
+            assert torch.equal(a_b[k], b_b[k]), k
+
+
 def _check_model_vs_oracle(m, state, ocfg, x, bn_keys):
     """Train-mode forward + backward vs the oracle in fp32 and in the device's bf16 contract.
 
