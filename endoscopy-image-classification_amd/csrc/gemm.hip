@@ -905,7 +905,8 @@ struct TNBigTable {
   TNBigEntry e[TNG_MAX];
   int ng, pad;
 };
-// BKM x NST: the token step and ring depth (64 x 2 by default; es_set_tn_grouped_ring picks 32 x 4 / 32 x 3)
+// 64-token steps in a two-stage ring (147 KiB of LDS).  Round 5 measured 32-token steps in four- and three-stage
+// rings (bit-identical): F1 30.94 / 30.87 vs 30.73 ms, the live launch 1.02-1.03 / 1.006 vs 1.028 ms -- removed.
 template <int BKM = 64, int NST = 2>
 __global__ __launch_bounds__(512, 1) void gemm_tn_big_grouped_kernel(const TNBigTable t) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1165,7 +1166,6 @@ using namespace es_gemm;
 static int g_gemm_variant = -1;
 static int g_tn_variant = -1;
 static int g_small_tile = 1;  // the 64 x 128 tile rules (es_set_gemm_small_tile; 0 = without them)
-static int g_tn_grouped_ring = 0;  // es_gemm_tn_big_grouped's token step x ring depth (es_set_tn_grouped_ring)
 
 
 extern "C" {
@@ -1294,17 +1294,6 @@ int es_set_tn_variant(int v) {
   if (v != -1 && v != 0 && v != 7) return ES_BAD_ARG;
   const int old = g_tn_variant;
   g_tn_variant = v;
-  return old;
-}
-
-// Tuning knob for es_gemm_tn_big_grouped: 0 (default) = 64-token steps in a two-stage ring (147 KiB of LDS:
-// one 72-KiB stage in flight behind the MFMAs), 1 = 32-token steps in a four-stage ring (three 36-KiB stages in
-// flight, twice the barriers), 2 = 32-token steps, three stages.  Bit-identical results (the same per-token
-// MFMA order).  Returns the previous value, or ES_BAD_ARG (state unchanged) for any other value.
-int es_set_tn_grouped_ring(int v) {
-  if (v < 0 || v > 2) return ES_BAD_ARG;
-  const int old = g_tn_grouped_ring;
-  g_tn_grouped_ring = v;
   return old;
 }
 
@@ -1538,9 +1527,7 @@ static int tn_big_grouped_launch(const void* table, int count, const int* dims, 
       hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_tn_big_grouped_kernel<BKM_, NST_>), dim3(dims[0]), dim3(512), lds, \
                          stream, bt);                                                                     \
   }
-  if (g_tn_grouped_ring == 1) TNG_LAUNCH(32, 4)
-  else if (g_tn_grouped_ring == 2) TNG_LAUNCH(32, 3)
-  else TNG_LAUNCH(64, 2)
+  TNG_LAUNCH(64, 2)
 #undef TNG_LAUNCH
   if (dims[2] > 0) {
     TNRedTable rt{};

@@ -25,7 +25,6 @@ SIGNATURES = {
     "es_gemm_tn": (I, [V, I, V, I, I, I, I, I, V, V, I, V, V]),
     "es_gemm_tn_ex": (I, [V, I, V, I, I, I, I, I, V, V, I, V, I, V]),
     "es_set_tn_variant": (I, [I]),
-    "es_set_tn_grouped_ring": (I, [I]),
     "es_set_attn_variant": (I, [I]),
     "es_set_attn_bwd_variant": (I, [I]),
     "es_set_attn_bwd_grid": (I, [I]),
@@ -204,8 +203,7 @@ def load(path=None):
         raise EndosslLibraryError(f"ABI mismatch: library {lib.es_abi_version()} != python {ABI_VERSION}")
     # kernel-family pins for A/B runs (scripts/): ENDOSSL_GEMM_VARIANT / ENDOSSL_TN_VARIANT (the other
     # es_set_* knobs are reached through the library handle)
-    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant"),
-                    ("ENDOSSL_TN_GROUPED_RING", "es_set_tn_grouped_ring")):
+    for env, fn in (("ENDOSSL_TN_VARIANT", "es_set_tn_variant"), ("ENDOSSL_GEMM_VARIANT", "es_set_gemm_variant")):
         if os.environ.get(env) and getattr(lib, fn)(int(os.environ[env])) == -2:
             raise EndosslLibraryError(f"{env}={os.environ[env]}: no such kernel family ({fn} returned ES_BAD_ARG)")
     if path is None:

@@ -160,7 +160,9 @@ class _Acts:
         D, Hd, L = cfg.dim, cfg.hidden, cfg.depth
         self.n, self.train = n, train
         self.M = n * cfg.T
-        Mp = _rup(self.M, 256)
+        # 256 rows beyond the padded token count: a half-batch lane's GEMM tiles (Engine.SHARD_LANES) start at
+        # an image boundary and read up to 256 rows past their last token
+        Mp = _rup(self.M, 256) + 256
         self.Mp = Mp
         Lk = L if train else 1
         f32 = torch.float32
@@ -196,7 +198,7 @@ class _Grads:
 
     def __init__(self, cfg, n, device, b16=torch.bfloat16):
         D, Hd = cfg.dim, cfg.hidden
-        Mp = _rup(n * cfg.T, 256)
+        Mp = _rup(n * cfg.T, 256) + 256  # (+ 256: the half-batch lanes' tile over-read, as _Acts)
         f32 = torch.float32
         z = lambda *s, dt=f32: torch.zeros(*s, dtype=dt, device=device)  # noqa: E731
         self.n = n
@@ -249,6 +251,12 @@ class Engine:
     GROUP_WGRAD = "auto"
     GROUP_WGRAD_MAX_M = 16384
     GROUP_LAYERS = 6
+    # ... and the data-gradient chain of blocks depth-2..0 as TWO lanes, the train images' halves on the caller's
+    # stream and the side stream, the grouped weight gradients on a third stream after both lanes.  The second
+    # stream is worth 13 % at N = 8 (6.25 -> 5.41 ms, weak forward / weight gradients beside the chain), but the
+    # split chain measured slower: 5.35 / 5.35 / 5.44 vs 5.30 / 5.29 / 5.29 ms (r05, one box, interleaved; the
+    # half-batch kernels lose more than the concurrency gains).  Off; bit-identical when on (test_gpu_step.py).
+    SHARD_LANES = False
     # A block's long-axis weight gradients (fc2, fc1, proj, qkv: 24 tiles of 384 x 192 at ViT-S) as ONE
     # split-K launch on the side stream once the block's data-gradient chain has produced its last dY
     # (es_gemm_tn_big_grouped) plus one reduce launch, sized to LAYER_TN_SHARE of the CUs (4 splits):
@@ -404,6 +412,12 @@ class Engine:
         if prio not in self._side:
             self._side[prio] = torch.cuda.Stream(device=self.device, priority=prio)
         return self._side[prio]
+
+    def third_stream(self):
+        """A third HIP stream: the small shard's grouped weight gradients beside the two chain lanes."""
+        if getattr(self, "_third", None) is None:
+            self._third = torch.cuda.Stream(device=self.device)
+        return self._third
 
     # -------------------------------------------------------------- forward
     def forward(self, flat, images_list, train):
@@ -571,12 +585,12 @@ class Engine:
         else:
             self._call(fn, *args)
 
-    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None):
+    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None, accumulate=0):
         D = self.cfg.dim
         ws = self.ln_workspace(lane)
         fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"  # (_f32 in parity mode)
         self._call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
-             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), LN_BWD_BLOCKS, M, D, 0, _lib.stream())
+             ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), LN_BWD_BLOCKS, M, D, accumulate, _lib.stream())
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True, grad_ready=None):
         """dlogits fp32 [n, C] (head "cls") or dfts fp32 [n, D] (head "emb") for the last train
@@ -615,6 +629,10 @@ class Engine:
                 self._grads[key] = [G] + [_Grads(cfg, n, self.device, self.op_dtype) for _ in range(cfg.depth)]
             GS = self._grads[key]
         ovw = ov and not grouped
+        nh = n // 2
+        lanes = (grouped and ov and self.SHARD_LANES and self.capture is None and n % 2 == 0 and nh > 0
+                 and self.precision == "bf16")
+        third = self.third_stream() if lanes else None
         problems = []
         layer_wg = self.LAYER_WGRAD and not grouped and self.precision == "bf16" and M >= self.TN_SHARE_MIN_M
         lp = []  # this block's long-axis weight gradients (layer_wg): one grouped launch at the block's end
@@ -655,9 +673,15 @@ class Engine:
             if self.capture is not None:
                 self.capture("bwd", True, i, G.dx[:M])
             if grouped and i > 0 and i % self.GROUP_LAYERS == 0 and problems:
-                # these layers' weight gradients as one grouped launch on the side stream, beside the
-                # rest of the data-gradient chain (their dY sets are never rewritten within the step)
-                if ov:
+                # these layers' weight gradients as one grouped launch on the side stream (two lanes: a third
+                # stream after both), beside the rest of the data-gradient chain (their dY sets are never
+                # rewritten within the step)
+                if lanes:
+                    third.wait_stream(main)
+                    third.wait_stream(side)
+                    with torch.cuda.stream(third):
+                        self._launch_grouped(problems, i)
+                elif ov:
                     side.wait_stream(main)
                     with torch.cuda.stream(side):
                         self._launch_grouped(problems, i)
@@ -735,6 +759,16 @@ class Engine:
                              gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
                 block_done(i)
                 continue
+            if lanes:
+                if i == (cfg.depth - 2 if prune else cfg.depth - 1):
+                    side.wait_stream(main)  # lane 1 starts from the last block's (or the head's) output gradient
+                self._lanes_block(flat, grad, A, G, Gi, Gn, i, n, nh, main, side)
+                wgrad_side(Gi.dxb, D, A.act[i], Hd, M, gv(b + "mlp.fc2.weight"), gv(b + "mlp.fc2.bias"))
+                wgrad_side(Gi.dpre, Hd, A.h2[i], D, M, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
+                wgrad_side(Gi.dxmb, D, A.o[i], D, M, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
+                wgrad_side(Gi.dqkv, 3 * D, A.h1[i], D, M, gv(b + "attn.qkv.weight"), gv(b + "attn.qkv.bias"))
+                block_done(i)
+                continue
             # ---- MLP:  x_{i+1} = xmid + fc2(gelu(fc1(LN2(xmid))))
             cap = self.capture  # test hook: each reverse-pass intermediate as the next op reads it
             if cap is not None:
@@ -775,6 +809,8 @@ class Engine:
             block_done(i)
         # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
         K0 = 3 * cfg.patch * cfg.patch
+        if lanes:
+            main.wait_stream(side)  # lane 1's rows of d(loss)/d(x_0)
         self._call("es_embed_bwd", ptr(G.dx), D, ptr(G.dpatch), D, ptr(gv("pos_embed")), ptr(gv("cls_token")), n, T, D, 0,
              s)
         npat = n * cfg.np
@@ -784,7 +820,54 @@ class Engine:
             self._launch_grouped(problems, 0)
         if ov:
             main.wait_stream(side)
+        if lanes:
+            main.wait_stream(third)
         return grad
+
+    def _lanes_block(self, flat, grad, A, G, Gi, Gn, i, n, nh, main, side):
+        """Block i's data-gradient chain as two lanes (Engine.SHARD_LANES): images [0, nh) on the caller's
+        stream, [nh, n) on the side stream, each on its rows of the same buffers (token rows are per image, the
+        chain never mixes images).  The LayerNorm parameter gradients are the only sums over both halves: lane 1
+        adds its share to lane 0's (accumulate), ordered by an event.  Lane 0 finished block i+1 on main, lane 1
+        on side; the embedding backward waits for both."""
+        cfg = self.cfg
+        D, Hd, T, H = cfg.dim, cfg.hidden, cfg.T, cfg.heads
+        EPI_DH = EPI_BF16 if self.DH_BF16 else EPI_F32  # noqa: N806
+        b = f"blocks.{i}."
+        fv = lambda name: self.view(flat, name)  # noqa: E731
+        gv = lambda name: self.view(grad, name)  # noqa: E731
+        ev = {}
+        for ln, st in ((0, main), (1, side)):
+            i0, nl = (0, nh) if ln == 0 else (nh, n - nh)
+            r0, Ml = i0 * T, nl * T
+            with torch.cuda.stream(st):
+                s = _lib.stream()
+                rp = lambda t, r0=r0: ptr(t[r0:])  # noqa: E731
+                self._call("es_gemm_nt", EPI_MULAUX if self.GELU_D else EPI_DGELU, rp(Gi.dxb), D,
+                           ptr(self.wt[b + "mlp.fc2.weight"]), D, None, rp(Gi.dpre), Hd, None, rp(A.pre[i]), Hd, Ml, Hd,
+                           D, 0, s)
+                self._call("es_gemm_nt", EPI_DH, rp(Gi.dpre), Hd, ptr(self.wt[b + "mlp.fc1.weight"]), Hd, None,
+                           rp(G.dh), D, None, None, 0, Ml, D, Hd, 0, s)
+                if ln == 1:
+                    st.wait_event(ev["ln2"])
+                self._ln_bwd(G.dh[r0:], A.xmid[i][r0:], A.mean2[i][r0:], A.rstd2[i][r0:], fv(b + "norm2.weight"),
+                             G.dx[r0:], G.dxm[r0:], Gi.dxmb[r0:], gv(b + "norm2.weight"), gv(b + "norm2.bias"), Ml,
+                             lane=ln, accumulate=ln)
+                if ln == 0:
+                    ev["ln2"] = st.record_event()
+                self._call("es_gemm_nt", EPI_BF16, rp(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
+                           rp(G.do), D, None, None, 0, Ml, D, D, 0, s)
+                self._call("es_attn_bwd", rp(A.qkv[i]), 3 * D, rp(A.o[i]), D, ptr(A.lse[i][i0 * H * T:]),
+                           ptr(G.delta[i0 * H * T:]), rp(G.do), D, rp(Gi.dqkv), 3 * D, nl, T, H, 64 ** -0.5, s)
+                self._call("es_gemm_nt", EPI_DH, rp(Gi.dqkv), 3 * D, ptr(self.wt[b + "attn.qkv.weight"]), 3 * D, None,
+                           rp(G.dh), D, None, None, 0, Ml, D, 3 * D, 0, s)
+                if ln == 1:
+                    st.wait_event(ev["ln1"])
+                self._ln_bwd(G.dh[r0:], A.x[i][r0:], A.mean1[i][r0:], A.rstd1[i][r0:], fv(b + "norm1.weight"),
+                             G.dxm[r0:], G.dx[r0:], Gn.dxb[r0:], gv(b + "norm1.weight"), gv(b + "norm1.bias"), Ml,
+                             lane=ln, accumulate=ln)
+                if ln == 0:
+                    ev["ln1"] = st.record_event()
 
     def _wgrad_layer(self, problems, layer):
         """One es_gemm_tn_big_grouped launch (+ its reduce) over a block's weight gradients, on the

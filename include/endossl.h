@@ -94,9 +94,6 @@ int es_gemm_tn_grouped(const void* device_table, int count, int total_tiles, hip
  * es_gemm_tn_big_grouped passes it by value in the kernel arguments) and dims[3] = {workgroups, reduce
  * blocks, reduce entries}; workspace >= es_gemm_tn_big_grouped_workspace floats.  Replaces the per-Linear es_gemm_tn launches of code/models/conformer.py:13-23,35-50's
  * backward (autograd's addmm weight gradients). */
-/* tuning knob: es_gemm_tn_big_grouped's token step x ring depth -- 0 (default) 64 x 2 stages, 1 = 32 x 4,
- * 2 = 32 x 3 (bit-identical results); returns the previous value, or -2 (state unchanged) for any other value */
-int es_set_tn_grouped_ring(int v);
 size_t es_gemm_tn_big_grouped_table_bytes(int count);
 size_t es_gemm_tn_big_grouped_workspace(const void* problems, int count, int target_wgs);
 int es_gemm_tn_big_grouped_prepare(const void* problems, int count, int target_wgs, float* workspace,

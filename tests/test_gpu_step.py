@@ -291,7 +291,11 @@ def test_grouped_weight_gradients_match_split_k(nimg):
     sequence.  nimg 64: the last block's CLS-row Q weight gradient (strided rows) is in the group."""
     from endossl.vit import NativeViT
     vcfg, _ = _tiny_cfgs()
-    m = NativeViT(vcfg, seed=6).to(DEV)
+    m = NativeViT(vcfg, seed=6)
+    with torch.no_grad():  # a non-zero head (timm zero-inits it): otherwise every trunk gradient is exactly zero
+        m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(3)))
+    m.mark_updated()
+    m = m.to(DEV)
     eng = m.engine()
     eng.pack(m.flat, m.version)
     g = torch.Generator(device=DEV).manual_seed(3)
@@ -311,10 +315,62 @@ def test_grouped_weight_gradients_match_split_k(nimg):
     for name, _ in eng.layout:
         a, b = eng.view(grads["1"], name), eng.view(grads["0"], name)
         assert torch.isfinite(a).all()
+        if name.endswith("weight") and name.startswith("blocks."):
+            assert b.abs().max() > 0, name  # the comparison is not vacuous
         if b.abs().max() > 0:
             worst = max(worst, _rel(a, b))
     _record(f"grouped_wgrad_{nimg}", worst_rel_l2=worst)
     assert worst <= 1e-5, worst
+
+
+@pytest.mark.parametrize("nimg,prune,full", [(40, True, False), (64, True, False), (38, False, False), (64, True, True)])
+def test_shard_lanes_match_single_lane(nimg, prune, full):
+    """Engine.SHARD_LANES (the small shard's data-gradient chain as two half-batch lanes on two streams, the
+    grouped weight gradients on a third): every gradient the lanes leave untouched by reordering -- all but the
+    LayerNorm parameters, whose halves lane 1 adds to lane 0's -- BIT-identical to the single-lane reverse pass
+    (rows are per image, the tiles and kernels the same), the LayerNorm ones within fp32 summation order.
+    nimg 38: 19 images per lane, token counts not multiples of the tile rows (the lanes' over-read padding);
+    full: ViT-S/16 at 224^2 with the N = 8 shard's 64 train images (M = 12,608 tokens, the production case)."""
+    from endossl.vit import NativeViT, ViTConfig
+    vcfg, _ = _tiny_cfgs()
+    if full:
+        vcfg = ViTConfig(num_classes=23)
+    m = NativeViT(vcfg, seed=8)
+    with torch.no_grad():  # a non-zero head (timm zero-inits it): otherwise every trunk gradient is exactly zero
+        m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(3)))
+    m.mark_updated()
+    m = m.to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    eng.GROUP_WGRAD = "1"
+    eng.PRUNE_LAST = prune
+    g = torch.Generator(device=DEV).manual_seed(5)
+    S = vcfg.img_size
+    x = torch.randn(nimg, 3, S, S, device=DEV, generator=g)
+    dl = torch.randn(nimg, 23, device=DEV, generator=g) * 1e-2
+    grads = {}
+    for lanes in (False, True):
+        eng.SHARD_LANES = lanes
+        for _ in range(2):  # the second pass reuses the cached tables / buffers
+            eng.forward(m.flat, [x], train=True)
+            gr = torch.full_like(m.flat, 7.0)
+            eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        grads[lanes] = gr.clone()
+    for k in ("GROUP_WGRAD", "PRUNE_LAST", "SHARD_LANES"):
+        delattr(eng, k)
+    worst_ln = 0.0
+    for name, _ in eng.layout:
+        a, b = eng.view(grads[True], name), eng.view(grads[False], name)
+        assert torch.isfinite(a).all(), name
+        if name.startswith("blocks."):
+            assert b.abs().max() > 0, name  # the comparison is not vacuous
+        if ".norm1." in name or ".norm2." in name:
+            worst_ln = max(worst_ln, _rel(a, b))
+        else:
+            assert torch.equal(a, b), (name, (a - b).abs().max().item())
+    _record(f"shard_lanes_{nimg}_{int(prune)}", worst_ln_rel_l2=worst_ln)
+    assert worst_ln <= 1e-6, worst_ln
 
 
 @pytest.mark.parametrize("head,nimg", [("cls", 40), ("emb", 40), ("cls", 64), ("emb", 64)])
@@ -327,7 +383,12 @@ def test_last_block_cls_rows_match_full_rows(head, nimg):
     vcfg, _ = _tiny_cfgs()
     if head == "emb":
         vcfg = type(vcfg)(**{**vcfg.as_dict(), "head": "emb"})
-    m = NativeViT(vcfg, seed=7).to(DEV)
+    m = NativeViT(vcfg, seed=7)
+    if head == "cls":  # a non-zero head (timm zero-inits it): otherwise every trunk gradient is exactly zero
+        with torch.no_grad():
+            m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(3)))
+        m.mark_updated()
+    m = m.to(DEV)
     eng = m.engine()
     eng.pack(m.flat, m.version)
     g = torch.Generator(device=DEV).manual_seed(4)
