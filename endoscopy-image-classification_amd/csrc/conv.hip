@@ -577,6 +577,7 @@ struct ChanFin {
   float *run_mean, *run_var;
   float eps, momentum;
   int rows, half, accumulate;
+  int64_t* nbt = nullptr;  // FIN 2: num_batches_tracked += 1 by one thread of the launch
 };
 template <int FIN>
 __global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict__ P, int G, int ncols, ChanFin f) {
@@ -601,6 +602,7 @@ __global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict
   } else if constexpr (FIN == 1) {
     f.out[c] = s / (float)f.rows;
   } else if constexpr (FIN == 2) {
+    if (c == 0 && f.nbt) *f.nbt += 1;
     const float var = s / (float)f.rows;
     f.out[c] = 1.0f / sqrtf(var + f.eps);
     if (f.run_mean) {
@@ -614,7 +616,6 @@ __global__ __launch_bounds__(256) void chan_final_kernel(const float* __restrict
     *o = f.accumulate ? *o + s : s;
   }
 }
-__global__ void nbt_inc_kernel(int64_t* nbt) { *nbt += 1; }
 
 // y = (x - mean) * rstd * gamma + beta (+ res) (relu); eval: rstd from the running variance.
 // nv = elements / VEC, CV = C / VEC (32-bit index arithmetic: the host checks nv < 2^31)
@@ -1439,8 +1440,9 @@ __global__ void bn_mean_from_sum_kernel(const float* __restrict__ sum_g, float r
 __global__ void bn_finalize_global_kernel(const float* __restrict__ sum_g, const float* __restrict__ sq_g, float rows_g,
                                           int C, float eps, float momentum, float* __restrict__ mean,
                                           float* __restrict__ rstd, float* __restrict__ run_mean,
-                                          float* __restrict__ run_var) {
+                                          float* __restrict__ run_var, int64_t* __restrict__ nbt) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;  // num_batches_tracked: one thread of the launch (no launch of its own)
   if (c >= C) return;
   const float mu = sum_g[c] / rows_g, var = sq_g[c] / rows_g;
   mean[c] = mu;
@@ -1461,8 +1463,10 @@ __global__ __launch_bounds__(256) void bn_stats_from_partials_kernel(float* __re
                                                                      float momentum, float* __restrict__ mean,
                                                                      float* __restrict__ rstd,
                                                                      float* __restrict__ run_mean,
-                                                                     float* __restrict__ run_var) {
+                                                                     float* __restrict__ run_var,
+                                                                     int64_t* __restrict__ nbt) {
   __shared__ float red[4][64];
+  if (FINAL && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;  // num_batches_tracked (FINAL: one launch)
   const int cl = threadIdx.x & 63, bl = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const bool ok = c < C;
@@ -1586,12 +1590,12 @@ int bn2d_fwd_impl(const T* x, int rows, int C, const float* gamma, const float* 
   const RowMap rm{(long)rows * C, (long)C, rows};
   const dim3 fg((C + 15) / 16);
   ChanFin fm{mean, nullptr, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, rows, 0, 0};
-  ChanFin fv{rstd, nullptr, nullptr, mean, running_mean, running_var, eps, momentum, rows, 0, 0};
+  ChanFin fv{rstd, nullptr, nullptr, mean, running_mean, running_var, eps, momentum, rows, 0, 0,
+             (int64_t*)num_batches_tracked};
   chan_partial_launch<0, T>(v4, G, x, rm, rows, C, per, nullptr, nullptr, nullptr, nullptr, 0, workspace, stream);
   hipLaunchKernelGGL(chan_final_kernel<1>, fg, 256, 0, stream, workspace, G, C, fm);
   chan_partial_launch<1, T>(v4, G, x, rm, rows, C, per, mean, nullptr, nullptr, nullptr, 0, workspace, stream);
   hipLaunchKernelGGL(chan_final_kernel<2>, fg, 256, 0, stream, workspace, G, C, fv);
-  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
   bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
@@ -1670,8 +1674,7 @@ int bn2d_fwd_global_impl(const T* x, int rows, int C, const float* gamma, const 
   const long n = (long)rows * C;
   if (n >= (1L << 31)) return ES_BAD_SHAPE;
   hipLaunchKernelGGL(bn_finalize_global_kernel, (C + 255) / 256, 256, 0, stream, sum_g, sq_g, (float)rows_g, C, eps,
-                     momentum, mean, rstd, running_mean, running_var);
-  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
+                     momentum, mean, rstd, running_mean, running_var, (int64_t*)num_batches_tracked);
   if (y) {
     const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
     bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);
@@ -1695,14 +1698,13 @@ int bn2d_fwd_partials_impl(const T* x, int rows, int C, float* partials, const f
   if (nblk > G) {
     const int ng = (nblk + G - 1) / G;
     hipLaunchKernelGGL(bn_stats_from_partials_kernel<false>, dim3((C + 63) / 64, ng), 256, 0, stream, P, nblk, 128, 1,
-                       G, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+                       G, rows, C, eps, momentum, mean, rstd, running_mean, running_var, nullptr);
     hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, ng, 128 * G, G,
-                       ng, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+                       ng, rows, C, eps, momentum, mean, rstd, running_mean, running_var, (int64_t*)num_batches_tracked);
   } else {
     hipLaunchKernelGGL(bn_stats_from_partials_kernel<true>, dim3((C + 63) / 64, 1), 256, 0, stream, P, nblk, 128, 1,
-                       nblk, rows, C, eps, momentum, mean, rstd, running_mean, running_var);
+                       nblk, rows, C, eps, momentum, mean, rstd, running_mean, running_var, (int64_t*)num_batches_tracked);
   }
-  if (num_batches_tracked) hipLaunchKernelGGL(nbt_inc_kernel, 1, 1, 0, stream, (int64_t*)num_batches_tracked);
   if (y) {
     const bool v4 = map_v4<T>(C, x, y, res, gamma, beta) && al16(mean) && al16(rstd);
     bn_apply_launch<T>(v4, x, n, C, mean, rstd, nullptr, eps, gamma, beta, res, relu, y, stream);

@@ -509,6 +509,26 @@ __global__ void convb_pack_kernel(const float* __restrict__ w, int Cout, int Cin
   }
 }
 
+// Every conv weight of a model in one launch (es_conv2d_pack_bf16_multi): workgroup row y packs entry y,
+// the same element mapping as convb_pack_kernel
+struct ConvPackEntry {
+  const float* w;
+  bf16 *wp, *wt;
+  int Cout, Cin, T, pad;
+};
+__global__ void convb_pack_multi_kernel(const ConvPackEntry* __restrict__ tab) {
+  const ConvPackEntry e = tab[blockIdx.y];
+  const long n = (long)e.Cout * e.Cin * e.T;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int tap = (int)(i % e.T);
+    const long t2 = i / e.T;
+    const int ci = (int)(t2 % e.Cin), co = (int)(t2 / e.Cin);
+    const bf16 v = (bf16)e.w[i];
+    if (e.wp) e.wp[((long)co * e.T + tap) * e.Cin + ci] = v;
+    if (e.wt) e.wt[((long)ci * e.T + tap) * e.Cout + co] = v;
+  }
+}
+
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 inline bool st4(long a, long b, long c) { return a % 4 == 0 && b % 4 == 0 && c % 4 == 0; }
 
@@ -598,6 +618,20 @@ int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void*
   long b = (n + 255) / 256;
   hipLaunchKernelGGL(convb_pack_kernel, (unsigned)(b > 4096 ? 4096 : b), 256, 0, stream, w, Cout, Cin, kh * kw, (bf16*)wp,
                      (bf16*)wt);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+int es_conv_pack_entry_size() { return (int)sizeof(ConvPackEntry); }
+
+// es_conv2d_pack_bf16 over n weights in one launch: table = n device-resident entries of
+// es_conv_pack_entry_size() bytes {const float* w; bf16* wp; bf16* wt; int Cout, Cin, kh * kw, 0};
+// max_elems = the largest Cout * Cin * kh * kw among them (sizes the grid)
+int es_conv2d_pack_bf16_multi(const void* table, int n, long max_elems, hipStream_t stream) {
+  if (!table) return ES_BAD_ARG;
+  if (n <= 0 || n > 65535 || max_elems <= 0) return ES_BAD_SHAPE;
+  const long b = (max_elems + 255) / 256;
+  hipLaunchKernelGGL(convb_pack_multi_kernel, dim3((unsigned)(b > 1024 ? 1024 : b), n), 256, 0, stream,
+                     (const ConvPackEntry*)table);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -198,6 +198,11 @@ def _queue_join(main, side):
 # fusion block joins them (code/models/conformer.py:334-357 data flow, unchanged arithmetic).
 BRANCH_STREAMS = True
 _branch_streams = {}
+# every conv weight's bf16 images packed in ONE launch per parameter version (NativeConformer.conv_pack) instead
+# of one launch per weight at its first use: 96 launches fewer per S1 step; same box, interleaved (r05,
+# scripts/gpu_r5k.sh): S1 139.16 / 139.89 / 139.30 vs 139.43 / 139.52 / 139.12 ms, P0 within its noise -- kept for
+# the launch count (the small-batch P0 / shard steps are launch-bound), not for a measured gain
+CONV_PACK_MULTI = True
 # HIP priorities of the branch stream and the weight-gradient stream (0 = the default stream's, -1 = higher).
 # S1 same box (scripts/gpu_prio.sh, profiles/r04_stream_priority.txt): both 0 139.81 / 140.01 ms, branch -1
 # 139.53 / 139.00, weight gradients -1 140.26 / 139.92, both -1 139.21 / 139.20
@@ -1067,16 +1072,54 @@ class NativeConformer(nn.Module):
 
     def conv_pack(self, name, Cout, Cin, k):
         """bf16 images of conv weight `name` -- wp [Cout][k k][Cin] and wt [Cin][k k][Cout] -- packed
-        once per parameter version (es_conv2d_pack_bf16)."""
+        once per parameter version.  The first step packs each weight at its first use (es_conv2d_pack_bf16)
+        and records the model's conv weights; every later version packs them all in one launch
+        (es_conv2d_pack_bf16_multi) at the first conv_pack of the version -- the stem, on the caller's
+        stream: a conv on another stream waits for that launch's event."""
         ent = self._cpack.get(name)
         if ent is None:
             n = Cout * Cin * k * k
             ent = self._cpack[name] = [-1, torch.empty(n, dtype=torch.bfloat16, device=self.flat.device),
-                                       torch.empty(n, dtype=torch.bfloat16, device=self.flat.device)]
+                                       torch.empty(n, dtype=torch.bfloat16, device=self.flat.device), (Cout, Cin, k)]
+            self._cpack_tab = None
         if ent[0] != self.version:
-            call("es_conv2d_pack_bf16", ptr(self.pview(name)), Cout, Cin, k, k, ptr(ent[1]), ptr(ent[2]), _s())
-            ent[0] = self.version
+            if self._cpack_next and CONV_PACK_MULTI:
+                self._cpack_table()  # a new version: the previous one's forward has used every conv
+            if self._cpack_tab is not None and self.flat.is_cuda and CONV_PACK_MULTI:
+                tab, nent, mx = self._cpack_tab
+                call("es_conv2d_pack_bf16_multi", ptr(tab), nent, mx, _s())
+                for e in self._cpack.values():
+                    e[0] = self.version
+                st = torch.cuda.current_stream(self.flat.device)
+                self._cpack_ev = (st, torch.cuda.Event(), {st})
+                self._cpack_ev[1].record(st)
+            else:
+                call("es_conv2d_pack_bf16", ptr(self.pview(name)), Cout, Cin, k, k, ptr(ent[1]), ptr(ent[2]), _s())
+                ent[0] = self.version
+                self._cpack_next = True  # build the table once this version's weights are all seen
+        elif self._cpack_ev is not None:
+            st = torch.cuda.current_stream(self.flat.device)
+            if st not in self._cpack_ev[2]:  # once per stream and version
+                st.wait_event(self._cpack_ev[1])
+                self._cpack_ev[2].add(st)
         return ent[1], ent[2]
+
+    def _cpack_table(self):
+        """The device table of every conv weight seen so far (es_conv2d_pack_bf16_multi)."""
+        self._cpack_next = False
+        if not self.flat.is_cuda or not self._cpack:
+            return
+        esz = _lib.load().es_conv_pack_entry_size()
+        ents = list(self._cpack.items())
+        raw = bytearray(esz * len(ents))
+        mx = 0
+        for j, (name, (_, wp, wt, (Cout, Cin, k))) in enumerate(ents):
+            entry = (ctypes.c_void_p(ptr(self.pview(name))), ctypes.c_void_p(ptr(wp)), ctypes.c_void_p(ptr(wt)),
+                     ctypes.c_int(Cout), ctypes.c_int(Cin), ctypes.c_int(k * k), ctypes.c_int(0))
+            buf = b"".join(bytes(e) for e in entry)
+            raw[j * esz:j * esz + len(buf)] = buf
+            mx = max(mx, Cout * Cin * k * k)
+        self._cpack_tab = (torch.frombuffer(raw, dtype=torch.uint8).to(self.flat.device), len(ents), mx)
 
     def bwd_scratch(self, name, shape, dtype):
         """Zero-initialised scratch for the transformer blocks' backward, allocated once per shape."""
@@ -1119,6 +1162,7 @@ class NativeConformer(nn.Module):
         self._packed_version = -1
         self._wtab = None
         self._cpack = {}
+        self._cpack_tab, self._cpack_ev, self._cpack_next = None, None, False
         self._bn_partials = {}
         self._anchor = torch.zeros((), device=device, requires_grad=True)
 

@@ -315,6 +315,12 @@ int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw);
    each split writes an fp32 slab of the gradient that a reduce kernel sums); returns the previous value */
 int es_set_conv_dw_target(int v);
 int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);
+/* es_conv2d_pack_bf16 for n weights in ONE launch (a model's conv weights after each optimizer step):
+ * table = n device-resident entries of es_conv_pack_entry_size() bytes
+ * {const float* w; void* wp; void* wt; int Cout; int Cin; int kh_x_kw; int pad}, max_elems = the largest
+ * Cout * Cin * kh * kw (sizes the grid).  Same images, bit for bit. */
+int es_conv_pack_entry_size(void);
+int es_conv2d_pack_bf16_multi(const void* table, int n, long max_elems, hipStream_t stream);
 int es_conv2d_fwd_bf16(const float* x, int N, int H, int W, int Cin, long sxn, long sxh, long sxw, long sxc,
                        const void* wp, const float* bias, int Cout, int kh, int kw, int stride, int pad, float* y,
                        long syn, long syh, long syw, int accumulate, hipStream_t stream);

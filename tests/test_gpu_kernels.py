@@ -792,3 +792,55 @@ def test_pack_weights_exact():
         assert torch.equal(wb, W.bfloat16()), name
         if name in eng.wt:
             assert torch.equal(eng.wt[name], W.t().contiguous().bfloat16()), name
+
+
+def test_conv_pack_multi_matches_single_pack():
+    """es_conv2d_pack_bf16_multi (every conv weight of a model in one launch) writes the same images as
+    es_conv2d_pack_bf16 per weight: wp [Cout][k k][Cin], wt [Cin][k k][Cout], bit for bit."""
+    import ctypes
+    from endossl import _lib
+    shapes = [(64, 32, 3), (256, 64, 1), (32, 96, 7), (768, 256, 1), (128, 128, 3)]
+    g = torch.Generator().manual_seed(5)
+    ws = [torch.randn(co, ci, k, k, generator=g).to(DEV) for co, ci, k in shapes]
+    outs = [(torch.empty(w.numel(), dtype=torch.bfloat16, device=DEV),
+             torch.empty(w.numel(), dtype=torch.bfloat16, device=DEV)) for w in ws]
+    esz = _lib.load().es_conv_pack_entry_size()
+    raw = bytearray(esz * len(ws))
+    for j, ((co, ci, k), w, (wp, wt)) in enumerate(zip(shapes, ws, outs)):
+        ent = (ctypes.c_void_p(ptr(w)), ctypes.c_void_p(ptr(wp)), ctypes.c_void_p(ptr(wt)), ctypes.c_int(co),
+               ctypes.c_int(ci), ctypes.c_int(k * k), ctypes.c_int(0))
+        buf = b"".join(bytes(e) for e in ent)
+        raw[j * esz:j * esz + len(buf)] = buf
+    tab = torch.frombuffer(raw, dtype=torch.uint8).to(DEV)
+    call("es_conv2d_pack_bf16_multi", ptr(tab), len(ws), max(w.numel() for w in ws), S())
+    for (co, ci, k), w, (wp, wt) in zip(shapes, ws, outs):
+        rp = torch.empty_like(wp)
+        rt = torch.empty_like(wt)
+        call("es_conv2d_pack_bf16", ptr(w), co, ci, k, k, ptr(rp), ptr(rt), S())
+        torch.cuda.synchronize()
+        assert torch.equal(wp, rp) and torch.equal(wt, rt), (co, ci, k)
+        assert torch.equal(wp.view(co, k * k, ci), w.permute(0, 2, 3, 1).reshape(co, k * k, ci).bfloat16())
+        assert torch.equal(wt.view(ci, k * k, co), w.permute(1, 2, 3, 0).reshape(ci, k * k, co).bfloat16())
+
+
+def test_conformer_conv_pack_multi_after_first_version():
+    """NativeConformer.conv_pack: the first parameter version packs per weight and records the table; the
+    next version packs every recorded weight in one launch; the images equal a fresh per-weight pack."""
+    from endossl.conformer import ConformerConfig, NativeConformer
+    m = NativeConformer(ConformerConfig(img_size=64, base_channel=32, embed_dim=128, depth=3, heads=2), seed=1).to(DEV)
+    x = torch.randn(2, 3, 64, 64, device=DEV)
+    m.train()
+    m(x)
+    assert m._cpack and m._cpack_tab is None and m._cpack_next
+    with torch.no_grad():
+        m.flat.add_(0.01 * torch.randn_like(m.flat))
+    m.mark_updated()
+    m(x)
+    torch.cuda.synchronize()
+    assert m._cpack_tab is not None and m._cpack_tab[1] == len(m._cpack)
+    for name, (ver, wp, wt, (co, ci, k)) in m._cpack.items():
+        assert ver == m.version, name
+        rp, rt = torch.empty_like(wp), torch.empty_like(wt)
+        call("es_conv2d_pack_bf16", ptr(m.pview(name)), co, ci, k, k, ptr(rp), ptr(rt), S())
+        torch.cuda.synchronize()
+        assert torch.equal(wp, rp) and torch.equal(wt, rt), name
