@@ -25,6 +25,8 @@
 // row-major [token][64] LDS images.  LDS row = 128 B; chunk c of row r is stored at
 // c ^ (((r >> 1) & 3) << 1), which is conflict-free for both the row reads (ds_read_b128) and the
 // transposed reads used here.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -229,7 +231,10 @@ __global__ __launch_bounds__(NW * 64, OCC) void attn_fwd_kernel(AttnArgs a) {
 // kernel: scores in log2 units, bf16(P) into P.V, fp32 accumulation; P is exp2(s - running max).
 constexpr int FCH = 8;
 
-template <int NT>
+// MASK: the chunk holds key rows >= T (only the last chunk(s) of the head).  Unmasked chunks are straight-line
+// code, so the compiler issues all of the chunk's K fragment reads ahead of its MFMAs; a per-tile branch on the
+// padding (round 4) split the chunk into blocks and exposed each tile's LDS and MFMA latency.
+template <int NT, bool MASK>
 __device__ __forceinline__ void fwd_long_chunk(const char* Ks, const char* Vs, int t0, int T, float sl, int g, int r,
                                                const bf16x8& qf0, const bf16x8& qf1, float& m, float& l, f32x4* o) {
   f32x4 s[NT];
@@ -241,14 +246,14 @@ __device__ __forceinline__ void fwd_long_chunk(const char* Ks, const char* Vs, i
     acc = mfma16(lds_row8(Ks, kt * 16 + r, g), qf0, acc);
     acc = mfma16(lds_row8(Ks, kt * 16 + r, 4 + g), qf1, acc);
     acc *= sl;
-    if (kt * 16 + 16 > T) {
+    if constexpr (MASK) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (kt * 16 + 4 * g + i >= T) acc[i] = -INFINITY;
+      for (int i = 0; i < 4; ++i) acc[i] = kt * 16 + 4 * g + i >= T ? -INFINITY : acc[i];
     }
-    cm = fmaxf(cm, fmaxf(fmaxf(acc[0], acc[1]), fmaxf(acc[2], acc[3])));
     s[t] = acc;
   }
+#pragma unroll
+  for (int t = 0; t < NT; ++t) cm = fmaxf(cm, fmaxf(fmaxf(s[t][0], s[t][1]), fmaxf(s[t][2], s[t][3])));
   cm = fmaxf(cm, __shfl_xor(cm, 16, 64));
   cm = fmaxf(cm, __shfl_xor(cm, 32, 64));
   const float mn = fmaxf(m, cm);
@@ -327,8 +332,12 @@ __global__ __launch_bounds__(512) void attn_fwd_long_kernel(AttnArgs a) {
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
-    for (int c = 0; c < NT16 / FCH; ++c) fwd_long_chunk<FCH>(Ks, Vs, c * FCH, T, sl, g, r, qf0, qf1, m, l, o);
-    if constexpr (NT16 % FCH) fwd_long_chunk<NT16 % FCH>(Ks, Vs, NT16 - NT16 % FCH, T, sl, g, r, qf0, qf1, m, l, o);
+    for (int c = 0; c < NT16 / FCH; ++c) {
+      if ((c + 1) * FCH * 16 <= T) fwd_long_chunk<FCH, false>(Ks, Vs, c * FCH, T, sl, g, r, qf0, qf1, m, l, o);
+      else fwd_long_chunk<FCH, true>(Ks, Vs, c * FCH, T, sl, g, r, qf0, qf1, m, l, o);
+    }
+    if constexpr (NT16 % FCH)
+      fwd_long_chunk<NT16 % FCH, true>(Ks, Vs, NT16 - NT16 % FCH, T, sl, g, r, qf0, qf1, m, l, o);
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     // whole-row stores through the wave's 1-KiB slot past K and V (two halves: the LDS is full)
@@ -1055,8 +1064,10 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
     o.lq = o.qv ? x.lse * 1.44269504088896341f : 0.f;            // log2 units
     return o;
   };
-  // dS^T tile t (keys 16t + 4g + i on this lane's query) from the key tile's K / V rows
-  auto ds_tile = [&](const QOps& Q, int t, bf16x8 k0, bf16x8 k1, bf16x8 v0, bf16x8 v1) {
+  // dS^T tile t (keys 16t + 4g + i on this lane's query) from the key tile's K / V rows.  maskc: whether the
+  // tile may hold key rows >= T (std::true_type only for the head's last tile / pair: the other pairs are
+  // straight-line code, so their LDS reads and MFMAs interleave -- a per-tile branch split them into blocks)
+  auto ds_tile = [&](auto maskc, const QOps& Q, int t, bf16x8 k0, bf16x8 k1, bf16x8 v0, bf16x8 v1) {
     f32x4 sv = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
     sv = mfma16(k0, Q.qf0, sv);
     sv = mfma16(k1, Q.qf1, sv);
@@ -1065,10 +1076,9 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
     f32x4 pv;
 #pragma unroll
     for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sv[i] * sl - Q.lq);
-    if (t * 16 + 16 > T) {
+    if constexpr (decltype(maskc)::value) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (t * 16 + 4 * g + i >= T) pv[i] = 0.f;
+      for (int i = 0; i < 4; ++i) pv[i] = t * 16 + 4 * g + i >= T ? 0.f : pv[i];
     }
     f32x4 ds;
 #pragma unroll
@@ -1092,8 +1102,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
     f32x4 dqA[4], dqB[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dqA[dt] = dqB[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int sc = 0; sc < NP; ++sc) {
+    auto pair = [&](auto maskc, int sc) {
       const int ta = 2 * sc * 16 + r, tb = ta + 16;
       const bf16x8 ka0 = lds_row8(Ks, ta, g), ka1 = lds_row8(Ks, ta, 4 + g);
       const bf16x8 va0 = lds_row8(Vs, ta, g), va1 = lds_row8(Vs, ta, 4 + g);
@@ -1103,7 +1112,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) tk[dt] = lds_trT(Ks, sc * 32, dt * 16, g, r);
       {
-        const f32x4 d0 = ds_tile(QA, 2 * sc, ka0, ka1, va0, va1), d1 = ds_tile(QA, 2 * sc + 1, kb0, kb1, vb0, vb1);
+        const f32x4 d0 = ds_tile(maskc, QA, 2 * sc, ka0, ka1, va0, va1);
+        const f32x4 d1 = ds_tile(maskc, QA, 2 * sc + 1, kb0, kb1, vb0, vb1);
         bf16x8 dsf;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1114,7 +1124,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
         for (int dt = 0; dt < 4; ++dt) dqA[dt] = mfma16(tk[dt], dsf, dqA[dt]);
       }
       {
-        const f32x4 d0 = ds_tile(QB, 2 * sc, ka0, ka1, va0, va1), d1 = ds_tile(QB, 2 * sc + 1, kb0, kb1, vb0, vb1);
+        const f32x4 d0 = ds_tile(maskc, QB, 2 * sc, ka0, ka1, va0, va1);
+        const f32x4 d1 = ds_tile(maskc, QB, 2 * sc + 1, kb0, kb1, vb0, vb1);
         bf16x8 dsf;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -1124,6 +1135,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) dqB[dt] = mfma16(tk[dt], dsf, dqB[dt]);
       }
+    };
+#pragma unroll 1
+    for (int sc = 0; sc < NP; ++sc) {
+      if ((2 * sc + 2) * 16 <= T) pair(std::false_type{}, sc);
+      else pair(std::true_type{}, sc);
     }
     if constexpr (NT16 & 1) {
       const int t = NT16 - 1;
@@ -1132,11 +1148,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_bwd_dq2_kernel(AttnArgs 
       bf16x4 tk4[4];
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) tk4[dt] = lds_trT4(Ks, t * 16, dt * 16, g, r);
-      f32x4 d0 = ds_tile(QA, t, k0, k1, v0, v1);
+      f32x4 d0 = ds_tile(std::true_type{}, QA, t, k0, k1, v0, v1);
       bf16x4 dsf = {(bf16)d0[0], (bf16)d0[1], (bf16)d0[2], (bf16)d0[3]};
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dqA[dt] = mfma16k16(tk4[dt], dsf, dqA[dt]);
-      d0 = ds_tile(QB, t, k0, k1, v0, v1);
+      d0 = ds_tile(std::true_type{}, QB, t, k0, k1, v0, v1);
       dsf = bf16x4{(bf16)d0[0], (bf16)d0[1], (bf16)d0[2], (bf16)d0[3]};
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) dqB[dt] = mfma16k16(tk4[dt], dsf, dqB[dt]);

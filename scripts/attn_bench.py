@@ -1,7 +1,9 @@
 """Attention microbenchmark at the F1 train shape (512 images x 6 heads x 197 tokens; --s1: 120 x 12 x 577), forward
 occupancy variants A/B'd in one process (interleaved rounds, median); backward (dQ + dK/dV).
 
-  python scripts/attn_bench.py [--rounds 5] [--iters 10]
+  python scripts/attn_bench.py [--rounds 5] [--iters 10] [--save out.pt | --compare out.pt]
+(--save / --compare: the outputs of one build against another's, bit for bit -- run the first under
+ENDOSSL_LIB=<other build>)
 """
 import argparse
 import json
@@ -35,6 +37,8 @@ def main():
                     "(Conformer-B at 384^2, the long-sequence kernels)")
     ap.add_argument("--bwd", default="0,1,2,3,4", help="backward variants to time (es_set_attn_bwd_variant)")
     ap.add_argument("--no-fwd", action="store_true", help="skip the forward occupancy variants")
+    ap.add_argument("--save", default=None, help="torch.save the outputs (forward o / lse, backward dqkv)")
+    ap.add_argument("--compare", default=None, help="compare the outputs bit for bit with a --save file")
     args = ap.parse_args()
     bwd_vs = [int(v) for v in args.bwd.split(",")]
     lib = _lib.load()
@@ -75,6 +79,18 @@ def main():
     if "bwd_plain" in outs:
         print("bwd == plain (bit-exact):", {k: torch.equal(v, outs["bwd_plain"]) for k, v in outs.items()
                                             if k.startswith("bwd_")}, flush=True)
+    if args.save:
+        torch.save({k: (tuple(x.cpu() for x in v) if isinstance(v, tuple) else v.cpu()) for k, v in outs.items()},
+                   args.save)
+    if args.compare:
+        ref = torch.load(args.compare, weights_only=True)
+        same = {}
+        for k, v in outs.items():
+            if k in ref:
+                a = v if isinstance(v, tuple) else (v,)
+                b = ref[k] if isinstance(ref[k], tuple) else (ref[k],)
+                same[k] = all(torch.equal(x.cpu(), y) for x, y in zip(a, b))
+        print("bit-identical to", args.compare, same, flush=True)
     flops_f = 4.0 * n * H * T * T * 64
     out = {}
     for k, v in res.items():
