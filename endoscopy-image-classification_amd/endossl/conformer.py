@@ -294,6 +294,13 @@ TOKEN_SINK = True
 # add, and bn2 -> conv3 where x2 has no other consumer) is applied by that conv's gathers instead of being
 # written as a map (_BNConvFn); False materialises it (bn, then conv)
 BN_CONV_FUSED = True
+# ... for k x k convs too (bn1 -> conv2, 3 x 3): off.  Each input pixel is gathered k^2 times and the BatchNorm
+# parameters cost the gather kernels a wave per SIMD: at the Conformer-B/384 shapes (scripts/convb_bench.py --bnin)
+# the 3 x 3 forward takes 342 / 210 / 219 us fused vs 246 / 167 / 171 plain (stages 1-3) and its weight gradient
+# 632 / 515 / 570 vs 522 / 302 / 363, more than the BatchNorm apply it saves; the 1 x 1 convs lose 4-18 % (fwd) and
+# 4-27 % (weight gradient).  S1, same box, interleaved (scripts/gpu_r5o.sh): every pair fused 138.56 / 138.86 /
+# 138.76 ms, 1 x 1 only 138.46 / 138.12 / 137.80, none 138.33 / 138.27 / 138.69
+BN_CONV_FUSED_KXK = False
 # bf16 activation / gradient maps in the CNN branch when every conv after the stem runs on conv_bf16.hip
 # (NativeConformer.map_bf16); ENDOSSL_MAP_BF16=0 keeps fp32 maps with bf16 conv operands
 MAP_BF16 = os.environ.get("ENDOSSL_MAP_BF16", "1") != "0"
@@ -654,7 +661,8 @@ def bn_conv(m, x, pre, wname, bname, Cout, k, s=1, p=0, stats=False, out_dtype=N
     out_dtype = out_dtype or _map_dtype(m)
     world = dist.world_size() if getattr(m, "sync_bn", True) else 1
     part = m._bn_partials.get(x.data_ptr())
-    if (BN_CONV_FUSED and BN_Y_FREE and m.training and world == 1 and CAPTURE is None and part is not None
+    if (BN_CONV_FUSED and (k == 1 or BN_CONV_FUSED_KXK) and BN_Y_FREE and m.training and world == 1
+            and CAPTURE is None and part is not None
             and part[1] == x.shape and x.is_contiguous() and _conv_bf16(m, _Map.nhwc(x), Cout, k)):
         return _BNConvFn.apply(x, m, pre, eps, wname, bname, Cout, k, s, p, stats, out_dtype)
     h = bn(m, x, pre, eps=eps, relu=True)

@@ -2,7 +2,10 @@
 (SemiFormer S1: B=8, mu=7 -> 120 images).  Per shape and pass: HIP-event time of one launch
 (+ its reduce for dW), algorithmic TFLOP/s (2 Cout Cin k^2 per output pixel) and GB/s of the
 algorithmic bytes (fp32 maps read / written once, bf16 weights).
-  python scripts/convb_bench.py [--n 120] [--iters 5]"""
+  python scripts/convb_bench.py [--n 120] [--iters 5]
+  --bnin: bf16 maps, the shapes whose input is a BatchNorm + ReLU output (conv2 / conv3 of the ConvBlocks), each
+  forward (with the next BatchNorm's statistics) and weight gradient timed plain and with the BatchNorm applied
+  by the gather (es_conv2d_*_bf16_bnin_ex), interleaved"""
 import argparse
 import json
 import os
@@ -28,7 +31,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=120)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--bnin", action="store_true")
     a = ap.parse_args()
+    if a.bnin:
+        return bnin_main(a)
     lib = _lib.load()
     s = _lib.stream()
     dev = "cuda"
@@ -83,6 +89,63 @@ def main():
         torch.cuda.empty_cache()
     tot = {p: sum(r[p]["us"] for r in out) for p in ("fwd", "dgrad", "wgrad")}
     print(json.dumps({"total_us": tot}))
+
+
+def bnin_main(a):
+    lib = _lib.load()
+    s = _lib.stream()
+    dev = "cuda"
+    res = {}
+    for name, H, Cin, Cout, k, st, p in SHAPES:
+        if "conv2" not in name and "conv3" not in name:
+            continue
+        N = a.n
+        Ho = (H + 2 * p - k) // st + 1
+        M = N * Ho * Ho
+        x = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+        w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
+        y = torch.empty(N, Ho, Ho, Cout, device=dev, dtype=torch.bfloat16)
+        dy = torch.randn_like(y)
+        mean, rstd = torch.randn(Cin, device=dev) * 0.1, torch.rand(Cin, device=dev) + 0.5
+        gam, bet = torch.rand(Cin, device=dev) + 0.5, torch.randn(Cin, device=dev) * 0.1
+        n = Cout * Cin * k * k
+        wp = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        wt = torch.empty(n, dtype=torch.bfloat16, device=dev)
+        dw = torch.empty_like(w)
+        ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, Cin, k, k, 0), device=dev)
+        part = torch.empty(lib.es_conv2d_bnstats_size(M, Cout), device=dev)
+        call("es_conv2d_pack_bf16", ptr(w), Cout, Cin, k, k, ptr(wp), ptr(wt), s)
+        xs = (H * H * Cin, H * Cin, Cin, 1)
+        ys = (Ho * Ho * Cout, Ho * Cout, Cout)
+        bn = (ptr(mean), ptr(rstd), ptr(gam), ptr(bet))
+        fns = {
+            "fwd": lambda: call("es_conv2d_fwd_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k, st, p,
+                                ptr(y), *ys, 0, ptr(part), 3, s),
+            "fwd_bnin": lambda: call("es_conv2d_fwd_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k,
+                                     st, p, ptr(y), *ys, 0, ptr(part), 3, *bn, s),
+            "wgrad": lambda: call("es_conv2d_bwd_weight_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys, Cout, k, k,
+                                  st, p, 0, ptr(ws), ptr(dw), 0, 3, s),
+            "wgrad_bnin": lambda: call("es_conv2d_bwd_weight_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys,
+                                       Cout, k, k, st, p, 0, ptr(ws), ptr(dw), 0, 3, *bn, s),
+        }
+        ts = {kk: [] for kk in fns}
+        for kk, fn in fns.items():
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(a.iters):
+            for kk, fn in fns.items():
+                e0.record(torch.cuda.current_stream())
+                fn()
+                e1.record(torch.cuda.current_stream())
+                e1.synchronize()
+                ts[kk].append(e0.elapsed_time(e1) * 1e3)
+        res[name] = {kk: round(sorted(v)[len(v) // 2], 1) for kk, v in ts.items()}
+        print(name, json.dumps(res[name]), flush=True)
+        del x, y, dy, ws
+        torch.cuda.empty_cache()
+    tot = {kk: round(sum(r[kk] for r in res.values()), 1) for kk in ("fwd", "fwd_bnin", "wgrad", "wgrad_bnin")}
+    print(json.dumps({"total_us": tot}), flush=True)
 
 
 if __name__ == "__main__":

@@ -747,12 +747,13 @@ def test_bn_relu_fused_into_conv_gather_bit_identical():
     from endossl import conformer as cf
     from endossl.conformer import ConformerConfig, NativeConformer
     kw = dict(img_size=64, patch=16, base_channel=64, channel_ratio=4, embed_dim=128, depth=3, heads=2, num_classes=23)
-    saved = cf.BN_CONV_FUSED
+    saved = cf.BN_CONV_FUSED, cf.BN_CONV_FUSED_KXK
     res = {}
     calls = {}
     try:
         for fused in (False, True):
             cf.BN_CONV_FUSED = fused
+            cf.BN_CONV_FUSED_KXK = True  # the 3 x 3 pairs too (off by default: measured slower)
             m = NativeConformer(ConformerConfig(**kw), seed=11).to(DEV)
             assert m.conv_bf16 and m.map_bf16
             m.train()
@@ -779,7 +780,7 @@ def test_bn_relu_fused_into_conv_gather_bit_identical():
                 cf._BNConvFn.apply = orig
             res[fused], calls[fused] = outs, n_fused[0]
     finally:
-        cf.BN_CONV_FUSED = saved
+        cf.BN_CONV_FUSED, cf.BN_CONV_FUSED_KXK = saved
     # conv_1's bn1 / bn2, each stage's cnn_block bn1 and fusion_block bn2 (fusion bn1 feeds the FCUUp add)
     nst = len(list(ConformerConfig(**kw).stages()))
     assert calls[False] == 0 and calls[True] == 2 * (2 + 2 * nst), calls
