@@ -1087,6 +1087,53 @@ int reduce_partials_pair(const float* P0, float* out0, const float* P1, float* o
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+// many LayerNorm backwards' dgamma / dbeta reductions in one launch (es_ln_param_grads_multi): entry e owns
+// blocks [blk0_e, blk0_e + 2 nb), the first nb reducing P_e -> out0_e, the next nb P_e + G N -> out1_e, every
+// column as reduce_partials_kernel<CW> (bit-identical to the per-LayerNorm reduce_partials_pair launches)
+struct RedPairEntry {
+  const float* P;
+  float *out0, *out1;
+  int G, N, accumulate, blk0;
+};
+constexpr int RPM_MAX = 32;
+struct RedPairTable {
+  RedPairEntry e[RPM_MAX];
+  int n, pad;
+};
+template <int CW>
+__global__ __launch_bounds__(256) void reduce_partials_multi_kernel(const RedPairTable t) {
+  int e = 0;
+  while (e + 1 < t.n && t.e[e + 1].blk0 <= (int)blockIdx.x) ++e;
+  const RedPairEntry& r = t.e[e];
+  const int nb = (r.N + CW - 1) / CW, b = blockIdx.x - r.blk0;
+  const bool second = b >= nb;
+  reduce_partials_body<CW>(second ? r.P + (size_t)r.G * r.N : r.P, second ? r.out1 : r.out0, r.G, r.N, r.accumulate,
+                           b - (second ? nb : 0));
+}
+
+// entries {P (= pg [G][N] then pb [G][N]), out0, out1, G, N, accumulate}: one launch; every entry must take the
+// same column width as reduce_partials_pair would (N <= 2048 && G >= 64 -> 4 columns, else 16)
+int reduce_partials_multi(const RedPairEntry* ents, int n, hipStream_t stream) {
+  if (!ents || n <= 0) return ES_BAD_ARG;
+  if (n > RPM_MAX) return ES_BAD_SHAPE;
+  RedPairTable t{};
+  const bool narrow = ents[0].N <= 2048 && ents[0].G >= 64;
+  const int CW = narrow ? 4 : 16;
+  int blk = 0;
+  for (int i = 0; i < n; ++i) {
+    const RedPairEntry& r = ents[i];
+    if (!r.P || !r.out0 || !r.out1) return ES_BAD_ARG;
+    if (r.G <= 0 || r.N <= 0 || ((r.N <= 2048 && r.G >= 64) != narrow)) return ES_BAD_SHAPE;
+    t.e[i] = r;
+    t.e[i].blk0 = blk;
+    blk += 2 * ((r.N + CW - 1) / CW);
+  }
+  t.n = n;
+  if (narrow) hipLaunchKernelGGL(reduce_partials_multi_kernel<4>, blk, 256, 0, stream, t);
+  else hipLaunchKernelGGL(reduce_partials_multi_kernel<16>, blk, 256, 0, stream, t);
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
 // template commas out of the launch macro; a kernel referenced only through a function pointer
 // gets no host stub).

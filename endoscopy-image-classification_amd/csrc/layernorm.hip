@@ -256,6 +256,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const DY* __restrict__ dy, 
 namespace es_gemm {  // gemm.hip: dgamma and dbeta reductions in one launch (the LayerNorm backward's two tails)
 int reduce_partials_pair(const float* P0, float* out0, const float* P1, float* out1, int G, int N, int accumulate,
                          hipStream_t stream);
+struct RedPairEntry {
+  const float* P;
+  float *out0, *out1;
+  int G, N, accumulate, blk0;
+};
+int reduce_partials_multi(const RedPairEntry* ents, int n, hipStream_t stream);
 }
 
 #define LN_DISPATCH(KER, V_, GRID, STREAM, ...)                                \
@@ -283,13 +289,17 @@ static int ln_bwd_launch(const DY* dy, int lddy, const float* x, int ldx, const 
                          float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
                          hipStream_t stream) {
   if (M <= 0 || D % 128 || blocks <= 0) return ES_BAD_SHAPE;
-  if (!dy || !x || !mean || !rstd || !gamma || !dx || !dgamma || !dbeta || !workspace) return ES_BAD_ARG;
+  // dgamma == dbeta == NULL: the per-block partials stay in the workspace (pg [grid][D], then pb) for a later
+  // es_ln_param_grads_multi launch
+  const bool defer = !dgamma && !dbeta;
+  if (!dy || !x || !mean || !rstd || !gamma || !dx || (!defer && (!dgamma || !dbeta)) || !workspace) return ES_BAD_ARG;
   const int grid = blocks < (M + 7) / 8 ? blocks : (M + 7) / 8;
   float* pg = workspace;
   float* pb = workspace + (size_t)grid * D;
   LN_BWD_DISPATCH(DY, D / 128, grid, stream, dy, lddy, x, ldx, mean, rstd, gamma, dres, ldres, dx, lddx, (bf16*)dxb,
                   lddxb, pg, pb, M);
   if (hipGetLastError() != hipSuccess) return ES_HIP_ERROR;
+  if (defer) return ES_OK;
   return es_gemm::reduce_partials_pair(pg, dgamma, pb, dbeta, grid, D, accumulate, stream);
 }
 
@@ -334,6 +344,18 @@ int es_layernorm_bwd(const float* dy, int lddy, const float* x, int ldx, const f
 }
 
 // es_layernorm_bwd with dy in bf16 (the dgrad GEMM's output image)
+// the partial-row count a backward over M rows on `blocks` workgroups leaves in its workspace
+int es_layernorm_bwd_grid(int blocks, int M) { return blocks <= 0 || M <= 0 ? 0 : (blocks < (M + 7) / 8 ? blocks : (M + 7) / 8); }
+
+// dgamma / dbeta of n deferred LayerNorm backwards in one launch: table = n host entries of
+// es_ln_param_grads_entry_size() bytes {const float* workspace; float* dgamma; float* dbeta; int grid; int D;
+// int accumulate; int pad} (grid = es_layernorm_bwd_grid of that backward); same sums, bit for bit, as the
+// backwards' own reductions
+int es_ln_param_grads_entry_size() { return (int)sizeof(es_gemm::RedPairEntry); }
+int es_ln_param_grads_multi(const void* table, int n, hipStream_t stream) {
+  return es_gemm::reduce_partials_multi((const es_gemm::RedPairEntry*)table, n, stream);
+}
+
 int es_layernorm_bwd_b16(const void* dy, int lddy, const float* x, int ldx, const float* mean, const float* rstd,
                          const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
                          float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,

@@ -52,6 +52,9 @@ SIGNATURES = {
     "es_layernorm_fwd": (I, [V, I, V, V, V, I, V, V, I, I, F, V]),
     "es_layernorm_bwd": (I, [V, I, V, I, V, V, V, V, I, V, I, V, I, V, V, V, I, I, I, I, V]),
     "es_layernorm_bwd_b16": (I, [V, I, V, I, V, V, V, V, I, V, I, V, I, V, V, V, I, I, I, I, V]),
+    "es_layernorm_bwd_grid": (I, [I, I]),
+    "es_ln_param_grads_entry_size": (I, []),
+    "es_ln_param_grads_multi": (I, [V, I, V]),
     "es_gelu_fwd": (I, [V, V, L, V]),
     "es_gelu_bwd": (I, [V, V, V, L, V]),
     "es_patch_im2col": (I, [V, V, I, I, I, V]),

@@ -257,6 +257,10 @@ class Engine:
     # split chain measured slower: 5.35 / 5.35 / 5.44 vs 5.30 / 5.29 / 5.29 ms (r05, one box, interleaved; the
     # half-batch kernels lose more than the concurrency gains).  Off; bit-identical when on (test_gpu_step.py).
     SHARD_LANES = False
+    # the LayerNorm backwards' parameter-gradient reductions off the data-gradient chain: each backward leaves its
+    # per-workgroup partials in a workspace of its own and one es_ln_param_grads_multi launch per weight-gradient
+    # launch reduces them on the side stream (24 launches fewer on the chain per step; bit-identical)
+    DEFER_LN_GRADS = True
     # A block's long-axis weight gradients (fc2, fc1, proj, qkv: 24 tiles of 384 x 192 at ViT-S) as ONE
     # split-K launch on the side stream once the block's data-gradient chain has produced its last dY
     # (es_gemm_tn_big_grouped) plus one reduce launch, sized to LAYER_TN_SHARE of the CUs (4 splits):
@@ -306,6 +310,8 @@ class Engine:
         self._grads = {}
         self._ws = None
         self._ws_ln = None
+        self._ws_lnp = None
+        self._lnp_next = 0
         self._side = None
         self._ncu = None
         self._lane_state = {}
@@ -585,12 +591,46 @@ class Engine:
         else:
             self._call(fn, *args)
 
-    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None, accumulate=0):
+    def _ln_bwd(self, dy, x, mean, rstd, gamma, dres, dx, dxb, dgamma, dbeta, M, lane=0, lddx=None, accumulate=0,
+                defer=None):
+        """defer (a list): the parameter gradients' partials stay in a workspace of their own, recorded in
+        `defer` for one es_ln_param_grads_multi launch later (Engine.DEFER_LN_GRADS)."""
         D = self.cfg.dim
-        ws = self.ln_workspace(lane)
         fn = "es_layernorm_bwd_b16" if dy.dtype == torch.bfloat16 else "es_layernorm_bwd"  # (_f32 in parity mode)
+        grid = _lib.load().es_layernorm_bwd_grid(LN_BWD_BLOCKS, M)
+        if defer is not None and grid >= 64:  # (one multi-reduce launch takes one column-width class: grid >= 64)
+            ws = self.ln_part_workspace(self._lnp_next)  # never reused within a reverse pass (the side stream
+            self._lnp_next += 1                           # may reduce a flushed one after the chain moved on)
+            self._call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
+                       ptr(dxb), D, None, None, ptr(ws), LN_BWD_BLOCKS, M, D, 0, _lib.stream())
+            defer.append((ws, dgamma, dbeta, grid, accumulate))
+            return
+        ws = self.ln_workspace(lane)
         self._call(fn, ptr(dy), D, ptr(x), D, ptr(mean), ptr(rstd), ptr(gamma), ptr(dres), D, ptr(dx), lddx or D,
              ptr(dxb), D, ptr(dgamma), ptr(dbeta), ptr(ws), LN_BWD_BLOCKS, M, D, accumulate, _lib.stream())
+
+    def ln_part_workspace(self, k):
+        """The k-th deferred LayerNorm backward's partials of a reverse pass (Engine.DEFER_LN_GRADS)."""
+        if self._ws_lnp is None:
+            self._ws_lnp = []
+        while len(self._ws_lnp) <= k:
+            self._ws_lnp.append(torch.empty(2 * LN_BWD_BLOCKS * self.cfg.dim, dtype=torch.float32, device=self.device))
+        return self._ws_lnp[k]
+
+    def _ln_grads_flush(self, pending):
+        """One es_ln_param_grads_multi launch over the deferred LayerNorm backwards in `pending` (then cleared)."""
+        if not pending:
+            return
+        lib = _lib.load()
+        esz = lib.es_ln_param_grads_entry_size()
+        raw = (ctypes.c_char * (esz * len(pending)))()
+        for j, (ws, dg, db, grid, acc) in enumerate(pending):
+            ent = (ctypes.c_void_p(ptr(ws)), ctypes.c_void_p(ptr(dg)), ctypes.c_void_p(ptr(db)), ctypes.c_int(grid),
+                   ctypes.c_int(self.cfg.dim), ctypes.c_int(acc), ctypes.c_int(0))
+            buf = b"".join(bytes(e) for e in ent)
+            ctypes.memmove(ctypes.byref(raw, j * esz), buf, len(buf))
+        self._call("es_ln_param_grads_multi", ctypes.addressof(raw), len(pending), _lib.stream())
+        pending.clear()
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True, grad_ready=None):
         """dlogits fp32 [n, C] (head "cls") or dfts fp32 [n, D] (head "emb") for the last train
@@ -636,6 +676,10 @@ class Engine:
         problems = []
         layer_wg = self.LAYER_WGRAD and not grouped and self.precision == "bf16" and M >= self.TN_SHARE_MIN_M
         lp = []  # this block's long-axis weight gradients (layer_wg): one grouped launch at the block's end
+        # deferred LayerNorm parameter gradients (Engine.DEFER_LN_GRADS): reduced with the weight-gradient launches
+        lnd = ([] if self.DEFER_LN_GRADS and grad_ready is None and self.capture is None and not lanes
+               and (grouped or layer_wg) else None)
+        self._lnp_next = 0
 
         def wgrad_side(dy, N1, x, N2, Mw, out, bias_out=None, ld1=None, ld2=None, label=None):
             """Weight-gradient GEMM on the side stream once the main stream has produced dY (or, grouped,
@@ -657,17 +701,24 @@ class Engine:
         done = {}
 
         def flush_layer(i):
-            """Block i's recorded weight gradients as one grouped split-K launch on the side stream."""
-            if not lp:
+            """Block i's recorded weight gradients as one grouped split-K launch on the side stream (and the
+            LayerNorm parameter gradients deferred so far)."""
+            if not lp and not (layer_wg and lnd):
                 return
             probs = list(lp)
             lp.clear()
+
+            def run():
+                if probs:
+                    self._wgrad_layer(probs, i)
+                if layer_wg and lnd:
+                    self._ln_grads_flush(lnd)
             if ov:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    self._wgrad_layer(probs, i)
+                    run()
             else:
-                self._wgrad_layer(probs, i)
+                run()
 
         def block_done(i):
             if self.capture is not None:
@@ -685,8 +736,12 @@ class Engine:
                     side.wait_stream(main)
                     with torch.cuda.stream(side):
                         self._launch_grouped(problems, i)
+                        if lnd:
+                            self._ln_grads_flush(lnd)
                 else:
                     self._launch_grouped(problems, i)
+                    if lnd:
+                        self._ln_grads_flush(lnd)
                 problems.clear()
             if grad_ready is None:
                 return
@@ -736,7 +791,7 @@ class Engine:
                 wgrad_side(Gi.c_dpre, Hd, A.c_h2, D, n, gv(b + "mlp.fc1.weight"), gv(b + "mlp.fc1.bias"))
                 # d(xmid) lands on the CLS rows of the full token image dxm_cls (zero elsewhere)
                 self._ln_bwd(Gi.c_dh, A.c_xmid, A.c_mean2, A.c_rstd2, fv(b + "norm2.weight"), Gi.c_dx, Gi.dxm_cls,
-                             Gi.c_dxmb, gv(b + "norm2.weight"), gv(b + "norm2.bias"), n, lddx=T * D)
+                             Gi.c_dxmb, gv(b + "norm2.weight"), gv(b + "norm2.bias"), n, lddx=T * D, defer=lnd)
                 self._call("es_gemm_nt", EPI_BF16, ptr(Gi.c_dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None,
                      ptr(Gi.c_do), D, None, None, 0, n, D, D, 0, s)
                 wgrad_side(Gi.c_dxmb, D, A.c_o, D, n, gv(b + "attn.proj.weight"), gv(b + "attn.proj.bias"))
@@ -756,7 +811,7 @@ class Engine:
                 if ovw:
                     done[i] = side.record_event()
                 self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), Gi.dxm_cls, G.dx, Gn.dxb,
-                             gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
+                             gv(b + "norm1.weight"), gv(b + "norm1.bias"), M, defer=lnd)
                 block_done(i)
                 continue
             if lanes:
@@ -783,7 +838,7 @@ class Engine:
                 cap("b_dpre", True, i, Gi.dpre[:M])
                 cap("b_dh2", True, i, G.dh[:M])
             self._ln_bwd(G.dh, A.xmid[i], A.mean2[i], A.rstd2[i], fv(b + "norm2.weight"), G.dx, G.dxm, Gi.dxmb,
-                         gv(b + "norm2.weight"), gv(b + "norm2.bias"), M)
+                         gv(b + "norm2.weight"), gv(b + "norm2.bias"), M, defer=lnd)
             # ---- attention:  xmid = x_i + proj(attn(LN1(x_i)))
             self._call("es_gemm_nt", EPI_BF16, ptr(Gi.dxmb), D, ptr(self.wt[b + "attn.proj.weight"]), D, None, ptr(G.do), D,
                  None, None, 0, M, D, D, 0, s)
@@ -805,7 +860,7 @@ class Engine:
                 if i + 1 in done:  # set (i-1) % 2 was layer i+1's: its weight gradients must be done
                     main.wait_event(done.pop(i + 1))
             self._ln_bwd(G.dh, A.x[i], A.mean1[i], A.rstd1[i], fv(b + "norm1.weight"), G.dxm, G.dx, Gn.dxb,
-                         gv(b + "norm1.weight"), gv(b + "norm1.bias"), M)
+                         gv(b + "norm1.weight"), gv(b + "norm1.bias"), M, defer=lnd)
             block_done(i)
         # ---- embedding: x_0 = [cls; patch_embed(img)] + pos
         K0 = 3 * cfg.patch * cfg.patch
@@ -818,6 +873,8 @@ class Engine:
         flush_layer(-1)  # the patch-embedding weight gradient (layer_wg): the backward's last launch
         if grouped:
             self._launch_grouped(problems, 0)
+        if lnd:
+            self._ln_grads_flush(lnd)
         if ov:
             main.wait_stream(side)
         if lanes:

@@ -159,6 +159,15 @@ int es_layernorm_bwd_b16(const void* dy, int lddy, const float* x, int ldx, cons
                          const float* gamma, const float* dres, int ldres, float* dx, int lddx, void* dxb, int lddxb,
                          float* dgamma, float* dbeta, float* workspace, int blocks, int M, int D, int accumulate,
                          hipStream_t stream);
+// Both backwards with dgamma == dbeta == NULL leave their per-workgroup partials in `workspace`
+// (es_layernorm_bwd_grid(blocks, M) rows of D floats for dgamma, then as many for dbeta);
+// es_ln_param_grads_multi then reduces up to 32 such workspaces in ONE launch (the ViT engine defers its
+// LayerNorms' parameter gradients off the data-gradient chain).  Table entries (host memory, passed by value):
+// {const float* workspace; float* dgamma; float* dbeta; int grid; int D; int accumulate; int pad}, all with the
+// same (grid >= 64 && D <= 2048) class.  Same sums, bit for bit, as the undeferred backward.
+int es_layernorm_bwd_grid(int blocks, int M);
+int es_ln_param_grads_entry_size(void);
+int es_ln_param_grads_multi(const void* table, int n, hipStream_t stream);
 
 /* ---- standalone GELU (nn.GELU, exact erf) ---------------------------------------------------- */
 int es_gelu_fwd(const void* x, void* y, long n, hipStream_t stream);

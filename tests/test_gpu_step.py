@@ -373,6 +373,48 @@ def test_shard_lanes_match_single_lane(nimg, prune, full):
     assert worst_ln <= 1e-6, worst_ln
 
 
+@pytest.mark.parametrize("mode,nimg", [("grouped", 40), ("grouped", 64), ("layer", 88)])
+def test_deferred_ln_grads_bit_identical(mode, nimg):
+    """Engine.DEFER_LN_GRADS (each LayerNorm backward's dgamma / dbeta partials kept, reduced by one
+    es_ln_param_grads_multi launch per weight-gradient launch on the side stream) gives every gradient BIT-identical
+    to the per-LayerNorm reductions on the chain.  grouped: the small-shard path (GROUP_WGRAD, flushed with each
+    grouped launch, the last block's CLS-row LN2 too small to defer at nimg 40); layer: ViT-S/16 at 224^2 with
+    M = 17,336 train tokens (LAYER_WGRAD: flushed with each block's split-K launch)."""
+    from endossl.vit import NativeViT, ViTConfig
+    vcfg, _ = _tiny_cfgs()
+    if mode == "layer":
+        vcfg = ViTConfig(num_classes=23)
+    m = NativeViT(vcfg, seed=9)
+    with torch.no_grad():  # a non-zero head (timm zero-inits it): otherwise every trunk gradient is exactly zero
+        m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(3)))
+    m.mark_updated()
+    m = m.to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    eng.GROUP_WGRAD = "1" if mode == "grouped" else "0"
+    g = torch.Generator(device=DEV).manual_seed(4)
+    S = vcfg.img_size
+    x = torch.randn(nimg, 3, S, S, device=DEV, generator=g)
+    dl = torch.randn(nimg, 23, device=DEV, generator=g) * 1e-2
+    grads, used = {}, {}
+    for defer in (False, True):
+        eng.DEFER_LN_GRADS = defer
+        for _ in range(2):  # the second pass reuses the partial workspaces
+            eng.forward(m.flat, [x], train=True)
+            gr = torch.full_like(m.flat, 5.0)
+            eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        grads[defer], used[defer] = gr.clone(), eng._lnp_next
+    for k in ("GROUP_WGRAD", "DEFER_LN_GRADS"):
+        delattr(eng, k)
+    assert used[False] == 0 and used[True] >= 2 * vcfg.depth - 1, used  # the deferred path ran
+    for name, _ in eng.layout:
+        a, b = eng.view(grads[True], name), eng.view(grads[False], name)
+        if name.startswith("blocks.") and (".norm1." in name or ".norm2." in name):
+            assert b.abs().max() > 0, name  # the comparison is not vacuous
+        assert torch.equal(a, b), (name, (a - b).abs().max().item())
+
+
 @pytest.mark.parametrize("head,nimg", [("cls", 40), ("emb", 40), ("cls", 64), ("emb", 64)])
 def test_last_block_cls_rows_match_full_rows(head, nimg):
     """Engine.PRUNE_LAST (the last block's attention for the CLS queries only, its projection / LN2 /
