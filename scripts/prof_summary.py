@@ -1,6 +1,8 @@
 """Summarise a rocprofv3 --kernel-trace --stats run of bench.py into profiles/<tag>_*.
 
-  python scripts/prof_summary.py gpurun_out/prof <tag> [steps_profiled]
+  python scripts/prof_summary.py gpurun_out/prof <tag> [steps_profiled | 0] [bench log of the profiled process]
+(with the bench log: the line's live roofline span next to the trace's span of the same launches in the timed
+steps -- the bench's warm-up steps, then its timed ones, are the first optimizer launches of the trace)
 Writes <tag>_kernel_stats.csv (rocprofv3's own summary, copied) and <tag>_summary.md
 (per-kernel ms/step, per-shape GEMM/attention breakdown from the trace)."""
 import collections
@@ -11,7 +13,8 @@ import shutil
 import sys
 
 src, tag = sys.argv[1], sys.argv[2]
-steps = int(sys.argv[3]) if len(sys.argv) > 3 else None  # default: the optimizer launches (one per step)
+steps = int(sys.argv[3]) if len(sys.argv) > 3 and int(sys.argv[3]) > 0 else None  # default: optimizer launches
+benchlog = sys.argv[4] if len(sys.argv) > 4 else None
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 out = os.path.join(root, "profiles")
 os.makedirs(out, exist_ok=True)
@@ -20,7 +23,7 @@ rows = list(csv.DictReader(open(os.path.join(src, "run_kernel_stats.csv"))))
 tot = sum(float(r["TotalDurationNs"]) for r in rows)
 if steps is None:  # every step the bench runs (warm-up, timed, its probes) ends in one adam_ema launch
     steps = sum(int(r["Calls"]) for r in rows if "adam_ema_kernel(" in r["Name"]) or 7
-lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py --steps 5 --warmup 2` (F1, 1x MI355X)", "",
+lines = [f"# {tag}: rocprofv3 --kernel-trace --stats of `bench.py` (1x MI355X)", "",
          f"Total GPU kernel time / step: **{tot / 1e6 / steps:.2f} ms** (every kernel of the profiled process over its {steps} "
          "optimizer launches, so the bench's isolated-kernel and probe launches are included; one step's own kernel "
          "time is in the step-counter table)", "",
@@ -61,9 +64,35 @@ if os.path.exists(tr):
     site = (f" In this trace: {len(spans)} such launches, kernel {sum(kern) / len(kern):.1f} us on average, "
             f"kernel start to reduce end {sum(spans) / len(spans):.1f} us (the span the bench's `mean_launch_ms` "
             "times with kernel-stamped events).") if spans else ""
+    if spans and benchlog and os.path.exists(benchlog):
+        import json
+        line = json.loads([x for x in open(benchlog) if x.startswith('{"metric')][-1])
+        w, k = line["warmup"], line["steps"]
+        # launches per optimizer step, in trace order (all queues): the timed steps are steps [w, w + k)
+        bounds = [int(r["Start_Timestamp"]) for r in rows if "adam_ema_kernel(" in r["Kernel_Name"]]
+        t0 = bounds[w - 1] if w > 0 else 0
+        t1 = bounds[w + k - 1]
+        per_step = collections.defaultdict(list)  # the timed steps' launches, by step, in start order
+        for q in byq.values():
+            for i, r in enumerate(q[:-1]):
+                st = int(r["Start_Timestamp"])
+                if ("tn_big_grouped" in r["Kernel_Name"] and int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]) == 96
+                        and "splitk_reduce_grouped" in q[i + 1]["Kernel_Name"] and t0 < st < t1):
+                    step = sum(1 for x in bounds if x < st)
+                    per_step[step].append((st, (int(q[i + 1]["End_Timestamp"]) - st) / 1e3,
+                                           (int(r["End_Timestamp"]) - st) / 1e3))
+        # each step's first such launch is the last block's (its K / V slice only, ~0.19 ms): the line times
+        # blocks 10..1
+        tspan = [sp for v in per_step.values() for _, sp, _ in sorted(v)[1:]]
+        tkern = [kk for v in per_step.values() for _, _, kk in sorted(v)[1:]]
+        rl = line["roofline"]
+        site += (f" In the {k} timed steps of the same process, blocks 10..1 ({len(tspan)} launches): kernel start to "
+                 f"reduce end {sum(tspan) / len(tspan):.1f} us (kernel alone {sum(tkern) / len(tkern):.1f} us) against "
+                 f"the bench line's `mean_launch_ms` {rl['mean_launch_ms'] * 1e3:.1f} us over its {rl.get('launches')} "
+                 f"launches: {rl['mean_launch_ms'] * 1e3 / (sum(tspan) / len(tspan)):.3f}x.")
     lines += ["", "The bench's roofline site (a block's four weight-gradient GEMMs, fc2 / fc1 / proj / qkv over "
               "M = 100,864 tokens) is the `gemm_tn_big_grouped_kernel` launch of 96 workgroups (24 tiles of 384 x 192 "
-              "x 4 splits, 3/8 of the CUs, 12 per step) plus its `splitk_reduce_grouped_kernel`; the first block's "
+              "x 4 splits, 3/8 of the CUs, 11 per step: blocks 11..1, block 11's on its K / V slice alone) plus its `splitk_reduce_grouped_kernel`; the first block's "
               "launch (whole chip, the end of the backward) and the patch embedding's are other grid sizes above."
               + site + " Durations under the profiler run at lower clocks (MI355X_MICROARCH.md 'DVFS give-back' "
               "item 2)."]
