@@ -58,9 +58,119 @@ struct NTConv {
   // forward only (INBN): the gathered map is a train-mode BatchNorm's INPUT; each in-range gathered channel
   // quad becomes relu(bn_affine(x)) in the map's type -- the normalised map itself is never written
   const float* bnm; const float* bnr; const float* bng; const float* bnb;
+  // the output pixel m lives at out + m * osw (a dense NHWC map and no stride phase): the epilogue skips the
+  // per-row (n, h, w) decomposition -- four integer divisions by run-time values per stored row
+  int olin;
 };
 
 constexpr int NT_BM = 128, NT_BK = 32;
+
+// sum over the 16 lanes of each row of 16 (every lane gets its row's sum): DPP quad swaps, then the half-row and
+// row mirrors -- the same pairwise tree for every lane, no LDS traffic (__shfl_xor is ds_bpermute_b32)
+__device__ __forceinline__ float row16_sum(float t) {
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0xB1, 0xF, 0xF, true));  // [1,0,3,2]
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0x4E, 0xF, 0xF, true));  // [2,3,0,1]
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0x141, 0xF, 0xF, true));  // half mirror
+  t += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, t), 0x140, 0xF, 0xF, true));  // row mirror
+  return t;
+}
+
+// The forward / data-grad epilogue shared by the register-staged and the ring kernels: BatchNorm statistics of
+// the tile (forward, STATS), then the outputs through LDS as whole-row quads.
+template <int BN, bool DX, bool STATS, typename TO>
+__device__ __forceinline__ void nt_tail(const NTConv& a, f32x4 (&acc)[4][BN / 32], int M, int m0, int n0, int Hm,
+                                        int Wm, int om, int oa0, int ob0, char* smem) {
+  constexpr int NF = BN / 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+  const int wm = w >> 1, wn = w & 1;
+  // BatchNorm statistics of this tile (forward, STATS: a separate instantiation, so the plain
+  // forward keeps its registers): per output channel the block's sum and its
+  // centred sum of squares M2 over the valid pixels of the 128-pixel block (Chan's parallel form;
+  // es_bn2d_fwd_partials combines the blocks).  Lane (g, r) holds rows wm 64 + 16 i + r of the 4
+  // channels wn BN/2 + 16 j + 4 g + q: sums over i in-lane, over r by xor shuffles within each
+  // 16-lane group, over the two row waves (wm) through LDS.
+  if constexpr (STATS && !DX) {
+    // the bias shifts a channel's values uniformly: M2 is computed on the accumulators alone and the
+    // sum gets nb bias[col] added once (no per-lane bias registers: the plain instantiation's occupancy)
+    float* red = (float*)smem;  // [2 (wm)][BN] partial sums, then [2][BN] partial M2
+    const int nb = min(NT_BM, M - m0);
+    bool rv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rv[i] = m0 + wm * 64 + i * 16 + r < M;
+    float mu[NF][4];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float t = 0.f;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = pass == 0 ? acc[i][j][q] : acc[i][j][q] - mu[j][q];
+            t += rv[i] ? (pass == 0 ? d : d * d) : 0.f;
+          }
+          t = row16_sum(t);
+          if (r == 0) red[wm * BN + wn * (BN / 2) + j * 16 + 4 * g + q] = t;
+        }
+      __syncthreads();
+      const bool wr = tid < BN && n0 + tid < a.Ncol;
+      if (pass == 0) {
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int cl = wn * (BN / 2) + j * 16 + 4 * g + q;
+            mu[j][q] = (red[cl] + red[BN + cl]) / (float)nb;
+          }
+        if (wr)
+          a.stats[(long)blockIdx.x * 2 * a.Ncol + n0 + tid] =
+              red[tid] + red[BN + tid] + (a.bias ? (float)nb * a.bias[n0 + tid] : 0.f);
+        __syncthreads();
+      } else if (wr) {
+        a.stats[(long)blockIdx.x * 2 * a.Ncol + a.Ncol + n0 + tid] = red[tid] + red[BN + tid];
+      }
+    }
+    __syncthreads();
+  }
+
+  // Epilogue through LDS (the stage buffers are free after the loop's last barrier): lane holds
+  // out[pixel m0 + wm 64 + 16 i + r][col wn BN/2 + 16 j + 4 g .. + 3]; per 16-pixel chunk the wave
+  // writes its [16][BN/2] tile to its LDS region and reads it back as whole-row quads, so every store
+  // instruction covers RPI pixel rows x BN/2 contiguous channels (256 B per row at BN = 128).
+  constexpr int NCOL = BN / 2, QPR = NCOL / 4, RPI = 64 / QPR, ROWF = NCOL + 4;
+  float* wl = (float*)smem + w * 16 * ROWF;
+  const int eq = lane % QPR, er = lane / QPR;
+  const int ecol = n0 + wn * NCOL + eq * 4;
+  const bool ecol_ok = ecol < a.Ncol;
+  const f32x4 bv = (a.bias && ecol_ok) ? *(const f32x4*)(a.bias + ecol) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+#pragma unroll
+    for (int j = 0; j < NF; ++j) *(f32x4*)(wl + r * ROWF + j * 16 + 4 * g) = acc[i][j];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < 16 / RPI; ++it) {
+      const int row = er + it * RPI;
+      const f32x4 v0 = *(const f32x4*)(wl + row * ROWF + eq * 4);
+      const int m = m0 + wm * 64 + i * 16 + row;
+      if (m < M && ecol_ok) {
+        TO* o;
+        if (a.olin) {
+          o = (TO*)a.out + (long)m * a.osw + ecol;
+        } else {
+          const int bb = m % Wm, t = m / Wm, aa = t % Hm, n = t / Hm;
+          o = (TO*)a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw + ecol;
+        }
+        f32x4 v = v0 + bv;
+        if (a.accumulate) v += q4_f32(q4_load(o));
+        q4_store(o, v);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
 
 // out[pixel][col] (+)= bias[col] + sum_{tap, c} src[gathered pixel(tap)][c] . wp[col][tap][c]
 // DX = false: pixels (n, ho, wo); source (n, ho s - p + ky, wo s - p + kx).
@@ -204,90 +314,144 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
     __syncthreads();
   }
 
-  // BatchNorm statistics of this tile (forward, STATS: a separate instantiation, so the plain
-  // forward keeps its registers): per output channel the block's sum and its
-  // centred sum of squares M2 over the valid pixels of the 128-pixel block (Chan's parallel form;
-  // es_bn2d_fwd_partials combines the blocks).  Lane (g, r) holds rows wm 64 + 16 i + r of the 4
-  // channels wn BN/2 + 16 j + 4 g + q: sums over i in-lane, over r by xor shuffles within each
-  // 16-lane group, over the two row waves (wm) through LDS.
-  if constexpr (STATS && !DX) {
-    // the bias shifts a channel's values uniformly: M2 is computed on the accumulators alone and the
-    // sum gets nb bias[col] added once (no per-lane bias registers: the plain instantiation's occupancy)
-    float* red = (float*)smem;  // [2 (wm)][BN] partial sums, then [2][BN] partial M2
-    const int nb = min(NT_BM, M - m0);
-    bool rv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rv[i] = m0 + wm * 64 + i * 16 + r < M;
-    float mu[NF][4];
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-#pragma unroll
-      for (int j = 0; j < NF; ++j)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float t = 0.f;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float d = pass == 0 ? acc[i][j][q] : acc[i][j][q] - mu[j][q];
-            t += rv[i] ? (pass == 0 ? d : d * d) : 0.f;
-          }
-          t += __shfl_xor(t, 1, 64);
-          t += __shfl_xor(t, 2, 64);
-          t += __shfl_xor(t, 4, 64);
-          t += __shfl_xor(t, 8, 64);
-          if (r == 0) red[wm * BN + wn * (BN / 2) + j * 16 + 4 * g + q] = t;
-        }
-      __syncthreads();
-      const bool wr = tid < BN && n0 + tid < a.Ncol;
-      if (pass == 0) {
-#pragma unroll
-        for (int j = 0; j < NF; ++j)
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int cl = wn * (BN / 2) + j * 16 + 4 * g + q;
-            mu[j][q] = (red[cl] + red[BN + cl]) / (float)nb;
-          }
-        if (wr)
-          a.stats[(long)blockIdx.x * 2 * a.Ncol + n0 + tid] =
-              red[tid] + red[BN + tid] + (a.bias ? (float)nb * a.bias[n0 + tid] : 0.f);
-        __syncthreads();
-      } else if (wr) {
-        a.stats[(long)blockIdx.x * 2 * a.Ncol + a.Ncol + n0 + tid] = red[tid] + red[BN + tid];
-      }
-    }
-    __syncthreads();
-  }
+  nt_tail<BN, DX, STATS, TO>(a, acc, M, m0, n0, Hm, Wm, om, oa0, ob0, smem);
+}
 
-  // Epilogue through LDS (the stage buffers are free after the loop's last barrier): lane holds
-  // out[pixel m0 + wm 64 + 16 i + r][col wn BN/2 + 16 j + 4 g .. + 3]; per 16-pixel chunk the wave
-  // writes its [16][BN/2] tile to its LDS region and reads it back as whole-row quads, so every store
-  // instruction covers RPI pixel rows x BN/2 contiguous channels (256 B per row at BN = 128).
-  constexpr int NCOL = BN / 2, QPR = NCOL / 4, RPI = 64 / QPR, ROWF = NCOL + 4;
-  float* wl = (float*)smem + w * 16 * ROWF;
-  const int eq = lane % QPR, er = lane / QPR;
-  const int ecol = n0 + wn * NCOL + eq * 4;
-  const bool ecol_ok = ecol < a.Ncol;
-  const f32x4 bv = (a.bias && ecol_ok) ? *(const f32x4*)(a.bias + ecol) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-#pragma unroll
-    for (int j = 0; j < NF; ++j) *(f32x4*)(wl + r * ROWF + j * 16 + 4 * g) = acc[i][j];
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int it = 0; it < 16 / RPI; ++it) {
-      const int row = er + it * RPI;
-      const f32x4 v0 = *(const f32x4*)(wl + row * ROWF + eq * 4);
-      const int m = m0 + wm * 64 + i * 16 + row;
-      if (m < M && ecol_ok) {
-        const int bb = m % Wm, t = m / Wm, aa = t % Hm, n = t / Hm;
-        TO* o = (TO*)a.out + (long)n * a.osn + (long)(aa * om + oa0) * a.osh + (long)(bb * om + ob0) * a.osw + ecol;
-        f32x4 v = v0 + bv;
-        if (a.accumulate) v += q4_f32(q4_load(o));
-        q4_store(o, v);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
+// The same forward / data-grad convolution for a bf16 gathered map with the operand tiles brought in by LDS-DMA
+// (buffer_load ... lds: a padding or past-M pixel is an out-of-range offset and reads as zeros) through an
+// NST-stage ring, stage k + NST - 1 issued right after the barrier that publishes stage k (counted vmcnt, raw
+// s_barrier) -- the register-staged kernel above keeps ONE step of gathers in flight behind 16 MFMAs per wave,
+// which leaves the 1 x 1 / 3 x 3 convs at 3-5x their HBM floors.  Same LDS images (cswz64: the DMA lane writing
+// physical chunk p of row r fetches logical chunk cswz64(r, p)), same fragments and MFMAs, same epilogue:
+// bit-identical outputs.
+template <int P3>
+__device__ __forceinline__ void conv_wait_vmcnt(int n) {
+  switch (n) {
+#define ES_CVM(N) case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    ES_CVM(1) ES_CVM(2) ES_CVM(3) ES_CVM(4) ES_CVM(5) ES_CVM(6) ES_CVM(8) ES_CVM(9) ES_CVM(12)
+#undef ES_CVM
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
+}
+
+template <int BN, bool DX, bool STATS, typename TO, int NST = 4>
+__global__ __launch_bounds__(256) void convb_nt_ring_kernel(NTConv a) {
+  constexpr int NF = BN / 32;
+  constexpr int ABYTES = NT_BM * 64, BBYTES = BN * 64, STAGE = ABYTES + BBYTES;
+  constexpr int IA = 2, IB = BN / 64, PER = IA + IB;  // 1-KiB DMA pieces per wave per stage
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  int Hm, Wm, ra, ca, cb, sy, twx, twy, by0, bx0, bs, om, oa0, ob0;
+  if constexpr (!DX) {
+    Hm = a.Ho; Wm = a.Wo; ra = a.s; ca = -a.p; cb = -a.p; sy = 1; twy = a.kh; twx = a.kw;
+    by0 = 0; bx0 = 0; bs = 1; om = 1; oa0 = 0; ob0 = 0;
+  } else {
+    const int s = a.s, py = blockIdx.z / s, px = blockIdx.z - py * s;
+    Hm = (a.Ho - py + s - 1) / s;
+    Wm = (a.Wo - px + s - 1) / s;
+    const int ky0 = (py + a.p) % s, kx0 = (px + a.p) % s;
+    twy = a.kh > ky0 ? (a.kh - ky0 + s - 1) / s : 0;
+    twx = a.kw > kx0 ? (a.kw - kx0 + s - 1) / s : 0;
+    ca = (py + a.p - ky0) / s; cb = (px + a.p - kx0) / s; ra = 1; sy = -1;
+    by0 = ky0; bx0 = kx0; bs = s; om = s; oa0 = py; ob0 = px;
+  }
+  const int M = a.N * Hm * Wm;
+  const int m0 = blockIdx.x * NT_BM, n0 = blockIdx.y * BN;
+  if (m0 >= M) return;  // a smaller stride phase (block-uniform)
+  const int nk = twy * twx * (a.C / NT_BK);
+  const int Kfull = a.kh * a.kw * a.C;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int g = lane >> 4, r = lane & 15;
+
+  // A pieces: wave w, piece j covers tile rows (4 j + w) 16 .. + 15; lane -> row + lane / 4, physical chunk lane % 4
+  const i32x4 srs = rsrc_i4(a.src, (unsigned)(((long)(a.N - 1) * a.ssn + (long)(a.Hs - 1) * a.ssh +
+                                                (long)(a.Ws - 1) * a.ssw + a.C) * 2));
+  long abase[IA];
+  int ahb[IA], awb[IA], alc[IA];
+#pragma unroll
+  for (int j = 0; j < IA; ++j) {
+    const int row = (4 * j + w) * 16 + (lane >> 2);
+    alc[j] = cswz64(row, lane & 3) * 8;  // the logical channel chunk this lane's physical chunk holds
+    const int am = m0 + row;
+    abase[j] = 0;
+    ahb[j] = -(1 << 28);  // a pixel row past M: every tap out of range, zeros
+    awb[j] = 0;
+    if (am < M) {
+      const int bb = am % Wm, t = am / Wm, aa = t % Hm, n = t / Hm;
+      abase[j] = (long)n * a.ssn;
+      ahb[j] = aa * ra + ca;
+      awb[j] = bb * ra + cb;
+    }
+  }
+  // B pieces: weight rows (4 j + w) 16 .. (BN = 128: j < 2; BN = 64: j = 0); rows past Ncol read zeros
+  const i32x4 wrs = rsrc_i4(a.wp, (unsigned)((long)a.Ncol * Kfull * 2));
+  unsigned bofs[IB];
+#pragma unroll
+  for (int j = 0; j < IB; ++j) {
+    const int row = (4 * j + w) * 16 + (lane >> 2);
+    const int col = n0 + row;
+    bofs[j] = col < a.Ncol ? (unsigned)(((long)col * Kfull + cswz64(row, lane & 3) * 8) * 2) : ES_OOB;
+  }
+  auto issue = [&](int buf, int kt) {
+    const int k0 = kt * NT_BK;
+    const int tq = k0 / a.C, c0 = k0 - tq * a.C;
+    const int tyq = tq / twx, txq = tq - tyq * twx;
+    char* As = smem + buf * STAGE;
+    char* Bs = As + ABYTES;
+#pragma unroll
+    for (int j = 0; j < IA; ++j) {
+      const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
+      const bool ok = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
+      const unsigned off = ok ? (unsigned)((abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0 + alc[j]) * 2) : ES_OOB;
+      bl16_asm(srs, off, 0u, As + (4 * j + w) * 1024);
+    }
+    const int btap = (by0 + tyq * bs) * a.kw + bx0 + txq * bs;
+    const unsigned bsoff = (unsigned)((btap * a.C + c0) * 2);
+#pragma unroll
+    for (int j = 0; j < IB; ++j)
+      bl16_asm(wrs, bofs[j] == ES_OOB ? ES_OOB : bofs[j] + bsoff, 0u, Bs + (4 * j + w) * 1024);
+  };
+
+  const int wm = w >> 1, wn = w & 1;
+  f32x4 acc[4][NF];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NF; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) issue(st, st);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    conv_wait_vmcnt<0>(min(NST - 2, nk - 1 - kt) * PER);
+    __builtin_amdgcn_s_barrier();
+    if (kt + NST - 1 < nk) {
+      int nb = buf + NST - 1;
+      nb = nb >= NST ? nb - NST : nb;
+      issue(nb, kt + NST - 1);
+    }
+    const char* As = smem + buf * STAGE;
+    const char* Bs = As + ABYTES;
+    bf16x8 af[4], bfr[NF];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = wm * 64 + i * 16 + r;
+      af[i] = *(const bf16x8*)(As + rr * 64 + cswz64(rr, g) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {
+      const int rr = wn * (BN / 2) + j * 16 + r;
+      bfr[j] = *(const bf16x8*)(Bs + rr * 64 + cswz64(rr, g) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j) acc[i][j] = mfma16(bfr[j], af[i], acc[i][j]);
+    buf = buf + 1 == NST ? 0 : buf + 1;
+  }
+  __syncthreads();  // every wave's last fragment reads are done before the tail reuses the ring as scratch
+  nt_tail<BN, DX, STATS, TO>(a, acc, M, m0, n0, Hm, Wm, om, oa0, ob0, smem);
 }
 
 // ---- weight gradient -------------------------------------------------------------------------
@@ -582,9 +746,36 @@ void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
   }
 }
 
+// bf16 gathered maps on the LDS-DMA ring (convb_nt_ring_kernel): 0 = off (the register-staged kernel), else its
+// stage count (3 or 4); es_set_conv_ring.  Isolated at the Conformer-B/384 shapes (r05, scripts/convb_bench.py
+// --bnin --all-shapes, ring 0 / 3 / 4): every data gradient is 7-20 % faster on 3 stages (48 KiB: three workgroups
+// per CU; 4 stages hold two), and so is every forward that does not widen the channels (the 3 x 3, the 1 x 1
+// reductions, FCUUp: 146 vs 163 us at stage 1's conv1); the widening 1 x 1 forwards (conv3, the strided residual
+// conv) lose 5-15 % on it (a 2-8-step K loop cannot use the ring; the staged kernel's 32 KiB fit more tiles)
+int g_conv_ring = 3;
+
+template <int BN, bool DX, bool STATS, int NST>
+void launch_ring_n(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
+  const size_t lds = (size_t)NST * (NT_BM + BN) * 64;
+  if (flags & 2) hipLaunchKernelGGL((convb_nt_ring_kernel<BN, DX, STATS, bf16, NST>), grid, 256, lds, stream, a);
+  else hipLaunchKernelGGL((convb_nt_ring_kernel<BN, DX, STATS, float, NST>), grid, 256, lds, stream, a);
+}
+// true when the ring kernel took the launch: a bf16 source map under 2 GiB (32-bit DMA offsets), no input BatchNorm
+template <int BN, bool DX, bool STATS>
+bool launch_ring(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
+  const long src_bytes = ((long)(a.N - 1) * a.ssn + (long)(a.Hs - 1) * a.ssh + (long)(a.Ws - 1) * a.ssw + a.C) * 2;
+  const long w_bytes = (long)a.Ncol * a.kh * a.kw * a.C * 2;
+  if (!g_conv_ring || !(flags & 1) || a.bnm || src_bytes >= 0x7fff0000L || w_bytes >= 0x7fff0000L) return false;
+  if (!DX && a.Ncol > a.C) return false;  // a widening forward: the staged kernel
+  if (g_conv_ring == 3) launch_ring_n<BN, DX, STATS, 3>(grid, flags, a, stream);
+  else launch_ring_n<BN, DX, STATS, 4>(grid, flags, a, stream);
+  return true;
+}
+
 // the forward / weight-gradient launches with or without the input BatchNorm
 template <int BN, bool STATS>
 void launch_fwd(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
+  if (launch_ring<BN, false, STATS>(grid, flags, a, stream)) return;
   if (a.bnm) launch_nt<BN, false, STATS, true>(grid, flags, a, stream);
   else launch_nt<BN, false, STATS, false>(grid, flags, a, stream);
 }
@@ -601,6 +792,16 @@ extern "C" {
 // 1 if the bf16 kernels take a conv of these channel counts (both multiples of 32)
 // tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 512);
 // returns the previous value (v <= 0: unchanged)
+// tuning knob: the bf16-map data-gradient convs and the forwards that do not widen the channels on the LDS-DMA
+// ring kernel with this many stages (3 or 4, default 3), or 0 = the register-staged kernel (bit-identical);
+// returns the previous value, or ES_BAD_ARG (unchanged) for any other value
+int es_set_conv_ring(int v) {
+  if (v != 0 && v != 3 && v != 4) return ES_BAD_ARG;
+  const int old = g_conv_ring;
+  g_conv_ring = v;
+  return old;
+}
+
 int es_set_conv_dw_target(int v) {
   const int old = g_dw_target_wg;
   if (v > 0) g_dw_target_wg = v;
@@ -655,7 +856,7 @@ static int conv_fwd_bf16_impl(const void* x, int N, int H, int W, int Cin, long 
     return ES_BAD_SHAPE;
   if (bnm && (!bnr || !bng || !bnb || !al16(bnm) || !al16(bnr) || !al16(bng) || !al16(bnb))) return ES_BAD_ARG;
   NTConv a{x, (const bf16*)wp, bias, y, N, Cin, Cout, H, W, sxn, sxh, sxw, kh, kw, stride, pad, Ho, Wo, syn, syh, syw,
-           accumulate, bn_partials, bnm, bnr, bng, bnb};
+           accumulate, bn_partials, bnm, bnr, bng, bnb, syh == (long)Wo * syw && syn == (long)Ho * syh};
   if (bn_partials && accumulate) return ES_BAD_ARG;
   const int M = N * Ho * Wo;
   const dim3 g128((M + 127) / 128, Cout / 128), g64((M + 127) / 128, (Cout + 63) / 64);
@@ -728,13 +929,17 @@ int es_conv2d_bwd_data_bf16_ex(const void* dy, long syn, long syh, long syw, con
       !al16(wt))
     return ES_BAD_SHAPE;
   NTConv a{dy, (const bf16*)wt, nullptr, dx, N, Cout, Cin, Ho, Wo, syn, syh, syw, kh, kw, stride, pad, H, W, sxn, sxh,
-           sxw, accumulate, nullptr};
+           sxw, accumulate, nullptr, nullptr, nullptr, nullptr, nullptr,
+           stride == 1 && sxh == (long)W * sxw && sxn == (long)H * sxh};
   const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
   const unsigned ph = (unsigned)(stride * stride);
-  if (Cin % 128 == 0)
-    launch_nt<128, true, false>(dim3((Mq + 127) / 128, Cin / 128, ph), flags, a, stream);
-  else
-    launch_nt<64, true, false>(dim3((Mq + 127) / 128, (Cin + 63) / 64, ph), flags, a, stream);
+  if (Cin % 128 == 0) {
+    const dim3 gr((Mq + 127) / 128, Cin / 128, ph);
+    if (!launch_ring<128, true, false>(gr, flags, a, stream)) launch_nt<128, true, false>(gr, flags, a, stream);
+  } else {
+    const dim3 gr((Mq + 127) / 128, (Cin + 63) / 64, ph);
+    if (!launch_ring<64, true, false>(gr, flags, a, stream)) launch_nt<64, true, false>(gr, flags, a, stream);
+  }
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 

@@ -323,6 +323,10 @@ int es_conv2d_bf16_eligible(int Cin, int Cout, int kh, int kw);
 /* tuning knob: the workgroup count the bf16 weight gradient's automatic pixel split aims at (default 512;
    each split writes an fp32 slab of the gradient that a reduce kernel sums); returns the previous value */
 int es_set_conv_dw_target(int v);
+/* tuning knob: the bf16-map data-gradient convs and the forwards that do not widen the channels on the LDS-DMA
+ * ring kernel with 3 or 4 stages (default 3), or 0 = the register-staged gather (bit-identical); returns the
+ * previous value, or -2 (unchanged) otherwise */
+int es_set_conv_ring(int stages);
 int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);
 /* es_conv2d_pack_bf16 for n weights in ONE launch (a model's conv weights after each optimizer step):
  * table = n device-resident entries of es_conv_pack_entry_size() bytes

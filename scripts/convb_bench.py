@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--n", type=int, default=120)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--bnin", action="store_true")
+    ap.add_argument("--all-shapes", action="store_true", help="--bnin: every shape, not only conv2 / conv3")
+    ap.add_argument("--ring", type=int, default=None, help="es_set_conv_ring first (0 = the register-staged gather)")
     a = ap.parse_args()
     if a.bnin:
         return bnin_main(a)
@@ -93,11 +95,13 @@ def main():
 
 def bnin_main(a):
     lib = _lib.load()
+    if a.ring is not None:
+        lib.es_set_conv_ring(a.ring)
     s = _lib.stream()
     dev = "cuda"
     res = {}
     for name, H, Cin, Cout, k, st, p in SHAPES:
-        if "conv2" not in name and "conv3" not in name:
+        if not a.all_shapes and "conv2" not in name and "conv3" not in name:
             continue
         N = a.n
         Ho = (H + 2 * p - k) // st + 1
@@ -106,6 +110,7 @@ def bnin_main(a):
         w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
         y = torch.empty(N, Ho, Ho, Cout, device=dev, dtype=torch.bfloat16)
         dy = torch.randn_like(y)
+        dx = torch.empty_like(x)
         mean, rstd = torch.randn(Cin, device=dev) * 0.1, torch.rand(Cin, device=dev) + 0.5
         gam, bet = torch.rand(Cin, device=dev) + 0.5, torch.randn(Cin, device=dev) * 0.1
         n = Cout * Cin * k * k
@@ -123,6 +128,8 @@ def bnin_main(a):
                                 ptr(y), *ys, 0, ptr(part), 3, s),
             "fwd_bnin": lambda: call("es_conv2d_fwd_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k,
                                      st, p, ptr(y), *ys, 0, ptr(part), 3, *bn, s),
+            "dgrad": lambda: call("es_conv2d_bwd_data_bf16_ex", ptr(dy), *ys, ptr(wt), N, H, H, Cin, Cout, k, k, st, p,
+                                  ptr(dx), *xs, 0, 3, s),
             "wgrad": lambda: call("es_conv2d_bwd_weight_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys, Cout, k, k,
                                   st, p, 0, ptr(ws), ptr(dw), 0, 3, s),
             "wgrad_bnin": lambda: call("es_conv2d_bwd_weight_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys,
@@ -142,9 +149,9 @@ def bnin_main(a):
                 ts[kk].append(e0.elapsed_time(e1) * 1e3)
         res[name] = {kk: round(sorted(v)[len(v) // 2], 1) for kk, v in ts.items()}
         print(name, json.dumps(res[name]), flush=True)
-        del x, y, dy, ws
+        del x, y, dy, dx, ws
         torch.cuda.empty_cache()
-    tot = {kk: round(sum(r[kk] for r in res.values()), 1) for kk in ("fwd", "fwd_bnin", "wgrad", "wgrad_bnin")}
+    tot = {kk: round(sum(r[kk] for r in res.values()), 1) for kk in ("fwd", "fwd_bnin", "dgrad", "wgrad", "wgrad_bnin")}
     print(json.dumps({"total_us": tot}), flush=True)
 
 

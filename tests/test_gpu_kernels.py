@@ -844,3 +844,54 @@ def test_conformer_conv_pack_multi_after_first_version():
         call("es_conv2d_pack_bf16", ptr(m.pview(name)), co, ci, k, k, ptr(rp), ptr(rt), S())
         torch.cuda.synchronize()
         assert torch.equal(wp, rp) and torch.equal(wt, rt), name
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [(3, 12, 64, 128, 3, 1, 1), (2, 16, 128, 64, 1, 1, 0),
+                                                (2, 15, 64, 256, 3, 2, 1), (3, 9, 32, 96, 1, 2, 0),
+                                                (2, 24, 64, 768, 4, 4, 0), (1, 7, 96, 128, 3, 1, 1),
+                                                (2, 13, 128, 128, 3, 2, 1), (2, 10, 256, 64, 3, 1, 1),
+                                                (3, 11, 96, 32, 3, 1, 1)])
+def test_conv_ring_bit_identical(N, H, Cin, Cout, k, s, p):
+    """The bf16-map forward (plain and with BatchNorm statistics) and data-gradient convs on the LDS-DMA ring kernel
+    (es_set_conv_ring 3 / 4) against the register-staged gather (es_set_conv_ring 0): outputs, accumulated outputs
+    and statistics partials BIT-identical -- padding, strides / stride phases, pixel counts off the 128-pixel tile,
+    64- and 128-column tiles, bf16 and fp32 outputs (the widening forwards stay on the staged kernel either way:
+    Cin >= Cout cases exercise the ring forward)."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(N * 100 + H)
+    Ho = (H + 2 * p - k) // s + 1
+    M = N * Ho * Ho
+    x = torch.randn(N, H, H, Cin, device=DEV, generator=g).bfloat16()
+    w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) * 0.05
+    dy = torch.randn(N, Ho, Ho, Cout, device=DEV, generator=g).bfloat16()
+    wp = torch.empty(w.numel(), dtype=torch.bfloat16, device=DEV)
+    wt = torch.empty_like(wp)
+    call("es_conv2d_pack_bf16", ptr(w), Cout, Cin, k, k, ptr(wp), ptr(wt), S())
+    bias = torch.randn(Cout, device=DEV, generator=g)
+    xs = (H * H * Cin, H * Cin, Cin, 1)
+    ys = (Ho * Ho * Cout, Ho * Cout, Cout)
+    res = {}
+    try:
+        for ring in (0, 3, 4):
+            assert lib.es_set_conv_ring(ring) in (0, 3, 4)
+            out = {}
+            for od, fl in ((torch.bfloat16, 3), (torch.float32, 1)):
+                y = torch.zeros(N, Ho, Ho, Cout, device=DEV, dtype=od)
+                part = torch.zeros(lib.es_conv2d_bnstats_size(M, Cout), device=DEV)
+                call("es_conv2d_fwd_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), ptr(bias), Cout, k, k, s, p, ptr(y), *ys,
+                     0, ptr(part), fl, S())
+                ya = torch.randn(N, Ho, Ho, Cout, device=DEV, generator=torch.Generator(device=DEV).manual_seed(7)).to(od)
+                call("es_conv2d_fwd_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k, s, p, ptr(ya), *ys,
+                     1, None, fl, S())
+                dx = torch.zeros(N, H, H, Cin, device=DEV, dtype=od)
+                call("es_conv2d_bwd_data_bf16_ex", ptr(dy), *ys, ptr(wt), N, H, H, Cin, Cout, k, k, s, p, ptr(dx), *xs, 0,
+                     fl, S())
+                torch.cuda.synchronize()
+                out[od] = (y, part, ya, dx)
+            res[ring] = out
+    finally:
+        lib.es_set_conv_ring(3)
+    for ring in (3, 4):
+        for od in (torch.bfloat16, torch.float32):
+            for name, a, b in zip(("y", "stats", "y_acc", "dx"), res[ring][od], res[0][od]):
+                assert torch.equal(a, b), (ring, od, name, (a.float() - b.float()).abs().max().item())
