@@ -463,6 +463,10 @@ struct DWConv {
   long sxn, sxh, sxw, syn, syh, syw;
   int M, mchunk;
   const float* bnm; const float* bnr; const float* bng; const float* bnb;  // INBN: x is a BatchNorm's input
+  // branch-free loads (BUF kernels): the maps' byte extents (< 2 GiB: 32-bit buffer offsets) and the pixel walk's
+  // per-step advance 32 = wdq Wo + wdr (one wrap of wo and of ho per step at most when wdq + 1 < Ho)
+  unsigned xbytes, ybytes;
+  int wdq, wdr;
 };
 
 // pixel index -> (n, ho, wo), advanced without division
@@ -484,11 +488,33 @@ struct PixWalk {
       }
     }
   }
+  // the same +32 pixels as selects (DWConv wdq / wdr; valid while wdq + 1 < Ho): no loop, no branch
+  __device__ void advance32(int dq, int dr, int Ho, int Wo) {
+    wo += dr;
+    ho += dq;
+    const bool cw = wo >= Wo;
+    wo = cw ? wo - Wo : wo;
+    ho = cw ? ho + 1 : ho;
+    const bool ch = ho >= Ho;
+    ho = ch ? ho - Ho : ho;
+    n = ch ? n + 1 : n;
+  }
 };
+
+// 4 map elements by a range-checked buffer load (out-of-range offsets read zeros): no branch around the load
+template <typename T> __device__ __forceinline__ typename Q4<T>::t q4_buf_load(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ f32x4 q4_buf_load<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ bf16x4 q4_buf_load<bf16>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
 
 // P[split][co][k'] = sum_{pixels m of the split} dy[m][co] . im2col(x)[m][k'], tile B1 (co) x B2 (k')
 // INBN: x is a train-mode BatchNorm's input; the gathered quads get its affine map + ReLU (as the forward's)
-template <int B1, int B2, typename TX, typename TD, bool INBN = false>
+// BUF: branch-free loads (buffer loads, out-of-range offsets for the rows past the split / padding taps) and the
+// select-only pixel walk; the branchy form (maps >= 2 GiB, or maps too small for one wrap per step) otherwise
+template <int B1, int B2, typename TX, typename TD, bool INBN = false, bool BUF = true>
 __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
   constexpr int WA = (B1 == 128 && B2 == 64) ? 4 : (B1 == 64 && B2 == 128) ? 1 : 2, WB = 4 / WA;
   constexpr int F1 = B1 / WA / 16, F2 = B2 / WB / 16;  // fragments per wave along co / k'
@@ -537,26 +563,47 @@ __global__ __launch_bounds__(256) void convb_dw_kernel(DWConv a) {
   typename Q4<TD>::t v1[J1];
   typename Q4<TX>::t v2[J2];
   bool xok[J2];  // INBN: in-range im2col rows (the BatchNorm is applied in store(), padding stays zero)
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(a.dy, BUF ? a.ybytes : 0u), xr = buf_rsrc(a.x, BUF ? a.xbytes : 0u);
   auto load = [&](int mm) {
+    if constexpr (BUF) {
 #pragma unroll
-    for (int j = 0; j < J1; ++j) {
-      const int m = mm + r1 + RP1 * j;
-      v1[j] = q4_zero<TD>();
-      if (m < mend && co_ok)
-        v1[j] = q4_load(dys + (long)pw1[j].n * a.syn + (long)pw1[j].ho * a.syh + (long)pw1[j].wo * a.syw + co);
-      pw1[j].advance(32, a.Ho, a.Wo);
-    }
-#pragma unroll
-    for (int j = 0; j < J2; ++j) {
-      const int m = mm + r2 + RP2 * j;
-      v2[j] = q4_zero<TX>();
-      xok[j] = false;
-      if (m < mend && kc_ok) {
-        const int h = pw2[j].ho * a.s - a.p + ky, ww = pw2[j].wo * a.s - a.p + kx;
-        xok[j] = (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-        if (xok[j]) v2[j] = q4_load(xs + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
+      for (int j = 0; j < J1; ++j) {
+        const int m = mm + r1 + RP1 * j;
+        const bool ok = m < mend && co_ok;
+        const long e = (long)pw1[j].n * a.syn + (long)pw1[j].ho * a.syh + (long)pw1[j].wo * a.syw + co;
+        v1[j] = q4_buf_load<TD>(yr, ok ? (unsigned)(e * (long)sizeof(TD)) : ES_OOB);
+        pw1[j].advance32(a.wdq, a.wdr, a.Ho, a.Wo);
       }
-      pw2[j].advance(32, a.Ho, a.Wo);
+#pragma unroll
+      for (int j = 0; j < J2; ++j) {
+        const int m = mm + r2 + RP2 * j;
+        const int h = pw2[j].ho * a.s - a.p + ky, ww = pw2[j].wo * a.s - a.p + kx;
+        xok[j] = m < mend && kc_ok && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+        const long e = (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci;
+        v2[j] = q4_buf_load<TX>(xr, xok[j] ? (unsigned)(e * (long)sizeof(TX)) : ES_OOB);
+        pw2[j].advance32(a.wdq, a.wdr, a.Ho, a.Wo);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < J1; ++j) {
+        const int m = mm + r1 + RP1 * j;
+        v1[j] = q4_zero<TD>();
+        if (m < mend && co_ok)
+          v1[j] = q4_load(dys + (long)pw1[j].n * a.syn + (long)pw1[j].ho * a.syh + (long)pw1[j].wo * a.syw + co);
+        pw1[j].advance(32, a.Ho, a.Wo);
+      }
+#pragma unroll
+      for (int j = 0; j < J2; ++j) {
+        const int m = mm + r2 + RP2 * j;
+        v2[j] = q4_zero<TX>();
+        xok[j] = false;
+        if (m < mend && kc_ok) {
+          const int h = pw2[j].ho * a.s - a.p + ky, ww = pw2[j].wo * a.s - a.p + kx;
+          xok[j] = (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+          if (xok[j]) v2[j] = q4_load(xs + (long)pw2[j].n * a.sxn + (long)h * a.sxh + (long)ww * a.sxw + ci);
+        }
+        pw2[j].advance(32, a.Ho, a.Wo);
+      }
     }
   };
   auto store = [&](int buf) {
@@ -736,14 +783,22 @@ void launch_nt(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
   }
 }
 
+template <int B1, int B2, bool INBN, bool BUF>
+void launch_dw_b(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
+  switch (flags & 3) {
+    case 0: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, float, INBN, BUF>), grid, 256, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, float, INBN, BUF>), grid, 256, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, bf16, INBN, BUF>), grid, 256, 0, stream, a); break;
+    default: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, bf16, INBN, BUF>), grid, 256, 0, stream, a); break;
+  }
+}
+// the branch-free kernel when both maps are under 2 GiB and a 32-pixel step wraps the walk at most once per
+// dimension (es_set_conv_dw_buf 0: always the branchy one)
+int g_conv_dw_buf = 1;
 template <int B1, int B2, bool INBN = false>
 void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
-  switch (flags & 3) {
-    case 0: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, float, INBN>), grid, 256, 0, stream, a); break;
-    case 1: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, float, INBN>), grid, 256, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, float, bf16, INBN>), grid, 256, 0, stream, a); break;
-    default: hipLaunchKernelGGL((convb_dw_kernel<B1, B2, bf16, bf16, INBN>), grid, 256, 0, stream, a); break;
-  }
+  if (g_conv_dw_buf && a.xbytes && a.ybytes && a.wdq + 1 < a.Ho) launch_dw_b<B1, B2, INBN, true>(grid, flags, a, stream);
+  else launch_dw_b<B1, B2, INBN, false>(grid, flags, a, stream);
 }
 
 // bf16 gathered maps on the LDS-DMA ring (convb_nt_ring_kernel): 0 = off (the register-staged kernel), else its
@@ -799,6 +854,15 @@ int es_set_conv_ring(int v) {
   if (v != 0 && v != 3 && v != 4) return ES_BAD_ARG;
   const int old = g_conv_ring;
   g_conv_ring = v;
+  return old;
+}
+
+// tuning knob: 1 (default) = the conv weight gradient's branch-free loads / pixel walk where they apply, 0 = the
+// branchy loads everywhere (bit-identical); returns the previous value, or ES_BAD_ARG (unchanged) otherwise
+int es_set_conv_dw_buf(int v) {
+  if (v != 0 && v != 1) return ES_BAD_ARG;
+  const int old = g_conv_dw_buf;
+  g_conv_dw_buf = v;
   return old;
 }
 
@@ -978,8 +1042,11 @@ static int conv_dw_bf16_impl(const void* x, int N, int H, int W, int Cin, long s
   int chunk = (M + S0 - 1) / S0;
   chunk = (chunk + 31) / 32 * 32;
   const int S = (M + chunk - 1) / chunk;
+  const long xb = ((long)(N - 1) * sxn + (long)(H - 1) * sxh + (long)(W - 1) * sxw + Cin) * ((flags & 1) ? 2 : 4);
+  const long yb = ((long)(N - 1) * syn + (long)(Ho - 1) * syh + (long)(Wo - 1) * syw + Cout) * ((flags & 2) ? 2 : 4);
   DWConv a{x, dy, workspace, N, H, W, Cin, Ho, Wo, Cout, kh, kw, stride, pad, sxn, sxh, sxw, syn, syh, syw, M, chunk,
-           bnm, bnr, bng, bnb};
+           bnm, bnr, bng, bnb, xb < 0x7fff0000L ? (unsigned)xb : 0u, yb < 0x7fff0000L ? (unsigned)yb : 0u, 32 / Wo,
+           32 % Wo};
   int b1, b2;
   dw_tile(Cout, K, b1, b2);
   const dim3 grid((Cout + b1 - 1) / b1, (K + b2 - 1) / b2, S);

@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--bnin", action="store_true")
     ap.add_argument("--all-shapes", action="store_true", help="--bnin: every shape, not only conv2 / conv3")
     ap.add_argument("--ring", type=int, default=None, help="es_set_conv_ring first (0 = the register-staged gather)")
+    ap.add_argument("--dwbuf", type=int, default=None, help="es_set_conv_dw_buf first (0 = the branchy weight gradient)")
     a = ap.parse_args()
     if a.bnin:
         return bnin_main(a)
@@ -97,6 +98,8 @@ def bnin_main(a):
     lib = _lib.load()
     if a.ring is not None:
         lib.es_set_conv_ring(a.ring)
+    if a.dwbuf is not None:
+        lib.es_set_conv_dw_buf(a.dwbuf)
     s = _lib.stream()
     dev = "cuda"
     res = {}

@@ -895,3 +895,44 @@ def test_conv_ring_bit_identical(N, H, Cin, Cout, k, s, p):
         for od in (torch.bfloat16, torch.float32):
             for name, a, b in zip(("y", "stats", "y_acc", "dx"), res[ring][od], res[0][od]):
                 assert torch.equal(a, b), (ring, od, name, (a.float() - b.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [(3, 12, 64, 128, 3, 1, 1), (2, 16, 128, 64, 1, 1, 0),
+                                                (2, 15, 64, 256, 3, 2, 1), (3, 9, 32, 96, 1, 2, 0),
+                                                (2, 24, 64, 768, 4, 4, 0), (2, 40, 64, 64, 3, 1, 1),
+                                                (1, 4, 64, 64, 3, 1, 1)])
+def test_conv_dw_branch_free_bit_identical(N, H, Cin, Cout, k, s, p):
+    """The bf16 conv weight gradient with branch-free loads / pixel walk (es_set_conv_dw_buf 1) against the branchy
+    kernel (0): the weight gradient BIT-identical, plain and with the input BatchNorm applied by the gather, bf16 and
+    fp32 dy; maps wide and narrow (Wo < 32: several rows per 32-pixel step; a 2 x 2 map takes the branchy kernel)."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(N * 10 + H)
+    Ho = (H + 2 * p - k) // s + 1
+    M = N * Ho * Ho
+    x = torch.randn(N, H, H, Cin, device=DEV, generator=g).bfloat16()
+    mean, rstd = torch.randn(Cin, device=DEV, generator=g) * 0.1, torch.rand(Cin, device=DEV, generator=g) + 0.5
+    gam, bet = torch.rand(Cin, device=DEV, generator=g) + 0.5, torch.randn(Cin, device=DEV, generator=g) * 0.1
+    xs = (H * H * Cin, H * Cin, Cin, 1)
+    ys = (Ho * Ho * Cout, Ho * Cout, Cout)
+    ws = torch.empty(lib.es_conv2d_bwd_weight_bf16_workspace(M, Cout, Cin, k, k, 0), device=DEV)
+    res = {}
+    try:
+        for buf in (0, 1):
+            lib.es_set_conv_dw_buf(buf)
+            out = []
+            for dyt, fl in ((torch.bfloat16, 3), (torch.float32, 1)):
+                dy = torch.randn(N, Ho, Ho, Cout, device=DEV, generator=torch.Generator(device=DEV).manual_seed(3)).to(dyt)
+                dw = torch.zeros(Cout, Cin, k, k, device=DEV)
+                call("es_conv2d_bwd_weight_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys, Cout, k, k, s, p, 0,
+                     ptr(ws), ptr(dw), 0, fl, S())
+                dwb = torch.zeros_like(dw)
+                call("es_conv2d_bwd_weight_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys, Cout, k, k, s, p, 0,
+                     ptr(ws), ptr(dwb), 0, fl, ptr(mean), ptr(rstd), ptr(gam), ptr(bet), S())
+                torch.cuda.synchronize()
+                out += [dw, dwb]
+            res[buf] = out
+    finally:
+        lib.es_set_conv_dw_buf(1)
+    for a, b in zip(res[1], res[0]):
+        assert b.abs().max() > 0
+        assert torch.equal(a, b), (a - b).abs().max().item()
