@@ -43,6 +43,15 @@ __device__ __forceinline__ u32x4 f8_to_bf16x8(f32x4 a, f32x4 b) {
   return __builtin_bit_cast(u32x4, o);
 }
 
+// 4 map elements by a range-checked buffer load (out-of-range offsets read zeros): no branch around the load
+template <typename T> __device__ __forceinline__ typename Q4<T>::t q4_buf_load(__amdgpu_buffer_rsrc_t r, unsigned off);
+template <> __device__ __forceinline__ f32x4 q4_buf_load<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ bf16x4 q4_buf_load<bf16>(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+
 struct NTConv {
   const void* src;    // gathered operand (fp32 or bf16 map): x (forward) or dy (data grad), channel stride 1
   const bf16* wp;     // packed weights [Ncol][kh kw][C]
@@ -61,6 +70,9 @@ struct NTConv {
   // the output pixel m lives at out + m * osw (a dense NHWC map and no stride phase): the epilogue skips the
   // per-row (n, h, w) decomposition -- four integer divisions by run-time values per stored row
   int olin;
+  // the gathered map's and the packed weights' byte extents when both are under 2 GiB (else 0): the staged
+  // kernel's gathers are then branch-free buffer loads (out-of-range offsets read zeros)
+  unsigned sbytes, wbytes;
 };
 
 constexpr int NT_BM = 128, NT_BK = 32;
@@ -179,7 +191,8 @@ __device__ __forceinline__ void nt_tail(const NTConv& a, f32x4 (&acc)[4][BN / 32
 //             (hq + qh - kyq, wq + qw - kxq) (conv.hip conv_dx_kernel's decomposition).
 // TS / TO: element types of the gathered map and of the output map (float or bf16).
 // INBN (forward): BatchNorm + ReLU applied to every in-range gathered quad (padding stays zero).
-template <int BN, bool DX, bool STATS, typename TS, typename TO, bool INBN = false>
+// BUFL: the gathers as branch-free buffer loads (NTConv sbytes / wbytes set), else the branchy loads
+template <int BN, bool DX, bool STATS, typename TS, typename TO, bool INBN = false, bool BUFL = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void convb_nt_kernel(NTConv a) {
   constexpr int NF = BN / 32;       // 16-col fragments per wave (wave covers BN / 2 cols)
   constexpr int BJ = BN / 64;       // 16-byte weight loads per thread per step
@@ -229,6 +242,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   const int bchunk = tid & 3, brow0 = tid >> 2;
 
   const TS* src = (const TS*)a.src;
+  const __amdgpu_buffer_rsrc_t srs = buf_rsrc(a.src, a.sbytes), wrs = buf_rsrc(a.wp, a.wbytes);
   typename Q4<TS>::t ra4[4];
   u32x4 rb[BJ];
   // INBN: the step's BatchNorm channel quad and which gathered rows are in range (padding stays zero); the
@@ -246,19 +260,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
       bg = *(const f32x4*)(a.bng + cq);
       bb = *(const f32x4*)(a.bnb + cq);
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
-      ra4[j] = q4_zero<TS>();
-      aok[j] = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
-      if (aok[j]) ra4[j] = q4_load(src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
-    }
     const int btap = (by0 + tyq * bs) * a.kw + bx0 + txq * bs;
+    if constexpr (BUFL) {  // branch-free: a branch around each load made the waitcnt pass drain them at its join
 #pragma unroll
-    for (int j = 0; j < BJ; ++j) {
-      const int col = n0 + brow0 + 64 * j;
-      rb[j] = col < a.Ncol ? *(const u32x4*)(a.wp + (long)col * Kfull + btap * a.C + c0 + bchunk * 8)
-                           : u32x4{0u, 0u, 0u, 0u};
+      for (int j = 0; j < 4; ++j) {
+        const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
+        aok[j] = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
+        const long e = abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0;
+        ra4[j] = q4_buf_load<TS>(srs, aok[j] ? (unsigned)(e * (long)sizeof(TS)) : ES_OOB);
+      }
+#pragma unroll
+      for (int j = 0; j < BJ; ++j) {
+        const int col = n0 + brow0 + 64 * j;
+        const long e = (long)col * Kfull + btap * a.C + c0 + bchunk * 8;
+        rb[j] = buf_load16(wrs, col < a.Ncol ? (unsigned)(e * 2) : ES_OOB);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int h = ahb[j] + sy * tyq, ww = awb[j] + sy * txq;
+        ra4[j] = q4_zero<TS>();
+        aok[j] = (unsigned)h < (unsigned)a.Hs && (unsigned)ww < (unsigned)a.Ws;
+        if (aok[j]) ra4[j] = q4_load(src + abase[j] + (long)h * a.ssh + (long)ww * a.ssw + c0);
+      }
+#pragma unroll
+      for (int j = 0; j < BJ; ++j) {
+        const int col = n0 + brow0 + 64 * j;
+        rb[j] = col < a.Ncol ? *(const u32x4*)(a.wp + (long)col * Kfull + btap * a.C + c0 + bchunk * 8)
+                             : u32x4{0u, 0u, 0u, 0u};
+      }
     }
   };
   auto store = [&](int buf) {
@@ -501,14 +531,7 @@ struct PixWalk {
   }
 };
 
-// 4 map elements by a range-checked buffer load (out-of-range offsets read zeros): no branch around the load
-template <typename T> __device__ __forceinline__ typename Q4<T>::t q4_buf_load(__amdgpu_buffer_rsrc_t r, unsigned off);
-template <> __device__ __forceinline__ f32x4 q4_buf_load<float>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-template <> __device__ __forceinline__ bf16x4 q4_buf_load<bf16>(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
+
 
 // P[split][co][k'] = sum_{pixels m of the split} dy[m][co] . im2col(x)[m][k'], tile B1 (co) x B2 (k')
 // INBN: x is a train-mode BatchNorm's input; the gathered quads get its affine map + ReLU (as the forward's)
@@ -773,14 +796,19 @@ inline int dw_splits(int M, int Cout, int K, int splits) {
 // the _ex entry points' map element-type flags: bit 0 = the gathered / input map is bf16, bit 1 = the
 // output map (bwd_weight: dy) is bf16
 
+template <int BN, bool DX, bool STATS, bool INBN, bool BUFL>
+void launch_nt_b(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
+  switch (flags & 3) {
+    case 0: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, float, INBN, BUFL>), grid, 256, 0, stream, a); break;
+    case 1: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, float, INBN, BUFL>), grid, 256, 0, stream, a); break;
+    case 2: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, bf16, INBN, BUFL>), grid, 256, 0, stream, a); break;
+    default: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, bf16, INBN, BUFL>), grid, 256, 0, stream, a); break;
+  }
+}
 template <int BN, bool DX, bool STATS, bool INBN = false>
 void launch_nt(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
-  switch (flags & 3) {
-    case 0: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, float, INBN>), grid, 256, 0, stream, a); break;
-    case 1: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, float, INBN>), grid, 256, 0, stream, a); break;
-    case 2: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, float, bf16, INBN>), grid, 256, 0, stream, a); break;
-    default: hipLaunchKernelGGL((convb_nt_kernel<BN, DX, STATS, bf16, bf16, INBN>), grid, 256, 0, stream, a); break;
-  }
+  if (a.sbytes) launch_nt_b<BN, DX, STATS, INBN, true>(grid, flags, a, stream);
+  else launch_nt_b<BN, DX, STATS, INBN, false>(grid, flags, a, stream);
 }
 
 template <int B1, int B2, bool INBN, bool BUF>
@@ -799,6 +827,17 @@ template <int B1, int B2, bool INBN = false>
 void launch_dw(dim3 grid, int flags, const DWConv& a, hipStream_t stream) {
   if (g_conv_dw_buf && a.xbytes && a.ybytes && a.wdq + 1 < a.Ho) launch_dw_b<B1, B2, INBN, true>(grid, flags, a, stream);
   else launch_dw_b<B1, B2, INBN, false>(grid, flags, a, stream);
+}
+
+// the staged kernel's branch-free gathers: both operands' byte extents when under 2 GiB (es_set_conv_dw_buf 0:
+// the branchy loads here too)
+inline void nt_extents(NTConv& a, int flags) {
+  const long sb = ((long)(a.N - 1) * a.ssn + (long)(a.Hs - 1) * a.ssh + (long)(a.Ws - 1) * a.ssw + a.C) *
+                  ((flags & 1) ? 2 : 4);
+  const long wb = (long)a.Ncol * a.kh * a.kw * a.C * 2;
+  const bool ok = g_conv_dw_buf && sb < 0x7fff0000L && wb < 0x7fff0000L;
+  a.sbytes = ok ? (unsigned)sb : 0u;
+  a.wbytes = ok ? (unsigned)wb : 0u;
 }
 
 // bf16 gathered maps on the LDS-DMA ring (convb_nt_ring_kernel): 0 = off (the register-staged kernel), else its
@@ -857,8 +896,9 @@ int es_set_conv_ring(int v) {
   return old;
 }
 
-// tuning knob: 1 (default) = the conv weight gradient's branch-free loads / pixel walk where they apply, 0 = the
-// branchy loads everywhere (bit-identical); returns the previous value, or ES_BAD_ARG (unchanged) otherwise
+// tuning knob: 1 (default) = the register-staged conv kernels' branch-free loads (weight gradient: and pixel walk)
+// where they apply, 0 = the branchy loads everywhere (bit-identical); returns the previous value, or ES_BAD_ARG
+// (unchanged) otherwise
 int es_set_conv_dw_buf(int v) {
   if (v != 0 && v != 1) return ES_BAD_ARG;
   const int old = g_conv_dw_buf;
@@ -921,6 +961,7 @@ static int conv_fwd_bf16_impl(const void* x, int N, int H, int W, int Cin, long 
   if (bnm && (!bnr || !bng || !bnb || !al16(bnm) || !al16(bnr) || !al16(bng) || !al16(bnb))) return ES_BAD_ARG;
   NTConv a{x, (const bf16*)wp, bias, y, N, Cin, Cout, H, W, sxn, sxh, sxw, kh, kw, stride, pad, Ho, Wo, syn, syh, syw,
            accumulate, bn_partials, bnm, bnr, bng, bnb, syh == (long)Wo * syw && syn == (long)Ho * syh};
+  nt_extents(a, flags);
   if (bn_partials && accumulate) return ES_BAD_ARG;
   const int M = N * Ho * Wo;
   const dim3 g128((M + 127) / 128, Cout / 128), g64((M + 127) / 128, (Cout + 63) / 64);
@@ -995,6 +1036,7 @@ int es_conv2d_bwd_data_bf16_ex(const void* dy, long syn, long syh, long syw, con
   NTConv a{dy, (const bf16*)wt, nullptr, dx, N, Cout, Cin, Ho, Wo, syn, syh, syw, kh, kw, stride, pad, H, W, sxn, sxh,
            sxw, accumulate, nullptr, nullptr, nullptr, nullptr, nullptr,
            stride == 1 && sxh == (long)W * sxw && sxn == (long)H * sxh};
+  nt_extents(a, flags);
   const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
   const unsigned ph = (unsigned)(stride * stride);
   if (Cin % 128 == 0) {

@@ -327,8 +327,9 @@ int es_set_conv_dw_target(int v);
  * ring kernel with 3 or 4 stages (default 3), or 0 = the register-staged gather (bit-identical); returns the
  * previous value, or -2 (unchanged) otherwise */
 int es_set_conv_ring(int stages);
-/* tuning knob: 1 (default) = the bf16 conv weight gradient with branch-free (range-checked buffer) loads and pixel
- * walk where they apply, 0 = the branchy loads (bit-identical); returns the previous value, or -2 otherwise */
+/* tuning knob: 1 (default) = the register-staged bf16 conv kernels (weight gradient; forward / data gradient off the
+ * ring) with branch-free (range-checked buffer) loads and pixel walk where they apply, 0 = the branchy loads
+ * (bit-identical); returns the previous value, or -2 otherwise */
 int es_set_conv_dw_buf(int v);
 int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);
 /* es_conv2d_pack_bf16 for n weights in ONE launch (a model's conv weights after each optimizer step):

@@ -26,6 +26,13 @@ SHAPES = [("st1_conv1_256to64", 96, 256, 64, 1, 1, 0), ("st1_conv2_64_3x3", 96, 
           ("patch_64to768_k4s4", 96, 64, 768, 4, 4, 0), ("st2_res_256to512_s2", 96, 256, 512, 1, 2, 0),
           ("fcu_up_768to64", 24, 768, 64, 1, 1, 0)]
 
+# P0: timm resnet18 at 224^2 (B = 32 labeled images): every bf16 conv shape of the trunk
+P0_SHAPES = [("l1_3x3_64", 56, 64, 64, 3, 1, 1), ("l2_3x3_64to128_s2", 56, 64, 128, 3, 2, 1),
+             ("l2_3x3_128", 28, 128, 128, 3, 1, 1), ("l2_ds_64to128_s2", 56, 64, 128, 1, 2, 0),
+             ("l3_3x3_128to256_s2", 28, 128, 256, 3, 2, 1), ("l3_3x3_256", 14, 256, 256, 3, 1, 1),
+             ("l3_ds_128to256_s2", 28, 128, 256, 1, 2, 0), ("l4_3x3_256to512_s2", 14, 256, 512, 3, 2, 1),
+             ("l4_3x3_512", 7, 512, 512, 3, 1, 1), ("l4_ds_256to512_s2", 14, 256, 512, 1, 2, 0)]
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -33,6 +40,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--bnin", action="store_true")
     ap.add_argument("--all-shapes", action="store_true", help="--bnin: every shape, not only conv2 / conv3")
+    ap.add_argument("--p0", action="store_true", help="--bnin: the ResNet-18 (P0, n = 32) shapes instead")
+    ap.add_argument("--f32maps", action="store_true", help="--bnin: fp32 activation / gradient maps (flags 0)")
     ap.add_argument("--ring", type=int, default=None, help="es_set_conv_ring first (0 = the register-staged gather)")
     ap.add_argument("--dwbuf", type=int, default=None, help="es_set_conv_dw_buf first (0 = the branchy weight gradient)")
     a = ap.parse_args()
@@ -103,15 +112,17 @@ def bnin_main(a):
     s = _lib.stream()
     dev = "cuda"
     res = {}
-    for name, H, Cin, Cout, k, st, p in SHAPES:
-        if not a.all_shapes and "conv2" not in name and "conv3" not in name:
+    for name, H, Cin, Cout, k, st, p in (P0_SHAPES if a.p0 else SHAPES):
+        if not (a.all_shapes or a.p0) and "conv2" not in name and "conv3" not in name:
             continue
-        N = a.n
+        N = 32 if a.p0 else a.n
         Ho = (H + 2 * p - k) // st + 1
         M = N * Ho * Ho
-        x = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+        mdt = torch.float32 if a.f32maps else torch.bfloat16
+        fl = 0 if a.f32maps else 3
+        x = torch.randn(N, H, H, Cin, device=dev).to(mdt)
         w = torch.randn(Cout, Cin, k, k, device=dev) * 0.05
-        y = torch.empty(N, Ho, Ho, Cout, device=dev, dtype=torch.bfloat16)
+        y = torch.empty(N, Ho, Ho, Cout, device=dev, dtype=mdt)
         dy = torch.randn_like(y)
         dx = torch.empty_like(x)
         mean, rstd = torch.randn(Cin, device=dev) * 0.1, torch.rand(Cin, device=dev) + 0.5
@@ -128,15 +139,15 @@ def bnin_main(a):
         bn = (ptr(mean), ptr(rstd), ptr(gam), ptr(bet))
         fns = {
             "fwd": lambda: call("es_conv2d_fwd_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k, st, p,
-                                ptr(y), *ys, 0, ptr(part), 3, s),
+                                ptr(y), *ys, 0, ptr(part), fl, s),
             "fwd_bnin": lambda: call("es_conv2d_fwd_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k,
-                                     st, p, ptr(y), *ys, 0, ptr(part), 3, *bn, s),
+                                     st, p, ptr(y), *ys, 0, ptr(part), fl, *bn, s),
             "dgrad": lambda: call("es_conv2d_bwd_data_bf16_ex", ptr(dy), *ys, ptr(wt), N, H, H, Cin, Cout, k, k, st, p,
-                                  ptr(dx), *xs, 0, 3, s),
+                                  ptr(dx), *xs, 0, fl, s),
             "wgrad": lambda: call("es_conv2d_bwd_weight_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys, Cout, k, k,
-                                  st, p, 0, ptr(ws), ptr(dw), 0, 3, s),
+                                  st, p, 0, ptr(ws), ptr(dw), 0, fl, s),
             "wgrad_bnin": lambda: call("es_conv2d_bwd_weight_bf16_bnin_ex", ptr(x), N, H, H, Cin, *xs, ptr(dy), *ys,
-                                       Cout, k, k, st, p, 0, ptr(ws), ptr(dw), 0, 3, *bn, s),
+                                       Cout, k, k, st, p, 0, ptr(ws), ptr(dw), 0, fl, *bn, s),
         }
         ts = {kk: [] for kk in fns}
         for kk, fn in fns.items():

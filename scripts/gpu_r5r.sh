@@ -3,7 +3,7 @@
 # per-shape timing with the knob at 0 / 1 (scripts/convb_bench.py --bnin --all-shapes), S1 and P0 A/Bs
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; OUT="$GRAFT_REPO_ROOT/gpurun_out"; export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -q -p no:cacheprovider --timeout 200 --timeout-method thread -m gpu tests/test_gpu_kernels.py -k "conv_dw_branch_free or conv_ring" > "$OUT/tw.log" 2>&1; rc=$?; tail -2 "$OUT/tw.log"; [ $rc -ne 0 ] && exit 1
-for b in 0 1; do
+for b in 0 1; do  # (dw_buf also switches the staged forward / data-grad gathers)
   timeout -k 10 300 python3 scripts/convb_bench.py --bnin --all-shapes --iters 7 --dwbuf $b > "$OUT/cw$b.log" 2>&1 || { tail -3 "$OUT/cw$b.log"; exit 1; }
 done
 for f in cw0 cw1; do echo "== $f"; grep -v "^/opt\|amdgpu.ids" "$OUT/$f.log" | cut -c1-200; done

@@ -853,7 +853,8 @@ def test_conformer_conv_pack_multi_after_first_version():
                                                 (3, 11, 96, 32, 3, 1, 1)])
 def test_conv_ring_bit_identical(N, H, Cin, Cout, k, s, p):
     """The bf16-map forward (plain and with BatchNorm statistics) and data-gradient convs on the LDS-DMA ring kernel
-    (es_set_conv_ring 3 / 4) against the register-staged gather (es_set_conv_ring 0): outputs, accumulated outputs
+    (es_set_conv_ring 3 / 4) and on the staged kernel's branch-free gathers (es_set_conv_dw_buf 1) against the
+    staged kernel's branchy gathers (ring 0, dw_buf 0): outputs, accumulated outputs
     and statistics partials BIT-identical -- padding, strides / stride phases, pixel counts off the 128-pixel tile,
     64- and 128-column tiles, bf16 and fp32 outputs (the widening forwards stay on the staged kernel either way:
     Cin >= Cout cases exercise the ring forward)."""
@@ -872,8 +873,9 @@ def test_conv_ring_bit_identical(N, H, Cin, Cout, k, s, p):
     ys = (Ho * Ho * Cout, Ho * Cout, Cout)
     res = {}
     try:
-        for ring in (0, 3, 4):
+        for ring, dwb in ((0, 0), (0, 1), (3, 1), (4, 1)):  # (0, 0): the staged kernel with its branchy gathers
             assert lib.es_set_conv_ring(ring) in (0, 3, 4)
+            assert lib.es_set_conv_dw_buf(dwb) in (0, 1)
             out = {}
             for od, fl in ((torch.bfloat16, 3), (torch.float32, 1)):
                 y = torch.zeros(N, Ho, Ho, Cout, device=DEV, dtype=od)
@@ -888,13 +890,14 @@ def test_conv_ring_bit_identical(N, H, Cin, Cout, k, s, p):
                      fl, S())
                 torch.cuda.synchronize()
                 out[od] = (y, part, ya, dx)
-            res[ring] = out
+            res[(ring, dwb)] = out
     finally:
         lib.es_set_conv_ring(3)
-    for ring in (3, 4):
+        lib.es_set_conv_dw_buf(1)
+    for key in ((0, 1), (3, 1), (4, 1)):
         for od in (torch.bfloat16, torch.float32):
-            for name, a, b in zip(("y", "stats", "y_acc", "dx"), res[ring][od], res[0][od]):
-                assert torch.equal(a, b), (ring, od, name, (a.float() - b.float()).abs().max().item())
+            for name, a, b in zip(("y", "stats", "y_acc", "dx"), res[key][od], res[(0, 0)][od]):
+                assert torch.equal(a, b), (key, od, name, (a.float() - b.float()).abs().max().item())
 
 
 @pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [(3, 12, 64, 128, 3, 1, 1), (2, 16, 128, 64, 1, 1, 0),
