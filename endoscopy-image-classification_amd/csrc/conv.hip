@@ -21,6 +21,8 @@
 // implicit GEMMs (64x64 / 128x32 / 256x16 output tiles, 4x4 per thread, 16-deep K steps staged
 // through LDS) -- no bf16 rounding on the BatchNorm-coupled CNN path (BatchNorm over the whole
 // batch amplifies operand noise, the same effect as CoMatch's BatchNorm1d head).
+#include <numeric>
+
 #include "common.h"
 
 namespace {
@@ -415,9 +417,12 @@ struct RowMap {
 // VEC consecutive floats (VEC = 4: one 16-byte load)
 template <int VEC>
 __device__ __forceinline__ void ldv(const float* __restrict__ p, float (&o)[VEC]) {
-  if constexpr (VEC == 4) {
-    const f32x4 t = *(const f32x4*)p;
-    o[0] = t[0]; o[1] = t[1]; o[2] = t[2]; o[3] = t[3];
+  if constexpr (VEC == 4 || VEC == 8) {
+#pragma unroll
+    for (int h = 0; h < VEC / 4; ++h) {
+      const f32x4 t = *(const f32x4*)(p + 4 * h);
+      o[4 * h] = t[0]; o[4 * h + 1] = t[1]; o[4 * h + 2] = t[2]; o[4 * h + 3] = t[3];
+    }
   } else {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = p[j];
@@ -425,8 +430,9 @@ __device__ __forceinline__ void ldv(const float* __restrict__ p, float (&o)[VEC]
 }
 template <int VEC>
 __device__ __forceinline__ void stv(float* __restrict__ p, const float (&v)[VEC]) {
-  if constexpr (VEC == 4) {
-    *(f32x4*)p = f32x4{v[0], v[1], v[2], v[3]};
+  if constexpr (VEC == 4 || VEC == 8) {
+#pragma unroll
+    for (int h = 0; h < VEC / 4; ++h) *(f32x4*)(p + 4 * h) = f32x4{v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
   } else {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) p[j] = v[j];
@@ -438,6 +444,10 @@ __device__ __forceinline__ void ldv(const bf16* __restrict__ p, float (&o)[VEC])
   if constexpr (VEC == 4) {
     const bf16x4 t = *(const bf16x4*)p;
     o[0] = (float)t[0]; o[1] = (float)t[1]; o[2] = (float)t[2]; o[3] = (float)t[3];
+  } else if constexpr (VEC == 8) {
+    const bf16x8 t = *(const bf16x8*)p;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (float)t[j];
   } else {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) o[j] = (float)p[j];
@@ -447,6 +457,11 @@ template <int VEC>
 __device__ __forceinline__ void stv(bf16* __restrict__ p, const float (&v)[VEC]) {
   if constexpr (VEC == 4) {
     *(bf16x4*)p = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  } else if constexpr (VEC == 8) {
+    bf16x8 t;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) t[j] = (bf16)v[j];
+    *(bf16x8*)p = t;
   } else {
 #pragma unroll
     for (int j = 0; j < VEC; ++j) p[j] = (bf16)v[j];
@@ -465,6 +480,22 @@ __device__ __forceinline__ bool bn_relu_live(float x, float mu, float rs, float 
 // A thread owns VEC channels and walks every rp-th row of the block's chunk; contiguous views
 // (sn = HW * sp, every BatchNorm) take 4 rows per iteration so 4 (MODE 2: 12) loads are in flight.
 // T: element type of the maps v, dy, y (fp32 or bf16); sums in fp32.
+// eval-mode 1 / sqrt(running_var + eps), correctly rounded (the same bits in every apply kernel)
+__device__ __forceinline__ float bn_eval_rstd(float rv, float eps) {
+#pragma clang fp contract(off)
+  return __fdiv_rn(1.0f, __fsqrt_rn(rv + eps));
+}
+
+// dx of the BatchNorm backward at one element, rounding pinned (no contraction): the per-iteration and the
+// channel-stationary kernels give the same bits however the compiler schedules or hoists the per-channel terms
+__device__ __forceinline__ float bn_bwd_dx(float x, float g, float mu, float rs, float ga, float s0, float s1,
+                                           float inv) {
+#pragma clang fp contract(off)
+  const float xh = (x - mu) * rs;
+  const float t = (g - s0 * inv) - (xh * s1) * inv;
+  return (rs * ga) * t;
+}
+
 // REBUILD (MODE 2, relu): the mask rebuilt from x with gamma / beta (bn_relu_live), y not read
 template <int MODE, int VEC, typename T = float, bool REBUILD = false>
 __global__ __launch_bounds__(256) void chan_partial_kernel(const T* __restrict__ v, RowMap rm, int rows, int C,
@@ -635,7 +666,7 @@ __global__ void bn_apply_kernel(const T* __restrict__ x, int nv, int CV, const f
     if (rvar) {
       ldv<VEC>(rvar + c, rv);
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) rs[j] = 1.0f / sqrtf(rv[j] + eps);
+      for (int j = 0; j < VEC; ++j) rs[j] = bn_eval_rstd(rv[j], eps);
     } else {
       ldv<VEC>(rstd + c, rs);
     }
@@ -693,13 +724,105 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict
     ldv<VEC>(sums + c, s0);
     ldv<VEC>(sums + C + c, s1);
 #pragma unroll
-    for (int j = 0; j < VEC; ++j) {
-      const float xh = (xv[j] - mu[j]) * rs[j];
-      o[j] = rs[j] * ga[j] * (gg[j] - s0[j] * inv - xh * s1[j] * inv);
-    }
+    for (int j = 0; j < VEC; ++j) o[j] = bn_bwd_dx(xv[j], gg[j], mu[j], rs[j], ga[j], s0[j], s1[j], inv);
     stv<VEC>(dx + (long)i * VEC, o);
   }
 }
+
+// Channel-stationary forms of bn_apply_kernel / bn_bwd_apply_kernel: the launch makes the grid's thread count a
+// multiple of CV = C / VEC, so a thread's channel group never changes -- its BatchNorm parameters are loaded once
+// instead of every iteration (with an integer modulo by a run-time value), and VEC = 8 on bf16 maps gives 16-byte
+// accesses.  The same arithmetic per element: bit-identical maps.
+template <int VEC, typename T>
+__global__ __launch_bounds__(256) void bn_apply_cs_kernel(const T* __restrict__ x, int nv, int CV,
+                                                          const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                          const float* __restrict__ rvar, float eps,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, const T* __restrict__ res,
+                                                          int relu, T* __restrict__ y) {
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  const int c = (t0 % CV) * VEC;
+  float mu[VEC], ga[VEC], be[VEC], rs[VEC];
+  ldv<VEC>(mean + c, mu);
+  ldv<VEC>(gamma + c, ga);
+  ldv<VEC>(beta + c, be);
+  if (rvar) {
+    float rv[VEC];
+    ldv<VEC>(rvar + c, rv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) rs[j] = bn_eval_rstd(rv[j], eps);
+  } else {
+    ldv<VEC>(rstd + c, rs);
+  }
+  for (int i = t0; i < nv; i += stride) {
+    float xv[VEC], o[VEC];
+    ldv<VEC>(x + (long)i * VEC, xv);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = bn_affine(xv[j], mu[j], rs[j], ga[j], be[j]);
+    if (res) {
+      float rr[VEC];
+      ldv<VEC>(res + (long)i * VEC, rr);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] += rr[j];
+    }
+    if (relu) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = fmaxf(o[j], 0.f);
+    }
+    stv<VEC>(y + (long)i * VEC, o);
+  }
+}
+
+template <int VEC, typename T, bool REBUILD = false>
+__global__ __launch_bounds__(256) void bn_bwd_apply_cs_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                              const T* __restrict__ y, int relu, int nv, int CV, int rows,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ sums, T* __restrict__ dx,
+                                                              T* __restrict__ gout, const float* __restrict__ beta) {
+  const float inv = 1.0f / (float)rows;
+  const int C = CV * VEC;
+  const int t0 = blockIdx.x * blockDim.x + threadIdx.x, stride = gridDim.x * blockDim.x;
+  const int c = (t0 % CV) * VEC;
+  float mu[VEC], rs[VEC], ga[VEC], s0[VEC], s1[VEC], be[VEC];
+  ldv<VEC>(mean + c, mu);
+  ldv<VEC>(rstd + c, rs);
+  ldv<VEC>(gamma + c, ga);
+  ldv<VEC>(sums + c, s0);
+  ldv<VEC>(sums + C + c, s1);
+  if constexpr (REBUILD) ldv<VEC>(beta + c, be);
+  for (int i = t0; i < nv; i += stride) {
+    float xv[VEC], gg[VEC], o[VEC];
+    ldv<VEC>(x + (long)i * VEC, xv);
+    ldv<VEC>(dy + (long)i * VEC, gg);
+    if constexpr (REBUILD) {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (!bn_relu_live<T>(xv[j], mu[j], rs[j], ga[j], be[j])) gg[j] = 0.f;
+    } else if (relu) {
+      float yy[VEC];
+      ldv<VEC>(y + (long)i * VEC, yy);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (!(yy[j] > 0.f)) gg[j] = 0.f;
+    }
+    if (gout) stv<VEC>(gout + (long)i * VEC, gg);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) o[j] = bn_bwd_dx(xv[j], gg[j], mu[j], rs[j], ga[j], s0[j], s1[j], inv);
+    stv<VEC>(dx + (long)i * VEC, o);
+  }
+}
+
+// the channel-stationary grid: ~16,384 workgroups at most, thread count a multiple of CV
+inline int cs_grid(long nv, int CV) {
+  const long b = (nv + 255) / 256;
+  int g = (int)(b > 16384 ? 16384 : (b < 1 ? 1 : b));  // grid1d's cap
+  const int a = CV / std::gcd(CV, 256);  // workgroups per whole number of channel groups
+  g = (g + a - 1) / a * a;
+  return g;
+}
+int g_bn_cs = 1;  // es_set_bn_cs: the channel-stationary BatchNorm applies (0: the per-iteration forms)
 
 // eval-mode BatchNorm backward is an affine map: dx = g * gamma * rstd_running (not on the training
 // path; kept for completeness of the autograd surface)
@@ -1526,6 +1649,13 @@ bool map_v4(int C, const void* a, const void* b = nullptr, const void* c = nullp
 template <typename T>
 void bn_apply_launch(bool v4, const T* x, long n, int C, const float* mu, const float* rs, const float* rv, float eps,
                      const float* gamma, const float* beta, const T* res, int relu, T* y, hipStream_t stream) {
+  constexpr int CVEC = sizeof(T) == 2 ? 8 : 4;  // 16-byte map accesses
+  if (g_bn_cs && v4 && C % CVEC == 0) {
+    const long nv = n / CVEC;
+    hipLaunchKernelGGL((bn_apply_cs_kernel<CVEC, T>), cs_grid(nv, C / CVEC), 256, 0, stream, x, (int)nv, C / CVEC, mu,
+                       rs, rv, eps, gamma, beta, res, relu, y);
+    return;
+  }
   if (v4)
     hipLaunchKernelGGL((bn_apply_kernel<4, T>), grid1d(n / 4), 256, 0, stream, x, (int)(n / 4), C / 4, mu, rs, rv, eps,
                        gamma, beta, res, relu, y);
@@ -1600,6 +1730,24 @@ int bn2d_fwd_impl(const T* x, int rows, int C, const float* gamma, const float* 
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+// the backward's apply pass (dx, optional gout); true when the channel-stationary kernel took it
+template <typename T>
+bool bn_bwd_apply_cs_launch(bool v4, bool rebuild, const T* x, const T* dy, const T* y, int relu, long n, int C,
+                            int rows, const float* mean, const float* rstd, const float* gamma, const float* sums, T* dx,
+                            T* gout, const float* beta, hipStream_t stream) {
+  constexpr int CVEC = sizeof(T) == 2 ? 8 : 4;
+  if (!g_bn_cs || !v4 || C % CVEC) return false;
+  const long nv = n / CVEC;
+  const int g = cs_grid(nv, C / CVEC);
+  if (rebuild)
+    hipLaunchKernelGGL((bn_bwd_apply_cs_kernel<CVEC, T, true>), g, 256, 0, stream, x, dy, y, relu, (int)nv, C / CVEC,
+                       rows, mean, rstd, gamma, sums, dx, gout, beta);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_cs_kernel<CVEC, T, false>), g, 256, 0, stream, x, dy, y, relu, (int)nv, C / CVEC,
+                       rows, mean, rstd, gamma, sums, dx, gout, beta);
+  return true;
+}
+
 // y == null with relu: the mask rebuilt from x (train mode, no residual; beta required)
 template <typename T>
 int bn2d_bwd_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu, const float* gamma, const float* mean,
@@ -1627,7 +1775,10 @@ int bn2d_bwd_impl(const T* x, const T* y, const T* dy, int rows, int C, int relu
   ChanFin f{dbeta, dgamma, sums, nullptr, nullptr, nullptr, 0.f, 0.f, rows, C, accumulate};
   hipLaunchKernelGGL(chan_final_kernel<3>, (2 * C + 15) / 16, 256, 0, stream, workspace, G, 2 * C, f);
   const bool rebuild = relu && !y;
-  if (v4 && rebuild)
+  if (bn_bwd_apply_cs_launch<T>(v4, rebuild, x, dy, y, relu, n, C, rows, mean, rstd, gamma, sums, dx, gout,
+                                rebuild ? beta : nullptr, stream))
+    ;
+  else if (v4 && rebuild)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<4, T, true>), grid1d(n / 4), 256, 0, stream, x, dy, y, relu, (int)(n / 4),
                        C / 4, rows, mean, rstd, gamma, sums, dx, gout, beta);
   else if (rebuild)
@@ -1757,6 +1908,16 @@ extern "C" {
 
 // 1 (default): the specialised stem kernels for 3 -> 64 channel 7x7 / 2 / 3 convs on NHWC images;
 // 0: the generic implicit-GEMM kernels (bit-identical forward).  Returns the previous value.
+// tuning knob: 1 (default) = the channel-stationary BatchNorm apply kernels (parameters loaded once per thread,
+// 16-byte map accesses) where the channel count allows, 0 = the per-iteration forms (bit-identical); returns the
+// previous value, or ES_BAD_ARG (unchanged) for any other value
+int es_set_bn_cs(int v) {
+  if (v != 0 && v != 1) return ES_BAD_ARG;
+  const int old = g_bn_cs;
+  g_bn_cs = v;
+  return old;
+}
+
 int es_set_stem_kernels(int v) {
   const int old = g_stem_kernels;
   g_stem_kernels = v;

@@ -130,6 +130,7 @@ SIGNATURES = {
     "es_conv2d_bwd_weight_bf16_bnin_ex": (I, [V, I, I, I, I, L, L, L, L, V, L, L, L, I, I, I, I, I, I, V, V, I, I,
                                              V, V, V, V, V]),
     "es_chan_sum_ex": (I, [V, I, I, L, L, I, V, V, I, I, V]),
+    "es_set_bn_cs": (I, [I]),
     "es_bn2d_fwd_ex": (I, [V, I, I, V, V, V, V, V, F, F, I, V, I, V, V, V, V, I, V]),
     "es_bn2d_bwd_ex": (I, [V, V, V, I, I, I, V, V, V, I, V, F, V, V, V, V, I, V, I, V]),
     "es_bn2d_bwd_recompute_ex": (I, [V, V, I, I, V, V, V, V, V, V, V, I, V, I, V]),

@@ -439,6 +439,9 @@ int es_conv2d_bwd_weight_bf16_bnin_ex(const void* x, int N, int H, int W, int Ci
                                       const float* in_beta, hipStream_t stream);
 int es_chan_sum_ex(const void* v, int rows, int C, long sn, long sp, int HW, float* workspace, float* out,
                    int accumulate, int flags, hipStream_t stream);
+/* tuning knob: 1 (default) = the channel-stationary BatchNorm apply kernels (forward apply and the backward's dx
+ * pass), 0 = the per-iteration forms (bit-identical); returns the previous value, or -2 (unchanged) otherwise */
+int es_set_bn_cs(int v);
 int es_bn2d_fwd_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
                    float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const void* res,
                    int relu, void* y, float* mean, float* rstd, float* workspace, int flags, hipStream_t stream);

@@ -483,6 +483,52 @@ def test_bn_bwd_recompute_matches_bwd_with_y(C, fl):
     assert (y.float() == 0).any() and (y.float() > 0).any()
 
 
+@pytest.mark.parametrize("C,fl,relu,with_res", [(64, 1, 1, 1), (256, 1, 1, 0), (768, 1, 0, 0), (96, 0, 1, 1),
+                                                (512, 0, 1, 0), (12, 1, 1, 1)])
+def test_bn_channel_stationary_bit_identical(C, fl, relu, with_res):
+    """es_set_bn_cs: the channel-stationary BatchNorm apply kernels (forward apply; the backward's dx / gout pass,
+    with y and with the ReLU mask rebuilt from x) against the per-iteration forms: every output BIT-identical, bf16
+    (16-byte groups of 8) and fp32 maps, C a multiple of 8 / 4 or not (the fallback)."""
+    torch.manual_seed(C + fl)
+    N, H, W = 3, 11, 9
+    rows = N * H * W
+    lib = _lib.load()
+    dt = B16 if fl else torch.float32
+    x, dy = _rep(N, H, W, C, scale=1.5, shift=0.1).to(dt), _rep(N, H, W, C).to(dt)
+    res = _rep(N, H, W, C).to(dt) if with_res else None
+    g, b = 1 + 0.1 * torch.randn(C, device=DEV), 0.1 * torch.randn(C, device=DEV)
+    ws = torch.empty(lib.es_chan_workspace(rows, C), device=DEV)
+    out = {}
+    try:
+        for cs in (0, 1):
+            assert lib.es_set_bn_cs(cs) in (0, 1)
+            rm, rv = torch.zeros(C, device=DEV), torch.ones(C, device=DEV)
+            y, mean, rstd = torch.empty_like(x), torch.empty(C, device=DEV), torch.empty(C, device=DEV)
+            call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm), ptr(rv), None, 0.1, 1e-6, 1,
+                 ptr(res) if res is not None else None, relu, ptr(y), ptr(mean), ptr(rstd), ptr(ws), fl, S())
+            ye = torch.empty_like(x)  # eval mode: rstd from the running variance inside the apply
+            call("es_bn2d_fwd_ex", ptr(x), rows, C, ptr(g), ptr(b), ptr(rm), ptr(rv), None, 0.1, 1e-6, 0,
+                 ptr(res) if res is not None else None, relu, ptr(ye), None, None, None, fl, S())
+            dx, gout = torch.empty_like(x), torch.empty_like(x)
+            dg, db = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+            call("es_bn2d_bwd_ex", ptr(x), ptr(y), ptr(dy), rows, C, relu, ptr(g), ptr(mean), ptr(rstd), 1, ptr(rv),
+                 1e-6, ptr(dx), ptr(gout), ptr(dg), ptr(db), 0, ptr(ws), fl, S())
+            got = [y, ye, dx, gout, dg, db]
+            if relu and not with_res:
+                dx2 = torch.empty_like(x)
+                dg2, db2 = torch.zeros(C, device=DEV), torch.zeros(C, device=DEV)
+                call("es_bn2d_bwd_recompute_ex", ptr(x), ptr(dy), rows, C, ptr(g), ptr(b), ptr(mean), ptr(rstd),
+                     ptr(dx2), ptr(dg2), ptr(db2), 0, ptr(ws), fl, S())
+                got += [dx2, dg2, db2]
+            torch.cuda.synchronize()
+            out[cs] = [t.clone() for t in got]
+    finally:
+        lib.es_set_bn_cs(1)
+    names = ["y", "y_eval", "dx", "gout", "dgamma", "dbeta", "dx_recompute", "dgamma_recompute", "dbeta_recompute"]
+    for name, a, c in zip(names, out[1], out[0]):
+        assert torch.equal(a, c), (name, (a.float() - c.float()).abs().max().item())
+
+
 @pytest.mark.parametrize("relu,with_res,C", [(True, True, 64), (True, False, 256), (False, False, 128), (True, True, 6)])
 def test_bn_pool_bf16_maps_match_fp32_maps_rounded(relu, with_res, C):
     """BatchNorm (statistics pass, conv partials, eval, backward, SyncBatchNorm halves), channel sums, max /
