@@ -316,6 +316,8 @@ def run_secondary(args):
         B = args.batch if args.batch != 64 else 16
         model = NativeResNet(ResNetConfig(num_classes=23), seed=0)
         tr = SupLearning(model, device=dev)
+        if args.graph != "auto":  # auto: SupLearning's default (the forward / backward replayed as one hipGraph)
+            tr.use_graph = args.graph == "on"
 
         class _DS:
             df = None
@@ -333,7 +335,8 @@ def run_secondary(args):
         exe = tfl
         desc = (f"P0: supervised ResNet-18 step (timm resnet18, 23 classes; code/supervised.py:111-138), B={B}, "
                 f"224^2, weighted CE, Adam 1e-3, EMA 0.999; convs with channels % 32 == 0 on bf16 MFMA "
-                f"({'on' if model.conv_bf16 else 'off'}), the stem fp32")
+                f"({'on' if model.conv_bf16 else 'off'}), the stem fp32; forward / backward "
+                f"{'replayed as one hipGraph' if tr.use_graph else 'eager'}")
     else:
         from endossl.conformer import ConformerConfig, NativeConformer
         from endossl.semiformer import SemiFormer

@@ -70,20 +70,63 @@ class SupLearning:
         else:
             self.class_weights = None
 
-    def step(self, batch):
-        """batch = (images [n, 3, H, W], targets [n]) -> {"loss", "logits"} (device tensors)."""
-        images, targets = batch
+    # The forward / loss / backward of a step as one hipGraph (torch.cuda.CUDAGraph over the C-ABI launches,
+    # the conv weight-gradient side stream forked and joined inside): ResNet-18 at B=16 is host-bound eager
+    # (Python autograd walks ~250 launches a step).  Captured after GRAPH_WARM eager steps of a shape (the
+    # first versions build the conv-weight pack table; the captured step packs in one launch), then
+    # replayed; inputs are copied into the graph's own buffers.  The optimizer, EMA and LR schedule stay
+    # outside (their scalars change per step).  One process only: at world > 1 the weighted loss
+    # all-reduces inside the step.  ENDOSSL_SUP_GRAPH=0 keeps every step eager.
+    use_graph = os.environ.get("ENDOSSL_SUP_GRAPH", "1") == "1"
+    GRAPH_WARM = 2
+
+    def _compute(self, images, targets):
+        """Forward, weighted CE and its gradient, backward into model.flat_grad (no host sync)."""
         dev = self.model.flat.device
-        self._inflight.wait()
-        targets = targets.to(dev, non_blocking=True).to(torch.int64).contiguous()
-        self.model.train()
-        logits = self.model(images.to(dev, non_blocking=True))
+        logits = self.model(images)
         stats = torch.zeros(1, dtype=torch.float32, device=dev)
         dl = torch.empty_like(logits)
         weighted_ce_fwd_bwd(logits.detach(), targets, self.class_weights, dl, stats)
         self.optimizer.zero_grad()
         torch.autograd.backward([logits], [dl])
         join_wgrad_stream(dev)
+        return stats, logits.detach()
+
+    def _run_graph(self, images, targets):
+        m = self.model
+        cw = self.class_weights
+        key = (tuple(images.shape), images.dtype, tuple(targets.shape), m.flat.data_ptr(), m.flat_grad.data_ptr(),
+               cw.data_ptr() if cw is not None else 0)
+        if getattr(self, "_gkey", None) != key:
+            self._graph, self._gkey, self._gwarm = None, key, 0
+        if self._graph is None:
+            if self._gwarm < self.GRAPH_WARM:
+                self._gwarm += 1
+                return self._compute(images, targets)
+            gin = (images.clone(), targets.clone())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                gout = self._compute(*gin)
+            self._graph, self._gin, self._gout = g, gin, gout
+        else:
+            for dst, src in zip(self._gin, (images, targets)):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src, non_blocking=True)
+        self._graph.replay()
+        return self._gout
+
+    def step(self, batch):
+        """batch = (images [n, 3, H, W], targets [n]) -> {"loss", "logits"} (device tensors)."""
+        images, targets = batch
+        dev = self.model.flat.device
+        self._inflight.wait()
+        targets = targets.to(dev, non_blocking=True).to(torch.int64).contiguous()
+        images = images.to(dev, non_blocking=True)
+        self.model.train()
+        if self.use_graph and dist.world_size() == 1 and images.is_cuda:
+            stats, logits = self._run_graph(images, targets)
+        else:
+            stats, logits = self._compute(images, targets)
         gscale = dist.allreduce_sum_(self.model.flat_grad)
         ema = self.ema_model
         self.optimizer.step(ema_flat=ema.ema.flat if ema is not None else None,

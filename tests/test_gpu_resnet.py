@@ -123,3 +123,48 @@ def test_suplearning_step_vs_oracle():
             continue
         assert (v.cpu() - traj.p[k].detach()).abs().max().item() <= 2 * 2e-3 + 1e-6, k
         assert (esd[k].cpu() - traj.ema[k]).abs().max().item() <= 1e-3 * 4e-3 + 1e-6, k
+
+
+def test_suplearning_graph_replay_bit_identical():
+    """SupLearning.use_graph: the forward / loss / backward captured once (after GRAPH_WARM eager steps) and
+    replayed, new batches copied into the graph's inputs, against every step eager -- losses, logits,
+    parameters, EMA and BatchNorm buffers BIT-identical over six steps (bf16 convs; the captured steps
+    pack the conv weights themselves)."""
+    from endossl.supervised import SupLearning
+    from endossl.utils import AttrDict
+    g = torch.Generator().manual_seed(11)
+    batches = [(torch.randn(8, 3, 64, 64, generator=g), torch.randint(0, 23, (8,), generator=g)) for _ in range(6)]
+
+    class _DS:
+        df = None
+
+    class _DL(list):
+        dataset = _DS()
+
+    runs = {}
+    for graph in (False, True):
+        m, _ = _model(seed=6, conv="bf16")
+        tr = SupLearning(m, opt_func="Adam", lr=1e-3, device=DEV)
+        tr.use_graph = graph
+        tr.get_dataloader(_DL(batches), None, None)
+        tr.get_config(AttrDict(DATA=AttrDict(BATCH_SIZE=8, IMG_SIZE=64, TARGET_NAME="target"),
+                               MODEL=AttrDict(NAME="resnet18", NUM_CLASSES=23, MARGIN="None", IS_TRIPLET=False),
+                               TRAIN=AttrDict(USE_EMA=True, EMA_DECAY=0.999, BASE_LR=1e-3, CLS_WEIGHT=False,
+                                              EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4,
+                                              LR_DECAY=0.8, SCH_NAME="const", FREQ_EVAL=1)))
+        tr.class_weights = torch.linspace(0.5, 2.0, 23).to(DEV)
+        losses, logits = [], []
+        for x, y in batches:
+            out = tr.step((x.to(DEV), y.to(DEV)))
+            losses.append(out["loss"].item())
+            logits.append(out["logits"].cpu().clone())
+        assert (getattr(tr, "_graph", None) is not None) == graph
+        runs[graph] = (losses, logits, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
+                       {k: v.detach().cpu().clone() for k, v in tr.ema_model.ema.state_dict().items()})
+    (le, ge, se, ee), (lg, gg, sg, eg) = runs[False], runs[True]
+    assert le == lg, (le, lg)
+    for i, (a, b) in enumerate(zip(ge, gg)):
+        assert torch.equal(a, b), i
+    for k in se:
+        assert torch.equal(se[k], sg[k]), k
+        assert torch.equal(ee[k], eg[k]), k
