@@ -8,9 +8,11 @@ shortcut, ReLU) -> global average pool -> fc).  `model(x) -> logits`, the timm s
 and order), so checkpoints interchange.
 
 MI355X layout (as NativeConformer, whose parameter plumbing it shares): parameters in one flat fp32
-buffer, NHWC fp32 maps, every conv an implicit GEMM (bf16 operands for channel counts % 32 == 0 --
+buffer, NHWC maps, every conv an implicit GEMM (bf16 operands for channel counts % 32 == 0 --
 all but the 3-channel stem; `set_conv_precision("fp32")` for parity), BatchNorm with the residual add
-and ReLU fused into its apply pass, SyncBatchNorm at N > 1 (as the Conformer).
+and ReLU fused into its apply pass, SyncBatchNorm at N > 1 (as the Conformer).  With the bf16 convs
+the activation and gradient maps after the stem's max-pool are bf16 (map_bf16; the stem and BatchNorm
+statistics stay fp32, ENDOSSL_MAP_BF16=0 keeps fp32 maps): every conv after the stem is bf16-eligible.
 """
 import math
 
@@ -18,8 +20,8 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .conformer import (BN_EPS_STEM, CONV_BF16, GRAD_SINKS, NativeConformer, _ConvHeadFn, _GradSink, _Map, _MaxPoolFn,
-                        _join_queued, _rup, bn, bn_conv, conv)
+from .conformer import (BN_EPS_STEM, CONV_BF16, GRAD_SINKS, MAP_BF16, NativeConformer, _ConvHeadFn, _GradSink, _Map,
+                        _map_dtype, _MaxPoolFn, _join_queued, _rup, bn, bn_conv, conv)
 
 BN_EPS = 1e-5  # timm BasicBlock norm_layer = nn.BatchNorm2d (default eps)
 
@@ -102,6 +104,12 @@ class NativeResNet(NativeConformer):
         self.conv_bf16 = CONV_BF16
 
     @property
+    def map_bf16(self):
+        """bf16 activation / gradient maps after the stem's max-pool (every later conv has channel counts
+        % 32 == 0, so all of them run on the bf16 kernels)."""
+        return bool(self.conv_bf16 and MAP_BF16)
+
+    @property
     def fc(self):  # a real submodule here (timm's classifier, IS_FREEZE's trainable part)
         return self._modules["fc"]
 
@@ -139,8 +147,8 @@ class NativeResNet(NativeConformer):
         on_tape = torch.is_grad_enabled() and self.training
         frozen = getattr(self, "frozen_trunk", False)
         anchor = self._anchor if (on_tape and not frozen) else None
-        h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor)
-        h = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1)
+        h = conv(self, x, img, "conv1.weight", None, 64, 7, 2, 3, anchor=anchor, out_dtype=torch.float32)
+        h = _MaxPoolFn.apply(bn(self, h, "bn1.", eps=BN_EPS_STEM, relu=True), 3, 2, 1, _map_dtype(self))
         for pre, inp, planes, stride, ds in cfg.blocks():
             h = self._block(h, pre, inp, planes, stride, ds)
         head_anchor = self._anchor if (on_tape and frozen) else None

@@ -12,12 +12,15 @@ reference's supervised trainer (BASELINE configs[0]).
                                 reduction='mean') (`ce_loss` type 'none', code/loss.py:118), Adam(wd 0,
                                 code/optimizer.py:13-53), EMA over every state entry (code/ema.py:51-59).
 bf16=True applies the device's rounding points: the operands of every conv with both channel counts
-multiples of 32 (conformer_ref.conv2d), i.e. all but the stem.
+multiples of 32 (conformer_ref.conv2d), i.e. all but the stem.  maps=True (with bf16) adds the device's
+bf16 activation / gradient maps (resnet.NativeResNet.map_bf16), as conformer_ref's bf16_maps: the
+max-pooled stem map, every BatchNorm (+ residual) (+ ReLU) output and the gradient arriving at each is
+rounded to bf16; BatchNorms take their batch statistics from the conv's fp32 output.
 """
 import torch
 import torch.nn.functional as F
 
-from .conformer_ref import conv2d, is_buffer
+from .conformer_ref import _bn_map, _RoundMap, conv2d, is_buffer
 from .ref import ema_update
 
 BN_EPS = 1e-5
@@ -41,16 +44,28 @@ def _bn(x, p, bufs, pre, train):
     return y
 
 
-def resnet18_forward(p, bufs, x, train=True, bf16=False):
-    """timm ResNet.forward (forward_features + global pool + fc)."""
-    h = F.max_pool2d(F.relu(_bn(F.conv2d(x, p["conv1.weight"], stride=2, padding=3), p, bufs, "bn1.", train)), 3, 2, 1)
+def resnet18_forward(p, bufs, x, train=True, bf16=False, maps=False):
+    """timm ResNet.forward (forward_features + global pool + fc); maps: the device's bf16 maps."""
+    maps = bool(maps and bf16)
+    if maps:
+        rm = _RoundMap.apply
+
+        def bn(y, pre):
+            return _bn_map(y, p, bufs, pre, BN_EPS, train)
+    else:
+        def rm(v):
+            return v
+
+        def bn(y, pre):
+            return _bn(y, p, bufs, pre, train)
+    h = rm(F.max_pool2d(F.relu(_bn(F.conv2d(x, p["conv1.weight"], stride=2, padding=3), p, bufs, "bn1.", train)),
+                        3, 2, 1))
     for pre, _, _, stride, ds in blocks():
-        o = F.relu(_bn(conv2d(h, p[pre + "conv1.weight"], stride=stride, padding=1, bf16=bf16), p, bufs,
-                       pre + "bn1.", train))
-        o = _bn(conv2d(o, p[pre + "conv2.weight"], padding=1, bf16=bf16), p, bufs, pre + "bn2.", train)
-        sc = _bn(conv2d(h, p[pre + "downsample.0.weight"], stride=stride, bf16=bf16), p, bufs, pre + "downsample.1.",
-                 train) if ds else h
-        h = F.relu(o + sc)
+        o = rm(F.relu(bn(conv2d(h, p[pre + "conv1.weight"], stride=stride, padding=1, bf16=bf16), pre + "bn1.")))
+        o = bn(conv2d(o, p[pre + "conv2.weight"], padding=1, bf16=bf16), pre + "bn2.")
+        sc = rm(bn(conv2d(h, p[pre + "downsample.0.weight"], stride=stride, bf16=bf16), pre + "downsample.1.")) \
+            if ds else h
+        h = rm(F.relu(o + sc))
     return F.linear(F.adaptive_avg_pool2d(h, 1).flatten(1), p["fc.weight"], p["fc.bias"])
 
 

@@ -6,7 +6,8 @@ unpinned -- timm is absent and no reference fixture holds a ResNet output): with
 logits within 1e-3 of scale and every gradient within 2e-3 |g| + 4x the fp32 oracle's own distance from
 fp64 (BatchNorm-amplified summation order); with the default bf16 convs the
 device within twice the bf16-contract emulation's distance from fp32 (the criterion of
-test_gpu_conformer.py: BatchNorm passes the rounding flips of the device's own conv inputs on).
+test_gpu_conformer.py: BatchNorm passes the rounding flips of the device's own conv inputs on); the
+emulation rounds the maps where the device stores them bf16 (NativeResNet.map_bf16).
 SupLearning.step against the oracle's step: loss, EMA and BatchNorm buffers, parameters after Adam.
 """
 import pytest
@@ -37,7 +38,7 @@ def test_resnet18_forward_backward_vs_oracle(conv):
         p = {k: v.clone().to(dt).requires_grad_(True) for k, v in state.items() if not is_buffer(k)}
         bufs = {k: (v.clone().to(dt) if v.is_floating_point() else v.clone()) for k, v in state.items()
                 if is_buffer(k)}
-        out = rr.resnet18_forward(p, bufs, x.to(dt), train=True, bf16=bf is True and conv == "bf16")
+        out = rr.resnet18_forward(p, bufs, x.to(dt), train=True, bf16=bf is True and conv == "bf16", maps=m.map_bf16)
         res[bf] = (out, p, bufs)
     m.train()
     m.flat_grad.zero_()
