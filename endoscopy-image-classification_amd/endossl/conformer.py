@@ -272,6 +272,34 @@ class _Map:
 CONF_TN_SHARE = 0.5
 
 
+# a transformer block's four weight gradients (fc2, fc1, proj, qkv) as ONE es_gemm_tn_big_grouped launch (384 x 192
+# tiles, split-K over the tokens) plus one reduce, issued on the side stream once the block's last data gradient
+# is made -- instead of four es_gemm_tn launches on the 128 x 128 tile (Conformer-B / 384: 938 us of weight
+# gradients per block alone on the chip); sized to CONF_TN_SHARE of the CUs beside the branch streams
+CONF_TN_GROUPED = True
+
+
+def _wgrad_grouped(m, probs, M, target, k):
+    """One es_gemm_tn_big_grouped launch (+ its reduce) on the current stream over probs = [(dy, N1, x, N2,
+    weight name, bias name)]: out / bias gradients overwritten (as es_gemm_tn with accumulate 0)."""
+    from .vit import _TNProblem
+    lib = _lib.load()
+    n = len(probs)
+    tab = (_TNProblem * n)()
+    for e, (dy, N1, x, N2, wname, bname) in zip(tab, probs):
+        e.dy, e.x, e.out = ptr(dy), ptr(x), ptr(m.gview(wname))
+        e.bias_out = ptr(m.gview(bname)) if bname else None
+        e.M, e.N1, e.N2, e.ld1, e.ld2 = M, N1, N2, N1, N2
+    need = lib.es_gemm_tn_big_grouped_workspace(ctypes.byref(tab), n, target)
+    ws = m.bwd_scratch(f"tn_grouped_ws/{k}", (max(int(need), 1),), torch.float32)
+    raw = ctypes.create_string_buffer(lib.es_gemm_tn_big_grouped_table_bytes(n))
+    dims = (ctypes.c_int * 3)()
+    rc = lib.es_gemm_tn_big_grouped_prepare(ctypes.byref(tab), n, target, ptr(ws), ws.numel(), raw, dims)
+    if rc != 0:
+        raise _lib.EndosslLibraryError(f"es_gemm_tn_big_grouped_prepare: status {rc}")
+    call("es_gemm_tn_big_grouped", raw, n, dims, _s())
+
+
 def _tn_splits(M, N1, N2):
     """0: es_gemm_tn sizes the split-K for the kernel it picks (as the ViT engine, Engine._tn_splits)."""
     return 0
@@ -914,7 +942,15 @@ class _BlockFn(torch.autograd.Function):
         wt, pv, gv = m.wt, m.pview, m.gview
         ws_ln = torch.empty(2 * 1024 * D, device=dev)
 
+        # the grouped launch's shapes: every N1 a multiple of 384, every N2 of 192; rows [M, Mp) of every
+        # operand zero (h1 / o / h2 / act zero-padded in the forward, the dy scratch zeroed once), Mp >= M + 63
+        grouped = (CONF_TN_GROUPED and xt.is_cuda and D % 384 == 0 and Hd % 384 == 0 and Mp >= _rup(M, 64))
+        probs = []
+
         def wgrad(dy, N1, x, N2, wname, bname):
+            if grouped:
+                probs.append((dy, N1, x, N2, wname, bname))
+                return
             sp = _tn_splits(M, N1, N2)
             if side is not None and CONF_TN_SHARE < 1.0 and M >= 65536 and N1 % 384 == 0 and N2 % 192 == 0:
                 # beside the branch streams: the 384 x 192 tile on a share of the CUs (as Engine.TN_SHARE)
@@ -951,6 +987,13 @@ class _BlockFn(torch.autograd.Function):
         call("es_gemm_nt", EPI_BF16, ptr(dqkv), 3 * D, ptr(wt[pre + "attn.qkv.weight"]), 3 * D, None, ptr(dh2), D,
              None, None, 0, M, D, 3 * D, 0, s)
         wgrad(dqkv, 3 * D, h1, D, pre + "attn.qkv.weight", pre + "attn.qkv.bias")
+        if probs:
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            target = max(1, int(ncu * CONF_TN_SHARE)) if side is not None else ncu
+            if side is not None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                _wgrad_grouped(m, probs, M, target, k)
         dx = _zero_pad(torch.empty(Mp, D, device=dev), M)  # returned to autograd: fresh
         call("es_layernorm_bwd_b16", ptr(dh2), D, ptr(xt), D, ptr(mean1), ptr(rstd1), ptr(pv(pre + "norm1.weight")),
              ptr(dxm), D, ptr(dx), D, None, 0, ptr(gv(pre + "norm1.weight")), ptr(gv(pre + "norm1.bias")),

@@ -1103,3 +1103,45 @@ def test_conv_weight_grads_on_side_stream_match_serial(golden):
         cnt = int(torch.tensor(sh).prod().item()) if len(sh) else 1
         assert torch.equal(grads[True][o:o + cnt], grads[False][o:o + cnt]), n
     torch.testing.assert_close(grads[True], grads[False], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("side", [True, False])
+def test_block_weight_grads_grouped_match_per_linear(side):
+    """conformer.CONF_TN_GROUPED: a transformer block's four weight gradients (fc2, fc1, proj, qkv) as one
+    es_gemm_tn_big_grouped launch + reduce (384 x 192 tiles, split-K over the tokens) against the four
+    es_gemm_tn launches -- D = 768, T = 577 (the S1 shape), on the side stream beside the branch streams and
+    serial.  Same products, another split-K summation order: the Linear weight / bias gradients within fp32
+    rounding of |g|, every other gradient (convs, LayerNorm, BatchNorm, tokens) bit-identical."""
+    from endossl import conformer as cf
+    from endossl.conformer import ConformerConfig, NativeConformer
+    kw = dict(img_size=384, patch=16, base_channel=16, channel_ratio=1, embed_dim=768, depth=3, heads=12,
+              num_classes=23)
+    m = NativeConformer(ConformerConfig(**kw), seed=3).to(DEV)
+    x = torch.randn(3, 3, 384, 384, generator=torch.Generator().manual_seed(4)).to(DEV)
+    g = torch.Generator().manual_seed(5)
+    m.train()
+    grads, w = {}, None
+    saved = cf.CONF_TN_GROUPED, cf.CONV_DW_SIDE
+    try:
+        cf.CONV_DW_SIDE = side
+        for grouped in (False, True):
+            cf.CONF_TN_GROUPED = grouped
+            hc, ht = m(x)
+            if w is None:
+                w = (torch.randn(hc.shape, generator=g).to(DEV), torch.randn(ht.shape, generator=g).to(DEV))
+            m.flat_grad.zero_()
+            (hc * w[0]).sum().add((ht * w[1]).sum()).backward()
+            grads[grouped] = m.flat_grad.clone()
+    finally:
+        cf.CONF_TN_GROUPED, cf.CONV_DW_SIDE = saved
+    lin = [n for n, _, k in m.layout if k == "p" and (".attn.qkv." in n or ".attn.proj." in n or ".mlp." in n)]
+    assert len(lin) == 24
+    mask = torch.zeros_like(grads[True], dtype=torch.bool)
+    for n in lin:
+        o, sh = m.offs[n], m.shapes[n]
+        cnt = int(torch.tensor(sh).prod().item())
+        a, b = grads[True][o:o + cnt], grads[False][o:o + cnt]
+        assert torch.isfinite(a).all(), n
+        assert (a - b).abs().max().item() <= 2e-5 * b.abs().max().item() + 1e-7, n
+        mask[o:o + cnt] = True
+    assert torch.equal(grads[True][~mask], grads[False][~mask])
