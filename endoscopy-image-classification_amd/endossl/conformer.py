@@ -275,8 +275,11 @@ CONF_TN_SHARE = 0.5
 # a transformer block's four weight gradients (fc2, fc1, proj, qkv) as ONE es_gemm_tn_big_grouped launch (384 x 192
 # tiles, split-K over the tokens) plus one reduce, issued on the side stream once the block's last data gradient
 # is made -- instead of four es_gemm_tn launches on the 128 x 128 tile (Conformer-B / 384: 938 us of weight
-# gradients per block alone on the chip); sized to CONF_TN_SHARE of the CUs beside the branch streams
-CONF_TN_GROUPED = True
+# gradients per block alone on the chip); sized to CONF_TN_SHARE of the CUs beside the branch streams.  Off: S1
+# wall neutral (126.5 vs 126.6 ms, the side stream already hid the per-Linear launches), and at one split per tile
+# (96 tiles on a 128-workgroup share) its fp32 chains over 36,928 tokens put the proj / qkv weight gradients at
+# 1.05-1.16e-5 of the exact product of the device's own inputs, above tests/test_gpu_s1_blocks.py's 1e-5 bar
+CONF_TN_GROUPED = False
 
 
 def _wgrad_grouped(m, probs, M, target, k):
