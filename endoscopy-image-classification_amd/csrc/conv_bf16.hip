@@ -847,6 +847,12 @@ inline void nt_extents(NTConv& a, int flags) {
 // reductions, FCUUp: 146 vs 163 us at stage 1's conv1); the widening 1 x 1 forwards (conv3, the strided residual
 // conv) lose 5-15 % on it (a 2-8-step K loop cannot use the ring; the staged kernel's 32 KiB fit more tiles)
 int g_conv_ring = 3;
+// the 128-channel tile leaves most CUs idle on a small map (P0's layer 4: 784 pixels x 512 channels = 28
+// workgroups over a 4,608-deep reduction): below g_conv_small workgroups the 64-channel tile runs instead
+// (twice the workgroups, the same per-element reduction order); es_set_conv_small, 0 = off
+static int g_conv_small = 128;
+static inline bool conv_small_grid(long wgs) { return wgs < g_conv_small; }
+
 
 template <int BN, bool DX, bool STATS, int NST>
 void launch_ring_n(dim3 grid, int flags, const NTConv& a, hipStream_t stream) {
@@ -903,6 +909,16 @@ int es_set_conv_dw_buf(int v) {
   if (v != 0 && v != 1) return ES_BAD_ARG;
   const int old = g_conv_dw_buf;
   g_conv_dw_buf = v;
+  return old;
+}
+
+// tuning knob: a bf16 conv forward / data gradient whose 128-channel tiling would launch fewer than `wgs`
+// workgroups runs on the 64-channel tile (default 128; 0 = never; bit-identical); returns the previous value,
+// or -2 (unchanged) for a negative value
+int es_set_conv_small(int wgs) {
+  if (wgs < 0) return ES_BAD_ARG;
+  const int old = g_conv_small;
+  g_conv_small = wgs;
   return old;
 }
 
@@ -965,7 +981,7 @@ static int conv_fwd_bf16_impl(const void* x, int N, int H, int W, int Cin, long 
   if (bn_partials && accumulate) return ES_BAD_ARG;
   const int M = N * Ho * Wo;
   const dim3 g128((M + 127) / 128, Cout / 128), g64((M + 127) / 128, (Cout + 63) / 64);
-  if (Cout % 128 == 0) {
+  if (Cout % 128 == 0 && !conv_small_grid((long)g128.x * g128.y)) {
     if (bn_partials) launch_fwd<128, true>(g128, flags, a, stream);
     else launch_fwd<128, false>(g128, flags, a, stream);
   } else {
@@ -1039,7 +1055,7 @@ int es_conv2d_bwd_data_bf16_ex(const void* dy, long syn, long syh, long syw, con
   nt_extents(a, flags);
   const int Mq = N * ((H + stride - 1) / stride) * ((W + stride - 1) / stride);  // largest phase
   const unsigned ph = (unsigned)(stride * stride);
-  if (Cin % 128 == 0) {
+  if (Cin % 128 == 0 && !conv_small_grid((long)((Mq + 127) / 128) * (Cin / 128) * ph)) {
     const dim3 gr((Mq + 127) / 128, Cin / 128, ph);
     if (!launch_ring<128, true, false>(gr, flags, a, stream)) launch_nt<128, true, false>(gr, flags, a, stream);
   } else {

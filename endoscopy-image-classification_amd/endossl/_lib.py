@@ -100,6 +100,7 @@ SIGNATURES = {
     "es_conv_pack_entry_size": (I, []),
     "es_set_conv_ring": (I, [I]),
     "es_set_conv_dw_buf": (I, [I]),
+    "es_set_conv_small": (I, [I]),
     "es_conv2d_pack_bf16_multi": (I, [V, I, L, V]),
     "es_conv2d_fwd_bf16": (I, [V, I, I, I, I, L, L, L, L, V, V, I, I, I, I, I, V, L, L, L, I, V]),
     "es_conv2d_bwd_data_bf16": (I, [V, L, L, L, V, I, I, I, I, I, I, I, I, I, V, L, L, L, L, I, V]),

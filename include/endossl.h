@@ -331,6 +331,10 @@ int es_set_conv_ring(int stages);
  * ring) with branch-free (range-checked buffer) loads and pixel walk where they apply, 0 = the branchy loads
  * (bit-identical); returns the previous value, or -2 otherwise */
 int es_set_conv_dw_buf(int v);
+/* tuning knob: a bf16 conv forward / data gradient whose 128-channel tiling would launch fewer than `wgs`
+ * workgroups (default 128; 0 = never) runs on the 64-channel tile: twice the workgroups on small maps, the same
+ * per-element reduction order (bit-identical); returns the previous value, or -2 (unchanged) for wgs < 0 */
+int es_set_conv_small(int wgs);
 int es_conv2d_pack_bf16(const float* w, int Cout, int Cin, int kh, int kw, void* wp, void* wt, hipStream_t stream);
 /* es_conv2d_pack_bf16 for n weights in ONE launch (a model's conv weights after each optimizer step):
  * table = n device-resident entries of es_conv_pack_entry_size() bytes

@@ -900,6 +900,51 @@ def test_conv_ring_bit_identical(N, H, Cin, Cout, k, s, p):
                 assert torch.equal(a, b), (key, od, name, (a.float() - b.float()).abs().max().item())
 
 
+@pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [(16, 7, 512, 512, 3, 1, 1), (16, 14, 256, 512, 3, 2, 1),
+                                                (16, 14, 256, 512, 1, 2, 0), (16, 14, 256, 256, 3, 1, 1),
+                                                (3, 12, 128, 128, 3, 1, 1)])
+def test_conv_small_grid_tile_bit_identical(N, H, Cin, Cout, k, s, p):
+    """es_set_conv_small: a bf16 conv forward (plain, with BatchNorm statistics, accumulating) and data gradient
+    whose 128-channel tiling launches few workgroups (P0's layer-3 / layer-4 shapes at B = 16) on the 64-channel
+    tile, against the 128-channel tile: every output and statistics partial BIT-identical."""
+    lib = _lib.load()
+    g = torch.Generator(device=DEV).manual_seed(N * 31 + H)
+    Ho = (H + 2 * p - k) // s + 1
+    M = N * Ho * Ho
+    x = torch.randn(N, H, H, Cin, device=DEV, generator=g).bfloat16()
+    w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) * 0.05
+    dy = torch.randn(N, Ho, Ho, Cout, device=DEV, generator=g).bfloat16()
+    wp = torch.empty(w.numel(), dtype=torch.bfloat16, device=DEV)
+    wt = torch.empty_like(wp)
+    call("es_conv2d_pack_bf16", ptr(w), Cout, Cin, k, k, ptr(wp), ptr(wt), S())
+    bias = torch.randn(Cout, device=DEV, generator=g)
+    xs = (H * H * Cin, H * Cin, Cin, 1)
+    ys = (Ho * Ho * Cout, Ho * Cout, Cout)
+    res = {}
+    try:
+        for small in (0, 1 << 20):  # 0: always the 128-channel tile; huge: the 64-channel tile wherever it applies
+            assert lib.es_set_conv_small(small) >= 0
+            out = []
+            for od, fl in ((torch.bfloat16, 3), (torch.float32, 1)):
+                y = torch.zeros(N, Ho, Ho, Cout, device=DEV, dtype=od)
+                part = torch.zeros(lib.es_conv2d_bnstats_size(M, Cout), device=DEV)
+                call("es_conv2d_fwd_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), ptr(bias), Cout, k, k, s, p, ptr(y), *ys,
+                     0, ptr(part), fl, S())
+                ya = torch.randn(N, Ho, Ho, Cout, device=DEV, generator=torch.Generator(device=DEV).manual_seed(7)).to(od)
+                call("es_conv2d_fwd_bf16_ex", ptr(x), N, H, H, Cin, *xs, ptr(wp), None, Cout, k, k, s, p, ptr(ya), *ys,
+                     1, None, fl, S())
+                dx = torch.zeros(N, H, H, Cin, device=DEV, dtype=od)
+                call("es_conv2d_bwd_data_bf16_ex", ptr(dy), *ys, ptr(wt), N, H, H, Cin, Cout, k, k, s, p, ptr(dx), *xs, 0,
+                     fl, S())
+                torch.cuda.synchronize()
+                out += [y, part, ya, dx]
+            res[small] = out
+    finally:
+        lib.es_set_conv_small(128)
+    for i, (a, b) in enumerate(zip(res[1 << 20], res[0])):
+        assert torch.equal(a, b), (i, (a.float() - b.float()).abs().max().item())
+
+
 @pytest.mark.parametrize("N,H,Cin,Cout,k,s,p", [(3, 12, 64, 128, 3, 1, 1), (2, 16, 128, 64, 1, 1, 0),
                                                 (2, 15, 64, 256, 3, 2, 1), (3, 9, 32, 96, 1, 2, 0),
                                                 (2, 24, 64, 768, 4, 4, 0), (2, 40, 64, 64, 3, 1, 1),
