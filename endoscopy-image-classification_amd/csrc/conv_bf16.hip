@@ -750,16 +750,35 @@ struct ConvPackEntry {
   bf16 *wp, *wt;
   int Cout, Cin, T, pad;
 };
-__global__ void convb_pack_multi_kernel(const ConvPackEntry* __restrict__ tab) {
+// Stores coalesced on both images: wp in its own element order (each thread gathers its source element: the
+// rows of w it reads are L2-resident), and wt -- w viewed as [Cout][K = Cin T] transposed to [K][Cout] -- through
+// 64 x 64 LDS tiles.  The same bf16 values as convb_pack_kernel.
+__global__ __launch_bounds__(256) void convb_pack_multi_kernel(const ConvPackEntry* __restrict__ tab) {
+  __shared__ float tile[64][65];
   const ConvPackEntry e = tab[blockIdx.y];
-  const long n = (long)e.Cout * e.Cin * e.T;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int tap = (int)(i % e.T);
-    const long t2 = i / e.T;
-    const int ci = (int)(t2 % e.Cin), co = (int)(t2 / e.Cin);
-    const bf16 v = (bf16)e.w[i];
-    if (e.wp) e.wp[((long)co * e.T + tap) * e.Cin + ci] = v;
-    if (e.wt) e.wt[((long)ci * e.T + tap) * e.Cout + co] = v;
+  const int K = e.Cin * e.T;
+  const long n = (long)e.Cout * K;
+  if (e.wp) {
+    for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+      const int ci = (int)(i % e.Cin);  // i = (co T + tap) Cin + ci
+      const long t2 = i / e.Cin;
+      const int tap = (int)(t2 % e.T), co = (int)(t2 / e.T);
+      e.wp[i] = (bf16)e.w[((long)co * e.Cin + ci) * e.T + tap];
+    }
+  }
+  if (!e.wt) return;
+  const int tco = (e.Cout + 63) / 64, tk = (K + 63) / 64;
+  const int c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  for (int t = blockIdx.x; t < tco * tk; t += gridDim.x) {
+    const int co0 = (t / tk) * 64, k0 = (t % tk) * 64;
+    __syncthreads();  // the previous tile's reads are done
+#pragma unroll 4
+    for (int r = r0; r < 64; r += 4)
+      if (co0 + r < e.Cout && k0 + c < K) tile[r][c] = e.w[(long)(co0 + r) * K + k0 + c];
+    __syncthreads();
+#pragma unroll 4
+    for (int r = r0; r < 64; r += 4)  // r: the k row of wt, c: the co column
+      if (k0 + r < K && co0 + c < e.Cout) e.wt[(long)(k0 + r) * e.Cout + co0 + c] = (bf16)tile[c][r];
   }
 }
 

@@ -799,7 +799,7 @@ def test_conv_pack_multi_matches_single_pack():
     es_conv2d_pack_bf16 per weight: wp [Cout][k k][Cin], wt [Cin][k k][Cout], bit for bit."""
     import ctypes
     from endossl import _lib
-    shapes = [(64, 32, 3), (256, 64, 1), (32, 96, 7), (768, 256, 1), (128, 128, 3)]
+    shapes = [(64, 32, 3), (256, 64, 1), (32, 96, 7), (768, 256, 1), (128, 128, 3), (512, 512, 3), (100, 60, 3)]
     g = torch.Generator().manual_seed(5)
     ws = [torch.randn(co, ci, k, k, generator=g).to(DEV) for co, ci, k in shapes]
     outs = [(torch.empty(w.numel(), dtype=torch.bfloat16, device=DEV),
