@@ -61,6 +61,31 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const float* __restrict_
   }
 }
 
+// The same Y for few output columns (N < 64: a classifier head, e.g. ResNet-18's 512 -> 23 at B = 16, where
+// dense_fwd_kernel keeps N of a workgroup's 256 threads busy over a serial K loop): one wave per output, lanes
+// strided over K, a fixed-order wave reduction (deterministic; another summation order than dense_fwd_kernel)
+__global__ __launch_bounds__(256) void dense_fwd_small_kernel(const float* __restrict__ X, int ldx,
+                                                              const float* __restrict__ W,
+                                                              const float* __restrict__ b, float* __restrict__ Y,
+                                                              int ldy, int n, int K, int N, int act, float slope,
+                                                              const uint8_t* __restrict__ keep, float keep_scale) {
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (o >= n * N) return;  // wave-uniform
+  const int r = o / N, c = o - r * N;
+  const float* x = X + (size_t)r * ldx;
+  const float* w = W + (size_t)c * K;
+  float acc = 0.f;
+  for (int k = lane; k < K; k += 64) acc = fmaf(x[k], w[k], acc);
+  acc = warp_sum(acc);
+  if (lane == 0) {
+    float v = acc + (b ? b[c] : 0.f);
+    if (act == 1) v = fmaxf(v, 0.f);
+    else if (act == 2) v = v > 0.f ? v : v * slope;
+    if (keep) v = v * ((float)keep[(size_t)r * N + c] * keep_scale);
+    Y[(size_t)r * ldy + c] = v;
+  }
+}
+
 // dpre[i][c] = dY[i][c] * act'(Yact[i][c]) (* keep * scale).  The activation derivative is read
 // off the stored output: ReLU / LeakyReLU(slope > 0) outputs are > 0 exactly where their inputs
 // are, and a dropped element's gradient is 0 whatever the sign.
@@ -710,6 +735,12 @@ int es_dense_fwd(const float* X, int ldx, const float* W, const float* b, float*
                  int act, float slope, const void* keep, float keep_scale, hipStream_t stream) {
   if (n <= 0 || K <= 0 || N <= 0 || K > 2048 || act < 0 || act > 2) return ES_BAD_SHAPE;
   if (!X || !W || !Y) return ES_BAD_ARG;
+  if (N < 64) {
+    const long outs = (long)n * N;
+    hipLaunchKernelGGL(dense_fwd_small_kernel, (unsigned)((outs + 3) / 4), 256, 0, stream, X, ldx, W, b, Y, ldy, n, K, N,
+                       act, slope, (const uint8_t*)keep, keep_scale);
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+  }
   const size_t lds = (size_t)DR * K * 4;
   allow_lds(dense_fwd_kernel, lds);
   hipLaunchKernelGGL(dense_fwd_kernel, (n + DR - 1) / DR, 256, lds, stream, X, ldx, W, b, Y, ldy, n, K, N, act, slope,

@@ -63,9 +63,10 @@ def test_cls_ln_fwd_bwd(n, T, D):
 
 @pytest.mark.parametrize("act", [0, 1, 2])
 @pytest.mark.parametrize("with_keep", [False, True])
-def test_dense_fwd_bwd(act, with_keep):
-    torch.manual_seed(act * 2 + with_keep)
-    n, K, N = 37, 384, 96
+@pytest.mark.parametrize("N", [96, 23])  # 23: the few-column forward (one wave per output)
+def test_dense_fwd_bwd(act, with_keep, N):
+    torch.manual_seed(act * 2 + with_keep + N)
+    n, K = 37, 384
     X = torch.randn(n, K, device=DEV)
     W = torch.randn(N, K, device=DEV) * 0.05
     b = torch.randn(N, device=DEV) * 0.1
