@@ -145,13 +145,13 @@ def host_input_run(tr, B, MU, steps, dev):
             "source": "synthetic decoded RGB 500x375 frames (64), IS_CROP, S=224; decode not timed"}
 
 
-def cpu_baseline(B=16, MU=7, steps=1, warmup=1):
+def cpu_baseline(B=16, MU=7, steps=3, warmup=1):
     """Oracle (pinned CPU restatement) FixMatch step on every host core this process may use -- a
     reported baseline (torch.set_num_threads(os.cpu_count()), capped by the CPU share the
     box grants: more threads than cores only oversubscribes).  Default: a bounded sample of the F1 step,
     B=16, mu=7 (112 unlabeled images), one warm-up step (thread pools, first-touch of the allocator's pages)
-    then one timed step, ~30 s in all; --cpu-batch 64 runs the full F1 batch (~100 GB of fp32 autograd
-    activations, ~55 s per step)."""
+    then the mean of three timed steps (BASELINE.md's plan), ~65 s in all; --cpu-batch 64 runs the full F1
+    batch (~100 GB of fp32 autograd activations, ~55 s per step)."""
     from oracle import ref
     threads, cpu_info = host_cpus()
     prev = torch.get_num_threads()
@@ -496,7 +496,7 @@ def main():
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=16, help="cpu_baseline labeled batch B (64 = the F1 batch)")
-    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--cpu-warmup", type=int, default=1)
     ap.add_argument("--inputs", choices=("u8", "f32"), default="u8",
                     help="F1 batch format in HBM: uint8 pixels (normalised in the patch gather) or fp32")

@@ -15,6 +15,7 @@
 // the SOURCE address so the fragment reads are bank-conflict free; two LDS stages; the stage for
 // step k+1 is issued before the MFMAs of step k.
 #include <algorithm>
+#include <cstdlib>
 
 #include <hip/hip_ext.h>
 
@@ -1134,10 +1135,371 @@ int reduce_partials_multi(const RedPairEntry* ents, int n, hipStream_t stream) {
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Weight-stationary NT GEMM for K = 384 (round 6, es_gemm_nt variant 12).
+//
+// Every tiled NT kernel above re-reads its operands from L2 into LDS once per output tile: a 256 x 128 tile at
+// K = 384 moves (256 + 128) x 768 B for 32 K outputs, 9 B per output, and the K = 384 GEMMs of the ViT step
+// measured their L2 -> LDS operand stream at ~14 TB/s (~23 B/clk/CU), which -- not the matrix cores -- set
+// their pace.  Here one persistent 8-wave workgroup per CU owns a 384-column group of C and
+// keeps that group's weight rows in REGISTERS for the whole launch: wave w holds W[n0 + 48 w .. + 48][0 .. 384)
+// as the MFMA A operand (3 column fragments x 12 K fragments of v_mfma_f32_16x16x32_bf16 = 144 VGPRs).  The
+// workgroup walks 32-row tiles of A; each tile is staged into LDS once by LDS-DMA (3-stage ring, 24 KiB per
+// stage, source-side XOR swizzle: chunk c of row r at chunk c ^ (r & 15), conflict-free fragment reads) and
+// consumed by all eight waves, so the L2 -> LDS stream carries 768 B per 384 outputs (2 B per output).
+//   Accumulation: each output is the same chain of 12 MFMAs in K order, with the same operand roles (weights as
+// the A operand, activations as B) as the tiled kernels, so the fp32 accumulators -- and every epilogue's
+// outputs -- are bit-identical to variants 0 / 5 / 10 (tested).
+//   Epilogue: the 32 x 384 fp32 tile (accumulator + bias) goes through one LDS staging tile (rows padded by
+//   16 B: conflict-free MFMA-layout writes), read back one step later as whole rows, 16 B per lane, so every
+//   C store instruction covers contiguous 512-B (bf16) or 1-KiB (fp32) row stretches.  Per step:
+//     [vmcnt: tile i landed] [B1] [DMA tile i + 2] [epilogue of tile i - 1] [MFMAs of tile i] [B2] [staging write]
+//   B1 publishes the ring stage and the staging tile, B2 keeps the staging writes behind every wave's reads.
+//   Work distribution: row tiles are claimed dynamically, in chunks of 2, from a per-column-group counter
+//   (agent-scope atomics on a code-object array, one counter block per HIP stream; the last workgroup to finish
+//   resets it), two chunks ahead of use.  A static split would be wrong for this engine: the data-gradient
+//   GEMMs share the chip with the weight-gradient launches of the side stream (3/8 of the CUs for ~1 ms), so a
+//   workgroup that only gets a CU late must find the work already taken instead of extending the launch.
+//   All ring DMA is inline asm (glds16_asm): the explicit counted vmcnt at the top of each step retires it (the
+//   count follows every VMEM op this wave issued since, in issue order: claim atomics, DMA pieces, C stores).
+namespace wsg {
+constexpr int R = 32;                      // output rows per step (one A tile)
+constexpr int KD = 384;                    // reduction depth
+constexpr int NG = 384;                    // output columns per workgroup (8 waves x 48)
+constexpr int ROWB = KD * 2;               // A row bytes in the ring
+constexpr int STAGE = R * ROWB;            // 24 KiB
+constexpr int NST = 4;                     // ring stages (three tiles in flight behind the current one)
+constexpr int PIECES = STAGE / 1024 / 8;   // LDS-DMA instructions per wave per stage
+constexpr int SROW = NG * 4 + 16;          // staging row bytes (fp32 + 16-B pad)
+constexpr int STG = R * SROW;
+constexpr int CH = 2;                      // row tiles per claimed chunk
+constexpr int QN = 8;                      // chunk-index ring (LDS)
+constexpr int SLOTS = 64, SLOT_INTS = 16;  // counter blocks (one per stream): [0, ncg) claim heads, [15] done
+constexpr int LDS = NST * STAGE + STG + QN * 4 + NG * 4;  // + the column group's bias
+}  // namespace wsg
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ int g_ws_ctr[wsg::SLOTS * wsg::SLOT_INTS];
+
+// A chunk claim: one lane's returning agent-scope add (the same instruction hipcc emits for
+// __hip_atomic_fetch_add(.., __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), as inline asm so that hipcc neither
+// waits for it nor moves the result to an SGPR right away; the caller retires it with a counted vmcnt before
+// ws_publish_asm reads the result (cdna_hip_programming.md §5.7 item 1, form ii: the destination is named again
+// by the consuming statement; audited in the .s: no copy of it between the two).
+__device__ __forceinline__ void ws_claim_asm(int* head, int& ret) {
+  unsigned long long save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "s_nop 4\n\t"
+      "global_atomic_add %0, %2, %3, off sc0\n\t"
+      "s_mov_b64 exec, %1"
+      : "=&v"(ret), "=&s"(save)
+      : "v"(head), "v"(1)
+      : "memory");
+}
+// lane 0 stores the claimed chunk index to the LDS ring (the other lanes store nothing)
+__device__ __forceinline__ void ws_publish_asm(int* slot_lds, int& v, int lane) {
+  const unsigned a = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)slot_lds;
+  unsigned long long save;
+  asm volatile(
+      "s_mov_b64 %1, exec\n\t"
+      "s_mov_b64 exec, 1\n\t"
+      "s_nop 4\n\t"
+      "ds_write_b32 %2, %0\n\t"
+      "s_mov_b64 exec, %1"
+      : "+v"(v), "=&s"(save)
+      : "v"(a)
+      : "memory");
+  (void)lane;
+}
+
+// The MFMA phase of a step: 24 activation fragments (2 row blocks x 12 K steps), each feeding 3 MFMAs, read by
+// inline-asm ds_read_b128 kept WS_PF ahead (hipcc, at ~240 VGPRs, issued each read right before its MFMAs and
+// waited for it: one LDS round trip per 3 MFMAs).  Each wait names its fragment ("+v", cdna_hip_programming.md
+// §5.7 item 1 form ii) so no MFMA is scheduled above it; LDS returns in order, so lgkmcnt(reads issued after
+// fragment t) retires fragment t.  Chunk 4 kk + g of row r sits at chunk (4 kk + g) ^ r =
+// 16 (kk >> 2) + 4 ((kk & 3) ^ (r >> 2)) + (g ^ (r & 3)): four per-lane bases (kk & 3) plus constants.
+constexpr int WS_PF = 4;
+__device__ __forceinline__ void ws_ds_read(bf16x8& x, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(x) : "v"(addr) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void ws_lgkm_wait(bf16x8& x) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(x) : "i"(N) : "memory");
+}
+template <int T>
+__device__ __forceinline__ unsigned ws_frag_addr(const unsigned (&xb4)[4]) {
+  constexpr int kk = T % 12;
+  return xb4[kk & 3] + (T / 12) * 16 * wsg::ROWB + (kk >> 2) * 256;
+}
+template <int T>
+__device__ __forceinline__ void ws_mfma_loop(f32x4 (&acc)[2][3], const bf16x8 (&wf)[3][12], const unsigned (&xb4)[4],
+                                             bf16x8 (&xs)[WS_PF]) {
+  if constexpr (T < 24) {
+    constexpr int after = (23 - T) < (WS_PF - 1) ? (23 - T) : (WS_PF - 1);
+    ws_lgkm_wait<after>(xs[T % WS_PF]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[T / 12][j] = mfma16(wf[j][T % 12], xs[T % WS_PF], acc[T / 12][j]);
+    if constexpr (T + WS_PF < 24) ws_ds_read(xs[T % WS_PF], ws_frag_addr<T + WS_PF>(xb4));
+    ws_mfma_loop<T + 1>(acc, wf, xb4, xs);
+  }
+}
+__device__ __forceinline__ void ws_mfma_phase(f32x4 (&acc)[2][3], const bf16x8 (&wf)[3][12], const unsigned (&xb4)[4]) {
+  static_assert(WS_PF == 4, "prologue reads");
+  bf16x8 xs[WS_PF];
+  ws_ds_read(xs[0], ws_frag_addr<0>(xb4));
+  ws_ds_read(xs[1], ws_frag_addr<1>(xb4));
+  ws_ds_read(xs[2], ws_frag_addr<2>(xb4));
+  ws_ds_read(xs[3], ws_frag_addr<3>(xb4));
+  ws_mfma_loop<0>(acc, wf, xb4, xs);
+}
+
+template <int EPI>
+constexpr bool ws_epi_ok() {
+  return EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_ACT || EPI == EPI_GELU_D || EPI == EPI_F32;
+}
+// C stores per wave per epilogue (6 items of 4 outputs per lane; two outputs for GELU / GELU_D)
+template <int EPI>
+constexpr int ws_nstore() {
+  return (EPI == EPI_GELU || EPI == EPI_GELU_D) ? 12 : 6;
+}
+
+template <int EPI, int STAUX, int PROBE = 0>
+__global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, int slot) {
+  using namespace wsg;
+  static_assert(ws_epi_ok<EPI>(), "epilogue");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const stg = smem + NST * STAGE;
+  int* const qring = (int*)(stg + STG);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  const int cg = blockIdx.x % ncg;
+  int* const ctr = g_ws_ctr + slot * SLOT_INTS;
+  const int nrt = (p.M + R - 1) / R, nch = (nrt + CH - 1) / CH;
+  const int n0 = cg * NG, nw = n0 + w * 48;
+
+  // the first two chunks: blocking claims (their latency hides behind the weight loads below)
+  if (tid == 0) {
+    if constexpr (PROBE >= 5) {  // measurement: static chunks rs, rs + nrs, ... (no claims)
+      const int rs = blockIdx.x / ncg, nrs = gridDim.x / ncg;
+      qring[0] = rs; qring[1] = rs + nrs; qring[2] = rs + 2 * nrs;
+    } else {
+    qring[0] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qring[1] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qring[2] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  bf16x8 wf[3][12];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk)
+      wf[j][kk] = *(const bf16x8*)(p.B + (size_t)(nw + 16 * j + r) * p.ldb + 32 * kk + 8 * g);
+  float* const bias_lds = (float*)(qring + QN);  // the column group's bias, added in the epilogue
+  if (tid < NG / 4)
+    *(f32x4*)(bias_lds + 4 * tid) = p.bias ? *(const f32x4*)(p.bias + n0 + 4 * tid) : f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // weights, bias and the first claims retired (no compiler-counted load crosses into the loop)
+  int prv = 0;
+  int cur = __builtin_amdgcn_readfirstlane(qring[0]);  // chunk of the current iteration, and the two after it
+  int n1 = __builtin_amdgcn_readfirstlane(qring[1]);
+  int n2 = __builtin_amdgcn_readfirstlane(qring[2]);
+
+  // LDS-DMA source offsets of this wave's pieces within a tile (bytes from the tile's first row)
+  unsigned so[PIECES];
+#pragma unroll
+  for (int j = 0; j < PIECES; ++j) {
+    const int off = ((j * 8 + w) * 64 + lane) * 16, row = off / ROWB, c = (off % ROWB) >> 4;
+    so[j] = (unsigned)(row * p.lda * 2 + ((c ^ (row & 15)) << 4));
+  }
+  auto dma = [&](int st, int tile) {
+    const char* src = (const char*)(p.A + (size_t)tile * R * p.lda);
+#pragma unroll
+    for (int j = 0; j < PIECES; ++j) glds16_asm(src + so[j], smem + st * STAGE + (j * 8 + w) * 1024);
+  };
+  int xbase[4];  // per-lane byte offsets of the activation fragments within a stage (see the MFMA loop)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) xbase[k] = r * ROWB + ((4 * (k ^ (r >> 2)) + (g ^ (r & 3))) << 4);
+  // epilogue items: lane owns 6 x 4 consecutive outputs of rows 4w .. 4w + 3 (item it: flat it * 64 + lane)
+  auto erow = [&](int it) { return 4 * w + (it * 64 + lane) / 96; };
+  auto ecol = [&](int it) { return 4 * ((it * 64 + lane) % 96); };
+  constexpr bool f32out = EPI == EPI_F32;
+  const unsigned crows = (unsigned)p.M;
+  const __amdgpu_buffer_rsrc_t rc = buf_rsrc(p.C, crows * p.ldc * (f32out ? 4u : 2u));
+  const __amdgpu_buffer_rsrc_t rc2 = buf_rsrc((EPI == EPI_GELU || EPI == EPI_GELU_D) ? p.C2 : p.C, crows * p.ldc * 2u);
+  auto epilogue = [&](int tile) {
+    const int m0 = tile * R;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      float v[8];
+      unsigned off[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int it = 2 * q + h;
+        const f32x4 x = *(const f32x4*)(stg + erow(it) * SROW + ecol(it) * 4) + *(const f32x4*)(bias_lds + ecol(it));
+        v[4 * h] = x[0]; v[4 * h + 1] = x[1]; v[4 * h + 2] = x[2]; v[4 * h + 3] = x[3];
+        const int m = m0 + erow(it);
+        off[h] = m < p.M ? (unsigned)(m * p.ldc + n0 + ecol(it)) * (f32out ? 4u : 2u) : ES_OOB;
+      }
+      auto st8 = [&](const float* s, __amdgpu_buffer_rsrc_t rr, unsigned o) {  // 4 bf16 = 8 B
+        bf16x4 b = bf16x4{(bf16)s[0], (bf16)s[1], (bf16)s[2], (bf16)s[3]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), rr, o, 0, STAUX);
+      };
+      if constexpr (EPI == EPI_F32) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(unsigned, v[4 * h]),
+                                                       __builtin_bit_cast(unsigned, v[4 * h + 1]),
+                                                       __builtin_bit_cast(unsigned, v[4 * h + 2]),
+                                                       __builtin_bit_cast(unsigned, v[4 * h + 3])},
+                                                 rc, off[h], 0, STAUX);
+      } else if constexpr (EPI == EPI_BF16) {
+        st8(v, rc, off[0]);
+        st8(v + 4, rc, off[1]);
+      } else {
+        float gg[8], dd[8];
+        gelu_and_grad_f8(v, gg, dd);
+        if constexpr (EPI == EPI_GELU_ACT) {
+          st8(gg, rc, off[0]);
+          st8(gg + 4, rc, off[1]);
+        } else if constexpr (EPI == EPI_GELU) {
+          st8(v, rc, off[0]);
+          st8(v + 4, rc, off[1]);
+          st8(gg, rc2, off[0]);
+          st8(gg + 4, rc2, off[1]);
+        } else {  // EPI_GELU_D: C = gelu', C2 = gelu
+          st8(dd, rc, off[0]);
+          st8(dd + 4, rc, off[1]);
+          st8(gg, rc2, off[0]);
+          st8(gg + 4, rc2, off[1]);
+        }
+      }
+    }
+  };
+
+  if (cur < nch) {
+    static_assert(NST == 4 && CH == 2, "the claim lookahead below is written for 4 stages and 2-tile chunks");
+    // vmcnt bookkeeping: this wave's VMEM ops since the loop started, in issue order
+    int seq = 0;
+    auto dma_valid = [&](int ch, int k) { return ch < nch && ch * CH + k < nrt; };
+    dma(0, cur * CH);  // positions 0, 1 (chunk cur) and 2 (chunk n1)
+    seq += PIECES;
+    int after_a = seq;  // seq right after the DMA of position i (retired at the top of step i), i + 1, i + 2
+    if (dma_valid(cur, 1)) {
+      dma(1, cur * CH + 1);
+      seq += PIECES;
+    }
+    int after_b = seq;
+    if (dma_valid(n1, 0)) {
+      dma(2, n1 * CH);
+      seq += PIECES;
+    }
+    int after_c = seq;
+    int st = 0;  // ring stage of the current position
+    // one step: the wait for this position's stage, B1, the DMA three positions ahead (tile tdma, or none),
+    // the previous position's epilogue (tile tepi; nrt = a dropped dummy that keeps the VMEM count fixed),
+    // the MFMAs, an optional hook before B2, B2, the staging write
+    auto top = [&]() {
+      wait_vmcnt_any(seq - after_a);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // B1: stage landed for every wave, staging tile published
+    };
+    auto body = [&](bool do_dma, int tdma, int tepi, auto&& before_b2) {
+      int st3 = st + 3;
+      st3 = st3 >= NST ? st3 - NST : st3;
+      after_a = after_b;
+      after_b = after_c;
+      if (do_dma && PROBE != 4 && PROBE != 5) {
+        dma(st3, tdma);
+        seq += PIECES;
+      }
+      after_c = seq;
+      if constexpr (PROBE != 1 && PROBE != 3 && PROBE != 4 && PROBE != 5) {
+        epilogue(tepi);
+        seq += ws_nstore<EPI>();
+      }
+      f32x4 acc[2][3];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) acc[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // the MFMA phase on this position's stage (ws_mfma_phase: fragment reads WS_PF ahead)
+      const char* As = smem + st * STAGE;
+      if constexpr (PROBE != 2 && PROBE != 3) {
+        unsigned xb4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          xb4[k] = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(As + xbase[k]);
+        ws_mfma_phase(acc, wf, xb4);
+      }
+      before_b2();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // B2: every wave has read the staging tile of the previous position
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+          *(f32x4*)(stg + (a * 16 + r) * SROW + (w * 48 + 16 * j + 4 * g) * 4) = acc[a][j];
+      st = st + 1 == NST ? 0 : st + 1;
+    };
+    // one iteration = one chunk (positions 2 lc, 2 lc + 1).  The claim for chunk lc + 3 is issued at the first
+    // position and consumed (published to LDS) at the end of the second, inside the iteration; the DMA of the
+    // first tile of chunk lc + 3 is issued at position 2 lc + 3, after the next iteration's first B1.
+    int last = 0;
+    for (int lc = 0;; ++lc) {
+      top();
+      if (lc > 0) {
+        prv = cur;
+        cur = n1;
+        n1 = n2;
+        n2 = __builtin_amdgcn_readfirstlane(qring[(lc + 2) & (QN - 1)]);
+        if (cur >= nch) {
+          last = prv * CH + 1;
+          break;
+        }
+      }
+      const bool live = n2 < nch;
+      const bool claimer = live && w == 0;  // wave-uniform
+      int claimed = nch, after_claim = 0;
+      if (claimer) {
+        if constexpr (PROBE >= 5) {
+          claimed = (int)(blockIdx.x / ncg) + (lc + 3) * (int)(gridDim.x / ncg);
+        } else {
+          ws_claim_asm(ctr + cg, claimed);
+          seq += 1;
+        }
+        after_claim = seq;
+      }
+      body(dma_valid(n1, 1), n1 * CH + 1, lc > 0 ? prv * CH + 1 : nrt, [] {});
+      top();
+      if (cur * CH + 1 >= nrt) {
+        last = cur * CH;
+        break;
+      }
+      body(dma_valid(n2, 0), n2 * CH, cur * CH, [&] {
+        if (w == 0) {  // publish chunk lc + 3 (nch: none claimed) for the iterations after this one
+          if (claimer) wait_vmcnt_any(seq - after_claim);
+          ws_publish_asm(qring + ((lc + 3) & (QN - 1)), claimed, lane);
+        }
+      });
+    }
+    epilogue(last);  // the last position's staging tile was published by the final B1
+  }
+  // every claim of this workgroup has landed; the last workgroup out resets the counter block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (tid == 0) {
+    const int d = __hip_atomic_fetch_add(ctr + SLOT_INTS - 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (int)gridDim.x - 1) {
+      for (int c = 0; c < ncg; ++c) __hip_atomic_store(ctr + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + SLOT_INTS - 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
 // template commas out of the launch macro; a kernel referenced only through a function pointer
 // gets no host stub).
-#define NT_LAUNCH(E, BKT_, NST_, TBM_, ...)                                                \
+#define NT_LAUNCH(E, BKT_, NST_, TBM_, ...)                                             \
   {                                                                                        \
     const size_t lds = std::max((size_t)NST_ * (TBM_ + BN) * BKT_ * 2, (size_t)4 * EPI_WAVE_BYTES); \
     allow_lds(gemm_nt_kernel<E, BKT_, NST_, TBM_, ##__VA_ARGS__>, lds);                   \
@@ -1206,6 +1568,65 @@ int launch_big(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) 
 #undef BIG_EPIS2
 #undef BIG_LAUNCH
 
+// The weight-stationary kernel's counter block for a stream: launches on one stream never overlap, so one block
+// per stream is never shared by two running launches (64 streams; beyond that streams share blocks by hash,
+// which is only wrong if two of them then run such GEMMs at the same time).
+static int ws_slot(hipStream_t s) {
+  static hipStream_t tab[wsg::SLOTS];
+  static int n = 0;
+  for (int i = 0; i < n; ++i)
+    if (tab[i] == s) return i;
+  if (n < wsg::SLOTS) {
+    tab[n] = s;
+    return n++;
+  }
+  return (int)(((uintptr_t)s >> 6) % wsg::SLOTS);
+}
+static bool ws_fits(int epi, int N, int K) {
+  const bool e = epi == EPI_BF16 || epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D || epi == EPI_F32;
+  return e && K == wsg::KD && N % wsg::NG == 0 && N / wsg::NG < wsg::SLOT_INTS;
+}
+#define WS_LAUNCH(E, AUX_, ...)                                                                                   \
+  {                                                                                                                \
+    allow_lds(gemm_nt_ws_kernel<E, AUX_, ##__VA_ARGS__>, (size_t)wsg::LDS);                                       \
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(gemm_nt_ws_kernel<E, AUX_, ##__VA_ARGS__>), dim3(grid), dim3(512), wsg::LDS, \
+                       stream, a, ncg, slot);                                                                      \
+    return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;                                                 \
+  }
+int launch_ws(int epi, hipStream_t stream, const NTArgs& a) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const int ncg = a.N / wsg::NG;
+  const int nrt = (a.M + wsg::R - 1) / wsg::R, nch = (nrt + wsg::CH - 1) / wsg::CH;
+  const int per = std::max(1, std::min(cus / ncg, nch));  // workgroups per column group
+  const int grid = per * ncg;
+  const int slot = ws_slot(stream);
+  static const int probe = getenv("ENDOSSL_WS_PROBE") ? atoi(getenv("ENDOSSL_WS_PROBE")) : 0;  // measurement only
+  if (probe && epi == EPI_BF16) {
+    switch (probe) {
+      case 1: WS_LAUNCH(EPI_BF16, 2, 1)
+      case 2: WS_LAUNCH(EPI_BF16, 2, 2)
+      case 3: WS_LAUNCH(EPI_BF16, 2, 3)
+      case 4: WS_LAUNCH(EPI_BF16, 2, 4)
+      case 5: WS_LAUNCH(EPI_BF16, 2, 5)
+      default: WS_LAUNCH(EPI_BF16, 2, 6)
+    }
+  }
+  switch (epi) {
+    case EPI_BF16: WS_LAUNCH(EPI_BF16, 2)
+    case EPI_GELU: WS_LAUNCH(EPI_GELU, 2)
+    case EPI_GELU_ACT: WS_LAUNCH(EPI_GELU_ACT, 2)
+    case EPI_GELU_D: WS_LAUNCH(EPI_GELU_D, 2)
+    case EPI_F32: WS_LAUNCH(EPI_F32, 0)
+    default: return ES_BAD_ARG;
+  }
+}
+#undef WS_LAUNCH
+
 }  // namespace es_gemm
 using namespace es_gemm;
 
@@ -1252,6 +1673,10 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   //  es_set_gemm_small_tile(0) drops the 64 x 128 rules.
   int variant = g_gemm_variant;
   const bool two_wg = true;
+  if (variant == 12) {  // the weight-stationary kernel where it applies, the per-shape rules elsewhere
+    if (ws_fits(epi, N, K)) return launch_ws(epi, stream, a);
+    variant = -1;
+  }
   if (variant < 0) {
     const bool gelu = epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D;
     const bool plain = epi == EPI_BF16 || epi == EPI_F32 || epi == EPI_F32_RESID || epi == EPI_MULAUX;
@@ -1315,7 +1740,7 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 // 2-stage).  Returns the previous value, or ES_BAD_ARG (state unchanged) for a family that does not
 // exist (the others were measured slower and removed in round 4).
 static bool gemm_variant_ok(int v) {
-  return v == -1 || v == 0 || v == 1 || v == 2 || v == 5 || v == 6 || v == 10 || v == 11;
+  return v == -1 || v == 0 || v == 1 || v == 2 || v == 5 || v == 6 || v == 10 || v == 11 || v == 12;
 }
 int es_set_gemm_variant(int v) {
   if (!gemm_variant_ok(v)) return ES_BAD_ARG;

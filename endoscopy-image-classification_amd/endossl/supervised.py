@@ -92,28 +92,39 @@ class SupLearning:
         join_wgrad_stream(dev)
         return stats, logits.detach()
 
-    def _run_graph(self, images, targets):
+    def _graph_key(self, images, targets):
+        """Everything that changes the captured launch sequence: shapes, buffers, the model's precision / map /
+        freezing state and which parameters take gradients."""
         m = self.model
         cw = self.class_weights
-        key = (tuple(images.shape), images.dtype, tuple(targets.shape), m.flat.data_ptr(), m.flat_grad.data_ptr(),
-               cw.data_ptr() if cw is not None else 0)
-        if getattr(self, "_gkey", None) != key:
-            self._graph, self._gkey, self._gwarm = None, key, 0
-        if self._graph is None:
-            if self._gwarm < self.GRAPH_WARM:
-                self._gwarm += 1
+        return (tuple(images.shape), images.dtype, tuple(targets.shape), m.flat.data_ptr(), m.flat_grad.data_ptr(),
+                cw.data_ptr() if cw is not None else 0, getattr(m, "conv_bf16", None), getattr(m, "map_bf16", None),
+                bool(getattr(m, "frozen_trunk", False)), tuple(p.requires_grad for p in m.parameters()))
+
+    def _run_graph(self, images, targets):
+        """One step replayed from the graph captured for its key (one graph per key, so the smaller last batch
+        of an epoch runs eagerly / gets its own graph without discarding the main one).  Returns fresh copies
+        of the graph's static outputs: the next replay overwrites them."""
+        key = self._graph_key(images, targets)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        ent = graphs.get(key)
+        if ent is None:
+            ent = graphs[key] = {"warm": 0, "graph": None}
+        if ent["graph"] is None:
+            if ent["warm"] < self.GRAPH_WARM:
+                ent["warm"] += 1
                 return self._compute(images, targets)
             gin = (images.clone(), targets.clone())
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 gout = self._compute(*gin)
-            self._graph, self._gin, self._gout = g, gin, gout
+            ent.update(graph=g, gin=gin, gout=gout)
         else:
-            for dst, src in zip(self._gin, (images, targets)):
+            for dst, src in zip(ent["gin"], (images, targets)):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src, non_blocking=True)
-        self._graph.replay()
-        return self._gout
+        ent["graph"].replay()
+        return tuple(t.clone() for t in ent["gout"])
 
     def step(self, batch):
         """batch = (images [n, 3, H, W], targets [n]) -> {"loss", "logits"} (device tensors)."""
@@ -123,7 +134,8 @@ class SupLearning:
         targets = targets.to(dev, non_blocking=True).to(torch.int64).contiguous()
         images = images.to(dev, non_blocking=True)
         self.model.train()
-        if self.use_graph and dist.world_size() == 1 and images.is_cuda:
+        # graph replay for the ResNet models (the host-bound P0 step); the ViT models step eagerly here
+        if self.use_graph and dist.world_size() == 1 and images.is_cuda and type(self.model).__name__ == "NativeResNet":
             stats, logits = self._run_graph(images, targets)
         else:
             stats, logits = self._compute(images, targets)

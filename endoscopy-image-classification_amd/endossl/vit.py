@@ -261,6 +261,7 @@ class Engine:
     # per-workgroup partials in a workspace of its own and one es_ln_param_grads_multi launch per weight-gradient
     # launch reduces them on the side stream (24 launches fewer on the chain per step; bit-identical)
     DEFER_LN_GRADS = True
+    LN_MULTI_MAX = 32  # entries per es_ln_param_grads_multi launch (RPM_MAX in csrc/gemm.hip)
     # A block's long-axis weight gradients (fc2, fc1, proj, qkv: 24 tiles of 384 x 192 at ViT-S) as ONE
     # split-K launch on the side stream once the block's data-gradient chain has produced its last dY
     # (es_gemm_tn_big_grouped) plus one reduce launch, sized to LAYER_TN_SHARE of the CUs (4 splits):
@@ -623,13 +624,17 @@ class Engine:
             return
         lib = _lib.load()
         esz = lib.es_ln_param_grads_entry_size()
-        raw = (ctypes.c_char * (esz * len(pending)))()
-        for j, (ws, dg, db, grid, acc) in enumerate(pending):
-            ent = (ctypes.c_void_p(ptr(ws)), ctypes.c_void_p(ptr(dg)), ctypes.c_void_p(ptr(db)), ctypes.c_int(grid),
-                   ctypes.c_int(self.cfg.dim), ctypes.c_int(acc), ctypes.c_int(0))
-            buf = b"".join(bytes(e) for e in ent)
-            ctypes.memmove(ctypes.byref(raw, j * esz), buf, len(buf))
-        self._call("es_ln_param_grads_multi", ctypes.addressof(raw), len(pending), _lib.stream())
+        # es_ln_param_grads_multi takes at most LN_MULTI_MAX entries (the C side's RPM_MAX): larger groups (a
+        # bigger GROUP_LAYERS, deeper models) go out as several launches
+        for c0 in range(0, len(pending), self.LN_MULTI_MAX):
+            chunk = pending[c0:c0 + self.LN_MULTI_MAX]
+            raw = (ctypes.c_char * (esz * len(chunk)))()
+            for j, (ws, dg, db, grid, acc) in enumerate(chunk):
+                ent = (ctypes.c_void_p(ptr(ws)), ctypes.c_void_p(ptr(dg)), ctypes.c_void_p(ptr(db)),
+                       ctypes.c_int(grid), ctypes.c_int(self.cfg.dim), ctypes.c_int(acc), ctypes.c_int(0))
+                buf = b"".join(bytes(e) for e in ent)
+                ctypes.memmove(ctypes.byref(raw, j * esz), buf, len(buf))
+            self._call("es_ln_param_grads_multi", ctypes.addressof(raw), len(chunk), _lib.stream())
         pending.clear()
 
     def backward(self, flat, grad, dlogits=None, dfts=None, zero_grad=True, grad_ready=None):

@@ -129,8 +129,10 @@ def test_suplearning_step_vs_oracle():
 def test_suplearning_graph_replay_bit_identical():
     """SupLearning.use_graph: the forward / loss / backward captured once (after GRAPH_WARM eager steps) and
     replayed, new batches copied into the graph's inputs, against every step eager -- losses, logits,
-    parameters, EMA and BatchNorm buffers BIT-identical over six steps (bf16 convs; the captured steps
-    pack the conv weights themselves)."""
+    parameters, EMA and BatchNorm buffers BIT-identical over eight steps (bf16 convs; the captured steps
+    pack the conv weights themselves).  The returned tensors are read only after the last step (the graph
+    path returns copies, not its static outputs), and a ragged batch between two full ones runs eagerly
+    without discarding the captured graph."""
     from endossl.supervised import SupLearning
     from endossl.utils import AttrDict
     g = torch.Generator().manual_seed(11)
@@ -142,6 +144,8 @@ def test_suplearning_graph_replay_bit_identical():
     class _DL(list):
         dataset = _DS()
 
+    batches.append((torch.randn(5, 3, 64, 64, generator=g), torch.randint(0, 23, (5,), generator=g)))  # ragged last
+    batches.append(batches[0])  # the main shape again: its graph survives the ragged batch
     runs = {}
     for graph in (False, True):
         m, _ = _model(seed=6, conv="bf16")
@@ -154,12 +158,12 @@ def test_suplearning_graph_replay_bit_identical():
                                               EPOCHS=1, WARMUP_EPOCHS=0, DECAY_EPOCHS=10, WARMUP_LR=5e-4,
                                               LR_DECAY=0.8, SCH_NAME="const", FREQ_EVAL=1)))
         tr.class_weights = torch.linspace(0.5, 2.0, 23).to(DEV)
-        losses, logits = [], []
-        for x, y in batches:
-            out = tr.step((x.to(DEV), y.to(DEV)))
-            losses.append(out["loss"].item())
-            logits.append(out["logits"].cpu().clone())
-        assert (getattr(tr, "_graph", None) is not None) == graph
+        outs = [tr.step((x.to(DEV), y.to(DEV))) for x, y in batches]  # kept un-cloned across later steps
+        torch.cuda.synchronize()
+        losses = [o["loss"].item() for o in outs]
+        logits = [o["logits"].cpu() for o in outs]
+        graphs = [e for e in getattr(tr, "_graphs", {}).values() if e["graph"] is not None]
+        assert len(graphs) == (1 if graph else 0)
         runs[graph] = (losses, logits, {k: v.detach().cpu().clone() for k, v in m.state_dict().items()},
                        {k: v.detach().cpu().clone() for k, v in tr.ema_model.ema.state_dict().items()})
     (le, ge, se, ee), (lg, gg, sg, eg) = runs[False], runs[True]
