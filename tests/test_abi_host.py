@@ -312,7 +312,7 @@ def test_kernel_family_pins_refuse_removed_families():
     leaves the setting alone (round-4 advice: removed pins used to fall back to family 0 silently)."""
     from endossl import _lib
     lib = _lib.load()
-    for setter, good, bad in (("es_set_gemm_variant", (-1, 0, 1, 2, 5, 6, 10, 11), (3, 4, 7, 8, 9, 12, 21, -2)),
+    for setter, good, bad in (("es_set_gemm_variant", (-1, 0, 1, 2, 5, 6, 10, 11, 12), (3, 4, 7, 8, 9, 13, 21, -2)),
                               ("es_set_tn_variant", (-1, 0, 7), (1, 2, 5, 6, 8, 13)),
                               ("es_set_attn_bwd_variant", (0, 1, 2, 3, 4), (5, -1)),
                               ("es_set_conv_ring", (0, 3, 4), (1, 2, 5, -1)),
