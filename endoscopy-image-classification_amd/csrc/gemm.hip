@@ -1170,12 +1170,10 @@ constexpr int ROWB = KD * 2;               // A row bytes in the ring
 constexpr int STAGE = R * ROWB;            // 24 KiB
 constexpr int NST = 4;                     // ring stages (three tiles in flight behind the current one)
 constexpr int PIECES = STAGE / 1024 / 8;   // LDS-DMA instructions per wave per stage
-constexpr int SROW = NG * 4 + 16;          // staging row bytes (fp32 + 16-B pad)
-constexpr int STG = R * SROW;
 constexpr int CH = 2;                      // row tiles per claimed chunk
 constexpr int QN = 8;                      // chunk-index ring (LDS)
 constexpr int SLOTS = 64, SLOT_INTS = 16;  // counter blocks (one per stream): [0, ncg) claim heads, [15] done
-constexpr int LDS = NST * STAGE + STG + QN * 4 + NG * 4;  // + the column group's bias
+constexpr int LDS = NST * STAGE + QN * 4 + NG * 4;  // ring, chunk ring, the column group's bias
 }  // namespace wsg
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ int g_ws_ctr[wsg::SLOTS * wsg::SLOT_INTS];
@@ -1232,26 +1230,30 @@ __device__ __forceinline__ unsigned ws_frag_addr(const unsigned (&xb4)[4]) {
   constexpr int kk = T % 12;
   return xb4[kk & 3] + (T / 12) * 16 * wsg::ROWB + (kk >> 2) * 256;
 }
-template <int T>
+template <int A, int T>
 __device__ __forceinline__ void ws_mfma_loop(f32x4 (&acc)[2][3], const bf16x8 (&wf)[3][12], const unsigned (&xb4)[4],
                                              bf16x8 (&xs)[WS_PF]) {
-  if constexpr (T < 24) {
-    constexpr int after = (23 - T) < (WS_PF - 1) ? (23 - T) : (WS_PF - 1);
+  if constexpr (T < 12) {
+    constexpr int after = (11 - T) < (WS_PF - 1) ? (11 - T) : (WS_PF - 1);
     ws_lgkm_wait<after>(xs[T % WS_PF]);
 #pragma unroll
-    for (int j = 0; j < 3; ++j) acc[T / 12][j] = mfma16(wf[j][T % 12], xs[T % WS_PF], acc[T / 12][j]);
-    if constexpr (T + WS_PF < 24) ws_ds_read(xs[T % WS_PF], ws_frag_addr<T + WS_PF>(xb4));
-    ws_mfma_loop<T + 1>(acc, wf, xb4, xs);
+    for (int j = 0; j < 3; ++j) acc[A][j] = mfma16(wf[j][T], xs[T % WS_PF], acc[A][j]);
+    if constexpr (T + WS_PF < 12) ws_ds_read(xs[T % WS_PF], ws_frag_addr<A * 12 + T + WS_PF>(xb4));
+    ws_mfma_loop<A, T + 1>(acc, wf, xb4, xs);
   }
 }
-__device__ __forceinline__ void ws_mfma_phase(f32x4 (&acc)[2][3], const bf16x8 (&wf)[3][12], const unsigned (&xb4)[4]) {
+// row block A (16 rows) of a step: 12 fragments x 3 MFMAs
+template <int A>
+__device__ __forceinline__ void ws_mfma_half(f32x4 (&acc)[2][3], const bf16x8 (&wf)[3][12], const unsigned (&xb4)[4]) {
   static_assert(WS_PF == 4, "prologue reads");
+#pragma unroll
+  for (int j = 0; j < 3; ++j) acc[A][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 xs[WS_PF];
-  ws_ds_read(xs[0], ws_frag_addr<0>(xb4));
-  ws_ds_read(xs[1], ws_frag_addr<1>(xb4));
-  ws_ds_read(xs[2], ws_frag_addr<2>(xb4));
-  ws_ds_read(xs[3], ws_frag_addr<3>(xb4));
-  ws_mfma_loop<0>(acc, wf, xb4, xs);
+  ws_ds_read(xs[0], ws_frag_addr<A * 12 + 0>(xb4));
+  ws_ds_read(xs[1], ws_frag_addr<A * 12 + 1>(xb4));
+  ws_ds_read(xs[2], ws_frag_addr<A * 12 + 2>(xb4));
+  ws_ds_read(xs[3], ws_frag_addr<A * 12 + 3>(xb4));
+  ws_mfma_loop<A, 0>(acc, wf, xb4, xs);
 }
 
 template <int EPI>
@@ -1268,9 +1270,10 @@ template <int EPI, int STAUX, int PROBE = 0>
 __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, int slot) {
   using namespace wsg;
   static_assert(ws_epi_ok<EPI>(), "epilogue");
+  static_assert(NST == 4 && CH == 2, "the claim lookahead below is written for 4 stages and 2-tile chunks");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* const stg = smem + NST * STAGE;
-  int* const qring = (int*)(stg + STG);
+  int* const qring = (int*)(smem + NST * STAGE);
+  float* const bias_lds = (float*)(qring + QN);  // the column group's bias
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r = lane & 15;
@@ -1278,16 +1281,17 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   int* const ctr = g_ws_ctr + slot * SLOT_INTS;
   const int nrt = (p.M + R - 1) / R, nch = (nrt + CH - 1) / CH;
   const int n0 = cg * NG, nw = n0 + w * 48;
+  const bool late = w >= 4;  // waves 4..7 interleave their epilogue differently (see the step body)
 
-  // the first two chunks: blocking claims (their latency hides behind the weight loads below)
+  // the first three chunks: blocking claims (their latency hides behind the weight loads below)
   if (tid == 0) {
-    if constexpr (PROBE >= 5) {  // measurement: static chunks rs, rs + nrs, ... (no claims)
+    if constexpr (PROBE == 5) {  // measurement: static chunks rs, rs + nrs, ... (no claims)
       const int rs = blockIdx.x / ncg, nrs = gridDim.x / ncg;
       qring[0] = rs; qring[1] = rs + nrs; qring[2] = rs + 2 * nrs;
     } else {
-    qring[0] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    qring[1] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    qring[2] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      qring[0] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      qring[1] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      qring[2] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   bf16x8 wf[3][12];
@@ -1296,11 +1300,9 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
 #pragma unroll
     for (int kk = 0; kk < 12; ++kk)
       wf[j][kk] = *(const bf16x8*)(p.B + (size_t)(nw + 16 * j + r) * p.ldb + 32 * kk + 8 * g);
-  float* const bias_lds = (float*)(qring + QN);  // the column group's bias, added in the epilogue
   if (tid < NG / 4)
     *(f32x4*)(bias_lds + 4 * tid) = p.bias ? *(const f32x4*)(p.bias + n0 + 4 * tid) : f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // weights, bias and the first claims retired (no compiler-counted load crosses into the loop)
-  int prv = 0;
   int cur = __builtin_amdgcn_readfirstlane(qring[0]);  // chunk of the current iteration, and the two after it
   int n1 = __builtin_amdgcn_readfirstlane(qring[1]);
   int n2 = __builtin_amdgcn_readfirstlane(qring[2]);
@@ -1317,68 +1319,54 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
 #pragma unroll
     for (int j = 0; j < PIECES; ++j) glds16_asm(src + so[j], smem + st * STAGE + (j * 8 + w) * 1024);
   };
-  int xbase[4];  // per-lane byte offsets of the activation fragments within a stage (see the MFMA loop)
+  int xbase[4];  // per-lane byte offsets of the activation fragments within a stage (ws_mfma_phase)
 #pragma unroll
   for (int k = 0; k < 4; ++k) xbase[k] = r * ROWB + ((4 * (k ^ (r >> 2)) + (g ^ (r & 3))) << 4);
-  // epilogue items: lane owns 6 x 4 consecutive outputs of rows 4w .. 4w + 3 (item it: flat it * 64 + lane)
-  auto erow = [&](int it) { return 4 * w + (it * 64 + lane) / 96; };
-  auto ecol = [&](int it) { return 4 * ((it * 64 + lane) % 96); };
+
+  // Epilogue straight from the MFMA layout: acc[a][j] holds C[m0 + 16 a + r][nw + 16 j + 4 g + 0..3] (the
+  // accumulator of D = W X^T: 4 consecutive columns of one row per lane), so each store instruction writes
+  // 16 rows x 32 (bf16) / 64 (fp32) contiguous bytes and a wave's 3 stores per row block cover 96 / 192 B;
+  // the L2 merges the eight waves' pieces of each row (plain stores: written back as whole lines).
   constexpr bool f32out = EPI == EPI_F32;
   const unsigned crows = (unsigned)p.M;
   const __amdgpu_buffer_rsrc_t rc = buf_rsrc(p.C, crows * p.ldc * (f32out ? 4u : 2u));
   const __amdgpu_buffer_rsrc_t rc2 = buf_rsrc((EPI == EPI_GELU || EPI == EPI_GELU_D) ? p.C2 : p.C, crows * p.ldc * 2u);
-  auto epilogue = [&](int tile) {
+  auto epilogue = [&](const f32x4 (&acc)[2][3], int tile, int a) {  // row block a of tile
     const int m0 = tile * R;
+    f32x4 bj[3];
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      float v[8];
-      unsigned off[2];
+    for (int j = 0; j < 3; ++j) bj[j] = *(const f32x4*)(bias_lds + w * 48 + 16 * j + 4 * g);
+    auto st8 = [&](const float* v, __amdgpu_buffer_rsrc_t rr, unsigned o) {  // 4 bf16 = 8 B
+      const bf16x4 b = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), rr, o, 0, STAUX);
+    };
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int it = 2 * q + h;
-        const f32x4 x = *(const f32x4*)(stg + erow(it) * SROW + ecol(it) * 4) + *(const f32x4*)(bias_lds + ecol(it));
-        v[4 * h] = x[0]; v[4 * h + 1] = x[1]; v[4 * h + 2] = x[2]; v[4 * h + 3] = x[3];
-        const int m = m0 + erow(it);
-        off[h] = m < p.M ? (unsigned)(m * p.ldc + n0 + ecol(it)) * (f32out ? 4u : 2u) : ES_OOB;
-      }
-      auto st8 = [&](const float* s, __amdgpu_buffer_rsrc_t rr, unsigned o) {  // 4 bf16 = 8 B
-        bf16x4 b = bf16x4{(bf16)s[0], (bf16)s[1], (bf16)s[2], (bf16)s[3]};
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, b), rr, o, 0, STAUX);
-      };
+    for (int j = 0; j < 3; ++j) {  // column fragment j: 4 consecutive outputs of one row
+      const f32x4 x = acc[a][j] + bj[j];
+      float v[4] = {x[0], x[1], x[2], x[3]};
+      const int m = m0 + 16 * a + r;
+      const unsigned off = m < p.M ? (unsigned)(m * p.ldc + nw + 16 * j + 4 * g) * (f32out ? 4u : 2u) : ES_OOB;
       if constexpr (EPI == EPI_F32) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          __builtin_amdgcn_raw_buffer_store_b128(u32x4{__builtin_bit_cast(unsigned, v[4 * h]),
-                                                       __builtin_bit_cast(unsigned, v[4 * h + 1]),
-                                                       __builtin_bit_cast(unsigned, v[4 * h + 2]),
-                                                       __builtin_bit_cast(unsigned, v[4 * h + 3])},
-                                                 rc, off[h], 0, STAUX);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, x), rc, off, 0, STAUX);
       } else if constexpr (EPI == EPI_BF16) {
-        st8(v, rc, off[0]);
-        st8(v + 4, rc, off[1]);
+        st8(v, rc, off);
       } else {
-        float gg[8], dd[8];
-        gelu_and_grad_f8(v, gg, dd);
+        float gg[4], dd[4];
+        gelu_and_grad_f4(v, gg, dd);
         if constexpr (EPI == EPI_GELU_ACT) {
-          st8(gg, rc, off[0]);
-          st8(gg + 4, rc, off[1]);
+          st8(gg, rc, off);
         } else if constexpr (EPI == EPI_GELU) {
-          st8(v, rc, off[0]);
-          st8(v + 4, rc, off[1]);
-          st8(gg, rc2, off[0]);
-          st8(gg + 4, rc2, off[1]);
+          st8(v, rc, off);
+          st8(gg, rc2, off);
         } else {  // EPI_GELU_D: C = gelu', C2 = gelu
-          st8(dd, rc, off[0]);
-          st8(dd + 4, rc, off[1]);
-          st8(gg, rc2, off[0]);
-          st8(gg + 4, rc2, off[1]);
+          st8(dd, rc, off);
+          st8(gg, rc2, off);
         }
       }
     }
   };
 
   if (cur < nch) {
-    static_assert(NST == 4 && CH == 2, "the claim lookahead below is written for 4 stages and 2-tile chunks");
     // vmcnt bookkeeping: this wave's VMEM ops since the loop started, in issue order
     int seq = 0;
     auto dma_valid = [&](int ch, int k) { return ch < nch && ch * CH + k < nrt; };
@@ -1396,73 +1384,60 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
     }
     int after_c = seq;
     int st = 0;  // ring stage of the current position
-    // one step: the wait for this position's stage, B1, the DMA three positions ahead (tile tdma, or none),
-    // the previous position's epilogue (tile tepi; nrt = a dropped dummy that keeps the VMEM count fixed),
-    // the MFMAs, an optional hook before B2, B2, the staging write
     auto top = [&]() {
       wait_vmcnt_any(seq - after_a);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // B1: stage landed for every wave, staging tile published
+      __builtin_amdgcn_s_barrier();  // stage of this position landed for every wave
     };
-    auto body = [&](bool do_dma, int tdma, int tepi, auto&& before_b2) {
+    // One step: the DMA three positions ahead (tile tdma, or none), then the MFMAs and epilogue of this position
+    // (tile tcur), one 16-row block at a time.  Each SIMD holds one wave of each half of the workgroup; waves 0..3
+    // run [MFMA 0][MFMA 1][epilogue 0][epilogue 1], waves 4..7 [MFMA 0][epilogue 0][MFMA 1][epilogue 1], so
+    // each wave's epilogue (VALU, stores) runs beside its partner's MFMAs instead of both partners alternating
+    // the two in step (MI355X_MICROARCH.md, two waves per SIMD, item 9: split roles by wave number >= 4).
+    auto body = [&](bool do_dma, int tdma, int tcur, auto&& tail) {
       int st3 = st + 3;
       st3 = st3 >= NST ? st3 - NST : st3;
       after_a = after_b;
       after_b = after_c;
-      if (do_dma && PROBE != 4 && PROBE != 5) {
+      if (do_dma) {
         dma(st3, tdma);
         seq += PIECES;
       }
       after_c = seq;
-      if constexpr (PROBE != 1 && PROBE != 3 && PROBE != 4 && PROBE != 5) {
-        epilogue(tepi);
-        seq += ws_nstore<EPI>();
-      }
       f32x4 acc[2][3];
+      unsigned xb4[4];
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) acc[a][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      // the MFMA phase on this position's stage (ws_mfma_phase: fragment reads WS_PF ahead)
-      const char* As = smem + st * STAGE;
-      if constexpr (PROBE != 2 && PROBE != 3) {
-        unsigned xb4[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          xb4[k] = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(As + xbase[k]);
-        ws_mfma_phase(acc, wf, xb4);
+      for (int k = 0; k < 4; ++k)
+        xb4[k] = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(smem + st * STAGE + xbase[k]);
+      ws_mfma_half<0>(acc, wf, xb4);
+      if (late) {
+        epilogue(acc, tcur, 0);
+        ws_mfma_half<1>(acc, wf, xb4);
+      } else {
+        ws_mfma_half<1>(acc, wf, xb4);
+        epilogue(acc, tcur, 0);
       }
-      before_b2();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // B2: every wave has read the staging tile of the previous position
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-          *(f32x4*)(stg + (a * 16 + r) * SROW + (w * 48 + 16 * j + 4 * g) * 4) = acc[a][j];
+      epilogue(acc, tcur, 1);
+      seq += ws_nstore<EPI>();
+      tail();
       st = st + 1 == NST ? 0 : st + 1;
     };
     // one iteration = one chunk (positions 2 lc, 2 lc + 1).  The claim for chunk lc + 3 is issued at the first
     // position and consumed (published to LDS) at the end of the second, inside the iteration; the DMA of the
-    // first tile of chunk lc + 3 is issued at position 2 lc + 3, after the next iteration's first B1.
-    int last = 0;
+    // first tile of chunk lc + 3 is issued at position 2 lc + 3, after the next iteration's first barrier.
     for (int lc = 0;; ++lc) {
       top();
       if (lc > 0) {
-        prv = cur;
         cur = n1;
         n1 = n2;
         n2 = __builtin_amdgcn_readfirstlane(qring[(lc + 2) & (QN - 1)]);
-        if (cur >= nch) {
-          last = prv * CH + 1;
-          break;
-        }
+        if (cur >= nch) break;
       }
       const bool live = n2 < nch;
       const bool claimer = live && w == 0;  // wave-uniform
       int claimed = nch, after_claim = 0;
       if (claimer) {
-        if constexpr (PROBE >= 5) {
+        if constexpr (PROBE == 5) {
           claimed = (int)(blockIdx.x / ncg) + (lc + 3) * (int)(gridDim.x / ncg);
         } else {
           ws_claim_asm(ctr + cg, claimed);
@@ -1470,20 +1445,16 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
         }
         after_claim = seq;
       }
-      body(dma_valid(n1, 1), n1 * CH + 1, lc > 0 ? prv * CH + 1 : nrt, [] {});
+      body(dma_valid(n1, 1), n1 * CH + 1, cur * CH, [] {});
       top();
-      if (cur * CH + 1 >= nrt) {
-        last = cur * CH;
-        break;
-      }
-      body(dma_valid(n2, 0), n2 * CH, cur * CH, [&] {
+      if (cur * CH + 1 >= nrt) break;
+      body(dma_valid(n2, 0), n2 * CH, cur * CH + 1, [&] {
         if (w == 0) {  // publish chunk lc + 3 (nch: none claimed) for the iterations after this one
           if (claimer) wait_vmcnt_any(seq - after_claim);
           ws_publish_asm(qring + ((lc + 3) & (QN - 1)), claimed, lane);
         }
       });
     }
-    epilogue(last);  // the last position's staging tile was published by the final B1
   }
   // every claim of this workgroup has landed; the last workgroup out resets the counter block
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1606,21 +1577,12 @@ int launch_ws(int epi, hipStream_t stream, const NTArgs& a) {
   const int grid = per * ncg;
   const int slot = ws_slot(stream);
   static const int probe = getenv("ENDOSSL_WS_PROBE") ? atoi(getenv("ENDOSSL_WS_PROBE")) : 0;  // measurement only
-  if (probe && epi == EPI_BF16) {
-    switch (probe) {
-      case 1: WS_LAUNCH(EPI_BF16, 2, 1)
-      case 2: WS_LAUNCH(EPI_BF16, 2, 2)
-      case 3: WS_LAUNCH(EPI_BF16, 2, 3)
-      case 4: WS_LAUNCH(EPI_BF16, 2, 4)
-      case 5: WS_LAUNCH(EPI_BF16, 2, 5)
-      default: WS_LAUNCH(EPI_BF16, 2, 6)
-    }
-  }
+  if (probe == 5 && epi == EPI_BF16) WS_LAUNCH(EPI_BF16, 0, 5)
   switch (epi) {
-    case EPI_BF16: WS_LAUNCH(EPI_BF16, 2)
-    case EPI_GELU: WS_LAUNCH(EPI_GELU, 2)
-    case EPI_GELU_ACT: WS_LAUNCH(EPI_GELU_ACT, 2)
-    case EPI_GELU_D: WS_LAUNCH(EPI_GELU_D, 2)
+    case EPI_BF16: WS_LAUNCH(EPI_BF16, 0)
+    case EPI_GELU: WS_LAUNCH(EPI_GELU, 0)
+    case EPI_GELU_ACT: WS_LAUNCH(EPI_GELU_ACT, 0)
+    case EPI_GELU_D: WS_LAUNCH(EPI_GELU_D, 0)
     case EPI_F32: WS_LAUNCH(EPI_F32, 0)
     default: return ES_BAD_ARG;
   }

@@ -288,7 +288,8 @@ __global__ __launch_bounds__(256) void cls_head_wgrad_kernel(const float* __rest
                                                              const float* __restrict__ gamma,
                                                              const float* __restrict__ beta, float* __restrict__ dW,
                                                              float* __restrict__ db, float* __restrict__ dgamma,
-                                                             float* __restrict__ dbeta, int n, int C, int D) {
+                                                             float* __restrict__ dbeta, int n, int C, int D,
+                                                             int accumulate) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + lane, r = blockIdx.y;
@@ -306,12 +307,12 @@ __global__ __launch_bounds__(256) void cls_head_wgrad_kernel(const float* __rest
   if (w == 0) {
     const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
     float* dst = r < C ? dW + (size_t)r * D : (r == C ? dgamma : dbeta);
-    dst[d] += t;
+    dst[d] = accumulate ? dst[d] + t : t;
     if (blockIdx.x == 0 && r < C) {
       float sb = 0.f;
       for (int i = lane; i < n; i += 64) sb += dl[(size_t)i * lddl + r];
       sb = warp_sum(sb);
-      if (lane == 0) db[r] += sb;
+      if (lane == 0) db[r] = accumulate ? db[r] + sb : sb;
     }
   }
 }
@@ -454,18 +455,26 @@ int es_cls_head_fwd(const float* x, int ldx, int T, const float* gamma, const fl
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
 }
 
-// dx rows img*T receive the CLS gradient (caller zeroes the other rows); dW/db/dgamma/dbeta are
-// ACCUMULATED with atomics (caller zeroes them per step); dyn: scratch [n, D].
-int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
-                    const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW, float* db,
-                    float* dgamma, float* dbeta, int n, int D, int C, hipStream_t stream) {
+// dx rows img*T receive the CLS gradient (caller zeroes the other rows); dW/db/dgamma/dbeta are summed over
+// the batch in a fixed order and then ADDED to the buffers (es_cls_head_bwd) or WRITTEN over them
+// (es_cls_head_bwd_ex, accumulate = 0: the step's first writer of those entries, so the flat gradient needs no
+// zeroing launch); dyn: scratch [n, D].
+int es_cls_head_bwd_ex(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
+                       const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW,
+                       float* db, float* dgamma, float* dbeta, int n, int D, int C, int accumulate, hipStream_t stream) {
   if (n <= 0 || D % 64 || C <= 0 || C > 256) return ES_BAD_SHAPE;
   const int grid = (n + 3) / 4;
   HEAD_DISPATCH(cls_head_bwd_kernel, D / 64, grid, stream, dl, lddl, W, gamma, xhat, rstd, dyn, dx, lddx, T, n, C);
   dim3 g2(D / 64, C + 2);
   hipLaunchKernelGGL(cls_head_wgrad_kernel, g2, 256, 0, stream, dl, lddl, xhat, dyn, gamma, beta, dW, db, dgamma,
-                     dbeta, n, C, D);
+                     dbeta, n, C, D, accumulate ? 1 : 0);
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
+                    const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW, float* db,
+                    float* dgamma, float* dbeta, int n, int D, int C, hipStream_t stream) {
+  return es_cls_head_bwd_ex(dl, lddl, W, gamma, beta, xhat, rstd, dyn, dx, lddx, T, dW, db, dgamma, dbeta, n, D, C, 1,
+                            stream);
 }
 
 // CoMatch feature path: fts [n, D] = LN(x_cls) and its backward (dgamma / dbeta accumulated)

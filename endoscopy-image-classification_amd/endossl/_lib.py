@@ -63,6 +63,7 @@ SIGNATURES = {
     "es_embed_bwd": (I, [V, I, V, I, V, V, I, I, I, I, V]),
     "es_cls_head_fwd": (I, [V, I, I, V, V, V, V, V, I, V, V, I, I, I, F, V]),
     "es_cls_head_bwd": (I, [V, I, V, V, V, V, V, V, V, I, I, V, V, V, V, I, I, I, V]),
+    "es_cls_head_bwd_ex": (I, [V, I, V, V, V, V, V, V, V, I, I, V, V, V, V, I, I, I, I, V]),
     "es_cls_ln_fwd": (I, [V, I, I, V, V, V, I, V, V, I, I, F, V]),
     "es_cls_ln_bwd": (I, [V, I, V, V, V, V, I, I, V, V, I, I, V]),
     "es_dense_fwd": (I, [V, I, V, V, V, I, I, I, I, I, F, V, F, V]),
@@ -132,6 +133,7 @@ SIGNATURES = {
                                              V, V, V, V, V]),
     "es_chan_sum_ex": (I, [V, I, I, L, L, I, V, V, I, I, V]),
     "es_set_bn_cs": (I, [I]),
+    "es_set_bn_sum8": (I, [I]),
     "es_bn2d_fwd_ex": (I, [V, I, I, V, V, V, V, V, F, F, I, V, I, V, V, V, V, I, V]),
     "es_bn2d_bwd_ex": (I, [V, V, V, I, I, I, V, V, V, I, V, F, V, V, V, V, I, V, I, V]),
     "es_bn2d_bwd_recompute_ex": (I, [V, V, I, I, V, V, V, V, V, V, V, I, V, I, V]),

@@ -755,7 +755,11 @@ class Engine:
             evs = [main.record_event()] + ([done[i]] if i in done else [])
             grad_ready(lo, hi, evs)
 
-        if zero_grad:
+        # zero_grad: no zero fill of the flat gradient -- every entry of it is written by its first writer of the
+        # reverse pass (the head / final-norm kernel with accumulate = 0, the LayerNorm and weight-gradient
+        # reductions and the embedding backward overwrite); test_gpu_step.py checks a NaN-filled buffer.  The
+        # emb head's final-norm kernel (es_cls_ln_bwd) adds, so that path keeps the fill.
+        if zero_grad and cfg.head == "emb":
             grad.zero_()
         prune = self._prune()
         GL = GS[cfg.depth - 1] if grouped else GS[(cfg.depth - 1) % 2]
@@ -769,10 +773,10 @@ class Engine:
                  ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D, s)
         else:
             dlogits = dlogits.contiguous()
-            self._call("es_cls_head_bwd", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
+            self._call("es_cls_head_bwd_ex", ptr(dlogits), cfg.num_classes, ptr(fv("head.weight")), ptr(fv("norm.weight")),
                  ptr(fv("norm.bias")), ptr(A.xhat), ptr(A.rstd_cls), ptr(G.dyn), ptr(dtop), D, Tt,
                  ptr(gv("head.weight")), ptr(gv("head.bias")), ptr(gv("norm.weight")), ptr(gv("norm.bias")), n, D,
-                 cfg.num_classes, s)
+                 cfg.num_classes, 0 if zero_grad else 1, s)
         if self.capture is not None:
             self.capture("dtop", True, cfg.depth - 1, dtop[:n] if prune else G.dx[:M])
         if prune:

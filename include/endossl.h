@@ -190,6 +190,11 @@ int es_cls_head_fwd(const float* x, int ldx, int T, const float* gamma, const fl
 int es_cls_head_bwd(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
                     const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW, float* db,
                     float* dgamma, float* dbeta, int n, int D, int C, hipStream_t stream);
+/* the same with dW / db / dgamma / dbeta written (accumulate = 0) instead of added to (1): the first writer of
+ * those gradient entries in a step, so the flat gradient buffer needs no zero fill before the backward */
+int es_cls_head_bwd_ex(const float* dl, int lddl, const float* W, const float* gamma, const float* beta,
+                       const float* xhat, const float* rstd, float* dyn, float* dx, int lddx, int T, float* dW,
+                       float* db, float* dgamma, float* dbeta, int n, int D, int C, int accumulate, hipStream_t stream);
 
 /* CoMatch features: fts [n, D] = LN(x_cls) (ModelwEmb's `fts` over the ViT trunk,
  * code/models/custom_model.py:207-209) and its backward into the CLS rows of dx; dgamma / dbeta
@@ -446,6 +451,9 @@ int es_chan_sum_ex(const void* v, int rows, int C, long sn, long sp, int HW, flo
 /* tuning knob: 1 (default) = the channel-stationary BatchNorm apply kernels (forward apply and the backward's dx
  * pass), 0 = the per-iteration forms (bit-identical); returns the previous value, or -2 (unchanged) otherwise */
 int es_set_bn_cs(int v);
+/* test knob: 1 = the bf16 maps' BatchNorm channel sums over 8-channel groups (a different fp32 summation order of
+ * the same sums), 0 (default) = 4-channel groups; returns the previous value, or -2 (unchanged) otherwise */
+int es_set_bn_sum8(int v);
 int es_bn2d_fwd_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
                    float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const void* res,
                    int relu, void* y, float* mean, float* rstd, float* workspace, int flags, hipStream_t stream);

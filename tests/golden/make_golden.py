@@ -509,7 +509,9 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
     """SemiFormer.train_one SSL branch (code/semiformer.py:103-146) on a tiny Conformer: 64x64
     images, embed 128, 2 heads, depth 6 (one stride-1 ConvTransBlock, a stride-2 res_conv block and
     a stride-1 block at 2x channels, a stride-2 block and the last_fusion block at 4x channels),
-    CLS_WEIGHT on, two steps; records both heads' logits, losses, pseudo-labels and the state."""
+    CLS_WEIGHT on, two steps; records both heads' logits, losses, pseudo-labels and the state.
+    Round 6: B = 4, mu = 7 (28 unlabeled rows per step, BatchNorm statistics over 60 images: a loss that
+    is a meaningful sample), tau in the widest gap of the step-0 weak confidences near their median."""
     import pandas as pd
     from sklearn.utils import class_weight as skcw
     import semiformer as ref_semiformer
@@ -523,12 +525,12 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
                 p.copy_(1.0 + 0.1 * torch.randn_like(p))
             elif name.endswith("bias"):
                 p.copy_(0.02 * torch.randn_like(p))
-        model.conv_cls_head.weight.normal_(0.0, 0.12)  # peaky logits: some pseudo-labels pass the threshold
-        model.trans_cls_head.weight.normal_(0.0, 0.12)
+        model.conv_cls_head.weight.normal_(0.0, 0.45)  # peaky logits: weak confidences spread over (0, 1)
+        model.trans_cls_head.weight.normal_(0.0, 0.45)
         nn.init.trunc_normal_(model.cls_token, std=0.02)
     init_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
 
-    B, MU, C = 2, 2, 23
+    B, MU, C = 4, 7, 23
     g = torch.Generator().manual_seed(66)
     df_y = np.concatenate([np.full(i + 1, i) for i in range(C)])
     df = pd.DataFrame({"target": df_y})
@@ -540,7 +542,18 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
         us = torch.randn(B * MU, 3, 64, 64, generator=g)
         lab.append((x, y))
         unlab.append(((uw, us), torch.arange(B * MU)))
-    thres = 0.28  # between the weak rows' max-probabilities: mixed masks in both steps
+    # tau: the middle of the widest gap between consecutive step-0 weak max-probabilities (conv head, the
+    # reference's train-mode forward of [x; u_w; u_s] on a copy of the model) within their middle half, so about
+    # half the rows pass and no row sits near tau
+    import copy
+    probe = copy.deepcopy(model).train()
+    with torch.no_grad():
+        oc0 = probe(torch.cat([lab[0][0], unlab[0][0][0], unlab[0][0][1]]))[0]
+    pm = torch.softmax(oc0[B:B + B * MU], -1).max(-1).values.sort().values.numpy()
+    lo, hi = len(pm) // 4, 3 * len(pm) // 4
+    k = lo + int(np.argmax(pm[lo + 1:hi + 1] - pm[lo:hi]))
+    thres = float((pm[k] + pm[k + 1]) / 2)
+    print(f"semiformer: step-0 weak max-probs {np.round(pm, 4).tolist()} -> tau {thres:.4f}")
     cfg = ref_utils.AttrDict(
         DATA=ref_utils.AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
         MODEL=ref_utils.AttrDict(NAME="conformer", NUM_CLASSES=C, MARGIN="None", TYPE_SEMI="SemiFormer"),
@@ -562,11 +575,14 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
         rec["lx"].append(out.item())
         return out
 
+    rec["pmax"] = []
+
     def cons_spy(lw, ls, *a, **k):
         out = o_cons(lw, ls, *a, **k)
         rec["lu"].append(out[0].item())
         rec["mask_mean"].append(out[1].item())
         rec["pl"].append(torch.softmax(lw.detach(), -1).max(-1).indices.numpy())
+        rec["pmax"].append(torch.softmax(lw.detach(), -1).max(-1).values.numpy())
         return out
 
     def out_hook(mod, inp, out):
@@ -606,7 +622,9 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
             arrs["final_abs/" + k] = np.float64(final_sd[k].double().abs().sum().item())
             arrs["ema_sum/" + k] = np.float64(ema_sd[k].double().sum().item())
     np.savez_compressed(os.path.join(OUT, "semiformer_step.npz"), **arrs)
-    print(f"semiformer: lx={rec['lx']} lu={rec['lu']} mask={rec['mask_mean']} meter_sum={meter.sum:.6f}")
+    gaps = [float(np.abs(pmx - thres).min()) for pmx in rec["pmax"]]
+    print(f"semiformer: lx={rec['lx']} lu={rec['lu']} mask={rec['mask_mean']} meter_sum={meter.sum:.6f} "
+          f"closest |pmax - tau| per step {gaps}")
 
 
 def main():

@@ -318,7 +318,8 @@ def test_kernel_family_pins_refuse_removed_families():
                               ("es_set_conv_ring", (0, 3, 4), (1, 2, 5, -1)),
                               ("es_set_conv_dw_buf", (1, 0), (2, -1)),
                               ("es_set_conv_small", (128, 0, 64, 512), (-1, -5)),
-                              ("es_set_bn_cs", (1, 0), (2, -1))):
+                              ("es_set_bn_cs", (1, 0), (2, -1)),
+                              ("es_set_bn_sum8", (0, 1), (2, -1))):
         fn = getattr(lib, setter)
         base = fn(good[0])
         for v in bad:

@@ -653,6 +653,15 @@ def test_cls_head_fwd_bwd(n):
          ptr(dW2), ptr(db2), ptr(dg2), ptr(dbt2), n, D, C, S())  # accumulates (+=), like the atomics did
     torch.testing.assert_close(dW2, 2 * dW, rtol=1e-6, atol=1e-7)
     torch.testing.assert_close(db2, 2 * db, rtol=1e-6, atol=1e-7)
+    # es_cls_head_bwd_ex(accumulate = 0) writes the sums over whatever the buffers held (NaN here): the bits of
+    # the accumulate-onto-zero form
+    nanf = lambda t: torch.full_like(t, float("nan"))  # noqa: E731
+    dW3, db3, dg3, dbt3 = nanf(W), nanf(b), nanf(gamma), nanf(beta)
+    call("es_cls_head_bwd_ex", ptr(dl), C, ptr(W), ptr(gamma), ptr(beta), ptr(xhat), ptr(rstd), ptr(dyn), ptr(dx), D,
+         T, ptr(dW3), ptr(db3), ptr(dg3), ptr(dbt3), n, D, C, 0, S())
+    torch.cuda.synchronize()
+    for a, c in ((dW, dW3), (db, db3), (dg, dg3), (dbt, dbt3)):
+        assert torch.equal(a, c)
 
 
 def test_embed_bwd():

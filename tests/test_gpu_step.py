@@ -373,6 +373,47 @@ def test_shard_lanes_match_single_lane(nimg, prune, full):
     assert worst_ln <= 1e-6, worst_ln
 
 
+@pytest.mark.parametrize("mode,nimg,prune", [("grouped", 40, True), ("split", 40, True), ("split", 38, False),
+                                             ("layer", 88, True)])
+def test_backward_writes_every_gradient_entry(mode, nimg, prune):
+    """Engine.backward(zero_grad=True) launches no zero fill of the flat gradient: every entry is written by its
+    first writer of the reverse pass (head / final norm with accumulate = 0, the LayerNorm and weight-gradient
+    reductions, the embedding backward).  A NaN-filled and a zero-filled buffer must come out BIT-identical and
+    finite, on the small-shard grouped path, the split-K side-stream path (with and without the CLS-row last
+    block) and the per-block grouped split-K path of ViT-S/16 at 224^2 (M = 17,336 train tokens)."""
+    from endossl.vit import NativeViT, ViTConfig
+    vcfg, _ = _tiny_cfgs()
+    if mode == "layer":
+        vcfg = ViTConfig(num_classes=23)
+    m = NativeViT(vcfg, seed=12)
+    with torch.no_grad():  # a non-zero head (timm zero-inits it): otherwise every trunk gradient is exactly zero
+        m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(3)))
+    m.mark_updated()
+    m = m.to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    eng.GROUP_WGRAD = "1" if mode == "grouped" else "0"
+    eng.PRUNE_LAST = prune
+    g = torch.Generator(device=DEV).manual_seed(6)
+    S = vcfg.img_size
+    x = torch.randn(nimg, 3, S, S, device=DEV, generator=g)
+    dl = torch.randn(nimg, 23, device=DEV, generator=g) * 1e-2
+    grads = {}
+    for fill in (0.0, float("nan")):
+        eng.forward(m.flat, [x], train=True)
+        gr = torch.full_like(m.flat, fill)
+        eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        grads[fill == 0.0] = gr
+    for k in ("GROUP_WGRAD", "PRUNE_LAST"):
+        delattr(eng, k)
+    for name, _ in eng.layout:
+        a, b = eng.view(grads[False], name), eng.view(grads[True], name)
+        assert torch.isfinite(a).all(), name
+        assert torch.equal(a, b), name
+    assert eng.view(grads[True], "blocks.0.attn.qkv.weight").abs().max() > 0  # not vacuous
+
+
 @pytest.mark.parametrize("mode,nimg", [("grouped", 40), ("grouped", 64), ("layer", 88)])
 def test_deferred_ln_grads_bit_identical(mode, nimg):
     """Engine.DEFER_LN_GRADS (each LayerNorm backward's dgamma / dbeta partials kept, reduced by one
