@@ -23,8 +23,6 @@
 // batch amplifies operand noise, the same effect as CoMatch's BatchNorm1d head).
 #include <numeric>
 
-#include <type_traits>
-
 #include "common.h"
 
 namespace {
@@ -825,7 +823,7 @@ inline int cs_grid(long nv, int CV) {
   return g;
 }
 int g_bn_cs = 1;  // es_set_bn_cs: the channel-stationary BatchNorm applies (0: the per-iteration forms)
-int g_bn_sum8 = 0;  // es_set_bn_sum8: 8-channel groups in the bf16 maps' channel sums (a test knob: another order)
+int g_bn_sum8 = 0;  // es_set_bn_sum8: 8-channel groups in the BatchNorm channel sums (a test knob: another order)
 
 // eval-mode BatchNorm backward is an affine map: dx = g * gamma * rstd_running (not on the training
 // path; kept for completeness of the autograd surface)
@@ -1671,10 +1669,10 @@ template <int MODE, typename T>
 void chan_partial_launch(bool v4, int G, const T* v, RowMap rm, int rows, int C, int per, const float* mean,
                          const float* rstd, const T* dy, const T* y, int relu, float* ws, hipStream_t stream,
                          const float* gamma = nullptr, const float* beta = nullptr) {
-  // es_set_bn_sum8(1): bf16 maps summed in 8-channel groups (16-byte loads): another fp32 summation order of the
-  // same channel sums (a thread's rows and the row-lane count change), kept as a test knob -- round 5 measured
+  // es_set_bn_sum8(1): the maps summed in 8-channel groups (bf16: 16-byte loads): another fp32 summation order of
+  // the same channel sums (a thread's rows and the row-lane count change), kept as a test knob -- round 5 measured
   // no gain -- so that the trainer-level parity bars are checked against a legitimate reordering
-  if (std::is_same<T, bf16>::value && g_bn_sum8 && v4 && C % 8 == 0 && rm.sn % 8 == 0 && rm.sp % 8 == 0) {
+  if (g_bn_sum8 && v4 && C % 8 == 0 && rm.sn % 8 == 0 && rm.sp % 8 == 0) {
     if (MODE == 2 && relu && !y)
       hipLaunchKernelGGL((chan_partial_kernel<MODE, 8, T, true>), G, 256, 0, stream, v, rm, rows, C, per, mean, rstd,
                          dy, y, relu, ws, gamma, beta);
@@ -1933,7 +1931,7 @@ int es_set_bn_cs(int v) {
   return old;
 }
 
-// test knob: 1 = the bf16 maps' BatchNorm channel sums over 8-channel groups (16-byte loads; a different fp32
+// test knob: 1 = the BatchNorm channel sums (chan_partial_kernel) over 8-channel groups (a different fp32
 // summation order of the same sums), 0 (default) = 4-channel groups; returns the previous value, or ES_BAD_ARG
 // (unchanged) for any other value
 int es_set_bn_sum8(int v) {

@@ -1144,24 +1144,31 @@ int reduce_partials_multi(const RedPairEntry* ents, int n, hipStream_t stream) {
 // their pace.  Here one persistent 8-wave workgroup per CU owns a 384-column group of C and
 // keeps that group's weight rows in REGISTERS for the whole launch: wave w holds W[n0 + 48 w .. + 48][0 .. 384)
 // as the MFMA A operand (3 column fragments x 12 K fragments of v_mfma_f32_16x16x32_bf16 = 144 VGPRs).  The
-// workgroup walks 32-row tiles of A; each tile is staged into LDS once by LDS-DMA (3-stage ring, 24 KiB per
+// workgroup walks 32-row tiles of A; each tile is staged into LDS once by LDS-DMA (4-stage ring, 24 KiB per
 // stage, source-side XOR swizzle: chunk c of row r at chunk c ^ (r & 15), conflict-free fragment reads) and
 // consumed by all eight waves, so the L2 -> LDS stream carries 768 B per 384 outputs (2 B per output).
 //   Accumulation: each output is the same chain of 12 MFMAs in K order, with the same operand roles (weights as
 // the A operand, activations as B) as the tiled kernels, so the fp32 accumulators -- and every epilogue's
 // outputs -- are bit-identical to variants 0 / 5 / 10 (tested).
-//   Epilogue: the 32 x 384 fp32 tile (accumulator + bias) goes through one LDS staging tile (rows padded by
-//   16 B: conflict-free MFMA-layout writes), read back one step later as whole rows, 16 B per lane, so every
-//   C store instruction covers contiguous 512-B (bf16) or 1-KiB (fp32) row stretches.  Per step:
-//     [vmcnt: tile i landed] [B1] [DMA tile i + 2] [epilogue of tile i - 1] [MFMAs of tile i] [B2] [staging write]
-//   B1 publishes the ring stage and the staging tile, B2 keeps the staging writes behind every wave's reads.
-//   Work distribution: row tiles are claimed dynamically, in chunks of 2, from a per-column-group counter
-//   (agent-scope atomics on a code-object array, one counter block per HIP stream; the last workgroup to finish
-//   resets it), two chunks ahead of use.  A static split would be wrong for this engine: the data-gradient
-//   GEMMs share the chip with the weight-gradient launches of the side stream (3/8 of the CUs for ~1 ms), so a
-//   workgroup that only gets a CU late must find the work already taken instead of extending the launch.
-//   All ring DMA is inline asm (glds16_asm): the explicit counted vmcnt at the top of each step retires it (the
-//   count follows every VMEM op this wave issued since, in issue order: claim atomics, DMA pieces, C stores).
+//   Epilogue: straight from the MFMA layout, one 16-row block at a time, interleaved with the other block's
+//   MFMAs by wave role (see the step body).  An LDS-staged epilogue (whole 768-B row stretches per store,
+//   double-buffered staging tiles) was built and measured too: bit-identical, but slower (qkv forward 133.7
+//   vs 122 us direct); so was the first version, a single fp32 staging tile behind a second barrier per step
+//   (119-126 us).
+//   Work distribution: row tiles are claimed dynamically, in chunks of 2, from per-(XCD range, column group)
+//   counters (agent-scope atomics on a code-object array, one counter block per HIP stream; the last workgroup
+//   to finish resets it), three chunks ahead of use.  A static split would be wrong for this engine: the
+//   data-gradient GEMMs share the chip with the weight-gradient launches of the side stream (3/8 of the CUs for
+//   ~1 ms), so a workgroup that only gets a CU late must find the work already taken instead of extending the
+//   launch.  All ring DMA is inline asm (glds16_asm): the explicit counted vmcnt at the top of each step retires
+//   it (the count follows every VMEM op this wave issued since, in issue order: claim atomics, DMA pieces, C
+//   stores).
+//   Measured (scripts/ws_bench.py, default rules vs variant 12, us): qkv forward 108 / 123, weak qkv 91 / 100,
+//   fc1 forward 190 / 246, weak fc1 154 / 162, proj dgrad 40 / 51, fp32-out N = 384 61 / 50.  So variant 12
+//   stays opt-in: per-step stamps (PROBE 7) show a wave's step ~6.4 K cycles with ~1.9 K waiting on its ring
+//   stage and each MFMA half ~1 K, and a no-MFMA probe streams the same bytes in 67 us -- the chain of ring
+//   wait, fragment reads and MFMAs per 32-row step, not HBM, sets the pace, and one workgroup per CU (the
+//   weights fill the registers) leaves no second workgroup to cover it.
 namespace wsg {
 constexpr int R = 32;                      // output rows per step (one A tile)
 constexpr int KD = 384;                    // reduction depth
@@ -1172,11 +1179,14 @@ constexpr int NST = 4;                     // ring stages (three tiles in flight
 constexpr int PIECES = STAGE / 1024 / 8;   // LDS-DMA instructions per wave per stage
 constexpr int CH = 2;                      // row tiles per claimed chunk
 constexpr int QN = 8;                      // chunk-index ring (LDS)
-constexpr int SLOTS = 64, SLOT_INTS = 16;  // counter blocks (one per stream): [0, ncg) claim heads, [15] done
-constexpr int LDS = NST * STAGE + QN * 4 + NG * 4;  // ring, chunk ring, the column group's bias
+constexpr int SLOTS = 64, SLOT_INTS = 64;  // counter blocks (one per stream): heads [xcd * 8 + cg], [63] done
+constexpr int LDS = NST * STAGE + QN * 4 + 16 + NG * 4;  // ring, chunk ring, scratch, the column group's bias
 }  // namespace wsg
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ int g_ws_ctr[wsg::SLOTS * wsg::SLOT_INTS];
+// measurement build (PROBE 7): per-step s_memtime stamps of workgroup 0's waves 0 and 4 (endossl_ws_debug_stamps)
+constexpr int WS_DBG = 2 * 64 * 8;
+__device__ unsigned long long g_ws_dbg[WS_DBG];
 
 // A chunk claim: one lane's returning agent-scope add (the same instruction hipcc emits for
 // __hip_atomic_fetch_add(.., __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), as inline asm so that hipcc neither
@@ -1256,6 +1266,22 @@ __device__ __forceinline__ void ws_mfma_half(f32x4 (&acc)[2][3], const bf16x8 (&
   ws_mfma_loop<A, 0>(acc, wf, xb4, xs);
 }
 
+// Row chunks are split into 8 contiguous ranges, one per XCD: a workgroup claims from its own XCD's range of its
+// column group first (the column groups of one XCD then stream the same A rows, which its L2 serves to all but
+// the first), then from the next XCDs' ranges once its own is exhausted.  One lane; blocking (the prologue's claims
+// and the rare range switch at the end of a range).
+__device__ __forceinline__ int ws_range_lo(int xr, int nch) { return (xr * nch) >> 3; }
+__device__ int ws_claim_blocking(int* heads, int cg, int& xr, int& visited, int nch) {
+  while (visited < 8) {
+    const int lo = ws_range_lo(xr, nch), len = ws_range_lo(xr + 1, nch) - lo;
+    const int r = __hip_atomic_fetch_add(heads + xr * 8 + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (r < len) return lo + r;
+    xr = (xr + 1) & 7;
+    ++visited;
+  }
+  return nch;
+}
+
 template <int EPI>
 constexpr bool ws_epi_ok() {
   return EPI == EPI_BF16 || EPI == EPI_GELU || EPI == EPI_GELU_ACT || EPI == EPI_GELU_D || EPI == EPI_F32;
@@ -1273,7 +1299,7 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   static_assert(NST == 4 && CH == 2, "the claim lookahead below is written for 4 stages and 2-tile chunks");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int* const qring = (int*)(smem + NST * STAGE);
-  float* const bias_lds = (float*)(qring + QN);  // the column group's bias
+  float* const bias_lds = (float*)(qring + QN + 4);  // the column group's bias (after 4 scratch words)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, r = lane & 15;
@@ -1283,15 +1309,22 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   const int n0 = cg * NG, nw = n0 + w * 48;
   const bool late = w >= 4;  // waves 4..7 interleave their epilogue differently (see the step body)
 
+  // claim state (wave 0): the XCD range claimed from and how many ranges were found exhausted
+  int xr;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xr));
+  xr &= 7;
+  int visited = 0;
   // the first three chunks: blocking claims (their latency hides behind the weight loads below)
   if (tid == 0) {
     if constexpr (PROBE == 5) {  // measurement: static chunks rs, rs + nrs, ... (no claims)
       const int rs = blockIdx.x / ncg, nrs = gridDim.x / ncg;
       qring[0] = rs; qring[1] = rs + nrs; qring[2] = rs + 2 * nrs;
     } else {
-      qring[0] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      qring[1] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      qring[2] = __hip_atomic_fetch_add(ctr + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      qring[0] = ws_claim_blocking(ctr, cg, xr, visited, nch);
+      qring[1] = ws_claim_blocking(ctr, cg, xr, visited, nch);
+      qring[2] = ws_claim_blocking(ctr, cg, xr, visited, nch);
+      qring[QN + 0] = xr;  // (the bias follows the ring: these two words are scratch before it is written)
+      qring[QN + 1] = visited;
     }
   }
   bf16x8 wf[3][12];
@@ -1303,6 +1336,10 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   if (tid < NG / 4)
     *(f32x4*)(bias_lds + 4 * tid) = p.bias ? *(const f32x4*)(p.bias + n0 + 4 * tid) : f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // weights, bias and the first claims retired (no compiler-counted load crosses into the loop)
+  if constexpr (PROBE != 5) {
+    xr = __builtin_amdgcn_readfirstlane(qring[QN + 0]);
+    visited = __builtin_amdgcn_readfirstlane(qring[QN + 1]);
+  }
   int cur = __builtin_amdgcn_readfirstlane(qring[0]);  // chunk of the current iteration, and the two after it
   int n1 = __builtin_amdgcn_readfirstlane(qring[1]);
   int n2 = __builtin_amdgcn_readfirstlane(qring[2]);
@@ -1384,7 +1421,12 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
     }
     int after_c = seq;
     int st = 0;  // ring stage of the current position
+    int nstep = 0;
     auto top = [&]() {
+      if constexpr (PROBE == 7) {
+        if (blockIdx.x == 0 && (w == 0 || w == 4) && lane == 0 && nstep < 64)
+          g_ws_dbg[((w >> 2) * 64 + nstep) * 8 + 7] = __builtin_amdgcn_s_memtime();
+      }
       wait_vmcnt_any(seq - after_a);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // stage of this position landed for every wave
@@ -1394,7 +1436,14 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
     // run [MFMA 0][MFMA 1][epilogue 0][epilogue 1], waves 4..7 [MFMA 0][epilogue 0][MFMA 1][epilogue 1], so
     // each wave's epilogue (VALU, stores) runs beside its partner's MFMAs instead of both partners alternating
     // the two in step (MI355X_MICROARCH.md, two waves per SIMD, item 9: split roles by wave number >= 4).
+    auto stamp = [&](int k) {
+      if constexpr (PROBE == 7) {
+        if (blockIdx.x == 0 && (w == 0 || w == 4) && lane == 0 && nstep < 64)
+          g_ws_dbg[((w >> 2) * 64 + nstep) * 8 + k] = __builtin_amdgcn_s_memtime();
+      }
+    };
     auto body = [&](bool do_dma, int tdma, int tcur, auto&& tail) {
+      stamp(0);
       int st3 = st + 3;
       st3 = st3 >= NST ? st3 - NST : st3;
       after_a = after_b;
@@ -1409,18 +1458,26 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         xb4[k] = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(smem + st * STAGE + xbase[k]);
+      stamp(1);
       ws_mfma_half<0>(acc, wf, xb4);
+      stamp(2);
       if (late) {
         epilogue(acc, tcur, 0);
+        stamp(3);
         ws_mfma_half<1>(acc, wf, xb4);
       } else {
         ws_mfma_half<1>(acc, wf, xb4);
+        stamp(3);
         epilogue(acc, tcur, 0);
       }
+      stamp(4);
       epilogue(acc, tcur, 1);
+      stamp(5);
       seq += ws_nstore<EPI>();
       tail();
+      stamp(6);
       st = st + 1 == NST ? 0 : st + 1;
+      ++nstep;
     };
     // one iteration = one chunk (positions 2 lc, 2 lc + 1).  The claim for chunk lc + 3 is issued at the first
     // position and consumed (published to LDS) at the end of the second, inside the iteration; the DMA of the
@@ -1440,7 +1497,7 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
         if constexpr (PROBE == 5) {
           claimed = (int)(blockIdx.x / ncg) + (lc + 3) * (int)(gridDim.x / ncg);
         } else {
-          ws_claim_asm(ctr + cg, claimed);
+          ws_claim_asm(ctr + xr * 8 + cg, claimed);
           seq += 1;
         }
         after_claim = seq;
@@ -1450,8 +1507,29 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
       if (cur * CH + 1 >= nrt) break;
       body(dma_valid(n2, 0), n2 * CH, cur * CH + 1, [&] {
         if (w == 0) {  // publish chunk lc + 3 (nch: none claimed) for the iterations after this one
-          if (claimer) wait_vmcnt_any(seq - after_claim);
-          ws_publish_asm(qring + ((lc + 3) & (QN - 1)), claimed, lane);
+          int chunk = nch;
+          if (claimer) {
+            wait_vmcnt_any(seq - after_claim);
+            asm volatile("" : "+v"(claimed));  // (ordered after the wait: the claim's data is in lane 0)
+            const int raw = __builtin_amdgcn_readfirstlane(claimed);
+            if constexpr (PROBE == 5) {
+              chunk = raw;
+            } else {
+              const int lo = ws_range_lo(xr, nch), len = ws_range_lo(xr + 1, nch) - lo;
+              if (raw < len) {
+                chunk = lo + raw;
+              } else {  // this XCD's range is exhausted: the next ones (blocking; once per range at its end)
+                xr = (xr + 1) & 7;
+                ++visited;
+                int c2 = nch, x2 = xr, v2 = visited;
+                if (lane == 0) c2 = ws_claim_blocking(ctr, cg, x2, v2, nch);
+                chunk = __builtin_amdgcn_readfirstlane(c2);
+                xr = __builtin_amdgcn_readfirstlane(x2);
+                visited = __builtin_amdgcn_readfirstlane(v2);
+              }
+            }
+          }
+          if (lane == 0) qring[(lc + 3) & (QN - 1)] = chunk;
         }
       });
     }
@@ -1461,7 +1539,8 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   if (tid == 0) {
     const int d = __hip_atomic_fetch_add(ctr + SLOT_INTS - 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == (int)gridDim.x - 1) {
-      for (int c = 0; c < ncg; ++c) __hip_atomic_store(ctr + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int x = 0; x < 8; ++x)
+        for (int c = 0; c < ncg; ++c) __hip_atomic_store(ctr + x * 8 + c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(ctr + SLOT_INTS - 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -1555,7 +1634,7 @@ static int ws_slot(hipStream_t s) {
 }
 static bool ws_fits(int epi, int N, int K) {
   const bool e = epi == EPI_BF16 || epi == EPI_GELU || epi == EPI_GELU_ACT || epi == EPI_GELU_D || epi == EPI_F32;
-  return e && K == wsg::KD && N % wsg::NG == 0 && N / wsg::NG < wsg::SLOT_INTS;
+  return e && K == wsg::KD && N % wsg::NG == 0 && N / wsg::NG <= 8;
 }
 #define WS_LAUNCH(E, AUX_, ...)                                                                                   \
   {                                                                                                                \
@@ -1578,6 +1657,7 @@ int launch_ws(int epi, hipStream_t stream, const NTArgs& a) {
   const int slot = ws_slot(stream);
   static const int probe = getenv("ENDOSSL_WS_PROBE") ? atoi(getenv("ENDOSSL_WS_PROBE")) : 0;  // measurement only
   if (probe == 5 && epi == EPI_BF16) WS_LAUNCH(EPI_BF16, 0, 5)
+  if (probe == 7 && epi == EPI_BF16) WS_LAUNCH(EPI_BF16, 0, 7)
   switch (epi) {
     case EPI_BF16: WS_LAUNCH(EPI_BF16, 0)
     case EPI_GELU: WS_LAUNCH(EPI_GELU, 0)
@@ -1599,6 +1679,12 @@ static int g_small_tile = 1;  // the 64 x 128 tile rules (es_set_gemm_small_tile
 
 
 extern "C" {
+
+// measurement builds only (ENDOSSL_WS_PROBE=7): the weight-stationary kernel's step stamps (not part of the es_ ABI)
+int endossl_ws_debug_stamps(unsigned long long* host, int n) {
+  if (n > WS_DBG) n = WS_DBG;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_dbg), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -3;
+}
 
 int es_gemm_tn_ex(const void* A1, int ld1, const void* A2, int ld2, int M, int N1, int N2, int splits,
                   float* workspace, float* out, int accumulate, float* bias_out, int variant, hipStream_t stream);

@@ -451,8 +451,8 @@ int es_chan_sum_ex(const void* v, int rows, int C, long sn, long sp, int HW, flo
 /* tuning knob: 1 (default) = the channel-stationary BatchNorm apply kernels (forward apply and the backward's dx
  * pass), 0 = the per-iteration forms (bit-identical); returns the previous value, or -2 (unchanged) otherwise */
 int es_set_bn_cs(int v);
-/* test knob: 1 = the bf16 maps' BatchNorm channel sums over 8-channel groups (a different fp32 summation order of
- * the same sums), 0 (default) = 4-channel groups; returns the previous value, or -2 (unchanged) otherwise */
+/* test knob: 1 = the BatchNorm channel sums over 8-channel groups (a different fp32 summation order of the same
+ * sums), 0 (default) = 4-channel groups; returns the previous value, or -2 (unchanged) otherwise */
 int es_set_bn_sum8(int v);
 int es_bn2d_fwd_ex(const void* x, int rows, int C, const float* gamma, const float* beta, float* running_mean,
                    float* running_var, void* num_batches_tracked, float momentum, float eps, int train, const void* res,

@@ -88,6 +88,19 @@ def main():
             row[f"v{v}_us"] = round(t * 1000, 1)
         res[name] = row
         print(name, json.dumps(row), flush=True)
+    if os.environ.get("ENDOSSL_WS_PROBE") == "7":  # per-step stamps of workgroup 0 (waves 0 and 4), last launch
+        import ctypes
+        buf = (ctypes.c_ulonglong * 1024)()
+        lib.endossl_ws_debug_stamps(buf, 1024)
+        st = [list(buf[i * 8:(i + 1) * 8]) for i in range(128)]
+        for half, name in ((0, "wave0"), (1, "wave4")):
+            rows = [r for r in st[half * 64:(half + 1) * 64] if r[0]]
+            for i, r in enumerate(rows[:16]):
+                # k: 7 top start, 0 after barrier, 1 after DMA issue, 2 after MFMA half 0, 3 after 2nd part,
+                # 4 after 3rd part, 5 after last epilogue, 6 after tail
+                print(name, i, "top-wait", r[0] - r[7], "dma", r[1] - r[0], "mfma0", r[2] - r[1], "part2", r[3] - r[2],
+                      "part3", r[4] - r[3], "epi1", r[5] - r[4], "tail", r[6] - r[5],
+                      "step", (rows[i + 1][7] - r[7]) if i + 1 < len(rows) else 0)
     lib.es_set_gemm_variant(-1)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(res, open(os.path.join(ROOT, "gpurun_out", "ws_bench.json"), "w"), indent=1)

@@ -953,8 +953,9 @@ def test_semiformer_trainer_vs_reference_train_one(golden, conv, sum8):
     """The SemiFormer trainer over the fixture's steps (round 6 fixture: B = 4, mu = 7 -- 28 unlabeled rows,
     BatchNorm statistics over 60 images).  kc / kr / kd: the tolerance factors on the bf16 envelope; with bf16
     convs the device is an independent bf16 sample (see _check_model_vs_oracle), so it is held to the envelope
-    itself rather than a fraction of it.  sum8: the bf16 maps' BatchNorm channel sums in the other fp32
-    summation order (es_set_bn_sum8) -- a legitimate reordering must pass the same bars."""
+    itself rather than a fraction of it.  sum8: the BatchNorm channel sums in the other fp32 summation order
+    (es_set_bn_sum8: 8-channel groups, round 5's reverted change) -- a legitimate reordering must pass the
+    same bars."""
     import pandas as pd
     from endossl.semiformer import SemiFormer
     from endossl.utils import AttrDict
