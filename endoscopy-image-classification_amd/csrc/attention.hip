@@ -1735,7 +1735,7 @@ int g_attn_bwd_pipe = 4;
 // the same variants for T = 577 (the 37-tile kernels: one 151-KiB head per CU, four waves)
 int g_attn_bwd_long = 1;
 // the single pass's grid: -1 (default) = max(CUs, heads / 4), 0 = one persistent workgroup per CU, else this
-// many.  Inside the two-stream F1 step (scripts/gpu_ab_attnv.sh, profiles/r04_attn_bwd_live_ab.txt) a head
+// many.  Inside the two-stream F1 step (profiles/r04_attn_bwd_live_ab.txt) a head
 // or two per workgroup lets the side stream's weight-gradient launches take CUs between them, twelve per
 // workgroup (one per CU) holds the CUs: 3072 heads on 768 workgroups 30.78-30.80 ms/step, 1024: 30.86-30.90,
 // 1536: 30.80-30.87, 3072: 31.05-31.09, 256: +0.5 ms, the two-pass kernels 30.95-31.03 (one box)

@@ -788,7 +788,7 @@ inline bool st4(long a, long b, long c) { return a % 4 == 0 && b % 4 == 0 && c %
 // ~8 workgroups per CU over the pixel splits (the small-tile shapes are load-latency bound: occupancy hides
 // it); every split writes an fp32 slab of the whole weight gradient that convb_dw_reduce_kernel sums, so
 // fewer, longer splits trade occupancy for slab traffic (es_set_conv_dw_target).  S1, one box, interleaved
-// twice (scripts/gpu_s1ab.sh): 2048 -> 144.4 / 145.4 ms/step, 1024 -> 143.0 / 143.8, 512 -> 143.2 / 142.6
+// twice (bench.py --workload s1, round 4): 2048 -> 144.4 / 145.4 ms/step, 1024 -> 143.0 / 143.8, 512 -> 143.2 / 142.6
 int g_dw_target_wg = 512;
 constexpr int DW_MAX_SPLITS = 1024;
 

@@ -1571,7 +1571,7 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   }
 // The residual-stream outputs (EPI_F32_RESID: the proj / fc2 forward's x + f(x), read right away by the
 // next LayerNorm) keep plain, cacheable C stores instead of nt: F1 30.82 / 30.84 -> 30.59 / 30.66 ms on one
-// box (scripts/gpu_storeplain.sh); plain stores for the qkv (EPI_BF16) or fc1 (EPI_GELU_D) outputs were
+// box (bench.py A/B, round 3); plain stores for the qkv (EPI_BF16) or fc1 (EPI_GELU_D) outputs were
 // slower (30.90 / 31.03 ms).
 int launch_nt(int cfg, int epi, int grid, hipStream_t stream, const NTArgs& a) {
   if (cfg == 11 && epi == EPI_F32_RESID) NT_LAUNCH(EPI_F32_RESID, 64, 2, 64, 0)

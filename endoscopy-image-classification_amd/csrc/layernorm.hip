@@ -304,7 +304,7 @@ static int ln_bwd_launch(const DY* dy, int lddy, const float* x, int ldx, const 
 }
 
 // > 0 (default 2048): the grid-stride forward on this many workgroups when the one-shot grid would be larger;
-// 0: the one-shot kernel.  F1 same box, interleaved three times (scripts/gpu_ab_knobs3.sh): 0 30.51 ms/step
+// 0: the one-shot kernel.  F1 same box, interleaved three times (bench.py A/B, round 5): 0 30.51 ms/step
 // mean, 1024 30.42, 2048 30.28, 4096 30.30; isolated at F1's LN2 (scripts/ln_bench.py, x L3-resident) the
 // one-shot kernel is faster (35.1 vs 37.9 us): the gain is in the two-stream step, where 12,608 short-lived
 // workgroups per launch interleave worse with the other stream's kernels

@@ -204,7 +204,7 @@ _branch_streams = {}
 # the launch count (the small-batch P0 / shard steps are launch-bound), not for a measured gain
 CONV_PACK_MULTI = True
 # HIP priorities of the branch stream and the weight-gradient stream (0 = the default stream's, -1 = higher).
-# S1 same box (scripts/gpu_prio.sh, profiles/r04_stream_priority.txt): both 0 139.81 / 140.01 ms, branch -1
+# S1 same box (profiles/r04_stream_priority.txt): both 0 139.81 / 140.01 ms, branch -1
 # 139.53 / 139.00, weight gradients -1 140.26 / 139.92, both -1 139.21 / 139.20
 BRANCH_PRIORITY = -1
 WGRAD_PRIORITY = 0

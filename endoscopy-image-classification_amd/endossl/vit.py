@@ -31,8 +31,8 @@ EPI_BF16, EPI_GELU, EPI_F32_RESID, EPI_DGELU, EPI_F32, EPI_PATCH, EPI_GELU_ACT, 
 # LayerNorm backward workgroups (grid-stride over row pairs; per-workgroup dgamma / dbeta partials)
 LN_BWD_BLOCKS = 1024
 # HIP priority of the second stream (weak forward, overlapped weight gradients) for steps of at least
-# SIDE_PRIORITY_MIN_M train tokens (below it: 0, the default stream's).  Same-box A/Bs (scripts/gpu_ab_knobs3.sh,
-# scripts/gpu_prio.sh, profiles/r04_stream_priority.txt): F1 (100,864 tokens) -1 vs 0 30.34 / 30.33 / 30.22 vs
+# SIDE_PRIORITY_MIN_M train tokens (below it: 0, the default stream's).  Same-box A/Bs (profiles/r04_stream_priority.txt,
+# DESIGN.md §5): F1 (100,864 tokens) -1 vs 0 30.34 / 30.33 / 30.22 vs
 # 30.59 / 30.51 / 30.39 ms; the N = 8 shard (12,608) 5.35 / 5.36 vs 5.32 / 5.31
 SIDE_PRIORITY = -1
 SIDE_PRIORITY_MIN_M = 65536

@@ -96,5 +96,30 @@ if os.path.exists(tr):
               "launch (whole chip, the end of the backward) and the patch embedding's are other grid sizes above."
               + site + " Durations under the profiler run at lower clocks (MI355X_MICROARCH.md 'DVFS give-back' "
               "item 2)."]
+    if benchlog and os.path.exists(benchlog):
+        # the timed steps alone: every launch that starts after the warm-up's last optimizer launch and ends by the
+        # last timed one (the process's allocations, warm-up, isolated-roofline and probe launches excluded)
+        import json
+        line = json.loads([x for x in open(benchlog) if x.startswith('{"metric')][-1])
+        w, k = line["warmup"], line["steps"]
+        bounds = [int(r["End_Timestamp"]) for r in rows if "adam_ema_kernel(" in r["Kernel_Name"]]
+        t0, t1 = (bounds[w - 1] if w > 0 else 0), bounds[w + k - 1]
+        inside = [r for r in rows if t0 < int(r["Start_Timestamp"]) and int(r["End_Timestamp"]) <= t1]
+        fills_in = sum(1 for r in inside if "FillFunctor" in r["Kernel_Name"])
+        fills_all = sum(1 for r in rows if "FillFunctor" in r["Kernel_Name"])
+        agg2 = collections.defaultdict(lambda: [0, 0.0])
+        for r in inside:
+            name = re.sub(r"\(anonymous namespace\)::|es_gemm::|void ", "", r["Kernel_Name"])
+            name = re.sub(r"\((?!anon).*", "", name)[:90].replace("|", "/")
+            agg2[name][0] += 1
+            agg2[name][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        ktot = sum(v[1] for v in agg2.values())
+        lines += ["", f"Inside the {k} timed steps alone ({len(inside) / k:.1f} launches / step, kernel time "
+                  f"{ktot / k / 1e3:.2f} ms / step over two streams, wall {(t1 - t0) / 1e6 / k:.2f} ms / step under the "
+                  f"profiler): torch `FillFunctor` launches inside the steps: **{fills_in}** (in the whole process: "
+                  f"{fills_all}, all at allocation / warm-up outside `step()`).", "",
+                  "| ms/step | calls/step | avg us | kernel |", "|---:|---:|---:|---|"]
+        for n, (c, t) in sorted(agg2.items(), key=lambda x: -x[1][1])[:40]:
+            lines.append(f"| {t / k / 1e3:.3f} | {c / k:.1f} | {t / c:.1f} | `{n}` |")
 open(os.path.join(out, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
 print("\n".join(lines[:20]))

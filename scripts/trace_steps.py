@@ -1,6 +1,6 @@
 """Per-step view of a bench.py rocprofv3 kernel trace (steps delimited by adam_ema_kernel): span, kernel
 time, the time at least one kernel runs (busy) and the per-kernel totals of the chosen steps.
-  python scripts/trace_steps.py <run_kernel_trace.csv> [first_step] [n_steps]"""
+  python scripts/trace_steps.py <run_kernel_trace.csv> [first_step] [n_steps] [n_rows]"""
 import collections
 import csv
 import re
@@ -35,5 +35,5 @@ for r in sel:
 tot = sum(v[0] for v in agg.values())
 print(f"steps {first}..{first + nst - 1}: span {span / 1e3:.3f} ms/step, kernels {tot / 1e3:.3f} ms, "
       f"busy {busy / 1e6 / nst:.3f} ms, launches {len(sel) / nst:.1f}")
-for k, (us, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:45]:
+for k, (us, c) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:int(sys.argv[4]) if len(sys.argv) > 4 else 45]:
     print(f"{us / 1e3:7.3f} ms {c:6.1f} x {us / c:8.1f} us  {k}")
