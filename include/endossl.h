@@ -41,7 +41,9 @@ int es_abi_version(void);
  * N % 128 == 0, K % 64 == 0; A readable for round_up(M,256) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
-/* tuning knob: NT kernel family (-1 = per-shape default; 0, 1, 2, 5, 6, 10, 11 = fixed tilings, see gemm.hip);
+/* tuning knob: NT kernel family (-1 = per-shape default; 0, 1, 2, 5, 6, 10, 11 = fixed tilings, see gemm.hip;
+ * 12 = the weight-stationary K = 384 kernel where it applies -- epi 0 / 1 / 4 / 6 / 7, K == 384, N a multiple
+ * of 384 up to 3072 -- and the per-shape rules elsewhere; opt-in, bit-identical to the tilings);
  * returns the old one, or -2 (state unchanged) for a family that does not exist */
 int es_set_gemm_variant(int variant);
 /* 1 (default): the 64 x 128 NT tile rules (N <= 384 outputs of small token shards, M < 32768, and the residual

@@ -167,6 +167,43 @@ def _gemm_nt_patch_epilogue(D):
     assert torch.all(xv[:, 0] == 7.0)  # CLS rows untouched
 
 
+@pytest.mark.parametrize("M,N", [(777, 384), (70000, 1152), (30000, 1536), (40, 384), (5, 1152)])
+def test_gemm_ws_matches_tiled_bit_for_bit(M, N):
+    """Variant 12, the weight-stationary K = 384 kernel (gemm_nt_ws_kernel, opt-in), against the per-shape
+    default: each output is the same chain of 12 MFMAs in K order, so every epilogue it takes gives the same
+    bits.  Three launches in a row check that the chunk-claim counters reset themselves; a second stream uses
+    its own counter block."""
+    torch.manual_seed(M + N)
+    K = 384
+    A = _pad_rows(torch.randn(M, K, device=DEV).bfloat16())
+    B = (torch.randn(N, K, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(N, device=DEV) * 0.1
+
+    def run(epi):
+        two = epi in (EPI_GELU, EPI_GELU_D)
+        dt = torch.float32 if epi == EPI_F32 else torch.bfloat16
+        C = torch.full((M, N), float("nan"), dtype=dt, device=DEV)
+        C2 = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV) if two else None
+        call("es_gemm_nt", epi, ptr(A), K, ptr(B), K, ptr(bias), ptr(C), N, ptr(C2) if two else None, None, 0, M,
+             N, K, 0, S())
+        return C, C2
+
+    for epi in (EPI_BF16, EPI_GELU, EPI_GELU_ACT, EPI_GELU_D, EPI_F32):
+        ref, ref2 = run(epi)
+        with _Pinned(12):
+            outs = [run(epi) for _ in range(3)]
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                outs.append(run(epi))
+            torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        for C, C2 in outs:
+            assert torch.equal(C, ref), f"epilogue {epi}"
+            if ref2 is not None:
+                assert torch.equal(C2, ref2), f"epilogue {epi} (second output)"
+
+
 # ------------------------------------------------------------------------------------- GEMM TN
 @pytest.fixture(params=[-1, 0, 7], ids=["auto", "t0", "b7"])
 def tn_variant(request):
