@@ -1546,6 +1546,256 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The attention projection with its residual add AND the LayerNorm that follows it (round 6,
+// es_gemm_nt_resid_ln): x = o W^T + b + x_in (fp32), h = LN(x) (bf16), mean / rstd -- for D = 384
+// (ViT-S: N = K = 384).  Replaces es_gemm_nt(EPI_F32_RESID) + es_layernorm_fwd (code/models/conformer.py:
+// 65-66: x = x + attn(norm1(x)); norm2(x)) in one pass: x is never re-read from memory for its
+// statistics.  The weight-stationary body of gemm_nt_ws_kernel (W in registers, one persistent 8-wave
+// workgroup per CU, 32-row tiles) with whole rows per workgroup (one column group), so the row
+// statistics need no cross-workgroup exchange:
+//   ring (2 stages): the A tile (24 KiB, swizzled as in gemm_nt_ws_kernel) and the residual tile (32 rows x
+//     1,536 B, 16-B chunk c of row r at chunk c ^ (r & 15): conflict-free both for the MFMA-layout reads of
+//     the epilogue and for the LayerNorm's row reads), both by LDS-DMA one tile ahead;
+//   per step: [vmcnt: tile i landed] [barrier] [DMA tile i + 1] [claim tile i + 2] [MFMAs] [x = acc + bias +
+//     residual, written over the residual tile in place] [barrier] [LayerNorm: one wave per row, 4 rows per
+//     wave, ln_fwd_kernel's lane map, arithmetic and warp sums, so h / mean / rstd are its bits for the same
+//     x] [x, h, mean, rstd stores] [the claim retired, published for step i + 2].
+// x's bits equal es_gemm_nt(EPI_F32_RESID)'s (the same MFMA chain, (acc + bias) + residual) and h's equal
+// es_layernorm_fwd's on that x (tested).
+namespace rlg {
+constexpr int R = 32, KD = 384, D = 384;
+constexpr int ROWA = KD * 2, TA = R * ROWA;        // A tile: 24 KiB
+constexpr int ROWX = D * 4, TX = R * ROWX;         // residual / x tile: 48 KiB
+constexpr int STAGE = TA + TX, NST = 2;
+constexpr int PA = TA / 1024 / 8, PX = TX / 1024 / 8;  // LDS-DMA instructions per wave per stage (3 + 6)
+constexpr int QN = 4;
+constexpr int LDS = NST * STAGE + QN * 4 + 16 + D * 4 * 3;  // ring, claim ring, scratch, bias, gamma, beta
+constexpr int SLOTS = 64, SLOT_INTS = 4;                    // per stream: [0] head, [3] done
+}  // namespace rlg
+__device__ int g_rl_ctr[rlg::SLOTS * rlg::SLOT_INTS];
+
+// a a + b b with both products rounded (no contraction: __fmul_rn is a plain multiply in this HIP, so the
+// pragma is what keeps hipcc from fusing), and fma(a, a, b b)
+__device__ __forceinline__ float sq2_rounded(float a, float b) {
+#pragma clang fp contract(off)
+  return a * a + b * b;
+}
+__device__ __forceinline__ float sq2_fused(float a, float b) {
+#pragma clang fp contract(off)
+  return __builtin_fmaf(a, a, b * b);
+}
+__device__ __forceinline__ float mul_rounded(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+
+struct RLArgs {
+  const float* gamma; const float* beta;
+  bf16* h; float* mean; float* rstd;
+  int ldh; float eps;
+};
+
+__global__ __launch_bounds__(512, 1) void gemm_resid_ln_kernel(NTArgs p, RLArgs l, int slot) {
+  using namespace rlg;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int* const qring = (int*)(smem + NST * STAGE);
+  float* const bias_lds = (float*)(qring + QN + 4);
+  float* const gam_lds = bias_lds + D;
+  float* const bet_lds = gam_lds + D;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, r = lane & 15;
+  int* const ctr = g_rl_ctr + slot * SLOT_INTS;
+  const int nt = (p.M + R - 1) / R;
+  if (tid == 0) {  // the first two tiles: blocking claims (their latency hides behind the weight loads)
+    qring[0] = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    qring[1] = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  bf16x8 wf[3][12];
+  const int nw = w * 48;
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int kk = 0; kk < 12; ++kk)
+      wf[j][kk] = *(const bf16x8*)(p.B + (size_t)(nw + 16 * j + r) * p.ldb + 32 * kk + 8 * g);
+  if (tid < D / 4) {
+    *(f32x4*)(bias_lds + 4 * tid) = p.bias ? *(const f32x4*)(p.bias + 4 * tid) : f32x4{0.f, 0.f, 0.f, 0.f};
+    *(f32x4*)(gam_lds + 4 * tid) = *(const f32x4*)(l.gamma + 4 * tid);
+    *(f32x4*)(bet_lds + 4 * tid) = *(const f32x4*)(l.beta + 4 * tid);
+  }
+  __syncthreads();  // weights, parameters and the first claims retired before the loop's counted waits
+  int cur = __builtin_amdgcn_readfirstlane(qring[0]);
+  int nxt = __builtin_amdgcn_readfirstlane(qring[1]);
+
+  // LDS-DMA pieces: A (row, 16-B chunk) and residual (row, chunk) of this wave's instructions within a tile
+  int ar[PA], ac[PA], xr[PX], xc[PX];
+#pragma unroll
+  for (int j = 0; j < PA; ++j) {
+    const int off = ((j * 8 + w) * 64 + lane) * 16;
+    ar[j] = off / ROWA;
+    ac[j] = ((off % ROWA) >> 4) ^ (ar[j] & 15);
+  }
+#pragma unroll
+  for (int j = 0; j < PX; ++j) {
+    const int P = (j * 8 + w) * 64 + lane;  // physical chunk of the tile (contiguous per instruction)
+    xr[j] = P / (ROWX / 16);
+    xc[j] = (P % (ROWX / 16)) ^ (xr[j] & 15);  // the logical chunk it holds
+  }
+  auto dma = [&](int st, int tile) {  // rows past M re-read row M - 1 (finite, never stored)
+    const int m0 = tile * R, lim = p.M - 1 - m0;
+    const char* a = (const char*)(p.A + (size_t)m0 * p.lda);
+    const char* x = (const char*)((const float*)p.aux + (size_t)m0 * p.ldaux);
+    char* S = smem + st * STAGE;
+#pragma unroll
+    for (int j = 0; j < PA; ++j)
+      glds16_asm(a + (size_t)min(ar[j], lim) * p.lda * 2 + ac[j] * 16, S + (j * 8 + w) * 1024);
+#pragma unroll
+    for (int j = 0; j < PX; ++j)
+      glds16_asm(x + (size_t)min(xr[j], lim) * p.ldaux * 4 + xc[j] * 16, S + TA + (j * 8 + w) * 1024);
+  };
+  int xbase[4];  // the activation fragments' per-lane offsets (gemm_nt_ws_kernel's layout)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) xbase[k] = r * ROWA + ((4 * (k ^ (r >> 2)) + (g ^ (r & 3))) << 4);
+
+  const unsigned rows = (unsigned)p.M;
+  const __amdgpu_buffer_rsrc_t rx = buf_rsrc(p.C, rows * p.ldc * 4u);
+  const __amdgpu_buffer_rsrc_t rh = buf_rsrc(l.h, rows * l.ldh * 2u);
+  const __amdgpu_buffer_rsrc_t rm = buf_rsrc(l.mean, rows * 4u);
+  const __amdgpu_buffer_rsrc_t rs = buf_rsrc(l.rstd, rows * 4u);
+
+  if (cur < nt) {
+    int seq = 0, after_cur = 0, after_nxt = 0;
+    dma(0, cur);
+    seq += PA + PX;
+    after_cur = seq;
+    if (nxt < nt) {
+      dma(1, nxt);
+      seq += PA + PX;
+    }
+    after_nxt = seq;
+    int st = 0;
+    for (int it = 0;; ++it) {
+      if (it > 0) {  // this step's tile: the one DMA'd last step (claims only grow, so past the end stays past it)
+        cur = nxt;
+        after_cur = after_nxt;
+        if (cur >= nt) break;
+      }
+      wait_vmcnt_any(seq - after_cur);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // tile `cur` landed for every wave; the other stage and the claim ring free
+      if (it > 0) {  // the next step's tile (published at the end of the last step) into the other stage
+        nxt = __builtin_amdgcn_readfirstlane(qring[(it + 1) & (QN - 1)]);
+        if (nxt < nt) {
+          dma(st ^ 1, nxt);
+          seq += PA + PX;
+        }
+        after_nxt = seq;
+      }
+      // claim the tile of step it + 2 (one lane of wave 0; retired by a counted wait at the end of the step)
+      int claimed = nt, after_claim = 0;
+      const bool claimer = w == 0;
+      if (claimer) {
+        ws_claim_asm(ctr, claimed);
+        seq += 1;
+        after_claim = seq;
+      }
+      char* S = smem + st * STAGE;
+      unsigned xb4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        xb4[k] = (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)(S + xbase[k]);
+      f32x4 acc[2][3];
+      ws_mfma_half<0>(acc, wf, xb4);
+      ws_mfma_half<1>(acc, wf, xb4);
+      // x = (acc + bias) + residual in the MFMA layout (lane: row 16 a + r, columns nw + 16 j + 4 g .. + 3),
+      // written over the residual
+      char* X = S + TA;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int row = 16 * a + r, c = w * 12 + 4 * j + g;
+          f32x4* q = (f32x4*)(X + row * ROWX + ((c ^ r) << 4));
+          const f32x4 v = acc[a][j] + *(const f32x4*)(bias_lds + nw + 16 * j + 4 * g);
+          *q = v + *q;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // the x tile complete
+      // LayerNorm, one wave per row (ln_fwd_kernel's map: lane holds columns (j * 64 + lane) * 2, + 1)
+      const int m0 = cur * R;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = w * 4 + q;
+        float2 v[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int cc = (j * 64 + lane) >> 1;
+          v[j] = *(const float2*)(X + row * ROWX + ((cc ^ (row & 15)) << 4) + (lane & 1) * 8);
+        }
+        // the statistics with the rounding of ln_fwd_kernel / ln_fwd_loop_kernel as hipcc (ROCm 7.2) compiles
+        // them, which differs between the two rows a wave holds: their ISA sums the three column pairs' squares
+        // as fma(a0, a0, b0 b0) + (a1 a1 + b1 b1) + fma(a2, a2, b2 b2) for the even row and with no fma for the
+        // odd row, left to right, fuses the variance scale with eps and forms the output as fma(g, (x - mean)
+        // rstd, b).  Written out here because where hipcc contracts a * b + c depends on the surrounding code
+        // (the same source expression gave rstd 1 ulp apart on ~2 % of rows); the bit-identity test
+        // (test_gemm_resid_ln_matches_two_launches_bit_for_bit) pins it to the LayerNorm kernels' build.
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) s += v[j].x + v[j].y;
+        const float mean = warp_sum(s) * (1.0f / D);
+        float a[3], b[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          a[j] = v[j].x - mean;
+          b[j] = v[j].y - mean;
+        }
+        const bool even = (q & 1) == 0;  // the row's place in ln_fwd_kernel's row pair (m0 and w * 4 are even)
+        const float t0 = even ? sq2_fused(a[0], b[0]) : sq2_rounded(a[0], b[0]);
+        const float t1 = sq2_rounded(a[1], b[1]);
+        const float t2 = even ? sq2_fused(a[2], b[2]) : sq2_rounded(a[2], b[2]);
+        const float ss = (t0 + t1) + t2;
+        const float rstd = 1.0f / sqrtf(__builtin_fmaf(warp_sum(ss), 1.0f / D, l.eps));
+        const int m = m0 + row;
+        const bool ok = m < p.M;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int c = (j * 64 + lane) * 2;
+          const float2 gm = *(const float2*)(gam_lds + c), bt = *(const float2*)(bet_lds + c);
+          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+          bf16x2 o = {(bf16)__builtin_fmaf(mul_rounded(a[j], rstd), gm.x, bt.x),
+                      (bf16)__builtin_fmaf(mul_rounded(b[j], rstd), gm.y, bt.y)};
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v[j]), rx,
+                                                ok ? (unsigned)(m * p.ldc + c) * 4u : ES_OOB, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, o), rh,
+                                                ok ? (unsigned)(m * l.ldh + c) * 2u : ES_OOB, 0, 0);
+        }
+        const bool one = ok && lane == 0;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, mean), rm, one ? (unsigned)m * 4u : ES_OOB,
+                                              0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, rstd), rs, one ? (unsigned)m * 4u : ES_OOB,
+                                              0, 0);
+      }
+      seq += 4 * 8;
+      if (claimer) {  // publish the tile of step it + 2
+        wait_vmcnt_any(seq - after_claim);
+        asm volatile("" : "+v"(claimed));
+        const int c2 = __builtin_amdgcn_readfirstlane(claimed);
+        if (lane == 0) qring[(it + 2) & (QN - 1)] = c2;
+      }
+      st ^= 1;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (tid == 0) {
+    const int d = __hip_atomic_fetch_add(ctr + SLOT_INTS - 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == (int)gridDim.x - 1) {
+      __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + SLOT_INTS - 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Launcher with every specialisation spelled out and launched by name (HIP_KERNEL_NAME keeps the
 // template commas out of the launch macro; a kernel referenced only through a function pointer
 // gets no host stub).
@@ -1669,6 +1919,20 @@ int launch_ws(int epi, hipStream_t stream, const NTArgs& a) {
 }
 #undef WS_LAUNCH
 
+int launch_resid_ln(hipStream_t stream, const NTArgs& a, const RLArgs& l) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const int nt = (a.M + rlg::R - 1) / rlg::R;
+  const int grid = std::max(1, std::min(cus, nt));
+  allow_lds(gemm_resid_ln_kernel, (size_t)rlg::LDS);
+  hipLaunchKernelGGL(gemm_resid_ln_kernel, dim3(grid), dim3(512), rlg::LDS, stream, a, l, ws_slot(stream));
+  return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
 }  // namespace es_gemm
 using namespace es_gemm;
 
@@ -1779,6 +2043,20 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
   const int rc = launch_nt(variant, epi, grid, stream, a);
   if (rc) return rc;
   return hipGetLastError() == hipSuccess ? ES_OK : ES_HIP_ERROR;
+}
+
+// x = A B^T + bias + aux (fp32 residual), h = LayerNorm(x) (bf16) with its per-row mean / rstd, for N = K = 384
+// (gemm_resid_ln_kernel): es_gemm_nt(EPI_F32_RESID) followed by es_layernorm_fwd in one launch, the same bits.
+int es_gemm_nt_resid_ln(const void* A, int lda, const void* B, int ldb, const float* bias, float* C, int ldc,
+                        const float* aux, int ldaux, const float* gamma, const float* beta, void* h, int ldh,
+                        float* mean, float* rstd, int M, int N, int K, float eps, hipStream_t stream) {
+  if (M <= 0 || N != rlg::D || K != rlg::KD || (lda % 8) || (ldb % 8) || (ldc % 2) || (ldaux % 4) || (ldh % 2) ||
+      (size_t)M * (size_t)std::max(ldc, ldaux) * 4 >= (1u << 31))
+    return ES_BAD_SHAPE;
+  if (!A || !B || !C || !aux || !gamma || !beta || !h || !mean || !rstd) return ES_BAD_ARG;
+  NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, nullptr, aux, M, N, K, lda, ldb, ldc, ldaux, 0};
+  RLArgs l{gamma, beta, (bf16*)h, mean, rstd, ldh, eps};
+  return launch_resid_ln(stream, a, l);
 }
 
 // Tuning knob: which NT kernel family es_gemm_nt launches (-1 = per-shape default, 0 = 128x128

@@ -19,6 +19,7 @@ U64 = ctypes.c_ulonglong
 SIGNATURES = {
     "es_abi_version": (I, []),
     "es_gemm_nt": (I, [I, V, I, V, I, V, V, I, V, V, I, I, I, I, I, V]),
+    "es_gemm_nt_resid_ln": (I, [V, I, V, I, V, V, I, V, I, V, V, V, I, V, V, I, I, I, F, V]),
     "es_set_gemm_variant": (I, [I]),
     "es_set_gemm_small_tile": (I, [I]),
     "es_gemm_tn_workspace": (Z, [I, I, I]),

@@ -290,6 +290,15 @@ class Engine:
     # ... and its Q projection (forward) and Q weight gradient on the CLS rows only (False: all rows,
     # with a dQ that is zero off the CLS rows)
     PRUNE_Q = True
+    # the attention projection, its residual add and LayerNorm 2 as one launch at D = 384 for token axes of at
+    # least RESID_LN_MIN_M rows (es_gemm_nt_resid_ln: x is not re-read for its statistics; the same bits as the
+    # two launches, tested).  Isolated (scripts/resid_ln_bench.py) 138 -> 108 us at F1's train rows, 121 -> 90 at
+    # the weak rows, 58 -> 56 at a rank's share at N = 2, slower below (one persistent workgroup per CU with
+    # 1.5-3 tiles each); F1 30.09 / 30.06 / 30.10 -> 29.85 / 29.90 / 29.86 ms and, on a second box, 30.38 / 30.40 /
+    # 30.40 -> 30.22 / 30.21 / 30.21 (same box each, interleaved, scripts/gpu_ab_residln.sh).  ENDOSSL_RESID_LN=0
+    # turns it off.
+    RESID_LN = os.environ.get("ENDOSSL_RESID_LN", "1") == "1"
+    RESID_LN_MIN_M = 40000
 
     # fp32 parity mode (csrc/parity.hip): the same launch sequence over fp32 operand storage; the
     # entry points with an fp32 form, by their bf16 names
@@ -485,11 +494,17 @@ class Engine:
                     self.capture("fwd_cls", train, i, xin[:M], A.c_xout[:n])
                 break
             self._call("es_attn_fwd", ptr(A.qkv[li]), 3 * D, ptr(A.o[li]), D, ptr(A.lse[li]), n, T, H, 64 ** -0.5, s)
-            self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
-                 ptr(self.view(flat, b + "attn.proj.bias")), ptr(xmid), D, None, ptr(xin), D, M, D, D, 0, s)
-            self._call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
-                 ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
-                 cfg.eps, s)
+            if self.RESID_LN and D == 384 and self.precision == "bf16" and M >= self.RESID_LN_MIN_M:
+                self._call("es_gemm_nt_resid_ln", ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
+                     ptr(self.view(flat, b + "attn.proj.bias")), ptr(xmid), D, ptr(xin), D,
+                     ptr(self.view(flat, b + "norm2.weight")), ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D,
+                     ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D, D, cfg.eps, s)
+            else:
+                self._call("es_gemm_nt", EPI_F32_RESID, ptr(A.o[li]), D, ptr(self.wb[b + "attn.proj.weight"]), D,
+                     ptr(self.view(flat, b + "attn.proj.bias")), ptr(xmid), D, None, ptr(xin), D, M, D, D, 0, s)
+                self._call("es_layernorm_fwd", ptr(xmid), D, ptr(self.view(flat, b + "norm2.weight")),
+                     ptr(self.view(flat, b + "norm2.bias")), ptr(h2), D, ptr(A.mean2[li]), ptr(A.rstd2[li]), M, D,
+                     cfg.eps, s)
             if train:
                 self._gemm("fc1_fwd", EPI_GELU_D if self.GELU_D else EPI_GELU, ptr(h2), D,
                            ptr(self.wb[b + "mlp.fc1.weight"]), D,

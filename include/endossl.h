@@ -41,6 +41,13 @@ int es_abi_version(void);
  * N % 128 == 0, K % 64 == 0; A readable for round_up(M,256) rows. */
 int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const float* bias, void* C, int ldc,
                void* C2, const void* aux, int ldaux, int M, int N, int K, int np, hipStream_t stream);
+/* x = A B^T + bias + aux, h = LayerNorm(x; gamma, beta, eps) with per-row mean / rstd, in one launch, for
+ * N == K == 384 (ViT-S's attention projection followed by norm2): the bits of es_gemm_nt(epi 2) followed by
+ * es_layernorm_fwd.  x fp32 [M, ldc], aux fp32 [M, ldaux] (16-B aligned rows), h bf16 [M, ldh]; bias nullable.
+ * Replaces code/models/conformer.py:65-66 (x + attn(...), then norm2).  ES_BAD_SHAPE for other N / K. */
+int es_gemm_nt_resid_ln(const void* A, int lda, const void* B, int ldb, const float* bias, float* C, int ldc,
+                        const float* aux, int ldaux, const float* gamma, const float* beta, void* h, int ldh,
+                        float* mean, float* rstd, int M, int N, int K, float eps, hipStream_t stream);
 /* tuning knob: NT kernel family (-1 = per-shape default; 0, 1, 2, 5, 6, 10, 11 = fixed tilings, see gemm.hip;
  * 12 = the weight-stationary K = 384 kernel where it applies -- epi 0 / 1 / 4 / 6 / 7, K == 384, N a multiple
  * of 384 up to 3072 -- and the per-shape rules elsewhere; opt-in, bit-identical to the tilings);

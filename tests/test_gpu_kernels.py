@@ -204,6 +204,52 @@ def test_gemm_ws_matches_tiled_bit_for_bit(M, N):
                 assert torch.equal(C2, ref2), f"epilogue {epi} (second output)"
 
 
+@pytest.mark.parametrize("M", [777, 100864, 12608, 5, 40])
+def test_gemm_resid_ln_matches_two_launches_bit_for_bit(M):
+    """es_gemm_nt_resid_ln (the attention projection + residual + norm2 in one launch, D = 384) against
+    es_gemm_nt(EPI_F32_RESID) followed by es_layernorm_fwd: x, h, mean and rstd bit for bit, every row written;
+    repeated launches (self-resetting tile claims) and a second stream."""
+    torch.manual_seed(M)
+    D, eps = 384, 1e-6
+    A = _pad_rows(torch.randn(M, D, device=DEV).bfloat16())
+    W = (torch.randn(D, D, device=DEV) * 0.05).bfloat16()
+    bias = torch.randn(D, device=DEV) * 0.1
+    xin = torch.randn(M, D, device=DEV)
+    gamma = 1.0 + 0.1 * torch.randn(D, device=DEV)
+    beta = 0.1 * torch.randn(D, device=DEV)
+
+    def bufs():
+        nan = float("nan")
+        return (torch.full((M, D), nan, device=DEV), torch.full((M, D), nan, dtype=torch.bfloat16, device=DEV),
+                torch.full((M,), nan, device=DEV), torch.full((M,), nan, device=DEV))
+
+    x0, h0, m0, r0 = bufs()
+    call("es_gemm_nt", EPI_F32_RESID, ptr(A), D, ptr(W), D, ptr(bias), ptr(x0), D, None, ptr(xin), D, M, D, D, 0, S())
+    call("es_layernorm_fwd", ptr(x0), D, ptr(gamma), ptr(beta), ptr(h0), D, ptr(m0), ptr(r0), M, D, eps, S())
+    outs = []
+    for k in range(4):
+        o = bufs()
+        side = torch.cuda.Stream() if k == 3 else None
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side) if side is not None else torch.cuda.stream(torch.cuda.current_stream()):
+            call("es_gemm_nt_resid_ln", ptr(A), D, ptr(W), D, ptr(bias), ptr(o[0]), D, ptr(xin), D, ptr(gamma),
+                 ptr(beta), ptr(o[1]), D, ptr(o[2]), ptr(o[3]), M, D, D, eps, S())
+        if side is not None:
+            torch.cuda.current_stream().wait_stream(side)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for x, h, m, r in outs:
+        assert torch.equal(x, x0) and torch.equal(h, h0) and torch.equal(m, m0) and torch.equal(r, r0)
+
+
+def test_gemm_resid_ln_rejects_other_widths():
+    z = torch.zeros(256, 768, device=DEV)
+    rc = _lib.load().es_gemm_nt_resid_ln(ptr(z), 768, ptr(z), 768, None, ptr(z), 768, ptr(z), 768, ptr(z), ptr(z),
+                                         ptr(z), 768, ptr(z), ptr(z), 64, 768, 768, 1e-6, S())
+    assert rc == -1  # ES_BAD_SHAPE: only D = 384
+
+
 # ------------------------------------------------------------------------------------- GEMM TN
 @pytest.fixture(params=[-1, 0, 7], ids=["auto", "t0", "b7"])
 def tn_variant(request):

@@ -456,6 +456,40 @@ def test_deferred_ln_grads_bit_identical(mode, nimg):
         assert torch.equal(a, b), (name, (a - b).abs().max().item())
 
 
+@pytest.mark.parametrize("nimg", [40, 7])
+def test_resid_ln_fusion_bit_identical(nimg):
+    """Engine.RESID_LN (the attention projection + residual + LayerNorm 2 as one es_gemm_nt_resid_ln launch)
+    gives the train and weak forwards' logits and every gradient BIT-identical to the two launches (threshold
+    lowered so the small batch takes the fused path)."""
+    from endossl.vit import NativeViT, ViTConfig
+    vcfg = ViTConfig(num_classes=23)
+    m = NativeViT(vcfg, seed=11)
+    with torch.no_grad():
+        m.head.weight.copy_(0.5 * torch.randn(m.head.weight.shape, generator=torch.Generator().manual_seed(5)))
+    m.mark_updated()
+    m = m.to(DEV)
+    eng = m.engine()
+    eng.pack(m.flat, m.version)
+    eng.RESID_LN_MIN_M = 0
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = torch.randn(nimg, 3, vcfg.img_size, vcfg.img_size, device=DEV, generator=g)
+    dl = torch.randn(nimg, 23, device=DEV, generator=g) * 1e-2
+    out = {}
+    for fused in (False, True):
+        eng.RESID_LN = fused
+        lw = eng.forward(m.flat, [x], train=False).clone()
+        lt = eng.forward(m.flat, [x], train=True).clone()
+        gr = torch.full_like(m.flat, 5.0)
+        eng.backward(m.flat, gr, dlogits=dl)
+        torch.cuda.synchronize()
+        out[fused] = (lw, lt, gr)
+    for k in ("RESID_LN", "RESID_LN_MIN_M"):
+        delattr(eng, k)
+    assert torch.equal(out[True][0], out[False][0]) and torch.equal(out[True][1], out[False][1])
+    assert out[True][2].abs().max() > 0
+    assert torch.equal(out[True][2], out[False][2]), (out[True][2] - out[False][2]).abs().max().item()
+
+
 @pytest.mark.parametrize("head,nimg", [("cls", 40), ("emb", 40), ("cls", 64), ("emb", 64)])
 def test_last_block_cls_rows_match_full_rows(head, nimg):
     """Engine.PRUNE_LAST (the last block's attention for the CLS queries only, its projection / LN2 /
