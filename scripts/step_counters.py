@@ -40,7 +40,8 @@ def rows(i):
 
 def family(name):
     n = name.lower()
-    for key, fam in (("gemm_panel", "NT GEMM (panel K=384)"), ("gemm_nt", "NT GEMM (tiled)"),
+    for key, fam in (("gemm_resid_ln", "projection + residual + LayerNorm 2 (fused)"),
+                     ("gemm_panel", "NT GEMM (panel K=384)"), ("gemm_nt", "NT GEMM (tiled)"),
                      ("gemm_tn", "weight-gradient GEMM (TN)"), ("splitk_reduce", "split-K / bias reductions"),
                      ("reduce_partials", "split-K / bias reductions"), ("colsum", "split-K / bias reductions"),
                      ("attn", "attention"), ("layernorm", "LayerNorm"), ("ln_", "LayerNorm"),
