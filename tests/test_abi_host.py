@@ -248,6 +248,22 @@ def test_tn_big_grouped_prepare_layout():
                                               dims) != 0
 
 
+def test_resid_ln_entry_validates_before_any_launch():
+    """es_gemm_nt_resid_ln refuses what its kernel cannot take before touching the GPU: any width but 384
+    (ES_BAD_SHAPE), misaligned row strides (ES_BAD_SHAPE: the LDS-DMA moves 16-B row pieces), a null operand
+    (ES_BAD_ARG)."""
+    from endossl import _lib
+    lib = _lib.load()
+    p = 0x7000000000  # never dereferenced on these paths
+
+    def rc(M=256, N=384, K=384, lda=384, ldc=384, ldaux=384, ldh=384, gamma=p):
+        return lib.es_gemm_nt_resid_ln(p, lda, p, 384, None, p, ldc, p, ldaux, gamma, p, p, ldh, p, p, M, N, K, 1e-6,
+                                       None)
+    assert rc(N=768) == -1 and rc(K=768) == -1 and rc(M=0) == -1
+    assert rc(lda=388) == -1 and rc(ldaux=386) == -1 and rc(ldc=385) == -1 and rc(ldh=385) == -1
+    assert rc(gamma=None) == -2
+
+
 INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
 
 
