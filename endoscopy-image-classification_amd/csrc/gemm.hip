@@ -1559,8 +1559,9 @@ __global__ __launch_bounds__(512, 2) void gemm_nt_ws_kernel(NTArgs p, int ncg, i
 //     the epilogue and for the LayerNorm's row reads), both by LDS-DMA one tile ahead;
 //   per step: [vmcnt: tile i landed] [barrier] [DMA tile i + 1] [claim tile i + 2] [MFMAs] [x = acc + bias +
 //     residual, written over the residual tile in place] [barrier] [LayerNorm: one wave per row, 4 rows per
-//     wave, ln_fwd_kernel's lane map, arithmetic and warp sums, so h / mean / rstd are its bits for the same
-//     x] [x, h, mean, rstd stores] [the claim retired, published for step i + 2].
+//     wave, ln_fwd_kernel's lane map, warp sums and rounding as compiled (see the statistics below), so h /
+//     mean / rstd are its bits for the same x] [x, h, mean, rstd stores] [the claim retired, published for
+//     step i + 2].
 // x's bits equal es_gemm_nt(EPI_F32_RESID)'s (the same MFMA chain, (acc + bias) + residual) and h's equal
 // es_layernorm_fwd's on that x (tested).
 namespace rlg {
