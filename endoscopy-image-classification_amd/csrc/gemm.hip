@@ -2055,6 +2055,10 @@ int es_gemm_nt_resid_ln(const void* A, int lda, const void* B, int ldb, const fl
       (size_t)M * (size_t)std::max(ldc, ldaux) * 4 >= (1u << 31))
     return ES_BAD_SHAPE;
   if (!A || !B || !C || !aux || !gamma || !beta || !h || !mean || !rstd) return ES_BAD_ARG;
+  // 16-B pieces by LDS-DMA (A, aux), 16-B weight / parameter loads, 8-B x and 4-B h stores
+  if ((((uintptr_t)A | (uintptr_t)aux | (uintptr_t)B | (uintptr_t)gamma | (uintptr_t)beta) & 15) ||
+      (bias && ((uintptr_t)bias & 15)) || ((uintptr_t)C & 7) || ((uintptr_t)h & 3))
+    return ES_BAD_ARG;
   NTArgs a{(const bf16*)A, (const bf16*)B, bias, C, nullptr, aux, M, N, K, lda, ldb, ldc, ldaux, 0};
   RLArgs l{gamma, beta, (bf16*)h, mean, rstd, ldh, eps};
   return launch_resid_ln(stream, a, l);

@@ -44,7 +44,8 @@ int es_gemm_nt(int epi, const void* A, int lda, const void* B, int ldb, const fl
 /* x = A B^T + bias + aux, h = LayerNorm(x; gamma, beta, eps) with per-row mean / rstd, in one launch, for
  * N == K == 384 (ViT-S's attention projection followed by norm2): the bits of es_gemm_nt(epi 2) followed by
  * es_layernorm_fwd.  x fp32 [M, ldc], aux fp32 [M, ldaux] (16-B aligned rows), h bf16 [M, ldh]; bias nullable.
- * Replaces code/models/conformer.py:65-66 (x + attn(...), then norm2).  ES_BAD_SHAPE for other N / K. */
+ * Replaces code/models/conformer.py:65-66 (x + attn(...), then norm2).  ES_BAD_SHAPE for other N / K;
+ * ES_BAD_ARG for a null or misaligned operand (A, B, aux, gamma, beta, bias 16-B; C 8-B; h 4-B). */
 int es_gemm_nt_resid_ln(const void* A, int lda, const void* B, int ldb, const float* bias, float* C, int ldc,
                         const float* aux, int ldaux, const float* gamma, const float* beta, void* h, int ldh,
                         float* mean, float* rstd, int M, int N, int K, float eps, hipStream_t stream);

@@ -262,6 +262,7 @@ def test_resid_ln_entry_validates_before_any_launch():
     assert rc(N=768) == -1 and rc(K=768) == -1 and rc(M=0) == -1
     assert rc(lda=388) == -1 and rc(ldaux=386) == -1 and rc(ldc=385) == -1 and rc(ldh=385) == -1
     assert rc(gamma=None) == -2
+    assert rc(gamma=p + 4) == -2  # a misaligned operand (16-B pieces)
 
 
 INTEGRATION = os.path.join(ROOT, "INTEGRATION.md")
